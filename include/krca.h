@@ -1,0 +1,109 @@
+/*
+ * krca.h — C-ABI of libkrca.so, the MI355X (gfx950) numeric core behind the RCA agents.
+ *
+ * The reference (vobbilis/kubernetes-rca-system) is pure Python, so there is no FFI of its own
+ * to mirror; these entry points replace the per-pod Python loops of its non-LLM agents and are
+ * bound from Python with ctypes (kubernetes-rca-system_amd/krca/native.py; INTEGRATION.md shows
+ * the binding a maintainer would add to the reference).  Each entry cites the reference code
+ * whose loop it replaces.
+ *
+ * Conventions:
+ *  - every buffer argument is a caller-owned DEVICE pointer unless the name ends in _host;
+ *  - `stream` is a hipStream_t (NULL = default stream); calls are asynchronous unless noted;
+ *  - no allocation on the hot path: scratch comes from caller workspaces sized by the
+ *    *_workspace_size / *_num_* helpers;
+ *  - return 0 on success, a negative errno-style code on failure; krca_last_error() returns a
+ *    thread-local message; no C++ exception crosses the ABI;
+ *  - re-entrant per stream; integer outputs are deterministic (no order-dependent reductions).
+ */
+#ifndef KRCA_H
+#define KRCA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KRCA_OK 0
+#define KRCA_EINVAL (-22)
+#define KRCA_ENOMEM (-12)
+#define KRCA_EDEVICE (-5) /* HIP runtime error */
+#define KRCA_ENOTCONV (-70) /* PageRank did not converge within max_iter */
+
+#define KRCA_NCAT 13 /* log error categories, ref:agents/logs_agent.py:20-34 */
+
+/* flag bits of krca_usage_flags / krca_rolling_score (ref:agents/metrics_agent.py:93,101,140,148) */
+#define KRCA_F_CPU80 1u
+#define KRCA_F_CPU90 2u
+#define KRCA_F_MEM80 4u
+#define KRCA_F_MEM90 8u
+
+int krca_version(void);
+const char* krca_last_error(void);
+int krca_device_count(int* n_host);
+
+/* ---- a1/a2: instantaneous usage thresholds ------------------------------------------------
+ * Replaces the pod loops of MetricsAgent._analyze_cpu_usage / _analyze_memory_usage
+ * (ref:agents/metrics_agent.py:88-94, 135-141): flags[p] gets KRCA_F_CPU80 iff usage[p][0] > 80,
+ * KRCA_F_CPU90 iff > 90, KRCA_F_MEM80 / KRCA_F_MEM90 likewise for usage[p][1] (strict, float32). */
+int krca_usage_flags(const float* usage /*[P][2]*/, int64_t P, uint8_t* flags /*[P]*/, void* stream);
+
+/* ---- a5: rolling z-score anomaly scoring (new primitive; plugs in at
+ * ref:agents/metrics_agent.py:44-47).  x is time-major [T][P][M] float32 (series s = p*M+m).
+ * For t in [W, T): mean/var of x[t-W..t-1] (ddof 0, float64 sliding sums in a fixed order),
+ * exceed(t) = var > 1e-12 && (x_t - mean)^2 > z_thr^2 * var.   Outputs:
+ *   z_last[p][m] = (x_{T-1} - mean)/sqrt(var) (0 if var <= 1e-12),   score[p] = max_m |z_last|,
+ *   n_exceed[p]  = sum over m, t of exceed(t) (bit-exact vs oracle/krca_oracle.c),
+ *   flags[p]     = KRCA_F_* of x[T-1][p][0] (CPU %) and x[T-1][p][1] (memory %) if M >= 2.
+ * M must be a power of two <= 64. */
+int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr,
+                       float* z_last, float* score, int32_t* n_exceed, uint8_t* flags, void* stream);
+
+/* ---- a11/a12: 13-category log histograms (ref:agents/logs_agent.py:124-181) ----------------
+ * text = UTF-8 bytes of D container logs, container d = text[doc_off[d], doc_off[d+1]).
+ * Lines are str.splitlines() lines; a line is in category c iff
+ * re.search(pattern_c, line, re.IGNORECASE) (compiled DFA, csrc/log_dfa_tables.h).
+ * Two phases (the line count is data-dependent):
+ *   krca_log_index: per-chunk line-start counts + scan into block_base (workspace of
+ *                   krca_log_index_size(nbytes) int64) and *n_lines (device int64).
+ *   krca_log_match: per line start/end byte offsets and 13-bit mask; per container the line
+ *                   count, the 13-bin histogram and the first three matching line ids per bin
+ *                   (-1 when fewer) — atomics-free segmented reduction. */
+int64_t krca_log_index_size(int64_t nbytes);
+int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
+                   int64_t* workspace, int64_t* n_lines, void* stream);
+int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
+                   const int64_t* workspace, int64_t n_lines,
+                   int64_t* line_start /*[L]*/, int64_t* line_end /*[L]*/, uint32_t* line_mask /*[L]*/,
+                   int32_t* doc_lines /*[D]*/, int32_t* hist /*[D][13]*/, int32_t* examples /*[D][13][3]*/,
+                   void* stream);
+
+/* ---- a10: personalized PageRank root-cause propagation (replaces the sink of
+ * Coordinator._identify_root_causes, ref:agents/coordinator.py:157-184; networkx 3.4.2
+ * pagerank semantics: dangling mass follows the personalization, L1 stop rule err < N*tol).
+ * Pull-CSR: row i lists the sources j of edges j->i; outdeg[j] = out-degree of j.
+ * seed[i] >= 0 (float32) is normalised inside.  Arithmetic is 2^-60 fixed point in int64, so
+ * the result is independent of summation order and bit-identical to oracle/krca_oracle.c.
+ * The plan (row blocks for the adaptive SpMV) is built once per graph.  r_out = float32 ranks;
+ * r_fixed (optional, int64 units of 2^-60) and *iters_host are returned for exact comparison. */
+int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N);
+int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, int64_t plan_len);
+int64_t krca_ppr_workspace_size(int64_t N);
+int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
+             const int32_t* plan, int64_t plan_len, const float* seed, double alpha, int32_t max_iter,
+             double tol, void* workspace, float* r_out, int64_t* r_fixed, int32_t* iters_host,
+             void* stream);
+
+/* ---- top-k (descending value, ties -> lower index), float32 or int64 keys ------------------ */
+int64_t krca_topk_workspace_size(int64_t N, int32_t k);
+int krca_topk_f32(const float* v, int64_t N, int32_t k, void* workspace, int32_t* idx, float* val,
+                  void* stream);
+int krca_topk_i64(const int64_t* v, int64_t N, int32_t k, void* workspace, int32_t* idx, int64_t* val,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KRCA_H */

@@ -1,0 +1,197 @@
+// Per-pod scoring kernels.
+//
+//  krca_usage_flags    — the instantaneous CPU / memory thresholds of
+//                        ref:agents/metrics_agent.py:88-114 and :135-161 (x > 80 strict, high if > 90).
+//  krca_rolling_score  — rolling-window z-scores over a time-major [T][P][M] float32 tensor.
+//
+// Design (MI355X): HBM-streaming, one lane per series s = p*M + m.  At every time step a wave
+// reads 64 consecutive floats (256 B, fully coalesced) and the trailing window of W samples
+// lives in registers (a W-entry ring indexed by the compile-time position inside an unrolled
+// W-step block), so each input byte crosses HBM exactly once: 4*P*M*T bytes per call.  The
+// window statistics are float64 sliding sums updated in a FIXED order, so the integer outputs
+// (n_exceed, flags) are bit-identical to the C restatement in oracle/krca_oracle.c; the
+// threshold test is |z| > thr  <=>  d*d > thr^2*var, with no division or square root.
+// Pod-level reductions (max |z|, sum of exceedances, flag OR) are wave shuffles inside the
+// aligned M-lane group of the pod.
+#include "krca_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr double kVarEps = 1e-12;
+
+__global__ __launch_bounds__(256) void usage_flags_kernel(const float2* __restrict__ usage, int64_t P,
+                                                          uint8_t* __restrict__ flags) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += stride) {
+    const float2 u = usage[p];
+    flags[p] = (u.x > 80.f ? KRCA_F_CPU80 : 0u) | (u.x > 90.f ? KRCA_F_CPU90 : 0u) |
+               (u.y > 80.f ? KRCA_F_MEM80 : 0u) | (u.y > 90.f ? KRCA_F_MEM90 : 0u);
+  }
+}
+
+struct StepState {
+  double s1, s2;  // window sum and sum of squares (float64, fixed order)
+  int cnt;        // exceedances of this series
+  double dl, varl;  // deviation and variance at t = T-1
+};
+
+// One time step of the rolling statistics.  `old` is x[t-W].
+__device__ __forceinline__ void step(StepState& st, float v, float old, double invW, double thr2, bool last) {
+  const double vd = (double)v;
+  const double mean = st.s1 * invW;
+  const double var = st.s2 * invW - mean * mean;
+  const double d = vd - mean;
+  st.cnt += (var > kVarEps) && (d * d > thr2 * var);
+  if (last) {
+    st.dl = d;
+    st.varl = var;
+  }
+  const double od = (double)old;
+  st.s1 = st.s1 + (vd - od);
+  st.s2 = st.s2 + (vd * vd - od * od);
+}
+
+// Pod epilogue shared by both kernels: z_last per series, pod max|z|, exceedance sum, flags.
+__device__ __forceinline__ void pod_epilogue(const StepState& st, int64_t s, bool active, int M, int T,
+                                             const float* __restrict__ xs, int64_t S,
+                                             float* __restrict__ z_last, float* __restrict__ score,
+                                             int32_t* __restrict__ n_exceed, uint8_t* __restrict__ flags) {
+  const bool has_z = st.varl > kVarEps;
+  const float z = has_z ? (float)(st.dl / sqrt(st.varl)) : 0.f;
+  const int m = (int)(s & (M - 1));
+  float vlast = (active && T > 0) ? xs[(int64_t)(T - 1) * S] : 0.f;
+  unsigned f = 0;
+  if (m == 0) f = (vlast > 80.f ? KRCA_F_CPU80 : 0u) | (vlast > 90.f ? KRCA_F_CPU90 : 0u);
+  if (m == 1) f = (vlast > 80.f ? KRCA_F_MEM80 : 0u) | (vlast > 90.f ? KRCA_F_MEM90 : 0u);
+  float az = fabsf(z);
+  int cnt = st.cnt;
+  for (int off = 1; off < M; off <<= 1) {  // the M lanes of a pod are aligned inside the wave
+    az = fmaxf(az, __shfl_xor(az, off, 64));
+    cnt += __shfl_xor(cnt, off, 64);
+    f |= __shfl_xor(f, off, 64);
+  }
+  if (!active) return;
+  z_last[s] = z;
+  if (m == 0) {
+    const int64_t p = s / M;
+    score[p] = az;
+    n_exceed[p] = cnt;
+    flags[p] = (uint8_t)f;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void rolling_score_ring(const float* __restrict__ x, int64_t S, int T, int M,
+                                                          double thr2, float* __restrict__ z_last,
+                                                          float* __restrict__ score, int32_t* __restrict__ n_exceed,
+                                                          uint8_t* __restrict__ flags) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = s < S;
+  const float* xs = x + (active ? s : 0);
+  const double invW = 1.0 / (double)W;
+  StepState st{0.0, 0.0, 0, 0.0, 0.0};
+  float ring[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const float v = (j < T && active) ? xs[(int64_t)j * S] : 0.f;
+    ring[j] = v;
+    const double vd = (double)v;
+    st.s1 = st.s1 + vd;
+    st.s2 = st.s2 + vd * vd;
+  }
+  int t0 = W;
+  for (; t0 + W <= T; t0 += W) {  // full W-step blocks: every ring slot index is static
+    float nx[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) nx[j] = active ? xs[(int64_t)(t0 + j) * S] : 0.f;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      step(st, nx[j], ring[j], invW, thr2, t0 + j == T - 1);
+      ring[j] = nx[j];
+    }
+  }
+  if (t0 < T) {  // tail block
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (t0 + j < T) {
+        const float v = active ? xs[(int64_t)(t0 + j) * S] : 0.f;
+        step(st, v, ring[j], invW, thr2, t0 + j == T - 1);
+        ring[j] = v;
+      }
+    }
+  }
+  pod_epilogue(st, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
+}
+
+// Any W: the outgoing sample x[t-W] is re-read (same values, same arithmetic -> same bits).
+__global__ __launch_bounds__(256) void rolling_score_reread(const float* __restrict__ x, int64_t S, int T, int W,
+                                                            int M, double thr2, float* __restrict__ z_last,
+                                                            float* __restrict__ score,
+                                                            int32_t* __restrict__ n_exceed,
+                                                            uint8_t* __restrict__ flags) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = s < S;
+  const float* xs = x + (active ? s : 0);
+  const double invW = 1.0 / (double)W;
+  StepState st{0.0, 0.0, 0, 0.0, 0.0};
+  for (int j = 0; j < W && j < T; ++j) {
+    const double vd = active ? (double)xs[(int64_t)j * S] : 0.0;
+    st.s1 = st.s1 + vd;
+    st.s2 = st.s2 + vd * vd;
+  }
+  for (int t = W; t < T; ++t) {
+    const float v = active ? xs[(int64_t)t * S] : 0.f;
+    const float o = active ? xs[(int64_t)(t - W) * S] : 0.f;
+    step(st, v, o, invW, thr2, t == T - 1);
+  }
+  pod_epilogue(st, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
+}
+
+}  // namespace
+
+extern "C" {
+
+int krca_usage_flags(const float* usage, int64_t P, uint8_t* flags, void* stream) {
+  KRCA_CHECK_ARG(P >= 0, "krca_usage_flags: P < 0");
+  if (P == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(usage && flags, "krca_usage_flags: null pointer");
+  const int64_t blocks = std::min<int64_t>(krca::ceil_div(P, 256), 4096);
+  hipLaunchKernelGGL(usage_flags_kernel, dim3((unsigned)blocks), dim3(256), 0, krca::as_stream(stream),
+                     reinterpret_cast<const float2*>(usage), P, flags);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr, float* z_last,
+                       float* score, int32_t* n_exceed, uint8_t* flags, void* stream) {
+  KRCA_CHECK_ARG(P >= 0 && T >= 0 && W >= 1, "krca_rolling_score: bad sizes P=%lld T=%d W=%d", (long long)P, T, W);
+  KRCA_CHECK_ARG(M >= 1 && M <= 64 && (M & (M - 1)) == 0, "krca_rolling_score: M=%d must be a power of two <= 64", M);
+  if (P == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(x && z_last && score && n_exceed && flags, "krca_rolling_score: null pointer");
+  const int64_t S = P * (int64_t)M;
+  const double thr2 = (double)z_thr * (double)z_thr;
+  const dim3 grid((unsigned)krca::ceil_div(S, 256)), block(256);
+  hipStream_t st = krca::as_stream(stream);
+  switch (W) {
+#define KRCA_W(WV)                                                                                     \
+  case WV:                                                                                             \
+    hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
+                       n_exceed, flags);                                                              \
+    break;
+    KRCA_W(10)
+    KRCA_W(15)
+    KRCA_W(20)
+    KRCA_W(30)
+    KRCA_W(60)
+#undef KRCA_W
+    default:
+      hipLaunchKernelGGL(rolling_score_reread, grid, block, 0, st, x, S, T, W, M, thr2, z_last, score, n_exceed,
+                         flags);
+  }
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+"""Coordinator: dispatch, cross-agent correlation, root causes (+ device PageRank ranking).
+
+Reference: ref:agents/coordinator.py:7-192.  ``run_analysis`` / the comprehensive result
+schema / ``_correlate_findings`` (group by component, first-seen order, max severity by
+:data:`SEVERITY_ORDER`) / ``_identify_root_causes`` (critical|high with >1 finding) are kept
+exactly.  New, additive: ``ranked_root_causes`` — personalized
+PageRank over the dependency graph, seeded by anomaly scores (bulk path) or by the trace
+backend's per-service error rates (C1 mock), computed by ``krca_ppr`` on the device.
+"""
+import numpy as np
+
+from .base import SEVERITY_ORDER
+from .events import EventsAgent
+from .logs import LogsAgent
+from .metrics import MetricsAgent
+from .topology import TopologyAgent, csr_from_edges
+from .traces import TracesAgent
+
+
+class Coordinator:
+    def __init__(self, k8s_client, engine=None, ppr_alpha=0.85, ppr_topk=10):
+        self.k8s_client = k8s_client
+        self._engine = engine
+        self.ppr_alpha = ppr_alpha
+        self.ppr_topk = ppr_topk
+        self.metrics_agent = MetricsAgent(k8s_client, engine)
+        self.logs_agent = LogsAgent(k8s_client, engine)
+        self.traces_agent = TracesAgent(k8s_client, engine)
+        self.topology_agent = TopologyAgent(k8s_client, engine)
+        self.events_agent = EventsAgent(k8s_client, engine)
+        self.agent_map = {
+            'comprehensive': self._run_comprehensive_analysis,
+            'metrics': self.metrics_agent.analyze,
+            'logs': self.logs_agent.analyze,
+            'traces': self.traces_agent.analyze,
+            'topology': self.topology_agent.analyze,
+            'events': self.events_agent.analyze,
+        }
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            from krca import native
+            self._engine = native.default_engine()
+        return self._engine
+
+    def run_analysis(self, analysis_type, namespace, context=None, **kwargs):  # ref :39-70
+        try:
+            if analysis_type not in self.agent_map:
+                return {'error': f"Unknown analysis type: {analysis_type}"}
+            results = self.agent_map[analysis_type](namespace=namespace, context=context, **kwargs)
+            results['metadata'] = {'analysis_type': analysis_type, 'namespace': namespace,
+                                   'context': context or self.k8s_client.get_current_context(),
+                                   'timestamp': self.k8s_client.get_current_time()}
+            return results
+        except Exception as e:
+            return {'error': str(e)}
+
+    def _run_comprehensive_analysis(self, namespace, context=None, **kwargs):  # ref :72-116
+        self._reset_agents()
+        order = ('metrics', 'logs', 'topology', 'events', 'traces')
+        agents = {'metrics': self.metrics_agent, 'logs': self.logs_agent, 'topology': self.topology_agent,
+                  'events': self.events_agent, 'traces': self.traces_agent}
+        results = {k: agents[k].analyze(namespace, context, **kwargs) for k in order}
+        correlated = self._correlate_findings(*(results[k].get('findings', []) for k in order))
+        out = {'correlated_findings': correlated, 'agent_results': results,
+               'root_causes': self._identify_root_causes(correlated)}
+        ranked = self._rank_root_causes(namespace)
+        if ranked is not None:
+            out['ranked_root_causes'] = ranked
+        return out
+
+    @staticmethod
+    def _correlate_findings(*lists):  # ref :118-155
+        groups = {}
+        for lst in lists:
+            for f in lst:
+                groups.setdefault(f['component'], []).append(f)
+        return [{'component': comp, 'related_findings': fs, 'correlation_type': 'component',
+                 'severity': max((f['severity'] for f in fs), key=SEVERITY_ORDER.index)}
+                for comp, fs in groups.items() if len(fs) > 1]
+
+    @staticmethod
+    def _identify_root_causes(correlated):  # ref :157-184
+        out = []
+        for c in correlated:
+            n = len(c['related_findings'])
+            if c['severity'] in ('critical', 'high') and n > 1:
+                out.append({'component': c['component'], 'related_findings_count': n, 'severity': c['severity'],
+                            'explanation': f"High severity issue with {n} related findings indicates a potential root cause."})
+        return out
+
+    def _reset_agents(self):
+        for a in (self.metrics_agent, self.logs_agent, self.traces_agent, self.topology_agent, self.events_agent):
+            a.reset()
+
+    # -- additive ranking ----------------------------------------------------------------
+    def _rank_root_causes(self, namespace):
+        c = self.k8s_client
+        scores = self.metrics_agent.last_scores
+        if scores is not None and hasattr(c, 'get_dependency_csr'):
+            names, row_ptr, col, outdeg = c.get_dependency_csr(namespace)
+            idx, val = self.engine.rank_root_causes(scores['score'], row_ptr, col, outdeg,
+                                                    alpha=self.ppr_alpha, k=self.ppr_topk)
+            return [{'component': f"Pod/{names[i]}", 'rank': r + 1, 'score': float(v)}
+                    for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]
+        if hasattr(c, 'get_service_dependencies') and hasattr(c, 'get_error_rate_by_service'):
+            deps = c.get_service_dependencies()
+            rates = c.get_error_rate_by_service()
+            names = list(deps.keys())
+            for ds in deps.values():
+                for d in ds:
+                    if d not in names:
+                        names.append(d)
+            pos = {n: i for i, n in enumerate(names)}
+            src = [pos[s] for s, ds in deps.items() for _ in ds]
+            dst = [pos[d] for _, ds in deps.items() for d in ds]
+            row_ptr, col, outdeg = csr_from_edges(len(names), src, dst)
+            seed = np.array([rates.get(n, 0.0) for n in names], dtype=np.float32)
+            if not seed.sum() > 0:
+                return None
+            k = min(self.ppr_topk, len(names))
+            idx, val = self.engine.rank_root_causes(seed, row_ptr, col, outdeg, alpha=self.ppr_alpha, k=k)
+            return [{'component': f"Service/{names[i]}", 'rank': r + 1, 'score': float(v)}
+                    for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]
+        return None

@@ -1,0 +1,370 @@
+"""TopologyAgent: service-dependency graph, its heuristics, and its CSR export.
+
+Reference: ref:agents/topology_agent.py:4-693.  Graph construction (:94-260) and the small-graph
+heuristics (cycles :262-287, longest simple path :289-320, betweenness SPOF :322-356, isolates
+:358-401) keep the reference's exact semantics on the host with networkx 3.4.2 — the
+reference's own pinned dependency (parity at C1 and small graphs only).  The
+quirks are kept: a deployment named like a service merges into that node (``type`` becomes
+``deployment``) and its ``selects`` edge becomes a self-loop.
+
+New (additive): :meth:`dependency_csr` exports the graph as the pull-CSR the device PageRank
+kernel consumes.
+"""
+import networkx as nx
+import numpy as np
+
+from .base import BaseAgent
+
+EDGE_TYPES = ("selects", "routes", "mounts", "env_from", "env_var", "depends_on")
+
+
+def _tmpl_spec(dep):
+    return dep.get('spec', {}).get('template', {}).get('spec', {})
+
+
+class TopologyAgent(BaseAgent):
+    def __init__(self, k8s_client, engine=None):
+        super().__init__(k8s_client, engine)
+        self.service_graph = nx.DiGraph()
+
+    def analyze(self, namespace, context=None, **kwargs):
+        self.reset()
+        self.service_graph = nx.DiGraph()
+        try:
+            self._maybe_set_context(context)
+            c = self.k8s_client
+            deployments = c.get_deployments(namespace)
+            services = c.get_services(namespace)
+            pods = c.get_pods(namespace)
+            ingresses = c.get_ingresses(namespace)
+            configmaps = c.get_configmaps(namespace)
+            secrets = c.get_secrets(namespace)
+            netpols = c.get_network_policies(namespace)
+            self.add_reasoning_step(observation=f"Collected resource data from namespace {namespace}",
+                                    conclusion="Beginning topology analysis")
+            self._build_service_graph(deployments, services, pods, ingresses, configmaps, secrets)
+            if self.service_graph.number_of_nodes() > 0:
+                self._analyze_service_dependencies()
+                self._analyze_single_points_of_failure()
+                self._analyze_isolated_services()
+            self._analyze_network_policies(netpols, services)
+            self._analyze_ingress_configurations(ingresses, services)
+            self._analyze_resource_dependencies(deployments, configmaps, secrets)
+            res = self.get_results()
+            res['topology_data'] = self._prepare_topology_data()
+            return res
+        except Exception as e:
+            return self._error_result("topology", e)
+
+    # -- graph construction (ref :94-260) ------------------------------------------------
+    def _build_service_graph(self, deployments, services, pods, ingresses, configmaps, secrets):
+        g = self.service_graph
+        for s in services:
+            spec = s.get('spec', {})
+            g.add_node(s['metadata']['name'], type='service', ports=spec.get('ports', []),
+                       selector=spec.get('selector', {}))
+        for d in deployments:
+            dname = d['metadata']['name']
+            labels = d.get('metadata', {}).get('labels', {})
+            g.add_node(dname, type='deployment', replicas=d.get('spec', {}).get('replicas', 1),
+                       labels=labels, containers=len(_tmpl_spec(d).get('containers', [])))
+            for s in services:
+                sel = s.get('spec', {}).get('selector', {})
+                if all(item in labels.items() for item in sel.items()):
+                    g.add_edge(s['metadata']['name'], dname, type='selects')
+        for ing in ingresses:
+            iname = ing['metadata']['name']
+            g.add_node(iname, type='ingress')
+            for rule in ing.get('spec', {}).get('rules', []):
+                if 'http' not in rule:
+                    continue
+                for path in rule.get('http', {}).get('paths', []):
+                    backend = path.get('backend', {}).get('serviceName', None)
+                    if backend and backend in g:
+                        g.add_edge(iname, backend, type='routes')
+        self._add_config_dependencies(deployments, configmaps, secrets)
+        self._infer_dependencies_from_env(deployments, services)
+        self.add_reasoning_step(
+            observation=f"Built service graph with {g.number_of_nodes()} nodes and {g.number_of_edges()} edges",
+            conclusion="Service topology mapping complete")
+
+    def _link(self, src, dst, kind):
+        if dst in self.service_graph:
+            self.service_graph.add_edge(src, dst, type=kind)
+
+    def _add_config_dependencies(self, deployments, configmaps, secrets):
+        g = self.service_graph
+        for cm in configmaps:
+            g.add_node(cm['metadata']['name'], type='configmap')
+        for sec in secrets:
+            g.add_node(sec['metadata']['name'], type='secret')
+        for d in deployments:
+            dname = d['metadata']['name']
+            spec = _tmpl_spec(d)
+            for vol in spec.get('volumes', []):
+                if 'configMap' in vol:
+                    self._link(dname, vol['configMap']['name'], 'mounts')
+                if 'secret' in vol:
+                    self._link(dname, vol['secret']['secretName'], 'mounts')
+            for ctr in spec.get('containers', []):
+                for src in ctr.get('envFrom', []):
+                    if 'configMapRef' in src:
+                        self._link(dname, src['configMapRef']['name'], 'env_from')
+                    if 'secretRef' in src:
+                        self._link(dname, src['secretRef']['name'], 'env_from')
+                for var in ctr.get('env', []):
+                    if 'valueFrom' not in var:
+                        continue
+                    vf = var['valueFrom']
+                    if 'configMapKeyRef' in vf:
+                        self._link(dname, vf['configMapKeyRef']['name'], 'env_var')
+                    if 'secretKeyRef' in vf:
+                        self._link(dname, vf['secretKeyRef']['name'], 'env_var')
+
+    def _infer_dependencies_from_env(self, deployments, services):
+        dns = {}
+        for s in services:
+            name, ns = s['metadata']['name'], s['metadata']['namespace']
+            for key in (name, f"{name}.{ns}", f"{name}.{ns}.svc", f"{name}.{ns}.svc.cluster.local"):
+                dns[key] = name
+        for d in deployments:
+            dname = d['metadata']['name']
+            for ctr in _tmpl_spec(d).get('containers', []):
+                for var in ctr.get('env', []):
+                    value = var.get('value', '')
+                    for key, svc in dns.items():
+                        if key in value and svc in self.service_graph:
+                            self.service_graph.add_edge(dname, svc, type='depends_on')
+
+    # -- heuristics (ref :262-401) -------------------------------------------------------
+    def _analyze_service_dependencies(self):
+        g = self.service_graph
+        try:
+            cycles = list(nx.simple_cycles(g))
+            if cycles:
+                first = cycles[0]
+                self.add_finding(component="Service Architecture",
+                                 issue="Circular dependency detected in service architecture", severity="medium",
+                                 evidence=f"Dependency cycle: {' → '.join(first + [first[0]])}",
+                                 recommendation="Refactor the service architecture to eliminate circular dependencies")
+                self.add_reasoning_step(observation=f"Detected {len(cycles)} circular dependencies in the service graph",
+                                        conclusion="Circular dependencies can lead to deployment and scaling issues")
+        except Exception as e:
+            self.add_reasoning_step(observation=f"Error detecting cycles: {str(e)}",
+                                    conclusion="Unable to analyze circular dependencies")
+        best, best_len = None, 0
+        nodes = list(g.nodes())
+        for src in nodes:
+            for dst in nodes:
+                if src == dst:
+                    continue
+                try:
+                    paths = list(nx.all_simple_paths(g, src, dst))
+                except nx.NetworkXNoPath:
+                    continue
+                if paths:
+                    longest = max(paths, key=len)
+                    if len(longest) > best_len:
+                        best_len, best = len(longest), longest
+        if best and len(best) >= 4:
+            chain = ' → '.join(best)
+            self.add_finding(component="Service Architecture", issue="Long dependency chain detected", severity="low",
+                             evidence=f"Long dependency path: {chain}",
+                             recommendation="Consider simplifying the architecture or implementing caching to reduce dependency chain impacts")
+            self.add_reasoning_step(observation=f"Detected a dependency chain of length {len(best)}: {chain}",
+                                    conclusion="Long dependency chains can increase latency and reduce reliability")
+
+    def _analyze_single_points_of_failure(self):
+        g = self.service_graph
+        try:
+            bc = nx.betweenness_centrality(g)
+            for node in [n for n, v in bc.items() if v > 0.5]:
+                ntype = g.nodes[node].get('type', 'unknown')
+                if ntype not in ('deployment', 'service'):
+                    continue
+                replicas = g.nodes[node].get('replicas', 1) if ntype == 'deployment' else 1
+                if replicas < 2:
+                    self.add_finding(component=f"{ntype.capitalize()}/{node}",
+                                     issue="Potential single point of failure with high centrality", severity="high",
+                                     evidence=f"This {ntype} is a central component with only {replicas} replica",
+                                     recommendation="Increase the number of replicas and consider implementing redundancy")
+                    self.add_reasoning_step(observation=f"Detected {node} as a central component with low redundancy",
+                                            conclusion="This component could be a single point of failure")
+        except Exception as e:
+            self.add_reasoning_step(observation=f"Error analyzing single points of failure: {str(e)}",
+                                    conclusion="Unable to identify potential single points of failure")
+
+    def _analyze_isolated_services(self):
+        g = self.service_graph
+        iso = list(nx.isolates(g))
+        for ntype, label, sev, rec, concl in (
+                ('service', 'services', 'low',
+                 "Verify if these services are still needed or if they should be connected to other components",
+                 "These services may be unused or misconfigured"),
+                ('deployment', 'deployments', 'medium',
+                 "Verify if these deployments are still needed or if they should be exposed via services",
+                 "These deployments may be unused or missing service selectors")):
+            names = [n for n in iso if g.nodes[n].get('type') == ntype]
+            if not names:
+                continue
+            what = "Services" if ntype == 'service' else "Deployments"
+            self.add_finding(component="Service Architecture", issue=f"Found {len(names)} isolated {label}",
+                             severity=sev, evidence=f"{what} without connections: {', '.join(names)}",
+                             recommendation=rec)
+            self.add_reasoning_step(observation=f"Detected {len(names)} {label} with no connections", conclusion=concl)
+
+    # -- policy / ingress / references (ref :403-655) ------------------------------------
+    def _analyze_network_policies(self, netpols, services):
+        if not netpols:
+            self.add_reasoning_step(observation="No network policies found in the namespace",
+                                    conclusion="No network security restrictions are in place")
+            if len(services) > 1:
+                self.add_finding(component="Network Security",
+                                 issue="No network policies defined in a multi-service namespace", severity="medium",
+                                 evidence=f"Found {len(services)} services but no network policies",
+                                 recommendation="Implement network policies to restrict communication between services")
+            return
+        self.add_reasoning_step(observation=f"Found {len(netpols)} network policies",
+                                conclusion="Analyzing network policy configurations")
+        permissive = []
+        for pol in netpols:
+            pname = pol['metadata']['name']
+            for rule in pol.get('spec', {}).get('ingress', []):
+                if not rule:
+                    permissive.append((pname, 'ingress', 'empty rule'))
+                elif 'from' not in rule or not rule['from']:
+                    permissive.append((pname, 'ingress', 'no from selector'))
+        if permissive:
+            self.add_finding(component="Network Policies", issue="Overly permissive network policies detected",
+                             severity="medium",
+                             evidence="Permissive policies: " + ", ".join(f"{n} ({k}: {i})" for n, k, i in permissive),
+                             recommendation="Restrict network policies to allow only necessary communication")
+            self.add_reasoning_step(observation=f"Detected {len(permissive)} overly permissive network policies",
+                                    conclusion="These policies may allow unnecessary network access")
+        covered = set()
+        for pol in netpols:
+            match = pol.get('spec', {}).get('podSelector', {}).get('matchLabels', {})
+            for s in services:
+                sel = s.get('spec', {}).get('selector', {})
+                if all(item in sel.items() for item in match.items()):
+                    covered.add(s['metadata']['name'])
+        # the reference prints a set difference (hash order); list order here is not
+        # significant and tests compare these names as a set
+        uncovered = {s['metadata']['name'] for s in services} - covered
+        if uncovered:
+            self.add_finding(component="Network Policies",
+                             issue=f"Found {len(uncovered)} services without network policies", severity="medium",
+                             evidence=f"Services without network policies: {', '.join(uncovered)}",
+                             recommendation="Implement network policies for all services to secure communication")
+            self.add_reasoning_step(observation=f"Detected {len(uncovered)} services without network policies",
+                                    conclusion="These services may accept traffic from any source")
+
+    def _analyze_ingress_configurations(self, ingresses, services):
+        if not ingresses:
+            cands = [s['metadata']['name'] for s in services
+                     if s.get('spec', {}).get('type', 'ClusterIP') == 'ClusterIP'
+                     and any(k in s['metadata']['name'].lower() for k in ('api', 'web', 'ui', 'frontend'))]
+            if cands:
+                self.add_finding(component="External Access",
+                                 issue="Potential external services without Ingress resources", severity="low",
+                                 evidence=f"Services that might need external access: {', '.join(cands)}",
+                                 recommendation="Consider creating Ingress resources for services that require external access")
+            return
+        self.add_reasoning_step(observation=f"Found {len(ingresses)} ingress resources",
+                                conclusion="Analyzing ingress configurations")
+        no_tls = [i['metadata']['name'] for i in ingresses if not i.get('spec', {}).get('tls', [])]
+        if no_tls:
+            self.add_finding(component="Ingress Security",
+                             issue=f"Found {len(no_tls)} ingresses without TLS configuration", severity="high",
+                             evidence=f"Ingresses without TLS: {', '.join(no_tls)}",
+                             recommendation="Configure TLS for all ingress resources to ensure encrypted communication")
+            self.add_reasoning_step(observation=f"Detected {len(no_tls)} ingresses without TLS",
+                                    conclusion="These ingresses are exposing services over unencrypted HTTP")
+        names = {s['metadata']['name'] for s in services}
+        broken = []
+        for ing in ingresses:
+            for rule in ing.get('spec', {}).get('rules', []):
+                if 'http' in rule:
+                    for path in rule.get('http', {}).get('paths', []):
+                        b = path.get('backend', {}).get('serviceName', None)
+                        if b and b not in names:
+                            broken.append((ing['metadata']['name'], b))
+        if broken:
+            self.add_finding(component="Ingress Configuration",
+                             issue=f"Found {len(broken)} ingress rules pointing to non-existent services",
+                             severity="high",
+                             evidence="Broken ingress rules: " + ", ".join(f"{i} → {s}" for i, s in broken),
+                             recommendation="Update or remove ingress rules pointing to non-existent services")
+            self.add_reasoning_step(observation=f"Detected {len(broken)} ingress rules with invalid service references",
+                                    conclusion="These ingress rules will not work as expected")
+
+    def _analyze_resource_dependencies(self, deployments, configmaps, secrets):
+        cms = {c['metadata']['name'] for c in configmaps}
+        secs = {s['metadata']['name'] for s in secrets}
+        missing = []
+        for d in deployments:
+            dname = d['metadata']['name']
+            spec = _tmpl_spec(d)
+            for vol in spec.get('volumes', []):
+                if 'configMap' in vol and vol['configMap']['name'] not in cms:
+                    missing.append((dname, 'ConfigMap', vol['configMap']['name']))
+                if 'secret' in vol and vol['secret']['secretName'] not in secs:
+                    missing.append((dname, 'Secret', vol['secret']['secretName']))
+            for ctr in spec.get('containers', []):
+                for src in ctr.get('envFrom', []):
+                    if 'configMapRef' in src and src['configMapRef']['name'] not in cms:
+                        missing.append((dname, 'ConfigMap', src['configMapRef']['name']))
+                    if 'secretRef' in src and src['secretRef']['name'] not in secs:
+                        missing.append((dname, 'Secret', src['secretRef']['name']))
+                for var in ctr.get('env', []):
+                    if 'valueFrom' not in var:
+                        continue
+                    vf = var['valueFrom']
+                    if 'configMapKeyRef' in vf and vf['configMapKeyRef']['name'] not in cms:
+                        missing.append((dname, 'ConfigMap', vf['configMapKeyRef']['name']))
+                    if 'secretKeyRef' in vf and vf['secretKeyRef']['name'] not in secs:
+                        missing.append((dname, 'Secret', vf['secretKeyRef']['name']))
+        if missing:
+            refs = ", ".join(f"{d} → {k}/{n}" for d, k, n in missing)
+            self.add_finding(component="Resource Dependencies",
+                             issue=f"Found {len(missing)} references to non-existent resources", severity="high",
+                             evidence=f"Missing references: {refs}",
+                             recommendation="Create the missing ConfigMaps and Secrets, or update the deployments to reference existing resources")
+            self.add_reasoning_step(observation=f"Detected {len(missing)} references to non-existent ConfigMaps or Secrets",
+                                    conclusion="These missing dependencies will prevent pods from starting correctly")
+
+    def _prepare_topology_data(self):
+        g = self.service_graph
+        nodes = [{'id': n, 'label': n, 'type': g.nodes[n].get('type', 'unknown'), 'data': g.nodes[n]} for n in g.nodes()]
+        edges = [{'source': s, 'target': t, 'label': d.get('type', 'unknown'), 'type': d.get('type', 'unknown')}
+                 for s, t, d in g.edges(data=True)]
+        return {'nodes': nodes, 'edges': edges}
+
+    # -- additive: pull-CSR of the current graph -----------------------
+    def dependency_csr(self):
+        """Return (names, in_row_ptr int64[N+1], in_col int32[E], out_degree int32[N], edge_type uint8[E]).
+
+        Row i of the pull-CSR lists the sources j of edges j -> i (so PageRank gathers), in
+        edge-insertion order; ``edge_type`` indexes :data:`EDGE_TYPES`.
+        """
+        g = self.service_graph
+        names = list(g.nodes())
+        idx = {n: i for i, n in enumerate(names)}
+        src = np.array([idx[s] for s, _ in g.edges()], dtype=np.int64)
+        dst = np.array([idx[t] for _, t in g.edges()], dtype=np.int64)
+        et = np.array([EDGE_TYPES.index(d.get('type')) if d.get('type') in EDGE_TYPES else 255
+                       for _, _, d in g.edges(data=True)], dtype=np.uint8)
+        return (names,) + csr_from_edges(len(names), src, dst) + (et[np.argsort(dst, kind='stable')] if len(et) else et,)
+
+
+def csr_from_edges(n, src, dst):
+    """Pull-CSR (rows = destinations) from an edge list; stable in edge order within a row."""
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    order = np.argsort(dst, kind='stable')
+    col = src[order].astype(np.int32)
+    row_ptr = np.zeros(n + 1, dtype=np.int64)
+    if len(dst):
+        np.cumsum(np.bincount(dst, minlength=n), out=row_ptr[1:])
+    outdeg = np.bincount(src, minlength=n).astype(np.int32) if len(src) else np.zeros(n, np.int32)
+    return row_ptr, col, outdeg

@@ -1,0 +1,192 @@
+"""Seeded synthetic meshes: pod metric tensors, dependency CSR, log corpora.
+
+Shapes follow the reference's mock cluster (ref:utils/mock_k8s_client.py:468-495: per-pod CPU /
+memory usage percentages; :909-934 per-container log text; :1251-1272 a caller -> dependency
+map) scaled to the BASELINE configs (C2: 10k pods / 200k edges, C4: 1M pods / 20M edges,
+M = 8 metrics x T = 1440 steps).  Metrics are generated with torch on any device (the 46 GB C4
+tensor is generated in place on the GPU); graphs with NumPy on the host.
+
+Metric model:  x[t,p,m] = clip(b + a*sin(2*pi*t/1440 + phi_p) + N(0, sigma^2), 0, 100),
+b ~ U(10,60), a ~ U(0,15), sigma ~ U(0.5,3); R root pods get a +6 sigma step over the last W
+steps and their callers (1..3 hops) a decayed +2 sigma step.  Channel 0 = CPU %, 1 = memory %.
+Graph model: pods grouped into services of 20; services wired by preferential attachment
+(caller -> callee); each pod calls ~deg pods of its service's callees; no self loops, no
+duplicate edges; edge direction symptom(caller) -> dependency.
+"""
+import math
+
+import numpy as np
+
+
+class Mesh:
+    def __init__(self, n_pods, row_ptr, col, outdeg, roots, names=None):
+        self.n_pods = n_pods
+        self.row_ptr = row_ptr  # pull-CSR: row i = callers j of i (edges j -> i), int64[N+1]
+        self.col = col          # int32[E]
+        self.outdeg = outdeg    # int32[N]
+        self.roots = roots      # int64[R] planted root causes
+        self._names = names
+
+    @property
+    def n_edges(self):
+        return int(self.row_ptr[-1])
+
+    def names(self):
+        if self._names is None:
+            self._names = [f"pod-{i:07d}" for i in range(self.n_pods)]
+        return self._names
+
+
+def _services_ba(n_services, m, rng):
+    """Preferential attachment over services; returns (caller, callee) arrays."""
+    m = max(1, min(m, n_services - 1)) if n_services > 1 else 0
+    src, dst = [], []
+    targets = list(range(m))
+    repeated = []
+    for s in range(m, n_services):
+        chosen = set()
+        while len(chosen) < m:
+            if repeated and rng.random() < 0.8:
+                chosen.add(repeated[int(rng.integers(len(repeated)))])
+            else:
+                chosen.add(int(rng.integers(s)))
+        for c in chosen:
+            src.append(s)
+            dst.append(c)
+        repeated.extend(chosen)
+        repeated.extend([s] * m)
+    del targets
+    return np.asarray(src, np.int64), np.asarray(dst, np.int64)
+
+
+def make_graph(n_pods, avg_degree=20, service_size=20, seed=0, n_roots=10, m_services=4):
+    rng = np.random.default_rng(seed)
+    n_srv = max(1, math.ceil(n_pods / service_size))
+    s_src, s_dst = _services_ba(n_srv, m_services, rng)
+    # callee lists per service (CSR over services)
+    order = np.argsort(s_src, kind="stable")
+    callee = s_dst[order]
+    cptr = np.zeros(n_srv + 1, np.int64)
+    np.cumsum(np.bincount(s_src, minlength=n_srv), out=cptr[1:])
+    pod_srv = np.arange(n_pods, dtype=np.int64) // service_size
+    ncallee = (cptr[1:] - cptr[:-1])[pod_srv]
+    deg = rng.poisson(avg_degree, n_pods).astype(np.int64)
+    deg[ncallee == 0] = 0
+    src = np.repeat(np.arange(n_pods, dtype=np.int64), deg)
+    k = rng.integers(0, np.iinfo(np.int64).max, len(src)) % np.repeat(np.maximum(ncallee, 1), deg)
+    tsrv = callee[cptr[pod_srv[src]] + k]
+    lo = tsrv * service_size
+    hi = np.minimum(lo + service_size, n_pods)
+    dst = lo + rng.integers(0, np.iinfo(np.int64).max, len(src)) % (hi - lo)
+    keep = src != dst
+    key = np.unique(src[keep] * n_pods + dst[keep])
+    src, dst = key // n_pods, key % n_pods
+    order = np.lexsort((src, dst))  # rows by destination, callers ascending inside a row
+    col = src[order].astype(np.int32)
+    row_ptr = np.zeros(n_pods + 1, np.int64)
+    np.cumsum(np.bincount(dst, minlength=n_pods), out=row_ptr[1:])
+    outdeg = np.bincount(src, minlength=n_pods).astype(np.int32)
+    # roots: pods of distinct, well-called services
+    indeg = np.diff(row_ptr)
+    cand = np.argsort(-indeg, kind="stable")[: max(n_roots * 50, n_roots)]
+    roots = np.sort(rng.choice(cand, size=min(n_roots, len(cand)), replace=False)).astype(np.int64)
+    return Mesh(n_pods, row_ptr, col, outdeg, roots)
+
+
+def caller_hops(mesh, roots, hops=3, cap=2000):
+    """Pods that (transitively) call the roots: list of int64 arrays per hop (capped)."""
+    seen = set(int(r) for r in roots)
+    frontier = np.asarray(roots, np.int64)
+    out = []
+    for _ in range(hops):
+        nxt = []
+        for r in frontier:
+            nxt.extend(mesh.col[mesh.row_ptr[r]:mesh.row_ptr[r + 1]].tolist())
+        nxt = [c for c in dict.fromkeys(nxt) if c not in seen][:cap]
+        seen.update(nxt)
+        frontier = np.asarray(nxt, np.int64)
+        out.append(frontier)
+    return out
+
+
+def make_metrics(n_pods, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(), hop_sets=(), device="cpu",
+                 dtype=None, chunk_steps=None):
+    """-> torch.float32 tensor [T, P, M] (time-major) on `device`."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    P, M, T = n_pods, n_metrics, n_steps
+    b = torch.rand((P, M), generator=g, device=device) * 50 + 10
+    a = torch.rand((P, M), generator=g, device=device) * 15
+    sig = torch.rand((P, M), generator=g, device=device) * 2.5 + 0.5
+    phi = torch.rand((P, 1), generator=g, device=device) * (2 * math.pi)
+    x = torch.empty((T, P, M), dtype=torch.float32, device=device)
+    cs = chunk_steps or max(1, min(T, (1 << 28) // max(P * M, 1)))
+    for t0 in range(0, T, cs):
+        t1 = min(T, t0 + cs)
+        tt = torch.arange(t0, t1, device=device, dtype=torch.float32).view(-1, 1, 1)
+        blk = b + a * torch.sin(2 * math.pi * tt / 1440.0 + phi) + sig * torch.randn(
+            (t1 - t0, P, M), generator=g, device=device)
+        x[t0:t1] = blk.clamp_(0.0, 100.0)
+    w0 = max(0, T - window)
+    if len(roots):
+        r = torch.as_tensor(np.asarray(roots), device=device)
+        x[w0:, r, :] = (x[w0:, r, :] + 6.0 * sig[r]).clamp_(0.0, 100.0)
+    for h, pods in enumerate(hop_sets):
+        if len(pods):
+            pr = torch.as_tensor(np.asarray(pods), device=device)
+            x[w0:, pr, :] = (x[w0:, pr, :] + (2.0 * 0.6 ** h) * sig[pr]).clamp_(0.0, 100.0)
+    return x
+
+
+# ------------------------------------------------------------------------------------------
+# log corpora (C5 shape): ASCII templates per category plus benign ones, 60-200 B lines
+# ------------------------------------------------------------------------------------------
+ERROR_LINES = (
+    "Out of memory: Kill process {n} ({w}) score {m}", "container {w} OOMKilled", "signal: killed",
+    "dial tcp 10.0.{m}.{n}:5432: connect: connection refused", "Connection refused by {w}",
+    "open /var/lib/{w}: permission denied", "403 Forbidden: {w}", "Access denied for {w}",
+    "request to {w} timed out after {n}ms", "Timeout waiting for {w}", "read tcp: ETIMEDOUT",
+    "Back-off restarting failed container {w}", "pod {w} CrashLoopBackOff",
+    "API server error: {w}", "upstream StatusCode=50{d}", "Unable to mount volumes for pod {w}",
+    "MountVolume.SetUp failed for volume {w}", "ErrImagePull {w}:{n}", "ImagePullBackOff {w}",
+    "DNS resolution failed for {w}", "could not resolve host {w}", "Unauthorized {w}",
+    "Authentication failed for {w}", "Invalid configuration {w}", "ConfigMap not found {w}",
+    "Secret not found {w}", "500 Internal Server Error {w}", "InternalServerError {w}",
+    "Exception in {w}", "ERROR processing batch {n}", "Traceback (most recent call last)",
+    "FATAL {w}", "CRITICAL {w}", "panic: {w}",
+)
+BENIGN_LINES = (
+    "INFO GET /api/v1/{w} 200 {n}ms", "DEBUG cache ratio 0.{n}", "Starting worker {n} queue {w}",
+    "healthcheck ok {n}", "INFO request id={h} user={w} latency={n}ms", "Reconciling {w} gen {n}",
+    "listening on 0.0.0.0:{n}", "WARN slow query {n}ms on {w}", "connected to {w}:{n}",
+)
+_WORDS = ("frontend", "backend", "db", "cache", "payments", "auth", "queue", "search", "gateway")
+
+
+def make_log_corpus(n_docs, lines_per_doc=2.5, error_rate=0.3, seed=0, hazard_rate=0.0):
+    """-> list[str] of container log texts (Poisson line counts, '\\n' separated)."""
+    rng = np.random.default_rng(seed)
+    counts = rng.poisson(lines_per_doc, n_docs)
+    total = int(counts.sum())
+    is_err = rng.random(total) < error_rate
+    e_idx = rng.integers(0, len(ERROR_LINES), total)
+    b_idx = rng.integers(0, len(BENIGN_LINES), total)
+    ns = rng.integers(0, 100000, total)
+    ms = rng.integers(0, 256, total)
+    ws = rng.integers(0, len(_WORDS), total)
+    pad = rng.integers(20, 120, total)
+    hz = rng.random(total) < hazard_rate
+    lines = []
+    for i in range(total):
+        t = ERROR_LINES[e_idx[i]] if is_err[i] else BENIGN_LINES[b_idx[i]]
+        s = t.format(n=int(ns[i]), m=int(ms[i]), w=_WORDS[ws[i]], d=int(ns[i]) % 10, h="%08x" % int(ns[i]))
+        s = "2024-05-01T00:00:%02d.%03dZ " % (int(ms[i]) % 60, int(ns[i]) % 1000) + s + " " + "k" * int(pad[i] // 4)
+        if hz[i]:
+            s += " café Kelvin ſ"
+        lines.append(s)
+    docs, k = [], 0
+    for c in counts:
+        docs.append("\n".join(lines[k:k + c]) + ("\n" if c and rng.random() < 0.5 else ""))
+        k += c
+    return docs

@@ -1,0 +1,139 @@
+/*
+ * krca_oracle.c — CPU restatement of the krca numeric core.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library;
+ * the product path (krca.native -> libkrca.so) never does.  It restates, with the same
+ * arithmetic in the same order, the device algorithms of include/krca.h, so that integer
+ * outputs can be compared bit-for-bit:
+ *
+ *   krco_usage_flags    ref:agents/metrics_agent.py:88-114, 135-161 (x > 80, high if > 90)
+ *   krco_rolling_score  rolling z-score (new primitive, no reference code):
+ *                       float64 sliding sums in a fixed order, |z| > thr <=> d*d > thr^2*var
+ *   krco_ppr            networkx 3.4.2 pagerank semantics (_pagerank_scipy) in 2^-60 fixed point
+ *
+ * The floating-point reference for a5/a10 (float64, independent formulation) is the NumPy
+ * oracle in oracle/oracle.py; this file pins the exact bits.  Build: oracle/Makefile
+ * (gcc -O2 -fopenmp -ffp-contract=off).  OpenMP parallelises over independent series / nodes
+ * only; every per-element computation is the sequential restatement.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define VAR_EPS 1e-12
+static const double kFix = 1152921504606846976.0; /* 2^60 */
+
+void krco_usage_flags(const float* usage, int64_t P, uint8_t* flags) {
+  for (int64_t p = 0; p < P; ++p) {
+    const float c = usage[2 * p], m = usage[2 * p + 1];
+    flags[p] = (uint8_t)((c > 80.f ? 1 : 0) | (c > 90.f ? 2 : 0) | (m > 80.f ? 4 : 0) | (m > 90.f ? 8 : 0));
+  }
+}
+
+/* x: time-major [T][P][M] float32.  Same outputs as krca_rolling_score. */
+void krco_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr, float* z_last,
+                        float* score, int32_t* n_exceed, uint8_t* flags) {
+  const int64_t S = P * (int64_t)M;
+  const double invW = 1.0 / (double)W;
+  const double thr2 = (double)z_thr * (double)z_thr;
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < P; ++p) {
+    float best = 0.f;
+    int32_t cnt = 0;
+    unsigned f = 0;
+    for (int32_t m = 0; m < M; ++m) {
+      const int64_t s = p * M + m;
+      double s1 = 0.0, s2 = 0.0, dl = 0.0, varl = 0.0;
+      for (int32_t j = 0; j < W && j < T; ++j) {
+        const double vd = (double)x[(int64_t)j * S + s];
+        s1 = s1 + vd;
+        s2 = s2 + vd * vd;
+      }
+      for (int32_t t = W; t < T; ++t) {
+        const double vd = (double)x[(int64_t)t * S + s];
+        const double mean = s1 * invW;
+        const double var = s2 * invW - mean * mean;
+        const double d = vd - mean;
+        cnt += (var > VAR_EPS) && (d * d > thr2 * var);
+        if (t == T - 1) {
+          dl = d;
+          varl = var;
+        }
+        const double od = (double)x[(int64_t)(t - W) * S + s];
+        s1 = s1 + (vd - od);
+        s2 = s2 + (vd * vd - od * od);
+      }
+      const float z = varl > VAR_EPS ? (float)(dl / sqrt(varl)) : 0.f;
+      z_last[s] = z;
+      const float az = fabsf(z);
+      if (az > best) best = az;
+      if (T > 0) {
+        const float v = x[(int64_t)(T - 1) * S + s];
+        if (m == 0) f |= (v > 80.f ? 1u : 0u) | (v > 90.f ? 2u : 0u);
+        if (m == 1) f |= (v > 80.f ? 4u : 0u) | (v > 90.f ? 8u : 0u);
+      }
+    }
+    score[p] = best;
+    n_exceed[p] = cnt;
+    flags[p] = (uint8_t)f;
+  }
+}
+
+static int64_t edge_weight(int64_t rj, int32_t deg, double alpha) {
+  if (deg == 0) return 0;
+  const double coef = alpha / (double)deg;
+  return (int64_t)((double)rj * coef);
+}
+
+/* Pull-CSR personalized PageRank; returns iterations (negative if no convergence). */
+int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const float* seed,
+                 double alpha, int32_t max_iter, double tol, int64_t* r, float* r_out) {
+  int64_t* q = (int64_t*)malloc(sizeof(int64_t) * N);
+  int64_t* w = (int64_t*)malloc(sizeof(int64_t) * N);
+  int64_t qtot = 0, dang = 0;
+  const int64_t r0 = (int64_t)(kFix / (double)N);
+  for (int64_t i = 0; i < N; ++i) {
+    const float s = seed[i];
+    q[i] = s > 0.f ? (int64_t)((double)s * 4294967296.0) : 0;
+    qtot += q[i];
+    r[i] = r0;
+    w[i] = edge_weight(r0, outdeg[i], alpha);
+    if (outdeg[i] == 0) dang += r0;
+  }
+  const double err_limit = tol > 0.0 ? (double)N * tol * kFix : 0.0;
+  double tele = (1.0 - alpha) * kFix + alpha * (double)dang;
+  int32_t it = 0, conv = 0;
+  int64_t* acc = (int64_t*)malloc(sizeof(int64_t) * N);
+  while (it < max_iter) {
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int64_t i = 0; i < N; ++i) {
+      int64_t s = 0;
+      for (int64_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) s += w[col[e]];
+      acc[i] = s;
+    }
+    int64_t err = 0, dn = 0;
+    const double qd = (double)qtot;
+    for (int64_t i = 0; i < N; ++i) {
+      const double pd = (double)q[i] / qd;
+      const int64_t t = (int64_t)(pd * tele);
+      const int64_t rn = acc[i] + t;
+      const int64_t ro = r[i];
+      r[i] = rn;
+      err += rn > ro ? rn - ro : ro - rn;
+      if (outdeg[i] == 0) dn += rn;
+      w[i] = edge_weight(rn, outdeg[i], alpha);
+    }
+    ++it;
+    if (err_limit > 0.0 && (double)err < err_limit) {
+      conv = 1;
+      break;
+    }
+    tele = (1.0 - alpha) * kFix + alpha * (double)dn;
+  }
+  for (int64_t i = 0; i < N; ++i) r_out[i] = (float)((double)r[i] * (1.0 / kFix));
+  free(q);
+  free(w);
+  free(acc);
+  return (err_limit > 0.0 && !conv) ? -it : it;
+}

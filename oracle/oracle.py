@@ -1,0 +1,180 @@
+"""CPU oracle for the krca numeric core.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg import this module.
+It is the checker, never the thing measured or shipped.
+
+Parity anchors:
+  * log histograms: :func:`log_hist` restates ref:agents/logs_agent.py:140-151 literally
+    (``str.splitlines`` + ``re.search(p, line, re.IGNORECASE)`` with the reference's 13
+    patterns) and is pinned by tests/golden/logs_corpus.json, captured from the reference;
+  * thresholds: pinned by tests/golden/metrics_scaled.json and the C1 goldens;
+  * PageRank: :func:`ppr_f64` is the networkx 3.4.2 ``_pagerank_scipy`` iteration in float64,
+    pinned by tests/golden/ppr_known.json (networkx on the reference's mock dependency map);
+  * rolling z-score / correlation / template hashing have no reference counterpart (new
+    primitives named by the north star): their float64 restatements here are
+    "parity unpinned" by the reference and define the semantics.
+The bit-exact twins of the device arithmetic live in oracle/krca_oracle.c (:func:`c_lib`).
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ERROR_PATTERNS = (  # ref:agents/logs_agent.py:20-34 (data)
+    ("oom_kill", r"(Out of memory|OOMKilled|Killed|signal: killed)"),
+    ("connection_refused", r"(Connection refused|connect: connection refused)"),
+    ("permission_denied", r"(Permission denied|Forbidden|Access denied)"),
+    ("timeout", r"(timeout|Timeout|timed out|ETIMEDOUT)"),
+    ("crash_loop", r"(CrashLoopBackOff|Back-off restarting)"),
+    ("api_error", r"(API server error|StatusCode=5\d\d)"),
+    ("volume_mount", r"(Unable to mount volumes|MountVolume.SetUp failed)"),
+    ("image_pull", r"(ErrImagePull|ImagePullBackOff)"),
+    ("dns_resolution", r"(DNS resolution failed|could not resolve)"),
+    ("authentication", r"(Unauthorized|Authentication failed)"),
+    ("config_error", r"(Invalid configuration|ConfigMap not found|Secret not found)"),
+    ("internal_server_error", r"(internal server error|InternalServerError|500 Internal Server Error)"),
+    ("exception", r"(Exception|Error|Traceback|FATAL|CRITICAL|Panic|panic:)"),
+)
+_COMPILED = [re.compile(p, re.IGNORECASE) for _, p in ERROR_PATTERNS]
+
+
+# ------------------------------------------------------------------------------------------
+# logs (a12)
+# ------------------------------------------------------------------------------------------
+def line_mask(line):
+    m = 0
+    for b, rx in enumerate(_COMPILED):
+        if rx.search(line):
+            m |= 1 << b
+    return m
+
+
+def log_hist(text):
+    """-> (n_lines, hist[13], first3[13] list of line strings) for one container's log text."""
+    lines = text.splitlines()
+    hist = [0] * 13
+    ex = [[] for _ in range(13)]
+    for ln in lines:
+        m = line_mask(ln)
+        for c in range(13):
+            if m >> c & 1:
+                hist[c] += 1
+                if len(ex[c]) < 3:
+                    ex[c].append(ln)
+    return len(lines), hist, ex
+
+
+# ------------------------------------------------------------------------------------------
+# rolling z-score (a5), float64 independent formulation (prefix sums)
+# ------------------------------------------------------------------------------------------
+def rolling_score_f64(x, W, z_thr=3.0):
+    """x [T, P, M] -> (z_last [P, M], score [P], n_exceed [P]) in float64 / int."""
+    x = np.asarray(x, dtype=np.float64)
+    T, P, M = x.shape
+    if T <= W:
+        return np.zeros((P, M)), np.zeros(P), np.zeros(P, np.int64)
+    c1 = np.concatenate([np.zeros((1, P, M)), np.cumsum(x, axis=0)])
+    c2 = np.concatenate([np.zeros((1, P, M)), np.cumsum(x * x, axis=0)])
+    t = np.arange(W, T)
+    s1 = c1[t] - c1[t - W]
+    s2 = c2[t] - c2[t - W]
+    mean = s1 / W
+    var = np.maximum(s2 / W - mean * mean, 0.0)
+    d = x[W:] - mean
+    ok = var > 1e-12
+    z = np.where(ok, d / np.sqrt(np.where(ok, var, 1.0)), 0.0)
+    n = (np.abs(z) > z_thr).sum(axis=(0, 2))
+    zl = z[-1]
+    return zl, np.abs(zl).max(axis=1), n
+
+
+# ------------------------------------------------------------------------------------------
+# personalized PageRank (a10): networkx 3.4.2 iteration in float64
+# ------------------------------------------------------------------------------------------
+def ppr_f64(row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6):
+    row_ptr = np.asarray(row_ptr, np.int64)
+    col = np.asarray(col, np.int64)
+    outdeg = np.asarray(outdeg, np.float64)
+    N = len(outdeg)
+    p = np.maximum(np.asarray(seed, np.float64), 0.0)
+    p = p / p.sum()
+    inv = np.where(outdeg > 0, 1.0 / np.where(outdeg > 0, outdeg, 1.0), 0.0)
+    dangling = outdeg == 0
+    rows = np.repeat(np.arange(N), np.diff(row_ptr))
+    x = np.full(N, 1.0 / N)
+    for it in range(max_iter):
+        xl = x
+        contrib = (xl * inv)[col]
+        y = np.bincount(rows, weights=contrib, minlength=N)
+        x = alpha * (y + xl[dangling].sum() * p) + (1 - alpha) * p
+        if tol > 0 and np.abs(x - xl).sum() < N * tol:
+            return x, it + 1
+    return x, max_iter
+
+
+def topk_ref(v, k):
+    """Descending, ties -> lower index (the device contract)."""
+    v = np.asarray(v)
+    order = np.lexsort((np.arange(len(v)), -v.astype(np.float64) if v.dtype.kind == "f" else -v))
+    idx = order[:k]
+    return idx.astype(np.int32), v[idx]
+
+
+# ------------------------------------------------------------------------------------------
+# C restatement (bit-exact twin of the device arithmetic)
+# ------------------------------------------------------------------------------------------
+_c = None
+
+
+def c_lib():
+    global _c
+    if _c is not None:
+        return _c
+    path = os.path.join(HERE, "_build", "libkrca_oracle.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+    lib = ctypes.CDLL(path)
+    vp, i64, i32, f32, f64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double
+    lib.krco_usage_flags.argtypes = [vp, i64, vp]
+    lib.krco_rolling_score.argtypes = [vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]
+    lib.krco_ppr.argtypes = [vp, vp, vp, i64, vp, f64, i32, f64, vp, vp]
+    lib.krco_ppr.restype = i32
+    _c = lib
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def c_usage_flags(usage):
+    u = np.ascontiguousarray(usage, np.float32).reshape(-1, 2)
+    out = np.zeros(len(u), np.uint8)
+    c_lib().krco_usage_flags(_p(u), len(u), _p(out))
+    return out
+
+
+def c_rolling_score(x, W, z_thr=3.0):
+    x = np.ascontiguousarray(x, np.float32)
+    T, P, M = x.shape
+    z = np.zeros((P, M), np.float32)
+    s = np.zeros(P, np.float32)
+    n = np.zeros(P, np.int32)
+    f = np.zeros(P, np.uint8)
+    c_lib().krco_rolling_score(_p(x), P, M, T, W, z_thr, _p(z), _p(s), _p(n), _p(f))
+    return dict(z_last=z, score=s, n_exceed=n, flags=f)
+
+
+def c_ppr(row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6):
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    od = np.ascontiguousarray(outdeg, np.int32)
+    sd = np.ascontiguousarray(seed, np.float32)
+    N = len(od)
+    r = np.zeros(N, np.int64)
+    rf = np.zeros(N, np.float32)
+    it = c_lib().krco_ppr(_p(rp), _p(cl), _p(od), N, _p(sd), alpha, max_iter, tol, _p(r), _p(rf))
+    return rf, r, it

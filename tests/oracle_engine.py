@@ -1,0 +1,54 @@
+"""CPU stand-in for krca.native.NativeEngine, built from oracle/ — TESTS ONLY.
+
+It lets the CPU test suite exercise the agents' host logic (findings formatting, ordering,
+error contracts) against the reference goldens without a GPU.  The product path never uses
+it: krca.native.default_engine() has no CPU fallback.
+"""
+import numpy as np
+
+import oracle
+
+
+class OracleLogScan:
+    def __init__(self, docs):
+        self.n_lines, self.hist, self._ex = [], [], []
+        for text in docs:
+            n, h, ex = oracle.log_hist(text)
+            self.n_lines.append(n)
+            self.hist.append(h)
+            self._ex.append(ex)
+        self.n_lines = np.asarray(self.n_lines, np.int32)
+        self.hist = np.asarray(self.hist, np.int32).reshape(-1, 13)
+
+    def examples(self, d, c):
+        return self._ex[d][c]
+
+
+class OracleEngine:
+    def usage_flags(self, usage):
+        return oracle.c_usage_flags(usage)
+
+    def rolling_score(self, x, window=60, z_threshold=3.0):
+        x = np.asarray(x.cpu() if hasattr(x, "cpu") else x, np.float32)
+        r = oracle.c_rolling_score(x, window, z_threshold)
+        r["n_exceed_host"] = r["n_exceed"]
+        r["_x"] = x
+        return r
+
+    def gather_last(self, x, idx):
+        x = np.asarray(x.cpu() if hasattr(x, "cpu") else x, np.float32)
+        return x[-1][np.asarray(idx, np.int64)]
+
+    def topk(self, v, k):
+        v = np.asarray(v.cpu() if hasattr(v, "cpu") else v)
+        return oracle.topk_ref(v, k)
+
+    def log_scan(self, blob, doc_off):
+        docs = [blob[doc_off[i]:doc_off[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(doc_off) - 1)]
+        return OracleLogScan(docs)
+
+    def rank_root_causes(self, seed, row_ptr, col, outdeg, alpha=0.85, k=10, max_iter=100, tol=1e-6):
+        seed = np.asarray(seed.cpu() if hasattr(seed, "cpu") else seed, np.float32)
+        rf, r, _ = oracle.c_ppr(row_ptr, col, outdeg, seed, alpha, max_iter, tol)
+        idx, _ = oracle.topk_ref(r, k)
+        return idx, rf[idx]

@@ -1,0 +1,67 @@
+"""The C-ABI library: it loads without a GPU and exports every symbol include/krca.h declares;
+host-only helpers (sizes, plans) are callable on CPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from conftest import ROOT
+from krca import native
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "krca.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(krca_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = native.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(native.SIGNATURES), "ctypes signatures out of sync with include/krca.h"
+
+
+def test_version_and_host_helpers():
+    lib = native.load_library()
+    assert lib.krca_version() == 100
+    assert lib.krca_log_index_size(0) > 0
+    assert lib.krca_log_index_size(1 << 30) > lib.krca_log_index_size(1 << 20)
+    assert lib.krca_topk_workspace_size(1 << 20, 10) > 0
+    assert lib.krca_ppr_workspace_size(1000) >= 4 * 1000 * 8
+
+
+def test_ppr_plan_blocks_cover_rows():
+    lib = native.load_library()
+    rng = np.random.default_rng(0)
+    deg = rng.integers(0, 40, 5000)
+    deg[[7, 999]] = [5000, 2049]  # long rows -> chunked
+    rp = np.zeros(len(deg) + 1, np.int64)
+    np.cumsum(deg, out=rp[1:])
+    n = lib.krca_ppr_plan_size(rp.ctypes.data_as(ctypes.c_void_p), len(deg))
+    plan = np.zeros(n, np.int32)
+    assert lib.krca_ppr_plan(rp.ctypes.data_as(ctypes.c_void_p), len(deg), plan.ctypes.data_as(ctypes.c_void_p), n) == 0
+    covered = np.zeros(len(deg), np.int64)
+    for rb, code in plan.reshape(-1, 2):
+        if code > 0:
+            assert code - rb <= 256 and rp[code] - rp[rb] <= 2048
+            covered[rb:code] += 1
+        else:
+            assert deg[rb] > 2048
+            covered[rb] += (-code == 0)
+    assert (covered == 1).all()
+
+
+def test_no_cpu_fallback_without_device():
+    import torch
+    if torch.cuda.is_available():
+        return
+    try:
+        native.NativeEngine()
+    except native.KrcaError as e:
+        assert "no CPU fallback" in str(e)
+    else:
+        raise AssertionError("NativeEngine must refuse to run without a HIP device")

@@ -1,0 +1,72 @@
+"""Host logic of the drop-in agents against the reference goldens, on CPU.
+
+The device kernels are replaced by the oracle engine (tests/oracle_engine.py); the same cases
+run through libkrca on the GPU in tests/test_gpu_agents.py.
+"""
+import agent_cases as A
+from oracle_engine import OracleEngine
+
+ENG = OracleEngine()
+
+
+def test_c1_raw_mock_all_types():
+    assert A.check_c1(ENG, "c1_raw.json", A.MockK8sClient) == []
+
+
+def test_c1_shimmed_mock_all_types():
+    assert A.check_c1(ENG, "c1_shim.json", A.Shim) == []
+
+
+def test_c1_other_namespaces_and_unknown_type():
+    assert A.check_c1_other(ENG) == []
+
+
+def test_resource_analyzer():
+    assert A.check_resource() == []
+
+
+def test_logs_corpus_findings():
+    assert A.check_logs_corpus(ENG) == []
+
+
+def test_topology_small_clusters():
+    assert A.check_topology(ENG) == []
+
+
+def test_metrics_scaled_boundaries():
+    assert A.check_metrics_scaled(ENG) == []
+
+
+def test_events_cases():
+    assert A.check_events() == []
+
+
+def test_comprehensive_roots_order():
+    res = A.Coordinator(A.Shim(), engine=ENG).run_analysis("comprehensive", A.NS)
+    assert [r["component"] for r in res["root_causes"]] == [
+        "Pod/database-7c9f8b6d5e-3x5qp/database", "Pod/api-gateway-6b7c8d9e5f-4q3zx/api-gateway"]
+    ranked = [r["component"] for r in res["ranked_root_causes"]]
+    assert ranked == ["Service/database", "Service/backend", "Service/api-gateway", "Service/resource-service",
+                      "Service/frontend"]
+
+
+def test_threshold_safe_conversion():
+    import numpy as np
+    from krca.agents.metrics import to_f32_threshold_safe
+    v = np.array([80.0, 80.0000001, 80.00000000001, 90.0000000001, 79.99999999, 90.0, np.nan, 1e300])
+    f = to_f32_threshold_safe(v)
+    assert list(f > 80) == list(v > 80)
+    assert list(f > 90) == list(v > 90)
+
+
+def test_topology_cycles_valid():
+    gold = A.load("topology_small.json")
+    for name, case in gold.items():
+        agent = A.TopologyAgent(A.DictClient(**case["inputs"]), engine=ENG)
+        res = agent.analyze("shop")
+        for f in res["findings"]:
+            if f["evidence"].startswith("Dependency cycle: "):
+                nodes = f["evidence"][len("Dependency cycle: "):].split(" → ")
+                assert nodes[0] == nodes[-1]
+                for u, v in zip(nodes, nodes[1:]):
+                    assert agent.service_graph.has_edge(u, v), (name, u, v)

@@ -1,0 +1,177 @@
+"""Parity of the HIP kernels (through the C-ABI) against the oracle, on an MI355X.
+
+Integer outputs bit-exact; float outputs within the tolerance stated per test; top-k identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from krca import native, synth
+from krca.agents.logs import pack_documents
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return native.NativeEngine()
+
+
+# ---- a1/a2 thresholds ------------------------------------------------------------------------
+def test_usage_flags_bit_exact(eng):
+    rng = np.random.default_rng(0)
+    u = rng.uniform(0, 100, (100003, 2)).astype(np.float32)
+    edge = np.array([80, 90, np.nextafter(np.float32(80), 100), np.nextafter(np.float32(90), 0), 0, 100,
+                     np.nan, -np.inf, np.inf], np.float32)
+    u[:len(edge), 0] = edge
+    u[:len(edge), 1] = edge[::-1]
+    assert np.array_equal(eng.usage_flags(u), oracle.c_usage_flags(u))
+
+
+# ---- a5 rolling z-score ------------------------------------------------------------------------
+ROLL_CASES = [  # (P, M, T, W)
+    (1000, 8, 1440, 60), (513, 8, 300, 60), (700, 8, 200, 30), (300, 4, 97, 20), (300, 2, 64, 15),
+    (200, 8, 50, 10), (128, 8, 60, 60), (128, 8, 61, 60), (64, 8, 20, 60), (100, 8, 300, 45), (77, 1, 90, 7),
+    (64, 16, 150, 60), (32, 64, 130, 60),
+]
+
+
+@pytest.mark.parametrize("P,M,T,W", ROLL_CASES)
+def test_rolling_score_vs_oracle(eng, P, M, T, W):
+    mesh_roots = np.arange(0, P, max(1, P // 7))
+    x = synth.make_metrics(P, M, T, window=W, seed=P + T, roots=mesh_roots)
+    got = eng.rolling_score(x.cuda(), window=W, z_threshold=3.0)
+    ref = oracle.c_rolling_score(x.numpy(), W, 3.0)
+    assert np.array_equal(got["n_exceed_host"], ref["n_exceed"])        # bit-exact
+    assert np.array_equal(got["flags"], ref["flags"])                    # bit-exact
+    z = got["z_last"].cpu().numpy()
+    assert np.allclose(z, ref["z_last"], rtol=1e-5, atol=1e-6)           # 1e-5 relative
+    assert np.allclose(got["score"].cpu().numpy(), ref["score"], rtol=1e-5, atol=1e-6)
+    zl, sc, _ = oracle.rolling_score_f64(x.numpy(), W)                   # independent f64 formulation
+    assert np.allclose(z, zl, rtol=1e-5, atol=1e-5)
+
+
+def test_rolling_score_deterministic_and_planted_roots(eng):
+    m = synth.make_graph(2000, avg_degree=10, seed=1)
+    hops = synth.caller_hops(m, m.roots)
+    x = synth.make_metrics(2000, 8, 1440, roots=m.roots, hop_sets=hops, seed=2).cuda()
+    a = eng.rolling_score(x)
+    b = eng.rolling_score(x)
+    assert torch.equal(a["score"], b["score"]) and np.array_equal(a["n_exceed_host"], b["n_exceed_host"])
+    idx, _ = eng.topk(a["score"], len(m.roots))
+    assert set(idx.tolist()) == set(m.roots.tolist())
+
+
+# ---- top-k -----------------------------------------------------------------------------------
+@pytest.mark.parametrize("N,k", [(1, 1), (10, 10), (1000, 10), (1 << 20, 10), (3_000_001, 16), (777, 5)])
+def test_topk_float_and_int(eng, N, k):
+    rng = np.random.default_rng(N)
+    v = rng.integers(0, 50, N).astype(np.float32)  # many ties -> index tie-break
+    idx, val = eng.topk(torch.from_numpy(v), k)
+    ridx, rval = oracle.topk_ref(v, k)
+    assert np.array_equal(idx, ridx) and np.array_equal(val, rval)
+    vi = rng.integers(-(1 << 62), 1 << 62, N).astype(np.int64)
+    vi[::7] = 12345
+    idx, val = eng.topk(torch.from_numpy(vi), k)
+    ridx, rval = oracle.topk_ref(vi, k)
+    assert np.array_equal(idx, ridx) and np.array_equal(val, rval)
+
+
+def test_topk_nan_never_selected(eng):
+    v = np.full(5000, np.nan, np.float32)
+    v[[3, 4000]] = [1.0, 2.0]
+    idx, val = eng.topk(torch.from_numpy(v), 2)
+    assert idx.tolist() == [4000, 3]
+
+
+# ---- a12 log histograms ----------------------------------------------------------------------
+def _check_docs(eng, docs):
+    blob, off = pack_documents(docs)
+    scan = eng.log_scan(blob, off)
+    for d, text in enumerate(docs):
+        n, h, ex = oracle.log_hist(text)
+        assert scan.n_lines[d] == n, (d, repr(text[:80]))
+        assert scan.hist[d].tolist() == h, (d, repr(text[:80]))
+        for c in range(13):
+            assert scan.examples(d, c) == ex[c], (d, c)
+
+
+def test_log_scan_reference_corpus(eng):
+    import json
+    import os
+    from conftest import GOLDEN
+    g = json.load(open(os.path.join(GOLDEN, "logs_corpus.json")))
+    docs = [c["text"] for c in g["containers"]]
+    _check_docs(eng, docs)
+    # per-line masks against the masks the reference produced
+    blob, off = pack_documents(docs)
+    r = eng.log_scan_device(eng.upload_blob(blob), torch.from_numpy(off).cuda())
+    masks = r["line_mask"].cpu().numpy().tolist()
+    assert masks == [m for c in g["containers"] for m in c["masks"]]
+
+
+def test_log_scan_boundaries(eng):
+    """Separators, multi-byte characters and lines straddling 256-byte chunks / 64 KiB tiles."""
+    rng = np.random.default_rng(7)
+    docs = ["", "\n", "\r\n", "\r", "a", "x\r\ny", "\n\n\n", "Killed\r", " ", "timeout Killed\x85panic:",
+            "", "e" * 255 + "\r\n" + "Error", "f" * 254 + "é" + "Timeout", "g" * 253 + " " + "ERROR",
+            "h" * 300000 + " Traceback " + "i" * 70000, "StatusCode=5" + "٣٤" + "\n" + "K" + "illed"]
+    for L in (250, 255, 256, 257, 511, 512, 65535, 65536, 65537):
+        docs.append("x" * (L - 8) + "timeout\r" + "\nERROR")
+    pieces = ["Error", "\r", "\n", "\r\n", "é", "KILLED", "\u0085", "ſecret not found", "a" * 37, "panic:",
+              "Back-off restarting", "\x1c", "\x0b", " "]
+    for _ in range(200):
+        docs.append("".join(pieces[i] for i in rng.integers(0, len(pieces), rng.integers(0, 60))))
+    _check_docs(eng, docs)
+
+
+def test_log_scan_synthetic_large(eng):
+    docs = synth.make_log_corpus(20000, lines_per_doc=6, seed=3, hazard_rate=0.01)
+    _check_docs(eng, docs)
+
+
+# ---- a10 personalized PageRank ---------------------------------------------------------------
+def test_ppr_known_answer(eng):
+    import json
+    import os
+    from conftest import GOLDEN
+    from krca.agents.topology import csr_from_edges
+    g = json.load(open(os.path.join(GOLDEN, "ppr_known.json")))
+    names = g["nodes"]
+    pos = {n: i for i, n in enumerate(names)}
+    rp, col, od = csr_from_edges(len(names), [pos[s] for s, _ in g["edges"]], [pos[d] for _, d in g["edges"]])
+    seed = np.array([g["personalization"][n] for n in names], np.float32)
+    r, rf, it = eng.ppr(rp, col, od, seed, g["alpha"])
+    ref = np.array([g["pagerank"][n] for n in names])
+    assert np.allclose(r.cpu().numpy(), ref, rtol=1e-5, atol=0)
+    rfo, ro, ito = oracle.c_ppr(rp, col, od, seed, g["alpha"])
+    assert np.array_equal(rf.cpu().numpy(), ro) and it == ito
+
+
+@pytest.mark.parametrize("n,deg,tol,iters", [(5000, 8, 1e-6, 100), (20000, 20, 0.0, 30), (3000, 3, 1e-9, 300)])
+def test_ppr_bit_exact_vs_oracle(eng, n, deg, tol, iters):
+    m = synth.make_graph(n, avg_degree=deg, seed=n)
+    rng = np.random.default_rng(n)
+    seed = (rng.random(n) ** 8).astype(np.float32)
+    r, rf, it = eng.ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, iters, tol)
+    rfo, ro, ito = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, iters, tol)
+    assert it == abs(ito)
+    assert np.array_equal(rf.cpu().numpy(), ro)  # bit-identical fixed point
+    x, _ = oracle.ppr_f64(m.row_ptr, m.col, m.outdeg, seed.astype(np.float64), 0.85, it, 0.0)
+    assert np.max(np.abs(r.cpu().numpy() - x) / np.maximum(x, 1e-30)) < 1e-5
+    idx, _ = eng.topk(rf, 10)
+    assert np.array_equal(idx, oracle.topk_ref(ro, 10)[0])
+
+
+def test_ppr_long_rows_and_dangling(eng):
+    # a hub with 10k callers (long-row chunks + int64 atomics), isolated and dangling nodes
+    n = 12000
+    src = np.concatenate([np.arange(1, 10001), np.arange(10001, 11999)])
+    dst = np.concatenate([np.zeros(10000, np.int64), np.arange(10002, 12000)])
+    from krca.agents.topology import csr_from_edges
+    rp, col, od = csr_from_edges(n, src, dst)
+    seed = np.ones(n, np.float32)
+    r, rf, it = eng.ppr(rp, col, od, seed, 0.85, 50, 0.0)
+    rfo, ro, _ = oracle.c_ppr(rp, col, od, seed, 0.85, 50, 0.0)
+    assert np.array_equal(rf.cpu().numpy(), ro)
