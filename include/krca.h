@@ -82,19 +82,40 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
 
 /* ---- a10: personalized PageRank root-cause propagation (replaces the sink of
  * Coordinator._identify_root_causes, ref:agents/coordinator.py:157-184; networkx 3.4.2
- * pagerank semantics: dangling mass follows the personalization, L1 stop rule err < N*tol).
- * Pull-CSR: row i lists the sources j of edges j->i; outdeg[j] = out-degree of j.
- * seed[i] >= 0 (float32) is normalised inside.  Arithmetic is 2^-60 fixed point in int64, so
- * the result is independent of summation order and bit-identical to oracle/krca_oracle.c.
- * The plan (row blocks for the adaptive SpMV) is built once per graph.  r_out = float32 ranks;
- * r_fixed (optional, int64 units of 2^-60) and *iters_host are returned for exact comparison. */
+ * pagerank semantics: dangling mass follows the personalization, L1 stop rule err < N*tol,
+ * tol <= 0 = exactly max_iter iterations).  Pull-CSR: row i lists the sources j of edges j->i;
+ * outdeg[j] = out-degree of j.  Personalization p_i ∝ max(seed_i - seed_floor, 0) (uniform if
+ * all are at the floor).  Arithmetic is 2^-60 fixed point in int64: results do not depend on
+ * summation order or GPU count and are bit-identical to oracle/krca_oracle.c.
+ * krca_ppr runs the whole iteration on one device (synchronous: returns *iters_host); the
+ * krca_ppr_shard_* steps are the same kernels for G pod-sharded ranks whose host loop
+ * all-gathers each rank's [w_local(n_max) | 3 partial sums] slice over RCCL between
+ * krca_ppr_shard_update and krca_ppr_shard_reduce (kubernetes-rca-system_amd/krca/rca.py). */
 int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N);
 int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, int64_t plan_len);
 int64_t krca_ppr_workspace_size(int64_t N);
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
-             const int32_t* plan, int64_t plan_len, const float* seed, double alpha, int32_t max_iter,
-             double tol, void* workspace, float* r_out, int64_t* r_fixed, int32_t* iters_host,
-             void* stream);
+             const int32_t* plan, int64_t plan_len, const float* seed, float seed_floor, double alpha,
+             int32_t max_iter, double tol, void* workspace, float* r_out, int64_t* r_fixed /*nullable*/,
+             int64_t* q_out /*nullable: quantised seeds*/, int32_t* iters_host, void* stream);
+int64_t krca_ppr_ctl_size(void);
+int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream);
+int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
+                        int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
+                        int64_t* r_local, int64_t* send /*[n_max+3]*/, void* stream);
+int krca_ppr_shard_spmv(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int32_t* plan,
+                        int64_t plan_len, const int64_t* w_all /*[G][n_max+3]*/, int64_t* acc,
+                        const void* ctl, void* stream);
+int krca_ppr_shard_update(const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
+                          int64_t N, double alpha, int64_t* r_local, int64_t* acc, int64_t* send,
+                          const void* ctl, void* stream);
+int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
+                          double tol, int32_t first, void* ctl, int64_t* send, void* stream);
+int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);
+int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream);
+/* root-cause key = bits of (double)r_i * (double)q_i: ranks pods by propagated mass times their
+ * own anomaly; order-preserving as int64, fed to krca_topk_i64 */
+int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key, void* stream);
 
 /* ---- top-k (descending value, ties -> lower index), float32 or int64 keys ------------------ */
 int64_t krca_topk_workspace_size(int64_t N, int32_t k);

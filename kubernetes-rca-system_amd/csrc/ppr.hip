@@ -3,6 +3,7 @@
 // Semantics: networkx 3.4.2 pagerank (_pagerank_scipy) — x <- alpha*(x·A + D(x)·p) + (1-alpha)*p,
 // A row-normalised by out-degree, dangling mass D(x) redistributed along the personalization p,
 // x0 = 1/N, stop when sum|x - x_prev| < N*tol (tol <= 0: exactly max_iter iterations).
+// Personalization p_i ∝ max(seed_i - seed_floor, 0) (uniform if every seed is at the floor).
 //
 // Determinism: the rank mass is held in int64 fixed point (1.0 == 2^60).  Per-node quantities
 // that need a product or quotient are formed in float64 with a fixed expression and truncated
@@ -10,13 +11,19 @@
 // result does not depend on the summation order, on atomics or on the number of GPUs, and is
 // bit-identical to oracle/krca_oracle.c.
 //
+// Sharding: rank g of G owns the contiguous node range [g*n_max, ...) and the
+// pull-CSR rows of those nodes.  Each iteration ends with ONE exchange: every rank's slice
+// [w_local (n_max int64) | residual | dangling mass | seed total] is all-gathered (RCCL over
+// xGMI, driven by the host: krca/rca.py) into w_all[G][n_max+3]; the column indices are
+// pre-remapped to that layout (col' = j + 3*(j / n_max)), so the SpMV gathers directly.
+// G = 1 is the same code with no collective (krca_ppr).
+//
 // SpMV (pull CSR, HBM-bound): CSR-adaptive row blocks from krca_ppr_plan —
 //   short-row blocks: <= 2048 edges and <= 256 rows; the block gathers w[col[e]] for its edge
 //                     range into LDS (coalesced col reads, lane per edge), then lane r sums row r
 //                     from LDS ("LDS-staged row segments");
 //   long rows:        split into 2048-edge chunks, each chunk block-reduced and added with one
 //                     int64 atomic (order-free integer add).
-// Per iteration: spmv -> update (r, residual, dangling mass, next w; fused) -> finalize (1 lane).
 #include <vector>
 
 #include "krca_common.h"
@@ -28,14 +35,13 @@ namespace {
 constexpr int TPB = 256;
 constexpr int EDGE_BUDGET = 2048;  // edges per short block == LDS slots
 constexpr int ROW_BUDGET = TPB;    // rows per short block
+constexpr int NSLOT = 3;           // residual, dangling, seed total
 
-struct Ctl {  // device control block (in the workspace)
-  double tele;          // (1-alpha)*2^60 + alpha*D   for the current iteration
-  int64_t acc_err;      // residual accumulator
-  int64_t acc_dangle;   // dangling-mass accumulator
-  int64_t q_total;      // sum of quantised seeds
-  int32_t converged;    // iteration count at convergence (0 = running)
-  int32_t iter;         // iterations done
+struct Ctl {        // device control block
+  double tele;      // (1-alpha)*2^60 + alpha*D   for the next update
+  int64_t q_total;  // sum of quantised seeds over all ranks
+  int32_t converged;  // iteration count at convergence (0 = running)
+  int32_t iter;       // iterations done
 };
 
 __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
@@ -50,6 +56,10 @@ __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
   return s;  // valid in thread 0
 }
 
+__device__ __forceinline__ void add_slot(int64_t* slot, int64_t v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)v);
+}
+
 // w_j for node j given its fixed-point rank rj
 __device__ __forceinline__ int64_t edge_weight(int64_t rj, int32_t deg, double alpha) {
   if (deg == 0) return 0;
@@ -57,53 +67,32 @@ __device__ __forceinline__ int64_t edge_weight(int64_t rj, int32_t deg, double a
   return (int64_t)((double)rj * coef);
 }
 
-__global__ __launch_bounds__(TPB) void ppr_seed_quant(const float* __restrict__ seed, int64_t N,
-                                                      int64_t* __restrict__ q, Ctl* ctl) {
-  __shared__ int64_t red[TPB / 64];
-  int64_t local = 0;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < N; i += (int64_t)gridDim.x * TPB) {
-    const float s = seed[i];
-    const int64_t qi = (s > 0.f) ? (int64_t)((double)s * 4294967296.0) : 0;
-    q[i] = qi;
-    local += qi;
-  }
-  const int64_t tot = block_sum_i64(local, red);
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&ctl->q_total, (unsigned long long)tot);
+__device__ __forceinline__ int64_t quantise(float s, float floor_) {
+  const double v = (double)s - (double)floor_;
+  return v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
 }
 
-// r0 = floor(2^60/N) everywhere, w0, dangling mass D0
-__global__ __launch_bounds__(TPB) void ppr_init(const int32_t* __restrict__ outdeg, int64_t N, double alpha,
-                                                int64_t* __restrict__ r, int64_t* __restrict__ w,
-                                                int64_t* __restrict__ acc, Ctl* ctl) {
+// r0 = floor(2^60/N), w0, seeds, partial slots (dangling mass, seed total)
+__global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, float seed_floor,
+                                                const int32_t* __restrict__ outdeg, int64_t n, int64_t N,
+                                                double alpha, int64_t* __restrict__ q, int64_t* __restrict__ r,
+                                                int64_t* __restrict__ send, int64_t n_max) {
   __shared__ int64_t red[TPB / 64];
   const int64_t r0 = (int64_t)(krca::kFix / (double)N);
-  int64_t dang = 0;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < N; i += (int64_t)gridDim.x * TPB) {
+  int64_t dang = 0, qs = 0;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
     const int32_t deg = outdeg[i];
+    const int64_t qi = quantise(seed[i], seed_floor);
+    q[i] = qi;
+    qs += qi;
     r[i] = r0;
-    w[i] = edge_weight(r0, deg, alpha);
-    acc[i] = 0;
+    send[i] = edge_weight(r0, deg, alpha);
     if (deg == 0) dang += r0;
   }
-  const int64_t tot = block_sum_i64(dang, red);
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&ctl->acc_dangle, (unsigned long long)tot);
-}
-
-// one lane: consume accumulators, decide convergence, set the teleport scale of the next iteration
-__global__ void ppr_finalize(Ctl* ctl, double alpha, double err_limit, int first) {
-  if (ctl->converged) return;
-  const int64_t err = ctl->acc_err;
-  const int64_t dang = ctl->acc_dangle;
-  ctl->acc_err = 0;
-  ctl->acc_dangle = 0;
-  if (!first) {
-    ctl->iter += 1;
-    if (err_limit > 0.0 && (double)err < err_limit) {
-      ctl->converged = ctl->iter;
-      return;
-    }
-  }
-  ctl->tele = (1.0 - alpha) * krca::kFix + alpha * (double)dang;
+  int64_t t = block_sum_i64(dang, red);
+  if (threadIdx.x == 0 && t) add_slot(&send[n_max + 1], t);
+  t = block_sum_i64(qs, red);
+  if (threadIdx.x == 0 && t) add_slot(&send[n_max + 2], t);
 }
 
 __global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -126,7 +115,7 @@ __global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_
       for (int64_t e = a; e < b; ++e) s += lds[e];
       acc[row] = s;
     }
-  } else {  // chunk -code of long row rb
+  } else {  // chunk -code of long row rb (acc[rb] was zeroed by the previous update)
     const int64_t c = -(int64_t)code;
     const int64_t r0 = row_ptr[rb], r1 = row_ptr[rb + 1];
     const int64_t e0 = r0 + c * EDGE_BUDGET;
@@ -134,20 +123,23 @@ __global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_
     int64_t s = 0;
     for (int64_t e = e0 + threadIdx.x; e < e1; e += TPB) s += w[col[e]];
     const int64_t tot = block_sum_i64(s, red);
-    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&acc[rb], (unsigned long long)tot);
+    if (threadIdx.x == 0) add_slot(&acc[rb], tot);
   }
 }
 
 __global__ __launch_bounds__(TPB) void ppr_update(const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
-                                                  int64_t N, double alpha, int64_t* __restrict__ r,
-                                                  int64_t* __restrict__ w, int64_t* __restrict__ acc, Ctl* ctl) {
+                                                  int64_t n, int64_t N, double alpha, int64_t* __restrict__ r,
+                                                  int64_t* __restrict__ acc, int64_t* __restrict__ send,
+                                                  int64_t n_max, const Ctl* __restrict__ ctl) {
   __shared__ int64_t red[TPB / 64];
   if (ctl->converged) return;
   const double tele = ctl->tele;
-  const double qtot = (double)ctl->q_total;
+  const int64_t qt = ctl->q_total;
+  const double qtot = (double)qt;
+  const double uni = 1.0 / (double)N;
   int64_t err = 0, dang = 0;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < N; i += (int64_t)gridDim.x * TPB) {
-    const double pd = (double)q[i] / qtot;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const double pd = qt > 0 ? (double)q[i] / qtot : uni;
     const int64_t t = (int64_t)(pd * tele);
     const int64_t rn = acc[i] + t;
     acc[i] = 0;
@@ -156,17 +148,61 @@ __global__ __launch_bounds__(TPB) void ppr_update(const int32_t* __restrict__ ou
     err += rn > ro ? rn - ro : ro - rn;
     const int32_t deg = outdeg[i];
     if (deg == 0) dang += rn;
-    w[i] = edge_weight(rn, deg, alpha);
+    send[i] = edge_weight(rn, deg, alpha);
   }
-  int64_t tot = block_sum_i64(err, red);
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&ctl->acc_err, (unsigned long long)tot);
-  tot = block_sum_i64(dang, red);
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&ctl->acc_dangle, (unsigned long long)tot);
+  int64_t t = block_sum_i64(err, red);
+  if (threadIdx.x == 0 && t) add_slot(&send[n_max], t);
+  t = block_sum_i64(dang, red);
+  if (threadIdx.x == 0 && t) add_slot(&send[n_max + 1], t);
 }
 
-__global__ __launch_bounds__(TPB) void ppr_to_float(const int64_t* __restrict__ r, int64_t N, float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < N; i += (int64_t)gridDim.x * TPB)
+// one lane: sum the G gathered partial slots (integer -> order-free), decide convergence,
+// set the teleport scale of the next update, zero this rank's send slots
+__global__ void ppr_reduce(const int64_t* __restrict__ w_all, int32_t G, int64_t n_max, double alpha,
+                           double err_limit, int first, Ctl* ctl, int64_t* __restrict__ send) {
+  int64_t err = 0, dang = 0, qs = 0;
+  for (int g = 0; g < G; ++g) {
+    const int64_t* s = w_all + (int64_t)g * (n_max + NSLOT) + n_max;
+    err += s[0];
+    dang += s[1];
+    qs += s[2];
+  }
+  send[n_max] = 0;
+  send[n_max + 1] = 0;
+  send[n_max + 2] = 0;
+  if (ctl->converged) return;
+  if (first) {
+    ctl->q_total = qs;
+  } else {
+    ctl->iter += 1;
+    if (err_limit > 0.0 && (double)err < err_limit) {
+      ctl->converged = ctl->iter;
+      return;
+    }
+  }
+  ctl->tele = (1.0 - alpha) * krca::kFix + alpha * (double)dang;
+}
+
+__global__ __launch_bounds__(TPB) void ppr_to_float(const int64_t* __restrict__ r, int64_t n, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
     out[i] = (float)((double)r[i] * (1.0 / krca::kFix));
+}
+
+// root-cause key: the bits of (double)r_i * (double)q_i (non-negative doubles order like int64)
+__global__ __launch_bounds__(TPB) void ppr_rca_key(const int64_t* __restrict__ r, const int64_t* __restrict__ q,
+                                                   int64_t n, int64_t* __restrict__ key) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const double v = (double)r[i] * (double)q[i];
+    key[i] = __double_as_longlong(v);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void remap_cols(const int32_t* __restrict__ col, int64_t E, int64_t n_max,
+                                                  int32_t* __restrict__ out) {
+  for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < E; e += (int64_t)gridDim.x * TPB) {
+    const int64_t j = col[e];
+    out[e] = (int32_t)(j + NSLOT * (j / n_max));
+  }
 }
 
 // host: CSR-adaptive row blocks; returns the number of int32 entries (2 per block)
@@ -199,28 +235,7 @@ int64_t build_plan(const int64_t* rp, int64_t N, int32_t* out) {
   return n;
 }
 
-struct Workspace {
-  Ctl* ctl;
-  int64_t* q;
-  int64_t* w;
-  int64_t* acc;
-  int64_t* rfix;
-};
-
-Workspace carve(void* ws, int64_t N) {
-  char* p = reinterpret_cast<char*>(ws);
-  Workspace W;
-  W.ctl = reinterpret_cast<Ctl*>(p);
-  p += 256;
-  W.q = reinterpret_cast<int64_t*>(p);
-  p += N * 8;
-  W.w = reinterpret_cast<int64_t*>(p);
-  p += N * 8;
-  W.acc = reinterpret_cast<int64_t*>(p);
-  p += N * 8;
-  W.rfix = reinterpret_cast<int64_t*>(p);
-  return W;
-}
+unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), 2048)); }
 
 }  // namespace
 
@@ -241,47 +256,127 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, in
   return KRCA_OK;
 }
 
-int64_t krca_ppr_workspace_size(int64_t N) { return 256 + 4 * N * 8 + 256; }
+int64_t krca_ppr_ctl_size(void) { return 256; }
+
+int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream) {
+  KRCA_CHECK_ARG(E >= 0 && n_max > 0, "krca_ppr_remap_cols: bad sizes");
+  if (E == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(col && out, "krca_ppr_remap_cols: null pointer");
+  hipLaunchKernelGGL(remap_cols, dim3(grid_for(E)), dim3(TPB), 0, krca::as_stream(stream), col, E, n_max, out);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local, int64_t n_max,
+                        int64_t N, double alpha, void* ctl, int64_t* q_local, int64_t* r_local, int64_t* send,
+                        void* stream) {
+  KRCA_CHECK_ARG(N > 0 && N < INT32_MAX && n_local >= 0 && n_local <= n_max, "krca_ppr_shard_init: bad sizes");
+  KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0, "krca_ppr_shard_init: alpha must be in (0, 1)");
+  KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)), "krca_ppr_shard_init: null pointer");
+  hipStream_t st = krca::as_stream(stream);
+  KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
+  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
+  hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N, alpha,
+                     q_local, r_local, send, n_max);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_shard_spmv(const int64_t* row_ptr, const int32_t* col, const int32_t* plan, int64_t plan_len,
+                        const int64_t* w_all, int64_t* acc, const void* ctl, void* stream) {
+  KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 2 == 0, "krca_ppr_shard_spmv: bad plan");
+  if (plan_len == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(row_ptr && col && plan && w_all && acc && ctl, "krca_ppr_shard_spmv: null pointer");
+  hipLaunchKernelGGL(ppr_spmv, dim3((unsigned)(plan_len / 2)), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col,
+                     plan, w_all, acc, reinterpret_cast<const Ctl*>(ctl));
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_shard_update(const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N,
+                          double alpha, int64_t* r_local, int64_t* acc, int64_t* send, const void* ctl, void* stream) {
+  KRCA_CHECK_ARG(n_local >= 0 && n_local <= n_max && N > 0, "krca_ppr_shard_update: bad sizes");
+  KRCA_CHECK_ARG(send && ctl && (n_local == 0 || (outdeg && q_local && r_local && acc)), "krca_ppr_shard_update: null pointer");
+  hipLaunchKernelGGL(ppr_update, dim3(grid_for(n_local)), dim3(TPB), 0, krca::as_stream(stream), outdeg, q_local,
+                     n_local, N, alpha, r_local, acc, send, n_max, reinterpret_cast<const Ctl*>(ctl));
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha, double tol,
+                          int32_t first, void* ctl, int64_t* send, void* stream) {
+  KRCA_CHECK_ARG(G >= 1 && n_max > 0 && N > 0, "krca_ppr_shard_reduce: bad sizes");
+  KRCA_CHECK_ARG(w_all && ctl && send, "krca_ppr_shard_reduce: null pointer");
+  const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
+  hipLaunchKernelGGL(ppr_reduce, dim3(1), dim3(1), 0, krca::as_stream(stream), w_all, G, n_max, alpha, err_limit,
+                     (int)first, reinterpret_cast<Ctl*>(ctl), send);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream) {
+  KRCA_CHECK_ARG(ctl && iters_host && converged_host, "krca_ppr_ctl_read: null pointer");
+  Ctl h{};
+  hipStream_t st = krca::as_stream(stream);
+  KRCA_HIP(hipMemcpyAsync(&h, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+  KRCA_HIP(hipStreamSynchronize(st));
+  *iters_host = h.converged ? h.converged : h.iter;
+  *converged_host = h.converged;
+  return KRCA_OK;
+}
+
+int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream) {
+  if (n <= 0) return KRCA_OK;
+  KRCA_CHECK_ARG(r && out, "krca_ppr_fixed_to_float: null pointer");
+  hipLaunchKernelGGL(ppr_to_float, dim3(grid_for(n)), dim3(TPB), 0, krca::as_stream(stream), r, n, out);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key, void* stream) {
+  if (n <= 0) return KRCA_OK;
+  KRCA_CHECK_ARG(r && q && key, "krca_ppr_rca_key: null pointer");
+  hipLaunchKernelGGL(ppr_rca_key, dim3(grid_for(n)), dim3(TPB), 0, krca::as_stream(stream), r, q, n, key);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+// workspace: ctl (256 B) | q[N] | acc[N] | send/w_all[N+3] | r (if r_fixed == NULL) [N]
+int64_t krca_ppr_workspace_size(int64_t N) { return 256 + (4 * N + NSLOT) * 8 + 256; }
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int32_t* plan,
-             int64_t plan_len, const float* seed, double alpha, int32_t max_iter, double tol, void* workspace,
-             float* r_out, int64_t* r_fixed, int32_t* iters_host, void* stream) {
+             int64_t plan_len, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
+             void* workspace, float* r_out, int64_t* r_fixed, int64_t* q_out, int32_t* iters_host, void* stream) {
   KRCA_CHECK_ARG(N > 0 && N < INT32_MAX, "krca_ppr: N=%lld out of range", (long long)N);
   KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && seed && workspace && r_out, "krca_ppr: null pointer");
   KRCA_CHECK_ARG(plan_len > 0 && plan_len % 2 == 0, "krca_ppr: bad plan");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0 && max_iter > 0, "krca_ppr: alpha in (0,1), max_iter > 0");
+  char* p = reinterpret_cast<char*>(workspace);
+  void* ctl = p;
+  int64_t* q = q_out ? q_out : reinterpret_cast<int64_t*>(p + 256);
+  int64_t* acc = reinterpret_cast<int64_t*>(p + 256 + N * 8);
+  int64_t* w = reinterpret_cast<int64_t*>(p + 256 + 2 * N * 8);
+  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + 256 + (3 * N + NSLOT) * 8);
   hipStream_t st = krca::as_stream(stream);
-  Workspace W = carve(workspace, N);
-  int64_t* r = r_fixed ? r_fixed : W.rfix;
-  const unsigned gN = (unsigned)std::min<int64_t>(krca::ceil_div(N, TPB), 2048);
-  const unsigned nblk = (unsigned)(plan_len / 2);
-  const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
-
-  KRCA_HIP(hipMemsetAsync(W.ctl, 0, sizeof(Ctl), st));
-  hipLaunchKernelGGL(ppr_seed_quant, dim3(gN), dim3(TPB), 0, st, seed, N, W.q, W.ctl);
-  hipLaunchKernelGGL(ppr_init, dim3(gN), dim3(TPB), 0, st, outdeg, N, alpha, r, W.w, W.acc, W.ctl);
-  hipLaunchKernelGGL(ppr_finalize, dim3(1), dim3(1), 0, st, W.ctl, alpha, err_limit, 1);
-  KRCA_LAUNCH_CHECK();
-  Ctl host{};
+  KRCA_HIP(hipMemsetAsync(acc, 0, N * 8, st));
+  int rc = krca_ppr_shard_init(seed, seed_floor, outdeg, N, N, N, alpha, ctl, q, r, w, stream);
+  if (rc) return rc;
+  if ((rc = krca_ppr_shard_reduce(w, 1, N, N, alpha, tol, 1, ctl, w, stream))) return rc;
   const int check_every = 8;
-  int it = 0;
-  for (; it < max_iter; ++it) {
-    hipLaunchKernelGGL(ppr_spmv, dim3(nblk), dim3(TPB), 0, st, row_ptr, col, plan, W.w, W.acc, W.ctl);
-    hipLaunchKernelGGL(ppr_update, dim3(gN), dim3(TPB), 0, st, outdeg, W.q, N, alpha, r, W.w, W.acc, W.ctl);
-    hipLaunchKernelGGL(ppr_finalize, dim3(1), dim3(1), 0, st, W.ctl, alpha, err_limit, 0);
-    KRCA_LAUNCH_CHECK();
-    if (err_limit > 0.0 && ((it + 1) % check_every == 0) && it + 1 < max_iter) {
-      KRCA_HIP(hipMemcpyAsync(&host, W.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
-      KRCA_HIP(hipStreamSynchronize(st));
-      if (host.converged) break;
+  int32_t iters = 0, conv = 0;
+  for (int it = 0; it < max_iter; ++it) {
+    if ((rc = krca_ppr_shard_spmv(row_ptr, col, plan, plan_len, w, acc, ctl, stream))) return rc;
+    if ((rc = krca_ppr_shard_update(outdeg, q, N, N, N, alpha, r, acc, w, ctl, stream))) return rc;
+    if ((rc = krca_ppr_shard_reduce(w, 1, N, N, alpha, tol, 0, ctl, w, stream))) return rc;
+    if (tol > 0.0 && (it + 1) % check_every == 0 && it + 1 < max_iter) {
+      if ((rc = krca_ppr_ctl_read(ctl, &iters, &conv, stream))) return rc;
+      if (conv) break;
     }
   }
-  hipLaunchKernelGGL(ppr_to_float, dim3(gN), dim3(TPB), 0, st, r, N, r_out);
-  KRCA_LAUNCH_CHECK();
-  KRCA_HIP(hipMemcpyAsync(&host, W.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
-  KRCA_HIP(hipStreamSynchronize(st));
-  if (iters_host) *iters_host = host.converged ? host.converged : host.iter;
-  if (err_limit > 0.0 && !host.converged) {
+  if ((rc = krca_ppr_fixed_to_float(r, N, r_out, stream))) return rc;
+  if ((rc = krca_ppr_ctl_read(ctl, &iters, &conv, stream))) return rc;
+  if (iters_host) *iters_host = iters;
+  if (tol > 0.0 && !conv) {
     krca::set_error("krca_ppr: no convergence in %d iterations", max_iter);
     return KRCA_ENOTCONV;
   }

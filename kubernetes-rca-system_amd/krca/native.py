@@ -31,8 +31,17 @@ SIGNATURES = {
     "krca_ppr_plan_size": (c_i64, [c_vp, c_i64]),
     "krca_ppr_plan": (c_i32, [c_vp, c_i64, c_vp, c_i64]),
     "krca_ppr_workspace_size": (c_i64, [c_i64]),
-    "krca_ppr": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_f64, c_i32, c_f64, c_vp, c_vp, c_vp,
-                         ctypes.POINTER(c_i32), c_vp]),
+    "krca_ppr": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_f64, c_i32, c_f64, c_vp, c_vp, c_vp,
+                         c_vp, ctypes.POINTER(c_i32), c_vp]),
+    "krca_ppr_ctl_size": (c_i64, []),
+    "krca_ppr_remap_cols": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "krca_ppr_shard_init": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_spmv": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_update": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_reduce": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp]),
+    "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),
+    "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "krca_topk_workspace_size": (c_i64, [c_i64, c_i32]),
     "krca_topk_f32": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "krca_topk_i64": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
@@ -224,8 +233,11 @@ class NativeEngine:
 
     def log_scan(self, blob, doc_off):
         torch = self.torch
+        doc_off = np.asarray(doc_off, dtype=np.int64)
+        if len(doc_off) < 2 or doc_off[0] != 0 or doc_off[-1] != len(blob) or np.any(np.diff(doc_off) < 0):
+            raise KrcaError("log_scan: doc_off must be monotone from 0 to len(blob)")
         text = self.upload_blob(blob)
-        off = self._dev(np.asarray(doc_off, dtype=np.int64))
+        off = self._dev(doc_off)
         r = self.log_scan_device(text, off)
         ex = r["examples"].cpu().numpy()
         ids = np.unique(ex[ex >= 0]).astype(np.int64)
@@ -248,33 +260,35 @@ class NativeEngine:
         return self._dev(plan), n
 
     def ppr_device(self, row_ptr, col, outdeg, plan, plan_len, seed, alpha=0.85, max_iter=100, tol=1e-6,
-                   r_out=None, r_fixed=None, allow_nonconv=False):
+                   seed_floor=0.0, allow_nonconv=False):
+        """Single-device PageRank (krca_ppr).  Returns (r float32, r_fixed int64, q int64, iters)."""
         torch = self.torch
         N = outdeg.numel()
         ws = self._workspace("ppr", self.lib.krca_ppr_workspace_size(N))
-        if r_out is None:
-            r_out = torch.empty(N, dtype=torch.float32, device=self.device)
-        if r_fixed is None:
-            r_fixed = torch.empty(N, dtype=torch.int64, device=self.device)
+        r_out = torch.empty(N, dtype=torch.float32, device=self.device)
+        r_fixed = torch.empty(N, dtype=torch.int64, device=self.device)
+        q = torch.empty(N, dtype=torch.int64, device=self.device)
         iters = c_i32(0)
         rc = self.lib.krca_ppr(self.ptr(row_ptr), self.ptr(col), self.ptr(outdeg), N, self.ptr(plan), plan_len,
-                               self.ptr(seed), float(alpha), int(max_iter), float(tol), self.ptr(ws),
-                               self.ptr(r_out), self.ptr(r_fixed), ctypes.byref(iters), self._stream())
+                               self.ptr(seed), float(seed_floor), float(alpha), int(max_iter), float(tol),
+                               self.ptr(ws), self.ptr(r_out), self.ptr(r_fixed), self.ptr(q), ctypes.byref(iters),
+                               self._stream())
         if not (allow_nonconv and rc == KRCA_ENOTCONV):
             _check(rc, "krca_ppr")
-        return r_out, r_fixed, iters.value
+        return r_out, r_fixed, q, iters.value
 
-    def ppr(self, row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6):
+    def ppr(self, row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6, seed_floor=0.0):
         torch = self.torch
         rp_host = np.asarray(row_ptr, dtype=np.int64)
         plan, n = self.ppr_plan(rp_host)
-        r, rf, iters = self.ppr_device(self._dev(rp_host), self._dev(np.asarray(col, np.int32)),
-                                       self._dev(np.asarray(outdeg, np.int32)), plan, n,
-                                       self._dev(seed, torch.float32) if isinstance(seed, torch.Tensor)
-                                       else self._dev(np.asarray(seed, np.float32)), alpha, max_iter, tol)
+        sd = self._dev(seed, torch.float32) if isinstance(seed, torch.Tensor) else self._dev(np.asarray(seed, np.float32))
+        r, rf, q, iters = self.ppr_device(self._dev(rp_host), self._dev(np.asarray(col, np.int32)),
+                                          self._dev(np.asarray(outdeg, np.int32)), plan, n, sd, alpha, max_iter, tol,
+                                          seed_floor)
         return r, rf, iters
 
     def rank_root_causes(self, seed, row_ptr, col, outdeg, alpha=0.85, k=10, max_iter=100, tol=1e-6):
+        """nx-compatible PageRank ranking (C1 / agent path): top-k of the rank itself."""
         r, rf, _ = self.ppr(row_ptr, col, outdeg, seed, alpha, max_iter, tol)
         idx, _ = self.topk_device(rf, k)
         idx = idx.cpu().numpy()

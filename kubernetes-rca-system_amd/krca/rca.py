@@ -1,0 +1,200 @@
+"""The RCA hot path as one step: rolling z-scores -> seeded PageRank -> root-cause top-k.
+
+This is the north-star path (BASELINE.json): for a pod mesh of N pods with M metrics x T steps
+and a caller -> dependency graph, one step scores every pod (krca_rolling_score), seeds a
+personalized PageRank with the anomalous pods (p_i ∝ max(score_i - seed_floor, 0)), propagates
+for a fixed number of iterations (krca_ppr_shard_*), and ranks pods by propagated mass x own
+anomaly (krca_ppr_rca_key + krca_topk_i64).
+
+Multi-GPU: one process per GPU; rank g owns pods [g*n_max, (g+1)*n_max): its
+slice of the metric tensor and its rows of the pull-CSR.  Scoring needs no communication.  Each
+PageRank iteration ends with ONE all-gather over RCCL/xGMI of every rank's
+[w_local | residual | dangling | seed-total] slice (n_max + 3 int64); the partial sums ride in
+the same payload and every rank reduces them identically, so no extra collective or broadcast
+is needed.  Arithmetic is integer fixed point: the result is bit-identical for any G and to
+oracle/krca_oracle.c.  The final top-k merges G x k candidates.
+
+The per-rank numeric work is behind a small backend interface so the same orchestration runs
+on the device (:class:`DeviceShard`, libkrca) and, in the CPU test-suite, on a NumPy restatement
+with the gloo backend (tests/test_rca_dist_cpu.py).
+"""
+import math
+
+import numpy as np
+
+NSLOT = 3
+
+
+def shard_range(N, world, rank):
+    n_max = max(1, math.ceil(N / world))
+    lo = min(N, rank * n_max)
+    hi = min(N, lo + n_max)
+    return lo, hi, n_max
+
+
+def shard_graph(row_ptr, col, outdeg, lo, hi):
+    """Rows [lo, hi) of a pull-CSR (column ids stay global)."""
+    rp = np.asarray(row_ptr[lo:hi + 1], np.int64) - int(row_ptr[lo])
+    c = np.asarray(col[int(row_ptr[lo]):int(row_ptr[hi])], np.int32)
+    return rp, c, np.asarray(outdeg[lo:hi], np.int32)
+
+
+class Config:
+    def __init__(self, window=60, z_threshold=3.0, seed_floor=4.0, alpha=0.5, iters=30, tol=0.0, k=10):
+        self.window = window
+        self.z_threshold = z_threshold
+        self.seed_floor = seed_floor
+        self.alpha = alpha
+        self.iters = iters
+        self.tol = tol
+        self.k = k
+
+    def as_dict(self):
+        return dict(window=self.window, z_threshold=self.z_threshold, seed_floor=self.seed_floor, alpha=self.alpha,
+                    iters=self.iters, tol=self.tol, k=self.k)
+
+
+class Comm:
+    """All-gather over torch.distributed (nccl == RCCL on ROCm; gloo in CPU tests)."""
+
+    def __init__(self, world=1, rank=0, group=None):
+        self.world, self.rank, self.group = world, rank, group
+
+    def all_gather(self, out, inp):
+        if self.world == 1:
+            if out.data_ptr() != inp.data_ptr():
+                out.copy_(inp)
+            return
+        import torch.distributed as dist
+        try:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        except (RuntimeError, AttributeError):  # gloo builds without all_gather_into_tensor
+            dist.all_gather(list(out.view(self.world, -1).unbind(0)), inp, group=self.group)
+
+
+class DeviceShard:
+    """Per-rank device state (libkrca kernels on torch's current stream)."""
+
+    def __init__(self, engine, x_local, row_ptr_local, col_local, outdeg_local, N, n_max, world, cfg):
+        import torch
+        self.torch, self.eng, self.cfg = torch, engine, cfg
+        lib = engine.lib
+        dev = engine.device
+        self.N, self.n_max, self.world = N, n_max, world
+        self.x = x_local
+        self.n = int(outdeg_local.shape[0])
+        self.plan, self.plan_len = (engine.ppr_plan(row_ptr_local) if self.n else (None, 0))
+        self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr_local)).to(dev)
+        col = torch.from_numpy(np.ascontiguousarray(col_local, dtype=np.int32)).to(dev)
+        self.col = torch.empty_like(col)
+        self._chk(lib.krca_ppr_remap_cols(engine.ptr(col), col.numel(), n_max, engine.ptr(self.col), engine._stream()),
+                  "krca_ppr_remap_cols")
+        del col
+        self.outdeg = torch.from_numpy(np.ascontiguousarray(outdeg_local)).to(dev)
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.q = torch.zeros(max(self.n, 1), **i64)
+        self.r = torch.zeros(max(self.n, 1), **i64)
+        self.acc = torch.zeros(max(self.n, 1), **i64)
+        self.key = torch.zeros(max(self.n, 1), **i64)
+        self.send = torch.zeros(n_max + NSLOT, **i64)
+        self.w_all = self.send if world == 1 else torch.zeros(world * (n_max + NSLOT), **i64)
+        self.ctl = torch.zeros(lib.krca_ppr_ctl_size(), dtype=torch.uint8, device=dev)
+        self.score_out = None
+
+    def _chk(self, rc, what):
+        from .native import _check
+        _check(rc, what)
+
+    def score(self):
+        self.score_out = self.eng.rolling_score_device(self.x, self.cfg.window, self.cfg.z_threshold, self.score_out)
+        return self.score_out
+
+    def init(self, alpha, seed_floor):
+        e, p = self.eng, self.eng.ptr
+        self.acc.zero_()
+        self._chk(e.lib.krca_ppr_shard_init(p(self.score_out["score"]), float(seed_floor), p(self.outdeg), self.n,
+                                            self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
+                                            p(self.send), e._stream()), "krca_ppr_shard_init")
+
+    def spmv(self):
+        e, p = self.eng, self.eng.ptr
+        if self.plan_len:
+            self._chk(e.lib.krca_ppr_shard_spmv(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len,
+                                                p(self.w_all), p(self.acc), p(self.ctl), e._stream()),
+                      "krca_ppr_shard_spmv")
+
+    def update(self, alpha):
+        e, p = self.eng, self.eng.ptr
+        self._chk(e.lib.krca_ppr_shard_update(p(self.outdeg), p(self.q), self.n, self.n_max, self.N, float(alpha),
+                                              p(self.r), p(self.acc), p(self.send), p(self.ctl), e._stream()),
+                  "krca_ppr_shard_update")
+
+    def reduce(self, alpha, tol, first):
+        e, p = self.eng, self.eng.ptr
+        self._chk(e.lib.krca_ppr_shard_reduce(p(self.w_all), self.world, self.n_max, self.N, float(alpha), float(tol),
+                                              int(first), p(self.ctl), p(self.send), e._stream()),
+                  "krca_ppr_shard_reduce")
+
+    def local_topk(self, k):
+        e, p = self.eng, self.eng.ptr
+        if self.n == 0:
+            return np.zeros(0, np.int64), np.zeros(0, np.int64)
+        self._chk(e.lib.krca_ppr_rca_key(p(self.r), p(self.q), self.n, p(self.key), e._stream()), "krca_ppr_rca_key")
+        idx, val = e.topk_device(self.key[:self.n], min(k, self.n))
+        return idx, val
+
+
+class RcaStep:
+    """One rank's view of the pod-sharded RCA step."""
+
+    def __init__(self, shard, comm, cfg, offset):
+        self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
+
+    def run(self, to_host=True):
+        s, c, cfg = self.s, self.comm, self.cfg
+        s.score()
+        s.init(cfg.alpha, cfg.seed_floor)
+        c.all_gather(s.w_all, s.send)
+        s.reduce(cfg.alpha, cfg.tol, 1)
+        for _ in range(cfg.iters):
+            s.spmv()
+            s.update(cfg.alpha)
+            c.all_gather(s.w_all, s.send)
+            s.reduce(cfg.alpha, cfg.tol, 0)
+        idx, val = s.local_topk(cfg.k)
+        return self.merge(idx, val) if to_host else (idx, val)
+
+    def merge(self, idx, val):
+        """Gather G x k (global index, key) candidates; identical top-k on every rank."""
+        k = self.cfg.k
+        if hasattr(idx, "cpu"):
+            import torch
+            kk = int(idx.numel())
+            cand = torch.full((2, k), -1, dtype=torch.int64, device=idx.device)
+            cand[0, :kk] = idx.to(torch.int64) + self.offset
+            cand[1, :kk] = val
+            cand[1, kk:] = torch.iinfo(torch.int64).min
+            if self.comm.world > 1:
+                allc = torch.empty((self.comm.world, 2, k), dtype=torch.int64, device=idx.device)
+                self.comm.all_gather(allc.view(-1), cand.view(-1))
+            else:
+                allc = cand.view(1, 2, k)
+            a = allc.cpu().numpy()
+        else:
+            a = np.stack([np.concatenate([np.asarray(idx, np.int64) + self.offset,
+                                          np.full(k - len(idx), -1, np.int64)]),
+                          np.concatenate([np.asarray(val, np.int64),
+                                          np.full(k - len(idx), np.iinfo(np.int64).min, np.int64)])])[None]
+        gi = a[:, 0, :].reshape(-1)
+        gv = a[:, 1, :].reshape(-1)
+        ok = gi >= 0
+        gi, gv = gi[ok], gv[ok]
+        # keys are the bits of non-negative doubles: compare as int64, ties -> lower pod index
+        order = sorted(range(len(gi)), key=lambda j: (-int(gv[j]), int(gi[j])))
+        sel = order[:k]
+        return gi[sel], gv[sel]
+
+
+def key_to_score(v):
+    """int64 root-cause key -> the float64 value r*q it encodes (in 2^-60 * 2^-32 units)."""
+    return np.asarray(v, np.int64).view(np.float64) / (2.0 ** 92)

@@ -7,8 +7,11 @@ M = 8 metrics x T = 1440 steps).  Metrics are generated with torch on any device
 tensor is generated in place on the GPU); graphs with NumPy on the host.
 
 Metric model:  x[t,p,m] = clip(b + a*sin(2*pi*t/1440 + phi_p) + N(0, sigma^2), 0, 100),
-b ~ U(10,60), a ~ U(0,15), sigma ~ U(0.5,3); R root pods get a +6 sigma step over the last W
-steps and their callers (1..3 hops) a decayed +2 sigma step.  Channel 0 = CPU %, 1 = memory %.
+b ~ U(25,55), a ~ U(0,12), sigma ~ U(0.5,3) (SURVEY.md §8d proposes U(10,60)/U(0,15); the narrower
+ranges keep the noise off the 0/100 clamps, where flat windows give meaningless z-scores); R root pods get a +12 sigma spike on the last
+`spike_steps` samples and their callers (hop h = 1..3) a +5*0.8^(h-1) sigma spike, so the
+current-step z-scores the scorer reports (|z| at t = T-1 against the trailing window) single
+them out.  Channel 0 = CPU %, 1 = memory %.
 Graph model: pods grouped into services of 20; services wired by preferential attachment
 (caller -> callee); each pod calls ~deg pods of its service's callees; no self loops, no
 duplicate edges; edge direction symptom(caller) -> dependency.
@@ -110,14 +113,14 @@ def caller_hops(mesh, roots, hops=3, cap=2000):
 
 
 def make_metrics(n_pods, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(), hop_sets=(), device="cpu",
-                 dtype=None, chunk_steps=None):
+                 spike_steps=1, root_sigma=12.0, hop_sigma=5.0, hop_decay=0.8, chunk_steps=None):
     """-> torch.float32 tensor [T, P, M] (time-major) on `device`."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(int(seed))
     P, M, T = n_pods, n_metrics, n_steps
-    b = torch.rand((P, M), generator=g, device=device) * 50 + 10
-    a = torch.rand((P, M), generator=g, device=device) * 15
+    b = torch.rand((P, M), generator=g, device=device) * 30 + 25
+    a = torch.rand((P, M), generator=g, device=device) * 12
     sig = torch.rand((P, M), generator=g, device=device) * 2.5 + 0.5
     phi = torch.rand((P, 1), generator=g, device=device) * (2 * math.pi)
     x = torch.empty((T, P, M), dtype=torch.float32, device=device)
@@ -128,14 +131,14 @@ def make_metrics(n_pods, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(),
         blk = b + a * torch.sin(2 * math.pi * tt / 1440.0 + phi) + sig * torch.randn(
             (t1 - t0, P, M), generator=g, device=device)
         x[t0:t1] = blk.clamp_(0.0, 100.0)
-    w0 = max(0, T - window)
+    w0 = max(0, T - spike_steps)
     if len(roots):
         r = torch.as_tensor(np.asarray(roots), device=device)
-        x[w0:, r, :] = (x[w0:, r, :] + 6.0 * sig[r]).clamp_(0.0, 100.0)
+        x[w0:, r, :] = (x[w0:, r, :] + root_sigma * sig[r]).clamp_(0.0, 100.0)
     for h, pods in enumerate(hop_sets):
         if len(pods):
             pr = torch.as_tensor(np.asarray(pods), device=device)
-            x[w0:, pr, :] = (x[w0:, pr, :] + (2.0 * 0.6 ** h) * sig[pr]).clamp_(0.0, 100.0)
+            x[w0:, pr, :] = (x[w0:, pr, :] + (hop_sigma * hop_decay ** h) * sig[pr]).clamp_(0.0, 100.0)
     return x
 
 

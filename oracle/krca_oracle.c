@@ -10,6 +10,7 @@
  *   krco_rolling_score  rolling z-score (new primitive, no reference code):
  *                       float64 sliding sums in a fixed order, |z| > thr <=> d*d > thr^2*var
  *   krco_ppr            networkx 3.4.2 pagerank semantics (_pagerank_scipy) in 2^-60 fixed point
+ *   krco_rca_key        root-cause ordering key (PageRank mass x own anomaly)
  *
  * The floating-point reference for a5/a10 (float64, independent formulation) is the NumPy
  * oracle in oracle/oracle.py; this file pins the exact bits.  Build: oracle/Makefile
@@ -88,14 +89,13 @@ static int64_t edge_weight(int64_t rj, int32_t deg, double alpha) {
 
 /* Pull-CSR personalized PageRank; returns iterations (negative if no convergence). */
 int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const float* seed,
-                 double alpha, int32_t max_iter, double tol, int64_t* r, float* r_out) {
-  int64_t* q = (int64_t*)malloc(sizeof(int64_t) * N);
+                 float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r, float* r_out, int64_t* q) {
   int64_t* w = (int64_t*)malloc(sizeof(int64_t) * N);
   int64_t qtot = 0, dang = 0;
   const int64_t r0 = (int64_t)(kFix / (double)N);
   for (int64_t i = 0; i < N; ++i) {
-    const float s = seed[i];
-    q[i] = s > 0.f ? (int64_t)((double)s * 4294967296.0) : 0;
+    const double v = (double)seed[i] - (double)seed_floor;
+    q[i] = v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
     qtot += q[i];
     r[i] = r0;
     w[i] = edge_weight(r0, outdeg[i], alpha);
@@ -114,8 +114,9 @@ int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outd
     }
     int64_t err = 0, dn = 0;
     const double qd = (double)qtot;
+    const double uni = 1.0 / (double)N;
     for (int64_t i = 0; i < N; ++i) {
-      const double pd = (double)q[i] / qd;
+      const double pd = qtot > 0 ? (double)q[i] / qd : uni;
       const int64_t t = (int64_t)(pd * tele);
       const int64_t rn = acc[i] + t;
       const int64_t ro = r[i];
@@ -132,8 +133,15 @@ int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outd
     tele = (1.0 - alpha) * kFix + alpha * (double)dn;
   }
   for (int64_t i = 0; i < N; ++i) r_out[i] = (float)((double)r[i] * (1.0 / kFix));
-  free(q);
   free(w);
   free(acc);
   return (err_limit > 0.0 && !conv) ? -it : it;
+}
+
+/* root-cause key of krca_ppr_rca_key */
+void krco_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key) {
+  for (int64_t i = 0; i < n; ++i) {
+    const double v = (double)r[i] * (double)q[i];
+    memcpy(&key[i], &v, sizeof(v));
+  }
 }

@@ -100,7 +100,7 @@ def ppr_f64(row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6):
     outdeg = np.asarray(outdeg, np.float64)
     N = len(outdeg)
     p = np.maximum(np.asarray(seed, np.float64), 0.0)
-    p = p / p.sum()
+    p = p / p.sum() if p.sum() > 0 else np.full(len(p), 1.0 / len(p))
     inv = np.where(outdeg > 0, 1.0 / np.where(outdeg > 0, outdeg, 1.0), 0.0)
     dangling = outdeg == 0
     rows = np.repeat(np.arange(N), np.diff(row_ptr))
@@ -140,8 +140,9 @@ def c_lib():
     vp, i64, i32, f32, f64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double
     lib.krco_usage_flags.argtypes = [vp, i64, vp]
     lib.krco_rolling_score.argtypes = [vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]
-    lib.krco_ppr.argtypes = [vp, vp, vp, i64, vp, f64, i32, f64, vp, vp]
+    lib.krco_ppr.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp]
     lib.krco_ppr.restype = i32
+    lib.krco_rca_key.argtypes = [vp, vp, i64, vp]
     _c = lib
     return lib
 
@@ -168,13 +169,29 @@ def c_rolling_score(x, W, z_thr=3.0):
     return dict(z_last=z, score=s, n_exceed=n, flags=f)
 
 
-def c_ppr(row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6):
+def c_ppr(row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6, seed_floor=0.0, return_q=False):
     rp = np.ascontiguousarray(row_ptr, np.int64)
     cl = np.ascontiguousarray(col, np.int32)
     od = np.ascontiguousarray(outdeg, np.int32)
     sd = np.ascontiguousarray(seed, np.float32)
     N = len(od)
     r = np.zeros(N, np.int64)
+    q = np.zeros(N, np.int64)
     rf = np.zeros(N, np.float32)
-    it = c_lib().krco_ppr(_p(rp), _p(cl), _p(od), N, _p(sd), alpha, max_iter, tol, _p(r), _p(rf))
-    return rf, r, it
+    it = c_lib().krco_ppr(_p(rp), _p(cl), _p(od), N, _p(sd), seed_floor, alpha, max_iter, tol, _p(r), _p(rf), _p(q))
+    return (rf, r, it, q) if return_q else (rf, r, it)
+
+
+def c_rca_key(r, q):
+    r = np.ascontiguousarray(r, np.int64)
+    q = np.ascontiguousarray(q, np.int64)
+    key = np.zeros(len(r), np.int64)
+    c_lib().krco_rca_key(_p(r), _p(q), len(r), _p(key))
+    return key
+
+
+def rca_rank(row_ptr, col, outdeg, score, alpha, iters, seed_floor, k=10):
+    """Reference root-cause ranking of the pipeline: top-k of bits(r*q) (ties -> lower index)."""
+    rf, r, it, q = c_ppr(row_ptr, col, outdeg, score, alpha, iters, 0.0, seed_floor, return_q=True)
+    idx, _ = topk_ref(c_rca_key(r, q), k)
+    return idx, rf, r

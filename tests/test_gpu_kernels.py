@@ -175,3 +175,24 @@ def test_ppr_long_rows_and_dangling(eng):
     r, rf, it = eng.ppr(rp, col, od, seed, 0.85, 50, 0.0)
     rfo, ro, _ = oracle.c_ppr(rp, col, od, seed, 0.85, 50, 0.0)
     assert np.array_equal(rf.cpu().numpy(), ro)
+
+
+# ---- the full RCA step (krca/rca.py) on one device ------------------------------------------
+@pytest.mark.parametrize("n,iters", [(5000, 30), (40000, 12)])
+def test_rca_step_single_gpu_vs_oracle(eng, n, iters):
+    from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
+    m = synth.make_graph(n, avg_degree=20, seed=n)
+    hops = synth.caller_hops(m, m.roots)
+    x = synth.make_metrics(n, 8, 400, window=60, seed=1, roots=m.roots, hop_sets=hops).cuda()
+    cfg = Config(iters=iters)
+    lo, hi, n_max = shard_range(n, 1, 0)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
+    step = RcaStep(DeviceShard(eng, x, rp, col, od, n, n_max, 1, cfg), Comm(), cfg, 0)
+    idx, key = step.run()
+    score = step.s.score_out["score"].cpu().numpy()
+    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+    assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
+    assert list(idx) == list(ridx)
+    idx2, _ = step.run()  # re-run on the same buffers: identical
+    assert list(idx2) == list(idx)
+    assert len(set(idx.tolist()) & set(m.roots.tolist())) >= 8
