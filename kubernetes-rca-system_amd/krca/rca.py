@@ -166,25 +166,19 @@ class RcaStep:
 
     def merge(self, idx, val):
         """Gather G x k (global index, key) candidates; identical top-k on every rank."""
+        import torch
         k = self.cfg.k
-        if hasattr(idx, "cpu"):
-            import torch
-            kk = int(idx.numel())
-            cand = torch.full((2, k), -1, dtype=torch.int64, device=idx.device)
-            cand[0, :kk] = idx.to(torch.int64) + self.offset
-            cand[1, :kk] = val
-            cand[1, kk:] = torch.iinfo(torch.int64).min
-            if self.comm.world > 1:
-                allc = torch.empty((self.comm.world, 2, k), dtype=torch.int64, device=idx.device)
-                self.comm.all_gather(allc.view(-1), cand.view(-1))
-            else:
-                allc = cand.view(1, 2, k)
-            a = allc.cpu().numpy()
-        else:
-            a = np.stack([np.concatenate([np.asarray(idx, np.int64) + self.offset,
-                                          np.full(k - len(idx), -1, np.int64)]),
-                          np.concatenate([np.asarray(val, np.int64),
-                                          np.full(k - len(idx), np.iinfo(np.int64).min, np.int64)])])[None]
+        if not isinstance(idx, torch.Tensor):
+            idx = torch.from_numpy(np.asarray(idx, np.int64))
+            val = torch.from_numpy(np.asarray(val, np.int64))
+        kk = int(idx.numel())
+        cand = torch.full((2, k), -1, dtype=torch.int64, device=idx.device)
+        cand[0, :kk] = idx.to(torch.int64) + self.offset
+        cand[1, :kk] = val.to(torch.int64)
+        cand[1, kk:] = torch.iinfo(torch.int64).min
+        allc = torch.empty((self.comm.world, 2, k), dtype=torch.int64, device=idx.device)
+        self.comm.all_gather(allc.view(-1), cand.view(-1))
+        a = allc.cpu().numpy()
         gi = a[:, 0, :].reshape(-1)
         gv = a[:, 1, :].reshape(-1)
         ok = gi >= 0

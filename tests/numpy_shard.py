@@ -1,0 +1,98 @@
+"""NumPy restatement of krca.rca.DeviceShard — TESTS ONLY.
+
+Same integer/float64 expressions as csrc/ppr.hip (shard kernels) and oracle/krca_oracle.c, so
+the distributed orchestration of krca/rca.py (partitioning, column remap, one all-gather per
+iteration with the partial sums in the payload, candidate merge) can be exercised on CPU with
+the gloo backend and compared bit-for-bit with the single-process oracle.
+"""
+import numpy as np
+import torch
+
+import oracle
+from krca.rca import NSLOT
+
+FIX = 1152921504606846976.0
+
+
+def _w(r, deg, alpha):
+    out = np.zeros(len(r), np.int64)
+    nz = deg > 0
+    coef = alpha / deg[nz].astype(np.float64)
+    out[nz] = (r[nz].astype(np.float64) * coef).astype(np.int64)
+    return out
+
+
+class NumpyShard:
+    def __init__(self, x_local, row_ptr_local, col_local, outdeg_local, N, n_max, world, cfg):
+        self.cfg, self.N, self.n_max, self.world = cfg, N, n_max, world
+        self.x = np.asarray(x_local, np.float32)
+        self.rp = np.asarray(row_ptr_local, np.int64)
+        c = np.asarray(col_local, np.int64)
+        self.col = c + NSLOT * (c // n_max)
+        self.deg = np.asarray(outdeg_local, np.int32)
+        self.n = len(self.deg)
+        self.rows = np.repeat(np.arange(self.n), np.diff(self.rp))
+        self.send = torch.zeros(n_max + NSLOT, dtype=torch.int64)
+        self.w_all = self.send if world == 1 else torch.zeros(world * (n_max + NSLOT), dtype=torch.int64)
+        self.ctl = {}
+
+    def score(self):
+        self.score_out = oracle.c_rolling_score(self.x, self.cfg.window, self.cfg.z_threshold)
+        return self.score_out
+
+    def init(self, alpha, floor):
+        s = self.score_out["score"]
+        v = s.astype(np.float64) - np.float64(np.float32(floor))
+        self.q = np.where(v > 0, (np.maximum(v, 0) * 4294967296.0).astype(np.int64), 0)
+        r0 = np.int64(FIX / float(self.N))
+        self.r = np.full(self.n, r0, np.int64)
+        self.acc = np.zeros(self.n, np.int64)
+        snd = self.send.numpy()
+        snd[:] = 0
+        snd[:self.n] = _w(self.r, self.deg, alpha)
+        snd[self.n_max + 1] = int(self.r[self.deg == 0].sum())
+        snd[self.n_max + 2] = int(self.q.sum())
+        self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
+
+    def spmv(self):
+        if self.ctl["converged"]:
+            return
+        w = self.w_all.numpy()
+        vals = w[self.col]
+        self.acc = np.zeros(self.n, np.int64)
+        np.add.at(self.acc, self.rows, vals)
+
+    def update(self, alpha):
+        if self.ctl["converged"]:
+            return
+        qt = self.ctl["q_total"]
+        pd = self.q.astype(np.float64) / float(qt) if qt > 0 else np.full(self.n, 1.0 / float(self.N))
+        t = (pd * self.ctl["tele"]).astype(np.int64)
+        rn = self.acc + t
+        err = int(np.abs(rn - self.r).sum())
+        self.r = rn
+        snd = self.send.numpy()
+        snd[:self.n] = _w(rn, self.deg, alpha)
+        snd[self.n_max] += err
+        snd[self.n_max + 1] += int(rn[self.deg == 0].sum())
+
+    def reduce(self, alpha, tol, first):
+        w = self.w_all.numpy().reshape(self.world, self.n_max + NSLOT)
+        err, dang, qs = (int(w[:, self.n_max + i].sum()) for i in range(NSLOT))
+        self.send.numpy()[self.n_max:] = 0
+        c = self.ctl
+        if c["converged"]:
+            return
+        if first:
+            c["q_total"] = qs
+        else:
+            c["iter"] += 1
+            lim = float(self.N) * tol * FIX if tol > 0 else 0.0
+            if lim > 0 and float(err) < lim:
+                c["converged"] = c["iter"]
+                return
+        c["tele"] = (1.0 - alpha) * FIX + alpha * float(dang)
+
+    def local_topk(self, k):
+        key = (self.r.astype(np.float64) * self.q.astype(np.float64)).view(np.int64)
+        return oracle.topk_ref(key, min(k, self.n))

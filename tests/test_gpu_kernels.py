@@ -158,8 +158,14 @@ def test_ppr_bit_exact_vs_oracle(eng, n, deg, tol, iters):
     rfo, ro, ito = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, iters, tol)
     assert it == abs(ito)
     assert np.array_equal(rf.cpu().numpy(), ro)  # bit-identical fixed point
-    x, _ = oracle.ppr_f64(m.row_ptr, m.col, m.outdeg, seed.astype(np.float64), 0.85, it, 0.0)
-    assert np.max(np.abs(r.cpu().numpy() - x) / np.maximum(x, 1e-30)) < 1e-5
+    # float64 restatement fed the same 2^-32-quantised seeds: 1e-5 relative on every rank that
+    # carries at least 1e-9 of the mass (below that the 2^-60 fixed point is the tolerance)
+    qs = np.floor(seed.astype(np.float64) * 2.0 ** 32) / 2.0 ** 32
+    x, _ = oracle.ppr_f64(m.row_ptr, m.col, m.outdeg, qs, 0.85, it, 0.0)
+    rr = r.cpu().numpy().astype(np.float64)
+    big = x >= 1e-9
+    assert np.max(np.abs(rr[big] - x[big]) / x[big]) < 1e-5
+    assert np.max(np.abs(rr[~big] - x[~big])) < 1e-13
     idx, _ = eng.topk(rf, 10)
     assert np.array_equal(idx, oracle.topk_ref(ro, 10)[0])
 
