@@ -52,9 +52,10 @@ int krca_usage_flags(const float* usage /*[P][2]*/, int64_t P, uint8_t* flags /*
 
 /* ---- a5: rolling z-score anomaly scoring (new primitive; plugs in at
  * ref:agents/metrics_agent.py:44-47).  x is time-major [T][P][M] float32 (series s = p*M+m).
- * For t in [W, T): mean/var of x[t-W..t-1] (ddof 0, float64 sliding sums in a fixed order),
- * exceed(t) = var > 1e-12 && (x_t - mean)^2 > z_thr^2 * var.   Outputs:
- *   z_last[p][m] = (x_{T-1} - mean)/sqrt(var) (0 if var <= 1e-12),   score[p] = max_m |z_last|,
+ * For t in [W, T), over the trailing window x[t-W..t-1] (float64 sliding sums s1, s2 in a fixed
+ * order): A = W*x_t - s1, B = W*s2 - s1^2 (= W^2 var, ddof 0), z = A/sqrt(B) = (x_t - mean)/std;
+ * exceed(t) = B > 1e-12*W^2 && A^2 > z_thr^2 * B.   Outputs:
+ *   z_last[p][m] = z at t = T-1 (0 if B <= 1e-12*W^2),   score[p] = max_m |z_last|,
  *   n_exceed[p]  = sum over m, t of exceed(t) (bit-exact vs oracle/krca_oracle.c),
  *   flags[p]     = KRCA_F_* of x[T-1][p][0] (CPU %) and x[T-1][p][1] (memory %) if M >= 2.
  * M must be a power of two <= 64. */

@@ -10,9 +10,12 @@
 // W-step block), so each input byte crosses HBM exactly once: 4*P*M*T bytes per call.  The
 // window statistics are float64 sliding sums updated in a FIXED order, so the integer outputs
 // (n_exceed, flags) are bit-identical to the C restatement in oracle/krca_oracle.c; the
-// threshold test is |z| > thr  <=>  d*d > thr^2*var, with no division or square root.
+// threshold test is |z| > thr  <=>  A^2 > thr^2*B (A = W*x - s1, B = W*s2 - s1^2), with no
+// division or square root; all products that feed a decision are explicit fma()s.
 // Pod-level reductions (max |z|, sum of exceedances, flag OR) are wave shuffles inside the
 // aligned M-lane group of the pod.
+#include <stdlib.h>
+
 #include "krca_common.h"
 
 #pragma clang fp contract(off)
@@ -34,32 +37,35 @@ __global__ __launch_bounds__(256) void usage_flags_kernel(const float2* __restri
 struct StepState {
   double s1, s2;  // window sum and sum of squares (float64, fixed order)
   int cnt;        // exceedances of this series
-  double dl, varl;  // deviation and variance at t = T-1
+  double al, bl;  // A and B (below) at t = T-1
 };
 
-// One time step of the rolling statistics.  `old` is x[t-W].
-__device__ __forceinline__ void step(StepState& st, float v, float old, double invW, double thr2, bool last) {
+// One time step of the rolling statistics; `old` is x[t-W].  With A = W*x_t - s1 and
+// B = W*s2 - s1^2 (= W^2 * var, ddof 0):  z = A / sqrt(B),  |z| > thr  <=>  A^2 > thr^2 * B,
+// var > 1e-12  <=>  B > 1e-12 * W^2 — 13 float64 operations per sample, no division or sqrt.
+// The fma()s are explicit (and mirrored in oracle/krca_oracle.c): one rounding each.
+__device__ __forceinline__ void step(StepState& st, float v, float old, double Wd, double epsB, double thr2,
+                                     bool last) {
   const double vd = (double)v;
-  const double mean = st.s1 * invW;
-  const double var = st.s2 * invW - mean * mean;
-  const double d = vd - mean;
-  st.cnt += (var > kVarEps) && (d * d > thr2 * var);
-  if (last) {
-    st.dl = d;
-    st.varl = var;
-  }
   const double od = (double)old;
-  st.s1 = st.s1 + (vd - od);
-  st.s2 = st.s2 + (vd * vd - od * od);
+  const double A = fma(Wd, vd, -st.s1);
+  const double B = fma(Wd, st.s2, -(st.s1 * st.s1));
+  st.cnt += (B > epsB) && (fma(A, A, -(thr2 * B)) > 0.0);
+  if (last) {
+    st.al = A;
+    st.bl = B;
+  }
+  st.s1 = (st.s1 + vd) - od;
+  st.s2 = fma(-od, od, fma(vd, vd, st.s2));
 }
 
 // Pod epilogue shared by both kernels: z_last per series, pod max|z|, exceedance sum, flags.
-__device__ __forceinline__ void pod_epilogue(const StepState& st, int64_t s, bool active, int M, int T,
+__device__ __forceinline__ void pod_epilogue(const StepState& st, double epsB, int64_t s, bool active, int M, int T,
                                              const float* __restrict__ xs, int64_t S,
                                              float* __restrict__ z_last, float* __restrict__ score,
                                              int32_t* __restrict__ n_exceed, uint8_t* __restrict__ flags) {
-  const bool has_z = st.varl > kVarEps;
-  const float z = has_z ? (float)(st.dl / sqrt(st.varl)) : 0.f;
+  const bool has_z = st.bl > epsB;
+  const float z = has_z ? (float)(st.al / sqrt(st.bl)) : 0.f;
   const int m = (int)(s & (M - 1));
   float vlast = (active && T > 0) ? xs[(int64_t)(T - 1) * S] : 0.f;
   unsigned f = 0;
@@ -90,7 +96,7 @@ __global__ __launch_bounds__(256) void rolling_score_ring(const float* __restric
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = s < S;
   const float* xs = x + (active ? s : 0);
-  const double invW = 1.0 / (double)W;
+  const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
   StepState st{0.0, 0.0, 0, 0.0, 0.0};
   float ring[W];
 #pragma unroll
@@ -99,7 +105,7 @@ __global__ __launch_bounds__(256) void rolling_score_ring(const float* __restric
     ring[j] = v;
     const double vd = (double)v;
     st.s1 = st.s1 + vd;
-    st.s2 = st.s2 + vd * vd;
+    st.s2 = fma(vd, vd, st.s2);
   }
   int t0 = W;
   for (; t0 + W <= T; t0 += W) {  // full W-step blocks: every ring slot index is static
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(256) void rolling_score_ring(const float* __restric
     for (int j = 0; j < W; ++j) nx[j] = active ? xs[(int64_t)(t0 + j) * S] : 0.f;
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-      step(st, nx[j], ring[j], invW, thr2, t0 + j == T - 1);
+      step(st, nx[j], ring[j], Wd, epsB, thr2, t0 + j == T - 1);
       ring[j] = nx[j];
     }
   }
@@ -117,12 +123,70 @@ __global__ __launch_bounds__(256) void rolling_score_ring(const float* __restric
     for (int j = 0; j < W; ++j) {
       if (t0 + j < T) {
         const float v = active ? xs[(int64_t)(t0 + j) * S] : 0.f;
-        step(st, v, ring[j], invW, thr2, t0 + j == T - 1);
+        step(st, v, ring[j], Wd, epsB, thr2, t0 + j == T - 1);
         ring[j] = v;
       }
     }
   }
-  pod_epilogue(st, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
+  pod_epilogue(st, epsB, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
+}
+
+// Same arithmetic as rolling_score_ring; addressing for gfx950 buffer loads: per W-step block a
+// wave-uniform buffer descriptor on the block's first row, the lane's 32-bit byte offset in
+// voffset and the row offset j*S*4 in soffset, so a load costs no per-lane address arithmetic
+// (`buffer_load_dword v, v_off, s[rsrc], s_off offen`).  Requires 4*S*W < 2^31.
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void rolling_score_ring_buf(const float* __restrict__ x, int64_t S, int T, int M,
+                                                              double thr2, float* __restrict__ z_last,
+                                                              float* __restrict__ score,
+                                                              int32_t* __restrict__ n_exceed,
+                                                              uint8_t* __restrict__ flags) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = s < S;
+  const uint32_t voff = active ? (uint32_t)s * 4u : 0u;
+  const uint32_t rowb = (uint32_t)(S * 4);  // bytes per time row
+  const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
+  StepState st{0.0, 0.0, 0, 0.0, 0.0};
+  float ring[W];
+  const int Tw = T < W ? T : W;
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(rowb * (uint32_t)Tw), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const float v = j < T ? bload(rs, voff, rowb * j) : 0.f;
+    ring[j] = v;
+    const double vd = (double)v;
+    st.s1 = st.s1 + vd;
+    st.s2 = fma(vd, vd, st.s2);
+  }
+  int t0 = W;
+  for (; t0 + W <= T; t0 += W) {
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)t0 * S), 0, (int)(rowb * (uint32_t)W), 0x00020000);
+    float nx[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) nx[j] = bload(rs, voff, rowb * j);
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      step(st, nx[j], ring[j], Wd, epsB, thr2, t0 + j == T - 1);
+      ring[j] = nx[j];
+    }
+  }
+  if (t0 < T) {
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)t0 * S), 0, (int)(rowb * (uint32_t)(T - t0)),
+                                           0x00020000);
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (t0 + j < T) {
+        const float v = bload(rs, voff, rowb * j);
+        step(st, v, ring[j], Wd, epsB, thr2, t0 + j == T - 1);
+        ring[j] = v;
+      }
+    }
+  }
+  pod_epilogue(st, epsB, s, active, M, T, x + (active ? s : 0), S, z_last, score, n_exceed, flags);
 }
 
 // Any W: the outgoing sample x[t-W] is re-read (same values, same arithmetic -> same bits).
@@ -134,19 +198,19 @@ __global__ __launch_bounds__(256) void rolling_score_reread(const float* __restr
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = s < S;
   const float* xs = x + (active ? s : 0);
-  const double invW = 1.0 / (double)W;
+  const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
   StepState st{0.0, 0.0, 0, 0.0, 0.0};
   for (int j = 0; j < W && j < T; ++j) {
     const double vd = active ? (double)xs[(int64_t)j * S] : 0.0;
     st.s1 = st.s1 + vd;
-    st.s2 = st.s2 + vd * vd;
+    st.s2 = fma(vd, vd, st.s2);
   }
   for (int t = W; t < T; ++t) {
     const float v = active ? xs[(int64_t)t * S] : 0.f;
     const float o = active ? xs[(int64_t)(t - W) * S] : 0.f;
-    step(st, v, o, invW, thr2, t == T - 1);
+    step(st, v, o, Wd, epsB, thr2, t == T - 1);
   }
-  pod_epilogue(st, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
+  pod_epilogue(st, epsB, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
 }
 
 }  // namespace
@@ -174,11 +238,20 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
   const double thr2 = (double)z_thr * (double)z_thr;
   const dim3 grid((unsigned)krca::ceil_div(S, 256)), block(256);
   hipStream_t st = krca::as_stream(stream);
+  static const int impl = [] {  // A/B switch for kernel development (0 = default)
+    const char* e = getenv("KRCA_SCORE_IMPL");
+    return e ? atoi(e) : 0;
+  }();
+  KRCA_CHECK_ARG(S < (int64_t(1) << 32), "krca_rolling_score: P*M must be < 2^32");
   switch (W) {
-#define KRCA_W(WV)                                                                                     \
-  case WV:                                                                                             \
-    hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
-                       n_exceed, flags);                                                              \
+#define KRCA_W(WV)                                                                                       \
+  case WV:                                                                                               \
+    if (impl == 0 && S * 4 * WV < (int64_t(1) << 31))                                                    \
+      hipLaunchKernelGGL(rolling_score_ring_buf<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
+                         n_exceed, flags);                                                              \
+    else                                                                                                 \
+      hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score,   \
+                         n_exceed, flags);                                                              \
     break;
     KRCA_W(10)
     KRCA_W(15)

@@ -8,7 +8,7 @@
  *
  *   krco_usage_flags    ref:agents/metrics_agent.py:88-114, 135-161 (x > 80, high if > 90)
  *   krco_rolling_score  rolling z-score (new primitive, no reference code):
- *                       float64 sliding sums in a fixed order, |z| > thr <=> d*d > thr^2*var
+ *                       float64 sliding sums in a fixed order, |z| > thr <=> A^2 > thr^2*B
  *   krco_ppr            networkx 3.4.2 pagerank semantics (_pagerank_scipy) in 2^-60 fixed point
  *   krco_rca_key        root-cause ordering key (PageRank mass x own anomaly)
  *
@@ -32,11 +32,13 @@ void krco_usage_flags(const float* usage, int64_t P, uint8_t* flags) {
   }
 }
 
-/* x: time-major [T][P][M] float32.  Same outputs as krca_rolling_score. */
+/* x: time-major [T][P][M] float32.  Same outputs as krca_rolling_score, same operations in the
+ * same order: A = fma(W, x_t, -s1), B = fma(W, s2, -s1*s1), exceed iff B > 1e-12*W*W and
+ * fma(A, A, -thr^2*B) > 0; s1 = (s1 + x_t) - x_{t-W}; s2 = fma(-x_{t-W}, x_{t-W}, fma(x_t, x_t, s2)). */
 void krco_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr, float* z_last,
                         float* score, int32_t* n_exceed, uint8_t* flags) {
   const int64_t S = P * (int64_t)M;
-  const double invW = 1.0 / (double)W;
+  const double Wd = (double)W, epsB = VAR_EPS * Wd * Wd;
   const double thr2 = (double)z_thr * (double)z_thr;
 #pragma omp parallel for schedule(static)
   for (int64_t p = 0; p < P; ++p) {
@@ -45,27 +47,26 @@ void krco_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t
     unsigned f = 0;
     for (int32_t m = 0; m < M; ++m) {
       const int64_t s = p * M + m;
-      double s1 = 0.0, s2 = 0.0, dl = 0.0, varl = 0.0;
+      double s1 = 0.0, s2 = 0.0, al = 0.0, bl = 0.0;
       for (int32_t j = 0; j < W && j < T; ++j) {
         const double vd = (double)x[(int64_t)j * S + s];
         s1 = s1 + vd;
-        s2 = s2 + vd * vd;
+        s2 = fma(vd, vd, s2);
       }
       for (int32_t t = W; t < T; ++t) {
         const double vd = (double)x[(int64_t)t * S + s];
-        const double mean = s1 * invW;
-        const double var = s2 * invW - mean * mean;
-        const double d = vd - mean;
-        cnt += (var > VAR_EPS) && (d * d > thr2 * var);
-        if (t == T - 1) {
-          dl = d;
-          varl = var;
-        }
         const double od = (double)x[(int64_t)(t - W) * S + s];
-        s1 = s1 + (vd - od);
-        s2 = s2 + (vd * vd - od * od);
+        const double A = fma(Wd, vd, -s1);
+        const double B = fma(Wd, s2, -(s1 * s1));
+        cnt += (B > epsB) && (fma(A, A, -(thr2 * B)) > 0.0);
+        if (t == T - 1) {
+          al = A;
+          bl = B;
+        }
+        s1 = (s1 + vd) - od;
+        s2 = fma(-od, od, fma(vd, vd, s2));
       }
-      const float z = varl > VAR_EPS ? (float)(dl / sqrt(varl)) : 0.f;
+      const float z = bl > epsB ? (float)(al / sqrt(bl)) : 0.f;
       z_last[s] = z;
       const float az = fabsf(z);
       if (az > best) best = az;

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Short driver for rocprofv3 runs (kernel trace / PMC passes) of single krca kernels.
+
+  python tools/prof_kernels.py score  [--pods 1000000] [--reps 3]
+  python tools/prof_kernels.py ppr    [--pods 1000000] [--reps 3]
+  python tools/prof_kernels.py logs   [--docs 1000000] [--reps 3]
+Prints per-kernel event-timed averages and the algorithmic bytes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
+
+
+def timed(torch, fn, reps):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["score", "ppr", "logs"])
+    ap.add_argument("--pods", type=int, default=1_000_000)
+    ap.add_argument("--docs", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--tsteps", type=int, default=1440)
+    a = ap.parse_args()
+    import torch
+    from krca import native, synth
+    eng = native.NativeEngine(0)
+    out = {}
+    if a.what == "score":
+        x = synth.make_metrics(a.pods, 8, a.tsteps, device="cuda")
+        o = eng.rolling_score_device(x)
+        ms = timed(torch, lambda: eng.rolling_score_device(x, out=o), a.reps)
+        nbytes = 4 * a.pods * 8 * a.tsteps + 4 * a.pods * 8 + 9 * a.pods
+        out = dict(kernel="krca_rolling_score", ms=ms, bytes=nbytes, gbs=nbytes / (min(ms) * 1e-3) / 1e9)
+    elif a.what == "ppr":
+        from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
+        m = synth.make_graph(a.pods, avg_degree=20, seed=0)
+        x = synth.make_metrics(a.pods, 8, 64, device="cuda", roots=m.roots)
+        cfg = Config(iters=30, window=30)
+        rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, a.pods)
+        sh = DeviceShard(eng, x, rp, col, od, a.pods, a.pods, 1, cfg)
+        step = RcaStep(sh, Comm(), cfg, 0)
+        step.run()
+        ms = timed(torch, lambda: step.run(to_host=False), a.reps)
+        N, E = a.pods, m.n_edges
+        per_iter = 8 * (N + 1) + 4 * E + 8 * N + 8 * N + 8 * N  # row_ptr, col, w(compulsory), acc, w out
+        out = dict(kernel="ppr step (30 it)", ms=ms, edges=E, bytes_per_iter=per_iter)
+    else:
+        from krca.agents.logs import pack_documents
+        docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
+        blob, off = pack_documents(docs)
+        text = eng.upload_blob(blob)
+        offd = torch.from_numpy(off).cuda()
+        eng.log_scan_device(text, offd)
+        ms = timed(torch, lambda: eng.log_scan_device(text, offd), a.reps)
+        L = sum(d.count("\n") + (1 if d and not d.endswith("\n") else 0) for d in docs[:1000]) / 1000 * a.docs
+        out = dict(kernel="log scan", ms=ms, bytes=len(blob), lines=L, docs=a.docs,
+                   gbs=len(blob) / (min(ms) * 1e-3) / 1e9)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
