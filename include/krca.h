@@ -109,7 +109,7 @@ int krca_ppr_shard_spmv(const int64_t* row_ptr, const int32_t* col /*remapped*/,
                         const void* ctl, void* stream);
 int krca_ppr_shard_update(const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                           int64_t N, double alpha, int64_t* r_local, int64_t* acc, int64_t* send,
-                          const void* ctl, void* stream);
+                          void* ctl, void* stream);
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
                           double tol, int32_t first, void* ctl, int64_t* send, void* stream);
 int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);

@@ -42,7 +42,14 @@ struct Ctl {        // device control block
   int64_t q_total;  // sum of quantised seeds over all ranks
   int32_t converged;  // iteration count at convergence (0 = running)
   int32_t iter;       // iterations done
+  uint32_t ticket;    // arrival counter of the last-block reduction (0 between kernels)
 };
+constexpr int MAX_BLOCKS = 2048;  // grid cap of the node-parallel kernels (partials array size)
+constexpr int CTL_BYTES = 256;    // Ctl, then int64 partials[2 * MAX_BLOCKS]
+
+__device__ __forceinline__ int64_t* partials(Ctl* ctl) {
+  return reinterpret_cast<int64_t*>(reinterpret_cast<char*>(ctl) + CTL_BYTES);
+}
 
 __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
   for (int off = 32; off > 0; off >>= 1) v += (int64_t)__shfl_xor((long long)v, off, 64);
@@ -58,6 +65,43 @@ __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
 
 __device__ __forceinline__ void add_slot(int64_t* slot, int64_t v) {
   atomicAdd(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)v);
+}
+
+// Two block sums (a, b) reduced over the grid without contended atomics (MI355X_MICROARCH
+// "fanin"): every block stores its pair, then arrives on ONE ticket (release -> relaxed agent
+// add, cdna_hip_programming.md §6 Guideline 16 counter form); the last arriver acquires, sums
+// the pairs in a fixed order (integers: order-free anyway) and stores them to out[0..1].
+__device__ void grid_sum2(int64_t a, int64_t b, Ctl* ctl, int64_t* out, int64_t* red) {
+  __shared__ int is_last;
+  a = block_sum_i64(a, red);
+  b = block_sum_i64(b, red);
+  int64_t* part = partials(ctl);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int64_t sa = 0, sb = 0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += TPB) {
+    sa += part[2 * i];
+    sb += part[2 * i + 1];
+  }
+  sa = block_sum_i64(sa, red);
+  sb = block_sum_i64(sb, red);
+  if (threadIdx.x == 0) {
+    out[0] = sa;
+    out[1] = sb;
+    ctl->ticket = 0;
+  }
 }
 
 // w_j for node j given its fixed-point rank rj
@@ -76,7 +120,7 @@ __device__ __forceinline__ int64_t quantise(float s, float floor_) {
 __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, float seed_floor,
                                                 const int32_t* __restrict__ outdeg, int64_t n, int64_t N,
                                                 double alpha, int64_t* __restrict__ q, int64_t* __restrict__ r,
-                                                int64_t* __restrict__ send, int64_t n_max) {
+                                                int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
   __shared__ int64_t red[TPB / 64];
   const int64_t r0 = (int64_t)(krca::kFix / (double)N);
   int64_t dang = 0, qs = 0;
@@ -89,39 +133,53 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
     send[i] = edge_weight(r0, deg, alpha);
     if (deg == 0) dang += r0;
   }
-  int64_t t = block_sum_i64(dang, red);
-  if (threadIdx.x == 0 && t) add_slot(&send[n_max + 1], t);
-  t = block_sum_i64(qs, red);
-  if (threadIdx.x == 0 && t) add_slot(&send[n_max + 2], t);
+  grid_sum2(dang, qs, ctl, send + n_max + 1, red);
 }
 
 __global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                                                 const int32_t* __restrict__ plan, const int64_t* __restrict__ w,
                                                 int64_t* __restrict__ acc, const Ctl* __restrict__ ctl) {
+  constexpr int K = EDGE_BUDGET / TPB;  // edges per lane: all col loads, then all gathers, in flight
   __shared__ int64_t lds[EDGE_BUDGET];
   __shared__ int64_t red[TPB / 64];
   if (ctl->converged) return;
   const int32_t rb = plan[2 * blockIdx.x];
   const int32_t code = plan[2 * blockIdx.x + 1];
-  if (code > 0) {  // short rows [rb, code)
-    const int32_t re = code;
-    const int64_t e0 = row_ptr[rb], e1 = row_ptr[re];
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += TPB) lds[e - e0] = w[col[e]];
+  int64_t e0, e1;
+  if (code > 0) {
+    e0 = row_ptr[rb];
+    e1 = row_ptr[code];
+  } else {
+    e0 = row_ptr[rb] + (int64_t)(-code) * EDGE_BUDGET;
+    e1 = std::min<int64_t>(row_ptr[rb + 1], e0 + EDGE_BUDGET);
+  }
+  int32_t c[K];
+  int64_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t e = e0 + threadIdx.x + k * TPB;
+    c[k] = e < e1 ? col[e] : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = c[k] >= 0 ? w[c[k]] : 0;
+  if (code > 0) {  // short rows [rb, code): stage the gathered segment in LDS, lane r sums row r
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t e = threadIdx.x + k * TPB;
+      if (e0 + e < e1) lds[e] = v[k];
+    }
     __syncthreads();
     const int32_t row = rb + (int32_t)threadIdx.x;
-    if (row < re) {
+    if (row < code) {
       const int64_t a = row_ptr[row] - e0, b = row_ptr[row + 1] - e0;
       int64_t s = 0;
       for (int64_t e = a; e < b; ++e) s += lds[e];
       acc[row] = s;
     }
-  } else {  // chunk -code of long row rb (acc[rb] was zeroed by the previous update)
-    const int64_t c = -(int64_t)code;
-    const int64_t r0 = row_ptr[rb], r1 = row_ptr[rb + 1];
-    const int64_t e0 = r0 + c * EDGE_BUDGET;
-    const int64_t e1 = std::min<int64_t>(r1, e0 + EDGE_BUDGET);
+  } else {  // chunk of long row rb (acc[rb] was zeroed by the previous update)
     int64_t s = 0;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += TPB) s += w[col[e]];
+#pragma unroll
+    for (int k = 0; k < K; ++k) s += v[k];
     const int64_t tot = block_sum_i64(s, red);
     if (threadIdx.x == 0) add_slot(&acc[rb], tot);
   }
@@ -130,7 +188,7 @@ __global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_
 __global__ __launch_bounds__(TPB) void ppr_update(const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
                                                   int64_t n, int64_t N, double alpha, int64_t* __restrict__ r,
                                                   int64_t* __restrict__ acc, int64_t* __restrict__ send,
-                                                  int64_t n_max, const Ctl* __restrict__ ctl) {
+                                                  int64_t n_max, Ctl* ctl) {
   __shared__ int64_t red[TPB / 64];
   if (ctl->converged) return;
   const double tele = ctl->tele;
@@ -150,10 +208,7 @@ __global__ __launch_bounds__(TPB) void ppr_update(const int32_t* __restrict__ ou
     if (deg == 0) dang += rn;
     send[i] = edge_weight(rn, deg, alpha);
   }
-  int64_t t = block_sum_i64(err, red);
-  if (threadIdx.x == 0 && t) add_slot(&send[n_max], t);
-  t = block_sum_i64(dang, red);
-  if (threadIdx.x == 0 && t) add_slot(&send[n_max + 1], t);
+  grid_sum2(err, dang, ctl, send + n_max, red);
 }
 
 // one lane: sum the G gathered partial slots (integer -> order-free), decide convergence,
@@ -235,7 +290,9 @@ int64_t build_plan(const int64_t* rp, int64_t N, int32_t* out) {
   return n;
 }
 
-unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), 2048)); }
+unsigned grid_for(int64_t n) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), MAX_BLOCKS));
+}
 
 }  // namespace
 
@@ -256,7 +313,7 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, in
   return KRCA_OK;
 }
 
-int64_t krca_ppr_ctl_size(void) { return 256; }
+int64_t krca_ppr_ctl_size(void) { return CTL_BYTES + 16 * MAX_BLOCKS; }
 
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream) {
   KRCA_CHECK_ARG(E >= 0 && n_max > 0, "krca_ppr_remap_cols: bad sizes");
@@ -275,9 +332,9 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
   KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)), "krca_ppr_shard_init: null pointer");
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
-  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
+  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));  // residual slot stays 0
   hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N, alpha,
-                     q_local, r_local, send, n_max);
+                     q_local, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -294,11 +351,11 @@ int krca_ppr_shard_spmv(const int64_t* row_ptr, const int32_t* col, const int32_
 }
 
 int krca_ppr_shard_update(const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N,
-                          double alpha, int64_t* r_local, int64_t* acc, int64_t* send, const void* ctl, void* stream) {
+                          double alpha, int64_t* r_local, int64_t* acc, int64_t* send, void* ctl, void* stream) {
   KRCA_CHECK_ARG(n_local >= 0 && n_local <= n_max && N > 0, "krca_ppr_shard_update: bad sizes");
   KRCA_CHECK_ARG(send && ctl && (n_local == 0 || (outdeg && q_local && r_local && acc)), "krca_ppr_shard_update: null pointer");
   hipLaunchKernelGGL(ppr_update, dim3(grid_for(n_local)), dim3(TPB), 0, krca::as_stream(stream), outdeg, q_local,
-                     n_local, N, alpha, r_local, acc, send, n_max, reinterpret_cast<const Ctl*>(ctl));
+                     n_local, N, alpha, r_local, acc, send, n_max, reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -341,8 +398,8 @@ int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key
   return KRCA_OK;
 }
 
-// workspace: ctl (256 B) | q[N] | acc[N] | send/w_all[N+3] | r (if r_fixed == NULL) [N]
-int64_t krca_ppr_workspace_size(int64_t N) { return 256 + (4 * N + NSLOT) * 8 + 256; }
+// workspace: ctl (krca_ppr_ctl_size) | q[N] | acc[N] | send/w_all[N+3] | r (if r_fixed == NULL) [N]
+int64_t krca_ppr_workspace_size(int64_t N) { return krca_ppr_ctl_size() + (4 * N + NSLOT) * 8 + 256; }
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int32_t* plan,
              int64_t plan_len, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
@@ -351,12 +408,12 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && seed && workspace && r_out, "krca_ppr: null pointer");
   KRCA_CHECK_ARG(plan_len > 0 && plan_len % 2 == 0, "krca_ppr: bad plan");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0 && max_iter > 0, "krca_ppr: alpha in (0,1), max_iter > 0");
-  char* p = reinterpret_cast<char*>(workspace);
-  void* ctl = p;
-  int64_t* q = q_out ? q_out : reinterpret_cast<int64_t*>(p + 256);
-  int64_t* acc = reinterpret_cast<int64_t*>(p + 256 + N * 8);
-  int64_t* w = reinterpret_cast<int64_t*>(p + 256 + 2 * N * 8);
-  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + 256 + (3 * N + NSLOT) * 8);
+  char* ctl = reinterpret_cast<char*>(workspace);
+  char* p = ctl + krca_ppr_ctl_size();
+  int64_t* q = q_out ? q_out : reinterpret_cast<int64_t*>(p);
+  int64_t* acc = reinterpret_cast<int64_t*>(p + N * 8);
+  int64_t* w = reinterpret_cast<int64_t*>(p + 2 * N * 8);
+  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + (3 * N + NSLOT) * 8);
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(acc, 0, N * 8, st));
   int rc = krca_ppr_shard_init(seed, seed_floor, outdeg, N, N, N, alpha, ctl, q, r, w, stream);

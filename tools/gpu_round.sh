@@ -18,4 +18,8 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -- pytho
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run -- python3 tools/prof_kernels.py score --reps 2 > /dev/null 2>> $OUT/err.log || echo "pmc write failed" >> $OUT/status
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_sq -o run -- python3 tools/prof_kernels.py score --reps 2 > /dev/null 2>> $OUT/err.log || echo "pmc sq failed" >> $OUT/status
 timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d $OUT/pmc_grbm -o run -- python3 tools/prof_kernels.py score --reps 2 > /dev/null 2>> $OUT/err.log || echo "pmc grbm failed" >> $OUT/status
-echo "all done" >> $OUT/status
+echo "pmc done" >> $OUT/status
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_ppr -o run -- python3 tools/prof_kernels.py ppr --reps 3 > $OUT/trace_ppr.json 2>> $OUT/err.log || echo "ppr trace failed" >> $OUT/status
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_logs -o run -- python3 tools/prof_kernels.py logs --reps 3 > $OUT/trace_logs.json 2>> $OUT/err.log || echo "logs trace failed" >> $OUT/status
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || echo "bench failed" >> $OUT/status
+echo "extra done" >> $OUT/status
