@@ -79,7 +79,23 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
                    const int64_t* workspace, int64_t n_lines,
                    int64_t* line_start /*[L]*/, int64_t* line_end /*[L]*/, uint32_t* line_mask /*[L]*/,
                    int32_t* doc_lines /*[D]*/, int32_t* hist /*[D][13]*/, int32_t* examples /*[D][13][3]*/,
-                   void* stream);
+                   int64_t* doc_line0 /*[D], nullable: first line id of each container*/, void* stream);
+
+/* ---- a13: error-template hashing + per-container template histograms (new primitive) ------
+ * template(line) = line bytes with every maximal [A-Za-z0-9_] run that contains an ASCII digit or
+ * is >= 8 hex digits long replaced by "<*>"; hash = FNV-1a-64(template) (csrc/template.hip).
+ * krca_template_hash: hash[l] for every line of krca_log_match.
+ * krca_template_hist: per container d, the distinct hashes of its lines in ascending order and
+ *   their counts, written to out_hash/out_count at the container's own line range
+ *   [doc_line0[d], doc_line0[d] + n_templates[d]); sort-based and atomics-free.  Containers with
+ *   more than 64 lines are listed (host) in big_docs_host (staged through big_docs_dev); at most
+ *   krca_template_max_lines() lines per container (KRCA_EINVAL beyond). */
+int krca_template_hash(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int64_t* line_end,
+                       int64_t n_lines, uint64_t* hash, void* stream);
+int krca_template_hist(const uint64_t* hash, const int32_t* doc_lines, const int64_t* doc_line0, int64_t ndocs,
+                       const int32_t* big_docs_host, int32_t n_big, int32_t* big_docs_dev, uint64_t* out_hash,
+                       int32_t* out_count, int32_t* n_templates, void* stream);
+int32_t krca_template_max_lines(void);
 
 /* ---- a10: personalized PageRank root-cause propagation (replaces the sink of
  * Coordinator._identify_root_causes, ref:agents/coordinator.py:157-184; networkx 3.4.2

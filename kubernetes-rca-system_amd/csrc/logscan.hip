@@ -414,7 +414,7 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
                                                 const int64_t* __restrict__ line_start,
                                                 const uint32_t* __restrict__ line_mask, int64_t L,
                                                 int32_t* __restrict__ doc_lines, int32_t* __restrict__ hist,
-                                                int32_t* __restrict__ examples) {
+                                                int32_t* __restrict__ examples, int64_t* __restrict__ doc_line0) {
   const int64_t d = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (d >= D) return;
@@ -444,6 +444,7 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
   }
   if (lane == 0) {
     doc_lines[d] = (int32_t)(hi - lo);
+    if (doc_line0) doc_line0[d] = lo;
 #pragma unroll
     for (int c = 0; c < KRCA_NCAT; ++c) {
       hist[d * KRCA_NCAT + c] = cnt[c];
@@ -483,7 +484,7 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
 
 int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, const int64_t* ws,
                    int64_t n_lines, int64_t* line_start, int64_t* line_end, uint32_t* line_mask, int32_t* doc_lines,
-                   int32_t* hist, int32_t* examples, void* stream) {
+                   int32_t* hist, int32_t* examples, int64_t* doc_line0, void* stream) {
   KRCA_CHECK_ARG(nbytes >= 0 && ndocs >= 1 && n_lines >= 0, "krca_log_match: bad sizes");
   KRCA_CHECK_ARG(doc_off && ws && doc_lines && hist && examples, "krca_log_match: null pointer");
   KRCA_CHECK_ARG(((uintptr_t)text & 15) == 0, "krca_log_match: text must be 16-byte aligned");
@@ -500,7 +501,7 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB / 64)), dim3(TPB), 0, st, doc_off, ndocs,
-                     line_start, line_mask, n_lines, doc_lines, hist, examples);
+                     line_start, line_mask, n_lines, doc_lines, hist, examples, doc_line0);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

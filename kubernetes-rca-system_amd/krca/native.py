@@ -27,7 +27,11 @@ SIGNATURES = {
     "krca_rolling_score": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_log_index_size": (c_i64, [c_i64]),
     "krca_log_index": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
-    "krca_log_match": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_log_match": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_vp]),
+    "krca_template_hash": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "krca_template_hist": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_template_max_lines": (c_i32, []),
     "krca_ppr_plan_size": (c_i64, [c_vp, c_i64]),
     "krca_ppr_plan": (c_i32, [c_vp, c_i64, c_vp, c_i64]),
     "krca_ppr_workspace_size": (c_i64, [c_i64]),
@@ -215,13 +219,50 @@ class NativeEngine:
         le = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
         lm = torch.empty(max(L, 1), dtype=torch.int32, device=self.device)
         dl = torch.empty(D, dtype=torch.int32, device=self.device)
+        d0 = torch.empty(D, dtype=torch.int64, device=self.device)
         hist = torch.empty((D, NCAT), dtype=torch.int32, device=self.device)
         ex = torch.empty((D, NCAT, 3), dtype=torch.int32, device=self.device)
         _check(self.lib.krca_log_match(self.ptr(text), nbytes, self.ptr(doc_off), D, self.ptr(ws), L,
                                        self.ptr(ls), self.ptr(le), self.ptr(lm), self.ptr(dl), self.ptr(hist),
-                                       self.ptr(ex), self._stream()), "krca_log_match")
+                                       self.ptr(ex), self.ptr(d0), self._stream()), "krca_log_match")
         return dict(n_lines_total=L, line_start=ls[:L], line_end=le[:L], line_mask=lm[:L], doc_lines=dl,
-                    hist=hist, examples=ex)
+                    doc_line0=d0, hist=hist, examples=ex, text=text)
+
+    # -- a13 ---------------------------------------------------------------------------------
+    def template_hist_device(self, scan):
+        """Template hashes of every line and per-container template histograms (device)."""
+        torch = self.torch
+        L = scan["n_lines_total"]
+        D = scan["doc_lines"].numel()
+        h = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
+        oh = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
+        oc = torch.empty(max(L, 1), dtype=torch.int32, device=self.device)
+        nt = torch.zeros(D, dtype=torch.int32, device=self.device)
+        _check(self.lib.krca_template_hash(self.ptr(scan["text"]), scan["text"].numel(), self.ptr(scan["line_start"]),
+                                           self.ptr(scan["line_end"]), L, self.ptr(h), self._stream()),
+               "krca_template_hash")
+        dl = scan["doc_lines"].cpu().numpy()
+        cap = self.lib.krca_template_max_lines()
+        if len(dl) and dl.max() > cap:
+            raise KrcaError(f"template histogram: a container has {int(dl.max())} lines (max {cap})")
+        big = np.nonzero(dl > 64)[0].astype(np.int32)
+        bigd = torch.empty(max(len(big), 1), dtype=torch.int32, device=self.device)
+        _check(self.lib.krca_template_hist(self.ptr(h), self.ptr(scan["doc_lines"]), self.ptr(scan["doc_line0"]), D,
+                                           big.ctypes.data_as(c_vp), len(big), self.ptr(bigd), self.ptr(oh),
+                                           self.ptr(oc), self.ptr(nt), self._stream()), "krca_template_hist")
+        torch.cuda.current_stream(self.device).synchronize()  # big-doc list lives on the host
+        return dict(hash=h[:L], tmpl_hash=oh[:L], tmpl_count=oc[:L], n_templates=nt)
+
+    def template_hist(self, blob, doc_off):
+        """-> list (per container) of [(hash uint64, count)] in ascending hash order."""
+        doc_off = np.asarray(doc_off, dtype=np.int64)
+        scan = self.log_scan_device(self.upload_blob(blob), self._dev(doc_off))
+        r = self.template_hist_device(scan)
+        d0 = scan["doc_line0"].cpu().numpy()
+        nt = r["n_templates"].cpu().numpy()
+        th = r["tmpl_hash"].cpu().numpy().view(np.uint64)
+        tc = r["tmpl_count"].cpu().numpy()
+        return [list(zip(th[d0[d]:d0[d] + nt[d]].tolist(), tc[d0[d]:d0[d] + nt[d]].tolist())) for d in range(len(nt))]
 
     def upload_blob(self, blob):
         torch = self.torch

@@ -68,6 +68,36 @@ def log_hist(text):
 
 
 # ------------------------------------------------------------------------------------------
+# error templates (a13): new primitive, semantics of csrc/template.hip restated
+# ------------------------------------------------------------------------------------------
+_WORD = re.compile(rb"[A-Za-z0-9_]+")
+_HEX = re.compile(rb"[0-9a-fA-F]{8,}")
+
+
+def template_of(line_bytes):
+    def sub(m):
+        w = m.group(0)
+        if any(48 <= c <= 57 for c in w) or _HEX.fullmatch(w):
+            return b"<*>"
+        return w
+    return _WORD.sub(sub, line_bytes)
+
+
+def fnv1a64(b):
+    h = 0xcbf29ce484222325
+    for c in b:
+        h = ((h ^ c) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def template_hist(text):
+    """-> [(hash, count)] ascending for one container's log text (lines as str.splitlines)."""
+    from collections import Counter
+    cnt = Counter(fnv1a64(template_of(ln.encode("utf-8", "surrogatepass"))) for ln in text.splitlines())
+    return sorted(cnt.items())
+
+
+# ------------------------------------------------------------------------------------------
 # rolling z-score (a5), float64 independent formulation (prefix sums)
 # ------------------------------------------------------------------------------------------
 def rolling_score_f64(x, W, z_thr=3.0):

@@ -202,3 +202,25 @@ def test_rca_step_single_gpu_vs_oracle(eng, n, iters):
     idx2, _ = step.run()  # re-run on the same buffers: identical
     assert list(idx2) == list(idx)
     assert len(set(idx.tolist()) & set(m.roots.tolist())) >= 8
+
+
+# ---- a13 error templates -------------------------------------------------------------------
+def test_template_hist_vs_oracle(eng):
+    import json
+    import os
+    from conftest import GOLDEN
+    g = json.load(open(os.path.join(GOLDEN, "logs_corpus.json")))
+    docs = [c["text"] for c in g["containers"]]  # up to 300 lines: wave and workgroup paths
+    docs += synth.make_log_corpus(5000, lines_per_doc=4, seed=11, hazard_rate=0.02)
+    docs += ["", "\n", "id=deadbeefcafe x", "user_42 7f9c4 0xFF", "a" * 5000 + " 123", "été 42 café"]
+    docs.append("\n".join("req %d from 10.0.%d.%d took %dms" % (i, i % 7, i % 250, i) for i in range(3000)))
+    got = eng.template_hist(*pack_documents(docs))
+    for d, text in enumerate(docs):
+        assert got[d] == oracle.template_hist(text), d
+
+
+def test_template_hash_examples(eng):
+    assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/<*>/items <*> <*>"
+    assert oracle.template_of(b"uuid 550e8400-e29b-41d4-a716-446655440000 deadbeef") == \
+        b"uuid <*>-<*>-<*>-<*>-<*> <*>"
+    assert oracle.template_of(b"user_42 caf\xc3\xa9 OK") == b"<*> caf\xc3\xa9 OK"

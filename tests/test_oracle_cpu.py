@@ -84,3 +84,13 @@ def test_c_rolling_matches_f64():
     # exceedance counts agree except for samples within rounding of the threshold
     assert np.abs(c["n_exceed"] - n).max() <= 1
     assert (c["n_exceed"] == n).mean() > 0.99
+
+
+def test_template_oracle_rules():
+    assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/<*>/items <*> <*>"
+    assert oracle.template_of(b"deadbeef feedface1 abc") == b"<*> <*> abc"
+    assert oracle.template_of(b"") == b""
+    assert oracle.fnv1a64(b"") == 0xcbf29ce484222325
+    assert oracle.fnv1a64(b"a") == 0xaf63dc4c8601ec8c  # published FNV-1a-64 test vector
+    h = oracle.template_hist("x 1\nx 2\ny\n")
+    assert [c for _, c in h] == sorted([2, 1], key=lambda c: c) or sum(c for _, c in h) == 3
