@@ -67,33 +67,30 @@ __device__ __forceinline__ void add_slot(int64_t* slot, int64_t v) {
   atomicAdd(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)v);
 }
 
-// Two block sums (a, b) reduced over the grid without contended atomics (MI355X_MICROARCH
-// "fanin"): every block stores its pair, then arrives on ONE ticket (release -> relaxed agent
-// add, cdna_hip_programming.md §6 Guideline 16 counter form); the last arriver acquires, sums
-// the pairs in a fixed order (integers: order-free anyway) and stores them to out[0..1].
+// Two block sums (a, b) reduced over the grid without contended atomics and without an L2
+// write-back per block: lane 0 stores the block's pair write-through (relaxed agent-scope atomic
+// store = global_store ... sc1, straight to memory), drains it (vmcnt(0)) and arrives on ONE
+// ticket; the last arriver reads every pair with agent-scope atomic loads (sc1: bypass the
+// non-coherent L1/L2 copies) and stores the totals (cdna_hip_programming.md split-K recipe,
+// write-through form; integer sums are order-free anyway).
 __device__ void grid_sum2(int64_t a, int64_t b, Ctl* ctl, int64_t* out, int64_t* red) {
   __shared__ int is_last;
   a = block_sum_i64(a, red);
   b = block_sum_i64(b, red);
   int64_t* part = partials(ctl);
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = a;
-    part[2 * blockIdx.x + 1] = b;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&part[2 * blockIdx.x], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&part[2 * blockIdx.x + 1], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (t == gridDim.x - 1);
   }
   __syncthreads();
   if (!is_last) return;
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   int64_t sa = 0, sb = 0;
   for (int i = threadIdx.x; i < (int)gridDim.x; i += TPB) {
-    sa += part[2 * i];
-    sb += part[2 * i + 1];
+    sa += __hip_atomic_load(&part[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sb += __hip_atomic_load(&part[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   sa = block_sum_i64(sa, red);
   sb = block_sum_i64(sb, red);

@@ -113,8 +113,13 @@ def caller_hops(mesh, roots, hops=3, cap=2000):
 
 
 def make_metrics(n_pods, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(), hop_sets=(), device="cpu",
-                 spike_steps=1, root_sigma=12.0, hop_sigma=5.0, hop_decay=0.8, chunk_steps=None):
-    """-> torch.float32 tensor [T, P, M] (time-major) on `device`."""
+                 spike_steps=1, root_sigma=12.0, hop_sigma=5.0, hop_decay=0.8, chunk_steps=None, group_size=0,
+                 group_sigma=12.0):
+    """-> torch.float32 tensor [T, P, M] (time-major) on `device`.
+
+    group_size > 0 adds a shared load signal per block of `group_size` consecutive pods (a
+    service's replicas): a per-group random walk scaled by a per-pod loading in [0.2, 1) *
+    group_sigma, which gives the cross-pod correlation structure a9 ranks."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(int(seed))
@@ -130,7 +135,17 @@ def make_metrics(n_pods, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(),
         tt = torch.arange(t0, t1, device=device, dtype=torch.float32).view(-1, 1, 1)
         blk = b + a * torch.sin(2 * math.pi * tt / 1440.0 + phi) + sig * torch.randn(
             (t1 - t0, P, M), generator=g, device=device)
-        x[t0:t1] = blk.clamp_(0.0, 100.0)
+        x[t0:t1] = blk
+    if group_size > 0:
+        G = (P + group_size - 1) // group_size
+        walk = torch.randn((T, G), generator=g, device=device).cumsum_(0)
+        walk = (walk - walk.mean(0)) / walk.std(0).clamp_min(1e-6)
+        load = (torch.rand((P, 1), generator=g, device=device) * 0.8 + 0.2) * group_sigma
+        gid = torch.arange(P, device=device) // group_size
+        for t0 in range(0, T, cs):
+            t1 = min(T, t0 + cs)
+            x[t0:t1] += walk[t0:t1][:, gid].unsqueeze(2) * load.view(1, P, 1)
+    x.clamp_(0.0, 100.0)
     w0 = max(0, T - spike_steps)
     if len(roots):
         r = torch.as_tensor(np.asarray(roots), device=device)

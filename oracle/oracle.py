@@ -153,6 +153,41 @@ def topk_ref(v, k):
     return idx.astype(np.int32), v[idx]
 
 
+def corr_standardize(x, channel=0):
+    """x [T, P, M] -> z [P, T] float64 with z·zᵀ = Pearson r (population std; flat -> 0).
+    New primitive a9: no reference counterpart, semantics defined here."""
+    s = np.asarray(x[:, :, channel], dtype=np.float64).T
+    T = s.shape[1]
+    mu = s.mean(axis=1, keepdims=True)
+    d = s - mu
+    var = (d * d).mean(axis=1, keepdims=True)
+    sc = np.where(var > 1e-20, 1.0 / np.sqrt(np.maximum(var, 1e-300) * T), 0.0)
+    return d * sc
+
+
+def corr_rows(z, rows, k, tau):
+    """For pods `rows`: (idx [n,k], r [n,k], count [n], gap [n]) by |r| desc, index asc, self
+    excluded; gap = |r|_(k) - |r|_(k+1) (how far the k-th is from being tied)."""
+    rows = np.asarray(rows)
+    P = z.shape[0]
+    R = z[rows] @ z.T
+    R[np.arange(len(rows)), rows] = np.nan
+    a = np.abs(R)
+    count = (a > tau).sum(axis=1)
+    a = np.where(np.isnan(a), -1.0, a)
+    idx = np.empty((len(rows), k), np.int64)
+    gap = np.empty(len(rows))
+    kk = min(k + 1, P - 1)
+    for n in range(len(rows)):
+        thr = np.partition(-a[n], kk - 1)[kk - 1]
+        part = np.nonzero(-a[n] <= thr)[0]  # every pod at least as good as the kk-th (ties kept)
+        o = part[np.lexsort((part, -a[n][part]))]
+        idx[n] = o[:k]
+        gap[n] = a[n][o[k - 1]] - (a[n][o[k]] if len(o) > k else -1.0)
+    r = np.take_along_axis(R, idx, axis=1)
+    return idx.astype(np.int32), r, count, gap
+
+
 # ------------------------------------------------------------------------------------------
 # C restatement (bit-exact twin of the device arithmetic)
 # ------------------------------------------------------------------------------------------

@@ -1,0 +1,91 @@
+"""a9 cross-pod Pearson correlation (krca_corr_prepare + krca_corr_topk) against the float64 oracle.
+
+Tolerances ("1e-5 rel on reported r"): reported r within 1e-5 relative (plus
+2e-6 absolute for |r| near 0) of float64; the top-k SET equals the oracle's wherever the oracle's
+k-th and (k+1)-th |r| are more than 2e-4 apart (closer than that, either pod is a valid k-th);
+|r| > tau counts exact except for pairs within 1e-4 of tau (the count is taken on the bf16x3 MFMA
+product).  Every row whose certificate is positive must match exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from krca import native, synth
+
+pytestmark = pytest.mark.gpu
+TAU = 0.5
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return native.NativeEngine()
+
+
+def check_rows(res, z, rows, k, tau=TAU):
+    oi, orr, oc, gap = oracle.corr_rows(z, rows, k, tau)
+    gi, gv, gc, cert = res["idx"][rows], res["val"][rows], res["count"][rows], res["cert"][rows]
+    # reported values: exact re-scoring of the reported partners
+    rv = np.einsum("nt,nkt->nk", z[rows], z[gi])
+    assert np.all(np.abs(gv - rv) <= 1e-5 * np.abs(rv) + 2e-6), np.max(np.abs(gv - rv))
+    clear = gap > 2e-4
+    for n in np.nonzero(clear)[0]:
+        assert set(gi[n].tolist()) == set(oi[n].tolist()), (rows[n], gi[n], oi[n], gap[n])
+    # descending |r| in the output
+    assert np.all(np.diff(np.abs(gv), axis=1) <= 1e-6)
+    # certified rows are exact
+    for n in np.nonzero(cert > 0)[0]:
+        assert set(gi[n].tolist()) == set(oi[n].tolist())
+    Rn = z[rows] @ z.T
+    Rn[np.arange(len(rows)), rows] = 0
+    a = np.abs(Rn)
+    lo, hi = (a > tau + 1e-4).sum(1), (a > tau - 1e-4).sum(1)
+    assert np.all((gc >= lo) & (gc <= hi))
+    return clear.mean(), (cert > 0).mean()
+
+
+@pytest.mark.parametrize("P,T,group,k", [(6000, 1440, 20, 10), (130, 200, 7, 16), (257, 64, 0, 5), (2, 30, 0, 1),
+                                         (1000, 100, 50, 10)])
+def test_corr_full_vs_oracle(eng, P, T, group, k):
+    x = synth.make_metrics(P, 2, T, seed=P + T, group_size=group)
+    x[:, 3 % P, 0] = 42.0  # a flat series: r = 0 with everything
+    if P > 20:
+        x[:, 17, 0] = x[:, 5, 0]  # duplicate pods: r = 1, tie broken by index
+        x[:, 18, 0] = x[:, 5, 0]
+    res = eng.corr_topk(x, k=k, tau=TAU, channel=0)
+    z = oracle.corr_standardize(x.numpy(), 0)
+    clear, certified = check_rows(res, z, np.arange(P), k)
+    if group:
+        assert certified > 0.5, certified
+    if P > 20:
+        assert res["idx"][5][:2].tolist() == [17, 18] and abs(res["val"][5][0] - 1) < 1e-6
+        assert res["idx"][17][:2].tolist() == [5, 18]
+
+
+def test_corr_channel_and_determinism(eng):
+    x = synth.make_metrics(777, 3, 300, seed=9, group_size=10).cuda()
+    a = eng.corr_topk(x, k=8, tau=0.3, channel=2)
+    b = eng.corr_topk(x, k=8, tau=0.3, channel=2)
+    for key in a:
+        assert np.array_equal(a[key], b[key])
+    z = oracle.corr_standardize(x.cpu().numpy(), 2)
+    check_rows(a, z, np.arange(777), 8, 0.3)
+
+
+def test_corr_100k_sampled_rows(eng):
+    P, T = 100_000, 1440
+    x = synth.make_metrics(P, 1, T, seed=1, group_size=20, device="cuda")
+    res = eng.corr_topk(x, k=10, tau=TAU)
+    z = oracle.corr_standardize(x.cpu().numpy(), 0)
+    rows = np.random.default_rng(0).choice(P, 256, replace=False)
+    rows = np.concatenate([rows, [0, P - 1, 127, 128, 99_968]])
+    clear, certified = check_rows(res, z, rows, 10)
+    assert certified > 0.5, certified
+
+
+def test_corr_rejects_bad_k(eng):
+    x = torch.rand(50, 10, 1)
+    with pytest.raises(native.KrcaError):
+        eng.corr_topk(x, k=17)
+    with pytest.raises(native.KrcaError):
+        eng.corr_topk(x, k=10)  # k must be < P

@@ -92,5 +92,25 @@ def test_template_oracle_rules():
     assert oracle.template_of(b"") == b""
     assert oracle.fnv1a64(b"") == 0xcbf29ce484222325
     assert oracle.fnv1a64(b"a") == 0xaf63dc4c8601ec8c  # published FNV-1a-64 test vector
-    h = oracle.template_hist("x 1\nx 2\ny\n")
-    assert [c for _, c in h] == sorted([2, 1], key=lambda c: c) or sum(c for _, c in h) == 3
+    h = dict(oracle.template_hist("x 1\nx 2\ny\n"))
+    assert h == {oracle.fnv1a64(b"x <*>"): 2, oracle.fnv1a64(b"y"): 1}
+
+
+def test_corr_oracle_matches_brute_force():
+    from krca import synth
+    x = synth.make_metrics(300, 2, 200, seed=4, group_size=10)
+    x[:, 7, 1] = 3.0
+    z = oracle.corr_standardize(x.numpy(), 1)
+    assert np.all(z[7] == 0)
+    s = x.numpy()[:, :, 1].astype(np.float64).T
+    ref = np.corrcoef(s[np.arange(300) != 7])
+    keep = np.arange(300) != 7
+    R = z @ z.T
+    assert np.allclose(R[np.ix_(keep, keep)], ref, atol=1e-12)
+    idx, r, cnt, gap = oracle.corr_rows(z, np.arange(300), 10, 0.5)
+    np.fill_diagonal(R, -2)
+    a = np.where(R == -2, -1, np.abs(R))
+    for p in range(300):
+        o = np.lexsort((np.arange(300), -a[p]))
+        assert idx[p].tolist() == o[:10].tolist()
+        assert cnt[p] == (a[p] > 0.5).sum()

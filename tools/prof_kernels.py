@@ -4,6 +4,7 @@
   python tools/prof_kernels.py score  [--pods 1000000] [--reps 3]
   python tools/prof_kernels.py ppr    [--pods 1000000] [--reps 3]
   python tools/prof_kernels.py logs   [--docs 1000000] [--reps 3]
+  python tools/prof_kernels.py corr   [--pods 100000] [--reps 3]
 Prints per-kernel event-timed averages and the algorithmic bytes.
 """
 import argparse
@@ -28,7 +29,7 @@ def timed(torch, fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["score", "ppr", "logs"])
+    ap.add_argument("what", choices=["score", "ppr", "logs", "corr"])
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--docs", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=3)
@@ -57,6 +58,16 @@ def main():
         N, E = a.pods, m.n_edges
         per_iter = 8 * (N + 1) + 4 * E + 8 * N + 8 * N + 8 * N  # row_ptr, col, w(compulsory), acc, w out
         out = dict(kernel="ppr step (30 it)", ms=ms, edges=E, bytes_per_iter=per_iter)
+    elif a.what == "corr":
+        x = synth.make_metrics(a.pods, 1, a.tsteps, device="cuda", group_size=20)
+        z = eng.corr_prepare_device(x)
+        r = eng.corr_topk_device(z, 10, 0.5)
+        ms_prep = timed(torch, lambda: eng.corr_prepare_device(x), a.reps)
+        ms = timed(torch, lambda: eng.corr_topk_device(z, 10, 0.5, out=r), a.reps)
+        P, T = a.pods, a.tsteps
+        flops = P * (P + 1) * T  # upper triangle incl. diagonal, 2 flops per MAC
+        out = dict(kernel="corr top-k", ms=ms, ms_prepare=ms_prep, flops=flops,
+                   tflops=flops / (min(ms) * 1e-3) / 1e12, certified=float((r["cert"] > 0).float().mean()))
     else:
         from krca.agents.logs import pack_documents
         docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
