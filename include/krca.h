@@ -102,20 +102,20 @@ int32_t krca_template_max_lines(void);
  * r(p,q) = Pearson over the T samples of metric channel `channel` of x[T][P][M] (population
  * std; a flat series correlates 0 with everything).  Per pod p: the k partners with the largest
  * |r| (self excluded, ties -> lower index) with r re-scored exactly (float64 over fp32 z), the
- * count of partners with |r| > tau (from the bf16x3 MFMA product, i.e. ~1e-6 from exact), and
- * cert[p] > 0 iff the reported set is provably the exact top-k (csrc/corr.hip).
- * Buffers: mean/scale [P]; z32 [P*T]; zhi/zlo [krca_corr_pad_rows(P) * krca_corr_pad_steps(T)]
- * (uint16 bf16 bits); cand_v/cand_i [krca_corr_cand_size(P)]; count [P]; out_idx/out_val [P*k];
- * cert [P].  k <= krca_corr_max_k(). */
+ * count of partners with |r| > tau taken on the fp16 MFMA screening product (within
+ * krca_corr_eps(T) of exact), and cert[p] > 0 iff the reported set is provably the exact top-k
+ * (csrc/corr.hip).  Buffers: mean/scale [P]; z32 [P*T]; zh [krca_corr_pad_rows(P) *
+ * krca_corr_pad_steps(T)] (fp16 bits); cand [krca_corr_cand_size(P, k) 4-byte words]; count [P];
+ * out_idx/out_val [P*k]; cert [P].  k <= krca_corr_max_k(). */
 int64_t krca_corr_pad_rows(int64_t P);
 int32_t krca_corr_pad_steps(int32_t T);
-int64_t krca_corr_cand_size(int64_t P);
+int64_t krca_corr_cand_size(int64_t P, int32_t k);
 int32_t krca_corr_max_k(void);
+float krca_corr_eps(int32_t T);
 int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t channel, float* mean, float* scale,
-                      float* z32, uint16_t* zhi, uint16_t* zlo, void* stream);
-int krca_corr_topk(const uint16_t* zhi, const uint16_t* zlo, const float* z32, int64_t P, int32_t T, int32_t k,
-                   float tau, float* cand_v, int32_t* cand_i, int32_t* count, int32_t* out_idx, float* out_val,
-                   float* cert, void* stream);
+                      float* z32, uint16_t* zh, void* stream);
+int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, void* cand,
+                   int32_t* count, int32_t* out_idx, float* out_val, float* cert, void* stream);
 
 /* ---- a10: personalized PageRank root-cause propagation (replaces the sink of
  * Coordinator._identify_root_causes, ref:agents/coordinator.py:157-184; networkx 3.4.2

@@ -7,38 +7,47 @@
 //
 //   krca_corr_prepare  time-major x[T][P][M] -> per-pod mean/scale (one float64 pass, shifted
 //                      sums), then an LDS-tiled transpose to pod-major rows: z32[P][T] (fp32,
-//                      used for the exact re-scoring) and the bf16 split z = hi + lo
-//                      (zhi/zlo[Pp][Tp], zero padded to 128 rows / 64 steps).
-//   krca_corr_tiles    MFMA (v_mfma_f32_32x32x16_bf16) over the UPPER triangle of 128x128
-//                      tiles only (P(P+1)/2 pairs, the algorithmic flop count): three bf16
-//                      products hi·hi + hi·lo + lo·hi per tile, fp32 accumulation (~fp32
-//                      accuracy at the bf16 rate).  Epilogue in LDS: each lane scans one row
-//                      (-> candidates of that row from this column block) or one column (-> the
-//                      symmetric candidates of that column's pod from this row block), keeping
-//                      the KC best (|r| desc, index asc); |r| > tau counts go out as int32 adds.
-//   krca_corr_merge    one workgroup per pod: best 16 of its nb*KC candidates, re-scored in
+//                      used for the exact re-scoring) and zh[Pp][Tp] = fp16(z) (zero padded to
+//                      128 rows / 64 steps).  |z| <= 1 (unit-norm rows), so fp16 keeps 11 bits.
+//   krca_corr_tiles    MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation) over the UPPER triangle
+//                      of 128x128 tiles only (P(P+1)/2 pairs, the algorithmic flop count), in an
+//                      XCD-aware super-tile order, LDS double-buffered with register prefetch.
+//                      Epilogue in LDS: each lane scans one row (-> candidates of that row from
+//                      this column block) or one column (-> the symmetric candidates of that
+//                      column's pod from this row block), keeping the KC best by |r|; |r| > tau
+//                      counts go out as one int32 add per row/column and tile.
+//   krca_corr_merge    one workgroup per pod: best KM of its nb*KC candidates, re-scored in
 //                      float64 from z32 (fixed-order wave reduction), final top-k; cert[p] =
 //                      (k-th re-scored |r|) - (best |r| the tiles could have dropped) - eps:
 //                      cert > 0 proves the reported set equals the exact top-k.
+//
+// Error bound of the screening product (eps, host-computed): fp16 rounding of unit-norm rows
+// moves a dot product by <= 2^-10 (+ 2^-24 sqrt(T) from subnormals), fp32 accumulation of T
+// terms of a unit-norm product by <= T 2^-24.  It bounds the ranking pool and the |r| > tau
+// counts (pairs within eps of tau may land on either side); reported r values are exact.
+#include <cmath>
+
 #include "krca_common.h"
 
 namespace {
 
 constexpr int TPB = 256;
-constexpr int BM = 128;  // tile rows == cols
-constexpr int BK = 64;   // K step (time samples)
-constexpr int KC = 12;   // candidates kept per (pod, block)
-constexpr int KM = 16;   // candidates re-scored per pod in the merge
-constexpr float kEps = 1e-4f;  // bound on |r_approx - r| used by the certificate (bf16x3, fp32 acc)
+constexpr int BM = 128;   // tile rows == cols
+constexpr int BK = 64;    // K step (time samples)
+constexpr int SUPER = 8;  // super-tile edge (tiles) of the XCD-aware order
+constexpr int KM = 24;    // candidates re-scored per pod in the merge
+constexpr int KMAX = 16;  // largest k served
+// KC = candidates kept per (pod, block): a template parameter >= k (so every member of a pod's
+// exact top-k survives its own block's cut), with headroom for the certificate: 8, 12 or 16
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct defeats SROA)
 
-__device__ __forceinline__ uint16_t bf16_rne(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+__device__ __forceinline__ uint16_t f16_bits(float f) {
+  const _Float16 h = (_Float16)f;  // round to nearest even
+  return __builtin_bit_cast(uint16_t, h);
 }
-__device__ __forceinline__ float bf16_to_f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 // ---- prepare -------------------------------------------------------------------------------
 __global__ __launch_bounds__(TPB) void corr_stats(const float* __restrict__ x, int64_t P, int M, int T, int ch,
@@ -60,11 +69,11 @@ __global__ __launch_bounds__(TPB) void corr_stats(const float* __restrict__ x, i
   scale[p] = var > 1e-20 ? (float)(1.0 / sqrt(var * (double)T)) : 0.f;
 }
 
-// 64 pods x 64 steps per block: coalesced-ish reads of the channel, LDS transpose, row writes
+// 64 pods x 64 steps per block: reads of the channel, LDS transpose, pod-major row writes
 __global__ __launch_bounds__(TPB) void corr_transpose(const float* __restrict__ x, int64_t P, int M, int T, int Tp,
                                                       int ch, const float* __restrict__ mean,
                                                       const float* __restrict__ scale, float* __restrict__ z32,
-                                                      uint16_t* __restrict__ zhi, uint16_t* __restrict__ zlo) {
+                                                      uint16_t* __restrict__ zh) {
   __shared__ float tile[64][65];
   const int64_t p0 = (int64_t)blockIdx.x * 64;
   const int t0 = blockIdx.y * 64;
@@ -84,76 +93,91 @@ __global__ __launch_bounds__(TPB) void corr_transpose(const float* __restrict__ 
     const int64_t pp = p0 + r;
     const int t = t0 + tx;
     const float z = tile[r][tx];
-    if (t < Tp) {
-      const uint16_t h = bf16_rne(z);
-      const uint16_t l = bf16_rne(z - bf16_to_f(h));
-      zhi[pp * Tp + t] = h;  // rows up to Pp (padding rows are zero: pp >= P -> z = 0)
-      zlo[pp * Tp + t] = l;
-      if (pp < P && t < T) z32[pp * T + t] = z;
-    }
+    zh[pp * Tp + t] = f16_bits(z);  // rows up to Pp (padding rows / steps are zero)
+    if (pp < P && t < T) z32[pp * T + t] = z;
   }
 }
 
 // ---- tiles -----------------------------------------------------------------------------------
+// Sorted candidate list of one row (or column) of a tile.  The scan visits partners in
+// ascending index order, so a later partner with an equal |r| never displaces an earlier one:
+// "better" is a strict |r| comparison and the index tie rule holds by construction.
+template <int KC>
 struct Cand {
   float v[KC];  // signed r
   int32_t i[KC];
+  float thr;    // |v[KC-1]| (-1 while the list is not full)
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      v[j] = 0.f;
+      i[j] = -1;
+    }
+    thr = -1.f;
+  }
+  __device__ __forceinline__ void insert(float nv, int32_t ni) {
+    const float a = fabsf(nv);
+#pragma unroll
+    for (int j = KC - 1; j > 0; --j) {
+      const bool up = a > fabsf(v[j - 1]) || i[j - 1] < 0;  // shift v[j-1] down
+      const bool here = a > fabsf(v[j]) || i[j] < 0;
+      const float pv = v[j - 1];
+      const int32_t pi = i[j - 1];
+      v[j] = up ? pv : (here ? nv : v[j]);
+      i[j] = up ? pi : (here ? ni : i[j]);
+    }
+    if (a > fabsf(v[0]) || i[0] < 0) {
+      v[0] = nv;
+      i[0] = ni;
+    }
+    thr = i[KC - 1] < 0 ? -1.f : fabsf(v[KC - 1]);
+  }
 };
 
-__device__ __forceinline__ bool cbetter(float a, int32_t ia, float b, int32_t ib) {
-  const float fa = fabsf(a), fb = fabsf(b);
-  return fa > fb || (fa == fb && (uint32_t)ia < (uint32_t)ib);
-}
-
-__device__ __forceinline__ void cinit(Cand& c) {
-#pragma unroll
-  for (int j = 0; j < KC; ++j) {
-    c.v[j] = 0.f;
-    c.i[j] = -1;
-  }
-}
-
-__device__ __forceinline__ void cinsert(Cand& c, float nv, int32_t ni) {
-  if (!cbetter(nv, ni, c.v[KC - 1], c.i[KC - 1])) return;
-#pragma unroll
-  for (int j = KC - 1; j > 0; --j) {
-    const bool up = cbetter(nv, ni, c.v[j - 1], c.i[j - 1]);
-    const bool here = cbetter(nv, ni, c.v[j], c.i[j]);
-    const float pv = c.v[j - 1];
-    const int32_t pi = c.i[j - 1];
-    c.v[j] = up ? pv : (here ? nv : c.v[j]);
-    c.i[j] = up ? pi : (here ? ni : c.i[j]);
-  }
-  if (cbetter(nv, ni, c.v[0], c.i[0])) {
-    c.v[0] = nv;
-    c.i[0] = ni;
-  }
-}
-
-constexpr int LDS_STAGE = 4 * BM * BK * 2;        // A_hi, A_lo, B_hi, B_lo (bf16)
-constexpr int LDS_EPI = BM * (BM + 1) * 4;        // fp32 tile, padded rows
+constexpr int STAGE_BYTES = 2 * BM * BK * 2;           // A and B, fp16
+constexpr int LDS_STAGE = 2 * STAGE_BYTES;             // double buffered
+constexpr int LDS_EPI = BM * (BM + 1) * 4;             // fp32 tile, padded rows
 constexpr int LDS_BYTES = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
 
-// 16-byte chunk c (0..7) of row r of a [128][64] bf16 tile, XOR-swizzled against bank conflicts
+// 16-byte chunk c (0..7) of row r of a [128][64] fp16 tile, XOR-swizzled against bank conflicts
 __device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
-__global__ __launch_bounds__(TPB) void corr_tiles(const uint16_t* __restrict__ zhi, const uint16_t* __restrict__ zlo,
-                                                  int64_t P, int Tp, int nb, float tau, float* __restrict__ cand_v,
-                                                  int32_t* __restrict__ cand_i, int32_t* __restrict__ count) {
+// SAMPLE = false: the upper triangle (all pairs), lists filtered by phi, heads + counts out.
+// SAMPLE = true: rows x the first nsb column blocks (the threshold sample), row lists only.
+template <int KC, bool SAMPLE>
+__global__ __launch_bounds__(TPB) void corr_tiles(const uint16_t* __restrict__ zh, int64_t P, int Tp, int nb,
+                                                  int64_t per_xcd, int nsb, float tau,
+                                                  const float* __restrict__ phi, float* __restrict__ cand_v,
+                                                  int32_t* __restrict__ cand_i, float* __restrict__ cand_hd,
+                                                  int32_t* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // triangular tile index -> (I, J), I <= J
+  int64_t I, J;
+  if (SAMPLE) {
+    I = blockIdx.x / nsb;
+    J = blockIdx.x % nsb;
+  } else {
+  // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs, so slot
+  // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the upper
+  // triangle in SUPER x SUPER super-tiles, so the ~64 tiles an XCD has in flight share 2*SUPER
+  // row blocks through its L2.  Slots below the diagonal or past nb exit at once.
   const int64_t b = blockIdx.x;
-  int64_t J = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
-  while ((J + 1) * (J + 2) / 2 <= b) ++J;
-  while (J * (J + 1) / 2 > b) --J;
-  const int64_t I = b - J * (J + 1) / 2;
+  const int64_t L = (b & 7) * per_xcd + (b >> 3);
+  const int64_t ns = (nb + SUPER - 1) / SUPER;
+  const int64_t st = L / (SUPER * SUPER);
+  if (st >= ns * (ns + 1) / 2) return;
+  int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
+  while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
+  while (SJ * (SJ + 1) / 2 > st) --SJ;
+  const int64_t SI = st - SJ * (SJ + 1) / 2;
+  const int64_t in = L % (SUPER * SUPER);
+  I = SI * SUPER + in / SUPER;
+  J = SJ * SUPER + in % SUPER;
+  if (I > J || J >= nb) return;
+  }
+
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
   const int64_t rowA = I * BM, rowB = J * BM;
-  char* sAh = smem;
-  char* sAl = smem + BM * BK * 2;
-  char* sBh = smem + 2 * BM * BK * 2;
-  char* sBl = smem + 3 * BM * BK * 2;
 
   floatx16 acc[2][2];
 #pragma unroll
@@ -163,50 +187,58 @@ __global__ __launch_bounds__(TPB) void corr_tiles(const uint16_t* __restrict__ z
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+  // register prefetch of one K step: A and B, 128 rows x 8 chunks each = 4 + 4 chunks per lane
+  u32x4 pa[4], pb[4];
+  const uint16_t* gA = zh + rowA * Tp;
+  const uint16_t* gB = zh + rowB * Tp;
+#define CORR_FETCH(K0)                                                    \
+  _Pragma("unroll") for (int q = 0; q < 4; ++q) {                         \
+    const int id = tid + q * TPB; /* row id>>3, 16-byte chunk id&7 */     \
+    const int64_t o = (int64_t)(id >> 3) * Tp + (K0) + (id & 7) * 8;      \
+    pa[q] = *reinterpret_cast<const u32x4*>(gA + o);                      \
+    pb[q] = *reinterpret_cast<const u32x4*>(gB + o);                      \
+  }
+#define CORR_STORE(BUF)                                                   \
+  _Pragma("unroll") for (int q = 0; q < 4; ++q) {                         \
+    const int id = tid + q * TPB;                                         \
+    const int o = chunk_off(id >> 3, id & 7);                             \
+    *reinterpret_cast<u32x4*>(smem + (BUF) * STAGE_BYTES + o) = pa[q];    \
+    *reinterpret_cast<u32x4*>(smem + (BUF) * STAGE_BYTES + BM * BK * 2 + o) = pb[q]; \
+  }
+  CORR_FETCH(0)
+  CORR_STORE(0)
+  __syncthreads();
   const int r32 = lane & 31, h = lane >> 5;
-  for (int k0 = 0; k0 < Tp; k0 += BK) {
-    // stage: 4 operands x 128 rows x 8 chunks = 4096 16-byte chunks, 16 per lane
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int id = tid + q * TPB;  // 0..1023
-      const int r = id >> 3, c = id & 7;
-      const int64_t ga = (rowA + r) * Tp + k0 + c * 8;
-      const int64_t gb = (rowB + r) * Tp + k0 + c * 8;
-      const uint4 ah = *reinterpret_cast<const uint4*>(zhi + ga);
-      const uint4 al = *reinterpret_cast<const uint4*>(zlo + ga);
-      const uint4 bh = *reinterpret_cast<const uint4*>(zhi + gb);
-      const uint4 bl = *reinterpret_cast<const uint4*>(zlo + gb);
-      const int o = chunk_off(r, c);
-      *reinterpret_cast<uint4*>(sAh + o) = ah;
-      *reinterpret_cast<uint4*>(sAl + o) = al;
-      *reinterpret_cast<uint4*>(sBh + o) = bh;
-      *reinterpret_cast<uint4*>(sBl + o) = bl;
+  const int nk = Tp / BK;
+  for (int s = 0; s < nk; ++s) {
+    const bool more = s + 1 < nk;
+    if (more) {
+      CORR_FETCH((s + 1) * BK)
     }
-    __syncthreads();
+    const char* sA = smem + (s & 1) * STAGE_BYTES;
+    const char* sB = sA + BM * BK * 2;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       const int c = ks * 2 + h;
-      bf16x8 ah[2], al[2], bh[2], bl[2];
+      halfx8 fa[2], fb[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int ra = wr * 64 + i * 32 + r32;
-        const int rb = wc * 64 + i * 32 + r32;
-        ah[i] = *reinterpret_cast<const bf16x8*>(sAh + chunk_off(ra, c));
-        al[i] = *reinterpret_cast<const bf16x8*>(sAl + chunk_off(ra, c));
-        bh[i] = *reinterpret_cast<const bf16x8*>(sBh + chunk_off(rb, c));
-        bl[i] = *reinterpret_cast<const bf16x8*>(sBl + chunk_off(rb, c));
+        fa[i] = *reinterpret_cast<const halfx8*>(sA + chunk_off(wr * 64 + i * 32 + r32, c));
+        fb[i] = *reinterpret_cast<const halfx8*>(sB + chunk_off(wc * 64 + i * 32 + r32, c));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      CORR_STORE((s + 1) & 1)
     }
     __syncthreads();
   }
+#undef CORR_FETCH
+#undef CORR_STORE
   // epilogue: tile -> LDS [row][col] (padded), then row / column scans
   float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -220,184 +252,378 @@ __global__ __launch_bounds__(TPB) void corr_tiles(const uint16_t* __restrict__ z
         tile[row * (BM + 1) + col] = acc[i][j][e];
       }
   __syncthreads();
-  Cand cd;
-  cinit(cd);
+  Cand<KC> cd;
+  cd.init();
   int n_over = 0;
+  int64_t g = -1, blk = 0;
   if (tid < BM) {  // row scan: pod rowA+tid against the columns of block J
-    const int64_t g = rowA + tid;
+    g = rowA + tid;
+    blk = J;
     if (g < P) {
-      for (int c = 0; c < BM; ++c) {
-        const int64_t gc = rowB + c;
-        if (gc >= P || gc == g) continue;
-        const float v = tile[tid * (BM + 1) + c];
-        n_over += fabsf(v) > tau;
-        cinsert(cd, v, (int32_t)gc);
+      const float ph = SAMPLE ? -1.f : phi[g];
+      const int cend = (int)std::min<int64_t>(BM, P - rowB);
+      const float* rowp = tile + tid * (BM + 1);
+      for (int c = 0; c < cend; ++c) {
+        if (rowB + c == g) continue;
+        const float v = rowp[c];
+        const float a = fabsf(v);
+        n_over += a > tau;
+        if (a > fmaxf(cd.thr, ph)) cd.insert(v, (int32_t)(rowB + c));
       }
-      float* ov = cand_v + (g * nb + J) * KC;
-      int32_t* oi = cand_i + (g * nb + J) * KC;
-#pragma unroll
-      for (int q = 0; q < KC; ++q) {
-        ov[q] = cd.v[q];
-        oi[q] = cd.i[q];
-      }
-      if (n_over) atomicAdd(&count[g], n_over);
     }
-  } else if (I != J) {  // column scan: pod rowB+c against the rows of block I (symmetric half)
+  } else if (!SAMPLE && I != J) {  // column scan: pod rowB+c against the rows of block I
     const int c = tid - BM;
-    const int64_t g = rowB + c;
+    g = rowB + c;
+    blk = I;
     if (g < P) {
-      for (int r = 0; r < BM; ++r) {
-        const int64_t gr = rowA + r;
-        if (gr >= P) continue;
+      const float ph = phi[g];
+      const int rend = (int)std::min<int64_t>(BM, P - rowA);
+      for (int r = 0; r < rend; ++r) {
         const float v = tile[r * (BM + 1) + c];
-        n_over += fabsf(v) > tau;
-        cinsert(cd, v, (int32_t)gr);
+        const float a = fabsf(v);
+        n_over += a > tau;
+        if (a > fmaxf(cd.thr, ph)) cd.insert(v, (int32_t)(rowA + r));
       }
-      float* ov = cand_v + (g * nb + I) * KC;
-      int32_t* oi = cand_i + (g * nb + I) * KC;
+    }
+  }
+  if (g >= 0 && g < P) {
+    const int64_t slot = SAMPLE ? g * nsb + blk : g * nb + blk;
+    if (SAMPLE || cd.i[0] >= 0) {  // empty main-pass lists are never read (head = -1)
+      float* ov = cand_v + slot * KC;
+      int32_t* oi = cand_i + slot * KC;
 #pragma unroll
       for (int q = 0; q < KC; ++q) {
         ov[q] = cd.v[q];
         oi[q] = cd.i[q];
       }
+    }
+    if (!SAMPLE) {
+      // list head (best |r|, -1 if empty) and floor (KC-th |r| if the list is full, else -1)
+      cand_hd[slot * 2] = cd.i[0] < 0 ? -1.f : fabsf(cd.v[0]);
+      cand_hd[slot * 2 + 1] = cd.thr;
       if (n_over) atomicAdd(&count[g], n_over);
     }
   }
+}
+
+// phi[g] = (k-th best |r| of g among the sampled partners) - 2 eps (-1 if fewer than k): every
+// member of g's exact top-k has a screening |r| above it (exact k-th >= sampled k-th - eps).
+template <int KC>
+__global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, const int32_t* __restrict__ si,
+                                                  int64_t P, int nsb, int k, float eps, float* __restrict__ phi) {
+  const int64_t g = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= P) return;
+  const int n = nsb * KC;  // <= 256
+  float a[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = lane + 64 * u;
+    a[u] = (q < n && si[g * n + q] >= 0) ? fabsf(sv[g * n + q]) : -1.f;
+  }
+  float kth = -1.f;
+  for (int r = 0; r < k; ++r) {
+    float m = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    kth = m;
+    if (m < 0.f) break;
+    // remove one instance of m: the lowest lane holding it, its first slot
+    const bool has = a[0] == m || a[1] == m || a[2] == m || a[3] == m;
+    const uint64_t bal = __ballot(has);
+    if (lane == __ffsll((unsigned long long)bal) - 1) {
+      if (a[0] == m) a[0] = -1.f;
+      else if (a[1] == m) a[1] = -1.f;
+      else if (a[2] == m) a[2] = -1.f;
+      else a[3] = -1.f;
+    }
+  }
+  if (lane == 0) phi[g] = kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f;
 }
 
 // ---- merge + exact re-scoring ------------------------------------------------------------------
-struct Cand16 {
-  float v[KM + 1];
-  int32_t i[KM + 1];
-};
-
-__device__ __forceinline__ void minsert(Cand16& c, float nv, int32_t ni) {
-  if (!cbetter(nv, ni, c.v[KM], c.i[KM])) return;
-#pragma unroll
-  for (int j = KM; j > 0; --j) {
-    const bool up = cbetter(nv, ni, c.v[j - 1], c.i[j - 1]);
-    const bool here = cbetter(nv, ni, c.v[j], c.i[j]);
-    const float pv = c.v[j - 1];
-    const int32_t pi = c.i[j - 1];
-    c.v[j] = up ? pv : (here ? nv : c.v[j]);
-    c.i[j] = up ? pi : (here ? ni : c.i[j]);
-  }
-  if (cbetter(nv, ni, c.v[0], c.i[0])) {
-    c.v[0] = nv;
-    c.i[0] = ni;
-  }
+__device__ __forceinline__ bool cbetter(float a, int32_t ia, float b, int32_t ib) {
+  if (ib < 0) return ia >= 0;
+  if (ia < 0) return false;
+  const float fa = fabsf(a), fb = fabsf(b);
+  return fa > fb || (fa == fb && ia < ib);
 }
 
+struct Pool {  // sorted (|r| desc, index asc) list of KM + 1
+  float v[KM + 1];
+  int32_t i[KM + 1];
+  __device__ __forceinline__ void insert(float nv, int32_t ni) {
+    if (!cbetter(nv, ni, v[KM], i[KM])) return;
+#pragma unroll
+    for (int j = KM; j > 0; --j) {
+      const bool up = cbetter(nv, ni, v[j - 1], i[j - 1]);
+      const bool here = cbetter(nv, ni, v[j], i[j]);
+      const float pv = v[j - 1];
+      const int32_t pi = i[j - 1];
+      v[j] = up ? pv : (here ? nv : v[j]);
+      i[j] = up ? pi : (here ? ni : i[j]);
+    }
+    if (cbetter(nv, ni, v[0], i[0])) {
+      v[0] = nv;
+      i[0] = ni;
+    }
+  }
+};
+
+constexpr int CAP = 2048;  // merge: candidates collected above the head threshold (else fallback)
+
+// theta = the (KM+1)-th largest list head (bitonic sort of the nb <= 4096 heads in LDS), or 0
+// when fewer than KM+1 lists are non-empty: at least KM+1 candidates are >= theta, so the best
+// KM+1 candidates all are.
+__device__ float head_threshold(const float* __restrict__ hd, int nb, float* key) {
+  const int tid = threadIdx.x;
+  int np = 64;
+  while (np < nb) np <<= 1;
+  for (int i = tid; i < np; i += TPB) key[i] = i < nb ? hd[2 * i] : -1.f;  // empty lists: -1
+  __syncthreads();
+  for (int kk = 2; kk <= np; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np; i += TPB) {
+        const int l = i ^ j;
+        if (l > i) {
+          const float a = key[i], c = key[l];
+          if ((a < c) == ((i & kk) == 0)) {  // descending runs first
+            key[i] = c;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const float t = key[KM];
+  __syncthreads();
+  return t < 0.f ? 0.f : t;
+}
+
+template <int KC>
 __global__ __launch_bounds__(TPB) void corr_merge(const float* __restrict__ cand_v, const int32_t* __restrict__ cand_i,
+                                                  const float* __restrict__ cand_hd, const float* __restrict__ phi,
                                                   const float* __restrict__ z32, int64_t P, int T, int nb, int k,
+                                                  float eps,
                                                   int32_t* __restrict__ out_i, float* __restrict__ out_v,
                                                   float* __restrict__ cert) {
+  __shared__ int hist[4096];  // the sorted list heads, then the collected candidates (v, i)
+  __shared__ int lid[4096];   // lists whose head is >= theta
+  __shared__ int n_lists;
+  __shared__ int ord[KM];
   __shared__ float sv[TPB / 64];
   __shared__ int32_t si[TPB / 64];
   __shared__ float top_v[KM + 1];
   __shared__ int32_t top_i[KM + 1];
   __shared__ double exact[KM];
-  __shared__ float dropped;
+  __shared__ int n_col;
   const int64_t g = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  Cand16 c;
-#pragma unroll
-  for (int j = 0; j <= KM; ++j) {
-    c.v[j] = 0.f;
-    c.i[j] = -1;
-  }
-  float tile_floor = 0.f;  // largest |r| a full tile list could have cut off
   const int64_t base = g * nb * KC;
-  for (int64_t q = tid; q < (int64_t)nb * KC; q += TPB) {
-    const int32_t id = cand_i[base + q];
-    if (id < 0) continue;
-    const float v = cand_v[base + q];
-    minsert(c, v, id);
-    if ((q % KC) == KC - 1) tile_floor = fmaxf(tile_floor, fabsf(v));
-  }
-  // block-wide extraction of the best KM+1 (k rounds of arg-max over the lane heads)
-  for (int r = 0; r <= KM; ++r) {
-    float bv = c.v[0];
-    int32_t bi = c.i[0];
-    for (int off = 32; off > 0; off >>= 1) {
-      const float ov = __shfl_xor(bv, off, 64);
-      const int32_t oi = __shfl_xor(bi, off, 64);
-      if (cbetter(ov, oi, bv, bi)) {
-        bv = ov;
-        bi = oi;
-      }
-    }
-    if (lane == 0) {
-      sv[w] = bv;
-      si[w] = bi;
-    }
-    __syncthreads();
-    float wv = sv[0];
-    int32_t wi = si[0];
-    for (int q = 1; q < TPB / 64; ++q)
-      if (cbetter(sv[q], si[q], wv, wi)) {
-        wv = sv[q];
-        wi = si[q];
-      }
-    __syncthreads();
-    if (tid == 0) {
-      top_v[r] = wv;
-      top_i[r] = wi;
-    }
-    if (wi != -1 && c.i[0] == wi && c.v[0] == wv) {
-#pragma unroll
-      for (int j = 0; j < KM; ++j) {
-        c.v[j] = c.v[j + 1];
-        c.i[j] = c.i[j + 1];
-      }
-      c.v[KM] = 0.f;
-      c.i[KM] = -1;
-    }
-  }
-  // tile_floor: max over lanes
-  for (int off = 32; off > 0; off >>= 1) tile_floor = fmaxf(tile_floor, __shfl_xor(tile_floor, off, 64));
-  if (lane == 0) sv[w] = tile_floor;
+  const float* hd = cand_hd + g * nb * 2;
+  // largest |r| any full per-block list could have cut off
+  float floor_ = 0.f;
+  for (int b = tid; b < nb; b += TPB) floor_ = fmaxf(floor_, hd[2 * b + 1]);
+  for (int off = 32; off > 0; off >>= 1) floor_ = fmaxf(floor_, __shfl_xor(floor_, off, 64));
+  if (lane == 0) sv[w] = floor_;
   __syncthreads();
-  if (tid == 0) dropped = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])), fabsf(top_v[KM]));
-  __syncthreads();
-  // exact float64 re-scoring of the best KM (one wave per candidate, fixed reduction order)
-  const float* zg = z32 + g * T;
-  for (int q = w; q < KM; q += TPB / 64) {
-    const int32_t j = top_i[q];
-    double s = 0.0;
-    if (j >= 0) {
-      const float* zj = z32 + (int64_t)j * T;
-      for (int t = lane; t < T; t += 64) s += (double)zg[t] * (double)zj[t];
-    }
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    if (lane == 0) exact[q] = s;
-  }
-  __syncthreads();
+  floor_ = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
+  const float theta = head_threshold(hd, nb, reinterpret_cast<float*>(hist));
+  // collect every candidate >= theta (lists are sorted, so a list is read only while >= theta)
+  float* cv = reinterpret_cast<float*>(hist);
+  int32_t* ci = hist + CAP;
   if (tid == 0) {
-    // order the re-scored candidates (|r| desc, index asc), keep k
-    int ord[KM];
-    for (int q = 0; q < KM; ++q) ord[q] = q;
-    for (int a = 1; a < KM; ++a) {
-      const int key = ord[a];
-      int bpos = a - 1;
-      while (bpos >= 0) {
-        const int o = ord[bpos];
-        const double fo = fabs(exact[o]), fk = fabs(exact[key]);
-        const bool kb = top_i[key] >= 0 && (top_i[o] < 0 || fk > fo ||
-                                            (fk == fo && (uint32_t)top_i[key] < (uint32_t)top_i[o]));
-        if (!kb) break;
-        ord[bpos + 1] = o;
-        --bpos;
-      }
-      ord[bpos + 1] = key;
-    }
-    for (int q = 0; q < k; ++q) {
-      out_i[g * k + q] = top_i[ord[q]];
-      out_v[g * k + q] = (float)exact[ord[q]];
-    }
-    cert[g] = (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)kEps);
+    n_col = 0;
+    n_lists = 0;
   }
+  __syncthreads();
+  for (int b = tid; b < nb; b += TPB)
+    if (hd[2 * b] >= theta && hd[2 * b] >= 0.f) lid[atomicAdd(&n_lists, 1)] = b;
+  __syncthreads();
+  const int nl = n_lists;
+  for (int item = tid; item < nl * KC; item += TPB) {  // every (list, entry): independent loads
+    const int64_t e = base + (int64_t)lid[item / KC] * KC + item % KC;
+    const int32_t id = cand_i[e];
+    const float v = cand_v[e];
+    if (id >= 0 && fabsf(v) >= theta) {
+      const int slot = atomicAdd(&n_col, 1);
+      if (slot < CAP) {
+        cv[slot] = v;
+        ci[slot] = id;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = n_col;
+  if (n <= CAP) {
+    // bitonic sort of the collected candidates (|r| desc, index asc; padding last)
+    int np = 32;
+    while (np < n) np <<= 1;
+    for (int i = n + tid; i < np; i += TPB) {
+      cv[i] = 0.f;
+      ci[i] = -1;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= np; kk <<= 1) {
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < np; i += TPB) {
+          const int l = i ^ j;
+          if (l > i) {
+            const bool desc = (i & kk) == 0;
+            const bool lbetter = cbetter(cv[l], ci[l], cv[i], ci[i]);
+            if (lbetter == desc) {
+              const float tv = cv[i];
+              const int32_t ti = ci[i];
+              cv[i] = cv[l];
+              ci[i] = ci[l];
+              cv[l] = tv;
+              ci[l] = ti;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (tid <= KM) {
+      top_v[tid] = tid < np ? cv[tid] : 0.f;
+      top_i[tid] = tid < np ? ci[tid] : -1;
+    }
+  } else {
+    // fallback (ties at the threshold, e.g. a flat series): per-lane pools over every candidate
+    Pool c;
+#pragma unroll
+    for (int j = 0; j <= KM; ++j) {
+      c.v[j] = 0.f;
+      c.i[j] = -1;
+    }
+    for (int64_t q = tid; q < (int64_t)nb * KC; q += TPB) {
+      const int32_t id = cand_i[base + q];
+      if (id >= 0) c.insert(cand_v[base + q], id);
+    }
+    for (int r = 0; r <= KM; ++r) {  // block-wide extraction, one winner per round
+      float bv = c.v[0];
+      int32_t bi = c.i[0];
+      for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int32_t oi = __shfl_xor(bi, off, 64);
+        if (cbetter(ov, oi, bv, bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (lane == 0) {
+        sv[w] = bv;
+        si[w] = bi;
+      }
+      __syncthreads();
+      float wv = sv[0];
+      int32_t wi = si[0];
+      for (int q = 1; q < TPB / 64; ++q)
+        if (cbetter(sv[q], si[q], wv, wi)) {
+          wv = sv[q];
+          wi = si[q];
+        }
+      __syncthreads();
+      if (tid == 0) {
+        top_v[r] = wv;
+        top_i[r] = wi;
+      }
+      if (wi >= 0 && c.i[0] == wi) {  // each partner sits in exactly one lane's pool
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+          c.v[j] = c.v[j + 1];
+          c.i[j] = c.i[j + 1];
+        }
+        c.v[KM] = 0.f;
+        c.i[KM] = -1;
+      }
+    }
+  }
+  __syncthreads();
+  // exact float64 re-scoring of the best km = min(KM, k + 6) (one wave per candidate, fixed
+  // reduction order); the certificate bounds everything outside them by the (km+1)-th
+  const int km = k + 6 < KM ? k + 6 : KM;
+  const float dropped = fmaxf(fmaxf(floor_, phi[g]), top_i[km] >= 0 ? fabsf(top_v[km]) : 0.f);
+  const float* zg = z32 + g * T;
+  {  // wave w re-scores candidates w, w+4, ... together (independent loads in flight)
+    constexpr int PER = (KM + TPB / 64 - 1) / (TPB / 64);
+    const float* zj[PER];
+    double acc2[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int q = w + u * (TPB / 64);
+      zj[u] = (q < km && top_i[q] >= 0) ? z32 + (int64_t)top_i[q] * T : nullptr;
+      acc2[u] = 0.0;
+    }
+    for (int t = lane; t < T; t += 64) {
+      const double a = (double)zg[t];
+#pragma unroll
+      for (int u = 0; u < PER; ++u)
+        if (zj[u]) acc2[u] += a * (double)zj[u][t];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      double s = acc2[u];
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      const int q = w + u * (TPB / 64);
+      if (lane == 0 && q < km) exact[q] = s;
+    }
+  }
+  __syncthreads();
+  if (tid < km) {  // rank of candidate tid: |exact| desc, index asc, empty last
+    const double fk = fabs(exact[tid]);
+    const int32_t ik = top_i[tid];
+    int rank = 0;
+    for (int o = 0; o < km; ++o) {
+      const double fo = fabs(exact[o]);
+      const int32_t io = top_i[o];
+      rank += o != tid && io >= 0 && (ik < 0 || fo > fk || (fo == fk && io < ik));
+    }
+    ord[rank] = tid;
+  }
+  __syncthreads();
+  for (int q = tid; q < k; q += TPB) {
+    out_i[g * k + q] = top_i[ord[q]];
+    out_v[g * k + q] = (float)exact[ord[q]];
+  }
+  if (tid == 0) cert[g] = (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
 }
+
+template <int KC>
+int launch_corr(const uint16_t* zh, const float* z32, int64_t P, int T, int Tp, int nb, int nsb, int k, float tau,
+                float eps, float* cand_v, int32_t* cand_i, float* cand_hd, float* samp_v, int32_t* samp_i, float* phi,
+                int32_t* count, int32_t* out_idx, float* out_val, float* cert, hipStream_t st) {
+  static bool lds_attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
+  if (!lds_attr) {
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    lds_attr = true;
+  }
+  // 1. threshold sample: every pod against the first nsb column blocks
+  hipLaunchKernelGGL((corr_tiles<KC, true>), dim3((unsigned)(nb * nsb)), dim3(TPB), LDS_BYTES, st, zh, P, Tp, nb,
+                     (int64_t)0, nsb, tau, (const float*)nullptr, samp_v, samp_i, (float*)nullptr,
+                     (int32_t*)nullptr);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, samp_v, samp_i, P,
+                     nsb, k, eps, phi);
+  KRCA_LAUNCH_CHECK();
+  // 2. all pairs (upper triangle), filtered by phi
+  const int64_t ns = (nb + SUPER - 1) / SUPER;
+  const int64_t slots = ns * (ns + 1) / 2 * SUPER * SUPER;
+  const int64_t per_xcd = (slots + 7) / 8;
+  hipLaunchKernelGGL((corr_tiles<KC, false>), dim3((unsigned)(8 * per_xcd)), dim3(TPB), LDS_BYTES, st, zh, P, Tp, nb,
+                     per_xcd, nsb, tau, (const float*)phi, cand_v, cand_i, cand_hd, count);
+  KRCA_LAUNCH_CHECK();
+  // 3. per pod: pool, exact re-scoring, top-k, certificate
+  hipLaunchKernelGGL(corr_merge<KC>, dim3((unsigned)P), dim3(TPB), 0, st, cand_v, cand_i, cand_hd, phi, z32, P, T, nb,
+                     k, eps, out_idx, out_val, cert);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int kc_for(int32_t k) { return k <= 4 ? 8 : k <= 8 ? 12 : 16; }
 
 }  // namespace
 
@@ -405,13 +631,23 @@ extern "C" {
 
 int64_t krca_corr_pad_rows(int64_t P) { return krca::ceil_div(P, BM) * BM; }
 int32_t krca_corr_pad_steps(int32_t T) { return (int32_t)krca::ceil_div(T, BK) * BK; }
-int64_t krca_corr_cand_size(int64_t P) { return P * (krca_corr_pad_rows(P) / BM) * KC; }
-int32_t krca_corr_max_k(void) { return KM; }
+constexpr int NSB = 16;  // column blocks in the threshold sample (2048 pods)
+// candidate workspace (4-byte words): values and indices [P][nb][KC] each, heads [P][nb][2],
+// sample lists [P][nsb][KC] x 2, phi [P]
+int64_t krca_corr_cand_size(int64_t P, int32_t k) {
+  const int64_t nb = krca_corr_pad_rows(P) / BM;
+  const int64_t nsb = nb < NSB ? nb : NSB;
+  return P * nb * (2 * kc_for(k) + 2) + P * nsb * 2 * kc_for(k) + P;
+}
+int32_t krca_corr_max_k(void) { return KMAX; }
+float krca_corr_eps(int32_t T) {
+  return (float)(std::ldexp(1.0, -10) * 1.001 + std::ldexp((double)T, -24) + std::ldexp(std::sqrt((double)T), -23));
+}
 
 int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t channel, float* mean, float* scale,
-                      float* z32, uint16_t* zhi, uint16_t* zlo, void* stream) {
+                      float* z32, uint16_t* zh, void* stream) {
   KRCA_CHECK_ARG(P > 0 && M > 0 && T > 0 && channel >= 0 && channel < M, "krca_corr_prepare: bad sizes");
-  KRCA_CHECK_ARG(x && mean && scale && z32 && zhi && zlo, "krca_corr_prepare: null pointer");
+  KRCA_CHECK_ARG(x && mean && scale && z32 && zh, "krca_corr_prepare: null pointer");
   const int64_t Pp = krca_corr_pad_rows(P);
   const int Tp = krca_corr_pad_steps(T);
   hipStream_t st = krca::as_stream(stream);
@@ -419,37 +655,39 @@ int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t c
                      scale);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(corr_transpose, dim3((unsigned)(Pp / 64), (unsigned)(Tp / 64)), dim3(TPB), 0, st, x, P, M, T, Tp,
-                     channel, mean, scale, z32, zhi, zlo);
+                     channel, mean, scale, z32, zh);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
 
-int krca_corr_topk(const uint16_t* zhi, const uint16_t* zlo, const float* z32, int64_t P, int32_t T, int32_t k,
-                   float tau, float* cand_v, int32_t* cand_i, int32_t* count, int32_t* out_idx, float* out_val,
-                   float* cert, void* stream) {
-  KRCA_CHECK_ARG(P > 1 && P < INT32_MAX && T > 0, "krca_corr_topk: bad sizes");
-  KRCA_CHECK_ARG(k >= 1 && k <= KM && k < P, "krca_corr_topk: k must be in [1, %d] and < P", KM);
-  KRCA_CHECK_ARG(zhi && zlo && z32 && cand_v && cand_i && count && out_idx && out_val && cert,
-                 "krca_corr_topk: null pointer");
+int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, void* cand,
+                   int32_t* count, int32_t* out_idx, float* out_val, float* cert, void* stream) {
+  KRCA_CHECK_ARG(P > 1 && krca_corr_pad_rows(P) <= 4096 * BM && T > 0,
+                 "krca_corr_topk: P must be in [2, %d]", 4096 * BM);
+  KRCA_CHECK_ARG(k >= 1 && k <= KMAX && k < P, "krca_corr_topk: k must be in [1, %d] and < P", KMAX);
+  KRCA_CHECK_ARG(zh && z32 && cand && count && out_idx && out_val && cert, "krca_corr_topk: null pointer");
   const int64_t Pp = krca_corr_pad_rows(P);
   const int Tp = krca_corr_pad_steps(T);
   const int nb = (int)(Pp / BM);
-  const int64_t ntiles = (int64_t)nb * (nb + 1) / 2;
+  const float eps = krca_corr_eps(T);
+  const int nsb = nb < NSB ? nb : NSB;
+  const int KCr = kc_for(k);
+  const int64_t lists = P * nb;
+  float* cand_v = reinterpret_cast<float*>(cand);
+  int32_t* cand_i = reinterpret_cast<int32_t*>(cand_v + lists * KCr);
+  float* cand_hd = reinterpret_cast<float*>(cand_i + lists * KCr);
+  float* samp_v = cand_hd + lists * 2;
+  int32_t* samp_i = reinterpret_cast<int32_t*>(samp_v + P * nsb * KCr);
+  float* phi = reinterpret_cast<float*>(samp_i + P * nsb * KCr);
   hipStream_t st = krca::as_stream(stream);
-  static bool lds_attr = false;
-  if (!lds_attr) {
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    lds_attr = true;
-  }
   KRCA_HIP(hipMemsetAsync(count, 0, P * sizeof(int32_t), st));
-  hipLaunchKernelGGL(corr_tiles, dim3((unsigned)ntiles), dim3(TPB), LDS_BYTES, st, zhi, zlo, P, Tp, nb, tau, cand_v,
-                     cand_i, count);
-  KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(corr_merge, dim3((unsigned)P), dim3(TPB), 0, st, cand_v, cand_i, z32, P, T, nb, k, out_idx,
-                     out_val, cert);
-  KRCA_LAUNCH_CHECK();
-  return KRCA_OK;
+  switch (kc_for(k)) {
+    case 8: return launch_corr<8>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, cand_v, cand_i, cand_hd, samp_v, samp_i, phi, count, out_idx, out_val, cert, st);
+    case 12:
+      return launch_corr<12>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, cand_v, cand_i, cand_hd, samp_v, samp_i, phi, count, out_idx, out_val, cert, st);
+    default:
+      return launch_corr<16>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, cand_v, cand_i, cand_hd, samp_v, samp_i, phi, count, out_idx, out_val, cert, st);
+  }
 }
 
 }  // extern "C"

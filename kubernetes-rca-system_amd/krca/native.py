@@ -34,11 +34,11 @@ SIGNATURES = {
     "krca_template_max_lines": (c_i32, []),
     "krca_corr_pad_rows": (c_i64, [c_i64]),
     "krca_corr_pad_steps": (c_i32, [c_i32]),
-    "krca_corr_cand_size": (c_i64, [c_i64]),
+    "krca_corr_cand_size": (c_i64, [c_i64, c_i32]),
     "krca_corr_max_k": (c_i32, []),
-    "krca_corr_prepare": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "krca_corr_topk": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                               c_vp]),
+    "krca_corr_eps": (c_f32, [c_i32]),
+    "krca_corr_prepare": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_corr_topk": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_ppr_plan_size": (c_i64, [c_vp, c_i64]),
     "krca_ppr_plan": (c_i32, [c_vp, c_i64, c_vp, c_i64]),
     "krca_ppr_workspace_size": (c_i64, [c_i64]),
@@ -280,10 +280,9 @@ class NativeEngine:
         z = dict(P=P, T=T, mean=torch.empty(P, dtype=torch.float32, device=self.device),
                  scale=torch.empty(P, dtype=torch.float32, device=self.device),
                  z32=torch.empty((P, T), dtype=torch.float32, device=self.device),
-                 zhi=torch.empty((Pp, Tp), dtype=torch.int16, device=self.device),
-                 zlo=torch.empty((Pp, Tp), dtype=torch.int16, device=self.device))
+                 zh=torch.empty((Pp, Tp), dtype=torch.int16, device=self.device))
         _check(self.lib.krca_corr_prepare(self.ptr(x), P, M, T, int(channel), self.ptr(z["mean"]), self.ptr(z["scale"]),
-                                          self.ptr(z["z32"]), self.ptr(z["zhi"]), self.ptr(z["zlo"]), self._stream()),
+                                          self.ptr(z["z32"]), self.ptr(z["zh"]), self._stream()),
                "krca_corr_prepare")
         return z
 
@@ -291,16 +290,15 @@ class NativeEngine:
         """Per-pod top-k |Pearson r| partners from corr_prepare_device's output (device, no sync)."""
         torch = self.torch
         P, T = z["P"], z["T"]
-        nc = self.lib.krca_corr_cand_size(P)
-        cv = self._workspace("corr_cv", 4 * nc)
-        ci = self._workspace("corr_ci", 4 * nc)
+        nc = self.lib.krca_corr_cand_size(P, int(k))
+        cand = self._workspace("corr_cand", 4 * nc)
         if out is None:
             out = dict(idx=torch.empty((P, k), dtype=torch.int32, device=self.device),
                        val=torch.empty((P, k), dtype=torch.float32, device=self.device),
                        count=torch.empty(P, dtype=torch.int32, device=self.device),
                        cert=torch.empty(P, dtype=torch.float32, device=self.device))
-        _check(self.lib.krca_corr_topk(self.ptr(z["zhi"]), self.ptr(z["zlo"]), self.ptr(z["z32"]), P, T, int(k),
-                                       float(tau), self.ptr(cv), self.ptr(ci), self.ptr(out["count"]),
+        _check(self.lib.krca_corr_topk(self.ptr(z["zh"]), self.ptr(z["z32"]), P, T, int(k),
+                                       float(tau), self.ptr(cand), self.ptr(out["count"]),
                                        self.ptr(out["idx"]), self.ptr(out["val"]), self.ptr(out["cert"]),
                                        self._stream()), "krca_corr_topk")
         return out

@@ -13,7 +13,7 @@ from krca import native
 def header_symbols():
     with open(os.path.join(ROOT, "include", "krca.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|const char\*)\s+(krca_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|float|const char\*)\s+(krca_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol():
