@@ -26,6 +26,7 @@
 // terms of a unit-norm product by <= T 2^-24.  It bounds the ranking pool and the |r| > tau
 // counts (pairs within eps of tau may land on either side); reported r values are exact.
 #include <cmath>
+#include <cstdlib>
 
 #include "krca_common.h"
 
@@ -134,175 +135,236 @@ struct Cand {
   }
 };
 
-constexpr int STAGE_BYTES = 2 * BM * BK * 2;           // A and B, fp16
-constexpr int LDS_STAGE = 2 * STAGE_BYTES;             // double buffered
-constexpr int LDS_EPI = BM * (BM + 1) * 4;             // fp32 tile, padded rows
-constexpr int LDS_BYTES = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
+// Tile kernel: 256 x 256 pods per workgroup (8 waves = 2 row halves x 4 column quarters, a
+// 128 x 64 wave tile = 4 x 2 MFMA 32x32 blocks), K steps of 64 through a double-buffered LDS
+// stage (A and B 256 x 64 fp16 each) fed by a register prefetch.  Candidate lists keep the
+// 128-pod block granularity: a row's list covers one 128-column half of the tile, a column's list
+// one 128-row half.
+constexpr int TB = 256;                                // tile edge (pods)
+constexpr int NT = 512;                                // threads per tile workgroup
+constexpr int STAGE_BYTES = 2 * TB * BK * 2;           // A and B, fp16
+constexpr int LDS_STAGE = 2 * STAGE_BYTES;             // double buffered: 128 KB
+constexpr int EPI_LD = TB + 4;  // padded row of the epilogue half tile (16-B rows; conflict-free b128 row reads)
+constexpr int LDS_EPI = BM * EPI_LD * 4;               // 128 rows x 256 columns fp32
+constexpr int LDS_MAIN = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
+constexpr int LDS_JUNK = NT * 4;                       // landing slots of the L2 prefetch loads
+constexpr int LDS_BYTES = LDS_MAIN + LDS_JUNK;
 
-// 16-byte chunk c (0..7) of row r of a [128][64] fp16 tile, XOR-swizzled against bank conflicts
-__device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+// 16-byte chunk c (0..7) of row r of a [rows][64] fp16 stage, XOR-swizzled against bank conflicts
+// (the XOR key (r >> 1) & 7 makes every 16-lane ds_read_b128 phase of 16 rows hit 16 distinct
+// 4-bank granules: row parity picks the 32-bank half, the key the granule inside it)
+__device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
-// SAMPLE = false: the upper triangle (all pairs), lists filtered by phi, heads + counts out.
-// SAMPLE = true: rows x the first nsb column blocks (the threshold sample), row lists only.
+// SAMPLE = false: the upper triangle of 256-blocks (all pairs), lists filtered by phi, heads and
+//                 |r| > tau counts out.
+// SAMPLE = true:  rows x the first nsb 128-column blocks (the threshold sample), row lists only.
 template <int KC, bool SAMPLE>
-__global__ __launch_bounds__(TPB) void corr_tiles(const uint16_t* __restrict__ zh, int64_t P, int Tp, int nb,
-                                                  int64_t per_xcd, int nsb, float tau,
-                                                  const float* __restrict__ phi, float* __restrict__ cand_v,
-                                                  int32_t* __restrict__ cand_i, float* __restrict__ cand_hd,
-                                                  int32_t* __restrict__ count) {
+__global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh, int64_t P, int Tp, int nb2,
+                                                 int64_t per_xcd, int nsb, float tau, const float* __restrict__ phi,
+                                                 float* __restrict__ cand_v, int32_t* __restrict__ cand_i,
+                                                 float* __restrict__ cand_hd, int32_t* __restrict__ count,
+                                                 int debug) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nb = 2 * nb2;  // 128-pod blocks
   int64_t I, J;
   if (SAMPLE) {
-    I = blockIdx.x / nsb;
-    J = blockIdx.x % nsb;
+    const int nsb2 = (nsb + 1) / 2;
+    I = blockIdx.x / nsb2;
+    J = blockIdx.x % nsb2;
   } else {
-  // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs, so slot
-  // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the upper
-  // triangle in SUPER x SUPER super-tiles, so the ~64 tiles an XCD has in flight share 2*SUPER
-  // row blocks through its L2.  Slots below the diagonal or past nb exit at once.
-  const int64_t b = blockIdx.x;
-  const int64_t L = (b & 7) * per_xcd + (b >> 3);
-  const int64_t ns = (nb + SUPER - 1) / SUPER;
-  const int64_t st = L / (SUPER * SUPER);
-  if (st >= ns * (ns + 1) / 2) return;
-  int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
-  while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
-  while (SJ * (SJ + 1) / 2 > st) --SJ;
-  const int64_t SI = st - SJ * (SJ + 1) / 2;
-  const int64_t in = L % (SUPER * SUPER);
-  I = SI * SUPER + in / SUPER;
-  J = SJ * SUPER + in % SUPER;
-  if (I > J || J >= nb) return;
+    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so slot
+    // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the
+    // upper triangle in SUPER x SUPER super-tiles, so the tiles an XCD has in flight share 2*SUPER
+    // row blocks through its L2.  Slots below the diagonal or past nb2 exit at once.
+    const int64_t b = blockIdx.x;
+    const int64_t L = (b & 7) * per_xcd + (b >> 3);
+    const int64_t ns = (nb2 + SUPER - 1) / SUPER;
+    const int64_t st = L / (SUPER * SUPER);
+    if (st >= ns * (ns + 1) / 2) return;
+    int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
+    while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
+    while (SJ * (SJ + 1) / 2 > st) --SJ;
+    const int64_t SI = st - SJ * (SJ + 1) / 2;
+    const int64_t in = L % (SUPER * SUPER);
+    I = SI * SUPER + in / SUPER;
+    J = SJ * SUPER + in % SUPER;
+    if (I > J || J >= nb2) return;
   }
-
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 1, wc = w & 1;
-  const int64_t rowA = I * BM, rowB = J * BM;
+  const int wr = w >> 2, wc = w & 3;
+  const int64_t rowA = I * TB, rowB = J * TB;
 
-  floatx16 acc[2][2];
+  floatx16 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  // register prefetch of one K step: A and B, 128 rows x 8 chunks each = 4 + 4 chunks per lane
-  u32x4 pa[4], pb[4];
+  // Staging: global -> LDS direct (global_load_lds_dwordx4, no VGPR round trip).  One wave
+  // instruction writes a lane-linear 1 KiB piece = 8 rows of 128 B; lane l lands on row l/8,
+  // slot l%8, so it fetches the global chunk (l%8) ^ key(row): the XOR swizzle is applied on the
+  // SOURCE address.  64 pieces per K step (32 A + 32 B), 8 per wave.
   const uint16_t* gA = zh + rowA * Tp;
   const uint16_t* gB = zh + rowB * Tp;
-#define CORR_FETCH(K0)                                                    \
-  _Pragma("unroll") for (int q = 0; q < 4; ++q) {                         \
-    const int id = tid + q * TPB; /* row id>>3, 16-byte chunk id&7 */     \
-    const int64_t o = (int64_t)(id >> 3) * Tp + (K0) + (id & 7) * 8;      \
-    pa[q] = *reinterpret_cast<const u32x4*>(gA + o);                      \
-    pb[q] = *reinterpret_cast<const u32x4*>(gB + o);                      \
+  const int prow = lane >> 3, pslot = lane & 7;
+#define CORR_GLDS(BUF, K0)                                                                             \
+  _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                      \
+    const int piece = w + 8 * q;      /* rows 8*piece .. +7 */                                         \
+    const int row = 8 * piece + prow;                                                                  \
+    const int64_t src = (int64_t)row * Tp + (K0) + ((pslot ^ ((row >> 1) & 7)) << 3);                 \
+    char* dA = smem + (BUF) * STAGE_BYTES + piece * 1024;                                              \
+    __builtin_amdgcn_global_load_lds(gA + src, (__attribute__((address_space(3))) void*)dA, 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds(gB + src, (__attribute__((address_space(3))) void*)(dA + TB * BK * 2), \
+                                     16, 0, 0);                                                       \
   }
-#define CORR_STORE(BUF)                                                   \
-  _Pragma("unroll") for (int q = 0; q < 4; ++q) {                         \
-    const int id = tid + q * TPB;                                         \
-    const int o = chunk_off(id >> 3, id & 7);                             \
-    *reinterpret_cast<u32x4*>(smem + (BUF) * STAGE_BYTES + o) = pa[q];    \
-    *reinterpret_cast<u32x4*>(smem + (BUF) * STAGE_BYTES + BM * BK * 2 + o) = pb[q]; \
-  }
-  CORR_FETCH(0)
-  CORR_STORE(0)
-  __syncthreads();
   const int r32 = lane & 31, h = lane >> 5;
+#define CORR_COMPUTE(BUF)                                                                         \
+  {                                                                                                \
+    const char* sA = smem + (BUF) * STAGE_BYTES;                                                   \
+    const char* sB = sA + TB * BK * 2;                                                             \
+    _Pragma("unroll") for (int ks = 0; ks < BK / 16; ++ks) {                                       \
+      const int c = ks * 2 + h;                                                                    \
+      halfx8 fa[4], fb[2];                                                                         \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
+        fa[i] = *reinterpret_cast<const halfx8*>(sA + chunk_off(wr * 128 + i * 32 + r32, c));      \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
+        fb[j] = *reinterpret_cast<const halfx8*>(sB + chunk_off(wc * 64 + j * 32 + r32, c));       \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);    \
+    }                                                                                              \
+  }
+  // L2 prefetch of K step s+2 while step s+1 streams into LDS: one 4-byte LDS-DMA per 128-B line
+  // (lane tid < 256: A row tid, else B row tid-256) into a junk LDS slot, so no VGPR is tied up;
+  // step s+2's 16-byte loads then hit L2 instead of paying the HBM/MALL latency inside one
+  // K step's compute.  The barrier waits vmcnt(1): the stage loads, issued before it, are done.
+  const uint16_t* gP = (tid < TB ? gA + (int64_t)tid * Tp : gB + (int64_t)(tid - TB) * Tp);
+  char* junk = smem + LDS_MAIN + w * 256;
+#define CORR_L2PF(K0) \
+  __builtin_amdgcn_global_load_lds(gP + (K0), (__attribute__((address_space(3))) void*)junk, 4, 0, 0);
   const int nk = Tp / BK;
+  CORR_GLDS(0, 0)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int s = 0; s < nk; ++s) {
-    const bool more = s + 1 < nk;
-    if (more) {
-      CORR_FETCH((s + 1) * BK)
+    // stage (s+1)&1 was last read in step s-1, which every wave finished before the barrier
+    if (s + 1 < nk) {
+      CORR_GLDS((s + 1) & 1, (s + 1) * BK)
     }
-    const char* sA = smem + (s & 1) * STAGE_BYTES;
-    const char* sB = sA + BM * BK * 2;
+    if (s + 2 < nk) {
+      CORR_L2PF((s + 2) * BK)
+    } else {
+      CORR_L2PF(0)  // keeps the count of outstanding loads uniform (re-touches a resident line)
+    }
+    __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs, not after
+    CORR_COMPUTE(s & 1)
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#undef CORR_GLDS
+#undef CORR_COMPUTE
+#undef CORR_L2PF
+  // epilogue, one 128-row half at a time: the half's waves park their accumulators in LDS, then
+  // 256 lanes scan rows (one 128-column half each) and 256 lanes scan columns (128 rows each)
+  float* tile = reinterpret_cast<float*>(smem);
+  const bool diag = I == J;
+  if (debug == 1) {  // profiling aid (KRCA_CORR_DEBUG=1): product only, no epilogue
+    if (tid == 0 && acc[0][0][0] == 12345.f) count[0] = 1;
+    return;
+  }
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int c = ks * 2 + h;
-      halfx8 fa[2], fb[2];
+  for (int half = 0; half < 2; ++half) {
+    if (wr == half) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        fa[i] = *reinterpret_cast<const halfx8*>(sA + chunk_off(wr * 64 + i * 32 + r32, c));
-        fb[i] = *reinterpret_cast<const halfx8*>(sB + chunk_off(wc * 64 + i * 32 + r32, c));
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      CORR_STORE((s + 1) & 1)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int col = wc * 64 + j * 32 + r32;
+            tile[row * EPI_LD + col] = acc[i][j][e];
+          }
     }
     __syncthreads();
-  }
-#undef CORR_FETCH
-#undef CORR_STORE
-  // epilogue: tile -> LDS [row][col] (padded), then row / column scans
-  float* tile = reinterpret_cast<float*>(smem);
+    Cand<KC> cd;
+    cd.init();
+    int n_over = 0;
+    int64_t g = -1, slot = 0;
+    bool write = false;
+    if (tid < 256) {  // row scan: pod rowA + half*128 + r against 128 columns of block 2J + ch
+      const int r = tid & 127, ch = tid >> 7;
+      g = rowA + half * BM + r;
+      const int jb = 2 * (int)J + ch;
+      const int64_t c0 = rowB + ch * BM;
+      if (g < P && (!SAMPLE || jb < nsb)) {
+        write = true;
+        slot = SAMPLE ? g * 16 + jb : g * nb + jb;
+        const float ph = SAMPLE ? -1.f : phi[g];
+        float lim = ph;  // = max(list floor, phi), refreshed on insert
+        const int cend = (int)std::min<int64_t>(BM, P - c0);
+        const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
+        const float* rowp = tile + r * EPI_LD + ch * BM;
+        for (int c4 = 0; c4 < cend; c4 += 4) {
+          const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int col = wc * 64 + j * 32 + r32;
-        tile[row * (BM + 1) + col] = acc[i][j][e];
+          for (int u = 0; u < 4; ++u) {
+            const int c = c4 + u;
+            const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
+            const float a = fabsf(vu);
+            const bool ok = c < cend && c != self;
+            n_over += (ok && a > tau) ? 1 : 0;
+            if (ok && a > lim) {
+              cd.insert(vu, (int32_t)(c0 + c));
+              lim = fmaxf(cd.thr, ph);
+            }
+          }
+        }
       }
-  __syncthreads();
-  Cand<KC> cd;
-  cd.init();
-  int n_over = 0;
-  int64_t g = -1, blk = 0;
-  if (tid < BM) {  // row scan: pod rowA+tid against the columns of block J
-    g = rowA + tid;
-    blk = J;
-    if (g < P) {
-      const float ph = SAMPLE ? -1.f : phi[g];
-      const int cend = (int)std::min<int64_t>(BM, P - rowB);
-      const float* rowp = tile + tid * (BM + 1);
-      for (int c = 0; c < cend; ++c) {
-        if (rowB + c == g) continue;
-        const float v = rowp[c];
-        const float a = fabsf(v);
-        n_over += a > tau;
-        if (a > fmaxf(cd.thr, ph)) cd.insert(v, (int32_t)(rowB + c));
-      }
-    }
-  } else if (!SAMPLE && I != J) {  // column scan: pod rowB+c against the rows of block I
-    const int c = tid - BM;
-    g = rowB + c;
-    blk = I;
-    if (g < P) {
-      const float ph = phi[g];
-      const int rend = (int)std::min<int64_t>(BM, P - rowA);
-      for (int r = 0; r < rend; ++r) {
-        const float v = tile[r * (BM + 1) + c];
-        const float a = fabsf(v);
-        n_over += a > tau;
-        if (a > fmaxf(cd.thr, ph)) cd.insert(v, (int32_t)(rowA + r));
-      }
-    }
-  }
-  if (g >= 0 && g < P) {
-    const int64_t slot = SAMPLE ? g * nsb + blk : g * nb + blk;
-    if (SAMPLE || cd.i[0] >= 0) {  // empty main-pass lists are never read (head = -1)
-      float* ov = cand_v + slot * KC;
-      int32_t* oi = cand_i + slot * KC;
-#pragma unroll
-      for (int q = 0; q < KC; ++q) {
-        ov[q] = cd.v[q];
-        oi[q] = cd.i[q];
+    } else if (!SAMPLE && !diag) {  // column scan: pod rowB + c against the 128 rows of this half
+      const int c = tid - 256;
+      g = rowB + c;
+      const int ib = 2 * (int)I + half;
+      const int64_t r0 = rowA + half * BM;
+      if (g < P) {
+        write = true;
+        slot = g * nb + ib;
+        const float ph = phi[g];
+        float lim = ph;
+        const int rend = (int)std::min<int64_t>(BM, P - r0);
+        for (int r = 0; r < rend; ++r) {
+          const float v = tile[r * EPI_LD + c];
+          const float a = fabsf(v);
+          n_over += a > tau ? 1 : 0;
+          if (a > lim) {
+            cd.insert(v, (int32_t)(r0 + r));
+            lim = fmaxf(cd.thr, ph);
+          }
+        }
       }
     }
-    if (!SAMPLE) {
-      // list head (best |r|, -1 if empty) and floor (KC-th |r| if the list is full, else -1)
-      cand_hd[slot * 2] = cd.i[0] < 0 ? -1.f : fabsf(cd.v[0]);
-      cand_hd[slot * 2 + 1] = cd.thr;
-      if (n_over) atomicAdd(&count[g], n_over);
+    if (write) {
+      if (SAMPLE || cd.i[0] >= 0) {  // empty main-pass lists are never read (head = -1)
+        float* ov = cand_v + slot * KC;
+        int32_t* oi = cand_i + slot * KC;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+          ov[q] = cd.v[q];
+          oi[q] = cd.i[q];
+        }
+      }
+      if (!SAMPLE) {
+        // list head (best |r|, -1 if empty) and floor (KC-th |r| if the list is full, else -1)
+        cand_hd[slot * 2] = cd.i[0] < 0 ? -1.f : fabsf(cd.v[0]);
+        cand_hd[slot * 2 + 1] = cd.thr;
+        if (n_over) atomicAdd(&count[g], n_over);
+      }
     }
+    __syncthreads();  // the next half overwrites the tile
   }
 }
 
@@ -314,12 +376,13 @@ __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, 
   const int64_t g = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= P) return;
-  const int n = nsb * KC;  // <= 256
+  const int n = nsb * KC;  // <= 256; sample lists are [P][16][KC]
   float a[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int q = lane + 64 * u;
-    a[u] = (q < n && si[g * n + q] >= 0) ? fabsf(sv[g * n + q]) : -1.f;
+    const int64_t e = g * 16 * KC + q;
+    a[u] = (q < n && si[e] >= 0) ? fabsf(sv[e]) : -1.f;
   }
   float kth = -1.f;
   for (int r = 0; r < k; ++r) {
@@ -589,6 +652,15 @@ __global__ __launch_bounds__(TPB) void corr_merge(const float* __restrict__ cand
   if (tid == 0) cert[g] = (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
 }
 
+int debug_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("KRCA_CORR_DEBUG");
+    m = e ? atoi(e) : 0;
+  }
+  return m;
+}
+
 template <int KC>
 int launch_corr(const uint16_t* zh, const float* z32, int64_t P, int T, int Tp, int nb, int nsb, int k, float tau,
                 float eps, float* cand_v, int32_t* cand_i, float* cand_hd, float* samp_v, int32_t* samp_i, float* phi,
@@ -602,19 +674,20 @@ int launch_corr(const uint16_t* zh, const float* z32, int64_t P, int T, int Tp, 
     lds_attr = true;
   }
   // 1. threshold sample: every pod against the first nsb column blocks
-  hipLaunchKernelGGL((corr_tiles<KC, true>), dim3((unsigned)(nb * nsb)), dim3(TPB), LDS_BYTES, st, zh, P, Tp, nb,
-                     (int64_t)0, nsb, tau, (const float*)nullptr, samp_v, samp_i, (float*)nullptr,
-                     (int32_t*)nullptr);
+  const int nb2 = nb / 2;
+  hipLaunchKernelGGL((corr_tiles<KC, true>), dim3((unsigned)(nb2 * ((nsb + 1) / 2))), dim3(NT), LDS_BYTES, st, zh, P,
+                     Tp, nb2, (int64_t)0, nsb, tau, (const float*)nullptr, samp_v, samp_i, (float*)nullptr,
+                     (int32_t*)nullptr, 0);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, samp_v, samp_i, P,
                      nsb, k, eps, phi);
   KRCA_LAUNCH_CHECK();
   // 2. all pairs (upper triangle), filtered by phi
-  const int64_t ns = (nb + SUPER - 1) / SUPER;
+  const int64_t ns = (nb2 + SUPER - 1) / SUPER;
   const int64_t slots = ns * (ns + 1) / 2 * SUPER * SUPER;
   const int64_t per_xcd = (slots + 7) / 8;
-  hipLaunchKernelGGL((corr_tiles<KC, false>), dim3((unsigned)(8 * per_xcd)), dim3(TPB), LDS_BYTES, st, zh, P, Tp, nb,
-                     per_xcd, nsb, tau, (const float*)phi, cand_v, cand_i, cand_hd, count);
+  hipLaunchKernelGGL((corr_tiles<KC, false>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, P, Tp, nb2,
+                     per_xcd, nsb, tau, (const float*)phi, cand_v, cand_i, cand_hd, count, debug_mode());
   KRCA_LAUNCH_CHECK();
   // 3. per pod: pool, exact re-scoring, top-k, certificate
   hipLaunchKernelGGL(corr_merge<KC>, dim3((unsigned)P), dim3(TPB), 0, st, cand_v, cand_i, cand_hd, phi, z32, P, T, nb,
@@ -629,15 +702,14 @@ int kc_for(int32_t k) { return k <= 4 ? 8 : k <= 8 ? 12 : 16; }
 
 extern "C" {
 
-int64_t krca_corr_pad_rows(int64_t P) { return krca::ceil_div(P, BM) * BM; }
+int64_t krca_corr_pad_rows(int64_t P) { return krca::ceil_div(P, TB) * TB; }
 int32_t krca_corr_pad_steps(int32_t T) { return (int32_t)krca::ceil_div(T, BK) * BK; }
 constexpr int NSB = 16;  // column blocks in the threshold sample (2048 pods)
 // candidate workspace (4-byte words): values and indices [P][nb][KC] each, heads [P][nb][2],
 // sample lists [P][nsb][KC] x 2, phi [P]
 int64_t krca_corr_cand_size(int64_t P, int32_t k) {
   const int64_t nb = krca_corr_pad_rows(P) / BM;
-  const int64_t nsb = nb < NSB ? nb : NSB;
-  return P * nb * (2 * kc_for(k) + 2) + P * nsb * 2 * kc_for(k) + P;
+  return P * nb * (2 * kc_for(k) + 2) + P * NSB * 2 * kc_for(k) + P;
 }
 int32_t krca_corr_max_k(void) { return KMAX; }
 float krca_corr_eps(int32_t T) {
@@ -677,8 +749,8 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
   int32_t* cand_i = reinterpret_cast<int32_t*>(cand_v + lists * KCr);
   float* cand_hd = reinterpret_cast<float*>(cand_i + lists * KCr);
   float* samp_v = cand_hd + lists * 2;
-  int32_t* samp_i = reinterpret_cast<int32_t*>(samp_v + P * nsb * KCr);
-  float* phi = reinterpret_cast<float*>(samp_i + P * nsb * KCr);
+  int32_t* samp_i = reinterpret_cast<int32_t*>(samp_v + P * NSB * KCr);
+  float* phi = reinterpret_cast<float*>(samp_i + P * NSB * KCr);
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(count, 0, P * sizeof(int32_t), st));
   switch (kc_for(k)) {
