@@ -13,7 +13,8 @@ from collections import defaultdict
 def load(d):
     out = defaultdict(lambda: defaultdict(float))
     calls = defaultdict(set)
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    files = [d] if os.path.isfile(d) else glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    for f in files:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
             out[k][r["Counter_Name"]] += float(r["Counter_Value"])
