@@ -92,18 +92,7 @@ def main():
     t_start = time.perf_counter()
     for i in range(args.steps):
         # HIP events on the stream the scoring kernel is launched on (torch's current stream)
-        ev[i][0].record()
-        shard.score()
-        ev[i][1].record()
-        shard.init(cfg.alpha, cfg.seed_floor)
-        step.comm.all_gather(shard.w_all, shard.send)
-        shard.reduce(cfg.alpha, cfg.tol, 1)
-        for _ in range(cfg.iters):
-            shard.spmv()
-            shard.update(cfg.alpha)
-            step.comm.all_gather(shard.w_all, shard.send)
-            shard.reduce(cfg.alpha, cfg.tol, 0)
-        top_idx, top_key = step.merge(*shard.local_topk(cfg.k))
+        top_idx, top_key = step.run(score_events=ev[i])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:

@@ -125,9 +125,14 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
  * all are at the floor).  Arithmetic is 2^-60 fixed point in int64: results do not depend on
  * summation order or GPU count and are bit-identical to oracle/krca_oracle.c.
  * krca_ppr runs the whole iteration on one device (synchronous: returns *iters_host); the
- * krca_ppr_shard_* steps are the same kernels for G pod-sharded ranks whose host loop
- * all-gathers each rank's [w_local(n_max) | 3 partial sums] slice over RCCL between
- * krca_ppr_shard_update and krca_ppr_shard_reduce (kubernetes-rca-system_amd/krca/rca.py). */
+ * krca_ppr_shard_* steps are the same kernels for G pod-sharded ranks.  Per iteration:
+ * krca_ppr_shard_step (pull SpMV fused with the rank update: gathers w_all, writes r_local and
+ * this rank's send slice [w_local(n_max) | krca_ppr_nslot() partial-sum slots]), then the host
+ * exchange (G > 1: RCCL all-gather of send into w_all[G][n_max+nslot]; G = 1: swap of two
+ * buffers, no copy), then krca_ppr_shard_reduce (kubernetes-rca-system_amd/krca/rca.py).
+ * ctl: krca_ppr_ctl_size(n_local) bytes, zero-filled by the caller once (long-row accumulators
+ * live there and reset themselves). */
+int32_t krca_ppr_nslot(void);
 int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N);
 int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, int64_t plan_len);
 int64_t krca_ppr_workspace_size(int64_t N);
@@ -135,19 +140,17 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
              const int32_t* plan, int64_t plan_len, const float* seed, float seed_floor, double alpha,
              int32_t max_iter, double tol, void* workspace, float* r_out, int64_t* r_fixed /*nullable*/,
              int64_t* q_out /*nullable: quantised seeds*/, int32_t* iters_host, void* stream);
-int64_t krca_ppr_ctl_size(void);
+int64_t krca_ppr_ctl_size(int64_t n_local);
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream);
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
-                        int64_t* r_local, int64_t* send /*[n_max+3]*/, void* stream);
-int krca_ppr_shard_spmv(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int32_t* plan,
-                        int64_t plan_len, const int64_t* w_all /*[G][n_max+3]*/, int64_t* acc,
-                        const void* ctl, void* stream);
-int krca_ppr_shard_update(const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
-                          int64_t N, double alpha, int64_t* r_local, int64_t* acc, int64_t* send,
-                          void* ctl, void* stream);
+                        int64_t* r_local, int64_t* send /*[n_max+nslot]*/, void* stream);
+int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int32_t* plan,
+                        int64_t plan_len, const int64_t* w_all /*[G][n_max+nslot]*/, const int32_t* outdeg,
+                        const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
+                        int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
-                          double tol, int32_t first, void* ctl, int64_t* send, void* stream);
+                          double tol, int32_t first, void* ctl, int64_t* send_next, void* stream);
 int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);
 int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream);
 /* root-cause key = bits of (double)r_i * (double)q_i: ranks pods by propagated mass times their

@@ -7,23 +7,27 @@
 //
 // Determinism: the rank mass is held in int64 fixed point (1.0 == 2^60).  Per-node quantities
 // that need a product or quotient are formed in float64 with a fixed expression and truncated
-// to int64; every SUM (SpMV rows, dangling mass, residual, seed total) is an integer sum, so the
-// result does not depend on the summation order, on atomics or on the number of GPUs, and is
-// bit-identical to oracle/krca_oracle.c.
+// to int64; every SUM (pulled row mass, dangling mass, residual, seed total) is an integer sum,
+// so the result does not depend on the summation order, on atomics or on the number of GPUs,
+// and is bit-identical to oracle/krca_oracle.c.
 //
 // Sharding: rank g of G owns the contiguous node range [g*n_max, ...) and the
 // pull-CSR rows of those nodes.  Each iteration ends with ONE exchange: every rank's slice
-// [w_local (n_max int64) | residual | dangling mass | seed total] is all-gathered (RCCL over
-// xGMI, driven by the host: krca/rca.py) into w_all[G][n_max+3]; the column indices are
-// pre-remapped to that layout (col' = j + 3*(j / n_max)), so the SpMV gathers directly.
-// G = 1 is the same code with no collective (krca_ppr).
+// [w_local (n_max int64) | NSLOT partial-sum slots] is all-gathered (RCCL over xGMI, driven by
+// the host: krca/rca.py) into w_all[G][n_max+NSLOT]; the column indices are pre-remapped to that
+// layout (col' = j + NSLOT*(j / n_max)), so the step kernel gathers directly.  At G = 1 the
+// "exchange" is a swap of two such buffers (ping-pong), no copy.
 //
-// SpMV (pull CSR, HBM-bound): CSR-adaptive row blocks from krca_ppr_plan —
-//   short-row blocks: <= 2048 edges and <= 256 rows; the block gathers w[col[e]] for its edge
-//                     range into LDS (coalesced col reads, lane per edge), then lane r sums row r
-//                     from LDS ("LDS-staged row segments");
-//   long rows:        split into 2048-edge chunks, each chunk block-reduced and added with one
-//                     int64 atomic (order-free integer add).
+// One iteration = ppr_step (pull SpMV fused with the rank update) + ppr_reduce (one block).
+//   ppr_step, short-row blocks (<= 2048 edges, <= 256 rows, from krca_ppr_plan): coalesced col
+//     loads and 8 independent w[col] gathers per lane (lane-strided), staged in LDS; each lane
+//     then sums 8 CONTIGUOUS staged edges as row segments (binary search of its first row in the
+//     LDS row offsets, int64 LDS atomics at row boundaries), so a 1800-edge hub row costs no more
+//     than 1800 one-edge rows; lane r then updates row r (teleport, residual, next w).
+//   ppr_step, long rows (> 2048 edges): 2048-edge chunks, block sum, one agent-scope int64 atomic
+//     into the row's accumulator and a per-row ticket; the last chunk to arrive updates the row.
+//   Residual / dangling mass: one int64 atomic per block into NSPREAD slots of the send tail, so
+//     the partial sums ride the same all-gather; ppr_reduce sums G*NSPREAD slots.
 #include <vector>
 
 #include "krca_common.h"
@@ -33,72 +37,45 @@
 namespace {
 
 constexpr int TPB = 256;
-constexpr int EDGE_BUDGET = 2048;  // edges per short block == LDS slots
-constexpr int ROW_BUDGET = TPB;    // rows per short block
-constexpr int NSLOT = 3;           // residual, dangling, seed total
+constexpr int EDGE_BUDGET = 2048;       // edges per short block == LDS slots
+constexpr int ROW_BUDGET = TPB;         // rows per short block (one updating lane per row)
+constexpr int SEG = EDGE_BUDGET / TPB;  // edges per lane: gathered lane-strided, summed contiguous
+constexpr int NSPREAD = 32;             // partial-sum slots per quantity (spreads the atomics)
+constexpr int NSLOT = 3 * NSPREAD;      // send tail: residual[32] | dangling[32] | seed total[32]
 
-struct Ctl {        // device control block
-  double tele;      // (1-alpha)*2^60 + alpha*D   for the next update
-  int64_t q_total;  // sum of quantised seeds over all ranks
+struct Ctl {          // device control block (header of the ctl buffer)
+  double tele;        // (1-alpha)*2^60 + alpha*D   for the next step
+  int64_t q_total;    // sum of quantised seeds over all ranks
   int32_t converged;  // iteration count at convergence (0 = running)
   int32_t iter;       // iterations done
-  uint32_t ticket;    // arrival counter of the last-block reduction (0 between kernels)
 };
-constexpr int MAX_BLOCKS = 2048;  // grid cap of the node-parallel kernels (partials array size)
-constexpr int CTL_BYTES = 256;    // Ctl, then int64 partials[2 * MAX_BLOCKS]
+// ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n].  The long-row
+// accumulators and tickets are zero when allocated and reset by the last chunk of each row.
+constexpr int CTL_BYTES = 256;
 
-__device__ __forceinline__ int64_t* partials(Ctl* ctl) {
+__device__ __forceinline__ int64_t* acc_long_of(Ctl* ctl) {
   return reinterpret_cast<int64_t*>(reinterpret_cast<char*>(ctl) + CTL_BYTES);
+}
+__device__ __forceinline__ uint32_t* ticket_of(Ctl* ctl, int64_t n) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctl) + CTL_BYTES + 8 * n);
 }
 
 __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
   for (int off = 32; off > 0; off >>= 1) v += (int64_t)__shfl_xor((long long)v, off, 64);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();  // red may still be read by a previous call
   if (lane == 0) red[wid] = v;
   __syncthreads();
   int64_t s = 0;
   if (threadIdx.x == 0)
-    for (int w = 0; w < TPB / 64; ++w) s += red[w];
-  __syncthreads();
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
   return s;  // valid in thread 0
 }
 
-__device__ __forceinline__ void add_slot(int64_t* slot, int64_t v) {
-  atomicAdd(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)v);
-}
-
-// Two block sums (a, b) reduced over the grid without contended atomics and without an L2
-// write-back per block: lane 0 stores the block's pair write-through (relaxed agent-scope atomic
-// store = global_store ... sc1, straight to memory), drains it (vmcnt(0)) and arrives on ONE
-// ticket; the last arriver reads every pair with agent-scope atomic loads (sc1: bypass the
-// non-coherent L1/L2 copies) and stores the totals (cdna_hip_programming.md split-K recipe,
-// write-through form; integer sums are order-free anyway).
-__device__ void grid_sum2(int64_t a, int64_t b, Ctl* ctl, int64_t* out, int64_t* red) {
-  __shared__ int is_last;
-  a = block_sum_i64(a, red);
-  b = block_sum_i64(b, red);
-  int64_t* part = partials(ctl);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&part[2 * blockIdx.x], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&part[2 * blockIdx.x + 1], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (t == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!is_last) return;
-  int64_t sa = 0, sb = 0;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += TPB) {
-    sa += __hip_atomic_load(&part[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sb += __hip_atomic_load(&part[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  sa = block_sum_i64(sa, red);
-  sb = block_sum_i64(sb, red);
-  if (threadIdx.x == 0) {
-    out[0] = sa;
-    out[1] = sb;
-    ctl->ticket = 0;
-  }
+// one int64 atomic per block into one of NSPREAD slots (integer: order-free)
+__device__ __forceinline__ void add_slot(int64_t* slots, int64_t v) {
+  if (v)
+    atomicAdd(reinterpret_cast<unsigned long long*>(slots + (blockIdx.x & (NSPREAD - 1))), (unsigned long long)v);
 }
 
 // w_j for node j given its fixed-point rank rj
@@ -113,11 +90,11 @@ __device__ __forceinline__ int64_t quantise(float s, float floor_) {
   return v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
 }
 
-// r0 = floor(2^60/N), w0, seeds, partial slots (dangling mass, seed total)
+// r0 = floor(2^60/N), w0, seeds; dangling mass and seed total into the send slots
 __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, float seed_floor,
                                                 const int32_t* __restrict__ outdeg, int64_t n, int64_t N,
                                                 double alpha, int64_t* __restrict__ q, int64_t* __restrict__ r,
-                                                int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
+                                                int64_t* __restrict__ send, int64_t n_max) {
   __shared__ int64_t red[TPB / 64];
   const int64_t r0 = (int64_t)(krca::kFix / (double)N);
   int64_t dang = 0, qs = 0;
@@ -130,16 +107,52 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
     send[i] = edge_weight(r0, deg, alpha);
     if (deg == 0) dang += r0;
   }
-  grid_sum2(dang, qs, ctl, send + n_max + 1, red);
+  dang = block_sum_i64(dang, red);
+  qs = block_sum_i64(qs, red);
+  if (threadIdx.x == 0) {
+    add_slot(send + n_max + NSPREAD, dang);
+    add_slot(send + n_max + 2 * NSPREAD, qs);
+  }
 }
 
-__global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+struct StepScalars {
+  double tele, qtot, uni, alpha;
+  int64_t qt;
+};
+
+// r_i <- pulled mass + teleport share; next w_i; residual and dangling contributions
+__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, const StepScalars& k,
+                                           const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
+                                           int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t& err,
+                                           int64_t& dang) {
+  const double pd = k.qt > 0 ? (double)q[i] / k.qtot : k.uni;
+  const int64_t t = (int64_t)(pd * k.tele);
+  const int64_t rn = pulled + t;
+  const int64_t ro = r[i];
+  r[i] = rn;
+  err += rn > ro ? rn - ro : ro - rn;
+  const int32_t deg = outdeg[i];
+  if (deg == 0) dang += rn;
+  send[i] = edge_weight(rn, deg, k.alpha);
+}
+
+__global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                                                 const int32_t* __restrict__ plan, const int64_t* __restrict__ w,
-                                                int64_t* __restrict__ acc, const Ctl* __restrict__ ctl) {
-  constexpr int K = EDGE_BUDGET / TPB;  // edges per lane: all col loads, then all gathers, in flight
-  __shared__ int64_t lds[EDGE_BUDGET];
+                                                const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
+                                                int64_t n, int64_t N, double alpha, int64_t* __restrict__ r,
+                                                int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
+  __shared__ int64_t vals[EDGE_BUDGET];
+  __shared__ unsigned long long rowsum[ROW_BUDGET];
+  __shared__ int32_t roff[ROW_BUDGET + 1];
   __shared__ int64_t red[TPB / 64];
   if (ctl->converged) return;
+  StepScalars k;
+  k.tele = ctl->tele;
+  k.qt = ctl->q_total;
+  k.qtot = (double)k.qt;
+  k.uni = 1.0 / (double)N;
+  k.alpha = alpha;
+  const int tid = threadIdx.x;
   const int32_t rb = plan[2 * blockIdx.x];
   const int32_t code = plan[2 * blockIdx.x + 1];
   int64_t e0, e1;
@@ -150,79 +163,102 @@ __global__ __launch_bounds__(TPB) void ppr_spmv(const int64_t* __restrict__ row_
     e0 = row_ptr[rb] + (int64_t)(-code) * EDGE_BUDGET;
     e1 = std::min<int64_t>(row_ptr[rb + 1], e0 + EDGE_BUDGET);
   }
-  int32_t c[K];
-  int64_t v[K];
+  // all col loads, then all gathers, in flight (lane-strided: fully coalesced col reads)
+  int32_t c[SEG];
+  int64_t v[SEG];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int64_t e = e0 + threadIdx.x + k * TPB;
-    c[k] = e < e1 ? col[e] : -1;
+  for (int j = 0; j < SEG; ++j) {
+    const int64_t e = e0 + tid + j * TPB;
+    c[j] = e < e1 ? col[e] : -1;
   }
 #pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = c[k] >= 0 ? w[c[k]] : 0;
-  if (code > 0) {  // short rows [rb, code): stage the gathered segment in LDS, lane r sums row r
+  for (int j = 0; j < SEG; ++j) v[j] = c[j] >= 0 ? w[c[j]] : 0;
+  int64_t err = 0, dang = 0;
+  if (code > 0) {
+    const int nrows = code - rb;
+    const int ne = (int)(e1 - e0);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int64_t e = threadIdx.x + k * TPB;
-      if (e0 + e < e1) lds[e] = v[k];
+    for (int j = 0; j < SEG; ++j) {
+      const int e = tid + j * TPB;
+      if (e < ne) vals[e] = v[j];
+    }
+    if (tid < nrows) roff[tid] = (int32_t)(row_ptr[rb + tid] - e0);
+    if (tid == 0) roff[nrows] = ne;
+    rowsum[tid] = 0ull;
+    __syncthreads();
+    const int a = tid * SEG;
+    if (a < ne) {  // this lane's contiguous edges [a, b) as row segments
+      const int b = min(a + SEG, ne);
+      int lo = 0, hi = nrows;  // roff[lo] <= a < roff[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (roff[mid] <= a) lo = mid;
+        else hi = mid;
+      }
+      int row = lo;
+      int end = roff[row + 1];
+      int64_t s = 0;
+      for (int e = a; e < b; ++e) {
+        while (e >= end) {
+          if (s) atomicAdd(&rowsum[row], (unsigned long long)s);
+          s = 0;
+          ++row;
+          end = roff[row + 1];
+        }
+        s += vals[e];
+      }
+      if (s) atomicAdd(&rowsum[row], (unsigned long long)s);
     }
     __syncthreads();
-    const int32_t row = rb + (int32_t)threadIdx.x;
-    if (row < code) {
-      const int64_t a = row_ptr[row] - e0, b = row_ptr[row + 1] - e0;
-      int64_t s = 0;
-      for (int64_t e = a; e < b; ++e) s += lds[e];
-      acc[row] = s;
-    }
-  } else {  // chunk of long row rb (acc[rb] was zeroed by the previous update)
+    if (tid < nrows) update_row(rb + tid, (int64_t)rowsum[tid], k, outdeg, q, r, send, err, dang);
+  } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
     int64_t s = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) s += v[k];
+    for (int j = 0; j < SEG; ++j) s += v[j];
     const int64_t tot = block_sum_i64(s, red);
-    if (threadIdx.x == 0) add_slot(&acc[rb], tot);
+    if (tid == 0) {
+      const int64_t deg_in = row_ptr[rb + 1] - row_ptr[rb];
+      const uint32_t nch = (uint32_t)((deg_in + EDGE_BUDGET - 1) / EDGE_BUDGET);
+      int64_t* acc = acc_long_of(ctl) + rb;
+      uint32_t* tk = ticket_of(ctl, n) + rb;
+      __hip_atomic_fetch_add(acc, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the add is performed before the ticket
+      const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == nch - 1) {
+        const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        update_row(rb, pulled, k, outdeg, q, r, send, err, dang);
+      }
+    }
+  }
+  err = block_sum_i64(err, red);
+  dang = block_sum_i64(dang, red);
+  if (tid == 0) {
+    add_slot(send + n_max, err);
+    add_slot(send + n_max + NSPREAD, dang);
   }
 }
 
-__global__ __launch_bounds__(TPB) void ppr_update(const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
-                                                  int64_t n, int64_t N, double alpha, int64_t* __restrict__ r,
-                                                  int64_t* __restrict__ acc, int64_t* __restrict__ send,
-                                                  int64_t n_max, Ctl* ctl) {
+// one block: sum the G*NSPREAD gathered slots of each quantity (integer -> order-free), decide
+// convergence, set the teleport scale of the next step, zero the next write target's slots
+__global__ __launch_bounds__(TPB) void ppr_reduce(const int64_t* __restrict__ w_all, int32_t G, int64_t n_max,
+                                                  double alpha, double err_limit, int first, Ctl* ctl,
+                                                  int64_t* __restrict__ send_next) {
   __shared__ int64_t red[TPB / 64];
-  if (ctl->converged) return;
-  const double tele = ctl->tele;
-  const int64_t qt = ctl->q_total;
-  const double qtot = (double)qt;
-  const double uni = 1.0 / (double)N;
-  int64_t err = 0, dang = 0;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
-    const double pd = qt > 0 ? (double)q[i] / qtot : uni;
-    const int64_t t = (int64_t)(pd * tele);
-    const int64_t rn = acc[i] + t;
-    acc[i] = 0;
-    const int64_t ro = r[i];
-    r[i] = rn;
-    err += rn > ro ? rn - ro : ro - rn;
-    const int32_t deg = outdeg[i];
-    if (deg == 0) dang += rn;
-    send[i] = edge_weight(rn, deg, alpha);
+  int64_t part[3] = {0, 0, 0};
+  for (int i = threadIdx.x; i < G * NSPREAD; i += TPB) {
+    const int64_t* s = w_all + (int64_t)(i / NSPREAD) * (n_max + NSLOT) + n_max + (i % NSPREAD);
+    part[0] += s[0];
+    part[1] += s[NSPREAD];
+    part[2] += s[2 * NSPREAD];
   }
-  grid_sum2(err, dang, ctl, send + n_max, red);
-}
-
-// one lane: sum the G gathered partial slots (integer -> order-free), decide convergence,
-// set the teleport scale of the next update, zero this rank's send slots
-__global__ void ppr_reduce(const int64_t* __restrict__ w_all, int32_t G, int64_t n_max, double alpha,
-                           double err_limit, int first, Ctl* ctl, int64_t* __restrict__ send) {
-  int64_t err = 0, dang = 0, qs = 0;
-  for (int g = 0; g < G; ++g) {
-    const int64_t* s = w_all + (int64_t)g * (n_max + NSLOT) + n_max;
-    err += s[0];
-    dang += s[1];
-    qs += s[2];
-  }
-  send[n_max] = 0;
-  send[n_max + 1] = 0;
-  send[n_max + 2] = 0;
-  if (ctl->converged) return;
+  const int64_t err = block_sum_i64(part[0], red);
+  const int64_t dang = block_sum_i64(part[1], red);
+  const int64_t qs = block_sum_i64(part[2], red);
+  __syncthreads();
+  if (threadIdx.x < NSLOT) send_next[n_max + threadIdx.x] = 0;
+  if (threadIdx.x != 0 || ctl->converged) return;
   if (first) {
     ctl->q_total = qs;
   } else {
@@ -287,13 +323,15 @@ int64_t build_plan(const int64_t* rp, int64_t N, int32_t* out) {
   return n;
 }
 
-unsigned grid_for(int64_t n) {
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), MAX_BLOCKS));
+unsigned grid_for(int64_t n, int64_t cap = 2048) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), cap));
 }
 
 }  // namespace
 
 extern "C" {
+
+int32_t krca_ppr_nslot(void) { return NSLOT; }
 
 int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N) {
   if (!row_ptr_host || N <= 0) return 0;
@@ -310,13 +348,13 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, in
   return KRCA_OK;
 }
 
-int64_t krca_ppr_ctl_size(void) { return CTL_BYTES + 16 * MAX_BLOCKS; }
+int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 16 * std::max<int64_t>(n_local, 1); }
 
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream) {
   KRCA_CHECK_ARG(E >= 0 && n_max > 0, "krca_ppr_remap_cols: bad sizes");
   if (E == 0) return KRCA_OK;
   KRCA_CHECK_ARG(col && out, "krca_ppr_remap_cols: null pointer");
-  hipLaunchKernelGGL(remap_cols, dim3(grid_for(E)), dim3(TPB), 0, krca::as_stream(stream), col, E, n_max, out);
+  hipLaunchKernelGGL(remap_cols, dim3(grid_for(E, 8192)), dim3(TPB), 0, krca::as_stream(stream), col, E, n_max, out);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -329,41 +367,38 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
   KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)), "krca_ppr_shard_init: null pointer");
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
-  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));  // residual slot stays 0
-  hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N, alpha,
-                     q_local, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
+  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
+  if (n_local > 0)
+    hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N,
+                       alpha, q_local, r_local, send, n_max);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
 
-int krca_ppr_shard_spmv(const int64_t* row_ptr, const int32_t* col, const int32_t* plan, int64_t plan_len,
-                        const int64_t* w_all, int64_t* acc, const void* ctl, void* stream) {
-  KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 2 == 0, "krca_ppr_shard_spmv: bad plan");
+int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int32_t* plan, int64_t plan_len,
+                        const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
+                        int64_t n_max, int64_t N, double alpha, int64_t* r_local, int64_t* send, void* ctl,
+                        void* stream) {
+  KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 2 == 0 && n_local >= 0 && n_local <= n_max && N > 0,
+                 "krca_ppr_shard_step: bad sizes");
   if (plan_len == 0) return KRCA_OK;
-  KRCA_CHECK_ARG(row_ptr && col && plan && w_all && acc && ctl, "krca_ppr_shard_spmv: null pointer");
-  hipLaunchKernelGGL(ppr_spmv, dim3((unsigned)(plan_len / 2)), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col,
-                     plan, w_all, acc, reinterpret_cast<const Ctl*>(ctl));
-  KRCA_LAUNCH_CHECK();
-  return KRCA_OK;
-}
-
-int krca_ppr_shard_update(const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N,
-                          double alpha, int64_t* r_local, int64_t* acc, int64_t* send, void* ctl, void* stream) {
-  KRCA_CHECK_ARG(n_local >= 0 && n_local <= n_max && N > 0, "krca_ppr_shard_update: bad sizes");
-  KRCA_CHECK_ARG(send && ctl && (n_local == 0 || (outdeg && q_local && r_local && acc)), "krca_ppr_shard_update: null pointer");
-  hipLaunchKernelGGL(ppr_update, dim3(grid_for(n_local)), dim3(TPB), 0, krca::as_stream(stream), outdeg, q_local,
-                     n_local, N, alpha, r_local, acc, send, n_max, reinterpret_cast<Ctl*>(ctl));
+  KRCA_CHECK_ARG(row_ptr && col && plan && w_all && outdeg && q_local && r_local && send && ctl,
+                 "krca_ppr_shard_step: null pointer");
+  KRCA_CHECK_ARG(w_all != send, "krca_ppr_shard_step: w_all and send must be distinct buffers (ping-pong)");
+  hipLaunchKernelGGL(ppr_step, dim3((unsigned)(plan_len / 2)), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col,
+                     plan, w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
+                     reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
 
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha, double tol,
-                          int32_t first, void* ctl, int64_t* send, void* stream) {
+                          int32_t first, void* ctl, int64_t* send_next, void* stream) {
   KRCA_CHECK_ARG(G >= 1 && n_max > 0 && N > 0, "krca_ppr_shard_reduce: bad sizes");
-  KRCA_CHECK_ARG(w_all && ctl && send, "krca_ppr_shard_reduce: null pointer");
+  KRCA_CHECK_ARG(w_all && ctl && send_next, "krca_ppr_shard_reduce: null pointer");
   const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
-  hipLaunchKernelGGL(ppr_reduce, dim3(1), dim3(1), 0, krca::as_stream(stream), w_all, G, n_max, alpha, err_limit,
-                     (int)first, reinterpret_cast<Ctl*>(ctl), send);
+  hipLaunchKernelGGL(ppr_reduce, dim3(1), dim3(TPB), 0, krca::as_stream(stream), w_all, G, n_max, alpha, err_limit,
+                     (int)first, reinterpret_cast<Ctl*>(ctl), send_next);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -395,8 +430,10 @@ int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key
   return KRCA_OK;
 }
 
-// workspace: ctl (krca_ppr_ctl_size) | q[N] | acc[N] | send/w_all[N+3] | r (if r_fixed == NULL) [N]
-int64_t krca_ppr_workspace_size(int64_t N) { return krca_ppr_ctl_size() + (4 * N + NSLOT) * 8 + 256; }
+// workspace: ctl (krca_ppr_ctl_size(N), zeroed here once) | q[N] | w0[N+NSLOT] | w1[N+NSLOT] | r[N]
+int64_t krca_ppr_workspace_size(int64_t N) {
+  return krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256 + (4 * N + 2 * NSLOT) * 8 + 256;
+}
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int32_t* plan,
              int64_t plan_len, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
@@ -406,22 +443,25 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   KRCA_CHECK_ARG(plan_len > 0 && plan_len % 2 == 0, "krca_ppr: bad plan");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0 && max_iter > 0, "krca_ppr: alpha in (0,1), max_iter > 0");
   char* ctl = reinterpret_cast<char*>(workspace);
-  char* p = ctl + krca_ppr_ctl_size();
+  const int64_t ctl_bytes = krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256;
+  char* p = ctl + ctl_bytes;
   int64_t* q = q_out ? q_out : reinterpret_cast<int64_t*>(p);
-  int64_t* acc = reinterpret_cast<int64_t*>(p + N * 8);
-  int64_t* w = reinterpret_cast<int64_t*>(p + 2 * N * 8);
-  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + (3 * N + NSLOT) * 8);
+  int64_t* wb[2] = {reinterpret_cast<int64_t*>(p + N * 8), reinterpret_cast<int64_t*>(p + (2 * N + NSLOT) * 8)};
+  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + (3 * N + 2 * NSLOT) * 8);
   hipStream_t st = krca::as_stream(stream);
-  KRCA_HIP(hipMemsetAsync(acc, 0, N * 8, st));
-  int rc = krca_ppr_shard_init(seed, seed_floor, outdeg, N, N, N, alpha, ctl, q, r, w, stream);
+  KRCA_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
+  int rc = krca_ppr_shard_init(seed, seed_floor, outdeg, N, N, N, alpha, ctl, q, r, wb[0], stream);
   if (rc) return rc;
-  if ((rc = krca_ppr_shard_reduce(w, 1, N, N, alpha, tol, 1, ctl, w, stream))) return rc;
+  if ((rc = krca_ppr_shard_reduce(wb[0], 1, N, N, alpha, tol, 1, ctl, wb[1], stream))) return rc;
   const int check_every = 8;
   int32_t iters = 0, conv = 0;
+  int cur = 0;  // w buffer the next step gathers from
   for (int it = 0; it < max_iter; ++it) {
-    if ((rc = krca_ppr_shard_spmv(row_ptr, col, plan, plan_len, w, acc, ctl, stream))) return rc;
-    if ((rc = krca_ppr_shard_update(outdeg, q, N, N, N, alpha, r, acc, w, ctl, stream))) return rc;
-    if ((rc = krca_ppr_shard_reduce(w, 1, N, N, alpha, tol, 0, ctl, w, stream))) return rc;
+    if ((rc = krca_ppr_shard_step(row_ptr, col, plan, plan_len, wb[cur], outdeg, q, N, N, N, alpha, r, wb[cur ^ 1],
+                                  ctl, stream)))
+      return rc;
+    cur ^= 1;
+    if ((rc = krca_ppr_shard_reduce(wb[cur], 1, N, N, alpha, tol, 0, ctl, wb[cur ^ 1], stream))) return rc;
     if (tol > 0.0 && (it + 1) % check_every == 0 && it + 1 < max_iter) {
       if ((rc = krca_ppr_ctl_read(ctl, &iters, &conv, stream))) return rc;
       if (conv) break;

@@ -189,6 +189,93 @@ __global__ __launch_bounds__(256) void rolling_score_ring_buf(const float* __res
   pod_epilogue(st, epsB, s, active, M, T, x + (active ? s : 0), S, z_last, score, n_exceed, flags);
 }
 
+// Software-pipelined form of rolling_score_ring_buf (same arithmetic, same bits).  The time axis
+// is walked in C-row chunks (W % C == 0, so every ring slot index stays static); the loads of
+// chunk c+1 are issued before chunk c is computed, so each wave keeps C rows (C*256 B) in flight
+// through its whole compute phase instead of alternating load bursts and VALU bursts.  Only the
+// final block (the one holding t = T-1) tracks the last-step A/B, so the steady-state loop has
+// no per-sample select.  Buffer descriptors cover exactly the rows < T of a chunk: loads past the
+// end return 0 and touch no memory, which lets the prefetch run ahead unconditionally.
+template <int C>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float* x, int64_t S, uint32_t rowb, int t,
+                                                             int T) {
+  int n = T - t;
+  n = n < 0 ? 0 : (n > C ? C : n);
+  n = __builtin_amdgcn_readfirstlane(n);  // wave-uniform: keeps the descriptor in SGPRs (no v_med3 waterfall)
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)(n ? t : 0) * S), 0, (int)(rowb * (uint32_t)n),
+                                           0x00020000);
+}
+
+template <int W, int C>
+__global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restrict__ x, int64_t S, int T, int M,
+                                                          double thr2, float* __restrict__ z_last,
+                                                          float* __restrict__ score, int32_t* __restrict__ n_exceed,
+                                                          uint8_t* __restrict__ flags) {
+  static_assert(W % C == 0, "chunk must divide the window");
+  constexpr int NC = W / C;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = s < S;
+  const uint32_t voff = active ? (uint32_t)s * 4u : 0u;
+  const uint32_t rowb = (uint32_t)(S * 4);
+  const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
+  StepState st{0.0, 0.0, 0, 0.0, 0.0};
+  float ring[W];
+  float cur[C];
+  // prologue: rows [0, W) fill the window (requires T > W, checked by the launcher)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, c * C, T);
+#pragma unroll
+    for (int j = 0; j < C; ++j) ring[c * C + j] = bload(rs, voff, rowb * j);
+  }
+  {
+    const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, W, T);
+#pragma unroll
+    for (int j = 0; j < C; ++j) cur[j] = bload(rs, voff, rowb * j);
+  }
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const double vd = (double)ring[j];
+    st.s1 = st.s1 + vd;
+    st.s2 = fma(vd, vd, st.s2);
+  }
+  int t0 = W;
+  for (; t0 + W < T; t0 += W) {  // full blocks that do not contain t = T-1
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float nxt[C];
+      const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t0 + (c + 1) * C, T);
+#pragma unroll
+      for (int j = 0; j < C; ++j) nxt[j] = bload(rs, voff, rowb * j);
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        step(st, cur[j], ring[c * C + j], Wd, epsB, thr2, false);
+        ring[c * C + j] = cur[j];
+      }
+#pragma unroll
+      for (int j = 0; j < C; ++j) cur[j] = nxt[j];
+    }
+  }
+  // final block: rows [t0, T), 1..W of them; cur already holds rows [t0, t0 + C)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c > 0) {
+      const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t0 + c * C, T);
+#pragma unroll
+      for (int j = 0; j < C; ++j) cur[j] = bload(rs, voff, rowb * j);
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int t = t0 + c * C + j;
+      if (t < T) {
+        step(st, cur[j], ring[c * C + j], Wd, epsB, thr2, t == T - 1);
+        ring[c * C + j] = cur[j];
+      }
+    }
+  }
+  pod_epilogue(st, epsB, s, active, M, T, x + (active ? s : 0), S, z_last, score, n_exceed, flags);
+}
+
 // Any W: the outgoing sample x[t-W] is re-read (same values, same arithmetic -> same bits).
 __global__ __launch_bounds__(256) void rolling_score_reread(const float* __restrict__ x, int64_t S, int T, int W,
                                                             int M, double thr2, float* __restrict__ z_last,
@@ -238,31 +325,56 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
   const double thr2 = (double)z_thr * (double)z_thr;
   const dim3 grid((unsigned)krca::ceil_div(S, 256)), block(256);
   hipStream_t st = krca::as_stream(stream);
-  static const int impl = [] {  // A/B switch for kernel development (0 = default)
-    const char* e = getenv("KRCA_SCORE_IMPL");
-    return e ? atoi(e) : 0;
-  }();
+  // A/B switches for kernel development, read per call (0 / 20 = default)
+  const char* e_impl = getenv("KRCA_SCORE_IMPL");
+  const char* e_chunk = getenv("KRCA_SCORE_CHUNK");
+  const int impl = e_impl ? atoi(e_impl) : 0;
+  const int chunk = e_chunk ? atoi(e_chunk) : 20;
   KRCA_CHECK_ARG(S < (int64_t(1) << 32), "krca_rolling_score: P*M must be < 2^32");
+  // impl 0: pipelined chunks (needs T > W and C*4*S < 2^31); 1: plain loads; 2: W-block buffer loads
+  const int cw = W == 60 ? chunk : (W == 30 ? 15 : (W == 20 ? 10 : W));  // rows per pipelined chunk
+  const bool fits = T > W && S * 4 * cw < (int64_t(1) << 31);
+#define KRCA_PIPE(WV, CV) \
+  hipLaunchKernelGGL((rolling_score_pipe<WV, CV>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed, flags)
+#define KRCA_RING(WV)                                                                                         \
+  if (impl == 2 && S * 4 * WV < (int64_t(1) << 31))                                                           \
+    hipLaunchKernelGGL(rolling_score_ring_buf<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score,        \
+                       n_exceed, flags);                                                                       \
+  else                                                                                                         \
+    hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed,  \
+                       flags);
+  const bool pipe = impl == 0 && fits;
   switch (W) {
-#define KRCA_W(WV)                                                                                       \
-  case WV:                                                                                               \
-    if (impl == 0 && S * 4 * WV < (int64_t(1) << 31))                                                    \
-      hipLaunchKernelGGL(rolling_score_ring_buf<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
-                         n_exceed, flags);                                                              \
-    else                                                                                                 \
-      hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score,   \
-                         n_exceed, flags);                                                              \
-    break;
-    KRCA_W(10)
-    KRCA_W(15)
-    KRCA_W(20)
-    KRCA_W(30)
-    KRCA_W(60)
-#undef KRCA_W
+    case 60:
+      if (pipe && chunk == 10) KRCA_PIPE(60, 10);
+      else if (pipe && chunk == 12) KRCA_PIPE(60, 12);
+      else if (pipe && chunk == 15) KRCA_PIPE(60, 15);
+      else if (pipe && chunk == 30) KRCA_PIPE(60, 30);
+      else if (pipe) KRCA_PIPE(60, 20);
+      else { KRCA_RING(60) }
+      break;
+    case 30:
+      if (pipe) KRCA_PIPE(30, 15);
+      else { KRCA_RING(30) }
+      break;
+    case 20:
+      if (pipe) KRCA_PIPE(20, 10);
+      else { KRCA_RING(20) }
+      break;
+    case 15:
+      if (pipe) KRCA_PIPE(15, 15);
+      else { KRCA_RING(15) }
+      break;
+    case 10:
+      if (pipe) KRCA_PIPE(10, 10);
+      else { KRCA_RING(10) }
+      break;
     default:
       hipLaunchKernelGGL(rolling_score_reread, grid, block, 0, st, x, S, T, W, M, thr2, z_last, score, n_exceed,
                          flags);
   }
+#undef KRCA_PIPE
+#undef KRCA_RING
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

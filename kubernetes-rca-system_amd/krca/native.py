@@ -44,11 +44,12 @@ SIGNATURES = {
     "krca_ppr_workspace_size": (c_i64, [c_i64]),
     "krca_ppr": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_f64, c_i32, c_f64, c_vp, c_vp, c_vp,
                          c_vp, ctypes.POINTER(c_i32), c_vp]),
-    "krca_ppr_ctl_size": (c_i64, []),
+    "krca_ppr_nslot": (c_i32, []),
+    "krca_ppr_ctl_size": (c_i64, [c_i64]),
     "krca_ppr_remap_cols": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "krca_ppr_shard_init": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "krca_ppr_shard_spmv": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
-    "krca_ppr_shard_update": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_step": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp,
+                                    c_vp, c_vp]),
     "krca_ppr_shard_reduce": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp]),
     "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),

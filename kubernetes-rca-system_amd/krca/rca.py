@@ -3,16 +3,17 @@
 This is the north-star path (BASELINE.json): for a pod mesh of N pods with M metrics x T steps
 and a caller -> dependency graph, one step scores every pod (krca_rolling_score), seeds a
 personalized PageRank with the anomalous pods (p_i ∝ max(score_i - seed_floor, 0)), propagates
-for a fixed number of iterations (krca_ppr_shard_*), and ranks pods by propagated mass x own
-anomaly (krca_ppr_rca_key + krca_topk_i64).
+for a fixed number of iterations (krca_ppr_shard_step: pull SpMV fused with the rank update),
+and ranks pods by propagated mass x own anomaly (krca_ppr_rca_key + krca_topk_i64).
 
 Multi-GPU: one process per GPU; rank g owns pods [g*n_max, (g+1)*n_max): its
 slice of the metric tensor and its rows of the pull-CSR.  Scoring needs no communication.  Each
 PageRank iteration ends with ONE all-gather over RCCL/xGMI of every rank's
-[w_local | residual | dangling | seed-total] slice (n_max + 3 int64); the partial sums ride in
-the same payload and every rank reduces them identically, so no extra collective or broadcast
-is needed.  Arithmetic is integer fixed point: the result is bit-identical for any G and to
-oracle/krca_oracle.c.  The final top-k merges G x k candidates.
+[w_local | partial-sum slots] slice (n_max + NSLOT int64: residual, dangling mass and seed total,
+NSPREAD slots each); the partial sums ride in the same payload and every rank reduces them
+identically, so no extra collective or broadcast is needed.  With one rank the exchange is a swap
+of two buffers (the step kernel reads one and writes the other).  Arithmetic is integer fixed
+point: the result is bit-identical for any G and to oracle/krca_oracle.c.  The final top-k merges G x k candidates.
 
 The per-rank numeric work is behind a small backend interface so the same orchestration runs
 on the device (:class:`DeviceShard`, libkrca) and, in the CPU test-suite, on a NumPy restatement
@@ -22,7 +23,8 @@ import math
 
 import numpy as np
 
-NSLOT = 3
+NSPREAD = 32
+NSLOT = 3 * NSPREAD  # == krca_ppr_nslot()
 
 
 def shard_range(N, world, rank):
@@ -60,6 +62,13 @@ class Comm:
     def __init__(self, world=1, rank=0, group=None):
         self.world, self.rank, self.group = world, rank, group
 
+    def exchange(self, shard):
+        """Make every rank's send slice visible in shard.w_all (G = 1: swap the ping-pong pair)."""
+        if self.world == 1:
+            shard.send, shard.w_all = shard.w_all, shard.send
+        else:
+            self.all_gather(shard.w_all, shard.send)
+
     def all_gather(self, out, inp):
         if self.world == 1:
             if out.data_ptr() != inp.data_ptr():
@@ -94,11 +103,11 @@ class DeviceShard:
         i64 = dict(dtype=torch.int64, device=dev)
         self.q = torch.zeros(max(self.n, 1), **i64)
         self.r = torch.zeros(max(self.n, 1), **i64)
-        self.acc = torch.zeros(max(self.n, 1), **i64)
         self.key = torch.zeros(max(self.n, 1), **i64)
         self.send = torch.zeros(n_max + NSLOT, **i64)
-        self.w_all = self.send if world == 1 else torch.zeros(world * (n_max + NSLOT), **i64)
-        self.ctl = torch.zeros(lib.krca_ppr_ctl_size(), dtype=torch.uint8, device=dev)
+        # G = 1: ping-pong pair (the step reads w_all, writes send; the exchange swaps them)
+        self.w_all = torch.zeros((1 if world == 1 else world) * (n_max + NSLOT), **i64)
+        self.ctl = torch.zeros(lib.krca_ppr_ctl_size(self.n), dtype=torch.uint8, device=dev)
         self.score_out = None
 
     def _chk(self, rc, what):
@@ -111,23 +120,17 @@ class DeviceShard:
 
     def init(self, alpha, seed_floor):
         e, p = self.eng, self.eng.ptr
-        self.acc.zero_()
         self._chk(e.lib.krca_ppr_shard_init(p(self.score_out["score"]), float(seed_floor), p(self.outdeg), self.n,
                                             self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
                                             p(self.send), e._stream()), "krca_ppr_shard_init")
 
-    def spmv(self):
+    def step(self, alpha):
         e, p = self.eng, self.eng.ptr
         if self.plan_len:
-            self._chk(e.lib.krca_ppr_shard_spmv(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len,
-                                                p(self.w_all), p(self.acc), p(self.ctl), e._stream()),
-                      "krca_ppr_shard_spmv")
-
-    def update(self, alpha):
-        e, p = self.eng, self.eng.ptr
-        self._chk(e.lib.krca_ppr_shard_update(p(self.outdeg), p(self.q), self.n, self.n_max, self.N, float(alpha),
-                                              p(self.r), p(self.acc), p(self.send), p(self.ctl), e._stream()),
-                  "krca_ppr_shard_update")
+            self._chk(e.lib.krca_ppr_shard_step(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len,
+                                                p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
+                                                float(alpha), p(self.r), p(self.send), p(self.ctl), e._stream()),
+                      "krca_ppr_shard_step")
 
     def reduce(self, alpha, tol, first):
         e, p = self.eng, self.eng.ptr
@@ -150,18 +153,26 @@ class RcaStep:
     def __init__(self, shard, comm, cfg, offset):
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
 
-    def run(self, to_host=True):
+    def propagate(self):
+        """Seeded PageRank on the current scores: init, exchange, then iters x (step, exchange, reduce)."""
         s, c, cfg = self.s, self.comm, self.cfg
-        s.score()
         s.init(cfg.alpha, cfg.seed_floor)
-        c.all_gather(s.w_all, s.send)
+        c.exchange(s)
         s.reduce(cfg.alpha, cfg.tol, 1)
         for _ in range(cfg.iters):
-            s.spmv()
-            s.update(cfg.alpha)
-            c.all_gather(s.w_all, s.send)
+            s.step(cfg.alpha)
+            c.exchange(s)
             s.reduce(cfg.alpha, cfg.tol, 0)
-        idx, val = s.local_topk(cfg.k)
+
+    def run(self, to_host=True, score_events=None):
+        """One RCA step; score_events = (start, end) HIP events recorded around the scoring kernel."""
+        if score_events is not None:
+            score_events[0].record()
+        self.s.score()
+        if score_events is not None:
+            score_events[1].record()
+        self.propagate()
+        idx, val = self.s.local_topk(self.cfg.k)
         return self.merge(idx, val) if to_host else (idx, val)
 
     def merge(self, idx, val):

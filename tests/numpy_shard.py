@@ -2,14 +2,16 @@
 
 Same integer/float64 expressions as csrc/ppr.hip (shard kernels) and oracle/krca_oracle.c, so
 the distributed orchestration of krca/rca.py (partitioning, column remap, one all-gather per
-iteration with the partial sums in the payload, candidate merge) can be exercised on CPU with
-the gloo backend and compared bit-for-bit with the single-process oracle.
+iteration with the partial sums in the payload, the G = 1 ping-pong swap, candidate merge) can be
+exercised on CPU with the gloo backend and compared bit-for-bit with the single-process oracle.
+Slot layout of the send tail: residual | dangling | seed total, NSPREAD slots each (the device
+spreads its atomics over them; only the sums matter).
 """
 import numpy as np
 import torch
 
 import oracle
-from krca.rca import NSLOT
+from krca.rca import NSLOT, NSPREAD
 
 FIX = 1152921504606846976.0
 
@@ -33,7 +35,7 @@ class NumpyShard:
         self.n = len(self.deg)
         self.rows = np.repeat(np.arange(self.n), np.diff(self.rp))
         self.send = torch.zeros(n_max + NSLOT, dtype=torch.int64)
-        self.w_all = self.send if world == 1 else torch.zeros(world * (n_max + NSLOT), dtype=torch.int64)
+        self.w_all = torch.zeros((1 if world == 1 else world) * (n_max + NSLOT), dtype=torch.int64)
         self.ctl = {}
 
     def score(self):
@@ -46,39 +48,34 @@ class NumpyShard:
         self.q = np.where(v > 0, (np.maximum(v, 0) * 4294967296.0).astype(np.int64), 0)
         r0 = np.int64(FIX / float(self.N))
         self.r = np.full(self.n, r0, np.int64)
-        self.acc = np.zeros(self.n, np.int64)
         snd = self.send.numpy()
-        snd[:] = 0
+        snd[self.n_max:] = 0
         snd[:self.n] = _w(self.r, self.deg, alpha)
-        snd[self.n_max + 1] = int(self.r[self.deg == 0].sum())
-        snd[self.n_max + 2] = int(self.q.sum())
+        snd[self.n_max + NSPREAD] = int(self.r[self.deg == 0].sum())
+        snd[self.n_max + 2 * NSPREAD] = int(self.q.sum())
         self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
 
-    def spmv(self):
+    def step(self, alpha):
+        """Pull SpMV fused with the update: reads w_all, writes r and send (krca_ppr_shard_step)."""
         if self.ctl["converged"]:
             return
         w = self.w_all.numpy()
-        vals = w[self.col]
-        self.acc = np.zeros(self.n, np.int64)
-        np.add.at(self.acc, self.rows, vals)
-
-    def update(self, alpha):
-        if self.ctl["converged"]:
-            return
+        acc = np.zeros(self.n, np.int64)
+        np.add.at(acc, self.rows, w[self.col])
         qt = self.ctl["q_total"]
         pd = self.q.astype(np.float64) / float(qt) if qt > 0 else np.full(self.n, 1.0 / float(self.N))
         t = (pd * self.ctl["tele"]).astype(np.int64)
-        rn = self.acc + t
+        rn = acc + t
         err = int(np.abs(rn - self.r).sum())
         self.r = rn
         snd = self.send.numpy()
         snd[:self.n] = _w(rn, self.deg, alpha)
         snd[self.n_max] += err
-        snd[self.n_max + 1] += int(rn[self.deg == 0].sum())
+        snd[self.n_max + NSPREAD] += int(rn[self.deg == 0].sum())
 
     def reduce(self, alpha, tol, first):
-        w = self.w_all.numpy().reshape(self.world, self.n_max + NSLOT)
-        err, dang, qs = (int(w[:, self.n_max + i].sum()) for i in range(NSLOT))
+        w = self.w_all.numpy().reshape(self.world, self.n_max + NSLOT)[:, self.n_max:]
+        err, dang, qs = (int(w[:, i * NSPREAD:(i + 1) * NSPREAD].sum()) for i in range(3))
         self.send.numpy()[self.n_max:] = 0
         c = self.ctl
         if c["converged"]:

@@ -32,6 +32,9 @@ def test_version_and_host_helpers():
     assert lib.krca_log_index_size(1 << 30) > lib.krca_log_index_size(1 << 20)
     assert lib.krca_topk_workspace_size(1 << 20, 10) > 0
     assert lib.krca_ppr_workspace_size(1000) >= 4 * 1000 * 8
+    from krca.rca import NSLOT
+    assert lib.krca_ppr_nslot() == NSLOT  # send-slice layout shared by the kernels and krca/rca.py
+    assert lib.krca_ppr_ctl_size(1000) >= 12 * 1000  # long-row accumulators + tickets
 
 
 def test_ppr_plan_blocks_cover_rows():

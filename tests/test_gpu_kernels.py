@@ -52,6 +52,28 @@ def test_rolling_score_vs_oracle(eng, P, M, T, W):
     assert np.allclose(z, zl, rtol=1e-5, atol=1e-5)
 
 
+SCORE_VARIANTS = [("2", "20"), ("1", "20")] + [("0", c) for c in ("10", "12", "15", "20", "30")]
+
+
+@pytest.mark.parametrize("P,M,T,W", [(1000, 8, 1440, 60), (128, 8, 61, 60), (129, 8, 139, 60), (700, 8, 200, 30)])
+def test_rolling_score_kernel_variants_bit_exact(eng, monkeypatch, P, M, T, W):
+    """Every kernel form (W-block buffer loads, plain loads, pipelined chunks) = the C oracle."""
+    x = synth.make_metrics(P, M, T, window=W, seed=P + T + 1, roots=np.arange(0, P, 9))
+    ref = oracle.c_rolling_score(x.numpy(), W, 3.0)
+    xd = x.cuda()
+    z0 = None
+    for impl, chunk in SCORE_VARIANTS:
+        monkeypatch.setenv("KRCA_SCORE_IMPL", impl)
+        monkeypatch.setenv("KRCA_SCORE_CHUNK", chunk)
+        got = eng.rolling_score(xd, window=W, z_threshold=3.0)
+        assert np.array_equal(got["n_exceed_host"], ref["n_exceed"]), (impl, chunk)
+        assert np.array_equal(got["flags"], ref["flags"]), (impl, chunk)
+        z = got["z_last"].cpu().numpy()
+        assert np.allclose(z, ref["z_last"], rtol=1e-5, atol=1e-6), (impl, chunk)
+        z0 = z if z0 is None else z0
+        assert np.array_equal(z, z0), (impl, chunk)                       # same arithmetic -> same bits
+
+
 def test_rolling_score_deterministic_and_planted_roots(eng):
     m = synth.make_graph(2000, avg_degree=10, seed=1)
     hops = synth.caller_hops(m, m.roots)
@@ -202,6 +224,45 @@ def test_rca_step_single_gpu_vs_oracle(eng, n, iters):
     idx2, _ = step.run()  # re-run on the same buffers: identical
     assert list(idx2) == list(idx)
     assert len(set(idx.tolist()) & set(m.roots.tolist())) >= 8
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_rca_sharded_path_emulated_on_one_gpu(eng, G):
+    """G pod shards on one device with the all-gather done by copies: the remapped-column /
+    slot-payload path of the multi-GPU step, bit-identical to the single-process oracle."""
+    from krca.rca import Config, DeviceShard, shard_graph, shard_range
+    n = 30000
+    m = synth.make_graph(n, avg_degree=20, seed=11)
+    hops = synth.caller_hops(m, m.roots)
+    x = synth.make_metrics(n, 8, 300, window=60, seed=3, roots=m.roots, hop_sets=hops).cuda()
+    cfg = Config(iters=15)
+    shards = []
+    for g in range(G):
+        lo, hi, n_max = shard_range(n, G, g)
+        rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
+        shards.append(DeviceShard(eng, x[:, lo:hi, :].contiguous(), rp, col, od, n, n_max, G, cfg))
+
+    def exchange():
+        wall = torch.cat([s.send for s in shards])
+        for s in shards:
+            s.w_all.copy_(wall)
+
+    for s in shards:
+        s.score()
+        s.init(cfg.alpha, cfg.seed_floor)
+    exchange()
+    for s in shards:
+        s.reduce(cfg.alpha, cfg.tol, 1)
+    for _ in range(cfg.iters):
+        for s in shards:
+            s.step(cfg.alpha)
+        exchange()
+        for s in shards:
+            s.reduce(cfg.alpha, cfg.tol, 0)
+    score = torch.cat([s.score_out["score"] for s in shards]).cpu().numpy()
+    _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+    got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
+    assert np.array_equal(got, r)
 
 
 # ---- a13 error templates -------------------------------------------------------------------
