@@ -134,10 +134,11 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
  * live there and reset themselves). */
 int32_t krca_ppr_nslot(void);
 int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N);
-int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, int64_t plan_len);
+int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host /*{rb,code,e0,e1} per block*/,
+                  int64_t plan_len);
 int64_t krca_ppr_workspace_size(int64_t N);
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
-             const int32_t* plan, int64_t plan_len, const float* seed, float seed_floor, double alpha,
+             const int64_t* plan, int64_t plan_len, const float* seed, float seed_floor, double alpha,
              int32_t max_iter, double tol, void* workspace, float* r_out, int64_t* r_fixed /*nullable*/,
              int64_t* q_out /*nullable: quantised seeds*/, int32_t* iters_host, void* stream);
 int64_t krca_ppr_ctl_size(int64_t n_local);
@@ -145,7 +146,7 @@ int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* o
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
                         int64_t* r_local, int64_t* send /*[n_max+nslot]*/, void* stream);
-int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int32_t* plan,
+int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int64_t* plan,
                         int64_t plan_len, const int64_t* w_all /*[G][n_max+nslot]*/, const int32_t* outdeg,
                         const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
                         int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);

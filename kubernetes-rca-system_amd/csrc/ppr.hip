@@ -121,23 +121,21 @@ struct StepScalars {
 };
 
 // r_i <- pulled mass + teleport share; next w_i; residual and dangling contributions
-__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, const StepScalars& k,
-                                           const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
-                                           int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t& err,
-                                           int64_t& dang) {
-  const double pd = k.qt > 0 ? (double)q[i] / k.qtot : k.uni;
+// (q_i, r_i, deg_i were loaded by the caller together with the row's edges)
+__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi, int64_t ro, int32_t deg,
+                                           const StepScalars& k, int64_t* __restrict__ r, int64_t* __restrict__ send,
+                                           int64_t& err, int64_t& dang) {
+  const double pd = k.qt > 0 ? (double)qi / k.qtot : k.uni;
   const int64_t t = (int64_t)(pd * k.tele);
   const int64_t rn = pulled + t;
-  const int64_t ro = r[i];
   r[i] = rn;
   err += rn > ro ? rn - ro : ro - rn;
-  const int32_t deg = outdeg[i];
   if (deg == 0) dang += rn;
   send[i] = edge_weight(rn, deg, k.alpha);
 }
 
 __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-                                                const int32_t* __restrict__ plan, const int64_t* __restrict__ w,
+                                                const int64_t* __restrict__ plan, const int64_t* __restrict__ w,
                                                 const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
                                                 int64_t n, int64_t N, double alpha, int64_t* __restrict__ r,
                                                 int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
@@ -145,7 +143,14 @@ __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_
   __shared__ unsigned long long rowsum[ROW_BUDGET];
   __shared__ int32_t roff[ROW_BUDGET + 1];
   __shared__ int64_t red[TPB / 64];
-  if (ctl->converged) return;
+  // The block is latency-bound (a handful of dependent memory round trips), so every load that
+  // depends only on the plan entry is issued in ONE wave of requests: col, the row offsets and
+  // the update operands (q, r, outdeg) of this lane's row, together; then the w gathers.
+  const int64_t* pe = plan + 4 * (int64_t)blockIdx.x;  // {rb, code, e0, e1}
+  const int32_t rb = (int32_t)pe[0];
+  const int32_t code = (int32_t)pe[1];
+  const int64_t e0 = pe[2], e1 = pe[3];
+  const int32_t conv = ctl->converged;  // loaded with the plan entry; tested only after the loads
   StepScalars k;
   k.tele = ctl->tele;
   k.qt = ctl->q_total;
@@ -153,17 +158,6 @@ __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_
   k.uni = 1.0 / (double)N;
   k.alpha = alpha;
   const int tid = threadIdx.x;
-  const int32_t rb = plan[2 * blockIdx.x];
-  const int32_t code = plan[2 * blockIdx.x + 1];
-  int64_t e0, e1;
-  if (code > 0) {
-    e0 = row_ptr[rb];
-    e1 = row_ptr[code];
-  } else {
-    e0 = row_ptr[rb] + (int64_t)(-code) * EDGE_BUDGET;
-    e1 = std::min<int64_t>(row_ptr[rb + 1], e0 + EDGE_BUDGET);
-  }
-  // all col loads, then all gathers, in flight (lane-strided: fully coalesced col reads)
   int32_t c[SEG];
   int64_t v[SEG];
 #pragma unroll
@@ -171,8 +165,14 @@ __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_
     const int64_t e = e0 + tid + j * TPB;
     c[j] = e < e1 ? col[e] : -1;
   }
+  const int nrows = code > 0 ? code - rb : 1;
+  const int64_t my_row = rb + (tid < nrows ? tid : 0);
+  const int64_t my_off = code > 0 && tid < nrows ? row_ptr[my_row] : 0;
+  const int64_t my_q = q[my_row], my_r = r[my_row];
+  const int32_t my_deg = outdeg[my_row];
 #pragma unroll
   for (int j = 0; j < SEG; ++j) v[j] = c[j] >= 0 ? w[c[j]] : 0;
+  if (conv) return;  // converged (tol > 0): no writes (uniform)
   int64_t err = 0, dang = 0;
   if (code > 0) {
     const int nrows = code - rb;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_
       const int e = tid + j * TPB;
       if (e < ne) vals[e] = v[j];
     }
-    if (tid < nrows) roff[tid] = (int32_t)(row_ptr[rb + tid] - e0);
+    if (tid < nrows) roff[tid] = (int32_t)(my_off - e0);
     if (tid == 0) roff[nrows] = ne;
     rowsum[tid] = 0ull;
     __syncthreads();
@@ -210,14 +210,14 @@ __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_
       if (s) atomicAdd(&rowsum[row], (unsigned long long)s);
     }
     __syncthreads();
-    if (tid < nrows) update_row(rb + tid, (int64_t)rowsum[tid], k, outdeg, q, r, send, err, dang);
+    if (tid < nrows) update_row(my_row, (int64_t)rowsum[tid], my_q, my_r, my_deg, k, r, send, err, dang);
   } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
     int64_t s = 0;
 #pragma unroll
     for (int j = 0; j < SEG; ++j) s += v[j];
     const int64_t tot = block_sum_i64(s, red);
     if (tid == 0) {
-      const int64_t deg_in = row_ptr[rb + 1] - row_ptr[rb];
+      const int64_t deg_in = row_ptr[rb + 1] - row_ptr[rb];  // (one lane, off the gather path)
       const uint32_t nch = (uint32_t)((deg_in + EDGE_BUDGET - 1) / EDGE_BUDGET);
       int64_t* acc = acc_long_of(ctl) + rb;
       uint32_t* tk = ticket_of(ctl, n) + rb;
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_
         const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        update_row(rb, pulled, k, outdeg, q, r, send, err, dang);
+        update_row(rb, pulled, my_q, my_r, my_deg, k, r, send, err, dang);
       }
     }
   }
@@ -293,31 +293,34 @@ __global__ __launch_bounds__(TPB) void remap_cols(const int32_t* __restrict__ co
   }
 }
 
-// host: CSR-adaptive row blocks; returns the number of int32 entries (2 per block)
-int64_t build_plan(const int64_t* rp, int64_t N, int32_t* out) {
+// host: CSR-adaptive row blocks {rb, code, e0, e1} (code > 0: short rows [rb, code); code <= 0:
+// chunk -code of long row rb); returns the number of int64 entries (4 per block)
+int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out) {
   int64_t n = 0;
   int64_t r = 0;
+  auto put = [&](int64_t rb, int64_t code, int64_t e0, int64_t e1) {
+    if (out) {
+      out[n] = rb;
+      out[n + 1] = code;
+      out[n + 2] = e0;
+      out[n + 3] = e1;
+    }
+    n += 4;
+  };
   while (r < N) {
     const int64_t deg = rp[r + 1] - rp[r];
     if (deg > EDGE_BUDGET) {
       const int64_t chunks = krca::ceil_div(deg, EDGE_BUDGET);
       for (int64_t c = 0; c < chunks; ++c) {
-        if (out) {
-          out[n] = (int32_t)r;
-          out[n + 1] = (int32_t)(-c);  // chunk 0 encodes as 0 (<= 0 means long-row chunk)
-        }
-        n += 2;
+        const int64_t e0 = rp[r] + c * EDGE_BUDGET;
+        put(r, -c, e0, std::min<int64_t>(rp[r + 1], e0 + EDGE_BUDGET));  // chunk 0 encodes as 0
       }
       r += 1;
       continue;
     }
     int64_t re = r + 1;
     while (re < N && re - r < ROW_BUDGET && rp[re + 1] - rp[r] <= EDGE_BUDGET) ++re;
-    if (out) {
-      out[n] = (int32_t)r;
-      out[n + 1] = (int32_t)re;
-    }
-    n += 2;
+    put(r, re, rp[r], rp[re]);
     r = re;
   }
   return n;
@@ -338,7 +341,7 @@ int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N) {
   return build_plan(row_ptr_host, N, nullptr);
 }
 
-int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int32_t* plan_host, int64_t plan_len) {
+int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host, int64_t plan_len) {
   KRCA_CHECK_ARG(row_ptr_host && plan_host && N > 0 && N < INT32_MAX, "krca_ppr_plan: bad arguments");
   for (int64_t i = 0; i < N; ++i)
     KRCA_CHECK_ARG(row_ptr_host[i + 1] >= row_ptr_host[i], "krca_ppr_plan: row_ptr not monotone at %lld", (long long)i);
@@ -375,17 +378,17 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
   return KRCA_OK;
 }
 
-int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int32_t* plan, int64_t plan_len,
+int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
                         const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, int64_t* r_local, int64_t* send, void* ctl,
                         void* stream) {
-  KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 2 == 0 && n_local >= 0 && n_local <= n_max && N > 0,
+  KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 4 == 0 && n_local >= 0 && n_local <= n_max && N > 0,
                  "krca_ppr_shard_step: bad sizes");
   if (plan_len == 0) return KRCA_OK;
   KRCA_CHECK_ARG(row_ptr && col && plan && w_all && outdeg && q_local && r_local && send && ctl,
                  "krca_ppr_shard_step: null pointer");
   KRCA_CHECK_ARG(w_all != send, "krca_ppr_shard_step: w_all and send must be distinct buffers (ping-pong)");
-  hipLaunchKernelGGL(ppr_step, dim3((unsigned)(plan_len / 2)), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col,
+  hipLaunchKernelGGL(ppr_step, dim3((unsigned)(plan_len / 4)), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col,
                      plan, w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
                      reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
@@ -435,12 +438,12 @@ int64_t krca_ppr_workspace_size(int64_t N) {
   return krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256 + (4 * N + 2 * NSLOT) * 8 + 256;
 }
 
-int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int32_t* plan,
+int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int64_t* plan,
              int64_t plan_len, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
              void* workspace, float* r_out, int64_t* r_fixed, int64_t* q_out, int32_t* iters_host, void* stream) {
   KRCA_CHECK_ARG(N > 0 && N < INT32_MAX, "krca_ppr: N=%lld out of range", (long long)N);
   KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && seed && workspace && r_out, "krca_ppr: null pointer");
-  KRCA_CHECK_ARG(plan_len > 0 && plan_len % 2 == 0, "krca_ppr: bad plan");
+  KRCA_CHECK_ARG(plan_len > 0 && plan_len % 4 == 0, "krca_ppr: bad plan");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0 && max_iter > 0, "krca_ppr: alpha in (0,1), max_iter > 0");
   char* ctl = reinterpret_cast<char*>(workspace);
   const int64_t ctl_bytes = krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256;

@@ -342,7 +342,7 @@ class NativeEngine:
         rp = np.ascontiguousarray(row_ptr_host, dtype=np.int64)
         N = len(rp) - 1
         n = self.lib.krca_ppr_plan_size(rp.ctypes.data_as(c_vp), N)
-        plan = np.zeros(max(n, 2), dtype=np.int32)
+        plan = np.zeros(max(n, 4), dtype=np.int64)
         _check(self.lib.krca_ppr_plan(rp.ctypes.data_as(c_vp), N, plan.ctypes.data_as(c_vp), n), "krca_ppr_plan")
         return self._dev(plan), n
 

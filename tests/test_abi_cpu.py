@@ -45,15 +45,17 @@ def test_ppr_plan_blocks_cover_rows():
     rp = np.zeros(len(deg) + 1, np.int64)
     np.cumsum(deg, out=rp[1:])
     n = lib.krca_ppr_plan_size(rp.ctypes.data_as(ctypes.c_void_p), len(deg))
-    plan = np.zeros(n, np.int32)
+    plan = np.zeros(n, np.int64)
     assert lib.krca_ppr_plan(rp.ctypes.data_as(ctypes.c_void_p), len(deg), plan.ctypes.data_as(ctypes.c_void_p), n) == 0
     covered = np.zeros(len(deg), np.int64)
-    for rb, code in plan.reshape(-1, 2):
+    for rb, code, e0, e1 in plan.reshape(-1, 4):
         if code > 0:
             assert code - rb <= 256 and rp[code] - rp[rb] <= 2048
+            assert (e0, e1) == (rp[rb], rp[code])
             covered[rb:code] += 1
         else:
             assert deg[rb] > 2048
+            assert e0 == rp[rb] + 2048 * (-code) and e1 == min(rp[rb + 1], e0 + 2048)
             covered[rb] += (-code == 0)
     assert (covered == 1).all()
 
