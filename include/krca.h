@@ -105,11 +105,13 @@ int32_t krca_template_max_lines(void);
  * count of partners with |r| > tau taken on the fp16 MFMA screening product (within
  * krca_corr_eps(T) of exact), and cert[p] > 0 iff the reported set is provably the exact top-k
  * (csrc/corr.hip).  Buffers: mean/scale [P]; z32 [P*T]; zh [krca_corr_pad_rows(P) *
- * krca_corr_pad_steps(T)] (fp16 bits); cand [krca_corr_cand_size(P, k) 4-byte words]; count [P];
- * out_idx/out_val [P*k]; cert [P].  k <= krca_corr_max_k(). */
+ * krca_corr_pad_steps(T)] (fp16 bits); cand [krca_corr_cand_size(P, T, k) 4-byte words]; count [P];
+ * out_idx/out_val [P*k]; cert [P].  k <= krca_corr_max_k(), 2 <= P <= 2^22.  krca_corr_topk
+ * synchronises the stream once (it reads how many candidate buffers overflowed to decide on the
+ * second pass). */
 int64_t krca_corr_pad_rows(int64_t P);
 int32_t krca_corr_pad_steps(int32_t T);
-int64_t krca_corr_cand_size(int64_t P, int32_t k);
+int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k);
 int32_t krca_corr_max_k(void);
 float krca_corr_eps(int32_t T);
 int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t channel, float* mean, float* scale,

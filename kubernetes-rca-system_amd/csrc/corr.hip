@@ -8,23 +8,31 @@
 //   krca_corr_prepare  time-major x[T][P][M] -> per-pod mean/scale (one float64 pass, shifted
 //                      sums), then an LDS-tiled transpose to pod-major rows: z32[P][T] (fp32,
 //                      used for the exact re-scoring) and zh[Pp][Tp] = fp16(z) (zero padded to
-//                      128 rows / 64 steps).  |z| <= 1 (unit-norm rows), so fp16 keeps 11 bits.
-//   krca_corr_tiles    MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation) over the UPPER triangle
-//                      of 128x128 tiles only (P(P+1)/2 pairs, the algorithmic flop count), in an
-//                      XCD-aware super-tile order, LDS double-buffered with register prefetch.
-//                      Epilogue in LDS: each lane scans one row (-> candidates of that row from
-//                      this column block) or one column (-> the symmetric candidates of that
-//                      column's pod from this row block), keeping the KC best by |r|; |r| > tau
-//                      counts go out as one int32 add per row/column and tile.
-//   krca_corr_merge    one workgroup per pod: best KM of its nb*KC candidates, re-scored in
-//                      float64 from z32 (fixed-order wave reduction), final top-k; cert[p] =
-//                      (k-th re-scored |r|) - (best |r| the tiles could have dropped) - eps:
-//                      cert > 0 proves the reported set equals the exact top-k.
+//                      256 rows / 64 steps).  |z| <= 1 (unit-norm rows), so fp16 keeps 11 bits.
+//   sample pass        every pod against the first NSB*128 pods and against its own 256-pod
+//                      block (its likely group): phi[p] = (k-th best sampled |r|) - 2 eps, a lower
+//                      bound every member of p's exact top-k clears on the screening product.
+//   main pass          MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation) over the UPPER triangle
+//                      of 256x256 tiles only (P(P+1)/2 pairs, the algorithmic flop count), in an
+//                      XCD-aware super-tile order, LDS double-buffered.  Epilogue straight from the
+//                      accumulators: a value above phi of its row pod (column pod) is appended to
+//                      that pod's candidate buffer (one atomic slot reservation per hit; hits are
+//                      sparse by construction of phi); |r| > tau counts via LDS, one global add per
+//                      row / column and tile.
+//   merge              one workgroup per pod: bitonic sort of its (<= CAPC) candidates, the best
+//                      k+6 re-scored in float64 from z32 (fixed-order wave reduction), final top-k;
+//                      cert[p] = (k-th re-scored |r|) - max(phi, first unre-scored |r|) - eps:
+//                      cert > 0 proves the reported set equals the exact top-k.  A pod whose buffer
+//                      overflowed gets phi2 = (k-th best stored |r|) - 2 eps (any subset bounds the
+//                      k-th from below) and a second main pass runs for those pods only.
+//   flat pods          (z = 0, detected by a zero self product) correlate 0 with everything:
+//                      their top-k is the k lowest other indices, exactly.
 //
 // Error bound of the screening product (eps, host-computed): fp16 rounding of unit-norm rows
 // moves a dot product by <= 2^-10 (+ 2^-24 sqrt(T) from subnormals), fp32 accumulation of T
-// terms of a unit-norm product by <= T 2^-24.  It bounds the ranking pool and the |r| > tau
-// counts (pairs within eps of tau may land on either side); reported r values are exact.
+// terms of a unit-norm product by <= T 2^-24.  It bounds the candidate pool and the |r| > tau
+// counts (pairs within eps of tau may land on either side); reported r values are exact.  The
+// sample and main passes run the same K loop, so a pair's screening value is the same bits in both.
 #include <cmath>
 #include <cstdlib>
 
@@ -36,10 +44,13 @@ constexpr int TPB = 256;
 constexpr int BM = 128;   // tile rows == cols
 constexpr int BK = 64;    // K step (time samples)
 constexpr int SUPER = 8;  // super-tile edge (tiles) of the XCD-aware order
-constexpr int KM = 24;    // candidates re-scored per pod in the merge
+constexpr int KM = 24;    // candidates re-scored per pod in the merge (>= k + 6)
 constexpr int KMAX = 16;  // largest k served
-// KC = candidates kept per (pod, block): a template parameter >= k (so every member of a pod's
-// exact top-k survives its own block's cut), with headroom for the certificate: 8, 12 or 16
+constexpr int NSB = 16;   // 128-pod column blocks in the threshold sample (2048 pods)
+constexpr int NSL = NSB + 2;  // sample lists per pod: NSB sample blocks + the pod's own 256-block
+constexpr int CAPC = 1024;    // candidate buffer per pod (main pass appends)
+// KC = candidates kept per (pod, sample block) in the sample pass: a template parameter >= k
+// (8, 12 or 16), so the k best sampled partners of a pod survive their blocks' cuts
 
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -137,9 +148,8 @@ struct Cand {
 
 // Tile kernel: 256 x 256 pods per workgroup (8 waves = 2 row halves x 4 column quarters, a
 // 128 x 64 wave tile = 4 x 2 MFMA 32x32 blocks), K steps of 64 through a double-buffered LDS
-// stage (A and B 256 x 64 fp16 each) fed by a register prefetch.  Candidate lists keep the
-// 128-pod block granularity: a row's list covers one 128-column half of the tile, a column's list
-// one 128-row half.
+// stage (A and B 256 x 64 fp16 each) fed by direct global->LDS loads.  Sample-pass lists keep a
+// 128-pod block granularity (a row's list covers one 128-column half of the tile).
 constexpr int TB = 256;                                // tile edge (pods)
 constexpr int NT = 512;                                // threads per tile workgroup
 constexpr int STAGE_BYTES = 2 * TB * BK * 2;           // A and B, fp16
@@ -149,28 +159,46 @@ constexpr int LDS_EPI = BM * EPI_LD * 4;               // 128 rows x 256 columns
 constexpr int LDS_MAIN = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
 constexpr int LDS_JUNK = NT * 4;                       // landing slots of the L2 prefetch loads
 constexpr int LDS_BYTES = LDS_MAIN + LDS_JUNK;
+constexpr int EPI_LIST_OFF = 8192;                     // main-pass epilogue: per-wave candidate lists
+constexpr int CAPW = (LDS_MAIN - EPI_LIST_OFF) / (8 * 16);
 
 // 16-byte chunk c (0..7) of row r of a [rows][64] fp16 stage, XOR-swizzled against bank conflicts
 // (the XOR key (r >> 1) & 7 makes every 16-lane ds_read_b128 phase of 16 rows hit 16 distinct
 // 4-bank granules: row parity picks the 32-bank half, the key the granule inside it)
 __device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
-// SAMPLE = false: the upper triangle of 256-blocks (all pairs), lists filtered by phi, heads and
-//                 |r| > tau counts out.
-// SAMPLE = true:  rows x the first nsb 128-column blocks (the threshold sample), row lists only.
-template <int KC, bool SAMPLE>
-__global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh, int64_t P, int Tp, int nb2,
-                                                 int64_t per_xcd, int nsb, float tau, const float* __restrict__ phi,
-                                                 float* __restrict__ cand_v, int32_t* __restrict__ cand_i,
-                                                 float* __restrict__ cand_hd, int32_t* __restrict__ count,
-                                                 int debug) {
+// MODE_MAIN:   the upper triangle of 256-blocks (all pairs); hits above phi appended to the
+//              per-pod candidate buffers (row and column side), |r| > tau counted.
+// MODE_SAMPLE: rows x (the first nsb 128-column blocks, then the row's own 256-block): row lists
+//              only (sample slots NSB, NSB+1 = own block), and each pod's self product.
+// MODE_RECT:   the gathered rows zA = zh[rect_pods] x every column block (second pass of the pods
+//              whose buffer overflowed): row-side appends only, against phi = phi2.
+constexpr int MODE_MAIN = 0, MODE_SAMPLE = 1, MODE_RECT = 2;
+
+template <int KC, int MODE>
+__global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA, const uint16_t* __restrict__ zh,
+                                                 int64_t P, int Tp, int nb2, int64_t per_xcd, int nsb, float tau,
+                                                 const float* __restrict__ phi, float* __restrict__ samp_v,
+                                                 int32_t* __restrict__ samp_i, float* __restrict__ selfd,
+                                                 int2* __restrict__ buf, int32_t* __restrict__ cnt,
+                                                 int32_t* __restrict__ count, const int32_t* __restrict__ rect_pods,
+                                                 int64_t n_rect, int debug) {
+  constexpr bool SAMPLE = MODE == MODE_SAMPLE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nb = 2 * nb2;  // 128-pod blocks
   int64_t I, J;
-  if (SAMPLE) {
+  bool own = false;
+  if (MODE == MODE_RECT) {
+    I = blockIdx.x / nb2;
+    J = blockIdx.x % nb2;
+  } else if (SAMPLE) {
     const int nsb2 = (nsb + 1) / 2;
-    I = blockIdx.x / nsb2;
-    J = blockIdx.x % nsb2;
+    I = blockIdx.x / (nsb2 + 1);
+    J = blockIdx.x % (nsb2 + 1);
+    if (J == nsb2) {  // the row block's own 256-block, unless it is already a sample block
+      if (I < nsb2) return;
+      J = I;
+      own = true;
+    }
   } else {
     // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so slot
     // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the
@@ -193,6 +221,21 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 2, wc = w & 3;
   const int64_t rowA = I * TB, rowB = J * TB;
+  // main / rect epilogue operands, loaded now so their latency hides behind the K loop: thread
+  // tid < 256 holds row pod tid of the tile and its phi, thread tid >= 256 column pod tid - 256
+  int my_pod = -1;
+  float my_phi = 4.f;  // 4 = never a candidate owner (padding, or column side of a rect pass)
+  if (!SAMPLE) {
+    const int q = tid & (TB - 1);
+    if (tid < TB) {
+      const int64_t g = MODE == MODE_RECT ? (rowA + q < n_rect ? rect_pods[rowA + q] : -1) : (rowA + q < P ? rowA + q : -1);
+      my_pod = (int)g;
+      if (g >= 0) my_phi = phi[g];
+    } else if (MODE == MODE_MAIN && rowB + q < P) {
+      my_pod = (int)(rowB + q);
+      my_phi = phi[rowB + q];
+    }
+  }
 
   floatx16 acc[4][2];
 #pragma unroll
@@ -206,7 +249,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh
   // instruction writes a lane-linear 1 KiB piece = 8 rows of 128 B; lane l lands on row l/8,
   // slot l%8, so it fetches the global chunk (l%8) ^ key(row): the XOR swizzle is applied on the
   // SOURCE address.  64 pieces per K step (32 A + 32 B), 8 per wave.
-  const uint16_t* gA = zh + rowA * Tp;
+  const uint16_t* gA = zA + rowA * Tp;
   const uint16_t* gB = zh + rowB * Tp;
   const int prow = lane >> 3, pslot = lane & 7;
 #define CORR_GLDS(BUF, K0)                                                                             \
@@ -268,14 +311,166 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh
 #undef CORR_GLDS
 #undef CORR_COMPUTE
 #undef CORR_L2PF
-  // epilogue, one 128-row half at a time: the half's waves park their accumulators in LDS, then
-  // 256 lanes scan rows (one 128-column half each) and 256 lanes scan columns (128 rows each)
-  float* tile = reinterpret_cast<float*>(smem);
-  const bool diag = I == J;
+  const bool diag = MODE != MODE_RECT && I == J;
   if (debug == 1) {  // profiling aid (KRCA_CORR_DEBUG=1): product only, no epilogue
     if (tid == 0 && acc[0][0][0] == 12345.f) count[0] = 1;
     return;
   }
+  if (!SAMPLE) {
+    // ---- main / rect pass: epilogue straight from the accumulators -------------------------
+    // lane holds rows wr*128 + i*32 + (e&3) + 8*(e>>2) + 4*h and columns wc*64 + j*32 + r32.
+    // Padding rows / columns have z = 0 (r = 0: never above tau >= 0) and phi = 4 (never a
+    // candidate); the self products of a diagonal tile are zeroed first.  The common case costs
+    // ~4 vector ops per value; only a 16-value group with a candidate takes the slow path.
+    constexpr bool RECT = MODE == MODE_RECT;
+    float* sphr = reinterpret_cast<float*>(smem);  // phi of the 256 row pods
+    float* sphc = sphr + TB;                        // phi of the 256 column pods
+    int* srcnt = reinterpret_cast<int*>(sphc + TB);  // |r| > tau counts per row / column
+    int* sccnt = srcnt + TB;
+    int* spod = sccnt + TB;  // row pod ids
+    int* wcount = spod + TB;  // candidate-list length per wave
+    {
+      const int q = tid & (TB - 1);
+      (tid < TB ? sphr : sphc)[q] = my_phi;
+      (tid < TB ? srcnt : sccnt)[q] = 0;
+      if (tid < TB) spod[q] = my_pod;
+    }
+    __syncthreads();
+    if (diag) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h == wc * 64 + j * 32 + r32) acc[i][j][e] = 0.f;
+    }
+    // per-wave candidate list in LDS {pod, partner, r bits}, compacted by ballot + mbcnt (no
+    // atomics, no waiting); past CAPW entries a hit goes to the global buffer directly (rare)
+    int4* wlist = reinterpret_cast<int4*>(smem + EPI_LIST_OFF) + w * CAPW;
+    int nlist = 0;  // wave-uniform
+    auto push = [&](bool hit, uint64_t m, int pod, int partner, float v) {
+      const int slot = nlist + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (hit) {
+        if (slot < CAPW) {
+          wlist[slot] = make_int4(pod, partner, __float_as_int(v), 0);
+        } else {
+          const int gs = atomicAdd(&cnt[pod], 1);
+          if (gs < CAPC) buf[(int64_t)pod * CAPC + gs] = make_int2(__float_as_int(v), partner);
+        }
+      }
+      nlist += __builtin_popcountll(m);
+    };
+    int rcl0 = 0, rcl1 = 0;  // lane L collects the row counts of (i, e) = (L >> 4, L & 15)
+    int colcnt[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float pr[16];
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const float4 q = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 32 + 8 * e4 + 4 * h);
+        pr[4 * e4] = q.x;
+        pr[4 * e4 + 1] = q.y;
+        pr[4 * e4 + 2] = q.z;
+        pr[4 * e4 + 3] = q.w;
+      }
+      int rc[16][2];  // wave-uniform row counts of this i, [e][h]
+#pragma unroll
+      for (int e = 0; e < 16; ++e) rc[e][0] = rc[e][1] = 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wc * 64 + j * 32 + r32;
+        const float pc = diag ? 4.f : sphc[col];  // diagonal tile: both orders present, rows only
+        uint64_t any = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float a = fabsf(acc[i][j][e]);
+          if (!RECT) {
+            const bool hit = a > tau;
+            const uint64_t m = __ballot(hit);
+            rc[e][0] += __builtin_popcount((uint32_t)m);
+            rc[e][1] += __builtin_popcount((uint32_t)(m >> 32));
+            colcnt[j] += hit ? 1 : 0;
+          }
+          any |= __ballot(a > fminf(pr[e], pc));
+        }
+        if (any && debug != 3) {  // slow path: this 16-value group holds at least one candidate
+          const int gc = (int)(rowB + col);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float v = acc[i][j][e];
+            const float a = fabsf(v);
+            const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int gr = RECT ? spod[row] : (int)(rowA + row);
+            const bool hr = a > pr[e] && gc < P && gc != gr;  // padding partners / zeroed self: r = 0
+            const bool hc = a > pc && rowA + row < P;
+            const uint64_t mr = __ballot(hr);
+            if (mr) push(hr, mr, gr, gc, v);
+            const uint64_t mc = __ballot(hc);
+            if (mc) push(hc, mc, gc, gr, v);
+          }
+        }
+      }
+      if (!RECT) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          rcl0 = lane == i * 16 + e ? rc[e][0] : rcl0;
+          rcl1 = lane == i * 16 + e ? rc[e][1] : rcl1;
+        }
+      }
+    }
+    // reserve the buffer slots of every listed candidate at once (independent atomics in flight)
+    if (lane == 0) wcount[w] = nlist < CAPW ? nlist : CAPW;
+    if (!RECT) {  // |r| > tau: one LDS add per row / column and wave
+      const int li = lane >> 4, le = lane & 15;
+      const int rbase = wr * 128 + li * 32 + (le & 3) + 8 * (le >> 2);
+      if (rcl0) atomicAdd(&srcnt[rbase], rcl0);
+      if (rcl1) atomicAdd(&srcnt[rbase + 4], rcl1);
+      if (!diag) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = colcnt[j] + __shfl_xor(colcnt[j], 32, 64);
+          if (h == 0 && c) atomicAdd(&sccnt[wc * 64 + j * 32 + r32], c);
+        }
+      }
+    }
+    __syncthreads();
+    if (!RECT) {  // one global add per row / column of the tile
+      const int q = tid & (TB - 1);
+      if (tid < TB) {
+        if (srcnt[q]) atomicAdd(&count[rowA + q], srcnt[q]);
+      } else if (!diag && sccnt[q]) {
+        atomicAdd(&count[rowB + q], sccnt[q]);
+      }
+    }
+    if (debug < 2) {
+      const int4* lists = reinterpret_cast<const int4*>(smem + EPI_LIST_OFF);
+      for (int base = 0;; base += NT) {
+        bool more = false;
+#pragma unroll
+        for (int u0 = 0; u0 < 8; u0 += 4) {
+          int4 ent[4];
+          int gs[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = base + tid;
+            const bool ok = q < wcount[u0 + u];
+            more = more || base + NT < wcount[u0 + u];
+            ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(-1, 0, 0, 0);
+            gs[u] = ok ? atomicAdd(&cnt[ent[u].x], 1) : CAPC;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (gs[u] < CAPC) buf[(int64_t)ent[u].x * CAPC + gs[u]] = make_int2(ent[u].z, ent[u].y);
+        }
+        if (!more) break;  // wave-uniform: every lane reads the same wcount[]
+      }
+    }
+    return;
+  }
+  // ---- sample pass: park each 128-row half in LDS, one lane per (row, 128-column half) --------
+  float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if (wr == half) {
@@ -291,77 +486,39 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh
           }
     }
     __syncthreads();
-    Cand<KC> cd;
-    cd.init();
-    int n_over = 0;
-    int64_t g = -1, slot = 0;
-    bool write = false;
     if (tid < 256) {  // row scan: pod rowA + half*128 + r against 128 columns of block 2J + ch
       const int r = tid & 127, ch = tid >> 7;
-      g = rowA + half * BM + r;
+      const int64_t g = rowA + half * BM + r;
       const int jb = 2 * (int)J + ch;
       const int64_t c0 = rowB + ch * BM;
-      if (g < P && (!SAMPLE || jb < nsb)) {
-        write = true;
-        slot = SAMPLE ? g * 16 + jb : g * nb + jb;
-        const float ph = SAMPLE ? -1.f : phi[g];
-        float lim = ph;  // = max(list floor, phi), refreshed on insert
+      if (g < P && (own || jb < nsb)) {
+        Cand<KC> cd;
+        cd.init();
+        const int64_t slot = g * NSL + (own ? NSB + ch : jb);
         const int cend = (int)std::min<int64_t>(BM, P - c0);
         const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
         const float* rowp = tile + r * EPI_LD + ch * BM;
+        if (self >= 0) selfd[g] = rowp[self];
+        float lim = -1.f;
         for (int c4 = 0; c4 < cend; c4 += 4) {
           const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int c = c4 + u;
             const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
-            const float a = fabsf(vu);
-            const bool ok = c < cend && c != self;
-            n_over += (ok && a > tau) ? 1 : 0;
-            if (ok && a > lim) {
+            if (c < cend && c != self && fabsf(vu) > lim) {
               cd.insert(vu, (int32_t)(c0 + c));
-              lim = fmaxf(cd.thr, ph);
+              lim = cd.thr;
             }
           }
         }
-      }
-    } else if (!SAMPLE && !diag) {  // column scan: pod rowB + c against the 128 rows of this half
-      const int c = tid - 256;
-      g = rowB + c;
-      const int ib = 2 * (int)I + half;
-      const int64_t r0 = rowA + half * BM;
-      if (g < P) {
-        write = true;
-        slot = g * nb + ib;
-        const float ph = phi[g];
-        float lim = ph;
-        const int rend = (int)std::min<int64_t>(BM, P - r0);
-        for (int r = 0; r < rend; ++r) {
-          const float v = tile[r * EPI_LD + c];
-          const float a = fabsf(v);
-          n_over += a > tau ? 1 : 0;
-          if (a > lim) {
-            cd.insert(v, (int32_t)(r0 + r));
-            lim = fmaxf(cd.thr, ph);
-          }
-        }
-      }
-    }
-    if (write) {
-      if (SAMPLE || cd.i[0] >= 0) {  // empty main-pass lists are never read (head = -1)
-        float* ov = cand_v + slot * KC;
-        int32_t* oi = cand_i + slot * KC;
+        float* ov = samp_v + slot * KC;
+        int32_t* oi = samp_i + slot * KC;
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
           ov[q] = cd.v[q];
           oi[q] = cd.i[q];
         }
-      }
-      if (!SAMPLE) {
-        // list head (best |r|, -1 if empty) and floor (KC-th |r| if the list is full, else -1)
-        cand_hd[slot * 2] = cd.i[0] < 0 ? -1.f : fabsf(cd.v[0]);
-        cand_hd[slot * 2 + 1] = cd.thr;
-        if (n_over) atomicAdd(&count[g], n_over);
       }
     }
     __syncthreads();  // the next half overwrites the tile
@@ -370,37 +527,48 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zh
 
 // phi[g] = (k-th best |r| of g among the sampled partners) - 2 eps (-1 if fewer than k): every
 // member of g's exact top-k has a screening |r| above it (exact k-th >= sampled k-th - eps).
+// A flat pod (self product 0: z = 0) gets phi = 3 (never a candidate owner; handled exactly).
 template <int KC>
 __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, const int32_t* __restrict__ si,
-                                                  int64_t P, int nsb, int k, float eps, float* __restrict__ phi) {
+                                                  const float* __restrict__ selfd, int64_t P, int nsb, int k,
+                                                  float eps, float* __restrict__ phi) {
   const int64_t g = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= P) return;
-  const int n = nsb * KC;  // <= 256; sample lists are [P][16][KC]
-  float a[4];
+  constexpr int PER = (NSL * KC + 63) / 64;
+  float a[PER];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < PER; ++u) {
     const int q = lane + 64 * u;
-    const int64_t e = g * 16 * KC + q;
-    a[u] = (q < n && si[e] >= 0) ? fabsf(sv[e]) : -1.f;
+    const int lst = q / KC;
+    const int64_t e = g * NSL * KC + q;
+    const bool used = q < NSL * KC && (lst < nsb || lst >= NSB);
+    a[u] = (used && si[e] >= 0) ? fabsf(sv[e]) : -1.f;
   }
   float kth = -1.f;
   for (int r = 0; r < k; ++r) {
-    float m = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+    float m = a[0];
+#pragma unroll
+    for (int u = 1; u < PER; ++u) m = fmaxf(m, a[u]);
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
     kth = m;
     if (m < 0.f) break;
     // remove one instance of m: the lowest lane holding it, its first slot
-    const bool has = a[0] == m || a[1] == m || a[2] == m || a[3] == m;
+    bool has = false;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) has = has || a[u] == m;
     const uint64_t bal = __ballot(has);
     if (lane == __ffsll((unsigned long long)bal) - 1) {
-      if (a[0] == m) a[0] = -1.f;
-      else if (a[1] == m) a[1] = -1.f;
-      else if (a[2] == m) a[2] = -1.f;
-      else a[3] = -1.f;
+      bool done = false;
+#pragma unroll
+      for (int u = 0; u < PER; ++u)
+        if (!done && a[u] == m) {
+          a[u] = -1.f;
+          done = true;
+        }
     }
   }
-  if (lane == 0) phi[g] = kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f;
+  if (lane == 0) phi[g] = selfd[g] < 0.25f ? 3.f : (kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f);
 }
 
 // ---- merge + exact re-scoring ------------------------------------------------------------------
@@ -411,130 +579,66 @@ __device__ __forceinline__ bool cbetter(float a, int32_t ia, float b, int32_t ib
   return fa > fb || (fa == fb && ia < ib);
 }
 
-struct Pool {  // sorted (|r| desc, index asc) list of KM + 1
-  float v[KM + 1];
-  int32_t i[KM + 1];
-  __device__ __forceinline__ void insert(float nv, int32_t ni) {
-    if (!cbetter(nv, ni, v[KM], i[KM])) return;
-#pragma unroll
-    for (int j = KM; j > 0; --j) {
-      const bool up = cbetter(nv, ni, v[j - 1], i[j - 1]);
-      const bool here = cbetter(nv, ni, v[j], i[j]);
-      const float pv = v[j - 1];
-      const int32_t pi = i[j - 1];
-      v[j] = up ? pv : (here ? nv : v[j]);
-      i[j] = up ? pi : (here ? ni : i[j]);
-    }
-    if (cbetter(nv, ni, v[0], i[0])) {
-      v[0] = nv;
-      i[0] = ni;
-    }
-  }
-};
-
-constexpr int CAP = 2048;  // merge: candidates collected above the head threshold (else fallback)
-
-// theta = the (KM+1)-th largest list head (bitonic sort of the nb <= 4096 heads in LDS), or 0
-// when fewer than KM+1 lists are non-empty: at least KM+1 candidates are >= theta, so the best
-// KM+1 candidates all are.
-__device__ float head_threshold(const float* __restrict__ hd, int nb, float* key) {
-  const int tid = threadIdx.x;
-  int np = 64;
-  while (np < nb) np <<= 1;
-  for (int i = tid; i < np; i += TPB) key[i] = i < nb ? hd[2 * i] : -1.f;  // empty lists: -1
-  __syncthreads();
-  for (int kk = 2; kk <= np; kk <<= 1) {
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < np; i += TPB) {
-        const int l = i ^ j;
-        if (l > i) {
-          const float a = key[i], c = key[l];
-          if ((a < c) == ((i & kk) == 0)) {  // descending runs first
-            key[i] = c;
-            key[l] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  const float t = key[KM];
-  __syncthreads();
-  return t < 0.f ? 0.f : t;
+// rows of the overflowed pods, gathered for the second (rectangle) pass; padding rows are zero
+__global__ __launch_bounds__(TPB) void corr_gather_rows(const uint16_t* __restrict__ zh, int Tp,
+                                                        const int32_t* __restrict__ pods, int64_t n,
+                                                        uint16_t* __restrict__ zs) {
+  const int64_t r = blockIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(zh + (int64_t)(r < n ? pods[r] : 0) * Tp);
+  uint4* dst = reinterpret_cast<uint4*>(zs + r * Tp);
+  for (int c = threadIdx.x; c < Tp / 8; c += TPB) dst[c] = r < n ? src[c] : make_uint4(0, 0, 0, 0);
 }
 
-template <int KC>
-__global__ __launch_bounds__(TPB) void corr_merge(const float* __restrict__ cand_v, const int32_t* __restrict__ cand_i,
-                                                  const float* __restrict__ cand_hd, const float* __restrict__ phi,
-                                                  const float* __restrict__ z32, int64_t P, int T, int nb, int k,
-                                                  float eps,
-                                                  int32_t* __restrict__ out_i, float* __restrict__ out_v,
-                                                  float* __restrict__ cert) {
-  __shared__ int hist[4096];  // the sorted list heads, then the collected candidates (v, i)
-  __shared__ int lid[4096];   // lists whose head is >= theta
-  __shared__ int n_lists;
-  __shared__ int ord[KM];
-  __shared__ float sv[TPB / 64];
-  __shared__ int32_t si[TPB / 64];
+// one workgroup per pod (or per listed pod in the second pass): sort the pod's candidates, re-score
+// the best km = k + 6 in float64, rank, certify.  Pass 0 turns an overflowed buffer into phi2 and
+// queues the pod for the second main pass (over[0] = count, over[1..] = pods).
+__global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, int32_t* __restrict__ cnt,
+                                                  const float* __restrict__ phi_used, const float* __restrict__ z32,
+                                                  int64_t P, int T, int k, float eps, int pass,
+                                                  const int32_t* __restrict__ pods, float* __restrict__ phi2,
+                                                  int32_t* __restrict__ over, int32_t* __restrict__ out_i,
+                                                  float* __restrict__ out_v, float* __restrict__ cert) {
+  __shared__ float cv[CAPC];
+  __shared__ int32_t ci[CAPC];
   __shared__ float top_v[KM + 1];
   __shared__ int32_t top_i[KM + 1];
   __shared__ double exact[KM];
-  __shared__ int n_col;
-  const int64_t g = blockIdx.x;
+  __shared__ int ord[KM];
+  const int64_t g = pods ? pods[blockIdx.x] : blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t base = g * nb * KC;
-  const float* hd = cand_hd + g * nb * 2;
-  // largest |r| any full per-block list could have cut off
-  float floor_ = 0.f;
-  for (int b = tid; b < nb; b += TPB) floor_ = fmaxf(floor_, hd[2 * b + 1]);
-  for (int off = 32; off > 0; off >>= 1) floor_ = fmaxf(floor_, __shfl_xor(floor_, off, 64));
-  if (lane == 0) sv[w] = floor_;
-  __syncthreads();
-  floor_ = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
-  const float theta = head_threshold(hd, nb, reinterpret_cast<float*>(hist));
-  // collect every candidate >= theta (lists are sorted, so a list is read only while >= theta)
-  float* cv = reinterpret_cast<float*>(hist);
-  int32_t* ci = hist + CAP;
-  if (tid == 0) {
-    n_col = 0;
-    n_lists = 0;
-  }
-  __syncthreads();
-  for (int b = tid; b < nb; b += TPB)
-    if (hd[2 * b] >= theta && hd[2 * b] >= 0.f) lid[atomicAdd(&n_lists, 1)] = b;
-  __syncthreads();
-  const int nl = n_lists;
-  for (int item = tid; item < nl * KC; item += TPB) {  // every (list, entry): independent loads
-    const int64_t e = base + (int64_t)lid[item / KC] * KC + item % KC;
-    const int32_t id = cand_i[e];
-    const float v = cand_v[e];
-    if (id >= 0 && fabsf(v) >= theta) {
-      const int slot = atomicAdd(&n_col, 1);
-      if (slot < CAP) {
-        cv[slot] = v;
-        ci[slot] = id;
+  const float ph = phi_used[g];
+  const bool flat = ph > 2.f;
+  const int n = cnt[g];
+  const bool overflow = n > CAPC;
+  const int km = k + 6 < KM ? k + 6 : KM;
+  if (flat) {  // r = 0 with every partner: the lowest other indices, in order
+    if (tid <= KM) {
+      const int64_t q = tid < g ? tid : tid + 1;
+      top_i[tid] = q < P ? (int32_t)q : -1;
+      top_v[tid] = 0.f;
+    }
+  } else {
+    const int nn = overflow ? CAPC : n;
+    int np = 32;
+    while (np < nn) np <<= 1;
+    for (int i = tid; i < np; i += TPB) {
+      if (i < nn) {
+        const int2 c = buf[g * CAPC + i];
+        cv[i] = __int_as_float(c.x);
+        ci[i] = c.y;
+      } else {
+        cv[i] = 0.f;
+        ci[i] = -1;
       }
     }
-  }
-  __syncthreads();
-  const int n = n_col;
-  if (n <= CAP) {
-    // bitonic sort of the collected candidates (|r| desc, index asc; padding last)
-    int np = 32;
-    while (np < n) np <<= 1;
-    for (int i = n + tid; i < np; i += TPB) {
-      cv[i] = 0.f;
-      ci[i] = -1;
-    }
     __syncthreads();
-    for (int kk = 2; kk <= np; kk <<= 1) {
+    for (int kk = 2; kk <= np; kk <<= 1) {  // bitonic: |r| desc, index asc, empties last
       for (int j = kk >> 1; j > 0; j >>= 1) {
         for (int i = tid; i < np; i += TPB) {
           const int l = i ^ j;
           if (l > i) {
             const bool desc = (i & kk) == 0;
-            const bool lbetter = cbetter(cv[l], ci[l], cv[i], ci[i]);
-            if (lbetter == desc) {
+            if (cbetter(cv[l], ci[l], cv[i], ci[i]) == desc) {
               const float tv = cv[i];
               const int32_t ti = ci[i];
               cv[i] = cv[l];
@@ -547,66 +651,21 @@ __global__ __launch_bounds__(TPB) void corr_merge(const float* __restrict__ cand
         __syncthreads();
       }
     }
+    if (overflow && pass == 0) {  // any stored subset bounds the exact k-th from below
+      if (tid == 0) {
+        phi2[g] = fabsf(cv[k - 1]) - 2.f * eps - 1e-6f;
+        cnt[g] = 0;
+        over[1 + atomicAdd(&over[0], 1)] = (int32_t)g;
+      }
+      return;
+    }
     if (tid <= KM) {
       top_v[tid] = tid < np ? cv[tid] : 0.f;
       top_i[tid] = tid < np ? ci[tid] : -1;
     }
-  } else {
-    // fallback (ties at the threshold, e.g. a flat series): per-lane pools over every candidate
-    Pool c;
-#pragma unroll
-    for (int j = 0; j <= KM; ++j) {
-      c.v[j] = 0.f;
-      c.i[j] = -1;
-    }
-    for (int64_t q = tid; q < (int64_t)nb * KC; q += TPB) {
-      const int32_t id = cand_i[base + q];
-      if (id >= 0) c.insert(cand_v[base + q], id);
-    }
-    for (int r = 0; r <= KM; ++r) {  // block-wide extraction, one winner per round
-      float bv = c.v[0];
-      int32_t bi = c.i[0];
-      for (int off = 32; off > 0; off >>= 1) {
-        const float ov = __shfl_xor(bv, off, 64);
-        const int32_t oi = __shfl_xor(bi, off, 64);
-        if (cbetter(ov, oi, bv, bi)) {
-          bv = ov;
-          bi = oi;
-        }
-      }
-      if (lane == 0) {
-        sv[w] = bv;
-        si[w] = bi;
-      }
-      __syncthreads();
-      float wv = sv[0];
-      int32_t wi = si[0];
-      for (int q = 1; q < TPB / 64; ++q)
-        if (cbetter(sv[q], si[q], wv, wi)) {
-          wv = sv[q];
-          wi = si[q];
-        }
-      __syncthreads();
-      if (tid == 0) {
-        top_v[r] = wv;
-        top_i[r] = wi;
-      }
-      if (wi >= 0 && c.i[0] == wi) {  // each partner sits in exactly one lane's pool
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-          c.v[j] = c.v[j + 1];
-          c.i[j] = c.i[j + 1];
-        }
-        c.v[KM] = 0.f;
-        c.i[KM] = -1;
-      }
-    }
   }
   __syncthreads();
-  // exact float64 re-scoring of the best km = min(KM, k + 6) (one wave per candidate, fixed
-  // reduction order); the certificate bounds everything outside them by the (km+1)-th
-  const int km = k + 6 < KM ? k + 6 : KM;
-  const float dropped = fmaxf(fmaxf(floor_, phi[g]), top_i[km] >= 0 ? fabsf(top_v[km]) : 0.f);
+  // exact float64 re-scoring of the best km (one wave per candidate, fixed reduction order)
   const float* zg = z32 + g * T;
   {  // wave w re-scores candidates w, w+4, ... together (independent loads in flight)
     constexpr int PER = (KM + TPB / 64 - 1) / (TPB / 64);
@@ -649,50 +708,92 @@ __global__ __launch_bounds__(TPB) void corr_merge(const float* __restrict__ cand
     out_i[g * k + q] = top_i[ord[q]];
     out_v[g * k + q] = (float)exact[ord[q]];
   }
-  if (tid == 0) cert[g] = (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
+  if (tid == 0) {
+    // everything not re-scored has a screening |r| <= max(phi, the first un-re-scored candidate)
+    const float dropped = fmaxf(ph, top_i[km] >= 0 ? fabsf(top_v[km]) : 0.f);
+    cert[g] = flat ? 1.f
+                   : overflow ? -1.f : (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
+  }
 }
 
+// profiling aid, KRCA_CORR_DEBUG (results are wrong when set): 1 = product only, 2 = no global
+// candidate appends, 3 = no candidate slow path either
 int debug_mode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("KRCA_CORR_DEBUG");
-    m = e ? atoi(e) : 0;
-  }
-  return m;
+  const char* e = getenv("KRCA_CORR_DEBUG");
+  return e ? atoi(e) : 0;
 }
+
+constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
+
+struct CorrWs {  // views into the caller's candidate workspace (4-byte words)
+  int2* buf;
+  int32_t *cnt, *samp_i, *over;
+  float *samp_v, *selfd, *phi, *phi2;
+  uint16_t* zs;  // [RECT_ROWS][Tp] gathered rows of the second pass
+};
 
 template <int KC>
 int launch_corr(const uint16_t* zh, const float* z32, int64_t P, int T, int Tp, int nb, int nsb, int k, float tau,
-                float eps, float* cand_v, int32_t* cand_i, float* cand_hd, float* samp_v, int32_t* samp_i, float* phi,
-                int32_t* count, int32_t* out_idx, float* out_val, float* cert, hipStream_t st) {
+                float eps, const CorrWs& ws, int32_t* count, int32_t* out_idx, float* out_val, float* cert,
+                hipStream_t st) {
   static bool lds_attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
   if (!lds_attr) {
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, false>),
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_MAIN>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, true>),
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_SAMPLE>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_RECT>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
     lds_attr = true;
   }
-  // 1. threshold sample: every pod against the first nsb column blocks
   const int nb2 = nb / 2;
-  hipLaunchKernelGGL((corr_tiles<KC, true>), dim3((unsigned)(nb2 * ((nsb + 1) / 2))), dim3(NT), LDS_BYTES, st, zh, P,
-                     Tp, nb2, (int64_t)0, nsb, tau, (const float*)nullptr, samp_v, samp_i, (float*)nullptr,
-                     (int32_t*)nullptr, 0);
+  KRCA_HIP(hipMemsetAsync(ws.samp_i, 0xff, (size_t)P * NSL * KC * sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)P * sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetAsync(ws.over, 0, sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.phi2), 0x40400000 /* 3.0f */, (size_t)P, st));
+  // 1. threshold sample: every pod against the first nsb column blocks and its own block
+  const int nsb2 = (nsb + 1) / 2;
+  hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)(nb2 * (nsb2 + 1))), dim3(NT), LDS_BYTES, st, zh,
+                     zh, P, Tp, nb2, (int64_t)0, nsb, tau, (const float*)nullptr, ws.samp_v, ws.samp_i, ws.selfd,
+                     (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, 0);
   KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, samp_v, samp_i, P,
-                     nsb, k, eps, phi);
+  hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
+                     ws.samp_i, ws.selfd, P, nsb, k, eps, ws.phi);
   KRCA_LAUNCH_CHECK();
-  // 2. all pairs (upper triangle), filtered by phi
+  // 2. all pairs (upper triangle): candidates above phi, |r| > tau counts
   const int64_t ns = (nb2 + SUPER - 1) / SUPER;
   const int64_t slots = ns * (ns + 1) / 2 * SUPER * SUPER;
   const int64_t per_xcd = (slots + 7) / 8;
-  hipLaunchKernelGGL((corr_tiles<KC, false>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, P, Tp, nb2,
-                     per_xcd, nsb, tau, (const float*)phi, cand_v, cand_i, cand_hd, count, debug_mode());
+  const int dbg = debug_mode();
+  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, zh, P,
+                     Tp, nb2, per_xcd, nsb, tau, (const float*)ws.phi, (float*)nullptr, (int32_t*)nullptr,
+                     (float*)nullptr, ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, dbg);
   KRCA_LAUNCH_CHECK();
-  // 3. per pod: pool, exact re-scoring, top-k, certificate
-  hipLaunchKernelGGL(corr_merge<KC>, dim3((unsigned)P), dim3(TPB), 0, st, cand_v, cand_i, cand_hd, phi, z32, P, T, nb,
-                     k, eps, out_idx, out_val, cert);
+  // 3. per pod: sort, exact re-scoring, top-k, certificate; overflowed pods are queued
+  hipLaunchKernelGGL(corr_merge, dim3((unsigned)P), dim3(TPB), 0, st, ws.buf, ws.cnt, (const float*)ws.phi, z32, P, T,
+                     k, eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert);
   KRCA_LAUNCH_CHECK();
+  int32_t n_over = 0;
+  KRCA_HIP(hipMemcpyAsync(&n_over, ws.over, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  KRCA_HIP(hipStreamSynchronize(st));
+  // 4. overflowed pods only: their rows x every column block against phi2 (RECT_ROWS per launch)
+  for (int64_t r0 = 0; r0 < n_over && dbg == 0; r0 += RECT_ROWS) {
+    const int64_t nr = std::min<int64_t>(RECT_ROWS, n_over - r0);
+    const int64_t npad = krca::ceil_div(nr, TB) * TB;
+    hipLaunchKernelGGL(corr_gather_rows, dim3((unsigned)npad), dim3(TPB), 0, st, zh, Tp,
+                       (const int32_t*)(ws.over + 1 + r0), nr, ws.zs);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * nb2)), dim3(NT), LDS_BYTES, st,
+                       (const uint16_t*)ws.zs, zh, P, Tp, nb2, (int64_t)0, nsb, tau, (const float*)ws.phi2,
+                       (float*)nullptr, (int32_t*)nullptr, (float*)nullptr, ws.buf, ws.cnt, count,
+                       (const int32_t*)(ws.over + 1 + r0), nr, 0);
+    KRCA_LAUNCH_CHECK();
+  }
+  if (n_over > 0 && dbg == 0) {
+    hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, ws.buf, ws.cnt, (const float*)ws.phi2,
+                       z32, P, T, k, eps, 1, (const int32_t*)(ws.over + 1), ws.phi2, ws.over, out_idx, out_val, cert);
+    KRCA_LAUNCH_CHECK();
+  }
   return KRCA_OK;
 }
 
@@ -704,12 +805,11 @@ extern "C" {
 
 int64_t krca_corr_pad_rows(int64_t P) { return krca::ceil_div(P, TB) * TB; }
 int32_t krca_corr_pad_steps(int32_t T) { return (int32_t)krca::ceil_div(T, BK) * BK; }
-constexpr int NSB = 16;  // column blocks in the threshold sample (2048 pods)
-// candidate workspace (4-byte words): values and indices [P][nb][KC] each, heads [P][nb][2],
-// sample lists [P][nsb][KC] x 2, phi [P]
-int64_t krca_corr_cand_size(int64_t P, int32_t k) {
-  const int64_t nb = krca_corr_pad_rows(P) / BM;
-  return P * nb * (2 * kc_for(k) + 2) + P * NSB * 2 * kc_for(k) + P;
+// candidate workspace (4-byte words): buf [P][CAPC] (r, partner) pairs, cnt [P], sample lists
+// [P][NSL][KC] x 2, selfd / phi / phi2 [P], over [P + 1], zs [RECT_ROWS][Tp] fp16
+int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k) {
+  const int64_t head = 2 * P * CAPC + P + 2 * P * NSL * kc_for(k) + 3 * P + P + 1;
+  return krca::ceil_div(head, 4) * 4 + (int64_t)RECT_ROWS * krca_corr_pad_steps(T) / 2;
 }
 int32_t krca_corr_max_k(void) { return KMAX; }
 float krca_corr_eps(int32_t T) {
@@ -734,31 +834,36 @@ int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t c
 
 int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, void* cand,
                    int32_t* count, int32_t* out_idx, float* out_val, float* cert, void* stream) {
-  KRCA_CHECK_ARG(P > 1 && krca_corr_pad_rows(P) <= 4096 * BM && T > 0,
-                 "krca_corr_topk: P must be in [2, %d]", 4096 * BM);
+  KRCA_CHECK_ARG(P > 1 && P <= (int64_t(1) << 22) && T > 0, "krca_corr_topk: P must be in [2, 2^22]");
   KRCA_CHECK_ARG(k >= 1 && k <= KMAX && k < P, "krca_corr_topk: k must be in [1, %d] and < P", KMAX);
+  KRCA_CHECK_ARG(tau >= 0.f, "krca_corr_topk: tau must be >= 0");
   KRCA_CHECK_ARG(zh && z32 && cand && count && out_idx && out_val && cert, "krca_corr_topk: null pointer");
   const int64_t Pp = krca_corr_pad_rows(P);
   const int Tp = krca_corr_pad_steps(T);
   const int nb = (int)(Pp / BM);
   const float eps = krca_corr_eps(T);
   const int nsb = nb < NSB ? nb : NSB;
-  const int KCr = kc_for(k);
-  const int64_t lists = P * nb;
-  float* cand_v = reinterpret_cast<float*>(cand);
-  int32_t* cand_i = reinterpret_cast<int32_t*>(cand_v + lists * KCr);
-  float* cand_hd = reinterpret_cast<float*>(cand_i + lists * KCr);
-  float* samp_v = cand_hd + lists * 2;
-  int32_t* samp_i = reinterpret_cast<int32_t*>(samp_v + P * NSB * KCr);
-  float* phi = reinterpret_cast<float*>(samp_i + P * NSB * KCr);
+  CorrWs ws;
+  const int KC = kc_for(k);
+  ws.buf = reinterpret_cast<int2*>(cand);
+  ws.cnt = reinterpret_cast<int32_t*>(ws.buf + P * CAPC);
+  ws.samp_v = reinterpret_cast<float*>(ws.cnt + P);
+  ws.samp_i = reinterpret_cast<int32_t*>(ws.samp_v + P * NSL * KC);
+  ws.selfd = reinterpret_cast<float*>(ws.samp_i + P * NSL * KC);
+  ws.phi = ws.selfd + P;
+  ws.phi2 = ws.phi + P;
+  ws.over = reinterpret_cast<int32_t*>(ws.phi2 + P);
+  const int64_t head = 2 * P * CAPC + P + 2 * P * NSL * KC + 3 * P + P + 1;
+  ws.zs = reinterpret_cast<uint16_t*>(reinterpret_cast<int32_t*>(cand) + krca::ceil_div(head, 4) * 4);
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(count, 0, P * sizeof(int32_t), st));
-  switch (kc_for(k)) {
-    case 8: return launch_corr<8>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, cand_v, cand_i, cand_hd, samp_v, samp_i, phi, count, out_idx, out_val, cert, st);
+  switch (KC) {
+    case 8:
+      return launch_corr<8>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, ws, count, out_idx, out_val, cert, st);
     case 12:
-      return launch_corr<12>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, cand_v, cand_i, cand_hd, samp_v, samp_i, phi, count, out_idx, out_val, cert, st);
+      return launch_corr<12>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, ws, count, out_idx, out_val, cert, st);
     default:
-      return launch_corr<16>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, cand_v, cand_i, cand_hd, samp_v, samp_i, phi, count, out_idx, out_val, cert, st);
+      return launch_corr<16>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, ws, count, out_idx, out_val, cert, st);
   }
 }
 

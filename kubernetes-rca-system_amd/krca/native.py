@@ -34,7 +34,7 @@ SIGNATURES = {
     "krca_template_max_lines": (c_i32, []),
     "krca_corr_pad_rows": (c_i64, [c_i64]),
     "krca_corr_pad_steps": (c_i32, [c_i32]),
-    "krca_corr_cand_size": (c_i64, [c_i64, c_i32]),
+    "krca_corr_cand_size": (c_i64, [c_i64, c_i32, c_i32]),
     "krca_corr_max_k": (c_i32, []),
     "krca_corr_eps": (c_f32, [c_i32]),
     "krca_corr_prepare": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -291,7 +291,7 @@ class NativeEngine:
         """Per-pod top-k |Pearson r| partners from corr_prepare_device's output (device, no sync)."""
         torch = self.torch
         P, T = z["P"], z["T"]
-        nc = self.lib.krca_corr_cand_size(P, int(k))
+        nc = self.lib.krca_corr_cand_size(P, T, int(k))
         cand = self._workspace("corr_cand", 4 * nc)
         if out is None:
             out = dict(idx=torch.empty((P, k), dtype=torch.int32, device=self.device),

@@ -1,3 +1,13 @@
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/dbg && export TMPDIR=/tmp && \
-KRCA_CORR_DEBUG=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/dbg/t1 -o run -- python3 tools/prof_kernels.py corr --pods 100000 --reps 2 > gpurun_out/dbg/c1.json 2>gpurun_out/dbg/e1.log && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/dbg/t0 -o run -- python3 tools/prof_kernels.py corr --pods 100000 --reps 2 > gpurun_out/dbg/c0.json 2>gpurun_out/dbg/e0.log; find gpurun_out/dbg -name '*trace.csv' -delete
+#!/bin/bash
+# GPU call: correlation product-only (KRCA_CORR_DEBUG=1) vs full, kernel-traced.
+set -u
+TAG=${1:-corrdbg}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+for d in 0 1 2 3; do
+  KRCA_CORR_DEBUG=$d timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_d$d -o run -- python3 tools/prof_kernels.py corr --pods 100000 --reps 3 > $OUT/corr_d$d.json 2> $OUT/err_d$d.log
+  rc=$?; echo "d$d EXIT=$rc" >> $OUT/status; [ $rc -eq 0 ] || exit $rc
+done
+find $OUT -name '*.db' -delete; find $OUT -name '*kernel_trace.csv' -delete

@@ -66,8 +66,11 @@ def main():
         ms = timed(torch, lambda: eng.corr_topk_device(z, 10, 0.5, out=r), a.reps)
         P, T = a.pods, a.tsteps
         flops = P * (P + 1) * T  # upper triangle incl. diagonal, 2 flops per MAC
+        ws = eng._ws["corr_cand"].view(torch.int32)
+        cnt = ws[2 * P * 1024: 2 * P * 1024 + P].float()  # candidates per pod (CAPC = 1024)
         out = dict(kernel="corr top-k", ms=ms, ms_prepare=ms_prep, flops=flops,
-                   tflops=flops / (min(ms) * 1e-3) / 1e12, certified=float((r["cert"] > 0).float().mean()))
+                   tflops=flops / (min(ms) * 1e-3) / 1e12, certified=float((r["cert"] > 0).float().mean()),
+                   cand_mean=float(cnt.mean()), cand_max=float(cnt.max()), cand_p99=float(cnt.quantile(0.99)))
     else:
         from krca.agents.logs import pack_documents
         docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
