@@ -118,6 +118,26 @@ int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t c
                       float* z32, uint16_t* zh, void* stream);
 int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, void* cand,
                    int32_t* count, int32_t* out_idx, float* out_val, float* cert, void* stream);
+/* a9 pod-sharded (kubernetes-rca-system_amd/krca/corr_dist.py): rank g of G owns pods
+ * [lo, lo + n_loc), lo a multiple of 256; zh / z32 / phi are the all-gathered full arrays.  The
+ * upper triangle is split by super-tile (every G-th from g); candidates travel to their pod's
+ * owner in one all-to-all of int4 {pod, partner, r bits, 0} entries; count and raw_cnt [P] are
+ * all-reduced (sum) by the caller.  ws: krca_corr_shard_ws_size(P, T, k, n_loc, G) 4-byte words. */
+int64_t krca_corr_shard_ws_size(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G);
+int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, int64_t lo, int64_t n_loc,
+                           int32_t G, void* ws, float* phi, void* stream);
+int krca_corr_shard_tiles(const uint16_t* zh, int64_t P, int32_t T, int32_t k, float tau, int32_t G, int32_t g,
+                          const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt,
+                          void* stream);
+int krca_corr_shard_pack_sizes(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t n_max, void* ws,
+                               int64_t* tot_host /*[G], synchronous*/, void* stream);
+int krca_corr_shard_pack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t n_max, void* ws,
+                         void* send, void* stream);
+int krca_corr_shard_unpack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t lo, void* ws,
+                           const void* recv, int64_t n_recv, void* stream);
+int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau,
+                          int64_t lo, int64_t n_loc, int32_t G, const float* phi, int32_t* lcnt, void* ws,
+                          int32_t* out_idx, float* out_val, float* cert, void* stream);
 
 /* ---- a10: personalized PageRank root-cause propagation (replaces the sink of
  * Coordinator._identify_root_causes, ref:agents/coordinator.py:157-184; networkx 3.4.2

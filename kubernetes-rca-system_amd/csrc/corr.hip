@@ -35,6 +35,7 @@
 // sample and main passes run the same K loop, so a pair's screening value is the same bits in both.
 #include <cmath>
 #include <cstdlib>
+#include <vector>
 
 #include "krca_common.h"
 
@@ -175,6 +176,15 @@ __device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ 
 //              whose buffer overflowed): row-side appends only, against phi = phi2.
 constexpr int MODE_MAIN = 0, MODE_SAMPLE = 1, MODE_RECT = 2;
 
+// Pod-sharded runs: rank g of G takes every G-th super-tile of the upper triangle
+// (MAIN), the row blocks [I0, ...) of its own pods (SAMPLE), and appends the candidates of its own
+// pods [lo, lo + n_loc) into local buffers indexed g - lo (RECT, merge).  Single device: {0, 1, 0, 0}.
+struct Shard {
+  int64_t lo;
+  int G, g;
+  int64_t I0;
+};
+
 template <int KC, int MODE>
 __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA, const uint16_t* __restrict__ zh,
                                                  int64_t P, int Tp, int nb2, int64_t per_xcd, int nsb, float tau,
@@ -182,7 +192,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
                                                  int32_t* __restrict__ samp_i, float* __restrict__ selfd,
                                                  int2* __restrict__ buf, int32_t* __restrict__ cnt,
                                                  int32_t* __restrict__ count, const int32_t* __restrict__ rect_pods,
-                                                 int64_t n_rect, int debug) {
+                                                 int64_t n_rect, Shard sh, int debug) {
   constexpr bool SAMPLE = MODE == MODE_SAMPLE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t I, J;
@@ -192,7 +202,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     J = blockIdx.x % nb2;
   } else if (SAMPLE) {
     const int nsb2 = (nsb + 1) / 2;
-    I = blockIdx.x / (nsb2 + 1);
+    I = sh.I0 + blockIdx.x / (nsb2 + 1);
     J = blockIdx.x % (nsb2 + 1);
     if (J == nsb2) {  // the row block's own 256-block, unless it is already a sample block
       if (I < nsb2) return;
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     const int64_t b = blockIdx.x;
     const int64_t L = (b & 7) * per_xcd + (b >> 3);
     const int64_t ns = (nb2 + SUPER - 1) / SUPER;
-    const int64_t st = L / (SUPER * SUPER);
+    const int64_t st = (L / (SUPER * SUPER)) * sh.G + sh.g;  // this rank's super-tiles
     if (st >= ns * (ns + 1) / 2) return;
     int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
     while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
@@ -356,8 +366,9 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
         if (slot < CAPW) {
           wlist[slot] = make_int4(pod, partner, __float_as_int(v), 0);
         } else {
-          const int gs = atomicAdd(&cnt[pod], 1);
-          if (gs < CAPC) buf[(int64_t)pod * CAPC + gs] = make_int2(__float_as_int(v), partner);
+          const int64_t lp = RECT ? pod - sh.lo : pod;
+          const int gs = atomicAdd(&cnt[lp], 1);
+          if (gs < CAPC) buf[lp * CAPC + gs] = make_int2(__float_as_int(v), partner);
         }
       }
       nlist += __builtin_popcountll(m);
@@ -458,6 +469,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
             const bool ok = q < wcount[u0 + u];
             more = more || base + NT < wcount[u0 + u];
             ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(-1, 0, 0, 0);
+            if (RECT && ok) ent[u].x -= (int)sh.lo;  // rect pass: the rank's local buffers
             gs[u] = ok ? atomicAdd(&cnt[ent[u].x], 1) : CAPC;
           }
 #pragma unroll
@@ -530,11 +542,11 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
 // A flat pod (self product 0: z = 0) gets phi = 3 (never a candidate owner; handled exactly).
 template <int KC>
 __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, const int32_t* __restrict__ si,
-                                                  const float* __restrict__ selfd, int64_t P, int nsb, int k,
-                                                  float eps, float* __restrict__ phi) {
-  const int64_t g = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+                                                  const float* __restrict__ selfd, int64_t g0, int64_t g1, int nsb,
+                                                  int k, float eps, float* __restrict__ phi) {
+  const int64_t g = g0 + (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (g >= P) return;
+  if (g >= g1) return;
   constexpr int PER = (NSL * KC + 63) / 64;
   float a[PER];
 #pragma unroll
@@ -597,18 +609,19 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
                                                   int64_t P, int T, int k, float eps, int pass,
                                                   const int32_t* __restrict__ pods, float* __restrict__ phi2,
                                                   int32_t* __restrict__ over, int32_t* __restrict__ out_i,
-                                                  float* __restrict__ out_v, float* __restrict__ cert) {
+                                                  float* __restrict__ out_v, float* __restrict__ cert, int64_t lo) {
   __shared__ float cv[CAPC];
   __shared__ int32_t ci[CAPC];
   __shared__ float top_v[KM + 1];
   __shared__ int32_t top_i[KM + 1];
   __shared__ double exact[KM];
   __shared__ int ord[KM];
-  const int64_t g = pods ? pods[blockIdx.x] : blockIdx.x;
+  const int64_t g = pods ? pods[blockIdx.x] : lo + blockIdx.x;  // global pod id
+  const int64_t gl = g - lo;  // index into this rank's buffers and outputs
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float ph = phi_used[g];
   const bool flat = ph > 2.f;
-  const int n = cnt[g];
+  const int n = cnt[gl];
   const bool overflow = n > CAPC;
   const int km = k + 6 < KM ? k + 6 : KM;
   if (flat) {  // r = 0 with every partner: the lowest other indices, in order
@@ -623,7 +636,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
     while (np < nn) np <<= 1;
     for (int i = tid; i < np; i += TPB) {
       if (i < nn) {
-        const int2 c = buf[g * CAPC + i];
+        const int2 c = buf[gl * CAPC + i];
         cv[i] = __int_as_float(c.x);
         ci[i] = c.y;
       } else {
@@ -654,7 +667,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
     if (overflow && pass == 0) {  // any stored subset bounds the exact k-th from below
       if (tid == 0) {
         phi2[g] = fabsf(cv[k - 1]) - 2.f * eps - 1e-6f;
-        cnt[g] = 0;
+        cnt[gl] = 0;
         over[1 + atomicAdd(&over[0], 1)] = (int32_t)g;
       }
       return;
@@ -705,13 +718,13 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
   }
   __syncthreads();
   for (int q = tid; q < k; q += TPB) {
-    out_i[g * k + q] = top_i[ord[q]];
-    out_v[g * k + q] = (float)exact[ord[q]];
+    out_i[gl * k + q] = top_i[ord[q]];
+    out_v[gl * k + q] = (float)exact[ord[q]];
   }
   if (tid == 0) {
     // everything not re-scored has a screening |r| <= max(phi, the first un-re-scored candidate)
     const float dropped = fmaxf(ph, top_i[km] >= 0 ? fabsf(top_v[km]) : 0.f);
-    cert[g] = flat ? 1.f
+    cert[gl] = flat ? 1.f
                    : overflow ? -1.f : (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
   }
 }
@@ -725,76 +738,208 @@ int debug_mode() {
 
 constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
 
-struct CorrWs {  // views into the caller's candidate workspace (4-byte words)
-  int2* buf;
-  int32_t *cnt, *samp_i, *over;
-  float *samp_v, *selfd, *phi, *phi2;
-  uint16_t* zs;  // [RECT_ROWS][Tp] gathered rows of the second pass
+// ---- exchange of the sharded run: candidates of pod p travel to its owner p / n_max ----------
+// totals per destination (clipped at CAPC: a pod past CAPC overflows at its owner anyway)
+__global__ __launch_bounds__(TPB) void corr_pack_count(const int32_t* __restrict__ cnt, int64_t P, int64_t n_max,
+                                                       unsigned long long* __restrict__ tot) {
+  const int64_t p = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (p >= P) return;
+  const int c = min(cnt[p], CAPC);
+  if (c) atomicAdd(&tot[p / n_max], (unsigned long long)c);
+}
+
+// one wave per pod: reserve its range in the destination's region, copy {pod, partner, r bits}
+__global__ __launch_bounds__(TPB) void corr_pack(const int32_t* __restrict__ cnt, const int2* __restrict__ buf, int64_t P,
+                                                 int64_t n_max, const unsigned long long* __restrict__ off,
+                                                 unsigned long long* __restrict__ cursor, int4* __restrict__ send) {
+  const int64_t p = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= P) return;
+  const int c = min(cnt[p], CAPC);
+  if (c == 0) return;
+  const int64_t h = p / n_max;
+  unsigned long long base = 0;
+  if (lane == 0) base = off[h] + atomicAdd(&cursor[h], (unsigned long long)c);
+  base = __shfl(base, 0, 64);
+  for (int i = lane; i < c; i += 64) {
+    const int2 e = buf[p * CAPC + i];
+    send[base + i] = make_int4((int)p, e.y, e.x, 0);
+  }
+}
+
+// received entries -> this rank's per-pod buffers (any order: the merge sorts)
+__global__ __launch_bounds__(TPB) void corr_unpack(const int4* __restrict__ recv, int64_t n, int64_t lo,
+                                                   int32_t* __restrict__ fill, int2* __restrict__ lbuf) {
+  const int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (e >= n) return;
+  const int4 v = recv[e];
+  const int64_t q = v.x - lo;
+  const int s = atomicAdd(&fill[q], 1);
+  if (s < CAPC) lbuf[q * CAPC + s] = make_int2(v.z, v.y);
+}
+
+struct CorrWs {  // views into a caller's candidate workspace
+  int2* buf;      // [P][CAPC] appends of the main pass (global pod index)
+  int32_t* cnt;   // [P]
+  float* samp_v;  // [P][NSL][KC]
+  int32_t* samp_i;
+  float *selfd, *phi2;  // [P]
+  int32_t* over;        // [n_loc + 1]
+  uint16_t* zs;         // [RECT_ROWS][Tp]
+  int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
+  int32_t* fill;        // sharded: [n_loc]
+  unsigned long long* xc;  // sharded: tot[G] | off[G] | cursor[G]
 };
 
+// layout in 4-byte words; sharded adds the local buffers and the exchange counters
+int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, CorrWs* ws) {
+  int64_t o = 0;
+  auto take = [&](int64_t words) {
+    char* ptr = base ? base + 4 * o : nullptr;
+    o += krca::ceil_div(words, 4) * 4;  // 16-byte aligned pieces
+    return ptr;
+  };
+  CorrWs w{};
+  w.buf = reinterpret_cast<int2*>(take(2 * P * CAPC));
+  w.cnt = reinterpret_cast<int32_t*>(take(P));
+  w.samp_v = reinterpret_cast<float*>(take(P * NSL * KC));
+  w.samp_i = reinterpret_cast<int32_t*>(take(P * NSL * KC));
+  w.selfd = reinterpret_cast<float*>(take(P));
+  w.phi2 = reinterpret_cast<float*>(take(P));
+  w.over = reinterpret_cast<int32_t*>(take(n_loc + 1));
+  w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
+  if (G > 0) {
+    w.lbuf = reinterpret_cast<int2*>(take(2 * n_loc * CAPC));
+    w.fill = reinterpret_cast<int32_t*>(take(n_loc));
+    w.xc = reinterpret_cast<unsigned long long*>(take(6 * (int64_t)G));
+  }
+  if (ws) *ws = w;
+  return o;
+}
+
 template <int KC>
-int launch_corr(const uint16_t* zh, const float* z32, int64_t P, int T, int Tp, int nb, int nsb, int k, float tau,
-                float eps, const CorrWs& ws, int32_t* count, int32_t* out_idx, float* out_val, float* cert,
-                hipStream_t st) {
-  static bool lds_attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
-  if (!lds_attr) {
+int set_lds_attr() {
+  static bool done = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
+  if (!done) {
     KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_MAIN>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
     KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_SAMPLE>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
     KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_RECT>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    lds_attr = true;
+    done = true;
   }
-  const int nb2 = nb / 2;
-  KRCA_HIP(hipMemsetAsync(ws.samp_i, 0xff, (size_t)P * NSL * KC * sizeof(int32_t), st));
-  KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)P * sizeof(int32_t), st));
+  return KRCA_OK;
+}
+
+struct Dims {
+  int64_t P;
+  int T, Tp, nb2, nsb, k;
+  float tau, eps;
+};
+
+Dims dims_of(int64_t P, int T, int k, float tau) {
+  Dims d;
+  d.P = P;
+  d.T = T;
+  d.Tp = (int)krca::ceil_div(T, BK) * BK;
+  d.nb2 = (int)krca::ceil_div(P, TB);
+  d.nsb = std::min(2 * d.nb2, NSB);
+  d.k = k;
+  d.tau = tau;
+  d.eps = (float)(std::ldexp(1.0, -10) * 1.001 + std::ldexp((double)T, -24) + std::ldexp(std::sqrt((double)T), -23));
+  return d;
+}
+
+// 1. threshold sample of the row blocks holding pods [lo, lo + n): phi for those pods
+template <int KC>
+int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const CorrWs& ws, float* phi,
+                 hipStream_t st) {
+  if (int rc = set_lds_attr<KC>()) return rc;
+  const int64_t I0 = lo / TB, I1 = krca::ceil_div(lo + n, TB);
+  const int nsb2 = (d.nsb + 1) / 2;
+  KRCA_HIP(hipMemsetAsync(ws.samp_i + lo * NSL * KC, 0xff, (size_t)n * NSL * KC * sizeof(int32_t), st));
+  const Shard sh{0, 1, 0, I0};
+  hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES, st,
+                     zh, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau, (const float*)nullptr, ws.samp_v, ws.samp_i,
+                     ws.selfd, (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
+                     (int64_t)0, sh, 0);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
+                     ws.samp_i, ws.selfd, lo, lo + n, d.nsb, d.k, d.eps, phi);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+// 2. upper-triangle tiles (every G-th super-tile from g): appends into ws.buf, tau counts
+template <int KC>
+int stage_tiles(const uint16_t* zh, const Dims& d, int G, int g, const float* phi, const CorrWs& ws, int32_t* count,
+                int dbg, hipStream_t st) {
+  if (int rc = set_lds_attr<KC>()) return rc;
+  KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
+  const int64_t ns = (d.nb2 + SUPER - 1) / SUPER;
+  const int64_t n_st = ns * (ns + 1) / 2;
+  const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
+  if (n_mine == 0) return KRCA_OK;
+  const int64_t per_xcd = (n_mine * SUPER * SUPER + 7) / 8;
+  const Shard sh{0, G, g, 0};
+  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, zh, d.P,
+                     d.Tp, d.nb2, per_xcd, d.nsb, d.tau, phi, (float*)nullptr, (int32_t*)nullptr, (float*)nullptr,
+                     ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, sh, dbg);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+// 3. per pod of [lo, lo + n): sort, exact re-scoring, top-k, certificate; overflowed pods get the
+//    rectangle pass (their rows x every column block against phi2) and a second merge.  Candidates
+//    in lbuf [n][CAPC] / lcnt [n] (raw counts).  Synchronises the stream once.
+template <int KC>
+int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo, int64_t n, const float* phi,
+                int2* lbuf, int32_t* lcnt, const CorrWs& ws, int32_t* out_idx, float* out_val, float* cert,
+                int dbg, hipStream_t st) {
+  if (n == 0) return KRCA_OK;
+  if (int rc = set_lds_attr<KC>()) return rc;
   KRCA_HIP(hipMemsetAsync(ws.over, 0, sizeof(int32_t), st));
-  KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.phi2), 0x40400000 /* 3.0f */, (size_t)P, st));
-  // 1. threshold sample: every pod against the first nsb column blocks and its own block
-  const int nsb2 = (nsb + 1) / 2;
-  hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)(nb2 * (nsb2 + 1))), dim3(NT), LDS_BYTES, st, zh,
-                     zh, P, Tp, nb2, (int64_t)0, nsb, tau, (const float*)nullptr, ws.samp_v, ws.samp_i, ws.selfd,
-                     (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, 0);
-  KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
-                     ws.samp_i, ws.selfd, P, nsb, k, eps, ws.phi);
-  KRCA_LAUNCH_CHECK();
-  // 2. all pairs (upper triangle): candidates above phi, |r| > tau counts
-  const int64_t ns = (nb2 + SUPER - 1) / SUPER;
-  const int64_t slots = ns * (ns + 1) / 2 * SUPER * SUPER;
-  const int64_t per_xcd = (slots + 7) / 8;
-  const int dbg = debug_mode();
-  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, zh, P,
-                     Tp, nb2, per_xcd, nsb, tau, (const float*)ws.phi, (float*)nullptr, (int32_t*)nullptr,
-                     (float*)nullptr, ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, dbg);
-  KRCA_LAUNCH_CHECK();
-  // 3. per pod: sort, exact re-scoring, top-k, certificate; overflowed pods are queued
-  hipLaunchKernelGGL(corr_merge, dim3((unsigned)P), dim3(TPB), 0, st, ws.buf, ws.cnt, (const float*)ws.phi, z32, P, T,
-                     k, eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert);
+  KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.phi2), 0x40400000 /* 3.0f */, (size_t)d.P, st));
+  hipLaunchKernelGGL(corr_merge, dim3((unsigned)n), dim3(TPB), 0, st, (const int2*)lbuf, lcnt, phi, z32, d.P, d.T,
+                     d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo);
   KRCA_LAUNCH_CHECK();
   int32_t n_over = 0;
   KRCA_HIP(hipMemcpyAsync(&n_over, ws.over, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   KRCA_HIP(hipStreamSynchronize(st));
-  // 4. overflowed pods only: their rows x every column block against phi2 (RECT_ROWS per launch)
-  for (int64_t r0 = 0; r0 < n_over && dbg == 0; r0 += RECT_ROWS) {
+  if (n_over == 0 || dbg != 0) return KRCA_OK;
+  const Shard sh{lo, 1, 0, 0};
+  for (int64_t r0 = 0; r0 < n_over; r0 += RECT_ROWS) {
     const int64_t nr = std::min<int64_t>(RECT_ROWS, n_over - r0);
     const int64_t npad = krca::ceil_div(nr, TB) * TB;
-    hipLaunchKernelGGL(corr_gather_rows, dim3((unsigned)npad), dim3(TPB), 0, st, zh, Tp,
+    hipLaunchKernelGGL(corr_gather_rows, dim3((unsigned)npad), dim3(TPB), 0, st, zh, d.Tp,
                        (const int32_t*)(ws.over + 1 + r0), nr, ws.zs);
     KRCA_LAUNCH_CHECK();
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * nb2)), dim3(NT), LDS_BYTES, st,
-                       (const uint16_t*)ws.zs, zh, P, Tp, nb2, (int64_t)0, nsb, tau, (const float*)ws.phi2,
-                       (float*)nullptr, (int32_t*)nullptr, (float*)nullptr, ws.buf, ws.cnt, count,
-                       (const int32_t*)(ws.over + 1 + r0), nr, 0);
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * d.nb2)), dim3(NT), LDS_BYTES, st,
+                       (const uint16_t*)ws.zs, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau,
+                       (const float*)ws.phi2, (float*)nullptr, (int32_t*)nullptr, (float*)nullptr, lbuf, lcnt,
+                       (int32_t*)nullptr, (const int32_t*)(ws.over + 1 + r0), nr, sh, 0);
     KRCA_LAUNCH_CHECK();
   }
-  if (n_over > 0 && dbg == 0) {
-    hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, ws.buf, ws.cnt, (const float*)ws.phi2,
-                       z32, P, T, k, eps, 1, (const int32_t*)(ws.over + 1), ws.phi2, ws.over, out_idx, out_val, cert);
-    KRCA_LAUNCH_CHECK();
-  }
+  hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,
+                     (const float*)ws.phi2, z32, d.P, d.T, d.k, d.eps, 1, (const int32_t*)(ws.over + 1), ws.phi2,
+                     ws.over, out_idx, out_val, cert, lo);
+  KRCA_LAUNCH_CHECK();
   return KRCA_OK;
+}
+
+template <int KC>
+int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, float* phi_unused, int32_t* count,
+               int32_t* out_idx, float* out_val, float* cert, hipStream_t st) {
+  (void)phi_unused;
+  CorrWs ws;
+  const int64_t head = ws_layout(d.P, d.Tp, KC, d.P, 0, cand, &ws);
+  float* phi = reinterpret_cast<float*>(cand + 4 * head);  // one more [P] after the layout
+  const int dbg = debug_mode();
+  if (int rc = stage_sample<KC>(zh, d, 0, d.P, ws, phi, st)) return rc;
+  if (int rc = stage_tiles<KC>(zh, d, 1, 0, phi, ws, count, dbg, st)) return rc;
+  return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
 }
 
 int kc_for(int32_t k) { return k <= 4 ? 8 : k <= 8 ? 12 : 16; }
@@ -805,11 +950,9 @@ extern "C" {
 
 int64_t krca_corr_pad_rows(int64_t P) { return krca::ceil_div(P, TB) * TB; }
 int32_t krca_corr_pad_steps(int32_t T) { return (int32_t)krca::ceil_div(T, BK) * BK; }
-// candidate workspace (4-byte words): buf [P][CAPC] (r, partner) pairs, cnt [P], sample lists
-// [P][NSL][KC] x 2, selfd / phi / phi2 [P], over [P + 1], zs [RECT_ROWS][Tp] fp16
+// single-device candidate workspace (4-byte words): see ws_layout, then phi [P]
 int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k) {
-  const int64_t head = 2 * P * CAPC + P + 2 * P * NSL * kc_for(k) + 3 * P + P + 1;
-  return krca::ceil_div(head, 4) * 4 + (int64_t)RECT_ROWS * krca_corr_pad_steps(T) / 2;
+  return ws_layout(P, krca_corr_pad_steps(T), kc_for(k), P, 0, nullptr, nullptr) + krca::ceil_div(P, 4) * 4;
 }
 int32_t krca_corr_max_k(void) { return KMAX; }
 float krca_corr_eps(int32_t T) {
@@ -838,33 +981,122 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
   KRCA_CHECK_ARG(k >= 1 && k <= KMAX && k < P, "krca_corr_topk: k must be in [1, %d] and < P", KMAX);
   KRCA_CHECK_ARG(tau >= 0.f, "krca_corr_topk: tau must be >= 0");
   KRCA_CHECK_ARG(zh && z32 && cand && count && out_idx && out_val && cert, "krca_corr_topk: null pointer");
-  const int64_t Pp = krca_corr_pad_rows(P);
-  const int Tp = krca_corr_pad_steps(T);
-  const int nb = (int)(Pp / BM);
-  const float eps = krca_corr_eps(T);
-  const int nsb = nb < NSB ? nb : NSB;
-  CorrWs ws;
-  const int KC = kc_for(k);
-  ws.buf = reinterpret_cast<int2*>(cand);
-  ws.cnt = reinterpret_cast<int32_t*>(ws.buf + P * CAPC);
-  ws.samp_v = reinterpret_cast<float*>(ws.cnt + P);
-  ws.samp_i = reinterpret_cast<int32_t*>(ws.samp_v + P * NSL * KC);
-  ws.selfd = reinterpret_cast<float*>(ws.samp_i + P * NSL * KC);
-  ws.phi = ws.selfd + P;
-  ws.phi2 = ws.phi + P;
-  ws.over = reinterpret_cast<int32_t*>(ws.phi2 + P);
-  const int64_t head = 2 * P * CAPC + P + 2 * P * NSL * KC + 3 * P + P + 1;
-  ws.zs = reinterpret_cast<uint16_t*>(reinterpret_cast<int32_t*>(cand) + krca::ceil_div(head, 4) * 4);
+  const Dims d = dims_of(P, T, k, tau);
   hipStream_t st = krca::as_stream(stream);
-  KRCA_HIP(hipMemsetAsync(count, 0, P * sizeof(int32_t), st));
-  switch (KC) {
-    case 8:
-      return launch_corr<8>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, ws, count, out_idx, out_val, cert, st);
-    case 12:
-      return launch_corr<12>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, ws, count, out_idx, out_val, cert, st);
-    default:
-      return launch_corr<16>(zh, z32, P, T, Tp, nb, nsb, k, tau, eps, ws, count, out_idx, out_val, cert, st);
+  char* c = reinterpret_cast<char*>(cand);
+  switch (kc_for(k)) {
+    case 8: return run_single<8>(zh, z32, d, c, nullptr, count, out_idx, out_val, cert, st);
+    case 12: return run_single<12>(zh, z32, d, c, nullptr, count, out_idx, out_val, cert, st);
+    default: return run_single<16>(zh, z32, d, c, nullptr, count, out_idx, out_val, cert, st);
   }
 }
+
+// ---- pod-sharded correlation (orchestrated by krca/corr_dist.py) -------------
+// Rank g owns pods [lo, lo + n_loc) (lo a multiple of 256).  Every rank holds the all-gathered
+// zh / z32 and phi.  Per run: shard_sample (phi of own pods) -> all-gather phi -> shard_tiles
+// (every G-th super-tile; candidates of ANY pod) -> all-reduce count and raw_cnt -> pack_sizes /
+// pack -> all-to-all by owner -> unpack -> shard_merge (own pods; may run the rectangle pass).
+int64_t krca_corr_shard_ws_size(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G) {
+  return ws_layout(P, krca_corr_pad_steps(T), kc_for(k), n_loc, G, nullptr, nullptr);
+}
+
+#define KRCA_CORR_SHARD_ARGS(name)                                                                        \
+  KRCA_CHECK_ARG(P > 1 && P <= (int64_t(1) << 22) && T > 0 && k >= 1 && k <= KMAX && k < P,               \
+                 name ": bad sizes");                                                                      \
+  KRCA_CHECK_ARG(n_loc >= 0 && G >= 1 && ws, name ": bad shard arguments");                                \
+  CorrWs w;                                                                                                \
+  ws_layout(P, krca_corr_pad_steps(T), kc_for(k), n_loc, G, reinterpret_cast<char*>(ws), &w);             \
+  hipStream_t st = krca::as_stream(stream);
+
+int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, int64_t lo, int64_t n_loc, int32_t G,
+                           void* ws, float* phi, void* stream) {
+  KRCA_CORR_SHARD_ARGS("krca_corr_shard_sample")
+  if (n_loc == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(zh && phi && lo % TB == 0 && lo + n_loc <= P, "krca_corr_shard_sample: bad range");
+  const Dims d = dims_of(P, T, k, 0.f);
+  switch (kc_for(k)) {
+    case 8: return stage_sample<8>(zh, d, lo, n_loc, w, phi, st);
+    case 12: return stage_sample<12>(zh, d, lo, n_loc, w, phi, st);
+    default: return stage_sample<16>(zh, d, lo, n_loc, w, phi, st);
+  }
+}
+
+int krca_corr_shard_tiles(const uint16_t* zh, int64_t P, int32_t T, int32_t k, float tau, int32_t G, int32_t g,
+                          const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt, void* stream) {
+  KRCA_CORR_SHARD_ARGS("krca_corr_shard_tiles")
+  KRCA_CHECK_ARG(zh && phi && count && raw_cnt && g >= 0 && g < G && tau >= 0.f, "krca_corr_shard_tiles: bad args");
+  const Dims d = dims_of(P, T, k, tau);
+  int rc;
+  switch (kc_for(k)) {
+    case 8: rc = stage_tiles<8>(zh, d, G, g, phi, w, count, 0, st); break;
+    case 12: rc = stage_tiles<12>(zh, d, G, g, phi, w, count, 0, st); break;
+    default: rc = stage_tiles<16>(zh, d, G, g, phi, w, count, 0, st);
+  }
+  if (rc) return rc;
+  KRCA_HIP(hipMemcpyAsync(raw_cnt, w.cnt, (size_t)P * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  return KRCA_OK;
+}
+
+// entries (int4 {pod, partner, r bits, 0}) this rank sends to each owner; synchronises the stream
+int krca_corr_shard_pack_sizes(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t n_max, void* ws,
+                               int64_t* tot_host, void* stream) {
+  KRCA_CORR_SHARD_ARGS("krca_corr_shard_pack_sizes")
+  KRCA_CHECK_ARG(tot_host && n_max > 0 && n_max * G >= P, "krca_corr_shard_pack_sizes: bad args");
+  KRCA_HIP(hipMemsetAsync(w.xc, 0, 3 * (size_t)G * sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(corr_pack_count, dim3((unsigned)krca::ceil_div(P, TPB)), dim3(TPB), 0, st, (const int32_t*)w.cnt,
+                     P, n_max, w.xc);
+  KRCA_LAUNCH_CHECK();
+  std::vector<unsigned long long> tot(G), off(G);
+  KRCA_HIP(hipMemcpyAsync(tot.data(), w.xc, G * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  KRCA_HIP(hipStreamSynchronize(st));
+  unsigned long long acc = 0;
+  for (int h = 0; h < G; ++h) {
+    off[h] = acc;
+    acc += tot[h];
+    tot_host[h] = (int64_t)tot[h];
+  }
+  KRCA_HIP(hipMemcpyAsync(w.xc + G, off.data(), G * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+  KRCA_HIP(hipStreamSynchronize(st));  // off[] is a stack copy
+  return KRCA_OK;
+}
+
+int krca_corr_shard_pack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t n_max, void* ws,
+                         void* send, void* stream) {
+  KRCA_CORR_SHARD_ARGS("krca_corr_shard_pack")
+  KRCA_CHECK_ARG(send && n_max > 0, "krca_corr_shard_pack: bad args");
+  hipLaunchKernelGGL(corr_pack, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, (const int32_t*)w.cnt,
+                     (const int2*)w.buf, P, n_max, (const unsigned long long*)(w.xc + G), w.xc + 2 * G,
+                     reinterpret_cast<int4*>(send));
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_corr_shard_unpack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t lo, void* ws,
+                           const void* recv, int64_t n_recv, void* stream) {
+  KRCA_CORR_SHARD_ARGS("krca_corr_shard_unpack")
+  KRCA_CHECK_ARG(n_recv >= 0 && (recv || n_recv == 0), "krca_corr_shard_unpack: bad args");
+  KRCA_HIP(hipMemsetAsync(w.fill, 0, (size_t)std::max<int64_t>(n_loc, 1) * sizeof(int32_t), st));
+  if (n_recv == 0) return KRCA_OK;
+  hipLaunchKernelGGL(corr_unpack, dim3((unsigned)krca::ceil_div(n_recv, TPB)), dim3(TPB), 0, st,
+                     reinterpret_cast<const int4*>(recv), n_recv, lo, w.fill, w.lbuf);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+// own pods: lcnt = this rank's slice of the all-reduced raw counts ([n_loc], may be reset here)
+int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau,
+                          int64_t lo, int64_t n_loc, int32_t G, const float* phi, int32_t* lcnt, void* ws,
+                          int32_t* out_idx, float* out_val, float* cert, void* stream) {
+  KRCA_CORR_SHARD_ARGS("krca_corr_shard_merge")
+  KRCA_CHECK_ARG(zh && z32 && phi && lcnt && out_idx && out_val && cert && lo + n_loc <= P,
+                 "krca_corr_shard_merge: bad args");
+  const Dims d = dims_of(P, T, k, tau);
+  switch (kc_for(k)) {
+    case 8: return stage_merge<8>(zh, z32, d, lo, n_loc, phi, w.lbuf, lcnt, w, out_idx, out_val, cert, 0, st);
+    case 12: return stage_merge<12>(zh, z32, d, lo, n_loc, phi, w.lbuf, lcnt, w, out_idx, out_val, cert, 0, st);
+    default: return stage_merge<16>(zh, z32, d, lo, n_loc, phi, w.lbuf, lcnt, w, out_idx, out_val, cert, 0, st);
+  }
+}
+#undef KRCA_CORR_SHARD_ARGS
 
 }  // extern "C"

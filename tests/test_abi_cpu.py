@@ -70,3 +70,16 @@ def test_no_cpu_fallback_without_device():
         assert "no CPU fallback" in str(e)
     else:
         raise AssertionError("NativeEngine must refuse to run without a HIP device")
+
+
+def test_corr_shard_ranges_tile_aligned_and_cover():
+    from krca.corr_dist import TB, corr_shard_range
+    for P in (2, 255, 256, 257, 6000, 100_000, 1_000_000):
+        for G in (1, 2, 3, 8):
+            spans = [corr_shard_range(P, G, g) for g in range(G)]
+            assert spans[0][0] == 0 and spans[-1][1] == P
+            for (lo, hi, n_max), (lo2, _, _) in zip(spans, spans[1:]):
+                assert hi == lo2 and n_max % TB == 0 and (lo % TB == 0 or lo == hi == P)
+    lib = native.load_library()
+    assert lib.krca_corr_shard_ws_size(100_000, 1440, 10, 12_544, 8) > lib.krca_corr_shard_ws_size(100_000, 1440, 10,
+                                                                                                     0, 8)

@@ -93,3 +93,17 @@ def test_corr_rejects_bad_k(eng):
         eng.corr_topk(x, k=17)
     with pytest.raises(native.KrcaError):
         eng.corr_topk(x, k=10)  # k must be < P
+
+
+@pytest.mark.parametrize("P,T,G", [(6000, 1440, 2), (6000, 1440, 3), (1000, 100, 4), (300, 64, 2)])
+def test_corr_sharded_path_emulated_on_one_gpu(eng, P, T, G):
+    """The pod-sharded correlation (krca/corr_dist.py: G super-tile shares of the triangle, one
+    all-to-all of candidates by owner) with the collectives done by copies: every output equals
+    the single-device run (same screening products, same candidate sets, same merge)."""
+    from krca.corr_dist import run_emulated
+    x = synth.make_metrics(P, 2, T, seed=P + G, group_size=20).cuda()
+    x[:, 3, 0] = 42.0  # a flat series
+    ref = eng.corr_topk(x, k=10, tau=TAU, channel=0)
+    got = run_emulated(eng, x, P, T, 10, TAU, G, channel=0)
+    for key in ("idx", "val", "count", "cert"):
+        assert np.array_equal(got[key], ref[key]), key
