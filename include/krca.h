@@ -187,6 +187,14 @@ int krca_topk_f32(const float* v, int64_t N, int32_t k, void* workspace, int32_t
 int krca_topk_i64(const int64_t* v, int64_t N, int32_t k, void* workspace, int32_t* idx, int64_t* val,
                   void* stream);
 
+/* ---- f1: pod status categorisation (ResourceAnalyzer._analyze_pods + _is_pod_healthy,
+ * ref:agents/resource_analyzer.py:264-380, :856-895) over columnar pod status (encoding in
+ * csrc/podstate.hip and krca/podstate.py): mask[p] bit b = membership of status group b in the
+ * reference's dict order; hist[krca_pod_groups()] = group sizes.  Bit-exact. */
+int32_t krca_pod_groups(void);
+int krca_pod_classify(const uint8_t* pod_code, const int64_t* cont_off, const uint16_t* cont_code, int64_t P,
+                      uint16_t* mask, int32_t* hist, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,18 +1,19 @@
 """ResourceAnalyzer (host, first slice): namespace resource health.
 
 Reference: ref:agents/resource_analyzer.py:15-959, called by the UI path through
-``MCPCoordinator.run_resource_analysis`` (ref:agents/mcp_coordinator.py:590).  SURVEY.md §8f f1
-schedules the per-pod categorisation (``_analyze_pods`` :264-380) as a later columnar kernel;
-this first slice keeps the reference's semantics on the host, including its quirks (a pod can
-sit in both the ``failed`` and ``error`` groups and is then reported twice; the non-standard
-phase ``CrashLoopBackOff`` is not categorised).  The reference's ``logging`` to a file in the
-CWD is not reproduced.
+``MCPCoordinator.run_resource_analysis`` (ref:agents/mcp_coordinator.py:590).  The per-pod
+categorisation (``_analyze_pods`` :264-380 with ``_is_pod_healthy`` :856-895)
+runs on the device: the pods are encoded once into columnar status (krca/podstate.py) and
+krca_pod_classify returns each pod's group memberships; the group lists keep the reference's
+order and its quirks (a pod can sit in both the ``failed`` and ``error`` groups and is then
+reported twice; the non-standard phase ``CrashLoopBackOff`` is not categorised).  The per-group
+findings stay on the host.  The reference's ``logging`` to a file in the CWD is not reproduced.
 """
 import json
 from datetime import datetime
 
-_GROUPS = ('pending', 'running', 'succeeded', 'failed', 'unknown', 'crashloopbackoff', 'imagepullbackoff',
-           'containercreating', 'error', 'evicted', 'init_crashloopbackoff', 'not_ready')
+from .. import podstate
+
 _RELATION_KEYWORDS = {  # ref :774-781
     'crash': ['backoff', 'crash', 'exit', 'fail', 'error'],
     'scheduling': ['schedule', 'resource', 'affinity', 'taint', 'toleration'],
@@ -139,52 +140,16 @@ class ResourceAnalyzer:
                                  "Check for node taints or affinity issues")
 
     # -- pod categorisation (ref :264-380) -------------------------------------------------
+    def _eng(self):
+        if self._engine is None:
+            from ..native import default_engine
+            self._engine = default_engine()
+        return self._engine
+
     def categorize_pods(self, pods):
-        groups = {g: [] for g in _GROUPS}
-        for pod in pods:
-            st = pod['status']
-            phase = st.get('phase', 'Unknown')
-            if phase == 'Pending':
-                groups['pending'].append(pod)
-            elif phase == 'Running':
-                if self._is_pod_healthy(pod):
-                    groups['running'].append(pod)
-                else:
-                    for cs in st.get('containerStatuses', []) + st.get('initContainerStatuses', []):
-                        state = cs.get('state', {})
-                        if 'waiting' not in state:
-                            continue
-                        reason = state['waiting'].get('reason', '')
-                        if reason == 'CrashLoopBackOff':
-                            groups['init_crashloopbackoff' if cs['name'].startswith('init-')
-                                   else 'crashloopbackoff'].append(pod)
-                            break
-                        if reason in ('ImagePullBackOff', 'ErrImagePull'):
-                            groups['imagepullbackoff'].append(pod)
-                            break
-                        if reason == 'ContainerCreating':
-                            groups['containercreating'].append(pod)
-                            break
-                    ready = True
-                    for cond in st.get('conditions', []):
-                        if cond.get('type') == 'Ready' and cond.get('status') != 'True':
-                            ready = False
-                            break
-                    if not ready:
-                        groups['not_ready'].append(pod)
-            elif phase == 'Succeeded':
-                groups['succeeded'].append(pod)
-            elif phase == 'Failed':
-                groups['failed'].append(pod)
-            elif phase == 'Unknown':
-                groups['unknown'].append(pod)
-            if st.get('reason', '') == 'Evicted':
-                groups['evicted'].append(pod)
-            for cs in st.get('containerStatuses', []):
-                if cs.get('state', {}).get('terminated', {}).get('reason', '') == 'Error':
-                    groups['error'].append(pod)
-                    break
-        return groups
+        """status_groups of ref :274-343, from the device's per-pod group masks."""
+        mask, _ = self._eng().pod_classify(*podstate.encode_pods(pods))
+        return podstate.groups_from_masks(pods, mask)
 
     def _analyze_pods(self, pods, namespace):
         g = self.categorize_pods(pods)

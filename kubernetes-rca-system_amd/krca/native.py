@@ -64,6 +64,8 @@ SIGNATURES = {
     "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "krca_pod_groups": (c_i32, []),
+    "krca_pod_classify": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "krca_topk_workspace_size": (c_i64, [c_i64, c_i32]),
     "krca_topk_f32": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "krca_topk_i64": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
@@ -198,6 +200,27 @@ class NativeEngine:
             return np.zeros((0, x.shape[2]), np.float32)
         sel = self._dev(idx)
         return x[x.shape[0] - 1].index_select(0, sel).cpu().numpy()
+
+    # -- f1 pod status groups ------------------------------------------------------------------
+    def pod_classify_device(self, pod_code, cont_off, cont_code):
+        """Columnar pod status (device tensors) -> (mask u16 [P] device, hist i32 [12] device)."""
+        torch = self.torch
+        P = int(pod_code.numel())
+        mask = torch.empty(max(P, 1), dtype=torch.int16, device=self.device)
+        hist = torch.empty(self.lib.krca_pod_groups(), dtype=torch.int32, device=self.device)
+        _check(self.lib.krca_pod_classify(self.ptr(pod_code), self.ptr(cont_off), self.ptr(cont_code), P,
+                                          self.ptr(mask), self.ptr(hist), self._stream()), "krca_pod_classify")
+        return mask[:P], hist
+
+    def pod_classify(self, pod_code, cont_off, cont_code):
+        """Host arrays in, host (mask uint16 [P], hist int32 [12]) out."""
+        t = self.torch
+        cc = np.asarray(cont_code, np.uint16)
+        m, h = self.pod_classify_device(self._dev(np.asarray(pod_code, np.uint8)),
+                                        self._dev(np.asarray(cont_off, np.int64)),
+                                        self._dev(cc.view(np.int16) if len(cc) else np.zeros(1, np.int16)))
+        del t
+        return m.cpu().numpy().view(np.uint16), h.cpu().numpy()
 
     # -- top-k -------------------------------------------------------------------------------
     def topk_device(self, v, k):

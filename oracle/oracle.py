@@ -10,6 +10,9 @@ Parity anchors:
   * thresholds: pinned by tests/golden/metrics_scaled.json and the C1 goldens;
   * PageRank: :func:`ppr_f64` is the networkx 3.4.2 ``_pagerank_scipy`` iteration in float64,
     pinned by tests/golden/ppr_known.json (networkx on the reference's mock dependency map);
+  * pod status groups: :func:`categorize_pods_ref` restates ref:agents/resource_analyzer.py:
+    264-380 + :856-895 on pod dicts (pinned by the C1 ResourceAnalyzer golden), and
+    :func:`pod_classify_ref` the same rules on the columnar encoding of krca/podstate.py;
   * rolling z-score / correlation / template hashing have no reference counterpart (new
     primitives named by the north star): their float64 restatements here are
     "parity unpinned" by the reference and define the semantics.
@@ -186,6 +189,124 @@ def corr_rows(z, rows, k, tau):
         gap[n] = a[n][o[k - 1]] - (a[n][o[k]] if len(o) > k else -1.0)
     r = np.take_along_axis(R, idx, axis=1)
     return idx.astype(np.int32), r, count, gap
+
+
+# ------------------------------------------------------------------------------------------
+# f1: pod status groups (ref:agents/resource_analyzer.py:264-380, _is_pod_healthy :856-895)
+# ------------------------------------------------------------------------------------------
+POD_GROUPS = ('pending', 'running', 'succeeded', 'failed', 'unknown', 'crashloopbackoff', 'imagepullbackoff',
+              'containercreating', 'error', 'evicted', 'init_crashloopbackoff', 'not_ready')
+
+
+def _pod_healthy_ref(pod):  # ref :856-895
+    st = pod['status']
+    if st.get('phase', '') != 'Running':
+        return False
+    ready = next((c for c in st.get('conditions', []) if c.get('type') == 'Ready'), None)
+    if not ready or ready.get('status') != 'True':
+        return False
+    css = st.get('containerStatuses', [])
+    if not css:
+        return False
+    for cs in css:
+        if not cs.get('ready', False):
+            return False
+        state = cs.get('state', {})
+        if 'waiting' in state:
+            return False
+        if 'terminated' in state and state['terminated'].get('reason', '') != 'Completed':
+            return False
+    return True
+
+
+def categorize_pods_ref(pods):
+    """ref :289-343 on pod dicts -> {group: [pod index, ...]} in the reference's order."""
+    g = {k: [] for k in POD_GROUPS}
+    for i, pod in enumerate(pods):
+        st = pod['status']
+        phase = st.get('phase', 'Unknown')
+        if phase == 'Pending':
+            g['pending'].append(i)
+        elif phase == 'Running':
+            if not _pod_healthy_ref(pod):
+                for cs in st.get('containerStatuses', []) + st.get('initContainerStatuses', []):
+                    state = cs.get('state', {})
+                    if 'waiting' in state:
+                        reason = state['waiting'].get('reason', '')
+                        if reason == 'CrashLoopBackOff':
+                            g['init_crashloopbackoff' if cs['name'].startswith('init-') else 'crashloopbackoff'].append(i)
+                            break
+                        elif reason == 'ImagePullBackOff' or reason == 'ErrImagePull':
+                            g['imagepullbackoff'].append(i)
+                            break
+                        elif reason == 'ContainerCreating':
+                            g['containercreating'].append(i)
+                            break
+                ready = True
+                for cond in st.get('conditions', []):
+                    if cond.get('type') == 'Ready' and cond.get('status') != 'True':
+                        ready = False
+                        break
+                if not ready:
+                    g['not_ready'].append(i)
+            else:
+                g['running'].append(i)
+        elif phase == 'Succeeded':
+            g['succeeded'].append(i)
+        elif phase == 'Failed':
+            g['failed'].append(i)
+        elif phase == 'Unknown':
+            g['unknown'].append(i)
+        if st.get('reason', '') == 'Evicted':
+            g['evicted'].append(i)
+        for cs in st.get('containerStatuses', []):
+            if cs.get('state', {}).get('terminated', {}).get('reason', '') == 'Error':
+                g['error'].append(i)
+                break
+    return g
+
+
+def pod_classify_ref(pod_code, cont_off, cont_code):
+    """The same rules on the columnar encoding -> (mask u16[P], hist i32[12])."""
+    P = len(pod_code)
+    mask = np.zeros(P, np.uint16)
+    for p in range(P):
+        pc = int(pod_code[p])
+        cc = [int(x) for x in cont_code[cont_off[p]:cont_off[p + 1]]]
+        main = [x for x in cc if not x & 1]
+        phase, m = pc & 7, 0
+        if phase == 0:
+            m |= 1
+        elif phase == 1:
+            healthy = bool(pc & 8) and len(main) > 0 and all(
+                (x & 2) and not (x & 4) and not ((x & 8) and ((x >> 7) & 3) != 1) for x in main)
+            if healthy:
+                m |= 2
+            else:
+                for x in cc:
+                    if not x & 4:
+                        continue
+                    wr = (x >> 4) & 7
+                    if wr == 1:
+                        m |= 1 << (10 if x & 512 else 5)
+                        break
+                    if wr in (2, 3):
+                        m |= 1 << 6
+                        break
+                    if wr == 4:
+                        m |= 1 << 7
+                        break
+                if pc & 16:
+                    m |= 1 << 11
+        elif phase in (2, 3, 4):
+            m |= 1 << phase
+        if pc & 32:
+            m |= 1 << 9
+        if any((x & 8) and ((x >> 7) & 3) == 2 for x in main):
+            m |= 1 << 8
+        mask[p] = m
+    hist = np.array([int(((mask >> b) & 1).sum()) for b in range(12)], np.int32)
+    return mask, hist
 
 
 # ------------------------------------------------------------------------------------------

@@ -132,9 +132,56 @@ def check_c1_other(engine):
     return bad
 
 
-def check_resource():
+def check_resource(engine):
     gold = load("c1_resource.json")
-    return [ns for ns in gold if not same(ResourceAnalyzer(MockK8sClient()).analyze_namespace_resources(ns), gold[ns])]
+    return [ns for ns in gold
+            if not same(ResourceAnalyzer(MockK8sClient(), engine=engine).analyze_namespace_resources(ns), gold[ns])]
+
+
+def random_pods(n, seed=0):
+    """Pod dicts covering every branch of the reference's categorisation (f1 parity cases)."""
+    import random
+    rnd = random.Random(seed)
+    phases = ['Pending', 'Running', 'Running', 'Running', 'Succeeded', 'Failed', 'Unknown', 'CrashLoopBackOff', None]
+    waits = ['CrashLoopBackOff', 'ImagePullBackOff', 'ErrImagePull', 'ContainerCreating', 'PodInitializing', '']
+    terms = ['Completed', 'Error', 'OOMKilled', '']
+
+    def status(name):
+        st = {}
+        r = rnd.random()
+        if r < 0.3:
+            st['waiting'] = {'reason': rnd.choice(waits)} if rnd.random() < 0.9 else {}
+        elif r < 0.5:
+            st['terminated'] = {'reason': rnd.choice(terms)} if rnd.random() < 0.9 else {}
+        elif r < 0.9:
+            st['running'] = {}
+        if rnd.random() < 0.05:
+            st['waiting'] = {'reason': rnd.choice(waits)}
+            st['terminated'] = {'reason': rnd.choice(terms)}
+        cs = {'name': name, 'state': st}
+        if rnd.random() < 0.9:
+            cs['ready'] = rnd.random() < 0.8
+        return cs
+
+    pods = []
+    for i in range(n):
+        st = {}
+        ph = rnd.choice(phases)
+        if ph is not None:
+            st['phase'] = ph
+        conds = []
+        for _ in range(rnd.randint(0, 3)):
+            conds.append({'type': rnd.choice(['Ready', 'PodScheduled', 'Initialized']),
+                          'status': rnd.choice(['True', 'False', 'Unknown'])})
+        st['conditions'] = conds
+        if rnd.random() < 0.9:
+            st['containerStatuses'] = [status(rnd.choice(['app', 'sidecar', 'init-db'])) for _ in range(rnd.randint(0, 3))]
+        if rnd.random() < 0.4:
+            st['initContainerStatuses'] = [status(rnd.choice(['init-x', 'setup'])) for _ in range(rnd.randint(0, 2))]
+        if rnd.random() < 0.05:
+            st['reason'] = 'Evicted'
+        pods.append({'metadata': {'name': f'pod-{i}'}, 'status': st})
+    return pods
 
 
 def check_logs_corpus(engine):

@@ -52,3 +52,6 @@ class OracleEngine:
         rf, r, _ = oracle.c_ppr(row_ptr, col, outdeg, seed, alpha, max_iter, tol)
         idx, _ = oracle.topk_ref(r, k)
         return idx, rf[idx]
+
+    def pod_classify(self, pod_code, cont_off, cont_code):
+        return oracle.pod_classify_ref(pod_code, cont_off, cont_code)

@@ -22,7 +22,20 @@ def test_c1_other_namespaces_and_unknown_type():
 
 
 def test_resource_analyzer():
-    assert A.check_resource() == []
+    assert A.check_resource(ENG) == []
+
+
+def test_pod_status_columns_restate_the_reference():
+    """f1: the columnar encoding + classification rules (oracle) == the reference's dict walk."""
+    import oracle
+    from krca import podstate
+    pods = A.random_pods(3000, seed=5)
+    ref = oracle.categorize_pods_ref(pods)
+    mask, hist = oracle.pod_classify_ref(*podstate.encode_pods(pods))
+    got = podstate.groups_from_masks(list(range(len(pods))), mask)
+    assert got == ref
+    assert hist.tolist() == [len(ref[g]) for g in oracle.POD_GROUPS]
+    assert all(len(ref[g]) for g in oracle.POD_GROUPS)  # every group exercised
 
 
 def test_logs_corpus_findings():

@@ -36,6 +36,41 @@ def test_topology(eng):
     assert A.check_topology(eng) == []
 
 
+def test_resource_analyzer_c1(eng):
+    assert A.check_resource(eng) == []
+
+
+def test_pod_classify_random_dicts(eng):
+    """f1 kernel on every branch of the reference's categorisation (dict walk restated in oracle)."""
+    import oracle
+    from krca import podstate
+    pods = A.random_pods(5000, seed=9)
+    mask, hist = eng.pod_classify(*podstate.encode_pods(pods))
+    assert podstate.groups_from_masks(list(range(len(pods))), mask) == oracle.categorize_pods_ref(pods)
+    ref_mask, ref_hist = oracle.pod_classify_ref(*podstate.encode_pods(pods))
+    assert (mask == ref_mask).all() and (hist == ref_hist).all()
+
+
+@pytest.mark.parametrize("P", [0, 1, 255, 300_000, 3_000_000])
+def test_pod_classify_columnar_scale(eng, P):
+    import numpy as np
+
+    import oracle
+    from krca import podstate
+    pc, off, cc = podstate.make_pod_states(P, seed=P)
+    mask, hist = eng.pod_classify(pc, off, cc)
+    sample = np.arange(P) if P <= 300_000 else np.random.default_rng(0).choice(P, 20000, replace=False)
+    if P <= 300_000:
+        ref_mask, ref_hist = oracle.pod_classify_ref(pc, off, cc)
+        assert (mask == ref_mask).all() and (hist == ref_hist).all()
+    else:  # sampled rows exact; histogram = the popcount of the kernel's own masks
+        sub_off = np.concatenate([[0], np.cumsum(off[sample + 1] - off[sample])])
+        sub_cc = np.concatenate([cc[off[i]:off[i + 1]] for i in sample])
+        ref_mask, _ = oracle.pod_classify_ref(pc[sample], sub_off, sub_cc)
+        assert (mask[sample] == ref_mask).all()
+        assert hist.tolist() == [int(((mask >> b) & 1).sum()) for b in range(12)]
+
+
 def test_ranked_root_causes_c1(eng):
     res = A.Coordinator(A.Shim(), engine=eng).run_analysis("comprehensive", A.NS)
     assert [r["component"] for r in res["ranked_root_causes"]] == [

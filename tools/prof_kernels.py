@@ -13,6 +13,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
 
@@ -29,7 +31,7 @@ def timed(torch, fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["score", "ppr", "logs", "corr"])
+    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods"])
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--docs", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=3)
@@ -71,6 +73,16 @@ def main():
         out = dict(kernel="corr top-k", ms=ms, ms_prepare=ms_prep, flops=flops,
                    tflops=flops / (min(ms) * 1e-3) / 1e12, certified=float((r["cert"] > 0).float().mean()),
                    cand_mean=float(cnt.mean()), cand_max=float(cnt.max()), cand_p99=float(cnt.quantile(0.99)))
+    elif a.what == "pods":
+        from krca import podstate
+        P = a.pods * 10
+        pc, off, cc = podstate.make_pod_states(P, seed=0)
+        d = [torch.from_numpy(pc).cuda(), torch.from_numpy(off).cuda(), torch.from_numpy(cc.view(np.int16)).cuda()]
+        eng.pod_classify_device(*d)
+        ms = timed(torch, lambda: eng.pod_classify_device(*d), a.reps)
+        nbytes = P * (1 + 8 + 2) + 8 + 2 * len(cc)
+        out = dict(kernel="krca_pod_classify", pods=P, containers=len(cc), ms=ms, bytes=nbytes,
+                   gbs=nbytes / (min(ms) * 1e-3) / 1e9)
     else:
         from krca.agents.logs import pack_documents
         docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
