@@ -168,6 +168,9 @@ int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* o
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
                         int64_t* r_local, int64_t* send /*[n_max+nslot]*/, void* stream);
+int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
+                             int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
+                             const int64_t* r_local /*start vector: the previous solve*/, int64_t* send, void* stream);
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int64_t* plan,
                         int64_t plan_len, const int64_t* w_all /*[G][n_max+nslot]*/, const int32_t* outdeg,
                         const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
@@ -186,6 +189,15 @@ int krca_topk_f32(const float* v, int64_t N, int32_t k, void* workspace, int32_t
                   void* stream);
 int krca_topk_i64(const int64_t* v, int64_t N, int32_t k, void* workspace, int32_t* idx, int64_t* val,
                   void* stream);
+
+/* ---- streaming rescoring (BASELINE configs[4]): krca_rolling_score carried
+ * forward over a stream, delta new steps [delta][P][M] per call, global steps t0 .. t0+delta-1
+ * (t0 == 0 starts the stream).  Outputs as krca_rolling_score over the whole series so far, with
+ * n_exceed counted over the last H evaluated steps.  state: krca_stream_state_size bytes. */
+int64_t krca_stream_state_size(int64_t P, int32_t M, int32_t W, int32_t H);
+int krca_stream_score(const float* x_new, int64_t P, int32_t M, int32_t delta, int64_t t0, int32_t W, int32_t H,
+                      float z_thr, void* state, float* z_last, float* score, int32_t* n_exceed, uint8_t* flags,
+                      void* stream);
 
 /* ---- f1: pod status categorisation (ResourceAnalyzer._analyze_pods + _is_pod_healthy,
  * ref:agents/resource_analyzer.py:264-380, :856-895) over columnar pod status (encoding in

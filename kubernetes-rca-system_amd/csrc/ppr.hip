@@ -115,6 +115,31 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
   }
 }
 
+// warm start (streaming re-ranking): keep r from the previous solve, new seeds, w and dangling
+// mass from the kept r (networkx's nstart, taken as the fixed-point vector itself)
+__global__ __launch_bounds__(TPB) void ppr_init_warm(const float* __restrict__ seed, float seed_floor,
+                                                     const int32_t* __restrict__ outdeg, int64_t n, double alpha,
+                                                     int64_t* __restrict__ q, const int64_t* __restrict__ r,
+                                                     int64_t* __restrict__ send, int64_t n_max) {
+  __shared__ int64_t red[TPB / 64];
+  int64_t dang = 0, qs = 0;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const int32_t deg = outdeg[i];
+    const int64_t qi = quantise(seed[i], seed_floor);
+    q[i] = qi;
+    qs += qi;
+    const int64_t ri = r[i];
+    send[i] = edge_weight(ri, deg, alpha);
+    if (deg == 0) dang += ri;
+  }
+  dang = block_sum_i64(dang, red);
+  qs = block_sum_i64(qs, red);
+  if (threadIdx.x == 0) {
+    add_slot(send + n_max + NSPREAD, dang);
+    add_slot(send + n_max + 2 * NSPREAD, qs);
+  }
+}
+
 struct StepScalars {
   double tele, qtot, uni, alpha;
   int64_t qt;
@@ -373,6 +398,23 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
   KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N,
+                       alpha, q_local, r_local, send, n_max);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
+                             int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
+                             const int64_t* r_local, int64_t* send, void* stream) {
+  KRCA_CHECK_ARG(N > 0 && N < INT32_MAX && n_local >= 0 && n_local <= n_max, "krca_ppr_shard_init_warm: bad sizes");
+  KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0, "krca_ppr_shard_init_warm: alpha must be in (0, 1)");
+  KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)),
+                 "krca_ppr_shard_init_warm: null pointer");
+  hipStream_t st = krca::as_stream(stream);
+  KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
+  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
+  if (n_local > 0)
+    hipLaunchKernelGGL(ppr_init_warm, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local,
                        alpha, q_local, r_local, send, n_max);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;

@@ -300,9 +300,102 @@ __global__ __launch_bounds__(256) void rolling_score_reread(const float* __restr
   pod_epilogue(st, epsB, s, active, M, T, xs, S, z_last, score, n_exceed, flags);
 }
 
+// ---- streaming rescoring (BASELINE configs[4]) ----------------------------
+// The batch scorer applied to an unbounded stream, carried forward window by window: state per
+// series = the float64 window sums (s1, s2), the last W samples (ring [W][S]) and the exceedance
+// bits of the last H evaluated steps (bits [ceil(H/32)][S]) with their count.  A window of delta
+// new steps t0 .. t0+delta-1 runs exactly the batch kernel's operations for those steps (the
+// prologue sums while t < W, step() after), so after any sequence of windows z_last / score /
+// flags equal krca_rolling_score over the whole series so far, and n_exceed counts its
+// exceedances over the last H evaluated steps (all of them while there are fewer than H).
+// Per series and window: 20 B of state read + written, 12*delta B of samples (new, old, ring
+// write) and 8*delta B of exceedance bits.
+struct StreamState {
+  double* s1;
+  double* s2;
+  int32_t* cnt;
+  float* ring;
+  uint32_t* bits;
+};
+
+__global__ __launch_bounds__(256) void stream_score(const float* __restrict__ xn, int64_t S, int delta, int64_t t0,
+                                                    int W, int H, int M, double thr2, StreamState stt,
+                                                    float* __restrict__ z_last, float* __restrict__ score,
+                                                    int32_t* __restrict__ n_exceed, uint8_t* __restrict__ flags) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = s < S;
+  const int64_t sl = active ? s : 0;
+  const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
+  StepState st{0.0, 0.0, 0, 0.0, 0.0};
+  int cnt = 0;
+  if (t0 > 0) {
+    st.s1 = stt.s1[sl];
+    st.s2 = stt.s2[sl];
+    cnt = stt.cnt[sl];
+  }
+  for (int j = 0; j < delta; ++j) {
+    const int64_t t = t0 + j;
+    const float v = xn[(int64_t)j * S + sl];
+    float* rp = stt.ring + (t % W) * S + sl;
+    if (t < W) {  // the batch prologue: window fill
+      const double vd = (double)v;
+      st.s1 = st.s1 + vd;
+      st.s2 = fma(vd, vd, st.s2);
+    } else {
+      const float o = *rp;
+      st.cnt = 0;
+      step(st, v, o, Wd, epsB, thr2, j == delta - 1);
+      const int64_t e = t - W;  // index among the evaluated steps
+      uint32_t* wp = stt.bits + ((e % H) >> 5) * S + sl;
+      const uint32_t bit = 1u << ((e % H) & 31);
+      const uint32_t word = *wp;  // zeroed when the stream starts (t0 == 0)
+      cnt += st.cnt - ((word & bit) ? 1 : 0);
+      if (active) *wp = st.cnt ? (word | bit) : (word & ~bit);
+    }
+    if (active) *rp = v;
+  }
+  if (active) {
+    stt.s1[sl] = st.s1;
+    stt.s2[sl] = st.s2;
+    stt.cnt[sl] = cnt;
+  }
+  st.cnt = cnt;
+  if (t0 + delta - 1 < W) st.bl = 0.0;  // no evaluated step yet: z = 0
+  pod_epilogue(st, epsB, s, active, M, delta, xn + sl, S, z_last, score, n_exceed, flags);
+}
+
 }  // namespace
 
 extern "C" {
+
+// state: s1, s2 f64 [S] | cnt i32 [S] | ring f32 [W][S] | bits u32 [ceil(H/32)][S]  (S = P*M)
+int64_t krca_stream_state_size(int64_t P, int32_t M, int32_t W, int32_t H) {
+  const int64_t S = P * M;
+  return S * (8 + 8 + 4) + (int64_t)W * S * 4 + krca::ceil_div(H, 32) * S * 4 + 64;
+}
+
+int krca_stream_score(const float* x_new, int64_t P, int32_t M, int32_t delta, int64_t t0, int32_t W, int32_t H,
+                      float z_thr, void* state, float* z_last, float* score, int32_t* n_exceed, uint8_t* flags,
+                      void* stream) {
+  KRCA_CHECK_ARG(P >= 0 && delta >= 1 && t0 >= 0 && W >= 1 && H >= 1, "krca_stream_score: bad sizes");
+  KRCA_CHECK_ARG(M >= 1 && M <= 64 && (M & (M - 1)) == 0, "krca_stream_score: M=%d must be a power of two <= 64", M);
+  if (P == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(x_new && state && z_last && score && n_exceed && flags, "krca_stream_score: null pointer");
+  const int64_t S = P * (int64_t)M;
+  char* b = reinterpret_cast<char*>(state);
+  StreamState stt;
+  stt.s1 = reinterpret_cast<double*>(b);
+  stt.s2 = stt.s1 + S;
+  stt.cnt = reinterpret_cast<int32_t*>(stt.s2 + S);
+  stt.ring = reinterpret_cast<float*>(stt.cnt + S);
+  stt.bits = reinterpret_cast<uint32_t*>(stt.ring + (int64_t)W * S);
+  hipStream_t st = krca::as_stream(stream);
+  if (t0 == 0) KRCA_HIP(hipMemsetAsync(stt.bits, 0, krca::ceil_div(H, 32) * S * 4, st));
+  hipLaunchKernelGGL(stream_score, dim3((unsigned)krca::ceil_div(S, 256)), dim3(256), 0, st, x_new, S, delta, t0, W,
+                     H, M, (double)z_thr * (double)z_thr, stt, z_last, score, n_exceed, flags);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
 
 int krca_usage_flags(const float* usage, int64_t P, uint8_t* flags, void* stream) {
   KRCA_CHECK_ARG(P >= 0, "krca_usage_flags: P < 0");

@@ -25,6 +25,9 @@ SIGNATURES = {
     "krca_device_count": (c_i32, [ctypes.POINTER(ctypes.c_int)]),
     "krca_usage_flags": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_rolling_score": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_stream_state_size": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
+    "krca_stream_score": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp]),
     "krca_log_index_size": (c_i64, [c_i64]),
     "krca_log_index": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "krca_log_match": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -58,6 +61,8 @@ SIGNATURES = {
     "krca_ppr_ctl_size": (c_i64, [c_i64]),
     "krca_ppr_remap_cols": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "krca_ppr_shard_init": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_init_warm": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp]),
     "krca_ppr_shard_step": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp,
                                     c_vp, c_vp]),
     "krca_ppr_shard_reduce": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp]),

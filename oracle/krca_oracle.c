@@ -88,9 +88,11 @@ static int64_t edge_weight(int64_t rj, int32_t deg, double alpha) {
   return (int64_t)((double)rj * coef);
 }
 
-/* Pull-CSR personalized PageRank; returns iterations (negative if no convergence). */
-int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const float* seed,
-                 float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r, float* r_out, int64_t* q) {
+/* Pull-CSR personalized PageRank; returns iterations (negative if no convergence).
+ * warm != 0: r holds the start vector on entry (krca_ppr_shard_init_warm), else r0 = 2^60/N. */
+int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
+                       const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r,
+                       float* r_out, int64_t* q, int warm) {
   int64_t* w = (int64_t*)malloc(sizeof(int64_t) * N);
   int64_t qtot = 0, dang = 0;
   const int64_t r0 = (int64_t)(kFix / (double)N);
@@ -98,9 +100,9 @@ int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outd
     const double v = (double)seed[i] - (double)seed_floor;
     q[i] = v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
     qtot += q[i];
-    r[i] = r0;
-    w[i] = edge_weight(r0, outdeg[i], alpha);
-    if (outdeg[i] == 0) dang += r0;
+    if (!warm) r[i] = r0;
+    w[i] = edge_weight(r[i], outdeg[i], alpha);
+    if (outdeg[i] == 0) dang += r[i];
   }
   const double err_limit = tol > 0.0 ? (double)N * tol * kFix : 0.0;
   double tele = (1.0 - alpha) * kFix + alpha * (double)dang;
@@ -137,6 +139,11 @@ int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outd
   free(w);
   free(acc);
   return (err_limit > 0.0 && !conv) ? -it : it;
+}
+
+int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const float* seed,
+                 float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r, float* r_out, int64_t* q) {
+  return krco_ppr_start(row_ptr, col, outdeg, N, seed, seed_floor, alpha, max_iter, tol, r, r_out, q, 0);
 }
 
 /* root-cause key of krca_ppr_rca_key */

@@ -328,6 +328,8 @@ def c_lib():
     lib.krco_rolling_score.argtypes = [vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]
     lib.krco_ppr.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp]
     lib.krco_ppr.restype = i32
+    lib.krco_ppr_start.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp, ctypes.c_int]
+    lib.krco_ppr_start.restype = i32
     lib.krco_rca_key.argtypes = [vp, vp, i64, vp]
     _c = lib
     return lib
@@ -366,6 +368,21 @@ def c_ppr(row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6, seed_f
     rf = np.zeros(N, np.float32)
     it = c_lib().krco_ppr(_p(rp), _p(cl), _p(od), N, _p(sd), seed_floor, alpha, max_iter, tol, _p(r), _p(rf), _p(q))
     return (rf, r, it, q) if return_q else (rf, r, it)
+
+
+def c_ppr_warm(row_ptr, col, outdeg, seed, r_start, alpha, max_iter, tol, seed_floor):
+    """krco_ppr started from the fixed-point vector r_start (streaming re-ranking) -> (r, iters, q)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    od = np.ascontiguousarray(outdeg, np.int32)
+    sd = np.ascontiguousarray(seed, np.float32)
+    N = len(od)
+    r = np.array(r_start, np.int64, copy=True)
+    q = np.zeros(N, np.int64)
+    rf = np.zeros(N, np.float32)
+    it = c_lib().krco_ppr_start(_p(rp), _p(cl), _p(od), N, _p(sd), seed_floor, alpha, max_iter, tol, _p(r), _p(rf),
+                                _p(q), 1)
+    return r, it, q
 
 
 def c_rca_key(r, q):

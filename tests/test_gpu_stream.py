@@ -1,0 +1,76 @@
+"""C5 streaming replay (krca/stream.py) against the batch kernels' oracle on the same chain.
+
+* krca_stream_score over any sequence of windows == krca_rolling_score over the whole series so
+  far (the C restatement): z_last / score within 1e-5 of it (bit-identical arithmetic), flags
+  bit-exact; n_exceed == the exceedances of the last H evaluated steps, i.e. the difference of two
+  batch prefix counts, bit-exact.
+* warm-started re-ranking: each window's fixed-point ranks and iteration count equal
+  oracle.c_ppr_warm started from the oracle's previous ranks; top-k identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from krca import native, synth
+from krca.rca import Config
+from krca.stream import StreamingRCA
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return native.NativeEngine()
+
+
+def _n_prefix(x, t, W):
+    """batch exceedance counts over the evaluated steps of x[:t] (0 while t <= W)."""
+    return oracle.c_rolling_score(x[:t], W)["n_exceed"] if t > W else np.zeros(x.shape[1], np.int32)
+
+
+@pytest.mark.parametrize("H", [10_000, 50])
+def test_stream_score_equals_batch_prefix(eng, H):
+    P, M, T, W = 1500, 8, 400, 60
+    m = synth.make_graph(P, avg_degree=8, seed=3)
+    x = synth.make_metrics(P, M, T, window=W, seed=4, roots=m.roots).numpy()
+    s = StreamingRCA(eng, m.row_ptr, m.col, m.outdeg, M, Config(window=W), horizon=H)
+    xd = torch.from_numpy(x).cuda()
+    t = 0
+    for d in [1, 7, 45, 1, 3, 60, 2, 100, 1, 180]:
+        o = s.push_metrics(xd[t:t + d].contiguous())
+        t += d
+        ref = oracle.c_rolling_score(x[:t], W)
+        assert np.array_equal(o["flags"].cpu().numpy(), ref["flags"]), t
+        assert np.allclose(o["z_last"].cpu().numpy(), ref["z_last"], rtol=1e-5, atol=1e-6), t
+        assert np.allclose(o["score"].cpu().numpy(), ref["score"], rtol=1e-5, atol=1e-6), t
+        want = _n_prefix(x, t, W) - _n_prefix(x, t - H, W) if t - H > W else _n_prefix(x, t, W)
+        assert np.array_equal(o["n_exceed"].cpu().numpy(), want), t
+    assert t == T
+
+
+def test_stream_windows_rerank_warm_started(eng):
+    P, M, T, W = 4000, 8, 300, 60
+    m = synth.make_graph(P, avg_degree=12, seed=6)
+    hops = synth.caller_hops(m, m.roots)
+    x = synth.make_metrics(P, M, T, window=W, seed=7, roots=m.roots, hop_sets=hops).numpy()
+    cfg = Config(window=W)
+    s = StreamingRCA(eng, m.row_ptr, m.col, m.outdeg, M, cfg, tol=1e-9, max_iter=60)
+    xd = torch.from_numpy(x).cuda()
+    r_ref = None
+    t = 0
+    for d in [W + 100, 20, 1, 1, 50, 1]:
+        out = s.window(xd[t:t + d].contiguous())
+        t += d
+        score = out["scores"]["score"].cpu().numpy()
+        if r_ref is None:
+            rf, r_ref, it = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, 60, 1e-9, cfg.seed_floor)
+            q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, 60, 1e-9, cfg.seed_floor,
+                             return_q=True)[3]
+        else:
+            r_ref, it, q = oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, score, r_ref, cfg.alpha, 60, 1e-9,
+                                             cfg.seed_floor)
+        assert np.array_equal(s.shard.r[:P].cpu().numpy(), r_ref), t
+        assert out["iters"] == it, (t, out["iters"], it)
+        ridx, _ = oracle.topk_ref(oracle.c_rca_key(r_ref, q), cfg.k)
+        assert [int(i) for i in out["top"][0]] == [int(i) for i in ridx], t
