@@ -17,8 +17,9 @@
 //               state depends on no more).  Line pieces that straddle chunks are combined in LDS
 //               by the owning lane; only lines straddling a 64 KiB tile use an atomic OR
 //               (deterministic: OR is order-free).
-//   log_hist    wave per container: binary-search its line range, 13 ballots per 64 lines give
-//               the bin counts and the first three line ids per bin — no atomics.
+//   log_hist    lane per container: one binary search for its first line (the next lane's is its
+//               end), a private loop over <= 32 line masks, or the whole wave (13 ballots per 64
+//               lines) for a larger container — counts and first three line ids per bin, no atomics.
 #include "krca_common.h"
 #define KRCA_DFA_QUAL static __device__ __constant__ const
 #include "log_dfa_tables.h"
@@ -410,45 +411,93 @@ __device__ __forceinline__ int64_t lower_bound_i64(const int64_t* __restrict__ a
   return lo;
 }
 
+// One lane per container: its first line by one binary search over line_start (the next lane's
+// result is its end), then, for a container of <= 32 lines, a private loop over the line masks;
+// larger containers are taken by the whole wave one at a time (13 ballots per 64 lines give the
+// counts and the first three line ids per bin).  No atomics; ~1M containers of ~2.5 lines are
+// one pass of short lane loops instead of a wave (and two dependent searches) each.
+constexpr int HIST_SMALL = 32;
+
 __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_off, int64_t D,
                                                 const int64_t* __restrict__ line_start,
                                                 const uint32_t* __restrict__ line_mask, int64_t L,
                                                 int32_t* __restrict__ doc_lines, int32_t* __restrict__ hist,
                                                 int32_t* __restrict__ examples, int64_t* __restrict__ doc_line0) {
-  const int64_t d = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  if (d >= D) return;
-  const int64_t lo = lower_bound_i64(line_start, L, doc_off[d]);
-  const int64_t hi = lower_bound_i64(line_start, L, doc_off[d + 1]);
-  int32_t cnt[KRCA_NCAT];
-  int32_t found[KRCA_NCAT];
-#pragma unroll
-  for (int c = 0; c < KRCA_NCAT; ++c) {
-    cnt[c] = 0;
-    found[c] = 0;
-  }
-  int32_t* ex = examples + d * KRCA_NCAT * 3;
-  for (int64_t b = lo; b < hi; b += 64) {
-    const uint32_t m = (b + lane < hi) ? line_mask[b + lane] : 0u;
+  const bool valid = d < D;
+  const int64_t lo = valid ? lower_bound_i64(line_start, L, doc_off[d]) : L;
+  int64_t hi = __shfl_down(lo, 1, 64);
+  if (valid && (lane == 63 || d + 1 == D)) hi = lower_bound_i64(line_start, L, doc_off[d + 1]);
+  const bool small = valid && hi - lo <= HIST_SMALL;
+  if (small) {
+    int32_t cnt[KRCA_NCAT], ex[KRCA_NCAT][3];
 #pragma unroll
     for (int c = 0; c < KRCA_NCAT; ++c) {
-      uint64_t bal = __ballot((m >> c) & 1u);
-      cnt[c] += __popcll(bal);
-      while (found[c] < 3 && bal) {
-        const int j = __ffsll((unsigned long long)bal) - 1;
-        if (lane == 0) ex[c * 3 + found[c]] = (int32_t)(b + j);
-        ++found[c];
-        bal &= bal - 1;
+      cnt[c] = 0;
+      ex[c][0] = ex[c][1] = ex[c][2] = -1;
+    }
+    for (int64_t l = lo; l < hi; ++l) {
+      const uint32_t m = line_mask[l];
+#pragma unroll
+      for (int c = 0; c < KRCA_NCAT; ++c) {
+        if ((m >> c) & 1u) {
+          const int f = cnt[c];
+          if (f == 0) ex[c][0] = (int32_t)l;
+          if (f == 1) ex[c][1] = (int32_t)l;
+          if (f == 2) ex[c][2] = (int32_t)l;
+          cnt[c] = f + 1;
+        }
       }
     }
-  }
-  if (lane == 0) {
     doc_lines[d] = (int32_t)(hi - lo);
     if (doc_line0) doc_line0[d] = lo;
+    int32_t* hd = hist + d * KRCA_NCAT;
+    int32_t* ed = examples + d * KRCA_NCAT * 3;
 #pragma unroll
     for (int c = 0; c < KRCA_NCAT; ++c) {
-      hist[d * KRCA_NCAT + c] = cnt[c];
-      for (int k = found[c]; k < 3; ++k) ex[c * 3 + k] = -1;
+      hd[c] = cnt[c];
+      ed[c * 3] = ex[c][0];
+      ed[c * 3 + 1] = ex[c][1];
+      ed[c * 3 + 2] = ex[c][2];
+    }
+  }
+  uint64_t big = __ballot(valid && !small);
+  while (big) {  // wave-uniform: the wave takes the large containers one at a time
+    const int j = __ffsll((unsigned long long)big) - 1;
+    big &= big - 1;
+    const int64_t dj = d - lane + j;
+    const int64_t blo = __shfl(lo, j, 64), bhi = __shfl(hi, j, 64);
+    int32_t cnt[KRCA_NCAT];
+    int32_t found[KRCA_NCAT];
+#pragma unroll
+    for (int c = 0; c < KRCA_NCAT; ++c) {
+      cnt[c] = 0;
+      found[c] = 0;
+    }
+    int32_t* ex = examples + dj * KRCA_NCAT * 3;
+    for (int64_t b = blo; b < bhi; b += 64) {
+      const uint32_t m = (b + lane < bhi) ? line_mask[b + lane] : 0u;
+#pragma unroll
+      for (int c = 0; c < KRCA_NCAT; ++c) {
+        uint64_t bal = __ballot((m >> c) & 1u);
+        cnt[c] += __popcll(bal);
+        while (found[c] < 3 && bal) {
+          const int q = __ffsll((unsigned long long)bal) - 1;
+          if (lane == 0) ex[c * 3 + found[c]] = (int32_t)(b + q);
+          ++found[c];
+          bal &= bal - 1;
+        }
+      }
+    }
+    if (lane == 0) {
+      doc_lines[dj] = (int32_t)(bhi - blo);
+      if (doc_line0) doc_line0[dj] = blo;
+#pragma unroll
+      for (int c = 0; c < KRCA_NCAT; ++c) {
+        hist[dj * KRCA_NCAT + c] = cnt[c];
+        for (int k = found[c]; k < 3; ++k) ex[c * 3 + k] = -1;
+      }
     }
   }
 }
@@ -500,7 +549,7 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
                        nt, n_lines, line_start, line_end, line_mask);
     KRCA_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB / 64)), dim3(TPB), 0, st, doc_off, ndocs,
+  hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
                      line_start, line_mask, n_lines, doc_lines, hist, examples, doc_line0);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
