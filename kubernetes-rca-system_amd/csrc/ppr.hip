@@ -28,6 +28,8 @@
 //     into the row's accumulator and a per-row ticket; the last chunk to arrive updates the row.
 //   Residual / dangling mass: one int64 atomic per block into NSPREAD slots of the send tail, so
 //     the partial sums ride the same all-gather; ppr_reduce sums G*NSPREAD slots.
+#include <stdlib.h>
+
 #include <vector>
 
 #include "krca_common.h"
@@ -159,103 +161,136 @@ __device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi
   send[i] = edge_weight(rn, deg, k.alpha);
 }
 
-__global__ __launch_bounds__(TPB) void ppr_step(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-                                                const int64_t* __restrict__ plan, const int64_t* __restrict__ w,
-                                                const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
-                                                int64_t n, int64_t N, double alpha, int64_t* __restrict__ r,
-                                                int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
+// Everything one plan entry {rb, code, e0, e1} needs before its gathers: the col indices (lane-
+// strided, coalesced), the row offsets and the update operands (q, r, outdeg) of the lane's row.
+struct EntryLoads {
+  int32_t rb, code;
+  int64_t e0, e1;
+  int32_t c[SEG];
+  int64_t my_off, my_q, my_r;
+  int32_t my_deg;
+};
+
+__device__ __forceinline__ void load_entry(const int64_t* __restrict__ plan, int64_t b,
+                                           const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+                                           const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
+                                           const int64_t* __restrict__ r, EntryLoads& L) {
+  const int64_t* pe = plan + 4 * b;
+  L.rb = (int32_t)pe[0];
+  L.code = (int32_t)pe[1];
+  L.e0 = pe[2];
+  L.e1 = pe[3];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < SEG; ++j) {
+    const int64_t e = L.e0 + tid + j * TPB;
+    L.c[j] = e < L.e1 ? col[e] : -1;
+  }
+  const int nrows = L.code > 0 ? L.code - L.rb : 1;
+  const int64_t my_row = L.rb + (tid < nrows ? tid : 0);
+  L.my_off = L.code > 0 && tid < nrows ? row_ptr[my_row] : 0;
+  L.my_q = q[my_row];
+  L.my_r = r[my_row];
+  L.my_deg = outdeg[my_row];
+}
+
+// Persistent, software-pipelined step: workgroup g takes plan entries g, g + G, ...; the loads of
+// entry i+1 (plan, col, row data) are issued while entry i's w gathers are in flight, so a
+// workgroup pays the dependent plan -> col latency once instead of once per entry.  The block is
+// latency-bound (dependent memory round trips), and the occupancy is already at 8 waves/SIMD.
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) void ppr_step(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col, const int64_t* __restrict__ plan, int64_t nblk,
+    const int64_t* __restrict__ w, const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n,
+    int64_t N, double alpha, int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
   __shared__ int64_t vals[EDGE_BUDGET];
   __shared__ unsigned long long rowsum[ROW_BUDGET];
   __shared__ int32_t roff[ROW_BUDGET + 1];
   __shared__ int64_t red[TPB / 64];
-  // The block is latency-bound (a handful of dependent memory round trips), so every load that
-  // depends only on the plan entry is issued in ONE wave of requests: col, the row offsets and
-  // the update operands (q, r, outdeg) of this lane's row, together; then the w gathers.
-  const int64_t* pe = plan + 4 * (int64_t)blockIdx.x;  // {rb, code, e0, e1}
-  const int32_t rb = (int32_t)pe[0];
-  const int32_t code = (int32_t)pe[1];
-  const int64_t e0 = pe[2], e1 = pe[3];
-  const int32_t conv = ctl->converged;  // loaded with the plan entry; tested only after the loads
+  int64_t b = blockIdx.x;
+  if (b >= nblk) return;
+  EntryLoads cur;
+  load_entry(plan, b, row_ptr, col, outdeg, q, r, cur);
+  const int32_t conv = ctl->converged;
   StepScalars k;
   k.tele = ctl->tele;
   k.qt = ctl->q_total;
   k.qtot = (double)k.qt;
   k.uni = 1.0 / (double)N;
   k.alpha = alpha;
-  const int tid = threadIdx.x;
-  int32_t c[SEG];
-  int64_t v[SEG];
-#pragma unroll
-  for (int j = 0; j < SEG; ++j) {
-    const int64_t e = e0 + tid + j * TPB;
-    c[j] = e < e1 ? col[e] : -1;
-  }
-  const int nrows = code > 0 ? code - rb : 1;
-  const int64_t my_row = rb + (tid < nrows ? tid : 0);
-  const int64_t my_off = code > 0 && tid < nrows ? row_ptr[my_row] : 0;
-  const int64_t my_q = q[my_row], my_r = r[my_row];
-  const int32_t my_deg = outdeg[my_row];
-#pragma unroll
-  for (int j = 0; j < SEG; ++j) v[j] = c[j] >= 0 ? w[c[j]] : 0;
   if (conv) return;  // converged (tol > 0): no writes (uniform)
+  const int tid = threadIdx.x;
   int64_t err = 0, dang = 0;
-  if (code > 0) {
-    const int nrows = code - rb;
-    const int ne = (int)(e1 - e0);
+  while (true) {
+    int64_t v[SEG];
 #pragma unroll
-    for (int j = 0; j < SEG; ++j) {
-      const int e = tid + j * TPB;
-      if (e < ne) vals[e] = v[j];
-    }
-    if (tid < nrows) roff[tid] = (int32_t)(my_off - e0);
-    if (tid == 0) roff[nrows] = ne;
-    rowsum[tid] = 0ull;
-    __syncthreads();
-    const int a = tid * SEG;
-    if (a < ne) {  // this lane's contiguous edges [a, b) as row segments
-      const int b = min(a + SEG, ne);
-      int lo = 0, hi = nrows;  // roff[lo] <= a < roff[hi]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (roff[mid] <= a) lo = mid;
-        else hi = mid;
+    for (int j = 0; j < SEG; ++j) v[j] = cur.c[j] >= 0 ? w[cur.c[j]] : 0;
+    const int64_t nb = b + gridDim.x;
+    EntryLoads nxt;
+    if (nb < nblk) load_entry(plan, nb, row_ptr, col, outdeg, q, r, nxt);
+    if (cur.code > 0) {
+      const int nrows = cur.code - cur.rb;
+      const int ne = (int)(cur.e1 - cur.e0);
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) {
+        const int e = tid + j * TPB;
+        if (e < ne) vals[e] = v[j];
       }
-      int row = lo;
-      int end = roff[row + 1];
-      int64_t s = 0;
-      for (int e = a; e < b; ++e) {
-        while (e >= end) {
-          if (s) atomicAdd(&rowsum[row], (unsigned long long)s);
-          s = 0;
-          ++row;
-          end = roff[row + 1];
+      if (tid < nrows) roff[tid] = (int32_t)(cur.my_off - cur.e0);
+      if (tid == 0) roff[nrows] = ne;
+      rowsum[tid] = 0ull;
+      __syncthreads();
+      const int a = tid * SEG;
+      if (a < ne) {  // this lane's contiguous edges [a, b) as row segments
+        const int bb = min(a + SEG, ne);
+        int lo = 0, hi = nrows;  // roff[lo] <= a < roff[hi]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (roff[mid] <= a) lo = mid;
+          else hi = mid;
         }
-        s += vals[e];
+        int row = lo;
+        int end = roff[row + 1];
+        int64_t sacc = 0;
+        for (int e = a; e < bb; ++e) {
+          while (e >= end) {
+            if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);
+            sacc = 0;
+            ++row;
+            end = roff[row + 1];
+          }
+          sacc += vals[e];
+        }
+        if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);
       }
-      if (s) atomicAdd(&rowsum[row], (unsigned long long)s);
-    }
-    __syncthreads();
-    if (tid < nrows) update_row(my_row, (int64_t)rowsum[tid], my_q, my_r, my_deg, k, r, send, err, dang);
-  } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
-    int64_t s = 0;
+      __syncthreads();
+      if (tid < nrows)
+        update_row(cur.rb + tid, (int64_t)rowsum[tid], cur.my_q, cur.my_r, cur.my_deg, k, r, send, err, dang);
+      __syncthreads();  // rowsum / vals / roff are rewritten by the next entry
+    } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
+      int64_t sacc = 0;
 #pragma unroll
-    for (int j = 0; j < SEG; ++j) s += v[j];
-    const int64_t tot = block_sum_i64(s, red);
-    if (tid == 0) {
-      const int64_t deg_in = row_ptr[rb + 1] - row_ptr[rb];  // (one lane, off the gather path)
-      const uint32_t nch = (uint32_t)((deg_in + EDGE_BUDGET - 1) / EDGE_BUDGET);
-      int64_t* acc = acc_long_of(ctl) + rb;
-      uint32_t* tk = ticket_of(ctl, n) + rb;
-      __hip_atomic_fetch_add(acc, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the add is performed before the ticket
-      const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == nch - 1) {
-        const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        update_row(rb, pulled, my_q, my_r, my_deg, k, r, send, err, dang);
+      for (int j = 0; j < SEG; ++j) sacc += v[j];
+      const int64_t tot = block_sum_i64(sacc, red);
+      if (tid == 0) {
+        const int32_t rb = cur.rb;
+        const int64_t deg_in = row_ptr[rb + 1] - row_ptr[rb];
+        const uint32_t nch = (uint32_t)((deg_in + EDGE_BUDGET - 1) / EDGE_BUDGET);
+        int64_t* acc = acc_long_of(ctl) + rb;
+        uint32_t* tk = ticket_of(ctl, n) + rb;
+        __hip_atomic_fetch_add(acc, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the add is performed before the ticket
+        const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == nch - 1) {
+          const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          update_row(rb, pulled, cur.my_q, cur.my_r, cur.my_deg, k, r, send, err, dang);
+        }
       }
     }
+    if (nb >= nblk) break;
+    cur = nxt;
+    b = nb;
   }
   err = block_sum_i64(err, red);
   dang = block_sum_i64(dang, red);
@@ -430,9 +465,21 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
   KRCA_CHECK_ARG(row_ptr && col && plan && w_all && outdeg && q_local && r_local && send && ctl,
                  "krca_ppr_shard_step: null pointer");
   KRCA_CHECK_ARG(w_all != send, "krca_ppr_shard_step: w_all and send must be distinct buffers (ping-pong)");
-  hipLaunchKernelGGL(ppr_step, dim3((unsigned)(plan_len / 4)), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col,
-                     plan, w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
-                     reinterpret_cast<Ctl*>(ctl));
+  const int64_t nblk = plan_len / 4;
+  static const int64_t resident = [] {  // workgroups the device keeps resident (occupancy API)
+    int dev = 0, cus = 256, per_cu = 4;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&ppr_step), TPB, 0) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 4;
+    const char* e = getenv("KRCA_PPR_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)cus * per_cu;
+  }();
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nblk, resident));
+  hipLaunchKernelGGL(ppr_step, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, nblk,
+                     w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
