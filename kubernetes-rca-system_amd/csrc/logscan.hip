@@ -20,6 +20,8 @@
 //   log_hist    lane per container: one binary search for its first line (the next lane's is its
 //               end), a private loop over <= 32 line masks, or the whole wave (13 ballots per 64
 //               lines) for a larger container — counts and first three line ids per bin, no atomics.
+#include <stdint.h>
+
 #include "krca_common.h"
 #define KRCA_DFA_QUAL static __device__ __constant__ const
 #include "log_dfa_tables.h"
@@ -82,26 +84,45 @@ __device__ __forceinline__ bool sep_before(uint32_t b3, uint32_t b2, uint32_t b1
   return b3 == 0xE2 && b2 == 0x80 && (b1 == 0xA8 || b1 == 0xA9);
 }
 
-// container of byte p: last d with doc_off[d] <= p (doc_off has D+1 entries, doc_off[D] = nbytes)
-__device__ __forceinline__ int64_t doc_of(const int64_t* __restrict__ off, int64_t D, int64_t p) {
-  int64_t lo = 0, hi = D;  // answer in [0, D-1]
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (off[mid] <= p) lo = mid;
-    else hi = mid;
+// The container window of a lane: the current container d and the next boundaries off[d .. d+4]
+// held in registers, refilled one load ahead, so crossing a container boundary (a ~184-byte
+// container per 256-byte chunk at C5) does not wait on a dependent global load.
+struct DocWin {
+  const int64_t* off;
+  int64_t D, d;
+  int64_t b[5];
+  __device__ __forceinline__ void load(const int64_t* o, int64_t nd, int64_t d0) {
+    off = o;
+    D = nd;
+    d = d0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) b[i] = d0 + i <= nd ? o[d0 + i] : INT64_MAX;
   }
-  return lo;
-}
+  // move to the container holding byte p (skipping empty containers sitting at p)
+  __device__ __forceinline__ void advance(int64_t p) {
+    while (d + 1 < D && b[1] <= p) {
+      ++d;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i] = b[i + 1];
+      b[4] = d + 4 <= D ? off[d + 4] : INT64_MAX;
+    }
+  }
+};
 
-// first doc index >= d whose end is > p (skips empty containers sitting at p)
-__device__ __forceinline__ int64_t skip_empty(const int64_t* __restrict__ off, int64_t D, int64_t d, int64_t p) {
-  while (d + 1 < D && off[d + 1] <= p) ++d;
-  return d;
+// chunk -> container holding its first byte: one thread per container writes the chunks that start
+// inside it (every chunk start lies in exactly one non-empty container), so no chunk searches
+__global__ __launch_bounds__(TPB) void log_chunk_doc(const int64_t* __restrict__ doc_off, int64_t D,
+                                                     int32_t* __restrict__ chunk_doc) {
+  const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (d >= D) return;
+  const int64_t s = doc_off[d], e = doc_off[d + 1];
+  for (int64_t c = (s + CH - 1) / CH; c * CH < e; ++c) chunk_doc[c] = (int32_t)d;
 }
 
 // ---- phase 1: line starts per chunk ---------------------------------------------------------
 __global__ __launch_bounds__(TPB) void log_count(const uint8_t* __restrict__ text, int64_t nbytes,
                                                  const int64_t* __restrict__ doc_off, int64_t D,
+                                                 const int32_t* __restrict__ chunk_doc,
                                                  int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_tot) {
   __shared__ int32_t red[TPB / 64];
   const int64_t g = (int64_t)blockIdx.x * TPB + threadIdx.x;
@@ -111,16 +132,17 @@ __global__ __launch_bounds__(TPB) void log_count(const uint8_t* __restrict__ tex
     const int64_t c1 = min(c0 + CH, nbytes);
     Bytes B;
     B.init(text, nbytes);
-    int64_t d = skip_empty(doc_off, D, doc_of(doc_off, D, c0), c0);
-    int64_t dstart = doc_off[d], dend = doc_off[d + 1];
+    DocWin dw;
+    dw.load(doc_off, D, chunk_doc[g]);
+    int64_t dstart = dw.b[0], dend = dw.b[1];
     uint32_t b1 = c0 - 1 >= dstart ? B.at(c0 - 1) : 0;
     uint32_t b2 = c0 - 2 >= dstart ? B.at(c0 - 2) : 0;
     uint32_t b3 = c0 - 3 >= dstart ? B.at(c0 - 3) : 0;
     for (int64_t p = c0; p < c1; ++p) {
       if (p >= dend) {  // next container(s)
-        d = skip_empty(doc_off, D, d + 1, p);
-        dstart = doc_off[d];
-        dend = doc_off[d + 1];
+        dw.advance(p);
+        dstart = dw.b[0];
+        dend = dw.b[1];
         b1 = b2 = b3 = 0;
       }
       const uint32_t b0 = B.at(p);
@@ -213,6 +235,7 @@ __device__ __forceinline__ int64_t cp_align(Bytes& B, int64_t p, int64_t lim) {
 
 __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ text, int64_t nbytes,
                                                  const int64_t* __restrict__ doc_off, int64_t D,
+                                                 const int32_t* __restrict__ chunk_doc,
                                                  const int32_t* __restrict__ chunk_cnt,
                                                  const int64_t* __restrict__ tile_base, int64_t ntiles, int64_t L,
                                                  int64_t* __restrict__ line_start, int64_t* __restrict__ line_end,
@@ -253,8 +276,9 @@ __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ tex
       const int64_t c1 = min(c0 + CH, nbytes);
       Bytes B;
       B.init(text, nbytes);
-      int64_t d = skip_empty(doc_off, D, doc_of(doc_off, D, c0), c0);
-      int64_t dstart = doc_off[d], dend = doc_off[d + 1];
+      DocWin dw;
+      dw.load(doc_off, D, chunk_doc[g]);
+      int64_t dstart = dw.b[0], dend = dw.b[1];
       const int64_t p0 = cp_align(B, c0, dend);  // first code point starting in this chunk
       int64_t cur = base - 1;  // id of the open line (lines before this chunk: base)
       bool open = false, own = false, after_sep = false, prev_cr = false;
@@ -304,9 +328,9 @@ __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ tex
             }
             open = false;
           }
-          d = skip_empty(doc_off, D, d + 1, p);
-          dstart = doc_off[d];
-          dend = doc_off[d + 1];
+          dw.advance(p);
+          dstart = dw.b[0];
+          dend = dw.b[1];
           after_sep = false;
           prev_cr = false;
         }
@@ -508,10 +532,11 @@ int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(n
 
 extern "C" {
 
-// workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts
+// workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts |
+// [ntiles*TPB] int32 chunk -> container
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
-  return (nt + 1) + krca::ceil_div(nt * TPB, 2) + 2;
+  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2;
 }
 
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
@@ -521,10 +546,15 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   KRCA_CHECK_ARG(nbytes == 0 || text, "krca_log_index: null text");
   KRCA_CHECK_ARG(((uintptr_t)text & 15) == 0, "krca_log_index: text must be 16-byte aligned");
   const int64_t nt = num_tiles(nbytes);
+  KRCA_CHECK_ARG(ndocs < INT32_MAX, "krca_log_index: too many containers");
   int64_t* tile = ws;
   int32_t* chunk = reinterpret_cast<int32_t*>(ws + nt + 1);
+  int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
   hipStream_t st = krca::as_stream(stream);
-  hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, chunk, tile);
+  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs, cdoc);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
+                     (const int32_t*)cdoc, chunk, tile);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(log_scan, dim3(1), dim3(1024), 0, st, tile, nt, n_lines);
   KRCA_LAUNCH_CHECK();
@@ -541,12 +571,13 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   const int64_t nt = num_tiles(nbytes);
   const int64_t* tile = ws;
   const int32_t* chunk = reinterpret_cast<const int32_t*>(ws + nt + 1);
+  const int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
   hipStream_t st = krca::as_stream(stream);
   if (n_lines > 0) {
     KRCA_HIP(hipMemsetAsync(line_mask, 0, n_lines * sizeof(uint32_t), st));
     const int64_t grid = std::min<int64_t>(nt, 256 * 4);
-    hipLaunchKernelGGL(log_match, dim3((unsigned)grid), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, chunk, tile,
-                       nt, n_lines, line_start, line_end, line_mask);
+    hipLaunchKernelGGL(log_match, dim3((unsigned)grid), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, cdoc, chunk,
+                       tile, nt, n_lines, line_start, line_end, line_mask);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
