@@ -199,6 +199,14 @@ int krca_stream_score(const float* x_new, int64_t P, int32_t M, int32_t delta, i
                       float z_thr, void* state, float* z_last, float* score, int32_t* n_exceed, uint8_t* flags,
                       void* stream);
 
+/* ---- f3: betweenness centrality for the SPOF check (TopologyAgent._analyze_single_points_of_failure,
+ * ref:agents/topology_agent.py:322-356, networkx 3.4.2 betweenness_centrality): Brandes over the
+ * OUT-edge CSR (row u = successors of u), `batch` sources in flight (one workgroup each),
+ * float64, normalized / directed as networkx.  ws: krca_betweenness_ws_size(N, batch) bytes. */
+int64_t krca_betweenness_ws_size(int64_t N, int32_t batch);
+int krca_betweenness(const int64_t* row_ptr, const int32_t* col, int64_t N, int32_t normalized, int32_t directed,
+                     int32_t batch, void* ws, double* bc, void* stream);
+
 /* ---- f1: pod status categorisation (ResourceAnalyzer._analyze_pods + _is_pod_healthy,
  * ref:agents/resource_analyzer.py:264-380, :856-895) over columnar pod status (encoding in
  * csrc/podstate.hip and krca/podstate.py): mask[p] bit b = membership of status group b in the

@@ -177,7 +177,7 @@ class TopologyAgent(BaseAgent):
     def _analyze_single_points_of_failure(self):
         g = self.service_graph
         try:
-            bc = nx.betweenness_centrality(g)
+            bc = self._betweenness(g)
             for node in [n for n, v in bc.items() if v > 0.5]:
                 ntype = g.nodes[node].get('type', 'unknown')
                 if ntype not in ('deployment', 'service'):
@@ -193,6 +193,20 @@ class TopologyAgent(BaseAgent):
         except Exception as e:
             self.add_reasoning_step(observation=f"Error analyzing single points of failure: {str(e)}",
                                     conclusion="Unable to identify potential single points of failure")
+
+    def _betweenness(self, g):
+        """nx.betweenness_centrality(g) (ref :329) on the device (krca_betweenness):
+        node order = g's insertion order, out-edges in adjacency order; {node: value}."""
+        nodes = list(g.nodes)
+        pos = {n: i for i, n in enumerate(nodes)}
+        row_ptr = [0]
+        col = []
+        nbrs = g.successors if g.is_directed() else g.neighbors
+        for n in nodes:
+            col.extend(pos[m] for m in nbrs(n))
+            row_ptr.append(len(col))
+        bc = self.engine.betweenness(row_ptr, col, normalized=True, directed=g.is_directed())
+        return {n: float(bc[i]) for i, n in enumerate(nodes)}
 
     def _analyze_isolated_services(self):
         g = self.service_graph

@@ -69,6 +69,8 @@ SIGNATURES = {
     "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "krca_betweenness_ws_size": (c_i64, [c_i64, c_i32]),
+    "krca_betweenness": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "krca_pod_groups": (c_i32, []),
     "krca_pod_classify": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "krca_topk_workspace_size": (c_i64, [c_i64, c_i32]),
@@ -205,6 +207,24 @@ class NativeEngine:
             return np.zeros((0, x.shape[2]), np.float32)
         sel = self._dev(idx)
         return x[x.shape[0] - 1].index_select(0, sel).cpu().numpy()
+
+    # -- f3 betweenness ---------------------------------------------------------------------------
+    def betweenness(self, row_ptr, col, normalized=True, directed=True, batch=1024):
+        """Out-edge CSR (host arrays) -> float64 betweenness per node (host), networkx semantics."""
+        torch = self.torch
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        N = len(rp) - 1
+        bc = torch.empty(max(N, 1), dtype=torch.float64, device=self.device)
+        if N == 0:
+            return np.zeros(0)
+        batch = int(max(1, min(batch, N)))
+        ws = self._workspace("betweenness", self.lib.krca_betweenness_ws_size(N, batch))
+        c = np.ascontiguousarray(col, np.int32)
+        rp_d = self._dev(rp)
+        col_d = self._dev(c if len(c) else np.zeros(1, np.int32))
+        _check(self.lib.krca_betweenness(self.ptr(rp_d), self.ptr(col_d), N, int(bool(normalized)), int(bool(directed)),
+                                         batch, self.ptr(ws), self.ptr(bc), self._stream()), "krca_betweenness")
+        return bc[:N].cpu().numpy()
 
     # -- f1 pod status groups ------------------------------------------------------------------
     def pod_classify_device(self, pod_code, cont_off, cont_code):

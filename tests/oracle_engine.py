@@ -55,3 +55,14 @@ class OracleEngine:
 
     def pod_classify(self, pod_code, cont_off, cont_code):
         return oracle.pod_classify_ref(pod_code, cont_off, cont_code)
+
+    def betweenness(self, row_ptr, col, normalized=True, directed=True, batch=1024):
+        import networkx as nx
+        N = len(row_ptr) - 1
+        g = nx.DiGraph() if directed else nx.Graph()
+        g.add_nodes_from(range(N))
+        for u in range(N):
+            for e in range(row_ptr[u], row_ptr[u + 1]):
+                g.add_edge(u, int(col[e]))
+        bc = nx.betweenness_centrality(g, normalized=normalized)
+        return np.array([bc[i] for i in range(N)])
