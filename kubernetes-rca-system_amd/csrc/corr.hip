@@ -393,6 +393,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
       for (int j = 0; j < 2; ++j) {
         const int col = wc * 64 + j * 32 + r32;
         const float pc = diag ? 4.f : sphc[col];  // diagonal tile: both orders present, rows only
+        uint64_t me[16];  // per value slot: the lanes holding a candidate of the row or column pod
         uint64_t any = 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -404,12 +405,16 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
             rc[e][1] += __builtin_popcount((uint32_t)(m >> 32));
             colcnt[j] += hit ? 1 : 0;
           }
-          any |= __ballot(a > fminf(pr[e], pc));
+          me[e] = __ballot(a > fminf(pr[e], pc));
+          any |= me[e];
         }
-        if (any && debug != 3) {  // slow path: this 16-value group holds at least one candidate
+        // slow path, only for the value slots that hold a candidate: at C3 densities nearly every
+        // 16-slot group has one, but only ~5 of its 16 slots do
+        if (any && debug != 3) {
           const int gc = (int)(rowB + col);
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
+            if (!me[e]) continue;  // wave-uniform
             const float v = acc[i][j][e];
             const float a = fabsf(v);
             const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;

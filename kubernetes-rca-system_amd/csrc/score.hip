@@ -135,8 +135,9 @@ __global__ __launch_bounds__(256) void rolling_score_ring(const float* __restric
 // wave-uniform buffer descriptor on the block's first row, the lane's 32-bit byte offset in
 // voffset and the row offset j*S*4 in soffset, so a load costs no per-lane address arithmetic
 // (`buffer_load_dword v, v_off, s[rsrc], s_off offen`).  Requires 4*S*W < 2^31.
+template <int AUX = 0>  // cache policy bits: 0 default, 2 = nt (streamed once)
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, AUX));
 }
 
 template <int W>
@@ -206,7 +207,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float* x, int
                                            0x00020000);
 }
 
-template <int W, int C>
+template <int W, int C, int AUX = 0>
 __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restrict__ x, int64_t S, int T, int M,
                                                           double thr2, float* __restrict__ z_last,
                                                           float* __restrict__ score, int32_t* __restrict__ n_exceed,
@@ -226,12 +227,12 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
   for (int c = 0; c < NC; ++c) {
     const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, c * C, T);
 #pragma unroll
-    for (int j = 0; j < C; ++j) ring[c * C + j] = bload(rs, voff, rowb * j);
+    for (int j = 0; j < C; ++j) ring[c * C + j] = bload<AUX>(rs, voff, rowb * j);
   }
   {
     const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, W, T);
 #pragma unroll
-    for (int j = 0; j < C; ++j) cur[j] = bload(rs, voff, rowb * j);
+    for (int j = 0; j < C; ++j) cur[j] = bload<AUX>(rs, voff, rowb * j);
   }
 #pragma unroll
   for (int j = 0; j < W; ++j) {
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
       float nxt[C];
       const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t0 + (c + 1) * C, T);
 #pragma unroll
-      for (int j = 0; j < C; ++j) nxt[j] = bload(rs, voff, rowb * j);
+      for (int j = 0; j < C; ++j) nxt[j] = bload<AUX>(rs, voff, rowb * j);
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         step(st, cur[j], ring[c * C + j], Wd, epsB, thr2, false);
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
     if (c > 0) {
       const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t0 + c * C, T);
 #pragma unroll
-      for (int j = 0; j < C; ++j) cur[j] = bload(rs, voff, rowb * j);
+      for (int j = 0; j < C; ++j) cur[j] = bload<AUX>(rs, voff, rowb * j);
     }
 #pragma unroll
     for (int j = 0; j < C; ++j) {
@@ -423,12 +424,21 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
   const char* e_chunk = getenv("KRCA_SCORE_CHUNK");
   const int impl = e_impl ? atoi(e_impl) : 0;
   const int chunk = e_chunk ? atoi(e_chunk) : 20;
+  // the metric stream is read once: non-temporal loads (cache policy nt) by default, 6.17 -> 6.61 TB/s
+  // at C4 (tools/score_ab.py); KRCA_SCORE_NT=0 restores the default policy
+  const char* e_nt = getenv("KRCA_SCORE_NT");
+  const bool nt = !(e_nt && atoi(e_nt) == 0);
   KRCA_CHECK_ARG(S < (int64_t(1) << 32), "krca_rolling_score: P*M must be < 2^32");
   // impl 0: pipelined chunks (needs T > W and C*4*S < 2^31); 1: plain loads; 2: W-block buffer loads
   const int cw = W == 60 ? chunk : (W == 30 ? 15 : (W == 20 ? 10 : W));  // rows per pipelined chunk
   const bool fits = T > W && S * 4 * cw < (int64_t(1) << 31);
-#define KRCA_PIPE(WV, CV) \
-  hipLaunchKernelGGL((rolling_score_pipe<WV, CV>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed, flags)
+#define KRCA_PIPE(WV, CV)                                                                                   \
+  if (nt)                                                                                                   \
+    hipLaunchKernelGGL((rolling_score_pipe<WV, CV, 2>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
+                       n_exceed, flags);                                                                    \
+  else                                                                                                      \
+    hipLaunchKernelGGL((rolling_score_pipe<WV, CV, 0>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
+                       n_exceed, flags);
 #define KRCA_RING(WV)                                                                                         \
   if (impl == 2 && S * 4 * WV < (int64_t(1) << 31))                                                           \
     hipLaunchKernelGGL(rolling_score_ring_buf<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score,        \
@@ -439,27 +449,27 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
   const bool pipe = impl == 0 && fits;
   switch (W) {
     case 60:
-      if (pipe && chunk == 10) KRCA_PIPE(60, 10);
-      else if (pipe && chunk == 12) KRCA_PIPE(60, 12);
-      else if (pipe && chunk == 15) KRCA_PIPE(60, 15);
-      else if (pipe && chunk == 30) KRCA_PIPE(60, 30);
-      else if (pipe) KRCA_PIPE(60, 20);
+      if (pipe && chunk == 10) { KRCA_PIPE(60, 10) }
+      else if (pipe && chunk == 12) { KRCA_PIPE(60, 12) }
+      else if (pipe && chunk == 15) { KRCA_PIPE(60, 15) }
+      else if (pipe && chunk == 30) { KRCA_PIPE(60, 30) }
+      else if (pipe) { KRCA_PIPE(60, 20) }
       else { KRCA_RING(60) }
       break;
     case 30:
-      if (pipe) KRCA_PIPE(30, 15);
+      if (pipe) { KRCA_PIPE(30, 15) }
       else { KRCA_RING(30) }
       break;
     case 20:
-      if (pipe) KRCA_PIPE(20, 10);
+      if (pipe) { KRCA_PIPE(20, 10) }
       else { KRCA_RING(20) }
       break;
     case 15:
-      if (pipe) KRCA_PIPE(15, 15);
+      if (pipe) { KRCA_PIPE(15, 15) }
       else { KRCA_RING(15) }
       break;
     case 10:
-      if (pipe) KRCA_PIPE(10, 10);
+      if (pipe) { KRCA_PIPE(10, 10) }
       else { KRCA_RING(10) }
       break;
     default:

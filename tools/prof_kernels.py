@@ -31,7 +31,8 @@ def timed(torch, fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods"])
+    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods", "bc"])
+    ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--docs", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=3)
@@ -73,6 +74,26 @@ def main():
         out = dict(kernel="corr top-k", ms=ms, ms_prepare=ms_prep, flops=flops,
                    tflops=flops / (min(ms) * 1e-3) / 1e12, certified=float((r["cert"] > 0).float().mean()),
                    cand_mean=float(cnt.mean()), cand_max=float(cnt.max()), cand_p99=float(cnt.quantile(0.99)))
+    elif a.what == "bc":
+        # f3: betweenness over a strongly connected service graph (each node links to 2 random
+        # earlier nodes, both directions: the worst case, every source reaches every node)
+        N = a.pods
+        rng = np.random.default_rng(0)
+        v = np.repeat(np.arange(1, N, dtype=np.int64), 2)
+        u = (rng.random(len(v)) * v).astype(np.int64)
+        key = np.unique(np.concatenate([u * N + v, v * N + u]))
+        src, dst = key // N, key % N
+        rp = np.zeros(N + 1, np.int64)
+        np.cumsum(np.bincount(src, minlength=N), out=rp[1:])
+        col = dst.astype(np.int32)
+        eng.betweenness(rp, col, batch=a.batch)
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            bc = eng.betweenness(rp, col, batch=a.batch)
+        s = (time.perf_counter() - t0) / a.reps
+        E = len(col)
+        # per source: the forward BFS and the dependency pull each read every reached edge once
+        out = dict(kernel="krca_betweenness", nodes=N, edges=E, s=s, teps=2 * N * E / s, bc_sum=float(bc.sum()))
     elif a.what == "pods":
         from krca import podstate
         P = a.pods * 10

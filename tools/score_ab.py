@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
 
 VARIANTS = [("ring_buf", {"KRCA_SCORE_IMPL": "2"}), ("ring", {"KRCA_SCORE_IMPL": "1"})] + [
-    (f"pipe_c{c}", {"KRCA_SCORE_IMPL": "0", "KRCA_SCORE_CHUNK": str(c)}) for c in (10, 12, 15, 20, 30)]
+    (f"pipe_c{c}", {"KRCA_SCORE_IMPL": "0", "KRCA_SCORE_CHUNK": str(c)}) for c in (10, 12, 15, 20, 30)] + [
+    ("pipe_c20_default_policy", {"KRCA_SCORE_IMPL": "0", "KRCA_SCORE_CHUNK": "20", "KRCA_SCORE_NT": "0"})]
 
 
 def main():
@@ -34,7 +35,7 @@ def main():
     for name, env in VARIANTS:
         if a.only and name not in a.only.split(","):
             continue
-        for k in ("KRCA_SCORE_IMPL", "KRCA_SCORE_CHUNK"):
+        for k in ("KRCA_SCORE_IMPL", "KRCA_SCORE_CHUNK", "KRCA_SCORE_NT"):
             os.environ.pop(k, None)
         os.environ.update(env)
         o = eng.rolling_score_device(x)
