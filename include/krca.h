@@ -207,6 +207,25 @@ int64_t krca_betweenness_ws_size(int64_t N, int32_t batch);
 int krca_betweenness(const int64_t* row_ptr, const int32_t* col, int64_t N, int32_t normalized, int32_t directed,
                      int32_t batch, void* ws, double* bc, void* stream);
 
+/* ---- f2: service-graph construction from Kubernetes objects (TopologyAgent._build_service_graph
+ * ref:agents/topology_agent.py:94-160, _infer_dependencies_from_env :228-260; the same selector
+ * test in ResourceAnalyzer._find_matching_pods ref:agents/resource_analyzer.py:835-854).
+ * selector_match: bits[d * ceil(S/64) + s/64] bit s%64 = every item id of selector s occurs among
+ *   the item ids of object d (ids interned by the host: krca/topograph.py); bit-exact.
+ * substr_match: every (value v, key k) with key k occurring in value v (bytes), appended to
+ *   out[cap] as v*K + k (once per occurrence, unordered); *n_out (device u64) = occurrences, may
+ *   exceed cap.  lens = the distinct key lengths >= 1, ascending; table / hash from
+ *   krca_substr_prepare (table_size = krca_substr_table_size(K) int32 slots). */
+int krca_selector_match(const int32_t* lab, const int64_t* lab_off, int64_t D, const int32_t* sel,
+                        const int64_t* sel_off, int64_t S, uint64_t* bits, void* stream);
+int64_t krca_substr_table_size(int64_t K);
+int krca_substr_prepare(const uint8_t* pat, const int64_t* pat_off, int64_t K, int32_t* table, int64_t table_size,
+                        uint64_t* hash, void* stream);
+int krca_substr_match(const uint8_t* text, const int64_t* val_off, int64_t V, const uint8_t* pat,
+                      const int64_t* pat_off, int64_t K, const int32_t* table, int64_t table_size,
+                      const uint64_t* hash, const int32_t* lens, int32_t n_lens, int64_t* out, int64_t cap,
+                      uint64_t* n_out, void* stream);
+
 /* ---- f1: pod status categorisation (ResourceAnalyzer._analyze_pods + _is_pod_healthy,
  * ref:agents/resource_analyzer.py:264-380, :856-895) over columnar pod status (encoding in
  * csrc/podstate.hip and krca/podstate.py): mask[p] bit b = membership of status group b in the

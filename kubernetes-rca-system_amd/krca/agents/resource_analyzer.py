@@ -12,7 +12,7 @@ findings stay on the host.  The reference's ``logging`` to a file in the CWD is 
 import json
 from datetime import datetime
 
-from .. import podstate
+from .. import podstate, topograph
 
 _RELATION_KEYWORDS = {  # ref :774-781
     'crash': ['backoff', 'crash', 'exit', 'fail', 'error'],
@@ -68,7 +68,8 @@ class ResourceAnalyzer:
                 'findings': self.findings, 'reasoning_steps': self.reasoning_steps}
 
     def _analyze_services(self, services, namespace):  # ref :96-148
-        for s in services:
+        device = self._service_matches(services, namespace)
+        for si, s in enumerate(services):
             name = s['metadata']['name']
             s['spec'].get('type', 'ClusterIP')
             sel = s['spec'].get('selector', {})
@@ -78,7 +79,7 @@ class ResourceAnalyzer:
                                  "No pod selector specified in service definition",
                                  "Add appropriate selectors to match target pods")
                 continue
-            matching = self._find_matching_pods(namespace, sel)
+            matching = device[si] if device is not None else self._find_matching_pods(namespace, sel)
             if not matching:
                 self.add_finding(comp, "Service selector matches no pods", "high",
                                  f"Selector {sel} does not match any pods in the namespace",
@@ -289,6 +290,26 @@ class ResourceAnalyzer:
                              "high" if reason in ('Failed', 'FailedCreate', 'FailedMount') else "medium",
                              f"Message: {last.get('message', '')} (event count: {len(lst)})",
                              "Investigate the reported issue and take appropriate action")
+
+    def _service_matches(self, services, namespace):
+        """Every service's matching pods (the O(S*P) loop of _find_matching_pods, ref :835-854)
+        from one krca_selector_match launch over (pod, service) pairs; the pod list is fetched
+        once instead of once per service.  None -> the per-service host loop (inputs that are not
+        plain dicts keep the reference's own errors)."""
+        try:
+            sels = [s['spec'].get('selector', {}) for s in services]
+            if not any(sels) or not all(isinstance(x, dict) for x in sels):
+                return None
+            pods = self.k8s_client.get_pods(namespace)
+            labels = [p['metadata'].get('labels', {}) for p in pods]
+        except Exception:
+            return None
+        if not pods or not all(isinstance(x, dict) for x in labels):
+            return None
+        bits = topograph.selector_bits(self._eng(), [x.items() for x in labels], [x.items() for x in sels],
+                                       identity=False)
+        cols = topograph.match_cols(bits, len(services))
+        return [[pods[i] for i in c] for c in cols]
 
     def _find_matching_pods(self, namespace, selector):
         return [p for p in self.k8s_client.get_pods(namespace)

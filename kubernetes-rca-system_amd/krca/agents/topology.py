@@ -13,6 +13,7 @@ kernel consumes.
 import networkx as nx
 import numpy as np
 
+from .. import topograph
 from .base import BaseAgent
 
 EDGE_TYPES = ("selects", "routes", "mounts", "env_from", "env_var", "depends_on")
@@ -59,6 +60,7 @@ class TopologyAgent(BaseAgent):
     # -- graph construction (ref :94-260) ------------------------------------------------
     def _build_service_graph(self, deployments, services, pods, ingresses, configmaps, secrets):
         g = self.service_graph
+        sel_rows = self._selector_rows(deployments, services)
         for s in services:
             spec = s.get('spec', {})
             g.add_node(s['metadata']['name'], type='service', ports=spec.get('ports', []),
@@ -68,10 +70,13 @@ class TopologyAgent(BaseAgent):
             labels = d.get('metadata', {}).get('labels', {})
             g.add_node(dname, type='deployment', replicas=d.get('spec', {}).get('replicas', 1),
                        labels=labels, containers=len(_tmpl_spec(d).get('containers', [])))
-            for s in services:
-                sel = s.get('spec', {}).get('selector', {})
-                if all(item in labels.items() for item in sel.items()):
-                    g.add_edge(s['metadata']['name'], dname, type='selects')
+            for si in (next(sel_rows) if sel_rows is not None else range(len(services))):
+                s = services[si]
+                if sel_rows is None:
+                    sel = s.get('spec', {}).get('selector', {})
+                    if not all(item in labels.items() for item in sel.items()):
+                        continue
+                g.add_edge(s['metadata']['name'], dname, type='selects')
         for ing in ingresses:
             iname = ing['metadata']['name']
             g.add_node(iname, type='ingress')
@@ -127,14 +132,52 @@ class TopologyAgent(BaseAgent):
             name, ns = s['metadata']['name'], s['metadata']['namespace']
             for key in (name, f"{name}.{ns}", f"{name}.{ns}.svc", f"{name}.{ns}.svc.cluster.local"):
                 dns[key] = name
+        hits = self._env_hits(deployments, dns)
+        keys = list(dns.items())
         for d in deployments:
             dname = d['metadata']['name']
             for ctr in _tmpl_spec(d).get('containers', []):
                 for var in ctr.get('env', []):
+                    if hits is not None:
+                        for k in next(hits):
+                            svc = keys[k][1]
+                            if svc in self.service_graph:
+                                self.service_graph.add_edge(dname, svc, type='depends_on')
+                        continue
                     value = var.get('value', '')
                     for key, svc in dns.items():
                         if key in value and svc in self.service_graph:
                             self.service_graph.add_edge(dname, svc, type='depends_on')
+
+    # -- all-pairs tests of the build on the device (csrc/topograph.hip) ---
+    def _selector_rows(self, deployments, services):
+        """Per deployment, the ascending indices of the services whose selector matches its labels
+        (ref :132-134), computed by krca_selector_match; None -> the host loop runs instead (inputs
+        that are not plain dicts, whose errors and short-circuits the loop itself defines)."""
+        if not deployments or not services:
+            return None
+        try:
+            labels = [d.get('metadata', {}).get('labels', {}) for d in deployments]
+            sels = [s.get('spec', {}).get('selector', {}) for s in services]
+        except Exception:
+            return None
+        if not all(isinstance(x, dict) for x in labels) or not all(isinstance(x, dict) for x in sels):
+            return None
+        bits = topograph.selector_bits(self.engine, [x.items() for x in labels], [x.items() for x in sels])
+        return topograph.match_rows(bits, len(services))
+
+    def _env_hits(self, deployments, dns):
+        """Per env var in visiting order, the ascending indices into ``dns`` of the keys contained in
+        its value (ref :255-260), computed by krca_substr_match; None -> host loop (non-str values)."""
+        try:
+            values = [var.get('value', '') for d in deployments for ctr in _tmpl_spec(d).get('containers', [])
+                      for var in ctr.get('env', [])]
+        except Exception:
+            return None
+        if not values or not dns or not all(type(v) is str for v in values) \
+                or not all(type(k) is str for k in dns):
+            return None
+        return iter(topograph.substring_matches(self.engine, values, list(dns)))
 
     # -- heuristics (ref :262-401) -------------------------------------------------------
     def _analyze_service_dependencies(self):

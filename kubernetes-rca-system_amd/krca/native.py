@@ -71,6 +71,11 @@ SIGNATURES = {
     "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "krca_betweenness_ws_size": (c_i64, [c_i64, c_i32]),
     "krca_betweenness": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "krca_selector_match": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "krca_substr_table_size": (c_i64, [c_i64]),
+    "krca_substr_prepare": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "krca_substr_match": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_i64,
+                                  c_vp, c_vp]),
     "krca_pod_groups": (c_i32, []),
     "krca_pod_classify": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "krca_topk_workspace_size": (c_i64, [c_i64, c_i32]),
@@ -225,6 +230,63 @@ class NativeEngine:
         _check(self.lib.krca_betweenness(self.ptr(rp_d), self.ptr(col_d), N, int(bool(normalized)), int(bool(directed)),
                                          batch, self.ptr(ws), self.ptr(bc), self._stream()), "krca_betweenness")
         return bc[:N].cpu().numpy()
+
+    # -- f2 service-graph construction --------------------------------------------------------
+    def selector_match(self, lab, lab_off, sel, sel_off):
+        """Interned item-id sets (krca/topograph.py) -> uint64 bits [D][ceil(S/64)] (host):
+        bit s of row d = every item of selector s is among the items of object d."""
+        torch = self.torch
+        D, S = len(lab_off) - 1, len(sel_off) - 1
+        SW = (S + 63) // 64
+        if D <= 0 or S <= 0:
+            return np.zeros((max(D, 0), SW), np.uint64)
+        pad = lambda a, dt: np.ascontiguousarray(a, dt) if len(a) else np.zeros(1, dt)  # noqa: E731
+        lab_d, lo_d = self._dev(pad(lab, np.int32)), self._dev(np.ascontiguousarray(lab_off, np.int64))
+        sel_d, so_d = self._dev(pad(sel, np.int32)), self._dev(np.ascontiguousarray(sel_off, np.int64))
+        bits = torch.empty((D, SW), dtype=torch.int64, device=self.device)
+        _check(self.lib.krca_selector_match(self.ptr(lab_d), self.ptr(lo_d), D, self.ptr(sel_d), self.ptr(so_d), S,
+                                            self.ptr(bits), self._stream()), "krca_selector_match")
+        return bits.cpu().numpy().view(np.uint64)
+
+    def substr_match(self, text, val_off, pat, pat_off):
+        """Byte blobs of V values / K keys -> sorted unique int64 v*K + k for every key k that
+        occurs in value v (Python's `key in value`; an empty key occurs in every value)."""
+        torch = self.torch
+        V, K = len(val_off) - 1, len(pat_off) - 1
+        if V <= 0 or K <= 0:
+            return np.zeros(0, np.int64)
+        pat_off = np.ascontiguousarray(pat_off, np.int64)
+        klen = np.diff(pat_off)
+        lens = np.unique(klen[klen > 0]).astype(np.int32)
+        pairs = np.zeros(0, np.int64)
+        if len(lens) and len(text):
+            dev = lambda b: self._dev(np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8))  # noqa: E731
+            text_d, pat_d = dev(bytes(text)), dev(bytes(pat))
+            vo_d, po_d = self._dev(np.ascontiguousarray(val_off, np.int64)), self._dev(pat_off)
+            lens_d = self._dev(lens)
+            tsize = int(self.lib.krca_substr_table_size(K))
+            table = torch.empty(tsize, dtype=torch.int32, device=self.device)
+            hashes = torch.empty(K, dtype=torch.int64, device=self.device)
+            _check(self.lib.krca_substr_prepare(self.ptr(pat_d), self.ptr(po_d), K, self.ptr(table), tsize,
+                                                self.ptr(hashes), self._stream()), "krca_substr_prepare")
+            n_out = torch.zeros(1, dtype=torch.int64, device=self.device)
+            cap = max(4096, 2 * V)
+            while True:
+                out = torch.empty(cap, dtype=torch.int64, device=self.device)
+                _check(self.lib.krca_substr_match(self.ptr(text_d), self.ptr(vo_d), V, self.ptr(pat_d), self.ptr(po_d),
+                                                  K, self.ptr(table), tsize, self.ptr(hashes), self.ptr(lens_d),
+                                                  len(lens), self.ptr(out), cap, self.ptr(n_out), self._stream()),
+                       "krca_substr_match")
+                n = int(n_out.item())
+                if n <= cap:
+                    break
+                cap = n
+            pairs = np.unique(out[:n].cpu().numpy())
+        empty = np.flatnonzero(klen == 0)
+        if len(empty):
+            allv = (np.arange(V, dtype=np.int64)[:, None] * K + empty[None, :]).ravel()
+            pairs = np.union1d(pairs, allv)
+        return pairs
 
     # -- f1 pod status groups ------------------------------------------------------------------
     def pod_classify_device(self, pod_code, cont_off, cont_code):

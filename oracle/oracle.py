@@ -13,6 +13,9 @@ Parity anchors:
   * pod status groups: :func:`categorize_pods_ref` restates ref:agents/resource_analyzer.py:
     264-380 + :856-895 on pod dicts (pinned by the C1 ResourceAnalyzer golden), and
     :func:`pod_classify_ref` the same rules on the columnar encoding of krca/podstate.py;
+  * service-graph construction: :func:`selector_match_ref` / :func:`substr_match_ref` are the
+    pair tests of ref:agents/topology_agent.py:133,257 and ref:agents/resource_analyzer.py:851,
+    pinned through the agents by tests/golden/topograph_cases.json (reference graphs);
   * rolling z-score / correlation / template hashing have no reference counterpart (new
     primitives named by the north star): their float64 restatements here are
     "parity unpinned" by the reference and define the semantics.
@@ -308,6 +311,40 @@ def pod_classify_ref(pod_code, cont_off, cont_code):
     hist = np.array([int(((mask >> b) & 1).sum()) for b in range(12)], np.int32)
     return mask, hist
 
+
+
+# ------------------------------------------------------------------------------------------
+# f2: service-graph construction (ref:agents/topology_agent.py:94-260,
+#     ref:agents/resource_analyzer.py:835-854) — semantics of csrc/topograph.hip
+# ------------------------------------------------------------------------------------------
+def selector_match_ref(lab, lab_off, sel, sel_off):
+    """Interned item-id sets -> uint64 bits [D][ceil(S/64)]: bit s of row d iff every id of
+    selector s occurs among the ids of object d (the ``all(item in labels.items() ...)`` test
+    of ref:agents/topology_agent.py:133 once the host has interned the items)."""
+    D, S = len(lab_off) - 1, len(sel_off) - 1
+    SW = (S + 63) // 64
+    bits = np.zeros((D, SW), np.uint64)
+    sels = [set(int(x) for x in sel[sel_off[s]:sel_off[s + 1]]) for s in range(S)]
+    for d in range(D):
+        have = set(int(x) for x in lab[lab_off[d]:lab_off[d + 1]])
+        for s in range(S):
+            if sels[s] <= have:
+                bits[d, s // 64] |= np.uint64(1 << (s % 64))
+    return bits
+
+
+def substr_match_ref(text, val_off, pat, pat_off):
+    """Byte blobs -> sorted int64 v*K + k for every key k contained in value v (``key in value``
+    of ref:agents/topology_agent.py:257; the empty key is in every value)."""
+    text, pat = bytes(text), bytes(pat)
+    V, K = len(val_off) - 1, len(pat_off) - 1
+    out = []
+    for v in range(V):
+        val = text[val_off[v]:val_off[v + 1]]
+        for k in range(K):
+            if pat[pat_off[k]:pat_off[k + 1]] in val:
+                out.append(v * K + k)
+    return np.asarray(out, np.int64)
 
 # ------------------------------------------------------------------------------------------
 # C restatement (bit-exact twin of the device arithmetic)

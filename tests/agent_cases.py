@@ -231,3 +231,39 @@ def check_events():
     if not same(EventsAgent(DictClient(events=[])).analyze("x"), gold["empty"]):
         bad.append("empty")
     return bad
+
+
+def _jsonable(x):
+    return json.loads(json.dumps(x))
+
+
+def check_topograph(engine, force_host=False):
+    """f2: the build's service-graph construction and the ResourceAnalyzer selector
+    matches against the reference's graphs on seeded random clusters (topograph_cases.json,
+    captured by tests/golden/capture_topograph.py).  Returns a list of mismatches."""
+    bad = []
+    for name, case in load("topograph_cases.json").items():
+        sc = case["inputs"]
+        ag = TopologyAgent(DictClient(**sc), engine=engine)
+        if force_host:
+            ag._selector_rows = lambda *a: None
+            ag._env_hits = lambda *a: None
+        ag._build_service_graph(sc["deployments"], sc["services"], sc["pods"], sc["ingresses"], sc["configmaps"],
+                                sc["secrets"])
+        g = ag.service_graph
+        nodes = _jsonable([[n, dict(a)] for n, a in g.nodes(data=True)])
+        edges = [[u, v, a.get("type")] for u, v, a in g.edges(data=True)]
+        if nodes != case["nodes"]:
+            bad.append((name, "nodes"))
+        if edges != case["edges"]:
+            bad.append((name, "edges", len(edges), len(case["edges"])))
+        ra = ResourceAnalyzer(DictClient(**sc), engine=engine)
+        dev = ra._service_matches(sc["services"], "shop")
+        if dev is None:
+            bad.append((name, "service matches not on the device path"))
+        else:
+            idx = {p["metadata"]["name"]: i for i, p in enumerate(sc["pods"])}
+            got = [[idx[p["metadata"]["name"]] for p in m] for m in dev]
+            if got != case["service_pods"]:
+                bad.append((name, "service_pods"))
+    return bad

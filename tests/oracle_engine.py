@@ -66,3 +66,9 @@ class OracleEngine:
                 g.add_edge(u, int(col[e]))
         bc = nx.betweenness_centrality(g, normalized=normalized)
         return np.array([bc[i] for i in range(N)])
+
+    def selector_match(self, lab, lab_off, sel, sel_off):
+        return oracle.selector_match_ref(lab, lab_off, sel, sel_off)
+
+    def substr_match(self, text, val_off, pat, pat_off):
+        return oracle.substr_match_ref(text, val_off, pat, pat_off)
