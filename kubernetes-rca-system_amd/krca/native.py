@@ -260,7 +260,7 @@ class NativeEngine:
         lens = np.unique(klen[klen > 0]).astype(np.int32)
         pairs = np.zeros(0, np.int64)
         if len(lens) and len(text):
-            dev = lambda b: self._dev(np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8))  # noqa: E731
+            dev = lambda b: self._dev(np.frombuffer(bytearray(b), np.uint8) if len(b) else np.zeros(1, np.uint8))  # noqa: E731
             text_d, pat_d = dev(bytes(text)), dev(bytes(pat))
             vo_d, po_d = self._dev(np.ascontiguousarray(val_off, np.int64)), self._dev(pat_off)
             lens_d = self._dev(lens)
