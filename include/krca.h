@@ -234,6 +234,20 @@ int32_t krca_pod_groups(void);
 int krca_pod_classify(const uint8_t* pod_code, const int64_t* cont_off, const uint16_t* cont_code, int64_t P,
                       uint16_t* mask, int32_t* hist, void* stream);
 
+/* ---- f4: group-bys of EventsAgent (ref:agents/events_agent.py:105-133 objects, :169-228 scheduling,
+ * :230-290 volumes, :330-375 control plane, :377-446 nodes) and Coordinator._correlate_findings
+ * (ref:agents/coordinator.py:118-155: group by component, max severity).  N membership records
+ * (slot[i], key[i]); slots outside [0, S) are ignored; key < 0 = member that is not selected.
+ * Output: one 8 x int64 record per slot, rec[s*8 + j]:
+ *   j = 0      first member index (dict insertion order; INT32_MAX if the slot is empty)
+ *   j = 1      (members << 32) | (members with key >= 0)
+ *   j = 2 + r  r-th largest key >= 0 (-1 if none), r < R; ranks r >= 1 only over i < n_ranked.
+ * Keys must be distinct within a slot for r >= 1 (the host packs (rank << 32) | (2^31-1-index)).
+ * Bit-exact; 1 <= R <= krca_group_max_rank(), N < 2^31, 0 <= n_ranked <= N. */
+int32_t krca_group_max_rank(void);
+int krca_group_reduce(const int32_t* slot, const int64_t* key, int64_t N, int64_t n_ranked, int32_t S, int32_t R,
+                      int64_t* rec, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,15 +70,37 @@ class Coordinator:
             out['ranked_root_causes'] = ranked
         return out
 
-    @staticmethod
-    def _correlate_findings(*lists):  # ref :118-155
-        groups = {}
-        for lst in lists:
-            for f in lst:
-                groups.setdefault(f['component'], []).append(f)
-        return [{'component': comp, 'related_findings': fs, 'correlation_type': 'component',
-                 'severity': max((f['severity'] for f in fs), key=SEVERITY_ORDER.index)}
-                for comp, fs in groups.items() if len(fs) > 1]
+    def _correlate_findings(self, *lists):  # ref :118-155
+        """Group by component (first-seen order), keep groups with > 1 finding, max severity by
+        SEVERITY_ORDER.  The group-by runs on the device (krca_group_reduce, f4): component ids
+        interned here, severity index as the key; member lists are split on the host."""
+        flat = [f for lst in lists for f in lst]
+        if not flat:
+            return []
+        ids, comps = {}, []
+        slot = np.empty(len(flat), np.int32)
+        sev = np.empty(len(flat), np.int64)
+        for i, f in enumerate(flat):
+            c = f['component']
+            slot[i] = j = ids.setdefault(c, len(ids))
+            if j == len(comps):
+                comps.append(c)
+            s = f['severity']
+            sev[i] = SEVERITY_ORDER.index(s) if type(s) is str and s in SEVERITY_ORDER else -1
+        S = len(comps)
+        first, count, n_key, top = self.engine.group_reduce(slot, sev, S, 1)
+        order = np.argsort(slot, kind='stable')
+        members = np.split(order, np.cumsum(count)[:-1])
+        out = []
+        for g in np.argsort(first, kind='stable').tolist():
+            if count[g] < 2:
+                continue
+            if n_key[g] != count[g]:  # the reference's max(key=list.index) raises on the first bad one
+                for i in members[g].tolist():
+                    list(SEVERITY_ORDER).index(flat[i]['severity'])
+            out.append({'component': comps[g], 'related_findings': [flat[i] for i in members[g].tolist()],
+                        'correlation_type': 'component', 'severity': SEVERITY_ORDER[int(top[0, g])]})
+        return out
 
     @staticmethod
     def _identify_root_causes(correlated):  # ref :157-184

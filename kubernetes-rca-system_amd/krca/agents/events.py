@@ -1,36 +1,18 @@
-"""EventsAgent (host): group-bys over a namespace's events.
+"""EventsAgent: group-bys over a namespace's events, on the device.
 
-Reference: ref:agents/events_agent.py:4-446.  Out of the hot-path scope (SURVEY.md §2 row 9;
-§8f f4 lists a device group-by as a later step); kept on the host with identical findings so
-``Coordinator.run_analysis('comprehensive')`` correlates the same five finding lists.
+Reference: ref:agents/events_agent.py:4-446.  The events are encoded into columns once
+(krca/eventcols.py) and the five group-bys run as one ``krca_group_reduce`` launch plus one
+``krca_topk_i64`` for the frequent events; findings and reasoning steps are replayed in the
+reference's order.  A client with a bulk accessor ``get_event_columns(namespace)`` hands the
+columns over directly.  Event lists that are not plain dicts of str / int fields take the
+reference's own loops below (``_host_analyze``), which also raise the reference's errors.
 """
+from .. import eventcols
 from .base import BaseAgent
 
-CRITICAL_REASONS = ('Failed', 'FailedCreate', 'FailedScheduling', 'FailedMount', 'NodeNotReady',
-                    'KubeletNotReady', 'FailedAttachVolume', 'FailedDetachVolume', 'FreeDiskSpaceFailed',
-                    'OutOfDisk', 'MemoryPressure', 'DiskPressure', 'NetworkUnavailable', 'Unhealthy',
-                    'FailedSync', 'Evicted', 'BackOff', 'Error')  # ref:agents/events_agent.py:28-34
-
-# (predicate on message, cause, recommendation) in priority order (ref :201-215, :266-277)
-_SCHED_CAUSES = (
-    (lambda m: "Insufficient cpu" in m, "insufficient CPU", "Increase CPU capacity in your cluster or reduce CPU requests"),
-    (lambda m: "Insufficient memory" in m, "insufficient memory", "Increase memory capacity in your cluster or reduce memory requests"),
-    (lambda m: "node(s) had taint" in m, "node taints", "Add appropriate tolerations to the pod or remove taints from nodes"),
-    (lambda m: "node(s) didn't match node selector" in m, "node selector mismatch", "Update the pod's node selector or label your nodes correctly"),
-    (lambda m: "persistentvolumeclaim" in m.lower() and "pending" in m.lower(), "pending PVC", "Check the PVC status and ensure storage is available"),
-)
-_VOLUME_CAUSES = (
-    (lambda m: "timeout" in m, "mounting timeout", "Check if storage system is responsive and resources are available"),
-    (lambda m: "no such file" in m, "path doesn't exist", "Verify the volume path exists in the source"),
-    (lambda m: "permission denied" in m, "permission issue", "Check volume permissions and pod security context"),
-    (lambda m: "not found" in m and "pvc" in m, "PVC not found", "Ensure the PVC exists and is in the correct namespace"),
-)
-_NODE_ISSUES = (("NotReady", "node not ready", "Check kubelet status, node connectivity, and system logs on the node"),
-                ("MemoryPressure", "memory pressure", "Free up memory on the node or add more memory resources"),
-                ("DiskPressure", "disk pressure", "Free up disk space on the node or expand storage"),
-                ("NetworkUnavailable", "network unavailable", "Check network configuration, CNI plugins, and network connectivity"))
-_CONTROL_PLANE = ('kube-apiserver', 'kube-controller-manager', 'kube-scheduler', 'etcd')
-_NODE_REASONS = ('NodeNotReady', 'KubeletNotReady', 'MemoryPressure', 'DiskPressure', 'NetworkUnavailable')
+from ..eventcols import (CONTROL_PLANE as _CONTROL_PLANE, CRITICAL_REASONS, NODE_ISSUES as _NODE_ISSUES,  # noqa: E402
+                         NODE_REASONS as _NODE_REASONS, SCHED_CAUSES as _SCHED_CAUSES,
+                         VOLUME_CAUSES as _VOLUME_CAUSES)
 
 
 def _group(items, key):
@@ -59,25 +41,37 @@ class EventsAgent(BaseAgent):
         self.reset()
         try:
             self._maybe_set_context(context)
-            events = self.k8s_client.get_events(namespace)
-            if not events:
+            bulk = getattr(self.k8s_client, 'get_event_columns', None)
+            cols = bulk(namespace) if bulk is not None else None
+            events = cols if cols is not None else self.k8s_client.get_events(namespace)
+            if (len(cols) == 0) if cols is not None else not events:
                 self.add_reasoning_step(observation=f"No events found in namespace {namespace}",
                                         conclusion="No event data to analyze")
                 return self.get_results()
             self.add_reasoning_step(observation=f"Found {len(events)} events in namespace {namespace}",
                                     conclusion="Beginning events analysis")
-            by_obj = _group(events, _obj_key)
-            self.add_reasoning_step(observation=f"Grouped events into {len(by_obj)} unique objects",
-                                    conclusion="Will analyze events by object type and name")
-            self._object_warnings(by_obj)
-            self._scheduling(events)
-            self._volumes(events)
-            self._frequent(events)
-            self._control_plane(events)
-            self._nodes(events)
+            if cols is None:
+                cols = eventcols.encode_events(events)
+            if cols is not None:
+                for kind, kw in eventcols.analyze(self.engine, cols):
+                    (self.add_finding if kind == 'finding' else self.add_reasoning_step)(**kw)
+                return self.get_results()
+            self._host_analyze(events)
             return self.get_results()
         except Exception as e:
             return self._error_result("events", e)
+
+    def _host_analyze(self, events):
+        """The reference's loops (ref :105-446) for events the columnar encoding cannot hold."""
+        by_obj = _group(events, _obj_key)
+        self.add_reasoning_step(observation=f"Grouped events into {len(by_obj)} unique objects",
+                                conclusion="Will analyze events by object type and name")
+        self._object_warnings(by_obj)
+        self._scheduling(events)
+        self._volumes(events)
+        self._frequent(events)
+        self._control_plane(events)
+        self._nodes(events)
 
     def _object_warnings(self, by_obj):  # ref :136-167
         for key, evs in by_obj.items():

@@ -78,6 +78,8 @@ SIGNATURES = {
                                   c_vp, c_vp]),
     "krca_pod_groups": (c_i32, []),
     "krca_pod_classify": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "krca_group_max_rank": (c_i32, []),
+    "krca_group_reduce": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "krca_topk_workspace_size": (c_i64, [c_i64, c_i32]),
     "krca_topk_f32": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "krca_topk_i64": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
@@ -308,6 +310,28 @@ class NativeEngine:
                                         self._dev(cc.view(np.int16) if len(cc) else np.zeros(1, np.int16)))
         del t
         return m.cpu().numpy().view(np.uint16), h.cpu().numpy()
+
+    # -- f4: event / finding group-bys ------------------------------------------------------
+    def group_reduce_device(self, slot, key, S, R, n_ranked=None):
+        """int64 records [S, 8] (include/krca.h, f4) on the device."""
+        torch = self.torch
+        N = slot.numel()
+        if key.numel() != N:
+            raise KrcaError(f"group_reduce: slot has {N} records, key {key.numel()}")
+        rec = torch.empty((max(int(S), 1), 8), dtype=torch.int64, device=self.device)
+        _check(self.lib.krca_group_reduce(self.ptr(slot), self.ptr(key), N, N if n_ranked is None else n_ranked,
+                                          int(S), R, self.ptr(rec), self._stream()), "krca_group_reduce")
+        return rec[:S]
+
+    def group_reduce(self, slot, key, S, R=1, n_ranked=None):
+        """(first, count, n_key, top[R, S]) host arrays; see include/krca.h (f4)."""
+        slot = np.ascontiguousarray(slot, np.int32)
+        key = np.ascontiguousarray(key, np.int64)
+        if len(slot) == 0:  # zero-sized tensors have no storage to hand over; the kernel only inits
+            slot, key, n_ranked = np.full(1, -1, np.int32), np.full(1, -1, np.int64), 0
+        rec = self.group_reduce_device(self._dev(slot), self._dev(key), S, R, n_ranked).cpu().numpy()
+        return (rec[:, 0].astype(np.int32), (rec[:, 1] >> 32).astype(np.int32),
+                (rec[:, 1] & 0xFFFFFFFF).astype(np.int32), np.ascontiguousarray(rec[:, 2:2 + R].T))
 
     # -- top-k -------------------------------------------------------------------------------
     def topk_device(self, v, k):

@@ -16,6 +16,10 @@ Parity anchors:
   * service-graph construction: :func:`selector_match_ref` / :func:`substr_match_ref` are the
     pair tests of ref:agents/topology_agent.py:133,257 and ref:agents/resource_analyzer.py:851,
     pinned through the agents by tests/golden/topograph_cases.json (reference graphs);
+  * event / finding group-bys: :func:`group_reduce_ref` is the dict-insertion-order group-by
+    with Python ``max`` / stable ``sorted(reverse=True)`` of ref:agents/events_agent.py:105-446
+    and ref:agents/coordinator.py:118-155, pinned through EventsAgent / Coordinator by
+    tests/golden/events_cases.json and tests/golden/events_random.json (reference outputs);
   * rolling z-score / correlation / template hashing have no reference counterpart (new
     primitives named by the north star): their float64 restatements here are
     "parity unpinned" by the reference and define the semantics.
@@ -350,6 +354,36 @@ def substr_match_ref(text, val_off, pat, pat_off):
 # C restatement (bit-exact twin of the device arithmetic)
 # ------------------------------------------------------------------------------------------
 _c = None
+
+
+def group_reduce_ref(slot, key, S, R, n_ranked=None):
+    """Group-by of krca_group_reduce, written as the reference's dict loops
+    (ref:agents/events_agent.py:122-127 ``object_events.setdefault(key, []).append(event)``,
+    ``max(..., key=lastTimestamp)`` :193, ``sorted(..., reverse=True)[:3]`` :148;
+    ref:agents/coordinator.py:134-139,150): groups in first-seen order, then per group the
+    member count, the selected count (key >= 0) and the R largest selected keys.
+    Ranks r >= 1 only over records i < n_ranked.  Returns (first, count, n_key, top[R, S])."""
+    n_ranked = len(slot) if n_ranked is None else n_ranked
+    groups = {}
+    for i, (s, k) in enumerate(zip(np.asarray(slot).tolist(), np.asarray(key).tolist())):
+        if 0 <= s < S:
+            groups.setdefault(s, []).append((i, k))
+    first = np.full(S, 2**31 - 1, np.int32)
+    count = np.zeros(S, np.int32)
+    n_key = np.zeros(S, np.int32)
+    top = np.full((R, S), -1, np.int64)
+    for s, mem in groups.items():
+        first[s] = mem[0][0]
+        count[s] = len(mem)
+        sel = sorted((k for _, k in mem if k >= 0), reverse=True)
+        n_key[s] = len(sel)
+        uniq = sorted(set(sel), reverse=True)
+        if uniq:
+            top[0, s] = uniq[0]
+        ranked = sorted({k for i, k in mem if k >= 0 and i < n_ranked and k < uniq[0]}, reverse=True) if uniq else []
+        for r, k in enumerate(ranked[:R - 1]):
+            top[r + 1, s] = k
+    return first, count, n_key, top
 
 
 def c_lib():

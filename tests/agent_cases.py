@@ -223,13 +223,35 @@ def check_metrics_scaled(engine):
     return bad
 
 
-def check_events():
+def check_events(engine):
     gold = load("events_cases.json")
     bad = []
-    if not same(EventsAgent(DictClient(events=gold["events"])).analyze("x"), gold["result"]):
+    if not same(EventsAgent(DictClient(events=gold["events"]), engine=engine).analyze("x"), gold["result"]):
         bad.append("events")
-    if not same(EventsAgent(DictClient(events=[])).analyze("x"), gold["empty"]):
+    if not same(EventsAgent(DictClient(events=[]), engine=engine).analyze("x"), gold["empty"]):
         bad.append("empty")
+    return bad
+
+
+def check_events_random(engine):
+    """f4: reference EventsAgent outputs on random event lists with hazards (capture_events.py)."""
+    gold = load("events_random.json")
+    bad = []
+    for name, case in gold["events"].items():
+        if not same(EventsAgent(DictClient(events=case["events"]), engine=engine).analyze("x"), case["result"]):
+            bad.append(name)
+    return bad
+
+
+def check_correlate(engine):
+    """f4: reference _correlate_findings / _identify_root_causes on random finding lists."""
+    gold = load("events_random.json")
+    bad = []
+    co = Coordinator(DictClient(), engine=engine)
+    for name, case in gold["correlate"].items():
+        corr = co._correlate_findings(*case["lists"])
+        if corr != case["correlated"] or co._identify_root_causes(corr) != case["root_causes"]:
+            bad.append(name)
     return bad
 
 

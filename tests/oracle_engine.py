@@ -72,3 +72,6 @@ class OracleEngine:
 
     def substr_match(self, text, val_off, pat, pat_off):
         return oracle.substr_match_ref(text, val_off, pat, pat_off)
+
+    def group_reduce(self, slot, key, S, R=1, n_ranked=None):
+        return oracle.group_reduce_ref(slot, key, S, R, n_ranked)

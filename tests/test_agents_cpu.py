@@ -51,7 +51,50 @@ def test_metrics_scaled_boundaries():
 
 
 def test_events_cases():
-    assert A.check_events() == []
+    assert A.check_events(ENG) == []
+
+
+def test_events_random_reference_cases():
+    assert A.check_events_random(ENG) == []
+
+
+def test_correlate_random_reference_cases():
+    assert A.check_correlate(ENG) == []
+
+
+def test_correlate_bad_severity_raises_like_reference():
+    co = A.Coordinator(A.DictClient(), engine=ENG)
+    ok = {"component": "x", "severity": "high"}
+    assert co._correlate_findings([ok, {"component": "y", "severity": "bogus"}]) == []  # singleton: never checked
+    try:
+        co._correlate_findings([ok, {"component": "x", "severity": "bogus"}])
+        raise AssertionError("expected ValueError")
+    except ValueError as e:
+        assert str(e) == "'bogus' is not in list"
+
+
+def test_events_columns_match_host_loop():
+    """The columnar replay == the reference's loops (_host_analyze) on synthetic columns."""
+    from krca import eventcols
+    cols = eventcols.make_events(3000, seed=3, n_obj=200, n_hosts=8)
+    evs = []
+    for e in range(len(cols)):
+        ev = {"involvedObject": {"kind": cols.kinds[cols.kind[e]], "name": cols.names[cols.name[e]]},
+              "type": "Warning" if cols.warn[e] else "Normal", "message": cols.messages[cols.message[e]],
+              "count": int(cols.count[e]), "lastTimestamp": "%08d" % cols.ts[e],
+              "source": {"host": cols.hosts[cols.host[e]]}}
+        if cols.reason[e] >= 0:
+            ev["reason"] = cols.reasons[cols.reason[e]]
+        if cols.comp[e] >= 0:
+            ev["source"]["component"] = cols.comps[cols.comp[e]]
+        evs.append(ev)
+    a = A.EventsAgent(A.DictClient(events=evs), engine=ENG)
+    dev = a.analyze("x")
+    a.reset()
+    a._host_analyze(evs)
+    host = a.get_results()
+    assert A.strip(dev["findings"]) == A.strip(host["findings"])
+    assert len(dev["findings"]) > 50
 
 
 def test_comprehensive_roots_order():

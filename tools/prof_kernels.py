@@ -31,7 +31,7 @@ def timed(torch, fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods", "bc"])
+    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods", "bc", "events"])
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--docs", type=int, default=1_000_000)
@@ -94,6 +94,22 @@ def main():
         E = len(col)
         # per source: the forward BFS and the dependency pull each read every reached edge once
         out = dict(kernel="krca_betweenness", nodes=N, edges=E, s=s, teps=2 * N * E / s, bc_sum=float(bc.sum()))
+    elif a.what == "events":
+        from krca import eventcols
+        E = a.pods * 10  # default 10M events
+        t0 = time.time()
+        cols = eventcols.make_events(E, seed=0, n_hosts=1024)
+        slot, key, layout = eventcols.group_records(cols)
+        t_host = time.time() - t0
+        S = layout[-1][0] + layout[-1][1]
+        ds, dk = torch.from_numpy(slot).cuda(), torch.from_numpy(key).cuda()
+        eng.group_reduce_device(ds, dk, S, 3, n_ranked=E)
+        ms = timed(torch, lambda: eng.group_reduce_device(ds, dk, S, 3, n_ranked=E), a.reps)
+        # algorithmic: one read of the records (12 B), the object records again for ranks 2-3
+        # (2 x 12 B + an 8-B top gather), one 64-B slot record written
+        nbytes = 12 * len(slot) + 2 * 20 * E + 64 * S
+        out = dict(kernel="krca_group_reduce", events=E, records=len(slot), slots=S, ms=ms, bytes=nbytes,
+                   gbs=nbytes / (min(ms) * 1e-3) / 1e9, host_records_s=t_host)
     elif a.what == "pods":
         from krca import podstate
         P = a.pods * 10
