@@ -6,8 +6,11 @@
 //
 // Input: one UTF-8 blob holding D container logs back to back (doc_off[D+1] byte offsets).
 // Pipeline (HBM-bound; the blob is read twice, the 2nd time mostly from L2):
-//   log_count   lane = 256-byte chunk: count line starts (str.splitlines separators: \n \r \r\n
-//               \v \f \x1c \x1d \x1e U+0085 U+2028 U+2029; container starts).
+//   log_count   count line starts per 256-byte chunk (str.splitlines separators: \n \r \r\n
+//               \v \f \x1c \x1d \x1e U+0085 U+2028 U+2029; container starts): streaming, a lane
+//               tests 16 bytes of a coalesced dwordx4; container starts are a per-container
+//               correction added by log_chunk_doc.  Containers must be valid UTF-8 each (they
+//               are encoded from str), so no multi-byte separator straddles two containers.
 //   log_scan    one workgroup: exclusive scan of the per-tile totals -> tile_base, n_lines.
 //   log_match   lane = chunk again, persistent workgroups with the DFA in LDS: line ids from
 //               the tile scan, UTF-8 decode, DFA step per code point (csrc/log_dfa_tables.h,
@@ -109,55 +112,118 @@ struct DocWin {
   }
 };
 
+// byte k (0..3) of a little-endian word
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xFFu; }
+
+// str.splitlines line start at a byte p that is not its container's first byte, from the raw
+// bytes before it: every container is valid UTF-8 on its own (encoded from a str), so a multi-byte
+// separator never straddles two containers and no container starts with a continuation byte.
+__device__ __forceinline__ uint32_t sep_raw(uint32_t b3, uint32_t b2, uint32_t b1, uint32_t b0) {
+  return sep_before(b3, b2, b1, b0) ? 1u : 0u;
+}
+
 // chunk -> container holding its first byte: one thread per container writes the chunks that start
-// inside it (every chunk start lies in exactly one non-empty container), so no chunk searches
-__global__ __launch_bounds__(TPB) void log_chunk_doc(const int64_t* __restrict__ doc_off, int64_t D,
-                                                     int32_t* __restrict__ chunk_doc) {
+// inside it (every chunk start lies in exactly one non-empty container), so no chunk searches.
+// It also adds the container-start correction of log_count to the chunk holding its first byte:
+// a non-empty container's first byte is a line start whatever precedes it (+1), and log_count
+// counts the raw separator test there (-sep_raw).  chunk_cnt is zeroed before this kernel.
+__global__ __launch_bounds__(TPB) void log_chunk_doc(const uint8_t* __restrict__ text,
+                                                     const int64_t* __restrict__ doc_off, int64_t D,
+                                                     int32_t* __restrict__ chunk_doc, int32_t* __restrict__ chunk_cnt) {
   const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (d >= D) return;
   const int64_t s = doc_off[d], e = doc_off[d + 1];
   for (int64_t c = (s + CH - 1) / CH; c * CH < e; ++c) chunk_doc[c] = (int32_t)d;
+  if (s < e) {
+    const uint32_t b0 = text[s];
+    const uint32_t b1 = s >= 1 ? text[s - 1] : 0, b2 = s >= 2 ? text[s - 2] : 0, b3 = s >= 3 ? text[s - 3] : 0;
+    const int32_t corr = 1 - (int32_t)sep_raw(b3, b2, b1, b0);
+    if (corr) atomicAdd(chunk_cnt + s / CH, corr);
+  }
 }
 
-// ---- phase 1: line starts per chunk ---------------------------------------------------------
-__global__ __launch_bounds__(TPB) void log_count(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                 const int64_t* __restrict__ doc_off, int64_t D,
-                                                 const int32_t* __restrict__ chunk_doc,
-                                                 int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_tot) {
-  __shared__ int32_t red[TPB / 64];
-  const int64_t g = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  const int64_t c0 = g * CH;
-  int32_t cnt = 0;
-  if (c0 < nbytes) {
-    const int64_t c1 = min(c0 + CH, nbytes);
-    Bytes B;
-    B.init(text, nbytes);
-    DocWin dw;
-    dw.load(doc_off, D, chunk_doc[g]);
-    int64_t dstart = dw.b[0], dend = dw.b[1];
-    uint32_t b1 = c0 - 1 >= dstart ? B.at(c0 - 1) : 0;
-    uint32_t b2 = c0 - 2 >= dstart ? B.at(c0 - 2) : 0;
-    uint32_t b3 = c0 - 3 >= dstart ? B.at(c0 - 3) : 0;
-    for (int64_t p = c0; p < c1; ++p) {
-      if (p >= dend) {  // next container(s)
-        dw.advance(p);
-        dstart = dw.b[0];
-        dend = dw.b[1];
-        b1 = b2 = b3 = 0;
-      }
-      const uint32_t b0 = B.at(p);
-      cnt += (p == dstart) || sep_before(b3, b2, b1, b0);
-      b3 = b2;
-      b2 = b1;
-      b1 = b0;
-    }
+// ---- phase 1: line starts per chunk (streaming) -------------------------------------------
+// A workgroup takes one 64 KiB tile in 16 passes of 4 KiB; a lane reads 16 consecutive bytes
+// (one coalesced dwordx4 per lane: a wave reads 1 KiB contiguous), the 3 bytes before them come
+// from the previous lane by a shuffle (lane 0: one extra 4-byte load).  16 lanes = one 256-byte
+// chunk: count = container-start correction (already in chunk_cnt) + raw separator tests.
+constexpr int PIECE = 16;
+constexpr int LANES_PER_CHUNK = CH / PIECE;  // 16
+
+// SWAR byte tests on 4 bytes at once: the high bit of each byte of the result is the test
+__device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t c) {  // byte == c
+  const uint32_t v = x ^ (c * 0x01010101u);
+  return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t swar_range(uint32_t x, uint32_t lo, uint32_t hi) {  // lo <= byte <= hi < 0x80
+  const uint32_t y = x & 0x7F7F7F7Fu;
+  const uint32_t ge = y + (0x80u - lo) * 0x01010101u;
+  const uint32_t gt = y + (0x7Fu - hi) * 0x01010101u;
+  return ge & ~gt & ~x & 0x80808080u;
+}
+
+// line starts at the 4 byte positions of word w (sep_before of each, raw bytes), given the word
+// before it; high bit per byte
+__device__ __forceinline__ uint32_t sep_flags(uint32_t wprev, uint32_t w) {
+  const uint32_t B1 = __builtin_amdgcn_alignbit(w, wprev, 24);  // text[p-1] at byte k
+  uint32_t f = (swar_range(B1, 0x0A, 0x0D) | swar_range(B1, 0x1C, 0x1E)) & ~(swar_eq(B1, 0x0D) & swar_eq(w, 0x0A));
+  if ((w | wprev) & 0x80808080u) {  // U+0085 (C2 85), U+2028 / U+2029 (E2 80 A8/A9)
+    const uint32_t B2 = __builtin_amdgcn_alignbit(w, wprev, 16);
+    const uint32_t B3 = __builtin_amdgcn_alignbit(w, wprev, 8);
+    f |= swar_eq(B2, 0xC2) & swar_eq(B1, 0x85);
+    f |= swar_eq(B3, 0xE2) & swar_eq(B2, 0x80) & (swar_eq(B1, 0xA8) | swar_eq(B1, 0xA9));
   }
-  chunk_cnt[g] = cnt;
-  int32_t s = cnt;
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  return f;
+}
+
+__global__ __launch_bounds__(TPB) void log_count(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                 int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_tot) {
+  constexpr int NIT = TILE / (TPB * PIECE);  // 16 passes of 4 KiB
+  __shared__ int32_t s_cnt[TPB];             // the tile's 256 chunk counts
+  __shared__ int64_t red[TPB / 64];
+  const int lane = threadIdx.x & 63;
+  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  s_cnt[threadIdx.x] = chunk_cnt[(int64_t)blockIdx.x * TPB + threadIdx.x];  // container-start corrections
   __syncthreads();
-  if (threadIdx.x == 0) tile_tot[blockIdx.x] = (int64_t)red[0] + red[1] + red[2] + red[3];
+#pragma unroll 4
+  for (int it = 0; it < NIT; ++it) {
+    const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (q + PIECE <= nbytes) {
+      const uint4 v = *reinterpret_cast<const uint4*>(text + q);
+      w[0] = v.x;
+      w[1] = v.y;
+      w[2] = v.z;
+      w[3] = v.w;
+    } else if (q < nbytes) {
+      for (int k = 0; k < PIECE; ++k)
+        if (q + k < nbytes) w[k >> 2] |= (uint32_t)text[q + k] << (8 * (k & 3));
+    }
+    uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
+    if (lane == 0) wp = q >= 4 && q <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q - 4) : 0u;
+    uint32_t f0 = sep_flags(wp, w[0]), f1 = sep_flags(w[0], w[1]), f2 = sep_flags(w[1], w[2]),
+             f3 = sep_flags(w[2], w[3]);
+    if (q + PIECE > nbytes) {  // positions past the text are no line starts
+      const int64_t n = nbytes - q;  // < 16
+      f0 &= n >= 4 ? ~0u : (n <= 0 ? 0u : (0x80808080u >> (8 * (4 - n))));
+      f1 &= n >= 8 ? ~0u : (n <= 4 ? 0u : (0x80808080u >> (8 * (8 - n))));
+      f2 &= n >= 12 ? ~0u : (n <= 8 ? 0u : (0x80808080u >> (8 * (12 - n))));
+      f3 &= n <= 12 ? 0u : (0x80808080u >> (8 * (16 - n)));
+    }
+    uint32_t c = __popc(f0) + __popc(f1) + __popc(f2) + __popc(f3);
+#pragma unroll
+    for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
+    if ((threadIdx.x & (LANES_PER_CHUNK - 1)) == 0)
+      s_cnt[it * (TPB / LANES_PER_CHUNK) + threadIdx.x / LANES_PER_CHUNK] += (int32_t)c;
+  }
+  __syncthreads();
+  const int32_t mine = s_cnt[threadIdx.x];
+  chunk_cnt[(int64_t)blockIdx.x * TPB + threadIdx.x] = mine;
+  int64_t tot = mine;
+  for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+  if (lane == 0) red[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_tot[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // ---- phase 2: exclusive scan of tile totals (one workgroup) --------------------------------
@@ -551,10 +617,11 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   int32_t* chunk = reinterpret_cast<int32_t*>(ws + nt + 1);
   int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
   hipStream_t st = krca::as_stream(stream);
-  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs, cdoc);
+  KRCA_HIP(hipMemsetAsync(chunk, 0, nt * TPB * sizeof(int32_t), st));
+  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, text, doc_off, ndocs,
+                     cdoc, chunk);
   KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
-                     (const int32_t*)cdoc, chunk, tile);
+  hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, chunk, tile);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(log_scan, dim3(1), dim3(1024), 0, st, tile, nt, n_lines);
   KRCA_LAUNCH_CHECK();

@@ -142,9 +142,12 @@ def test_log_scan_boundaries(eng):
     for L in (250, 255, 256, 257, 511, 512, 65535, 65536, 65537):
         docs.append("x" * (L - 8) + "timeout\r" + "\nERROR")
     pieces = ["Error", "\r", "\n", "\r\n", "é", "KILLED", "\u0085", "ſecret not found", "a" * 37, "panic:",
-              "Back-off restarting", "\x1c", "\x0b", " "]
+              "Back-off restarting", "\x1c", "\x0b", " ", "\u2028", "\u2029", "\x1d", "\x1e", "\x0c", "\u00e2\u0080"]
     for _ in range(200):
         docs.append("".join(pieces[i] for i in rng.integers(0, len(pieces), rng.integers(0, 60))))
+    # containers ending in a separator followed by containers starting with one (the line-start
+    # test at a container's first byte must not see the previous container's bytes)
+    docs += ["a\r", "\nb", "x\u2028", "\u2029y", "\r", "\n", "q\x85", "\x85", "", "\u2028", "z\r", "\r\n"]
     _check_docs(eng, docs)
 
 
