@@ -69,14 +69,15 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
  * Two phases (the line count is data-dependent):
  *   krca_log_index: per-chunk line-start counts + scan into block_base (workspace of
  *                   krca_log_index_size(nbytes) int64) and *n_lines (device int64).
- *   krca_log_match: per line start/end byte offsets and 13-bit mask; per container the line
+ *   krca_log_match: (same workspace; it also keeps the first line id of every 256-byte chunk
+ *                   there) per line start/end byte offsets and 13-bit mask; per container the line
  *                   count, the 13-bin histogram and the first three matching line ids per bin
  *                   (-1 when fewer) — atomics-free segmented reduction. */
 int64_t krca_log_index_size(int64_t nbytes);
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
                    int64_t* workspace, int64_t* n_lines, void* stream);
 int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
-                   const int64_t* workspace, int64_t n_lines,
+                   int64_t* workspace, int64_t n_lines,
                    int64_t* line_start /*[L]*/, int64_t* line_end /*[L]*/, uint32_t* line_mask /*[L]*/,
                    int32_t* doc_lines /*[D]*/, int32_t* hist /*[D][13]*/, int32_t* examples /*[D][13][3]*/,
                    int64_t* doc_line0 /*[D], nullable: first line id of each container*/, void* stream);

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ tex
                                                  const int32_t* __restrict__ chunk_cnt,
                                                  const int64_t* __restrict__ tile_base, int64_t ntiles, int64_t L,
                                                  int64_t* __restrict__ line_start, int64_t* __restrict__ line_end,
-                                                 uint32_t* __restrict__ line_mask) {
+                                                 uint32_t* __restrict__ line_mask, int64_t* __restrict__ chunk_line0) {
   __shared__ DfaLds dfa;
   __shared__ int64_t s_scan[TPB];
   __shared__ int64_t s_first_id[TPB];
@@ -331,6 +331,7 @@ __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ tex
     int64_t base = tile_base[tile];
     for (int w = 0; w < wid; ++w) base += s_scan[w];
     base += x - v;
+    chunk_line0[g] = base;  // first line id of the chunk (narrows log_hist's search)
 
     const int64_t c0 = g * CH;
     int64_t first_id = -1;
@@ -508,17 +509,38 @@ __device__ __forceinline__ int64_t lower_bound_i64(const int64_t* __restrict__ a
 // one pass of short lane loops instead of a wave (and two dependent searches) each.
 constexpr int HIST_SMALL = 32;
 
+// first line starting at or after byte s: only the lines of s's 256-byte chunk can be below it
+__device__ __forceinline__ int64_t first_line_at(const int64_t* __restrict__ line_start, int64_t L,
+                                                 const int64_t* __restrict__ chunk_line0, int64_t nchunks,
+                                                 int64_t s) {
+  const int64_t c = s / CH;
+  if (L == 0 || c >= nchunks) return L;
+  int64_t lo = chunk_line0[c], hi = c + 1 < nchunks ? chunk_line0[c + 1] : L;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (line_start[mid] < s) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_off, int64_t D,
+                                                const int64_t* __restrict__ chunk_line0, int64_t nchunks,
                                                 const int64_t* __restrict__ line_start,
                                                 const uint32_t* __restrict__ line_mask, int64_t L,
                                                 int32_t* __restrict__ doc_lines, int32_t* __restrict__ hist,
                                                 int32_t* __restrict__ examples, int64_t* __restrict__ doc_line0) {
-  const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  // the block's histograms and examples are assembled in LDS and leave in coalesced rows (a lane
+  // writing its own 52 ints at a 208-byte stride touched ~26 lines per store instruction)
+  __shared__ int32_t s_hist[TPB * KRCA_NCAT];
+  __shared__ int32_t s_ex[TPB * KRCA_NCAT * 3];
+  const int64_t d0 = (int64_t)blockIdx.x * TPB;
+  const int64_t d = d0 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const bool valid = d < D;
-  const int64_t lo = valid ? lower_bound_i64(line_start, L, doc_off[d]) : L;
+  const int64_t lo = valid ? first_line_at(line_start, L, chunk_line0, nchunks, doc_off[d]) : L;
   int64_t hi = __shfl_down(lo, 1, 64);
-  if (valid && (lane == 63 || d + 1 == D)) hi = lower_bound_i64(line_start, L, doc_off[d + 1]);
+  if (valid && (lane == 63 || d + 1 == D)) hi = first_line_at(line_start, L, chunk_line0, nchunks, doc_off[d + 1]);
   const bool small = valid && hi - lo <= HIST_SMALL;
   if (small) {
     int32_t cnt[KRCA_NCAT], ex[KRCA_NCAT][3];
@@ -542,8 +564,8 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
     }
     doc_lines[d] = (int32_t)(hi - lo);
     if (doc_line0) doc_line0[d] = lo;
-    int32_t* hd = hist + d * KRCA_NCAT;
-    int32_t* ed = examples + d * KRCA_NCAT * 3;
+    int32_t* hd = s_hist + threadIdx.x * KRCA_NCAT;
+    int32_t* ed = s_ex + threadIdx.x * KRCA_NCAT * 3;
 #pragma unroll
     for (int c = 0; c < KRCA_NCAT; ++c) {
       hd[c] = cnt[c];
@@ -565,7 +587,7 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
       cnt[c] = 0;
       found[c] = 0;
     }
-    int32_t* ex = examples + dj * KRCA_NCAT * 3;
+    int32_t* ex = s_ex + (threadIdx.x - lane + j) * KRCA_NCAT * 3;
     for (int64_t b = blo; b < bhi; b += 64) {
       const uint32_t m = (b + lane < bhi) ? line_mask[b + lane] : 0u;
 #pragma unroll
@@ -585,11 +607,15 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
       if (doc_line0) doc_line0[dj] = blo;
 #pragma unroll
       for (int c = 0; c < KRCA_NCAT; ++c) {
-        hist[dj * KRCA_NCAT + c] = cnt[c];
+        s_hist[(threadIdx.x - lane + j) * KRCA_NCAT + c] = cnt[c];
         for (int k = found[c]; k < 3; ++k) ex[c * 3 + k] = -1;
       }
     }
   }
+  __syncthreads();
+  const int nv = (int)(D - d0 < TPB ? D - d0 : TPB);
+  for (int i = threadIdx.x; i < nv * KRCA_NCAT; i += TPB) hist[d0 * KRCA_NCAT + i] = s_hist[i];
+  for (int i = threadIdx.x; i < nv * KRCA_NCAT * 3; i += TPB) examples[d0 * KRCA_NCAT * 3 + i] = s_ex[i];
 }
 
 int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, TILE)); }
@@ -599,10 +625,10 @@ int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(n
 extern "C" {
 
 // workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts |
-// [ntiles*TPB] int32 chunk -> container
+// [ntiles*TPB] int32 chunk -> container | [ntiles*TPB] int64 first line id per chunk
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
-  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2;
+  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB;
 }
 
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
@@ -628,7 +654,7 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   return KRCA_OK;
 }
 
-int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, const int64_t* ws,
+int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
                    int64_t n_lines, int64_t* line_start, int64_t* line_end, uint32_t* line_mask, int32_t* doc_lines,
                    int32_t* hist, int32_t* examples, int64_t* doc_line0, void* stream) {
   KRCA_CHECK_ARG(nbytes >= 0 && ndocs >= 1 && n_lines >= 0, "krca_log_match: bad sizes");
@@ -639,16 +665,18 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   const int64_t* tile = ws;
   const int32_t* chunk = reinterpret_cast<const int32_t*>(ws + nt + 1);
   const int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
+  int64_t* chunk_line0 = ws + (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2;
   hipStream_t st = krca::as_stream(stream);
   if (n_lines > 0) {
     KRCA_HIP(hipMemsetAsync(line_mask, 0, n_lines * sizeof(uint32_t), st));
     const int64_t grid = std::min<int64_t>(nt, 256 * 4);
     hipLaunchKernelGGL(log_match, dim3((unsigned)grid), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, cdoc, chunk,
-                       tile, nt, n_lines, line_start, line_end, line_mask);
+                       tile, nt, n_lines, line_start, line_end, line_mask, chunk_line0);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
-                     line_start, line_mask, n_lines, doc_lines, hist, examples, doc_line0);
+                     (const int64_t*)chunk_line0, nt * TPB, line_start, line_mask, n_lines, doc_lines, hist, examples,
+                     doc_line0);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
