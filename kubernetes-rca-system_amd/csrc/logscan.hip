@@ -47,23 +47,16 @@ struct Bytes {
     n = nbytes;
     base = -1;
   }
+  // b is 16-byte aligned and (callers read only p < n) holds at least one byte of the text: the
+  // aligned 16-byte block lies inside the text's last page, so the full load never faults; bytes
+  // past n are never returned by at()
   __device__ __forceinline__ void fill(int64_t b) {
     base = b;
-    if (b + 16 <= n) {
-      const uint4 v = *reinterpret_cast<const uint4*>(t + b);
-      w0 = v.x;
-      w1 = v.y;
-      w2 = v.z;
-      w3 = v.w;
-    } else {
-      uint32_t ww[4] = {0, 0, 0, 0};
-      for (int k = 0; k < 16; ++k)
-        if (b + k < n) ww[k >> 2] |= (uint32_t)t[b + k] << (8 * (k & 3));
-      w0 = ww[0];
-      w1 = ww[1];
-      w2 = ww[2];
-      w3 = ww[3];
-    }
+    const uint4 v = *reinterpret_cast<const uint4*>(t + b);
+    w0 = v.x;
+    w1 = v.y;
+    w2 = v.z;
+    w3 = v.w;
   }
   __device__ __forceinline__ uint32_t at(int64_t p) {
     const int64_t b = p & ~(int64_t)15;
