@@ -61,9 +61,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # KRCA_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
+    # the real multi-GPU run is one rank per GPU over RCCL ("nccl")
+    backend = os.environ.get("KRCA_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     eng = native.NativeEngine(local)
     cfg = Config(window=args.window, seed_floor=args.seed_floor, alpha=args.alpha, iters=args.iters)
 
@@ -73,10 +81,8 @@ def main():
     hops = synth.caller_hops(mesh, mesh.roots)
     lo, hi, n_max = shard_range(args.pods, world, rank)
     rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, lo, hi)
-    in_range = lambda a: np.asarray([v - lo for v in a if lo <= v < hi], np.int64)  # noqa: E731
-    x = synth.make_metrics(hi - lo, args.metrics, args.tsteps, window=args.window, seed=args.seed * 1000 + rank,
-                           roots=in_range(mesh.roots), hop_sets=[in_range(h) for h in hops],
-                           device=torch.device("cuda", local))
+    x = synth.make_metrics_range(lo, hi, args.metrics, args.tsteps, window=args.window, seed=args.seed,
+                                 roots=mesh.roots, hop_sets=hops, device=torch.device("cuda", local))
     shard = DeviceShard(eng, x, rp, col, od, args.pods, n_max, world, cfg)
     step = RcaStep(shard, Comm(world, rank), cfg, lo)
     torch.cuda.synchronize()

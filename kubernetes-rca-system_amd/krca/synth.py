@@ -157,6 +157,26 @@ def make_metrics(n_pods, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(),
     return x
 
 
+def make_metrics_range(lo, hi, n_metrics=8, n_steps=1440, window=60, seed=0, roots=(), hop_sets=(), device="cpu",
+                       block=62_500, **kw):
+    """Pods [lo, hi) of a mesh-wide metric tensor, independent of how the pods are sharded: the
+    mesh is generated in fixed blocks of `block` pods (block b seeded seed * 1000 + b), so a rank
+    owning [lo, hi) holds exactly the rows a single GPU would hold for those pods."""
+    import torch
+    x = torch.empty((n_steps, hi - lo, n_metrics), dtype=torch.float32, device=device)
+    roots = np.asarray(roots, np.int64)
+    hop_sets = [np.asarray(h, np.int64) for h in hop_sets]
+    for b in range(lo // block, (hi + block - 1) // block):
+        b0, b1 = b * block, (b + 1) * block
+        sel = lambda a: a[(a >= b0) & (a < b1)] - b0  # noqa: E731
+        xb = make_metrics(block, n_metrics, n_steps, window=window, seed=seed * 1000 + b, roots=sel(roots),
+                          hop_sets=[sel(h) for h in hop_sets], device=device, **kw)
+        s0, s1 = max(lo, b0), min(hi, b1)
+        x[:, s0 - lo:s1 - lo] = xb[:, s0 - b0:s1 - b0]
+        del xb
+    return x
+
+
 # ------------------------------------------------------------------------------------------
 # log corpora (C5 shape): ASCII templates per category plus benign ones, 60-200 B lines
 # ------------------------------------------------------------------------------------------

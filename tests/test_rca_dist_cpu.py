@@ -73,3 +73,15 @@ def test_sharded_rca_matches_single_process_oracle(world):
     assert np.array_equal(r_sharded, r)
     for _, _, _, idx, _ in res:  # every rank holds the same merged top-10
         assert idx == [int(i) for i in ridx]
+
+
+def test_bench_metrics_do_not_depend_on_sharding():
+    """bench.py's mesh is generated in fixed pod blocks: any shard holds the rows one GPU holds."""
+    import torch
+    from krca import synth
+    roots, hops = np.array([5, 120, 250]), [np.array([7, 130]), np.array([260])]
+    kw = dict(window=20, seed=3, roots=roots, hop_sets=hops, block=100)
+    full = synth.make_metrics_range(0, 300, 8, 100, **kw)
+    for cuts in ([0, 150, 300], [0, 100, 200, 300], [0, 77, 154, 231, 300]):
+        parts = [synth.make_metrics_range(a, b, 8, 100, **kw) for a, b in zip(cuts, cuts[1:])]
+        assert torch.equal(full, torch.cat(parts, 1))
