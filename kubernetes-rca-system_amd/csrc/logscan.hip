@@ -24,6 +24,7 @@
 //               end), a private loop over <= 32 line masks, or the whole wave (13 ballots per 64
 //               lines) for a larger container — counts and first three line ids per bin, no atomics.
 #include <stdint.h>
+#include <cstdlib>
 
 #include "krca_common.h"
 #define KRCA_DFA_QUAL static __device__ __constant__ const
@@ -269,7 +270,8 @@ __device__ __forceinline__ uint32_t cp_symbol(const DfaLds& dfa, uint32_t cp) {
 }
 
 // decode the code point starting at p (valid UTF-8 or surrogatepass); returns its byte length
-__device__ __forceinline__ int decode(Bytes& B, int64_t p, uint32_t& cp) {
+template <class SRC>
+__device__ __forceinline__ int decode(SRC& B, int64_t p, uint32_t& cp) {
   const uint32_t b = B.at(p);
   if (b < 0x80) {
     cp = b;
@@ -484,6 +486,212 @@ __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ tex
   }
 }
 
+// ---- phase 3 (default, KRCA_LOG_IMPL != 1): line index, then a DFA lane per line ---------------
+// log_lines  re-streams the text like log_count (coalesced 16-byte pieces, SWAR separator tests)
+//            plus the container starts of each piece, numbers every line start from the chunk
+//            bases and writes line_start[id] and line_end[id-1] (the previous line ends at the
+//            separator that precedes the start, or at its container's end).
+// log_dfa    one lane per line: the line holds no separator and lies inside one container, so the
+//            per-byte loop is just UTF-8 decode + DFA step + mask OR; lines longer than LONG_LINE
+//            are queued for
+// log_dfa_long  one wave per long line: 64 segments, each warmed up over the <= 23 code points
+//            before it (as log_match's chunks), OR-reduced across the wave.
+constexpr int LONG_LINE = 1024;
+
+// bytes of the separator that ends right before p (0: none), from the raw bytes before p; p1_cs:
+// p-1 is a container's first byte (then a "\r" before it belongs to the previous container)
+__device__ __forceinline__ int sep_len(uint32_t b3, uint32_t b2, uint32_t b1, bool p1_cs) {
+  if (b1 == 0x0A) return (b2 == 0x0D && !p1_cs) ? 2 : 1;
+  if (b1 == 0x0B || b1 == 0x0C || b1 == 0x0D || b1 == 0x1C || b1 == 0x1D || b1 == 0x1E) return 1;
+  if (b2 == 0xC2 && b1 == 0x85) return 2;
+  if (b3 == 0xE2 && b2 == 0x80 && (b1 == 0xA8 || b1 == 0xA9)) return 3;
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t high_bits4(uint32_t f) {  // byte high bits -> 4-bit mask
+  return ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+}
+
+__global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                 const int64_t* __restrict__ doc_off, int64_t D,
+                                                 const int32_t* __restrict__ chunk_doc,
+                                                 const int32_t* __restrict__ chunk_cnt,
+                                                 const int64_t* __restrict__ tile_base, int64_t L,
+                                                 int64_t* __restrict__ line_start, int64_t* __restrict__ line_end,
+                                                 int64_t* __restrict__ chunk_line0) {
+  constexpr int NIT = TILE / (TPB * PIECE);
+  __shared__ int64_t s_base[TPB];
+  __shared__ int64_t s_wsum[TPB / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t tile = blockIdx.x;
+  const int64_t tile0 = tile * TILE;
+  {  // first line id of each of the tile's 256 chunks
+    const int64_t v = chunk_cnt[tile * TPB + threadIdx.x];
+    int64_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = (int64_t)__shfl_up((long long)x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wsum[wid] = x;
+    __syncthreads();
+    int64_t base = tile_base[tile] + x - v;
+    for (int w = 0; w < wid; ++w) base += s_wsum[w];
+    s_base[threadIdx.x] = base;
+    chunk_line0[tile * TPB + threadIdx.x] = base;
+    __syncthreads();
+  }
+  for (int it = 0; it < NIT; ++it) {
+    const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (q < nbytes) {  // an aligned 16-byte block holding a text byte never crosses the last page
+      const uint4 v = *reinterpret_cast<const uint4*>(text + q);
+      w[0] = v.x;
+      w[1] = v.y;
+      w[2] = v.z;
+      w[3] = v.w;
+    }
+    uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
+    if (lane == 0) wp = q >= 4 && q <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q - 4) : 0u;
+    uint32_t S = high_bits4(sep_flags(wp, w[0])) | (high_bits4(sep_flags(w[0], w[1])) << 4) |
+                 (high_bits4(sep_flags(w[1], w[2])) << 8) | (high_bits4(sep_flags(w[2], w[3])) << 12);
+    uint32_t C = 0;  // container first bytes at q-1+j, j = 0..16 (non-empty containers only)
+    if (q < nbytes) {
+      const int64_t qm = q > 0 ? q - 1 : 0;
+      for (int64_t k = chunk_doc[qm / CH]; k < D; ++k) {
+        const int64_t st = doc_off[k];
+        if (st >= q + PIECE) break;
+        if (st >= q - 1 && doc_off[k + 1] > st) C |= 1u << (int)(st - (q - 1));
+      }
+      S |= C >> 1;
+      if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
+    } else {
+      S = 0;
+    }
+    // line ids: the chunk's base + the starts of the lanes before this one in the chunk (16 lanes)
+    const uint32_t n = __popc(S);
+    uint32_t x = n;
+#pragma unroll
+    for (int off = 1; off < LANES_PER_CHUNK; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if ((lane & (LANES_PER_CHUNK - 1)) >= off) x += y;
+    }
+    int64_t id = s_base[it * (TPB / LANES_PER_CHUNK) + threadIdx.x / LANES_PER_CHUNK] + (x - n);
+    uint32_t rem = S;
+    while (rem) {
+      const int k = __ffs(rem) - 1;
+      rem &= rem - 1;
+      const int64_t pos = q + k;
+      // bytes pos-1, pos-2, pos-3 from the piece (or the 4 bytes before it)
+      const uint64_t lo64 = ((uint64_t)w[0] << 32) | wp;  // bytes q-4 .. q+3
+      uint32_t b1, b2, b3;
+      if (k < 4) {
+        b1 = (uint32_t)(lo64 >> (8 * (k + 3))) & 0xFFu;
+        b2 = (uint32_t)(lo64 >> (8 * (k + 2))) & 0xFFu;
+        b3 = (uint32_t)(lo64 >> (8 * (k + 1))) & 0xFFu;
+      } else {
+        const uint32_t ww[4] = {w[0], w[1], w[2], w[3]};
+        auto at = [&](int j) { return (ww[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+        b1 = at(k - 1);
+        b2 = at(k - 2);
+        b3 = k >= 3 ? at(k - 3) : 0u;
+      }
+      if (id < L) line_start[id] = pos;
+      if (id >= 1 && id - 1 < L) line_end[id - 1] = pos - sep_len(b3, b2, b1, (C >> k) & 1u);
+      ++id;
+    }
+  }
+}
+
+// the end of the last line: the text's end, minus a trailing separator
+__global__ void log_last_end(const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off,
+                             int64_t D, int64_t L, int64_t* __restrict__ line_end) {
+  if (L == 0 || nbytes == 0) return;
+  int64_t k = D - 1;
+  while (k > 0 && doc_off[k] >= nbytes) --k;  // the last non-empty container
+  const uint32_t b1 = text[nbytes - 1], b2 = nbytes >= 2 ? text[nbytes - 2] : 0u, b3 = nbytes >= 3 ? text[nbytes - 3] : 0u;
+  line_end[L - 1] = nbytes - sep_len(b3, b2, b1, doc_off[k] == nbytes - 1);
+}
+
+__device__ __forceinline__ void dfa_load(DfaLds& dfa) {
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * KRCA_DFA_NSYM; i += blockDim.x) dfa.trans[i] = krca_dfa_trans[i];
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE; i += blockDim.x) dfa.out[i] = krca_dfa_out[i];
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) dfa.ascii[i] = krca_dfa_ascii_sym[i];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(TPB) void log_dfa(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
+                                               const int64_t* __restrict__ line_start,
+                                               const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
+                                               int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
+  __shared__ DfaLds dfa;
+  dfa_load(dfa);
+  Bytes B;
+  B.init(text, nbytes);
+  for (int64_t l = (int64_t)blockIdx.x * TPB + threadIdx.x; l < L; l += (int64_t)gridDim.x * TPB) {
+    const int64_t s = line_start[l], e = line_end[l];
+    if (e - s > LONG_LINE) {
+      long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // a wave per long line (log_dfa_long)
+      continue;
+    }
+    uint32_t st = 0, mask = 0;
+    for (int64_t p = s; p < e;) {
+      uint32_t cp = B.at(p);
+      int len = 1;
+      if (cp >= 0x80) len = decode(B, p, cp);
+      const uint32_t sym = cp < 128 ? (uint32_t)dfa.ascii[cp] : cp_symbol(dfa, cp);
+      st = dfa.trans[st * KRCA_DFA_NSYM + sym];
+      mask |= dfa.out[st];
+      p += len;
+    }
+    line_mask[l] = mask;
+  }
+}
+
+__global__ __launch_bounds__(TPB) void log_dfa_long(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                    const int64_t* __restrict__ line_start,
+                                                    const int64_t* __restrict__ line_end,
+                                                    uint32_t* __restrict__ line_mask, const int32_t* __restrict__ long_q,
+                                                    const int32_t* __restrict__ n_long) {
+  __shared__ DfaLds dfa;
+  dfa_load(dfa);
+  const int lane = threadIdx.x & 63;
+  const int nq = *n_long;
+  Bytes B;
+  B.init(text, nbytes);
+  for (int j = (int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)); j < nq; j += (int)(gridDim.x * (TPB / 64))) {
+    const int64_t l = long_q[j];
+    const int64_t s = line_start[l], e = line_end[l];
+    const int64_t seg = (e - s + 63) / 64;
+    const int64_t a = min(e, s + lane * seg), b = min(e, a + seg);
+    uint32_t st = 0, mask = 0;
+    const int64_t p0 = a > s ? cp_align(B, a, e) : s;  // first code point starting in [a, b)
+    if (p0 > s && p0 < b) {  // warm-up over the <= WARM code points of the line before p0
+      int64_t k = p0;
+      int seen = 0;
+      while (k > s && seen < WARM) {
+        const uint32_t c = B.at(k - 1);
+        --k;
+        if ((c & 0xC0) != 0x80) ++seen;
+      }
+      while (k < p0) {
+        uint32_t cp;
+        const int len = decode(B, k, cp);
+        st = dfa.trans[st * KRCA_DFA_NSYM + cp_symbol(dfa, cp)];
+        k += len;
+      }
+    }
+    for (int64_t p = p0; p < b;) {
+      uint32_t cp;
+      const int len = decode(B, p, cp);
+      st = dfa.trans[st * KRCA_DFA_NSYM + cp_symbol(dfa, cp)];
+      mask |= dfa.out[st];
+      p += len;
+    }
+    for (int off = 32; off > 0; off >>= 1) mask |= __shfl_xor(mask, off, 64);
+    if (lane == 0) line_mask[l] = mask;
+  }
+}
+
 // ---- phase 4: per-container histogram + first three examples (wave per container) ----------
 __device__ __forceinline__ int64_t lower_bound_i64(const int64_t* __restrict__ a, int64_t n, int64_t key) {
   int64_t lo = 0, hi = n;
@@ -618,10 +826,11 @@ int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(n
 extern "C" {
 
 // workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts |
-// [ntiles*TPB] int32 chunk -> container | [ntiles*TPB] int64 first line id per chunk
+// [ntiles*TPB] int32 chunk -> container | [ntiles*TPB] int64 first line id per chunk |
+// [1] long-line count | int32 long-line queue [nbytes / LONG_LINE + 1]
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
-  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB;
+  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2);
 }
 
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
@@ -659,13 +868,33 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   const int32_t* chunk = reinterpret_cast<const int32_t*>(ws + nt + 1);
   const int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
   int64_t* chunk_line0 = ws + (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2;
+  int32_t* n_long = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB);
+  int32_t* long_q = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB + 1);
   hipStream_t st = krca::as_stream(stream);
-  if (n_lines > 0) {
+  const char* impl_env = getenv("KRCA_LOG_IMPL");  // read per call: tests A/B both paths in one process
+  const int impl = impl_env ? atoi(impl_env) : 0;
+  if (n_lines > 0 && impl == 1) {  // A/B: lane per 256-byte chunk, DFA and line logic in one pass
     KRCA_HIP(hipMemsetAsync(line_mask, 0, n_lines * sizeof(uint32_t), st));
     const int64_t grid = std::min<int64_t>(nt, 256 * 4);
     hipLaunchKernelGGL(log_match, dim3((unsigned)grid), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, cdoc, chunk,
                        tile, nt, n_lines, line_start, line_end, line_mask, chunk_line0);
     KRCA_LAUNCH_CHECK();
+  } else if (n_lines > 0) {  // line index, then a DFA lane per line (long lines: a wave each)
+    KRCA_HIP(hipMemsetAsync(n_long, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(log_lines, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, cdoc, chunk, tile,
+                       n_lines, line_start, line_end, chunk_line0);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, n_lines, line_end);
+    KRCA_LAUNCH_CHECK();
+    const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, TPB), 256 * 4);
+    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(TPB), 0, st, text, nbytes, n_lines,
+                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,
+                       (const int64_t*)line_end, line_mask, (const int32_t*)long_q, (const int32_t*)n_long);
+    KRCA_LAUNCH_CHECK();
+  } else {  // no lines: chunk_line0 = 0 for log_hist
+    KRCA_HIP(hipMemsetAsync(chunk_line0, 0, nt * TPB * sizeof(int64_t), st));
   }
   hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
                      (const int64_t*)chunk_line0, nt * TPB, line_start, line_mask, n_lines, doc_lines, hist, examples,

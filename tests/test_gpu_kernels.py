@@ -151,6 +151,29 @@ def test_log_scan_boundaries(eng):
     _check_docs(eng, docs)
 
 
+def test_log_scan_impls_identical(eng, monkeypatch):
+    """The line-index + DFA-lane path (default) and the chunk-lane path (KRCA_LOG_IMPL=1) give the
+    same line offsets, masks, histograms and examples, long lines (> 1 KiB, a wave each) included."""
+    rng = np.random.default_rng(11)
+    docs = synth.make_log_corpus(3000, lines_per_doc=4, seed=5, hazard_rate=0.02)
+    docs += ["x" * 5000 + " Killed " + "y" * 3000 + "\n" + "z" * 1025 + "timeout", "é" * 2000 + "panic:",
+             "a\r", "\nb", "ſ" * 700 + "Error" + "\u2028" + "k" * 1100, ""]
+    docs += ["".join(rng.choice(["Error ", "\r\n", "é", "\x85", "OOMKilled", "w" * 300]) for _ in range(40))
+             for _ in range(50)]
+    blob, off = pack_documents(docs)
+    tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
+    out = {}
+    for impl in ("0", "1"):
+        monkeypatch.setenv("KRCA_LOG_IMPL", impl)
+        r = eng.log_scan_device(tb, toff)
+        out[impl] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
+    assert out["0"].keys() == out["1"].keys()
+    for k in out["0"]:
+        assert np.array_equal(out["0"][k], out["1"][k]), k
+    monkeypatch.setenv("KRCA_LOG_IMPL", "0")
+    _check_docs(eng, docs)
+
+
 def test_log_scan_synthetic_large(eng):
     docs = synth.make_log_corpus(20000, lines_per_doc=6, seed=3, hazard_rate=0.01)
     _check_docs(eng, docs)
