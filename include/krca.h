@@ -90,13 +90,21 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
  *   their counts, written to out_hash/out_count at the container's own line range
  *   [doc_line0[d], doc_line0[d] + n_templates[d]); sort-based and atomics-free.  Containers with
  *   more than 64 lines are listed (host) in big_docs_host (staged through big_docs_dev); at most
- *   krca_template_max_lines() lines per container (KRCA_EINVAL beyond). */
+ *   krca_template_max_lines() lines per container (beyond: krca_template_hist_huge). */
 int krca_template_hash(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int64_t* line_end,
                        int64_t n_lines, uint64_t* hash, void* stream);
 int krca_template_hist(const uint64_t* hash, const int32_t* doc_lines, const int64_t* doc_line0, int64_t ndocs,
                        const int32_t* big_docs_host, int32_t n_big, int32_t* big_docs_dev, uint64_t* out_hash,
                        int32_t* out_count, int32_t* n_templates, void* stream);
 int32_t krca_template_max_lines(void);
+/* containers with more than krca_template_max_lines() lines, one call each: the same output for
+ * the container's n_lines hashes (hash, out_hash, out_count already offset to its doc_line0),
+ * *n_templates set on the device; exact via a distinct-hash table + bucketed LDS sorts.
+ * workspace: krca_template_huge_ws_size(n_lines) bytes, 16-byte aligned; *flag (device int32) = 1
+ * if a bucket overflowed (then the output is incomplete and the caller must fail). */
+int64_t krca_template_huge_ws_size(int64_t n_lines);
+int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspace, uint64_t* out_hash,
+                            int32_t* out_count, int32_t* n_templates, int32_t* flag, void* stream);
 
 /* ---- a9: cross-pod Pearson correlation with per-pod top-k (new primitive; the
  * reference's only "correlation" is the string group-by of ref:agents/coordinator.py:118-155).

@@ -17,6 +17,9 @@
 //   <= 4096 lines: one workgroup, bitonic sort in LDS, run compaction by a block scan.
 #include "krca_common.h"
 
+#include <algorithm>
+#include <climits>
+
 namespace {
 
 constexpr int TPB = 256;
@@ -208,6 +211,192 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_big(const uint64_t* __restrict_
   if (threadIdx.x == 0) n_tmpl[d] = carry;
 }
 
+// ---- containers with more than BIG lines -----------------------------------------------------
+// Exact and sort-based on the DISTINCT templates: (1) an open-addressing table in the workspace
+// counts each distinct hash (CAS insert, count atomics — a chatty container repeats a few
+// templates millions of times, so deduplicating first keeps every later step small); (2) the
+// distinct (hash, count) pairs are bucketed by their top hash bits, buckets sized for <= 2048
+// expected entries (the hashes are FNV-1a-64 outputs, so the top bits spread them); (3) one
+// workgroup per bucket sorts its pairs in LDS; buckets are in hash order and placed at their
+// exclusive-scan offsets, so the output is globally ascending with no gaps.  A bucket above
+// BIG entries (practically impossible for distinct 64-bit hashes) sets the error flag.
+constexpr uint64_t kEmpty = ~0ull;
+
+struct HugeLayout {  // workspace of one huge container of n lines (byte offsets)
+  int64_t cap, nb, shift;
+  int64_t keys, cnts, bcnt, bfill, boff, tk, tc, misc, total;
+  __host__ __device__ explicit HugeLayout(int64_t n) {
+    cap = 1;
+    while (cap < 2 * n) cap <<= 1;
+    nb = 1;
+    int lg = 0;
+    while (nb * 2048 < n) {
+      nb <<= 1;
+      ++lg;
+    }
+    shift = 64 - lg;
+    keys = 0;
+    cnts = keys + cap * 8;
+    bcnt = cnts + cap * 4;
+    bfill = bcnt + nb * 4;
+    boff = bfill + nb * 4;
+    tk = ((boff + (nb + 1) * 4 + 15) / 16) * 16;
+    tc = tk + n * 8;
+    misc = ((tc + n * 4 + 15) / 16) * 16;  // [0] special count, [1] flag
+    total = misc + 16;
+  }
+};
+
+__device__ __forceinline__ int64_t bucket_of(uint64_t h, int64_t shift) { return shift >= 64 ? 0 : (int64_t)(h >> shift); }
+
+__global__ __launch_bounds__(TPB) void huge_init(char* ws, int64_t n) {
+  const HugeLayout L(n);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(ws + L.keys);
+  int32_t* cnts = reinterpret_cast<int32_t*>(ws + L.cnts);
+  const int64_t stride = (int64_t)gridDim.x * TPB;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < L.cap; i += stride) {
+    keys[i] = kEmpty;
+    cnts[i] = 0;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < L.nb; i += stride) {
+    reinterpret_cast<int32_t*>(ws + L.bcnt)[i] = 0;
+    reinterpret_cast<int32_t*>(ws + L.bfill)[i] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) reinterpret_cast<int32_t*>(ws + L.misc)[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(TPB) void huge_insert(const uint64_t* __restrict__ hash, int64_t n, char* ws) {
+  const HugeLayout L(n);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(ws + L.keys);
+  int32_t* cnts = reinterpret_cast<int32_t*>(ws + L.cnts);
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = hash[i];
+  if (h == kEmpty) {  // the sentinel value itself: counted aside, emitted last (largest key)
+    atomicAdd(reinterpret_cast<int32_t*>(ws + L.misc), 1);
+    return;
+  }
+  int64_t s = (int64_t)(h & (uint64_t)(L.cap - 1));
+  for (;;) {  // the table has >= 2n slots: a free or matching slot is always found
+    const uint64_t prev = atomicCAS((unsigned long long*)(keys + s), (unsigned long long)kEmpty, (unsigned long long)h);
+    if (prev == kEmpty || prev == h) {
+      atomicAdd(cnts + s, 1);
+      return;
+    }
+    s = (s + 1) & (L.cap - 1);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void huge_bucket(int64_t n, char* ws, bool scatter) {
+  const HugeLayout L(n);
+  const uint64_t* keys = reinterpret_cast<const uint64_t*>(ws + L.keys);
+  const int32_t* cnts = reinterpret_cast<const int32_t*>(ws + L.cnts);
+  int32_t* bcnt = reinterpret_cast<int32_t*>(ws + L.bcnt);
+  int32_t* bfill = reinterpret_cast<int32_t*>(ws + L.bfill);
+  const int32_t* boff = reinterpret_cast<const int32_t*>(ws + L.boff);
+  const int64_t stride = (int64_t)gridDim.x * TPB;
+  for (int64_t s = (int64_t)blockIdx.x * TPB + threadIdx.x; s < L.cap; s += stride) {
+    const int32_t c = cnts[s];
+    if (c == 0) continue;
+    const uint64_t k = keys[s];
+    const int64_t b = bucket_of(k, L.shift);
+    if (!scatter) {
+      atomicAdd(bcnt + b, 1);
+    } else {
+      const int64_t pos = boff[b] + atomicAdd(bfill + b, 1);
+      reinterpret_cast<uint64_t*>(ws + L.tk)[pos] = k;
+      reinterpret_cast<int32_t*>(ws + L.tc)[pos] = c;
+    }
+  }
+}
+
+// one workgroup: exclusive scan of the bucket sizes, the template count, the sentinel entry
+__global__ __launch_bounds__(1024) void huge_scan(int64_t n, char* ws, uint64_t* __restrict__ out_hash,
+                                                  int32_t* __restrict__ out_cnt, int32_t* __restrict__ n_tmpl) {
+  const HugeLayout L(n);
+  const int32_t* bcnt = reinterpret_cast<const int32_t*>(ws + L.bcnt);
+  int32_t* boff = reinterpret_cast<int32_t*>(ws + L.boff);
+  int32_t* misc = reinterpret_cast<int32_t*>(ws + L.misc);
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t base = 0; base < L.nb; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int32_t v = i < L.nb ? bcnt[i] : 0;
+    if (v > BIG) misc[1] = 1;
+    int32_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int32_t before = carry;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    if (i < L.nb) boff[i] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int32_t u = carry;
+    boff[L.nb] = u;
+    const int32_t sp = misc[0];
+    if (sp > 0) {
+      out_hash[u] = kEmpty;
+      out_cnt[u] = sp;
+    }
+    *n_tmpl = u + (sp > 0 ? 1 : 0);
+  }
+}
+
+// workgroup per bucket: LDS bitonic sort of its (hash, count) pairs, written at the bucket offset
+__global__ __launch_bounds__(TPB) void huge_sort(int64_t n, const char* __restrict__ ws, uint64_t* __restrict__ out_hash,
+                                                 int32_t* __restrict__ out_cnt) {
+  const HugeLayout L(n);
+  __shared__ uint64_t key[BIG];
+  __shared__ int32_t val[BIG];
+  const int64_t b = blockIdx.x;
+  if (b >= L.nb) return;
+  const int32_t m = reinterpret_cast<const int32_t*>(ws + L.bcnt)[b];
+  const int32_t o = reinterpret_cast<const int32_t*>(ws + L.boff)[b];
+  if (m == 0 || m > BIG) return;  // m > BIG: flagged by huge_scan
+  const uint64_t* tk = reinterpret_cast<const uint64_t*>(ws + L.tk) + o;
+  const int32_t* tc = reinterpret_cast<const int32_t*>(ws + L.tc) + o;
+  int np = 64;
+  while (np < m) np <<= 1;
+  for (int i = threadIdx.x; i < np; i += TPB) {
+    key[i] = i < m ? tk[i] : kEmpty;
+    val[i] = i < m ? tc[i] : 0;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np; i += TPB) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint64_t a = key[i], c = key[l];
+          const bool up = (i & k) == 0;
+          if ((a > c) == up) {
+            key[i] = c;
+            key[l] = a;
+            const int32_t t = val[i];
+            val[i] = val[l];
+            val[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < m; i += TPB) {
+    out_hash[o + i] = key[i];
+    out_cnt[o + i] = val[i];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -245,5 +434,33 @@ int krca_template_hist(const uint64_t* hash, const int32_t* doc_lines, const int
 }
 
 int32_t krca_template_max_lines(void) { return BIG; }
+
+int64_t krca_template_huge_ws_size(int64_t n_lines) { return HugeLayout(n_lines).total; }
+
+int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspace, uint64_t* out_hash,
+                            int32_t* out_count, int32_t* n_templates, int32_t* flag, void* stream) {
+  KRCA_CHECK_ARG(n_lines > 0 && n_lines < INT32_MAX, "krca_template_hist_huge: n_lines out of range");
+  KRCA_CHECK_ARG(hash && workspace && out_hash && out_count && n_templates && flag,
+                 "krca_template_hist_huge: null pointer");
+  KRCA_CHECK_ARG(((uintptr_t)workspace & 15) == 0, "krca_template_hist_huge: workspace must be 16-byte aligned");
+  const HugeLayout L(n_lines);
+  char* ws = static_cast<char*>(workspace);
+  hipStream_t st = krca::as_stream(stream);
+  const unsigned g_cap = (unsigned)std::min<int64_t>(krca::ceil_div(L.cap, TPB), 8192);
+  hipLaunchKernelGGL(huge_init, dim3(g_cap), dim3(TPB), 0, st, ws, n_lines);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(huge_insert, dim3((unsigned)krca::ceil_div(n_lines, TPB)), dim3(TPB), 0, st, hash, n_lines, ws);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(huge_bucket, dim3(g_cap), dim3(TPB), 0, st, n_lines, ws, false);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(huge_scan, dim3(1), dim3(1024), 0, st, n_lines, ws, out_hash, out_count, n_templates);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(huge_bucket, dim3(g_cap), dim3(TPB), 0, st, n_lines, ws, true);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(huge_sort, dim3((unsigned)L.nb), dim3(TPB), 0, st, n_lines, (const char*)ws, out_hash, out_count);
+  KRCA_LAUNCH_CHECK();
+  KRCA_HIP(hipMemcpyAsync(flag, ws + L.misc + 4, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  return KRCA_OK;
+}
 
 }  // extern "C"

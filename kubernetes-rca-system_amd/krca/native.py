@@ -35,6 +35,8 @@ SIGNATURES = {
     "krca_template_hash": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "krca_template_hist": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_template_max_lines": (c_i32, []),
+    "krca_template_huge_ws_size": (c_i64, [c_i64]),
+    "krca_template_hist_huge": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_corr_pad_rows": (c_i64, [c_i64]),
     "krca_corr_pad_steps": (c_i32, [c_i32]),
     "krca_corr_cand_size": (c_i64, [c_i64, c_i32, c_i32]),
@@ -395,13 +397,24 @@ class NativeEngine:
                "krca_template_hash")
         dl = scan["doc_lines"].cpu().numpy()
         cap = self.lib.krca_template_max_lines()
-        if len(dl) and dl.max() > cap:
-            raise KrcaError(f"template histogram: a container has {int(dl.max())} lines (max {cap})")
-        big = np.nonzero(dl > 64)[0].astype(np.int32)
+        big = np.nonzero((dl > 64) & (dl <= cap))[0].astype(np.int32)
+        huge = np.nonzero(dl > cap)[0]
         bigd = torch.empty(max(len(big), 1), dtype=torch.int32, device=self.device)
         _check(self.lib.krca_template_hist(self.ptr(h), self.ptr(scan["doc_lines"]), self.ptr(scan["doc_line0"]), D,
                                            big.ctypes.data_as(c_vp), len(big), self.ptr(bigd), self.ptr(oh),
                                            self.ptr(oc), self.ptr(nt), self._stream()), "krca_template_hist")
+        if len(huge):  # > cap lines: a distinct-hash table + bucketed sorts per container
+            d0 = scan["doc_line0"].cpu().numpy()
+            flag = torch.zeros(len(huge), dtype=torch.int32, device=self.device)
+            for i, d in enumerate(huge.tolist()):
+                n, lo = int(dl[d]), int(d0[d])
+                ws = self._workspace("tmpl_huge", self.lib.krca_template_huge_ws_size(n) + 16)
+                _check(self.lib.krca_template_hist_huge(c_vp(h.data_ptr() + 8 * lo), n, self.ptr(ws),
+                                                        c_vp(oh.data_ptr() + 8 * lo), c_vp(oc.data_ptr() + 4 * lo),
+                                                        c_vp(nt.data_ptr() + 4 * d), c_vp(flag.data_ptr() + 4 * i),
+                                                        self._stream()), "krca_template_hist_huge")
+            if int(flag.max().item()):
+                raise KrcaError("template histogram: a hash bucket overflowed (not expected for 64-bit hashes)")
         torch.cuda.current_stream(self.device).synchronize()  # big-doc list lives on the host
         return dict(hash=h[:L], tmpl_hash=oh[:L], tmpl_count=oc[:L], n_templates=nt)
 

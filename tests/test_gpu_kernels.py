@@ -306,6 +306,23 @@ def test_template_hist_vs_oracle(eng):
         assert got[d] == oracle.template_hist(text), d
 
 
+def test_template_hist_huge_containers(eng):
+    """Containers above krca_template_max_lines() lines: distinct-hash table + bucketed sorts,
+    exact vs the oracle (few templates repeated many times; all-distinct templates; a mix)."""
+    rng = np.random.default_rng(3)
+    letters = np.array(list("abcdefghijklmnopqrstuvwxyz"))
+    word = lambda n: "".join(rng.choice(letters, n))  # noqa: E731  (no digits: never masked)
+    docs = ["\n".join("GET /health %d ok" % i if i % 3 else "worker %s busy" % ("ab"[i % 2]) for i in range(6000))]
+    docs.append("\n".join("job %s done" % word(9) for _ in range(9000)))   # ~9000 distinct templates
+    docs.append("short 1\nshort 2")
+    docs.append("\n".join(("evt %s" % word(3)) if i % 2 else "tick %d" % i for i in range(40000)))
+    docs.append("\n".join("x" for _ in range(4097)))                         # one template, 4097 lines
+    assert max(len(d.splitlines()) for d in docs) > eng.lib.krca_template_max_lines()
+    got = eng.template_hist(*pack_documents(docs))
+    for d, text in enumerate(docs):
+        assert got[d] == oracle.template_hist(text), d
+
+
 def test_template_hash_examples(eng):
     assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/<*>/items <*> <*>"
     assert oracle.template_of(b"uuid 550e8400-e29b-41d4-a716-446655440000 deadbeef") == \
