@@ -35,6 +35,8 @@ def test_version_and_host_helpers():
     from krca.rca import NSLOT
     assert lib.krca_ppr_nslot() == NSLOT  # send-slice layout shared by the kernels and krca/rca.py
     assert lib.krca_ppr_ctl_size(1000) >= 12 * 1000  # long-row accumulators + tickets
+    assert lib.krca_group_max_rank() == 6  # 64-byte slot records: first, counts, 6 ranks
+    assert lib.krca_template_huge_ws_size(5000) >= 2 * 5000 * 12  # distinct-hash table of >= 2n slots
 
 
 def test_ppr_plan_blocks_cover_rows():
