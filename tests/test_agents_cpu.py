@@ -97,6 +97,24 @@ def test_events_columns_match_host_loop():
     assert len(dev["findings"]) > 50
 
 
+def test_events_bulk_columns_equal_dict_path():
+    """A client's get_event_columns (bulk accessor) gives the same findings as its event dicts."""
+    from krca import eventcols
+
+    class Bulk(A.DictClient):
+        def get_event_columns(self, ns):
+            return self.cols
+
+    evs = A.load("events_random.json")["events"]["medium"]["events"]
+    cols = eventcols.encode_events(evs)
+    assert cols is not None
+    c = Bulk(events=evs)
+    c.cols = cols
+    assert A.strip(A.EventsAgent(c, engine=ENG).analyze("x")) == A.strip(
+        A.EventsAgent(A.DictClient(events=evs), engine=ENG).analyze("x"))
+    assert eventcols.encode_events([{"involvedObject": {"name": 3}}]) is None  # non-str: reference loops
+
+
 def test_comprehensive_roots_order():
     res = A.Coordinator(A.Shim(), engine=ENG).run_analysis("comprehensive", A.NS)
     assert [r["component"] for r in res["root_causes"]] == [
