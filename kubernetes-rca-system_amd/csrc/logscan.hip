@@ -612,36 +612,62 @@ __global__ void log_last_end(const uint8_t* __restrict__ text, int64_t nbytes, c
   line_end[L - 1] = nbytes - sep_len(b3, b2, b1, doc_off[k] == nbytes - 1);
 }
 
+// LDS form of the transition table for log_dfa / log_dfa_long: an entry holds the target state's
+// row offset (target * NSYM, so the next lookup is one add, no multiply on the dependent chain) and
+// kAcc when the target state reports a category.  The walk reads out[] only on those rare entries:
+// two LDS loads per byte instead of three, same masks (or-ing a zero out[] entry is a no-op).
+constexpr uint32_t kAcc = 0x8000u;
+static_assert(KRCA_DFA_NSTATE * KRCA_DFA_NSYM <= (int)kAcc, "row offsets must fit below kAcc");
+
+__device__ __forceinline__ uint32_t dfa_row_entry(int i) {
+  const uint32_t t = krca_dfa_trans[i];
+  return t * KRCA_DFA_NSYM | (krca_dfa_out[t] ? kAcc : 0u);
+}
+
 __device__ __forceinline__ void dfa_load(DfaLds& dfa) {
-  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * KRCA_DFA_NSYM; i += blockDim.x) dfa.trans[i] = krca_dfa_trans[i];
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * KRCA_DFA_NSYM; i += blockDim.x) dfa.trans[i] = (uint16_t)dfa_row_entry(i);
   for (int i = threadIdx.x; i < KRCA_DFA_NSTATE; i += blockDim.x) dfa.out[i] = krca_dfa_out[i];
   for (int i = threadIdx.x; i < 128; i += blockDim.x) dfa.ascii[i] = krca_dfa_ascii_sym[i];
   __syncthreads();
 }
 
-__global__ __launch_bounds__(TPB) void log_dfa(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
-                                               const int64_t* __restrict__ line_start,
-                                               const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
-                                               int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
+// 512-lane workgroups: the 32 KB LDS table allows 4 workgroups per CU, so 512 lanes give 8 waves per
+// SIMD to hide the walk's dependent LDS round trips (256-lane groups left it at 4).
+constexpr int DFA_TPB = 512;
+
+__global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
+                                                   const int64_t* __restrict__ line_start,
+                                                   const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
+                                                   int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
   __shared__ DfaLds dfa;
   dfa_load(dfa);
   Bytes B;
   B.init(text, nbytes);
-  for (int64_t l = (int64_t)blockIdx.x * TPB + threadIdx.x; l < L; l += (int64_t)gridDim.x * TPB) {
+  for (int64_t l = (int64_t)blockIdx.x * DFA_TPB + threadIdx.x; l < L; l += (int64_t)gridDim.x * DFA_TPB) {
     const int64_t s = line_start[l], e = line_end[l];
     if (e - s > LONG_LINE) {
       long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // a wave per long line (log_dfa_long)
       continue;
     }
-    uint32_t st = 0, mask = 0;
-    for (int64_t p = s; p < e;) {
-      uint32_t cp = B.at(p);
-      int len = 1;
-      if (cp >= 0x80) len = decode(B, p, cp);
-      const uint32_t sym = cp < 128 ? (uint32_t)dfa.ascii[cp] : cp_symbol(dfa, cp);
-      st = dfa.trans[st * KRCA_DFA_NSYM + sym];
-      mask |= dfa.out[st];
-      p += len;
+    uint32_t row = 0, mask = 0;
+    if (s < e) {
+      // software-pipelined walk: the symbol of the next code point is looked up while the
+      // transition of the current one is in flight (one LDS round trip per byte, not two)
+      uint32_t cp;
+      int len = decode(B, s, cp);
+      uint32_t sym = cp_symbol(dfa, cp);
+      for (int64_t p = s;;) {
+        const uint32_t t = dfa.trans[row + sym];
+        p += len;
+        const bool more = p < e;
+        if (more) {
+          len = decode(B, p, cp);
+          sym = cp_symbol(dfa, cp);
+        }
+        row = t & (kAcc - 1);
+        if (__builtin_expect((t & kAcc) != 0, 0)) mask |= dfa.out[row / KRCA_DFA_NSYM];
+        if (!more) break;
+      }
     }
     line_mask[l] = mask;
   }
@@ -663,7 +689,7 @@ __global__ __launch_bounds__(TPB) void log_dfa_long(const uint8_t* __restrict__ 
     const int64_t s = line_start[l], e = line_end[l];
     const int64_t seg = (e - s + 63) / 64;
     const int64_t a = min(e, s + lane * seg), b = min(e, a + seg);
-    uint32_t st = 0, mask = 0;
+    uint32_t row = 0, mask = 0;
     const int64_t p0 = a > s ? cp_align(B, a, e) : s;  // first code point starting in [a, b)
     if (p0 > s && p0 < b) {  // warm-up over the <= WARM code points of the line before p0
       int64_t k = p0;
@@ -676,15 +702,16 @@ __global__ __launch_bounds__(TPB) void log_dfa_long(const uint8_t* __restrict__ 
       while (k < p0) {
         uint32_t cp;
         const int len = decode(B, k, cp);
-        st = dfa.trans[st * KRCA_DFA_NSYM + cp_symbol(dfa, cp)];
+        row = dfa.trans[row + cp_symbol(dfa, cp)] & (kAcc - 1);
         k += len;
       }
     }
     for (int64_t p = p0; p < b;) {
       uint32_t cp;
       const int len = decode(B, p, cp);
-      st = dfa.trans[st * KRCA_DFA_NSYM + cp_symbol(dfa, cp)];
-      mask |= dfa.out[st];
+      const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
+      row = t & (kAcc - 1);
+      if (__builtin_expect((t & kAcc) != 0, 0)) mask |= dfa.out[row / KRCA_DFA_NSYM];
       p += len;
     }
     for (int off = 32; off > 0; off >>= 1) mask |= __shfl_xor(mask, off, 64);
@@ -886,8 +913,8 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, n_lines, line_end);
     KRCA_LAUNCH_CHECK();
-    const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, TPB), 256 * 4);
-    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(TPB), 0, st, text, nbytes, n_lines,
+    const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, DFA_TPB), 256 * 4);
+    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, n_lines,
                        (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,
