@@ -520,11 +520,29 @@ __global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ tex
                                                  int64_t* __restrict__ line_start, int64_t* __restrict__ line_end,
                                                  int64_t* __restrict__ chunk_line0) {
   constexpr int NIT = TILE / (TPB * PIECE);
+  constexpr int NBW = (int)(TILE / 32) + 2;  // container-start bitmap: bytes tile0-32 .. tile0+TILE+31
   __shared__ int64_t s_base[TPB];
   __shared__ int64_t s_wsum[TPB / 64];
+  __shared__ uint32_t s_cs[NBW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
   const int64_t tile0 = tile * TILE;
+  for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;
+  __syncthreads();
+  {  // the tile's non-empty container starts in [tile0-1, tile0+TILE) as bits: one coalesced pass over
+     // doc_off from the container holding byte tile0-1, instead of a dependent doc_off walk per piece
+    const int64_t tend = tile0 + TILE;
+    const int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
+    for (int64_t kb = k0;; kb += TPB) {
+      const int64_t k = kb + threadIdx.x;
+      const int64_t st = k < D ? doc_off[k] : INT64_MAX;
+      if (st >= tile0 - 1 && st < tend && doc_off[k + 1] > st) {
+        const int64_t j = st - (tile0 - 32);
+        atomicOr(&s_cs[j >> 5], 1u << (int)(j & 31));
+      }
+      if (__syncthreads_or(st >= tend)) break;  // doc_off is sorted: no later container starts inside
+    }
+  }
   {  // first line id of each of the tile's 256 chunks
     const int64_t v = chunk_cnt[tile * TPB + threadIdx.x];
     int64_t x = v;
@@ -556,12 +574,9 @@ __global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ tex
                  (high_bits4(sep_flags(w[1], w[2])) << 8) | (high_bits4(sep_flags(w[2], w[3])) << 12);
     uint32_t C = 0;  // container first bytes at q-1+j, j = 0..16 (non-empty containers only)
     if (q < nbytes) {
-      const int64_t qm = q > 0 ? q - 1 : 0;
-      for (int64_t k = chunk_doc[qm / CH]; k < D; ++k) {
-        const int64_t st = doc_off[k];
-        if (st >= q + PIECE) break;
-        if (st >= q - 1 && doc_off[k + 1] > st) C |= 1u << (int)(st - (q - 1));
-      }
+      const int j = (int)(q - 1 - (tile0 - 32));  // bit of byte q-1 in s_cs
+      const uint64_t two = ((uint64_t)s_cs[(j >> 5) + 1] << 32) | s_cs[j >> 5];
+      C = (uint32_t)(two >> (j & 31)) & 0x1FFFFu;
       S |= C >> 1;
       if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
     } else {
