@@ -1,8 +1,8 @@
 // Deterministic top-k (descending value, ties -> lower index) for float32 and int64 keys.
 //
 // Used for the anomaly ranking (a5) and the root-cause top-10 (a10).  Two launches:
-//   stage 1: each lane keeps a sorted top-KMAX list in registers (unrolled insertion network,
-//            static register indices), then the workgroup extracts its top-k by k rounds of
+//   stage 1: each lane keeps a sorted top-KM list in registers (KM = 10 for k <= 10, else 16;
+//            unrolled insertion network, static register indices), then the workgroup extracts its top-k by k rounds of
 //            a block-wide arg-max over the lanes' list heads (wave shuffles + LDS);
 //   stage 2: one workgroup merges the G*k stage-1 candidates the same way.
 // NaN keys are never selected (ordered below every number).  Bandwidth: one read of v.
@@ -14,6 +14,7 @@ namespace {
 
 constexpr int KMAX = 16;
 constexpr int TPB = 256;
+constexpr int BATCH = 8;  // keys loaded per lane before they are inserted
 
 template <typename K>
 struct Key;
@@ -34,21 +35,21 @@ __device__ __forceinline__ bool better(K va, int32_t ia, K vb, int32_t ib) {
   return va > vb || (va == vb && (uint32_t)ia < (uint32_t)ib);
 }
 
-template <typename K>
+template <typename K, int KM>
 struct List {
-  K v[KMAX];
-  int32_t i[KMAX];
+  K v[KM];
+  int32_t i[KM];
   __device__ void init() {
 #pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
+    for (int j = 0; j < KM; ++j) {
       v[j] = Key<K>::lowest();
       i[j] = -1;  // (uint32)-1 = loses every tie
     }
   }
   __device__ void insert(K nv, int32_t ni) {
-    if (!better(nv, ni, v[KMAX - 1], i[KMAX - 1])) return;
+    if (!better(nv, ni, v[KM - 1], i[KM - 1])) return;
 #pragma unroll
-    for (int j = KMAX - 1; j > 0; --j) {
+    for (int j = KM - 1; j > 0; --j) {
       const bool up = better(nv, ni, v[j - 1], i[j - 1]);
       const bool here = better(nv, ni, v[j], i[j]);
       const K pv = v[j - 1];
@@ -63,12 +64,12 @@ struct List {
   }
   __device__ void pop() {
 #pragma unroll
-    for (int j = 0; j < KMAX - 1; ++j) {
+    for (int j = 0; j < KM - 1; ++j) {
       v[j] = v[j + 1];
       i[j] = i[j + 1];
     }
-    v[KMAX - 1] = Key<K>::lowest();
-    i[KMAX - 1] = -1;
+    v[KM - 1] = Key<K>::lowest();
+    i[KM - 1] = -1;
   }
 };
 
@@ -84,8 +85,8 @@ __device__ __forceinline__ int64_t shfl_xor_key<int64_t>(int64_t v, int off) {
 }
 
 // k rounds of block-wide arg-max over list heads; thread 0 writes (out_v, out_i)[0..k)
-template <typename K>
-__device__ void block_extract(List<K>& L, int k, K* out_v, int32_t* out_i) {
+template <typename K, int KM>
+__device__ void block_extract(List<K, KM>& L, int k, K* out_v, int32_t* out_i) {
   __shared__ K sv[TPB / 64];
   __shared__ int32_t si[TPB / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -122,26 +123,46 @@ __device__ void block_extract(List<K>& L, int k, K* out_v, int32_t* out_i) {
   }
 }
 
-template <typename K>
+template <typename K, int KM>
 __global__ __launch_bounds__(TPB) void topk_stage1(const K* __restrict__ v, int64_t N, int k, K* __restrict__ cv,
                                                    int32_t* __restrict__ ci) {
-  List<K> L;
+  List<K, KM> L;
   L.init();
   const int64_t stride = (int64_t)gridDim.x * TPB;
-  for (int64_t j = (int64_t)blockIdx.x * TPB + threadIdx.x; j < N; j += stride)
-    L.insert(Key<K>::sanitize(v[j]), (int32_t)j);
-  block_extract<K>(L, k, cv + (int64_t)blockIdx.x * k, ci + (int64_t)blockIdx.x * k);
+  for (int64_t j0 = (int64_t)blockIdx.x * TPB + threadIdx.x; j0 < N; j0 += stride * BATCH) {
+    K bv[BATCH];  // the batch's loads are issued together, not one per (branchy) insert
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int64_t j = j0 + u * stride;
+      bv[u] = j < N ? Key<K>::sanitize(v[j]) : Key<K>::lowest();
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u)
+      if (j0 + u * stride < N) L.insert(bv[u], (int32_t)(j0 + u * stride));
+  }
+  block_extract<K, KM>(L, k, cv + (int64_t)blockIdx.x * k, ci + (int64_t)blockIdx.x * k);
 }
 
-template <typename K>
+template <typename K, int KM>
 __global__ __launch_bounds__(TPB) void topk_stage2(const K* __restrict__ cv, const int32_t* __restrict__ ci,
                                                    int64_t M, int k, int32_t* __restrict__ idx,
                                                    K* __restrict__ val) {
-  List<K> L;
+  List<K, KM> L;
   L.init();
-  for (int64_t j = threadIdx.x; j < M; j += TPB)
-    if (ci[j] != -1) L.insert(cv[j], ci[j]);
-  block_extract<K>(L, k, val, idx);
+  for (int64_t j0 = threadIdx.x; j0 < M; j0 += TPB * BATCH) {
+    K bv[BATCH];
+    int32_t bi[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int64_t j = j0 + u * TPB;
+      bi[u] = j < M ? ci[j] : -1;
+      bv[u] = j < M ? cv[j] : Key<K>::lowest();
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u)
+      if (bi[u] != -1) L.insert(bv[u], bi[u]);
+  }
+  block_extract<K, KM>(L, k, val, idx);
 }
 
 int64_t stage1_blocks(int64_t N) { return std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(N, TPB * 8), 1024)); }
@@ -155,9 +176,15 @@ int topk_impl(const K* v, int64_t N, int32_t k, void* ws, int32_t* idx, K* val, 
   K* cv = reinterpret_cast<K*>(ws);
   int32_t* ci = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + G * k * sizeof(int64_t));
   hipStream_t st = krca::as_stream(stream);
-  hipLaunchKernelGGL(topk_stage1<K>, dim3((unsigned)G), dim3(TPB), 0, st, v, N, k, cv, ci);
-  KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(topk_stage2<K>, dim3(1), dim3(TPB), 0, st, cv, ci, G * k, k, idx, val);
+  if (k <= 10) {  // the insertion network sized to k: the stages are instruction-bound on it
+    hipLaunchKernelGGL((topk_stage1<K, 10>), dim3((unsigned)G), dim3(TPB), 0, st, v, N, k, cv, ci);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL((topk_stage2<K, 10>), dim3(1), dim3(TPB), 0, st, cv, ci, G * k, k, idx, val);
+  } else {
+    hipLaunchKernelGGL((topk_stage1<K, KMAX>), dim3((unsigned)G), dim3(TPB), 0, st, v, N, k, cv, ci);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL((topk_stage2<K, KMAX>), dim3(1), dim3(TPB), 0, st, cv, ci, G * k, k, idx, val);
+  }
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
