@@ -773,10 +773,13 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
                                                 const uint32_t* __restrict__ line_mask, int64_t L,
                                                 int32_t* __restrict__ doc_lines, int32_t* __restrict__ hist,
                                                 int32_t* __restrict__ examples, int64_t* __restrict__ doc_line0) {
-  // the block's histograms and examples are assembled in LDS and leave in coalesced rows (a lane
-  // writing its own 52 ints at a 208-byte stride touched ~26 lines per store instruction)
-  __shared__ int32_t s_hist[TPB * KRCA_NCAT];
+  // the block's examples, then its histograms, are assembled in one LDS buffer and leave in
+  // coalesced rows (a lane writing its own 52 ints at a 208-byte stride touched ~26 lines per store
+  // instruction); one 39 KB buffer instead of two (52 KB) keeps 4 workgroups per CU, not 3
   __shared__ int32_t s_ex[TPB * KRCA_NCAT * 3];
+  int32_t mycnt[KRCA_NCAT];  // this lane's container histogram (small or big path)
+#pragma unroll
+  for (int c = 0; c < KRCA_NCAT; ++c) mycnt[c] = 0;
   const int64_t d0 = (int64_t)blockIdx.x * TPB;
   const int64_t d = d0 + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -807,11 +810,10 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
     }
     doc_lines[d] = (int32_t)(hi - lo);
     if (doc_line0) doc_line0[d] = lo;
-    int32_t* hd = s_hist + threadIdx.x * KRCA_NCAT;
     int32_t* ed = s_ex + threadIdx.x * KRCA_NCAT * 3;
 #pragma unroll
     for (int c = 0; c < KRCA_NCAT; ++c) {
-      hd[c] = cnt[c];
+      mycnt[c] = cnt[c];
       ed[c * 3] = ex[c][0];
       ed[c * 3 + 1] = ex[c][1];
       ed[c * 3 + 2] = ex[c][2];
@@ -845,20 +847,26 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
         }
       }
     }
+    if (lane == j) {  // counts are wave-uniform (ballots): the container's own lane keeps them
+#pragma unroll
+      for (int c = 0; c < KRCA_NCAT; ++c) mycnt[c] = cnt[c];
+    }
     if (lane == 0) {
       doc_lines[dj] = (int32_t)(bhi - blo);
       if (doc_line0) doc_line0[dj] = blo;
 #pragma unroll
-      for (int c = 0; c < KRCA_NCAT; ++c) {
-        s_hist[(threadIdx.x - lane + j) * KRCA_NCAT + c] = cnt[c];
+      for (int c = 0; c < KRCA_NCAT; ++c)
         for (int k = found[c]; k < 3; ++k) ex[c * 3 + k] = -1;
-      }
     }
   }
   __syncthreads();
   const int nv = (int)(D - d0 < TPB ? D - d0 : TPB);
-  for (int i = threadIdx.x; i < nv * KRCA_NCAT; i += TPB) hist[d0 * KRCA_NCAT + i] = s_hist[i];
   for (int i = threadIdx.x; i < nv * KRCA_NCAT * 3; i += TPB) examples[d0 * KRCA_NCAT * 3 + i] = s_ex[i];
+  __syncthreads();  // the buffer now takes the histograms
+#pragma unroll
+  for (int c = 0; c < KRCA_NCAT; ++c) s_ex[threadIdx.x * KRCA_NCAT + c] = mycnt[c];
+  __syncthreads();
+  for (int i = threadIdx.x; i < nv * KRCA_NCAT; i += TPB) hist[d0 * KRCA_NCAT + i] = s_ex[i];
 }
 
 int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, TILE)); }
