@@ -694,9 +694,10 @@ __global__ __launch_bounds__(TPB) void log_dfa_long(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ line_mask, const int32_t* __restrict__ long_q,
                                                     const int32_t* __restrict__ n_long) {
   __shared__ DfaLds dfa;
+  const int nq = *n_long;
+  if ((int64_t)blockIdx.x * (TPB / 64) >= nq) return;  // no long line for this block: skip the table fill
   dfa_load(dfa);
   const int lane = threadIdx.x & 63;
-  const int nq = *n_long;
   Bytes B;
   B.init(text, nbytes);
   for (int j = (int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)); j < nq; j += (int)(gridDim.x * (TPB / 64))) {
