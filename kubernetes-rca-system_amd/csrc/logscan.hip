@@ -109,38 +109,23 @@ struct DocWin {
 // byte k (0..3) of a little-endian word
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xFFu; }
 
-// str.splitlines line start at a byte p that is not its container's first byte, from the raw
-// bytes before it: every container is valid UTF-8 on its own (encoded from a str), so a multi-byte
-// separator never straddles two containers and no container starts with a continuation byte.
-__device__ __forceinline__ uint32_t sep_raw(uint32_t b3, uint32_t b2, uint32_t b1, uint32_t b0) {
-  return sep_before(b3, b2, b1, b0) ? 1u : 0u;
-}
-
 // chunk -> container holding its first byte: one thread per container writes the chunks that start
 // inside it (every chunk start lies in exactly one non-empty container), so no chunk searches.
-// It also adds the container-start correction of log_count to the chunk holding its first byte:
-// a non-empty container's first byte is a line start whatever precedes it (+1), and log_count
-// counts the raw separator test there (-sep_raw).  chunk_cnt is zeroed before this kernel.
-__global__ __launch_bounds__(TPB) void log_chunk_doc(const uint8_t* __restrict__ text,
-                                                     const int64_t* __restrict__ doc_off, int64_t D,
-                                                     int32_t* __restrict__ chunk_doc, int32_t* __restrict__ chunk_cnt) {
+// (Line starts at container first bytes are counted by log_count from its tile bitmap: every
+// container is valid UTF-8 on its own, so away from those bytes the raw separator test is exact.)
+__global__ __launch_bounds__(TPB) void log_chunk_doc(const int64_t* __restrict__ doc_off, int64_t D,
+                                                     int32_t* __restrict__ chunk_doc) {
   const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (d >= D) return;
   const int64_t s = doc_off[d], e = doc_off[d + 1];
   for (int64_t c = (s + CH - 1) / CH; c * CH < e; ++c) chunk_doc[c] = (int32_t)d;
-  if (s < e) {
-    const uint32_t b0 = text[s];
-    const uint32_t b1 = s >= 1 ? text[s - 1] : 0, b2 = s >= 2 ? text[s - 2] : 0, b3 = s >= 3 ? text[s - 3] : 0;
-    const int32_t corr = 1 - (int32_t)sep_raw(b3, b2, b1, b0);
-    if (corr) atomicAdd(chunk_cnt + s / CH, corr);
-  }
 }
 
 // ---- phase 1: line starts per chunk (streaming) -------------------------------------------
 // A workgroup takes one 64 KiB tile in 16 passes of 4 KiB; a lane reads 16 consecutive bytes
 // (one coalesced dwordx4 per lane: a wave reads 1 KiB contiguous), the 3 bytes before them come
 // from the previous lane by a shuffle (lane 0: one extra 4-byte load).  16 lanes = one 256-byte
-// chunk: count = container-start correction (already in chunk_cnt) + raw separator tests.
+// chunk: count = line starts = raw separator tests OR non-empty container first bytes.
 constexpr int PIECE = 16;
 constexpr int LANES_PER_CHUNK = CH / PIECE;  // 16
 
@@ -170,15 +155,51 @@ __device__ __forceinline__ uint32_t sep_flags(uint32_t wprev, uint32_t w) {
   return f;
 }
 
+// The tile's non-empty container starts in [tile0-1, tile0+TILE) as bits of s_cs (bit j = byte
+// tile0-32+j): one coalesced pass over doc_off from the container holding byte tile0-1 (chunk_doc),
+// instead of a dependent doc_off walk per 16-byte piece.  Used by log_count and log_lines.
+constexpr int NBW = (int)(TILE / 32) + 2;  // bytes tile0-32 .. tile0+TILE+31
+__device__ __forceinline__ void tile_container_starts(uint32_t* s_cs, int64_t tile0, int64_t nbytes,
+                                                      const int64_t* __restrict__ doc_off, int64_t D,
+                                                      const int32_t* __restrict__ chunk_doc) {
+  for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;
+  __syncthreads();
+  const int64_t tend = tile0 + TILE;
+  const int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
+  for (int64_t kb = k0;; kb += TPB) {
+    const int64_t k = kb + threadIdx.x;
+    const int64_t st = k < D ? doc_off[k] : INT64_MAX;
+    if (st >= tile0 - 1 && st < tend && doc_off[k + 1] > st) {
+      const int64_t j = st - (tile0 - 32);
+      atomicOr(&s_cs[j >> 5], 1u << (int)(j & 31));
+    }
+    if (__syncthreads_or(st >= tend)) break;  // doc_off is sorted: no later container starts inside
+  }
+}
+
+// container first bytes at q-1+j, j = 0..16, from the tile bitmap
+__device__ __forceinline__ uint32_t piece_container_starts(const uint32_t* s_cs, int64_t tile0, int64_t q) {
+  const int j = (int)(q - 1 - (tile0 - 32));
+  const uint64_t two = ((uint64_t)s_cs[(j >> 5) + 1] << 32) | s_cs[j >> 5];
+  return (uint32_t)(two >> (j & 31)) & 0x1FFFFu;
+}
+
+__device__ __forceinline__ uint32_t high_bits4(uint32_t f) {  // byte high bits -> 4-bit mask
+  return ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+}
+
 __global__ __launch_bounds__(TPB) void log_count(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                 const int64_t* __restrict__ doc_off, int64_t D,
+                                                 const int32_t* __restrict__ chunk_doc,
                                                  int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_tot) {
   constexpr int NIT = TILE / (TPB * PIECE);  // 16 passes of 4 KiB
   __shared__ int32_t s_cnt[TPB];             // the tile's 256 chunk counts
   __shared__ int64_t red[TPB / 64];
+  __shared__ uint32_t s_cs[NBW];
   const int lane = threadIdx.x & 63;
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
-  s_cnt[threadIdx.x] = chunk_cnt[(int64_t)blockIdx.x * TPB + threadIdx.x];  // container-start corrections
-  __syncthreads();
+  s_cnt[threadIdx.x] = 0;
+  tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
 #pragma unroll 4
   for (int it = 0; it < NIT; ++it) {
     const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
@@ -204,7 +225,13 @@ __global__ __launch_bounds__(TPB) void log_count(const uint8_t* __restrict__ tex
       f2 &= n >= 12 ? ~0u : (n <= 8 ? 0u : (0x80808080u >> (8 * (12 - n))));
       f3 &= n <= 12 ? 0u : (0x80808080u >> (8 * (16 - n)));
     }
-    uint32_t c = __popc(f0) + __popc(f1) + __popc(f2) + __popc(f3);
+    // a non-empty container's first byte starts a line whatever precedes it
+    uint32_t S = high_bits4(f0) | (high_bits4(f1) << 4) | (high_bits4(f2) << 8) | (high_bits4(f3) << 12);
+    if (q < nbytes) {
+      S |= piece_container_starts(s_cs, tile0, q) >> 1;
+      if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
+    }
+    uint32_t c = __popc(S);
 #pragma unroll
     for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
     if ((threadIdx.x & (LANES_PER_CHUNK - 1)) == 0)
@@ -508,10 +535,6 @@ __device__ __forceinline__ int sep_len(uint32_t b3, uint32_t b2, uint32_t b1, bo
   return 0;
 }
 
-__device__ __forceinline__ uint32_t high_bits4(uint32_t f) {  // byte high bits -> 4-bit mask
-  return ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
-}
-
 __global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ text, int64_t nbytes,
                                                  const int64_t* __restrict__ doc_off, int64_t D,
                                                  const int32_t* __restrict__ chunk_doc,
@@ -520,29 +543,13 @@ __global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ tex
                                                  int64_t* __restrict__ line_start, int64_t* __restrict__ line_end,
                                                  int64_t* __restrict__ chunk_line0) {
   constexpr int NIT = TILE / (TPB * PIECE);
-  constexpr int NBW = (int)(TILE / 32) + 2;  // container-start bitmap: bytes tile0-32 .. tile0+TILE+31
   __shared__ int64_t s_base[TPB];
   __shared__ int64_t s_wsum[TPB / 64];
   __shared__ uint32_t s_cs[NBW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
   const int64_t tile0 = tile * TILE;
-  for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;
-  __syncthreads();
-  {  // the tile's non-empty container starts in [tile0-1, tile0+TILE) as bits: one coalesced pass over
-     // doc_off from the container holding byte tile0-1, instead of a dependent doc_off walk per piece
-    const int64_t tend = tile0 + TILE;
-    const int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
-    for (int64_t kb = k0;; kb += TPB) {
-      const int64_t k = kb + threadIdx.x;
-      const int64_t st = k < D ? doc_off[k] : INT64_MAX;
-      if (st >= tile0 - 1 && st < tend && doc_off[k + 1] > st) {
-        const int64_t j = st - (tile0 - 32);
-        atomicOr(&s_cs[j >> 5], 1u << (int)(j & 31));
-      }
-      if (__syncthreads_or(st >= tend)) break;  // doc_off is sorted: no later container starts inside
-    }
-  }
+  tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);
   {  // first line id of each of the tile's 256 chunks
     const int64_t v = chunk_cnt[tile * TPB + threadIdx.x];
     int64_t x = v;
@@ -574,9 +581,7 @@ __global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ tex
                  (high_bits4(sep_flags(w[1], w[2])) << 8) | (high_bits4(sep_flags(w[2], w[3])) << 12);
     uint32_t C = 0;  // container first bytes at q-1+j, j = 0..16 (non-empty containers only)
     if (q < nbytes) {
-      const int j = (int)(q - 1 - (tile0 - 32));  // bit of byte q-1 in s_cs
-      const uint64_t two = ((uint64_t)s_cs[(j >> 5) + 1] << 32) | s_cs[j >> 5];
-      C = (uint32_t)(two >> (j & 31)) & 0x1FFFFu;
+      C = piece_container_starts(s_cs, tile0, q);
       S |= C >> 1;
       if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
     } else {
@@ -896,11 +901,10 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   int32_t* chunk = reinterpret_cast<int32_t*>(ws + nt + 1);
   int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
   hipStream_t st = krca::as_stream(stream);
-  KRCA_HIP(hipMemsetAsync(chunk, 0, nt * TPB * sizeof(int32_t), st));
-  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, text, doc_off, ndocs,
-                     cdoc, chunk);
+  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs, cdoc);
   KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, chunk, tile);
+  hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
+                     (const int32_t*)cdoc, chunk, tile);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(log_scan, dim3(1), dim3(1024), 0, st, tile, nt, n_lines);
   KRCA_LAUNCH_CHECK();
