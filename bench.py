@@ -20,6 +20,7 @@ after step i+1 has been enqueued.  Every step still does all of its work;
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -31,28 +32,42 @@ sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
+    from krca.rca import RANKING
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pods", type=int, default=1_000_000)
-    ap.add_argument("--degree", type=int, default=20)
+    ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--metrics", type=int, default=8)
     ap.add_argument("--tsteps", type=int, default=1440)
-    ap.add_argument("--window", type=int, default=60)
-    ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--alpha", type=float, default=0.5)
-    ap.add_argument("--seed-floor", type=float, default=4.0)
+    ap.add_argument("--window", type=int, default=RANKING.window)
+    ap.add_argument("--iters", type=int, default=RANKING.iters)
+    ap.add_argument("--alpha", type=float, default=RANKING.alpha)
+    ap.add_argument("--seed-floor", type=float, default=RANKING.seed_floor)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample-pods", type=int, default=50_000)
+    ap.add_argument("--cpu-sample-pods", type=int, default=25_000)
+    ap.add_argument("--cpu-warmup", type=int, default=3)
+    ap.add_argument("--cpu-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run steps back to back on one stream (default: two streams, step i+1's scoring "
                          "overlaps step i's PageRank)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def cpu_model():
+    try:
+        for ln in subprocess.run(["lscpu"], capture_output=True, text=True, check=True).stdout.splitlines():
+            if ln.startswith("Model name:"):
+                return ln.split(":", 1)[1].strip()
+    except (OSError, subprocess.CalledProcessError):
+        pass
+    import platform
+    return platform.processor()
 
 
 def log(*a):
@@ -86,7 +101,7 @@ def main():
 
     # ---- synthetic mesh (host graph, device metrics; not timed) --------------------------
     t0 = time.time()
-    mesh = synth.make_graph(args.pods, avg_degree=args.degree, seed=args.seed)
+    mesh = synth.make_graph(args.pods, n_edges=args.edges, seed=args.seed)
     hops = synth.caller_hops(mesh, mesh.roots)
     lo, hi, n_max = shard_range(args.pods, world, rank)
     rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, lo, hi)
@@ -123,14 +138,20 @@ def main():
         with torch.cuda.stream(streams[j]):
             return steps[j].merge(idx, val)
 
-    def run_steps(n, events=None):
+    def run_steps(n, events=None, marks=None):
+        """marks: host time after each step's top-10 is on the host (per-step spacing)."""
         pending, top = None, None
         for i in range(n):
             cur = enqueue(i, events[i] if events else None)
             if pending is not None:
                 top = finish(*pending)
+                if marks is not None:
+                    marks.append(time.perf_counter())
             pending = cur
-        return finish(*pending)
+        top = finish(*pending)
+        if marks is not None:
+            marks.append(time.perf_counter())
+        return top
 
     # ---- warmup + timed steps ------------------------------------------------------------
     if args.warmup:
@@ -140,10 +161,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    marks = [t_start]
     # HIP events on the stream each scoring kernel is launched on
-    top_idx, top_key = run_steps(args.steps, ev)
+    top_idx, top_key = run_steps(args.steps, ev, marks)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    step_ms = np.diff(np.asarray(marks)) * 1e3  # completion spacing of consecutive steps
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -151,7 +174,7 @@ def main():
         elapsed = float(t.item())
     # end-to-end latency of one step (scores -> PageRank -> top-10 on the host), not pipelined
     lat = []
-    ev_solo = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    ev_solo = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
     for e_solo in ev_solo:
         if world > 1:
             dist.barrier()
@@ -163,6 +186,7 @@ def main():
         lat.append(time.perf_counter() - t1)
     solo_ms = float(np.median([a.elapsed_time(b) for a, b in ev_solo]))
     latency_ms = float(np.median(lat)) * 1e3
+    latency_p95_ms = float(np.percentile(lat, 95)) * 1e3
     if world > 1:
         t = torch.tensor([latency_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -192,11 +216,15 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f32 (f64 window sums, int64 fixed-point ranks)",
             "data": "synthetic (seeded mesh generator krca/synth.py; no network)",
             "config": {"workload": "C4: synthetic 1M-pod / 20M-edge mesh, 8 metrics x 1440 steps, full RCA step "
-                                   "(rolling z-score -> 30-iteration seeded PPR -> top-10)",
+                                   "(rolling z-score -> 30-iteration seeded PPR -> top-10), ranking of krca.rca.Config",
                        "pods": args.pods, "edges": mesh.n_edges, "metrics": args.metrics, "tsteps": args.tsteps,
                        "window": args.window, "ppr_iters": args.iters, "alpha": args.alpha,
                        "seed_floor": args.seed_floor, "parallelism": f"pod-sharded x{world}"},
-            "e2e_rca_latency_ms": latency_ms, "pipelined_streams": n_pipe,
+            "e2e_rca_latency_ms": latency_ms, "e2e_rca_latency_p95_ms": latency_p95_ms,
+            "step_ms_median": float(np.median(step_ms)), "step_ms_p95": float(np.percentile(step_ms, 95)),
+            "pipelined_streams": n_pipe,
+            "scoring_variant": native.SCORE_VARIANTS[eng.lib.krca_rolling_score_variant(n_loc, args.metrics,
+                                                                                      args.tsteps, args.window)],
             "roofline": {"kernel": "krca_rolling_score", "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": bytes_score,
@@ -238,22 +266,38 @@ def main():
         ps = min(args.cpu_sample_pods, n_loc)
         xs = x[:, :ps, :].cpu().numpy()
         cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        t1 = time.perf_counter()
-        oracle.c_rolling_score(xs, args.window)
-        t_score = time.perf_counter() - t1
         score = shard.score_out["score"].cpu().numpy()
-        t1 = time.perf_counter()
-        oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
-        t_ppr = time.perf_counter() - t1
+        t_sc, t_pr = [], []
+        for i in range(args.cpu_warmup + args.cpu_runs):  # BASELINE.md §3 protocol
+            t1 = time.perf_counter()
+            oracle.c_rolling_score(xs, args.window)
+            t2 = time.perf_counter()
+            oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+            t3 = time.perf_counter()
+            if i >= args.cpu_warmup:
+                t_sc.append(t2 - t1)
+                t_pr.append(t3 - t2)
         # whole step on the CPU at the same mesh size, scoring time scaled from the sample
-        t_step = t_score * (n_loc / ps) + t_ppr
+        t_step = np.asarray(t_sc) * (n_loc / ps) + np.asarray(t_pr)
+        med = float(np.median(t_step))
         result["cpu_baseline"] = {
-            "value": args.pods * args.tsteps / t_step, "unit": "pod·timesteps/s", "cores": cores, "kind": "port",
+            "value": args.pods * args.tsteps / med, "unit": "pod·timesteps/s", "cores": cores, "kind": "port",
             "sample": f"scoring: oracle/krca_oracle.c on {ps} pods x {args.metrics} x {args.tsteps} "
-                      f"({t_score:.2f} s, scaled x{n_loc / ps:.0f}); PPR+top-10: full {args.pods}-node graph "
-                      f"({t_ppr:.2f} s); OpenMP threads = {cores}",
-            "ms_per_step": t_step * 1e3,
+                      f"(median {np.median(t_sc):.3f} s, scaled x{n_loc / ps:.0f}); PPR+top-10: full {args.pods}-node "
+                      f"graph (median {np.median(t_pr):.3f} s); OpenMP threads = {cores}; "
+                      f"{args.cpu_warmup} warm-up + {args.cpu_runs} timed runs",
+            "ms_per_step": med * 1e3, "ms_per_step_p95": float(np.percentile(t_step, 95)) * 1e3,
+            "cpu_model": cpu_model(),
         }
+        ref_t = os.path.join(ROOT, "tests", "golden", "ref_cpu_timings.json")
+        if os.path.exists(ref_t):  # the reference's own Python, timed in the build container
+            rt = json.load(open(ref_t))
+            result["cpu_baseline"]["reference_python"] = {
+                "where": "build container (reference code never runs on the GPU box): " + rt["host"]["cpu_model"],
+                "cores": 1, "timings": {k: {kk: v[kk] for kk in ("median_s", "p95_s", "units", "unit") if kk in v}
+                                        for k, v in rt["timings"].items()},
+                "note": "the reference has no rolling scoring or PageRank; these are its per-pod threshold "
+                        "loop, 13-regex line histogram, SPOF betweenness and C1 comprehensive analysis"}
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -44,6 +44,13 @@ int krca_version(void);
 const char* krca_last_error(void);
 int krca_device_count(int* n_host);
 
+/* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID,
+ * KRCA_LOG_IMPL, KRCA_GROUP_IMPL, KRCA_CORR_DEBUG.  Initialised once from the environment variables
+ * of the same names when the library loads; launchers never call getenv.  Process-global, not
+ * thread-safe (set them before launching work).  Unknown names: KRCA_EINVAL. */
+int krca_tune_set(const char* name, int32_t value);
+int krca_tune_get(const char* name, int32_t* value_host);
+
 /* ---- a1/a2: instantaneous usage thresholds ------------------------------------------------
  * Replaces the pod loops of MetricsAgent._analyze_cpu_usage / _analyze_memory_usage
  * (ref:agents/metrics_agent.py:88-94, 135-141): flags[p] gets KRCA_F_CPU80 iff usage[p][0] > 80,
@@ -61,9 +68,22 @@ int krca_usage_flags(const float* usage /*[P][2]*/, int64_t P, uint8_t* flags /*
  * M must be a power of two <= 64. */
 int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr,
                        float* z_last, float* score, int32_t* n_exceed, uint8_t* flags, void* stream);
+/* which kernel krca_rolling_score launches for these sizes (host query, no device work):
+ * KRCA_SCORE_PIPE software-pipelined chunks (the default), KRCA_SCORE_PIPE_ROWS the same with one
+ * buffer descriptor per row (series counts past the 2^31-byte descriptor range),
+ * KRCA_SCORE_RING plain loads, KRCA_SCORE_RING_BUF W-block buffer loads, KRCA_SCORE_REREAD any W. */
+#define KRCA_SCORE_PIPE 0
+#define KRCA_SCORE_RING 1
+#define KRCA_SCORE_RING_BUF 2
+#define KRCA_SCORE_REREAD 3
+#define KRCA_SCORE_PIPE_ROWS 4
+int krca_rolling_score_variant(int64_t P, int32_t M, int32_t T, int32_t W);
 
 /* ---- a11/a12: 13-category log histograms (ref:agents/logs_agent.py:124-181) ----------------
  * text = UTF-8 bytes of D container logs, container d = text[doc_off[d], doc_off[d+1]).
+ * Contract: doc_off[0] == 0, doc_off[D] == nbytes, doc_off non-decreasing, each container valid
+ * UTF-8 on its own (the host wrappers check the offsets; off-contract offsets are clamped on the
+ * device so they cannot fault, but the results are then unspecified).
  * Lines are str.splitlines() lines; a line is in category c iff
  * re.search(pattern_c, line, re.IGNORECASE) (compiled DFA, csrc/log_dfa_tables.h).
  * Two phases (the line count is data-dependent):
@@ -192,7 +212,8 @@ int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* strea
  * own anomaly; order-preserving as int64, fed to krca_topk_i64 */
 int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key, void* stream);
 
-/* ---- top-k (descending value, ties -> lower index), float32 or int64 keys ------------------ */
+/* ---- top-k (descending value, ties -> lower index), float32 or int64 keys; NaN keys are never
+ * selected: with fewer than k non-NaN keys the remaining slots are idx -1, val -inf / INT64_MIN -- */
 int64_t krca_topk_workspace_size(int64_t N, int32_t k);
 int krca_topk_f32(const float* v, int64_t N, int32_t k, void* workspace, int32_t* idx, float* val,
                   void* stream);

@@ -1,6 +1,8 @@
 // libkrca: version, error reporting and device queries (host-only translation unit).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <hip/hip_runtime.h>
 
@@ -8,6 +10,34 @@
 
 namespace krca {
 static thread_local char g_err[1024] = "";
+
+namespace {
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+struct NamedKnob {
+  const char* name;
+  int Tuning::*field;
+};
+const NamedKnob kKnobs[] = {
+    {"KRCA_SCORE_IMPL", &Tuning::score_impl}, {"KRCA_SCORE_CHUNK", &Tuning::score_chunk},
+    {"KRCA_SCORE_NT", &Tuning::score_nt},     {"KRCA_PPR_GRID", &Tuning::ppr_grid},
+    {"KRCA_LOG_IMPL", &Tuning::log_impl},     {"KRCA_GROUP_IMPL", &Tuning::group_impl},
+    {"KRCA_CORR_DEBUG", &Tuning::corr_debug},
+};
+Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20), env_int("KRCA_SCORE_NT", 1),
+                 env_int("KRCA_PPR_GRID", 0),   env_int("KRCA_LOG_IMPL", 0),     env_int("KRCA_GROUP_IMPL", 0),
+                 env_int("KRCA_CORR_DEBUG", 0)};
+const NamedKnob* find_knob(const char* name) {
+  if (!name) return nullptr;
+  for (const NamedKnob& k : kKnobs)
+    if (!strcmp(k.name, name)) return &k;
+  return nullptr;
+}
+}  // namespace
+
+const Tuning& tuning() { return g_tune; }
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -22,6 +52,20 @@ extern "C" {
 int krca_version(void) { return 100; }  // 0.1.0
 
 const char* krca_last_error(void) { return krca::g_err; }
+
+int krca_tune_set(const char* name, int32_t value) {
+  const krca::NamedKnob* k = krca::find_knob(name);
+  KRCA_CHECK_ARG(k, "krca_tune_set: unknown knob '%s'", name ? name : "(null)");
+  krca::g_tune.*(k->field) = value;
+  return KRCA_OK;
+}
+
+int krca_tune_get(const char* name, int32_t* value_host) {
+  const krca::NamedKnob* k = krca::find_knob(name);
+  KRCA_CHECK_ARG(k && value_host, "krca_tune_get: unknown knob '%s' or null out pointer", name ? name : "(null)");
+  *value_host = krca::g_tune.*(k->field);
+  return KRCA_OK;
+}
 
 int krca_device_count(int* n_host) {
   KRCA_CHECK_ARG(n_host != nullptr, "krca_device_count: null out pointer");

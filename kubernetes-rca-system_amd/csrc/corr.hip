@@ -736,10 +736,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
 
 // profiling aid, KRCA_CORR_DEBUG (results are wrong when set): 1 = product only, 2 = no global
 // candidate appends, 3 = no candidate slow path either
-int debug_mode() {
-  const char* e = getenv("KRCA_CORR_DEBUG");
-  return e ? atoi(e) : 0;
-}
+int debug_mode() { return krca::tuning().corr_debug; }
 
 constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
 

@@ -124,10 +124,7 @@ int krca_group_reduce(const int32_t* slot, const int64_t* key, int64_t N, int64_
   KRCA_LAUNCH_CHECK();
   if (N == 0) return KRCA_OK;
   KRCA_CHECK_ARG(slot && key, "krca_group_reduce: null input");
-  static const int impl = [] {
-    const char* e = getenv("KRCA_GROUP_IMPL");
-    return e ? atoi(e) : 0;
-  }();
+  const int impl = krca::tuning().group_impl;
   if (impl == 1)
     hipLaunchKernelGGL((group_pass<true, false>), dim3(grid_for(N)), dim3(TPB), 0, st, slot, key, N, S, 0, rec);
   else

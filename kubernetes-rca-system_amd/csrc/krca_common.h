@@ -40,4 +40,18 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // 2^60: fixed-point unit of the PageRank mass (krca_ppr)
 constexpr double kFix = 1152921504606846976.0;
 
+// Kernel-development A/B switches (include/krca.h krca_tune_set).  Read from the environment
+// once when the library loads, changed only through krca_tune_set; launchers read the struct,
+// never the environment.
+struct Tuning {
+  int score_impl;   // KRCA_SCORE_IMPL: 0 pipelined chunks, 1 plain loads, 2 W-block buffer loads, 4 per-row descriptors
+  int score_chunk;  // KRCA_SCORE_CHUNK: rows per pipelined chunk at W = 60 (10/12/15/20/30)
+  int score_nt;     // KRCA_SCORE_NT: non-temporal metric loads
+  int ppr_grid;     // KRCA_PPR_GRID: persistent PageRank grid (0 = occupancy API)
+  int log_impl;     // KRCA_LOG_IMPL: 0 line index + DFA lanes, 1 chunk-lane single pass
+  int group_impl;   // KRCA_GROUP_IMPL: 0 peeled atomics, 1 one atomic per lane
+  int corr_debug;   // KRCA_CORR_DEBUG: profiling aid (results wrong when != 0)
+};
+const Tuning& tuning();
+
 }  // namespace krca

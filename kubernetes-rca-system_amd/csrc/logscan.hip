@@ -113,11 +113,13 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8
 // inside it (every chunk start lies in exactly one non-empty container), so no chunk searches.
 // (Line starts at container first bytes are counted by log_count from its tile bitmap: every
 // container is valid UTF-8 on its own, so away from those bytes the raw separator test is exact.)
-__global__ __launch_bounds__(TPB) void log_chunk_doc(const int64_t* __restrict__ doc_off, int64_t D,
+// doc_off outside the contract (include/krca.h) is clamped to [0, nbytes] so no write leaves the map.
+__global__ __launch_bounds__(TPB) void log_chunk_doc(const int64_t* __restrict__ doc_off, int64_t D, int64_t nbytes,
                                                      int32_t* __restrict__ chunk_doc) {
   const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (d >= D) return;
-  const int64_t s = doc_off[d], e = doc_off[d + 1];
+  const int64_t s = min(max(doc_off[d], (int64_t)0), nbytes);
+  const int64_t e = min(max(doc_off[d + 1], s), nbytes);
   for (int64_t c = (s + CH - 1) / CH; c * CH < e; ++c) chunk_doc[c] = (int32_t)d;
 }
 
@@ -165,7 +167,8 @@ __device__ __forceinline__ void tile_container_starts(uint32_t* s_cs, int64_t ti
   for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;
   __syncthreads();
   const int64_t tend = tile0 + TILE;
-  const int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
+  int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
+  k0 = k0 < 0 ? 0 : (k0 > D ? D : k0);  // memory safety only: the map is exact under the doc_off contract
   for (int64_t kb = k0;; kb += TPB) {
     const int64_t k = kb + threadIdx.x;
     const int64_t st = k < D ? doc_off[k] : INT64_MAX;
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(TPB) void log_match(const uint8_t* __restrict__ tex
       Bytes B;
       B.init(text, nbytes);
       DocWin dw;
-      dw.load(doc_off, D, chunk_doc[g]);
+      dw.load(doc_off, D, min(max((int64_t)chunk_doc[g], (int64_t)0), D - 1));
       int64_t dstart = dw.b[0], dend = dw.b[1];
       const int64_t p0 = cp_align(B, c0, dend);  // first code point starting in this chunk
       int64_t cur = base - 1;  // id of the open line (lines before this chunk: base)
@@ -901,7 +904,9 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   int32_t* chunk = reinterpret_cast<int32_t*>(ws + nt + 1);
   int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
   hipStream_t st = krca::as_stream(stream);
-  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs, cdoc);
+  KRCA_HIP(hipMemsetAsync(cdoc, 0, nt * TPB * sizeof(int32_t), st));  // defined map even off-contract
+  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
+                     nbytes, cdoc);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
                      (const int32_t*)cdoc, chunk, tile);
@@ -926,8 +931,7 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   int32_t* n_long = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB);
   int32_t* long_q = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB + 1);
   hipStream_t st = krca::as_stream(stream);
-  const char* impl_env = getenv("KRCA_LOG_IMPL");  // read per call: tests A/B both paths in one process
-  const int impl = impl_env ? atoi(impl_env) : 0;
+  const int impl = krca::tuning().log_impl;  // A/B: tests switch it with krca_tune_set
   if (n_lines > 0 && impl == 1) {  // A/B: lane per 256-byte chunk, DFA and line logic in one pass
     KRCA_HIP(hipMemsetAsync(line_mask, 0, n_lines * sizeof(uint32_t), st));
     const int64_t grid = std::min<int64_t>(nt, 256 * 4);

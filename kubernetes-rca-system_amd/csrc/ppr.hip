@@ -466,7 +466,7 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
                  "krca_ppr_shard_step: null pointer");
   KRCA_CHECK_ARG(w_all != send, "krca_ppr_shard_step: w_all and send must be distinct buffers (ping-pong)");
   const int64_t nblk = plan_len / 4;
-  static const int64_t resident = [] {  // workgroups the device keeps resident (occupancy API)
+  static const int64_t occupancy = [] {  // workgroups the device keeps resident (occupancy API)
     int dev = 0, cus = 256, per_cu = 4;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -474,9 +474,9 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&ppr_step), TPB, 0) !=
             hipSuccess || per_cu < 1)
       per_cu = 4;
-    const char* e = getenv("KRCA_PPR_GRID");
-    return e ? (int64_t)atoll(e) : (int64_t)cus * per_cu;
+    return (int64_t)cus * per_cu;
   }();
+  const int64_t resident = krca::tuning().ppr_grid > 0 ? (int64_t)krca::tuning().ppr_grid : occupancy;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nblk, resident));
   hipLaunchKernelGGL(ppr_step, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, nblk,
                      w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));

@@ -14,8 +14,6 @@
 // division or square root; all products that feed a decision are explicit fma()s.
 // Pod-level reductions (max |z|, sum of exceedances, flag OR) are wave shuffles inside the
 // aligned M-lane group of the pod.
-#include <stdlib.h>
-
 #include "krca_common.h"
 
 #pragma clang fp contract(off)
@@ -207,7 +205,52 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float* x, int
                                            0x00020000);
 }
 
-template <int W, int C, int AUX = 0>
+// Row sources of the pipelined kernel.  SpanRows: one descriptor per chunk spanning its C rows
+// (needs 4*S*C < 2^31: up to ~3.3M pods x 8 metrics at C = 20).  BlockRows: one descriptor per
+// row covering only the workgroup's 256 series (base = x + t*S + s0), so any S < 2^32 works; it
+// costs a few scalar instructions per row, off the vector path.
+struct SpanRows {
+  const float* x;
+  int64_t S;
+  uint32_t rowb, voff;
+  int T;
+  __device__ __forceinline__ SpanRows(const float* x_, int64_t S_, int T_, int64_t s, bool active)
+      : x(x_), S(S_), rowb((uint32_t)(S_ * 4)), voff(active ? (uint32_t)s * 4u : 0u), T(T_) {}
+  template <int C, int AUX>
+  __device__ __forceinline__ void load(int t, float (&out)[C]) const {
+    const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t, T);
+#pragma unroll
+    for (int j = 0; j < C; ++j) out[j] = bload<AUX>(rs, voff, rowb * j);
+  }
+};
+
+struct BlockRows {
+  const float* xb;  // x + s0, s0 = the workgroup's first series
+  int64_t S;
+  uint32_t voff;
+  int nrec;  // bytes of the workgroup's series inside [0, S)
+  int T;
+  __device__ __forceinline__ BlockRows(const float* x_, int64_t S_, int T_, int64_t, bool)
+      : S(S_), voff(threadIdx.x * 4u), T(T_) {
+    const int64_t s0 = (int64_t)blockIdx.x * blockDim.x;
+    xb = x_ + s0;
+    const int64_t n = S_ - s0;
+    nrec = __builtin_amdgcn_readfirstlane((int)(4 * (n < (int64_t)blockDim.x ? n : (int64_t)blockDim.x)));
+  }
+  template <int C, int AUX>
+  __device__ __forceinline__ void load(int t, float (&out)[C]) const {
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int tt = t + j;
+      const bool in = tt < T;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(xb + (int64_t)(in ? tt : 0) * S), 0, in ? nrec : 0, 0x00020000);
+      out[j] = bload<AUX>(rs, voff, 0);
+    }
+  }
+};
+
+template <int W, int C, int AUX = 0, class Rows = SpanRows>
 __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restrict__ x, int64_t S, int T, int M,
                                                           double thr2, float* __restrict__ z_last,
                                                           float* __restrict__ score, int32_t* __restrict__ n_exceed,
@@ -216,8 +259,7 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
   constexpr int NC = W / C;
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = s < S;
-  const uint32_t voff = active ? (uint32_t)s * 4u : 0u;
-  const uint32_t rowb = (uint32_t)(S * 4);
+  const Rows rows(x, S, T, s, active);
   const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
   StepState st{0.0, 0.0, 0, 0.0, 0.0};
   float ring[W];
@@ -225,15 +267,12 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
   // prologue: rows [0, W) fill the window (requires T > W, checked by the launcher)
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, c * C, T);
+    float tmp[C];
+    rows.template load<C, AUX>(c * C, tmp);
 #pragma unroll
-    for (int j = 0; j < C; ++j) ring[c * C + j] = bload<AUX>(rs, voff, rowb * j);
+    for (int j = 0; j < C; ++j) ring[c * C + j] = tmp[j];
   }
-  {
-    const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, W, T);
-#pragma unroll
-    for (int j = 0; j < C; ++j) cur[j] = bload<AUX>(rs, voff, rowb * j);
-  }
+  rows.template load<C, AUX>(W, cur);
 #pragma unroll
   for (int j = 0; j < W; ++j) {
     const double vd = (double)ring[j];
@@ -245,9 +284,7 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       float nxt[C];
-      const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t0 + (c + 1) * C, T);
-#pragma unroll
-      for (int j = 0; j < C; ++j) nxt[j] = bload<AUX>(rs, voff, rowb * j);
+      rows.template load<C, AUX>(t0 + (c + 1) * C, nxt);
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         step(st, cur[j], ring[c * C + j], Wd, epsB, thr2, false);
@@ -260,11 +297,7 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
   // final block: rows [t0, T), 1..W of them; cur already holds rows [t0, t0 + C)
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    if (c > 0) {
-      const __amdgpu_buffer_rsrc_t rs = chunk_rsrc<C>(x, S, rowb, t0 + c * C, T);
-#pragma unroll
-      for (int j = 0; j < C; ++j) cur[j] = bload<AUX>(rs, voff, rowb * j);
-    }
+    if (c > 0) rows.template load<C, AUX>(t0 + c * C, cur);
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       const int t = t0 + c * C + j;
@@ -365,6 +398,10 @@ __global__ __launch_bounds__(256) void stream_score(const float* __restrict__ xn
   pod_epilogue(st, epsB, s, active, M, delta, xn + sl, S, z_last, score, n_exceed, flags);
 }
 
+int rows_per_chunk(int W) {
+  return W == 60 ? krca::tuning().score_chunk : (W == 30 ? 15 : (W == 20 ? 10 : W));
+}
+bool pipe_window(int W) { return W == 60 || W == 30 || W == 20 || W == 15 || W == 10; }
 }  // namespace
 
 extern "C" {
@@ -409,6 +446,17 @@ int krca_usage_flags(const float* usage, int64_t P, uint8_t* flags, void* stream
   return KRCA_OK;
 }
 
+int krca_rolling_score_variant(int64_t P, int32_t M, int32_t T, int32_t W) {
+  const krca::Tuning& tu = krca::tuning();
+  const int64_t S = P * (int64_t)M;
+  if (!pipe_window(W)) return KRCA_SCORE_REREAD;
+  if (tu.score_impl == KRCA_SCORE_PIPE_ROWS && T > W) return KRCA_SCORE_PIPE_ROWS;  // A/B: forced
+  if (tu.score_impl == 0 && T > W) {
+    return S * 4 * rows_per_chunk(W) < (int64_t(1) << 31) ? KRCA_SCORE_PIPE : KRCA_SCORE_PIPE_ROWS;
+  }
+  return tu.score_impl == 2 && S * 4 * W < (int64_t(1) << 31) ? KRCA_SCORE_RING_BUF : KRCA_SCORE_RING;
+}
+
 int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr, float* z_last,
                        float* score, int32_t* n_exceed, uint8_t* flags, void* stream) {
   KRCA_CHECK_ARG(P >= 0 && T >= 0 && W >= 1, "krca_rolling_score: bad sizes P=%lld T=%d W=%d", (long long)P, T, W);
@@ -416,37 +464,33 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
   if (P == 0) return KRCA_OK;
   KRCA_CHECK_ARG(x && z_last && score && n_exceed && flags, "krca_rolling_score: null pointer");
   const int64_t S = P * (int64_t)M;
+  KRCA_CHECK_ARG(S < (int64_t(1) << 32), "krca_rolling_score: P*M must be < 2^32");
   const double thr2 = (double)z_thr * (double)z_thr;
   const dim3 grid((unsigned)krca::ceil_div(S, 256)), block(256);
   hipStream_t st = krca::as_stream(stream);
-  // A/B switches for kernel development, read per call (0 / 20 = default)
-  const char* e_impl = getenv("KRCA_SCORE_IMPL");
-  const char* e_chunk = getenv("KRCA_SCORE_CHUNK");
-  const int impl = e_impl ? atoi(e_impl) : 0;
-  const int chunk = e_chunk ? atoi(e_chunk) : 20;
   // the metric stream is read once: non-temporal loads (cache policy nt) by default, 6.17 -> 6.61 TB/s
   // at C4 (tools/score_ab.py); KRCA_SCORE_NT=0 restores the default policy
-  const char* e_nt = getenv("KRCA_SCORE_NT");
-  const bool nt = !(e_nt && atoi(e_nt) == 0);
-  KRCA_CHECK_ARG(S < (int64_t(1) << 32), "krca_rolling_score: P*M must be < 2^32");
-  // impl 0: pipelined chunks (needs T > W and C*4*S < 2^31); 1: plain loads; 2: W-block buffer loads
-  const int cw = W == 60 ? chunk : (W == 30 ? 15 : (W == 20 ? 10 : W));  // rows per pipelined chunk
-  const bool fits = T > W && S * 4 * cw < (int64_t(1) << 31);
-#define KRCA_PIPE(WV, CV)                                                                                   \
-  if (nt)                                                                                                   \
-    hipLaunchKernelGGL((rolling_score_pipe<WV, CV, 2>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
-                       n_exceed, flags);                                                                    \
-  else                                                                                                      \
-    hipLaunchKernelGGL((rolling_score_pipe<WV, CV, 0>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
+  const bool nt = krca::tuning().score_nt != 0;
+  const int chunk = rows_per_chunk(W);
+  const int variant = krca_rolling_score_variant(P, M, T, W);
+#define KRCA_PIPE_AS(WV, CV, ROWS)                                                                               \
+  if (nt)                                                                                                        \
+    hipLaunchKernelGGL((rolling_score_pipe<WV, CV, 2, ROWS>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
+                       n_exceed, flags);                                                                         \
+  else                                                                                                           \
+    hipLaunchKernelGGL((rolling_score_pipe<WV, CV, 0, ROWS>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, \
                        n_exceed, flags);
+#define KRCA_PIPE(WV, CV)                                    \
+  if (variant == KRCA_SCORE_PIPE) { KRCA_PIPE_AS(WV, CV, SpanRows) } \
+  else { KRCA_PIPE_AS(WV, CV, BlockRows) }
 #define KRCA_RING(WV)                                                                                         \
-  if (impl == 2 && S * 4 * WV < (int64_t(1) << 31))                                                           \
+  if (variant == KRCA_SCORE_RING_BUF)                                                                         \
     hipLaunchKernelGGL(rolling_score_ring_buf<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score,        \
                        n_exceed, flags);                                                                       \
   else                                                                                                         \
     hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed,  \
                        flags);
-  const bool pipe = impl == 0 && fits;
+  const bool pipe = variant == KRCA_SCORE_PIPE || variant == KRCA_SCORE_PIPE_ROWS;
   switch (W) {
     case 60:
       if (pipe && chunk == 10) { KRCA_PIPE(60, 10) }
@@ -477,6 +521,7 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
                          flags);
   }
 #undef KRCA_PIPE
+#undef KRCA_PIPE_AS
 #undef KRCA_RING
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;

@@ -5,7 +5,8 @@
 //            unrolled insertion network, static register indices), then the workgroup extracts its top-k by k rounds of
 //            a block-wide arg-max over the lanes' list heads (wave shuffles + LDS);
 //   stage 2: one workgroup merges the G*k stage-1 candidates the same way.
-// NaN keys are never selected (ordered below every number).  Bandwidth: one read of v.
+// NaN keys are never selected: they are skipped like the sentinel, so with fewer than k
+// non-NaN keys the missing slots come back as (idx -1, lowest()).  Bandwidth: one read of v.
 #include <float.h>
 
 #include "krca_common.h"
@@ -21,12 +22,12 @@ struct Key;
 template <>
 struct Key<float> {
   __device__ static float lowest() { return -INFINITY; }
-  __device__ static float sanitize(float v) { return v != v ? -INFINITY : v; }
+  __device__ static bool valid(float v) { return v == v; }
 };
 template <>
 struct Key<int64_t> {
   __device__ static int64_t lowest() { return INT64_MIN; }
-  __device__ static int64_t sanitize(int64_t v) { return v; }
+  __device__ static bool valid(int64_t) { return true; }
 };
 
 // a ranks before b
@@ -134,11 +135,11 @@ __global__ __launch_bounds__(TPB) void topk_stage1(const K* __restrict__ v, int6
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       const int64_t j = j0 + u * stride;
-      bv[u] = j < N ? Key<K>::sanitize(v[j]) : Key<K>::lowest();
+      bv[u] = j < N ? v[j] : Key<K>::lowest();
     }
 #pragma unroll
     for (int u = 0; u < BATCH; ++u)
-      if (j0 + u * stride < N) L.insert(bv[u], (int32_t)(j0 + u * stride));
+      if (j0 + u * stride < N && Key<K>::valid(bv[u])) L.insert(bv[u], (int32_t)(j0 + u * stride));
   }
   block_extract<K, KM>(L, k, cv + (int64_t)blockIdx.x * k, ci + (int64_t)blockIdx.x * k);
 }

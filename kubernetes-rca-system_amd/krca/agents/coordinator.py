@@ -3,9 +3,11 @@
 Reference: ref:agents/coordinator.py:7-192.  ``run_analysis`` / the comprehensive result
 schema / ``_correlate_findings`` (group by component, first-seen order, max severity by
 :data:`SEVERITY_ORDER`) / ``_identify_root_causes`` (critical|high with >1 finding) are kept
-exactly.  New, additive: ``ranked_root_causes`` — personalized
-PageRank over the dependency graph, seeded by anomaly scores (bulk path) or by the trace
-backend's per-service error rates (C1 mock), computed by ``krca_ppr`` on the device.
+exactly.  New, additive: ``ranked_root_causes`` — the root-cause ranking
+of krca.rca.Config (the same definition bench.py and RcaStep use: alpha 0.5, p ∝ max(s - 4, 0),
+30 iterations, key r·p) over the dependency graph, seeded by the metrics agent's anomaly scores
+(bulk path) or by the trace backend's per-service error rates (C1 mock; error rates are not in
+|z| units, so that path seeds with floor 0), computed by ``krca_ppr`` on the device.
 """
 import numpy as np
 
@@ -18,12 +20,13 @@ from .traces import TracesAgent
 
 
 class Coordinator:
-    def __init__(self, k8s_client, engine=None, ppr_alpha=0.85, ppr_topk=10):
+    def __init__(self, k8s_client, engine=None, rank_config=None):
+        from krca.rca import RANKING
         self.k8s_client = k8s_client
         self._engine = engine
-        self.ppr_alpha = ppr_alpha
-        self.ppr_topk = ppr_topk
-        self.metrics_agent = MetricsAgent(k8s_client, engine)
+        self.rank_config = rank_config or RANKING
+        self.metrics_agent = MetricsAgent(k8s_client, engine, window=self.rank_config.window,
+                                          z_threshold=self.rank_config.z_threshold)
         self.logs_agent = LogsAgent(k8s_client, engine)
         self.traces_agent = TracesAgent(k8s_client, engine)
         self.topology_agent = TopologyAgent(k8s_client, engine)
@@ -122,10 +125,10 @@ class Coordinator:
         scores = self.metrics_agent.last_scores
         if scores is not None and hasattr(c, 'get_dependency_csr'):
             names, row_ptr, col, outdeg = c.get_dependency_csr(namespace)
-            idx, val = self.engine.rank_root_causes(scores['score'], row_ptr, col, outdeg,
-                                                    alpha=self.ppr_alpha, k=self.ppr_topk)
-            return [{'component': f"Pod/{names[i]}", 'rank': r + 1, 'score': float(v)}
-                    for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]
+            idx, val, rank = self.engine.rank_root_causes(scores['score'], row_ptr, col, outdeg, self.rank_config)
+            sc = np.asarray(scores['score'].cpu() if hasattr(scores['score'], 'cpu') else scores['score'])
+            return [{'component': f"Pod/{names[i]}", 'rank': r + 1, 'score': float(v), 'pagerank': float(rank[i]),
+                     'anomaly': float(sc[i])} for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]
         if hasattr(c, 'get_service_dependencies') and hasattr(c, 'get_error_rate_by_service'):
             deps = c.get_service_dependencies()
             rates = c.get_error_rate_by_service()
@@ -141,8 +144,8 @@ class Coordinator:
             seed = np.array([rates.get(n, 0.0) for n in names], dtype=np.float32)
             if not seed.sum() > 0:
                 return None
-            k = min(self.ppr_topk, len(names))
-            idx, val = self.engine.rank_root_causes(seed, row_ptr, col, outdeg, alpha=self.ppr_alpha, k=k)
-            return [{'component': f"Service/{names[i]}", 'rank': r + 1, 'score': float(v)}
-                    for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]
+            idx, val, rank = self.engine.rank_root_causes(seed, row_ptr, col, outdeg,
+                                                          self.rank_config.replace(seed_floor=0.0))
+            return [{'component': f"Service/{names[i]}", 'rank': r + 1, 'score': float(v), 'pagerank': float(rank[i]),
+                     'anomaly': float(seed[i])} for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]
         return None

@@ -43,11 +43,8 @@ class TorchComm:
         self.world, self.rank, self.group = world, rank, group
 
     def all_gather(self, out, inp):
-        import torch.distributed as dist
-        try:
-            dist.all_gather_into_tensor(out, inp, group=self.group)
-        except (RuntimeError, AttributeError):  # gloo builds without all_gather_into_tensor
-            dist.all_gather(list(out.view(self.world, -1).unbind(0)), inp, group=self.group)
+        from .rca import all_gather_flat
+        all_gather_flat(out, inp, self.world, self.group)
 
     def all_reduce_sum(self, t):
         import torch.distributed as dist

@@ -179,3 +179,23 @@ class MockK8sClient:
 
     def are_traces_available(self):
         return True
+
+
+class MeshClient(MockK8sClient):
+    """The mock cluster with a synthetic pod mesh behind the bulk accessors:
+    ``get_pod_metric_tensor`` serves the [T][P][M] metric tensor (device or host) and
+    ``get_dependency_csr`` the pull-CSR of the mesh (krca.synth.Mesh), so the Coordinator's
+    comprehensive run scores the mesh and ranks its pods; the dict methods keep serving the C1
+    objects.  Used to check that ``ranked_root_causes`` equals the bench / RcaStep ranking."""
+
+    def __init__(self, mesh, x, names=None, **kw):
+        super().__init__(**kw)
+        self.mesh, self.x = mesh, x
+        self._mesh_names = names
+
+    def get_pod_metric_tensor(self, namespace):
+        return (self._mesh_names or self.mesh.names()), self.x
+
+    def get_dependency_csr(self, namespace):
+        m = self.mesh
+        return (self._mesh_names or m.names()), m.row_ptr, m.col, m.outdeg

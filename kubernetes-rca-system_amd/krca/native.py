@@ -23,6 +23,9 @@ SIGNATURES = {
     "krca_version": (c_i32, []),
     "krca_last_error": (ctypes.c_char_p, []),
     "krca_device_count": (c_i32, [ctypes.POINTER(ctypes.c_int)]),
+    "krca_tune_set": (c_i32, [ctypes.c_char_p, c_i32]),
+    "krca_tune_get": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32)]),
+    "krca_rolling_score_variant": (c_i32, [c_i64, c_i32, c_i32, c_i32]),
     "krca_usage_flags": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_rolling_score": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_stream_state_size": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
@@ -88,6 +91,7 @@ SIGNATURES = {
 }
 
 KRCA_ENOTCONV = -70
+SCORE_VARIANTS = {0: "pipe", 1: "ring", 2: "ring_buf", 3: "reread", 4: "pipe_rows"}  # krca_rolling_score_variant
 
 
 class KrcaError(RuntimeError):
@@ -110,15 +114,48 @@ def load_library(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if path is None:
+    if path is None or _lib is None:
         _lib = lib
     return lib
 
 
-def _check(rc, what):
+def _check(rc, what, lib=None):
+    """Raise KrcaError with krca_last_error() of the library that failed (thread-local message)."""
     if rc != 0:
-        msg = _lib.krca_last_error().decode(errors="replace")
+        src = lib if lib is not None else _lib
+        msg = src.krca_last_error().decode(errors="replace") if src is not None else "(library not loaded)"
         raise KrcaError(f"{what} failed ({rc}): {msg}")
+
+
+class tune:
+    """Context manager over the library's A/B knobs (include/krca.h krca_tune_set), e.g.
+    ``with native.tune(KRCA_SCORE_IMPL=1): ...``; the previous values are restored on exit."""
+
+    def __init__(self, lib=None, **knobs):
+        self.lib = lib or load_library()
+        self.knobs = knobs
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            old = c_i32(0)
+            _check(self.lib.krca_tune_get(k.encode(), ctypes.byref(old)), "krca_tune_get", self.lib)
+            self.saved[k] = old.value
+            _check(self.lib.krca_tune_set(k.encode(), int(v)), "krca_tune_set", self.lib)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            self.lib.krca_tune_set(k.encode(), int(v))
+        return False
+
+
+def check_doc_off(doc_off, nbytes):
+    """The container-offset contract of krca_log_index / krca_log_match (include/krca.h):
+    doc_off[0] == 0, doc_off[-1] == nbytes, non-decreasing.  Host array -> raises KrcaError."""
+    doc_off = np.asarray(doc_off)
+    if len(doc_off) < 2 or doc_off[0] != 0 or doc_off[-1] != nbytes or np.any(np.diff(doc_off) < 0):
+        raise KrcaError("log scan: doc_off must be non-decreasing from 0 to len(text)")
 
 
 class LogScan:
@@ -358,11 +395,18 @@ class NativeEngine:
         return idx.cpu().numpy(), val.cpu().numpy()
 
     # -- a12 ---------------------------------------------------------------------------------
-    def log_scan_device(self, text, doc_off):
-        """text uint8 device tensor (16-byte aligned), doc_off int64 device tensor [D+1]."""
+    def log_scan_device(self, text, doc_off, validate=True):
+        """text uint8 device tensor (16-byte aligned), doc_off int64 device tensor [D+1].
+        validate: check the doc_off contract on the device first (one stream sync); pass False only
+        when the offsets were checked on the host (check_doc_off) before the upload."""
         torch = self.torch
         nbytes = text.numel()
         D = doc_off.numel() - 1
+        if validate:
+            ok = D >= 1 and bool(((doc_off[0] == 0) & (doc_off[-1] == nbytes) &
+                                  (doc_off[1:] >= doc_off[:-1]).all()).item())
+            if not ok:
+                raise KrcaError("log scan: doc_off must be non-decreasing from 0 to len(text)")
         ws = self._workspace("logidx", 8 * self.lib.krca_log_index_size(nbytes))
         nl = torch.zeros(1, dtype=torch.int64, device=self.device)
         st = self._stream()
@@ -421,7 +465,8 @@ class NativeEngine:
     def template_hist(self, blob, doc_off):
         """-> list (per container) of [(hash uint64, count)] in ascending hash order."""
         doc_off = np.asarray(doc_off, dtype=np.int64)
-        scan = self.log_scan_device(self.upload_blob(blob), self._dev(doc_off))
+        check_doc_off(doc_off, len(blob))
+        scan = self.log_scan_device(self.upload_blob(blob), self._dev(doc_off), validate=False)
         r = self.template_hist_device(scan)
         d0 = scan["doc_line0"].cpu().numpy()
         nt = r["n_templates"].cpu().numpy()
@@ -478,11 +523,10 @@ class NativeEngine:
     def log_scan(self, blob, doc_off):
         torch = self.torch
         doc_off = np.asarray(doc_off, dtype=np.int64)
-        if len(doc_off) < 2 or doc_off[0] != 0 or doc_off[-1] != len(blob) or np.any(np.diff(doc_off) < 0):
-            raise KrcaError("log_scan: doc_off must be monotone from 0 to len(blob)")
+        check_doc_off(doc_off, len(blob))
         text = self.upload_blob(blob)
         off = self._dev(doc_off)
-        r = self.log_scan_device(text, off)
+        r = self.log_scan_device(text, off, validate=False)
         ex = r["examples"].cpu().numpy()
         ids = np.unique(ex[ex >= 0]).astype(np.int64)
         starts, ends = {}, {}
@@ -522,21 +566,37 @@ class NativeEngine:
         return r_out, r_fixed, q, iters.value
 
     def ppr(self, row_ptr, col, outdeg, seed, alpha=0.85, max_iter=100, tol=1e-6, seed_floor=0.0):
+        """networkx-compatible PageRank (defaults = nx.pagerank's): (r float32, r_fixed int64, iters)."""
+        r, rf, q, iters = self._ppr_full(row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor)
+        return r, rf, iters
+
+    def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None):
+        """The root-cause ranking of krca.rca.Config (the same definition as RcaStep / bench.py):
+        seeded PageRank (cfg.alpha, cfg.seed_floor, cfg.iters / cfg.tol), key r_i * q_i, top-k.
+        Returns host (idx int32 [k], score float64 [k] = r_i * p_i, r float64 [N] PageRank mass)."""
+        from .rca import RANKING
+        cfg = cfg or RANKING
+        torch = self.torch
+        k = min(int(k or cfg.k), len(outdeg))
+        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol, cfg.seed_floor)
+        key = torch.empty_like(rf)
+        _check(self.lib.krca_ppr_rca_key(self.ptr(rf), self.ptr(q), rf.numel(), self.ptr(key), self._stream()),
+               "krca_ppr_rca_key")
+        idx, _ = self.topk_device(key, k)
+        idx = idx.cpu().numpy()
+        qt = int(q.sum().item())
+        rr = rf.cpu().numpy().astype(np.float64) / 2.0 ** 60
+        qs = q.cpu().numpy()[idx].astype(np.float64)
+        p = qs / qt if qt > 0 else np.full(len(idx), 1.0 / len(outdeg))
+        return idx, rr[idx] * p, rr
+
+    def _ppr_full(self, row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor):
         torch = self.torch
         rp_host = np.asarray(row_ptr, dtype=np.int64)
         plan, n = self.ppr_plan(rp_host)
         sd = self._dev(seed, torch.float32) if isinstance(seed, torch.Tensor) else self._dev(np.asarray(seed, np.float32))
-        r, rf, q, iters = self.ppr_device(self._dev(rp_host), self._dev(np.asarray(col, np.int32)),
-                                          self._dev(np.asarray(outdeg, np.int32)), plan, n, sd, alpha, max_iter, tol,
-                                          seed_floor)
-        return r, rf, iters
-
-    def rank_root_causes(self, seed, row_ptr, col, outdeg, alpha=0.85, k=10, max_iter=100, tol=1e-6):
-        """nx-compatible PageRank ranking (C1 / agent path): top-k of the rank itself."""
-        r, rf, _ = self.ppr(row_ptr, col, outdeg, seed, alpha, max_iter, tol)
-        idx, _ = self.topk_device(rf, k)
-        idx = idx.cpu().numpy()
-        return idx, r.cpu().numpy()[idx]
+        return self.ppr_device(self._dev(rp_host), self._dev(np.asarray(col, np.int32)),
+                               self._dev(np.asarray(outdeg, np.int32)), plan, n, sd, alpha, max_iter, tol, seed_floor)
 
 
 _default = None

@@ -42,6 +42,20 @@ def shard_graph(row_ptr, col, outdeg, lo, hi):
 
 
 class Config:
+    """The one root-cause ranking definition ("Ranking"), shared by bench.py,
+    :class:`RcaStep`, the streaming replay and ``Coordinator.ranked_root_causes``:
+
+    * rolling z-scores over a trailing window of `window` steps, exceedance at |z| > z_threshold;
+    * personalized PageRank (networkx 3.4.2 semantics) with damping `alpha` = 0.5 and
+      personalization p_i ∝ max(s_i - seed_floor, 0), s_i = the pod's max |z| at the last step
+      (seed_floor is in |z| units: only pods past 4 sigma seed the walk);
+    * `iters` = 30 fixed iterations (tol = 0): at alpha = 0.5 that is within 1e-10 (L1) of the
+      converged vector, so the result is networkx's converged PageRank (pinned at 2k / 20k nodes,
+      tests/golden/ppr_nx_meshes.npz);
+    * pods ranked by the key r_i * p_i (propagated mass times own anomaly), top `k`, ties -> lower
+      index.  Ranking by r alone sends the mass to the dependency sinks below the faulty pods
+      (measured recall of the planted roots: DESIGN.md §3.2)."""
+
     def __init__(self, window=60, z_threshold=3.0, seed_floor=4.0, alpha=0.5, iters=30, tol=0.0, k=10):
         self.window = window
         self.z_threshold = z_threshold
@@ -54,6 +68,14 @@ class Config:
     def as_dict(self):
         return dict(window=self.window, z_threshold=self.z_threshold, seed_floor=self.seed_floor, alpha=self.alpha,
                     iters=self.iters, tol=self.tol, k=self.k)
+
+    def replace(self, **kw):
+        d = self.as_dict()
+        d.update(kw)
+        return Config(**d)
+
+
+RANKING = Config()
 
 
 class Comm:
@@ -74,11 +96,18 @@ class Comm:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             return
-        import torch.distributed as dist
-        try:
-            dist.all_gather_into_tensor(out, inp, group=self.group)
-        except (RuntimeError, AttributeError):  # gloo builds without all_gather_into_tensor
-            dist.all_gather(list(out.view(self.world, -1).unbind(0)), inp, group=self.group)
+        all_gather_flat(out, inp, self.world, self.group)
+
+
+def all_gather_flat(out, inp, world, group=None):
+    """out[world * inp.numel()] <- every rank's inp.  RCCL ("nccl") gathers into the flat tensor
+    directly; gloo has no all_gather_into_tensor, so it takes the list form.  Chosen once from the
+    backend, so a real RCCL failure (timeout, size mismatch) propagates instead of being retried."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(list(out.view(world, -1).unbind(0)), inp, group=group)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
 
 
 class DeviceShard:

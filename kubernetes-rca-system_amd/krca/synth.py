@@ -62,7 +62,12 @@ def _services_ba(n_services, m, rng):
     return np.asarray(src, np.int64), np.asarray(dst, np.int64)
 
 
-def make_graph(n_pods, avg_degree=20, service_size=20, seed=0, n_roots=10, m_services=4):
+def make_graph(n_pods, avg_degree=20, service_size=20, seed=0, n_roots=10, m_services=4, n_edges=None):
+    """Pull-CSR mesh with exactly `n_edges` distinct caller -> callee edges (default
+    avg_degree * n_pods; the BASELINE shapes: C2 10k pods / 200k edges, C4 1M / 20M).  Edges are
+    drawn per pod (Poisson out-degree) from its service's callee services, deduplicated, topped up
+    in further seeded rounds until the target is reached, then a seeded random subset of the
+    surplus is dropped.  Pods of callee-less services (the first m_services) call nobody."""
     rng = np.random.default_rng(seed)
     n_srv = max(1, math.ceil(n_pods / service_size))
     s_src, s_dst = _services_ba(n_srv, m_services, rng)
@@ -73,19 +78,37 @@ def make_graph(n_pods, avg_degree=20, service_size=20, seed=0, n_roots=10, m_ser
     np.cumsum(np.bincount(s_src, minlength=n_srv), out=cptr[1:])
     pod_srv = np.arange(n_pods, dtype=np.int64) // service_size
     ncallee = (cptr[1:] - cptr[:-1])[pod_srv]
-    deg = rng.poisson(avg_degree, n_pods).astype(np.int64)
-    deg[ncallee == 0] = 0
-    src = np.repeat(np.arange(n_pods, dtype=np.int64), deg)
-    k = rng.integers(0, np.iinfo(np.int64).max, len(src)) % np.repeat(np.maximum(ncallee, 1), deg)
-    tsrv = callee[cptr[pod_srv[src]] + k]
-    lo = tsrv * service_size
-    hi = np.minimum(lo + service_size, n_pods)
-    dst = lo + rng.integers(0, np.iinfo(np.int64).max, len(src)) % (hi - lo)
-    keep = src != dst
-    key = np.unique(src[keep] * n_pods + dst[keep])
+    callers = np.flatnonzero(ncallee > 0)
+    target = int(round(avg_degree * n_pods)) if n_edges is None else int(n_edges)
+    # capacity: a pod can call every pod of its callee services except itself
+    srv_pods = np.minimum((np.arange(n_srv) + 1) * service_size, n_pods) - np.arange(n_srv) * service_size
+    cap_srv = np.zeros(n_srv, np.int64)
+    np.add.at(cap_srv, s_src, srv_pods[s_dst])
+    target = min(target, int(cap_srv[pod_srv[callers]].sum()))
+    key = np.zeros(0, np.int64)
+    eff = 0.85  # new distinct edges per drawn edge (re-estimated every round)
+    for _ in range(64):
+        need = target - len(key)
+        if need <= 0:
+            break
+        draw = need / max(eff, 0.05) * 1.05 + 16
+        deg = rng.poisson(draw / max(len(callers), 1), len(callers)).astype(np.int64)
+        src = np.repeat(callers, deg)
+        k = rng.integers(0, np.iinfo(np.int64).max, len(src)) % np.repeat(ncallee[callers], deg)
+        tsrv = callee[cptr[pod_srv[src]] + k]
+        lo = tsrv * service_size
+        hi = np.minimum(lo + service_size, n_pods)
+        dst = lo + rng.integers(0, np.iinfo(np.int64).max, len(src)) % (hi - lo)
+        keep = src != dst
+        n0 = len(key)
+        key = np.union1d(key, src[keep] * n_pods + dst[keep])
+        eff = (len(key) - n0) / max(len(src), 1)
+    if len(key) > target:  # drop a seeded random subset of the surplus
+        key = np.delete(key, rng.choice(len(key), size=len(key) - target, replace=False))
     src, dst = key // n_pods, key % n_pods
-    order = np.lexsort((src, dst))  # rows by destination, callers ascending inside a row
-    col = src[order].astype(np.int32)
+    pull = np.sort(dst * n_pods + src)  # rows by destination, callers ascending inside a row
+    col = (pull % n_pods).astype(np.int32)
+    del pull
     row_ptr = np.zeros(n_pods + 1, np.int64)
     np.cumsum(np.bincount(dst, minlength=n_pods), out=row_ptr[1:])
     outdeg = np.bincount(src, minlength=n_pods).astype(np.int32)

@@ -2,7 +2,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+for p in (os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests"),
+          os.path.join(ROOT, "tests", "golden"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 

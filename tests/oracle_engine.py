@@ -47,11 +47,18 @@ class OracleEngine:
         docs = [blob[doc_off[i]:doc_off[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(doc_off) - 1)]
         return OracleLogScan(docs)
 
-    def rank_root_causes(self, seed, row_ptr, col, outdeg, alpha=0.85, k=10, max_iter=100, tol=1e-6):
+    def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None):
+        from krca.rca import RANKING
+        cfg = cfg or RANKING
         seed = np.asarray(seed.cpu() if hasattr(seed, "cpu") else seed, np.float32)
-        rf, r, _ = oracle.c_ppr(row_ptr, col, outdeg, seed, alpha, max_iter, tol)
-        idx, _ = oracle.topk_ref(r, k)
-        return idx, rf[idx]
+        k = min(int(k or cfg.k), len(outdeg))
+        rf, r, _, q = oracle.c_ppr(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol, cfg.seed_floor,
+                                   return_q=True)
+        idx, _ = oracle.topk_ref(oracle.c_rca_key(r, q), k)
+        rr = r.astype(np.float64) / 2.0 ** 60
+        qt = int(q.sum())
+        p = q[idx].astype(np.float64) / qt if qt > 0 else np.full(len(idx), 1.0 / len(outdeg))
+        return idx, rr[idx] * p, rr
 
     def pod_classify(self, pod_code, cont_off, cont_code):
         return oracle.pod_classify_ref(pod_code, cont_off, cont_code)

@@ -85,3 +85,22 @@ def test_corr_shard_ranges_tile_aligned_and_cover():
     lib = native.load_library()
     assert lib.krca_corr_shard_ws_size(100_000, 1440, 10, 12_544, 8) > lib.krca_corr_shard_ws_size(100_000, 1440, 10,
                                                                                                      0, 8)
+
+
+def test_tuning_knobs_and_score_variant():
+    """A/B knobs are read once at load and changed only through krca_tune_set; the scoring variant
+    query reports the pipelined kernel at C4 and the per-row-descriptor form past 2^31 bytes."""
+    lib = native.load_library()
+    v = ctypes.c_int32(-1)
+    assert lib.krca_tune_get(b"KRCA_SCORE_IMPL", ctypes.byref(v)) == 0 and v.value == 0
+    assert lib.krca_tune_set(b"NO_SUCH_KNOB", 1) != 0
+    assert b"NO_SUCH_KNOB" in lib.krca_last_error()
+    assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1_000_000, 8, 1440, 60)] == "pipe"
+    assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(4_000_000, 8, 1440, 60)] == "pipe_rows"
+    assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 50, 60)] == "ring"    # T <= W
+    assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 500, 7)] == "reread"  # any W
+    with native.tune(lib, KRCA_SCORE_IMPL=2):
+        assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 1440, 60)] == "ring_buf"
+    with native.tune(lib, KRCA_SCORE_IMPL=4):
+        assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 1440, 60)] == "pipe_rows"
+    assert lib.krca_tune_get(b"KRCA_SCORE_IMPL", ctypes.byref(v)) == 0 and v.value == 0  # restored

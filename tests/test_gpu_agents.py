@@ -74,7 +74,7 @@ def test_pod_classify_columnar_scale(eng, P):
 def test_ranked_root_causes_c1(eng):
     res = A.Coordinator(A.Shim(), engine=eng).run_analysis("comprehensive", A.NS)
     assert [r["component"] for r in res["ranked_root_causes"]] == [
-        "Service/database", "Service/backend", "Service/api-gateway", "Service/resource-service", "Service/frontend"]
+        "Service/api-gateway", "Service/database", "Service/backend", "Service/resource-service", "Service/frontend"]
 
 
 def test_default_engine_is_native():

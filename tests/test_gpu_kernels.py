@@ -52,7 +52,7 @@ def test_rolling_score_vs_oracle(eng, P, M, T, W):
     assert np.allclose(z, zl, rtol=1e-5, atol=1e-5)
 
 
-SCORE_VARIANTS = [("2", "20"), ("1", "20")] + [("0", c) for c in ("10", "12", "15", "20", "30")]
+SCORE_VARIANTS = [("2", "20"), ("1", "20"), ("4", "20"), ("4", "15")] + [("0", c) for c in ("10", "12", "15", "20", "30")]
 
 
 @pytest.mark.parametrize("P,M,T,W", [(1000, 8, 1440, 60), (128, 8, 61, 60), (129, 8, 139, 60), (700, 8, 200, 30)])
@@ -63,9 +63,8 @@ def test_rolling_score_kernel_variants_bit_exact(eng, monkeypatch, P, M, T, W):
     xd = x.cuda()
     z0 = None
     for impl, chunk in SCORE_VARIANTS:
-        monkeypatch.setenv("KRCA_SCORE_IMPL", impl)
-        monkeypatch.setenv("KRCA_SCORE_CHUNK", chunk)
-        got = eng.rolling_score(xd, window=W, z_threshold=3.0)
+        with native.tune(eng.lib, KRCA_SCORE_IMPL=int(impl), KRCA_SCORE_CHUNK=int(chunk)):
+            got = eng.rolling_score(xd, window=W, z_threshold=3.0)
         assert np.array_equal(got["n_exceed_host"], ref["n_exceed"]), (impl, chunk)
         assert np.array_equal(got["flags"], ref["flags"]), (impl, chunk)
         z = got["z_last"].cpu().numpy()
@@ -105,6 +104,14 @@ def test_topk_nan_never_selected(eng):
     v[[3, 4000]] = [1.0, 2.0]
     idx, val = eng.topk(torch.from_numpy(v), 2)
     assert idx.tolist() == [4000, 3]
+    # fewer than k non-NaN keys: the rest are the sentinel, never a NaN entry
+    idx, val = eng.topk(torch.from_numpy(v), 5)
+    assert idx.tolist() == [4000, 3, -1, -1, -1]
+    assert val[:2].tolist() == [2.0, 1.0] and np.all(np.isneginf(val[2:]))
+    w = np.full(300, np.nan, np.float32)
+    w[7] = -np.inf  # a real -inf key still beats the sentinel
+    idx, val = eng.topk(torch.from_numpy(w), 3)
+    assert idx.tolist() == [7, -1, -1]
 
 
 # ---- a12 log histograms ----------------------------------------------------------------------
@@ -151,6 +158,33 @@ def test_log_scan_boundaries(eng):
     _check_docs(eng, docs)
 
 
+def test_log_scan_container_starts_at_tile_boundaries(eng):
+    """Container starts placed exactly at 64 KiB tile boundaries (k*65536) and one byte before
+    (k*65536-1), with \r / \n / CRLF pairs split across the container edge and empty containers
+    there: log_count / log_lines read the container starts of a tile (and the byte at tile0-1)
+    from a per-tile LDS bitmap."""
+    TILE = 65536
+    tails = ["\r", "x\r", "Error\n", "", "timeout"]
+    heads = ["\nKilled", "\n", "\r\npanic:", "ERROR", "", "\x85z"]
+    docs, pos, k = [], 0, 1
+    for i in range(24):
+        target = k * TILE - (i % 2)  # even i: start at the boundary, odd: one byte before it
+        tail = tails[i % len(tails)]
+        fill = target - pos - len(tail.encode())
+        if fill < 0:
+            k += 1
+            continue
+        docs.append("a" * max(fill - 1, 0) + (" " if fill else "") + tail)
+        pos += len(docs[-1].encode())
+        assert pos == target
+        if i % 3 == 0:
+            docs += ["", ""]  # empty containers at the boundary
+        docs.append(heads[i % len(heads)] + " Error timeout")
+        pos += len(docs[-1].encode())
+        k += 1
+    _check_docs(eng, docs)
+
+
 def test_log_scan_impls_identical(eng, monkeypatch):
     """The line-index + DFA-lane path (default) and the chunk-lane path (KRCA_LOG_IMPL=1) give the
     same line offsets, masks, histograms and examples, long lines (> 1 KiB, a wave each) included."""
@@ -164,13 +198,12 @@ def test_log_scan_impls_identical(eng, monkeypatch):
     tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
     out = {}
     for impl in ("0", "1"):
-        monkeypatch.setenv("KRCA_LOG_IMPL", impl)
-        r = eng.log_scan_device(tb, toff)
-        out[impl] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
+        with native.tune(eng.lib, KRCA_LOG_IMPL=int(impl)):
+            r = eng.log_scan_device(tb, toff)
+            out[impl] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
     assert out["0"].keys() == out["1"].keys()
     for k in out["0"]:
         assert np.array_equal(out["0"][k], out["1"][k]), k
-    monkeypatch.setenv("KRCA_LOG_IMPL", "0")
     _check_docs(eng, docs)
 
 

@@ -1,0 +1,164 @@
+"""BASELINE configs at their stated shapes on an MI355X, through the C-ABI, against the oracle:
+
+* the one ranking definition (krca.rca.Config) pinned to networkx 3.4.2 at 2k / 20k nodes, and
+  the same top-10 from the bench path (RcaStep) and from Coordinator.ranked_root_causes;
+* C2-mini (SURVEY.md §8c golden #7) for a5 / a9 / a10 / a12 / a13;
+* C2: the full RCA step at 10k pods / 200k edges, 8 metrics x 1440 steps;
+* C4: the full RCA step at 1M pods / 20M edges, 8 x 1440 (46 GB resident).
+Integer outputs bit-exact, float scores within 1e-5 relative, top-k identical."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN
+from krca import native, synth
+from krca.rca import RANKING, Comm, DeviceShard, RcaStep, shard_graph, shard_range
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return native.NativeEngine()
+
+
+def _csr(edges, n):
+    src, dst = edges[:, 0].astype(np.int64), edges[:, 1].astype(np.int64)
+    o = np.lexsort((src, dst))
+    rp = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(dst, minlength=n), out=rp[1:])
+    return rp, src[o].astype(np.int32), np.bincount(src, minlength=n).astype(np.int32)
+
+
+def _rca_from_scores(eng, rp, col, od, score, cfg=RANKING):
+    """The bench path (DeviceShard + RcaStep on one rank) seeded with given scores."""
+    n = len(od)
+    sh = DeviceShard(eng, None, rp, col, od, n, n, 1, cfg)
+    sh.score_out = {"score": torch.from_numpy(np.ascontiguousarray(score, np.float32)).cuda()}
+    st = RcaStep(sh, Comm(), cfg, 0)
+    st.propagate()
+    idx, _ = st.merge(*sh.local_topk(cfg.k))
+    return [int(i) for i in idx], sh.r[:n].cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["m2k", "m20k"])
+def test_ranking_pinned_to_networkx(eng, name):
+    g = np.load(os.path.join(GOLDEN, "ppr_nx_meshes.npz"))
+    e, s, ref = g[f"{name}_edges"], g[f"{name}_seed"], g[f"{name}_rank"]
+    n = len(s)
+    rp, col, od = _csr(e, n)
+    idx, val, r = eng.rank_root_causes(s, rp, col, od)          # the Coordinator's entry point
+    big = ref >= 1e-12
+    assert np.max(np.abs(r[big] - ref[big]) / ref[big]) < 1e-5
+    assert np.max(np.abs(r[~big] - ref[~big])) < 1e-12
+    assert idx.tolist() == g[f"{name}_top10"].tolist()
+    top, rfix = _rca_from_scores(eng, rp, col, od, s)           # the bench / RcaStep path
+    assert top == g[f"{name}_top10"].tolist()
+    assert np.array_equal(rfix.astype(np.float64) / 2.0 ** 60, r)  # same fixed point
+
+
+def test_coordinator_ranking_equals_bench_path(eng):
+    """Coordinator.run_analysis('comprehensive') on a mesh client ranks exactly as RcaStep does."""
+    from krca.agents.coordinator import Coordinator
+    from krca.mock import MeshClient
+    n = 10_000
+    m = synth.make_graph(n, n_edges=200_000, seed=4)
+    x = synth.make_metrics(n, 8, 1440, seed=4, roots=m.roots, hop_sets=synth.caller_hops(m, m.roots)).cuda()
+    res = Coordinator(MeshClient(m, x), engine=eng).run_analysis("comprehensive", "test-microservices")
+    got = [int(r["component"].split("-")[-1]) for r in res["ranked_root_causes"]]
+    lo, hi, n_max = shard_range(n, 1, 0)
+    step = RcaStep(DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi), n, n_max, 1, RANKING),
+                   Comm(), RANKING, 0)
+    idx, _ = step.run()
+    assert got == [int(i) for i in idx]
+
+
+def test_c2mini_golden(eng):
+    import c2mini as C
+    g = np.load(os.path.join(GOLDEN, "c2mini.npz"))
+    e, x, blob, off = C.inputs()
+    assert C.sha(e, x, off) == str(g["sha"])
+    # a5
+    got = eng.rolling_score(torch.from_numpy(x).cuda(), window=C.W)
+    assert np.array_equal(got["n_exceed_host"], g["n_exceed"]) and np.array_equal(got["flags"], g["flags"])
+    assert np.array_equal(got["score"].cpu().numpy(), g["score"])  # same arithmetic as the C twin
+    assert np.allclose(got["z_last"].cpu().numpy(), g["z_last_f64"], rtol=1e-5, atol=1e-5)
+    # a10 (networkx-pinned ranking definition)
+    rp, col, od = _csr(e, C.P)
+    idx, _, r = eng.rank_root_causes(g["score"], rp, col, od)
+    assert idx.tolist() == g["ppr_top10"].tolist()
+    big = g["ppr_rank"] >= 1e-12
+    assert np.max(np.abs(r[big] - g["ppr_rank"][big]) / g["ppr_rank"][big]) < 1e-5
+    # a9: top-10 sets where the float64 gap to the 11th is beyond the screening epsilon
+    c = eng.corr_topk(torch.from_numpy(x).cuda(), k=10, tau=0.5)
+    eps = eng.lib.krca_corr_eps(C.T)
+    sure = g["corr_gap"] > 2 * eps
+    assert sure.mean() > 0.5
+    assert np.array_equal(np.sort(c["idx"][sure], 1), np.sort(g["corr_idx"][sure], 1))
+    ok = c["idx"] == g["corr_idx"]
+    assert np.allclose(c["val"][ok], g["corr_r"][ok], rtol=1e-5, atol=1e-6)
+    assert np.array_equal(c["count"], g["corr_count"])
+    # a12: reference-pattern histograms
+    scan = eng.log_scan(blob, off)
+    assert np.array_equal(scan.n_lines, g["log_lines"]) and np.array_equal(scan.hist, g["log_hist"])
+    # a13
+    th = eng.template_hist(blob, off)
+    flat = [(d, h, c_) for d, lst in enumerate(th) for h, c_ in lst]
+    assert [f[0] for f in flat] == g["tmpl_doc"].tolist()
+    assert [f[1] for f in flat] == g["tmpl_hash"].tolist()
+    assert [f[2] for f in flat] == g["tmpl_count"].tolist()
+
+
+def test_c2_full_rca_step(eng):
+    """C2 (BASELINE configs[1]): 10k pods / 200k edges, 8 x 1440; scores of every pod, PageRank
+    fixed point and top-10 against the C oracle."""
+    n = 10_000
+    m = synth.make_graph(n, n_edges=200_000, seed=0)
+    assert m.n_edges == 200_000
+    x = synth.make_metrics(n, 8, 1440, seed=0, roots=m.roots, hop_sets=synth.caller_hops(m, m.roots))
+    lo, hi, n_max = shard_range(n, 1, 0)
+    step = RcaStep(DeviceShard(eng, x.cuda(), *shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi), n, n_max, 1, RANKING),
+                   Comm(), RANKING, 0)
+    idx, _ = step.run()
+    ref = oracle.c_rolling_score(x.numpy(), RANKING.window)
+    so = step.s.score_out
+    assert np.array_equal(so["n_exceed"].cpu().numpy(), ref["n_exceed"])
+    assert np.array_equal(so["flags"].cpu().numpy(), ref["flags"])
+    assert np.array_equal(so["score"].cpu().numpy(), ref["score"])
+    assert np.allclose(so["z_last"].cpu().numpy(), ref["z_last"], rtol=1e-5, atol=1e-6)
+    ridx, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, ref["score"], RANKING.alpha, RANKING.iters,
+                                 RANKING.seed_floor, RANKING.k)
+    assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
+    assert [int(i) for i in idx] == ridx.tolist()
+    assert len(set(ridx.tolist()) & set(m.roots.tolist())) >= 8
+
+
+def test_c4_full_rca_step_1m_pods(eng):
+    """C4 (BASELINE configs[3]) on one device: 1M pods / 20M edges, 8 x 1440 (46 GB of metrics).
+    PageRank fixed point of all 1M pods and the top-10 bit-identical to the C oracle; scores of
+    a 20k-pod sample bit-exact."""
+    n = 1_000_000
+    m = synth.make_graph(n, n_edges=20_000_000, seed=0)
+    assert m.n_edges == 20_000_000
+    hops = synth.caller_hops(m, m.roots)
+    x = synth.make_metrics_range(0, n, 8, 1440, seed=0, roots=m.roots, hop_sets=hops, device=torch.device("cuda"))
+    lo, hi, n_max = shard_range(n, 1, 0)
+    step = RcaStep(DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi), n, n_max, 1, RANKING),
+                   Comm(), RANKING, 0)
+    idx, _ = step.run()
+    score = step.s.score_out["score"].cpu().numpy()
+    samp = np.sort(np.random.default_rng(0).choice(n, 20_000, replace=False))
+    sel = torch.from_numpy(samp).cuda()
+    ref = oracle.c_rolling_score(x[:, sel, :].cpu().numpy(), RANKING.window)
+    assert np.array_equal(step.s.score_out["n_exceed"][sel].cpu().numpy(), ref["n_exceed"])
+    assert np.array_equal(step.s.score_out["flags"][sel].cpu().numpy(), ref["flags"])
+    assert np.array_equal(score[samp], ref["score"])
+    ridx, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, RANKING.alpha, RANKING.iters,
+                                 RANKING.seed_floor, RANKING.k)
+    assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
+    assert [int(i) for i in idx] == ridx.tolist()
+    del x
+    torch.cuda.empty_cache()
