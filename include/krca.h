@@ -44,7 +44,7 @@ int krca_version(void);
 const char* krca_last_error(void);
 int krca_device_count(int* n_host);
 
-/* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID,
+/* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID, KRCA_PPR_DICT,
  * KRCA_LOG_IMPL, KRCA_GROUP_IMPL, KRCA_CORR_DEBUG.  Initialised once from the environment variables
  * of the same names when the library loads; launchers never call getenv.  Process-global, not
  * thread-safe (set them before launching work).  Unknown names: KRCA_EINVAL. */
@@ -93,6 +93,12 @@ int krca_rolling_score_variant(int64_t P, int32_t M, int32_t T, int32_t W);
  *                   there) per line start/end byte offsets and 13-bit mask; per container the line
  *                   count, the 13-bin histogram and the first three matching line ids per bin
  *                   (-1 when fewer) — atomics-free segmented reduction. */
+/* The compiled matcher's identity: the Unicode version of the interpreter that generated the
+ * tables (re.IGNORECASE folds, \d, str.splitlines separators; non-ASCII text matches the
+ * reference exactly only under that version) and gen_log_dfa.pattern_digest of the 13 patterns
+ * (krca/agents/logs.py refuses an edited LogsAgent.error_patterns that no longer matches it). */
+const char* krca_log_dfa_unicode(void);
+uint64_t krca_log_dfa_digest(void);
 int64_t krca_log_index_size(int64_t nbytes);
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
                    int64_t* workspace, int64_t* n_lines, void* stream);
@@ -188,11 +194,26 @@ int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N);
 int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host /*{rb,code,e0,e1} per block*/,
                   int64_t plan_len);
 int64_t krca_ppr_workspace_size(int64_t N);
-int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
-             const int64_t* plan, int64_t plan_len, const float* seed, float seed_floor, double alpha,
-             int32_t max_iter, double tol, void* workspace, float* r_out, int64_t* r_fixed /*nullable*/,
+int krca_ppr(const int64_t* row_ptr, const int32_t* col /*pk*/, const int32_t* outdeg, int64_t N,
+             const int64_t* plan, int64_t plan_len, const uint16_t* lane /*krca_ppr_pack*/, const float* seed,
+             float seed_floor, double alpha, int32_t max_iter, double tol, void* workspace, float* r_out, int64_t* r_fixed /*nullable*/,
              int64_t* q_out /*nullable: quantised seeds*/, int32_t* iters_host, void* stream);
 int64_t krca_ppr_ctl_size(int64_t n_local);
+/* Host (no device work): the plan of krca_ppr_plan plus the packed column array pk_host[E]
+ * (E = row_ptr_host[N]) the step kernel gathers through.  Columns are remapped to the exchange
+ * layout (j + nslot * (j / n_max); n_max = N on one device).  A short-row block whose distinct
+ * columns are few enough becomes a DICTIONARY block: pk[e0, e0+nu) = its distinct columns
+ * (ascending), then two uint16 slots per int32 word (16-byte aligned), one per edge; the plan
+ * entry's first word carries nu in its high 32 bits (0 = direct block: pk[e] = column of edge e).
+ * Each distinct column is gathered once per block instead of once per edge.  The DEVICE copy of
+ * pk must have 64 zero words of padding past E (the step issues clamped 16-byte loads).  lane_host
+ * [krca_ppr_lane_size(plan_len)] uint16: per block and lane t, (row holding edge 8t) << 8 | the
+ * bits of the edges 8t .. 8t+7 that start a non-empty row (the step's segmented row sums need no
+ * search).  Returns the number of dictionary blocks (>= 0) or a negative error.
+ * (KRCA_PPR_DICT=0 packs every block direct; krca_ppr_remap_cols remaps a column array alone.) */
+int64_t krca_ppr_lane_size(int64_t plan_len);
+int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
+                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host);
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream);
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
@@ -200,10 +221,15 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
 int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                              int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
                              const int64_t* r_local /*start vector: the previous solve*/, int64_t* send, void* stream);
-int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*remapped*/, const int64_t* plan,
-                        int64_t plan_len, const int64_t* w_all /*[G][n_max+nslot]*/, const int32_t* outdeg,
+/* flags of krca_ppr_shard_step: KRCA_PPR_RESIDUAL = accumulate |r_new - r_old| for the L1 stop
+ * rule (reads r_local; needed when tol > 0), KRCA_PPR_WRITE_R = store r_new into r_local (every
+ * iteration when tol > 0; a fixed-iteration solve needs it only on its last iteration). */
+#define KRCA_PPR_RESIDUAL 1
+#define KRCA_PPR_WRITE_R 2
+int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const int64_t* plan, int64_t plan_len,
+                        const uint16_t* lane /*krca_ppr_pack*/, const int64_t* w_all /*[G][n_max+nslot]*/, const int32_t* outdeg,
                         const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
-                        int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);
+                        int32_t flags, int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
                           double tol, int32_t first, void* ctl, int64_t* send_next, void* stream);
 int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);

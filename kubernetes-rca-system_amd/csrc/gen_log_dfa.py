@@ -24,7 +24,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, ".."))
-from krca.patterns import ERROR_PATTERNS  # noqa: E402
+from krca.patterns import ERROR_PATTERNS, pattern_digest  # noqa: E402
 
 MAXCP = 0x110000
 
@@ -174,6 +174,7 @@ def simulate(tables, line):
 
 
 def emit(t, path):
+    import unicodedata
     L = []
     L.append("// GENERATED by csrc/gen_log_dfa.py from krca/patterns.py -- do not edit.")
     L.append("// 13-category log matcher DFA (ref:agents/logs_agent.py:20-34, re.IGNORECASE, Python 3.10).")
@@ -188,6 +189,9 @@ def emit(t, path):
     L.append(f"#define KRCA_DFA_OTHER {t['OTHER']}")
     L.append(f"#define KRCA_DFA_NRANGE {len(t['ranges'])}")
     L.append(f"#define KRCA_NCAT {t['ncat']}")
+    L.append("// Unicode tables of the generating interpreter (IGNORECASE folds, \\d, line separators)")
+    L.append(f'#define KRCA_DFA_UNIDATA "{unicodedata.unidata_version}"')
+    L.append(f"#define KRCA_DFA_DIGEST 0x{pattern_digest(ERROR_PATTERNS):016X}ull  // gen_log_dfa.pattern_digest")
     L.append("KRCA_DFA_QUAL uint8_t krca_dfa_ascii_sym[128] = {" + ",".join(map(str, t["ascii_sym"])) + "};")
     L.append("// non-ASCII code point ranges [lo, hi] -> symbol (sorted); all others -> OTHER")
     L.append("KRCA_DFA_QUAL uint32_t krca_dfa_ranges[KRCA_DFA_NRANGE][3] = {")

@@ -48,6 +48,7 @@ struct Tuning {
   int score_chunk;  // KRCA_SCORE_CHUNK: rows per pipelined chunk at W = 60 (10/12/15/20/30)
   int score_nt;     // KRCA_SCORE_NT: non-temporal metric loads
   int ppr_grid;     // KRCA_PPR_GRID: persistent PageRank grid (0 = occupancy API)
+  int ppr_dict;     // KRCA_PPR_DICT: krca_ppr_pack builds dictionary blocks (0 = all direct)
   int log_impl;     // KRCA_LOG_IMPL: 0 line index + DFA lanes, 1 chunk-lane single pass
   int group_impl;   // KRCA_GROUP_IMPL: 0 peeled atomics, 1 one atomic per lane
   int corr_debug;   // KRCA_CORR_DEBUG: profiling aid (results wrong when != 0)

@@ -887,6 +887,9 @@ extern "C" {
 // workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts |
 // [ntiles*TPB] int32 chunk -> container | [ntiles*TPB] int64 first line id per chunk |
 // [1] long-line count | int32 long-line queue [nbytes / LONG_LINE + 1]
+const char* krca_log_dfa_unicode(void) { return KRCA_DFA_UNIDATA; }
+uint64_t krca_log_dfa_digest(void) { return KRCA_DFA_DIGEST; }
+
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
   return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2);

@@ -30,6 +30,7 @@
 //     the partial sums ride the same all-gather; ppr_reduce sums G*NSPREAD slots.
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "krca_common.h"
@@ -44,6 +45,8 @@ constexpr int ROW_BUDGET = TPB;         // rows per short block (one updating la
 constexpr int SEG = EDGE_BUDGET / TPB;  // edges per lane: gathered lane-strided, summed contiguous
 constexpr int NSPREAD = 32;             // partial-sum slots per quantity (spreads the atomics)
 constexpr int NSLOT = 3 * NSPREAD;      // send tail: residual[32] | dangling[32] | seed total[32]
+constexpr int PPR_RESIDUAL = KRCA_PPR_RESIDUAL;
+constexpr int PPR_WRITE_R = KRCA_PPR_WRITE_R;
 
 struct Ctl {          // device control block (header of the ctl buffer)
   double tele;        // (1-alpha)*2^60 + alpha*D   for the next step
@@ -70,7 +73,7 @@ __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
   __syncthreads();
   int64_t s = 0;
   if (threadIdx.x == 0)
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    for (int w = 0; w < TPB / 64; ++w) s += red[w];
   return s;  // valid in thread 0
 }
 
@@ -148,129 +151,225 @@ struct StepScalars {
 };
 
 // r_i <- pulled mass + teleport share; next w_i; residual and dangling contributions
-// (q_i, r_i, deg_i were loaded by the caller together with the row's edges)
+// (q_i, r_i, deg_i were loaded by the caller together with the row's edges).  flags: PPR_RESIDUAL
+// = the L1 stop rule needs |r_new - r_old| (ro was loaded), PPR_WRITE_R = store r_new (every
+// iteration under a tolerance; only the last one of a fixed-iteration solve).
+template <int FLAGS>
 __device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi, int64_t ro, int32_t deg,
-                                           const StepScalars& k, int64_t* __restrict__ r, int64_t* __restrict__ send,
-                                           int64_t& err, int64_t& dang) {
+                                           const StepScalars& k, int64_t* __restrict__ r,
+                                           int64_t* __restrict__ send, int64_t& err, int64_t& dang) {
   const double pd = k.qt > 0 ? (double)qi / k.qtot : k.uni;
   const int64_t t = (int64_t)(pd * k.tele);
   const int64_t rn = pulled + t;
-  r[i] = rn;
-  err += rn > ro ? rn - ro : ro - rn;
+  if (FLAGS & PPR_WRITE_R) r[i] = rn;
+  if (FLAGS & PPR_RESIDUAL) err += rn > ro ? rn - ro : ro - rn;
   if (deg == 0) dang += rn;
   send[i] = edge_weight(rn, deg, k.alpha);
 }
 
-// Everything one plan entry {rb, code, e0, e1} needs before its gathers: the col indices (lane-
-// strided, coalesced), the row offsets and the update operands (q, r, outdeg) of the lane's row.
-struct EntryLoads {
-  int32_t rb, code;
+// One plan entry, loaded in two parts so that a prefetched value is never copied or computed on
+// before it is used (that would make the compiler wait for it and, the vector memory counter
+// being in order, for every load issued before it):
+//   Head  the plan entry (wave-uniform, scalar loads) and the lane's columns to gather; loaded two
+//         entries ahead of the one being summed;
+//   Rows  what the sum and the update need; loaded one entry ahead, beside that entry's gathers.
+// Plan entry {rb | nu << 32, code, e0, e1}: code > 0: short rows [rb, code) with edges [e0, e1);
+// code <= 0: chunk -code of long row rb.  nu == 0 (direct block): pk[e0, e1) are the edges'
+// remapped columns, gathered one per edge.  nu > 0 (dictionary block, krca_ppr_pack): pk[e0, e0+nu)
+// are the block's DISTINCT columns (ascending, so neighbouring lanes gather neighbouring words) and
+// from pk[e0 + pad(nu)] on, two uint16 per word, each edge's slot in that list.  Lane tid gathers
+// slots / edges tid + j*TPB (coalesced) and sums the contiguous edges [8 tid, 8 tid + 8).
+struct Meta {
+  int32_t rb, code, nu;
   int64_t e0, e1;
+};
+struct Head {
+  Meta m;
   int32_t c[SEG];
-  int64_t my_off, my_q, my_r;
+};
+struct Rows {
+  int64_t my_off, my_end;  // row_ptr of the lane's row and the next (absolute; short blocks)
+  int64_t my_q, my_r;
   int32_t my_deg;
+  uint32_t li;  // krca_ppr_pack lane info: (row holding edge 8t) << 8 | head bits of edges 8t .. 8t+7
+  uint4 ix;     // dictionary blocks: the slots of edges 8t .. 8t+7 (uint16 pairs)
 };
 
-__device__ __forceinline__ void load_entry(const int64_t* __restrict__ plan, int64_t b,
-                                           const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-                                           const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
-                                           const int64_t* __restrict__ r, EntryLoads& L) {
-  const int64_t* pe = plan + 4 * b;
-  L.rb = (int32_t)pe[0];
-  L.code = (int32_t)pe[1];
-  L.e0 = pe[2];
-  L.e1 = pe[3];
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int j = 0; j < SEG; ++j) {
-    const int64_t e = L.e0 + tid + j * TPB;
-    L.c[j] = e < L.e1 ? col[e] : -1;
-  }
-  const int nrows = L.code > 0 ? L.code - L.rb : 1;
-  const int64_t my_row = L.rb + (tid < nrows ? tid : 0);
-  L.my_off = L.code > 0 && tid < nrows ? row_ptr[my_row] : 0;
-  L.my_q = q[my_row];
-  L.my_r = r[my_row];
-  L.my_deg = outdeg[my_row];
+__device__ __forceinline__ int64_t dict_words(int64_t e0, int32_t nu) {  // pk offset of the slot words
+  return ((e0 + nu + 3) & ~int64_t(3)) - e0;
 }
 
-// Persistent, software-pipelined step: workgroup g takes plan entries g, g + G, ...; the loads of
-// entry i+1 (plan, col, row data) are issued while entry i's w gathers are in flight, so a
-// workgroup pays the dependent plan -> col latency once instead of once per entry.  The block is
-// latency-bound (dependent memory round trips), and the occupancy is already at 8 waves/SIMD.
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) void ppr_step(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col, const int64_t* __restrict__ plan, int64_t nblk,
-    const int64_t* __restrict__ w, const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n,
-    int64_t N, double alpha, int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
-  __shared__ int64_t vals[EDGE_BUDGET];
+__device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int64_t b, const int32_t* __restrict__ pk,
+                                          Head& H) {
+  const int64_t* pe = plan + 4 * b;
+  const int64_t h = pe[0];
+  H.m.rb = (int32_t)(h & 0xFFFFFFFF);
+  H.m.nu = (int32_t)(h >> 32);
+  H.m.code = (int32_t)pe[1];
+  H.m.e0 = pe[2];
+  H.m.e1 = pe[3];
+  const int tid = threadIdx.x;
+  // every lane loads (clamped index; gather() masks the lanes past lim): a predicated default
+  // value would have to wait for whatever load last wrote that register
+  const int64_t lim = H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0;
+  const int64_t top = lim > 0 ? lim - 1 : 0;
+#pragma unroll
+  for (int j = 0; j < SEG; ++j) {
+    const int64_t u = tid + j * TPB;
+    H.c[j] = pk[H.m.e0 + (u < top ? u : top)];
+  }
+}
+
+template <int FLAGS>
+__device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16_t* __restrict__ lane_info,
+                                          const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk,
+                                          const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
+                                          const int64_t* __restrict__ r, Rows& R) {
+  const int tid = threadIdx.x;
+  const int nrows = m.code > 0 ? m.code - m.rb : 1;
+  const int64_t my_row = m.rb + (tid < nrows ? tid : 0);
+  R.my_off = row_ptr[my_row];
+  R.my_end = row_ptr[my_row + 1];
+  R.my_q = q[my_row];
+  R.my_r = (FLAGS & PPR_RESIDUAL) ? r[my_row] : 0;
+  R.my_deg = outdeg[my_row];
+  R.li = lane_info[b * TPB + tid];  // zero for long-row chunks
+  // unconditional 16-byte load (used by dictionary blocks only): in-bounds, 16-byte aligned
+  const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
+  R.ix = *reinterpret_cast<const uint4*>(pk + wb + (tid * SEG < m.e1 - m.e0 ? tid * (SEG / 2) : 0));
+}
+
+__device__ __forceinline__ void gather(const Head& H, const int64_t* __restrict__ w, int64_t (&v)[SEG]) {
+  const int64_t lim = H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0;
+#pragma unroll
+  for (int j = 0; j < SEG; ++j) v[j] = threadIdx.x + j * TPB < lim ? w[H.c[j]] : 0;
+}
+
+// Persistent, software-pipelined step.  Workgroup g takes plan entries g, g + G, g + 2G, ...;
+// while it sums entry i, the w gathers and row loads of entry i+1 and the plan / column loads of
+// entry i+2 are in flight, so neither the gather latency nor the dependent plan -> column latency
+// is paid per entry.  The loop is unrolled x2 over ping-pong Head / Rows slots (no copies of
+// in-flight loads).  A short block in three barrier-separated phases:
+//  stage   the gathered values (or distinct-column values) go to LDS; every non-empty row records
+//          its index at its first edge (headrow);
+//  sum     lane t sums its 8 contiguous edges [8t, 8t+8) as row segments: the row holding edge 8t
+//          and the head bits of its 8 edges come from the host-built lane info (krca_ppr_pack), its
+//          8 values and the rows at its heads are independent LDS reads, and each finished segment
+//          is one no-return LDS atomic into its row's sum: no dependent LDS chain (round 1 searched
+//          the row offsets and walked the row ends, ~25 dependent LDS round trips per lane);
+//  update  lane r updates row r (teleport, residual, next w).
+#ifdef PPR_TIMING
+__device__ unsigned long long g_ppr_timing[4096 * 5];  // per workgroup: stage, sum, update, long, blocks
+#endif
+#ifndef PPR_WAVES
+#define PPR_WAVES 4
+#endif
+
+template <int FLAGS>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 8))) void ppr_step(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
+    const uint16_t* __restrict__ lane_info, int64_t nblk, const int64_t* __restrict__ w,
+    const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
+    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
+  __shared__ int64_t vals[EDGE_BUDGET];  // staged values: edge (direct) or slot (dictionary) i
+  __shared__ __attribute__((aligned(16))) uint8_t headrow[EDGE_BUDGET];  // at a row's first edge: its row
   __shared__ unsigned long long rowsum[ROW_BUDGET];
-  __shared__ int32_t roff[ROW_BUDGET + 1];
   __shared__ int64_t red[TPB / 64];
   int64_t b = blockIdx.x;
   if (b >= nblk) return;
-  EntryLoads cur;
-  load_entry(plan, b, row_ptr, col, outdeg, q, r, cur);
   const int32_t conv = ctl->converged;
+  if (conv) return;  // converged (tol > 0): no writes (uniform)
   StepScalars k;
   k.tele = ctl->tele;
   k.qt = ctl->q_total;
   k.qtot = (double)k.qt;
   k.uni = 1.0 / (double)N;
   k.alpha = alpha;
-  if (conv) return;  // converged (tol > 0): no writes (uniform)
   const int tid = threadIdx.x;
+  Head H0, H1;
+  Rows R0, R1;
+  load_head(plan, b, pk, H0);
+  int64_t v[SEG];
+  gather(H0, w, v);
+  load_rows<FLAGS>(H0.m, b, lane_info, row_ptr, pk, outdeg, q, r, R0);
+  Meta cur = H0.m;
+  int64_t b1 = b + gridDim.x;
+  if (b1 < nblk) load_head(plan, b1, pk, H1);
   int64_t err = 0, dang = 0;
-  while (true) {
-    int64_t v[SEG];
-#pragma unroll
-    for (int j = 0; j < SEG; ++j) v[j] = cur.c[j] >= 0 ? w[cur.c[j]] : 0;
-    const int64_t nb = b + gridDim.x;
-    EntryLoads nxt;
-    if (nb < nblk) load_entry(plan, nb, row_ptr, col, outdeg, q, r, nxt);
-    if (cur.code > 0) {
-      const int nrows = cur.code - cur.rb;
-      const int ne = (int)(cur.e1 - cur.e0);
+#ifdef PPR_TIMING
+  uint64_t tacc[5] = {0, 0, 0, 0, 0};
+  uint64_t tp = clock64();
+#define PPR_T(i) do { const uint64_t tn = clock64(); tacc[i] += tn - tp; tp = tn; } while (0)
+#else
+#define PPR_T(i) do {} while (0)
+#endif
+  // one entry: stage `cur` (its values gathered last round, rows in rc), gather entry b1 (head hn)
+  // and load its rows into rn, load the head of entry b2 into hl; sum and update `cur`.
+  // False when `cur` was the workgroup's last entry.
+  auto entry = [&](Head& hn, Head& hl, const Rows& rc, Rows& rn) -> bool {
+    const bool shortb = cur.code > 0;
+    const int ne = (int)(cur.e1 - cur.e0);
+    const bool dict = cur.nu > 0;
+    int64_t sacc_long = 0;
+    if (shortb) {
+      const int nst = dict ? cur.nu : ne;  // staged values: slots or edges
 #pragma unroll
       for (int j = 0; j < SEG; ++j) {
         const int e = tid + j * TPB;
-        if (e < ne) vals[e] = v[j];
+        if (e < nst) vals[e] = v[j];
       }
-      if (tid < nrows) roff[tid] = (int32_t)(cur.my_off - cur.e0);
-      if (tid == 0) roff[nrows] = ne;
+      if (tid < cur.code - cur.rb && rc.my_end > rc.my_off)  // a non-empty row: its index at its first edge
+        headrow[(int)(rc.my_off - cur.e0)] = (uint8_t)tid;
       rowsum[tid] = 0ull;
+    } else {
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) sacc_long += v[j];
+    }
+    // v is free: gathers and rows of the next entry, head of the one after
+    const int64_t b2 = b1 + gridDim.x;
+    const Meta next = hn.m;
+    if (b1 < nblk) {
+      gather(hn, w, v);
+      load_rows<FLAGS>(next, b1, lane_info, row_ptr, pk, outdeg, q, r, rn);
+    }
+    if (b2 < nblk) load_head(plan, b2, pk, hl);
+    if (shortb) {
+      const int nrows = cur.code - cur.rb;
       __syncthreads();
+      PPR_T(0);
       const int a = tid * SEG;
-      if (a < ne) {  // this lane's contiguous edges [a, b) as row segments
-        const int bb = min(a + SEG, ne);
-        int lo = 0, hi = nrows;  // roff[lo] <= a < roff[hi]
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (roff[mid] <= a) lo = mid;
-          else hi = mid;
+      if (a < ne) {
+        const uint32_t M = rc.li & 0xFFu;  // head bits of edges a .. a+7
+        int row = (int)(rc.li >> 8);        // the row holding edge a
+        const uint2 hr = *reinterpret_cast<const uint2*>(headrow + a);  // rows at the lane's heads
+        const uint4 sx = rc.ix;  // this lane's own slots (prefetched with the rows)
+        int64_t x[SEG];
+#pragma unroll
+        for (int kk = 0; kk < SEG; ++kk) {
+          const uint32_t wd = kk < 2 ? sx.x : kk < 4 ? sx.y : kk < 6 ? sx.z : sx.w;
+          const int sl = dict ? (int)((wd >> (16 * (kk & 1))) & 0xFFFFu) : a + kk;
+          x[kk] = a + kk < ne ? vals[sl] : 0;
         }
-        int row = lo;
-        int end = roff[row + 1];
         int64_t sacc = 0;
-        for (int e = a; e < bb; ++e) {
-          while (e >= end) {
-            if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);
+#pragma unroll
+        for (int kk = 0; kk < SEG; ++kk) {
+          if (kk > 0 && ((M >> kk) & 1u)) {
+            if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);  // no return: no wait
             sacc = 0;
-            ++row;
-            end = roff[row + 1];
+            row = (int)(((kk < 4 ? hr.x : hr.y) >> (8 * (kk & 3))) & 0xFFu);
           }
-          sacc += vals[e];
+          sacc += x[kk];
         }
         if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);
       }
       __syncthreads();
+      PPR_T(1);
       if (tid < nrows)
-        update_row(cur.rb + tid, (int64_t)rowsum[tid], cur.my_q, cur.my_r, cur.my_deg, k, r, send, err, dang);
-      __syncthreads();  // rowsum / vals / roff are rewritten by the next entry
+        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[tid], rc.my_q, rc.my_r, rc.my_deg, k, r, send, err, dang);
+      __syncthreads();  // rowsum / vals / headrow are rewritten by the next entry
+      PPR_T(2);
     } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
-      int64_t sacc = 0;
-#pragma unroll
-      for (int j = 0; j < SEG; ++j) sacc += v[j];
-      const int64_t tot = block_sum_i64(sacc, red);
+      const int64_t tot = block_sum_i64(sacc_long, red);
       if (tid == 0) {
         const int32_t rb = cur.rb;
         const int64_t deg_in = row_ptr[rb + 1] - row_ptr[rb];
@@ -284,14 +383,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
           const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          update_row(rb, pulled, cur.my_q, cur.my_r, cur.my_deg, k, r, send, err, dang);
+          update_row<FLAGS>(rb, pulled, rc.my_q, rc.my_r, rc.my_deg, k, r, send, err, dang);
         }
       }
+      PPR_T(3);
     }
-    if (nb >= nblk) break;
-    cur = nxt;
-    b = nb;
+#ifdef PPR_TIMING
+    tacc[4] += 1;
+#endif
+    if (b1 >= nblk) return false;
+    cur = next;
+    b = b1;
+    b1 = b2;
+    return true;
+  };
+  while (entry(H1, H0, R0, R1) && entry(H0, H1, R1, R0)) {
   }
+#ifdef PPR_TIMING
+  if (tid == 0 && blockIdx.x < 4096)
+    for (int i = 0; i < 5; ++i) g_ppr_timing[blockIdx.x * 5 + i] += tacc[i];
+#endif
   err = block_sum_i64(err, red);
   dang = block_sum_i64(dang, red);
   if (tid == 0) {
@@ -386,6 +497,62 @@ int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out) {
   return n;
 }
 
+// host: the plan of build_plan plus the packed column array pk[E] (include/krca.h krca_ppr_pack):
+// columns remapped to the [G][n_max + NSLOT] exchange layout; a short-row block whose distinct
+// columns fit becomes a dictionary block (sorted distinct columns, then uint16 slots per edge),
+// every other block stays direct.  Returns the number of dictionary blocks.
+int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_max, int64_t* plan, int64_t plan_len,
+                    int32_t* pk, uint16_t* lane) {
+  auto remap = [n_max](int64_t j) { return (int32_t)(j + NSLOT * (j / n_max)); };
+  std::vector<int32_t> uniq;
+  std::vector<uint16_t> slot;
+  std::vector<int16_t> head;  // block-relative row starting at each edge (-1: none)
+  int64_t ndict = 0;
+  for (int64_t p = 0; p < plan_len; p += 4) {
+    const int64_t rb = plan[p], code = plan[p + 1], e0 = plan[p + 2], e1 = plan[p + 3];
+    const int64_t ne = e1 - e0;
+    uint16_t* li = lane + (p / 4) * TPB;
+    for (int t = 0; t < TPB; ++t) li[t] = 0;
+    if (code > 0) {  // lane t: (row holding edge 8t) << 8 | head bits of its edges 8t .. 8t+7
+      head.assign(ne, -1);
+      for (int64_t rr = rb; rr < code; ++rr)
+        if (rp[rr + 1] > rp[rr]) head[rp[rr] - e0] = (int16_t)(rr - rb);
+      int cur_row = 0;
+      for (int64_t e = 0; e < ne; ++e) {
+        if (head[e] >= 0) cur_row = head[e];
+        const int t = (int)(e / SEG), k = (int)(e % SEG);
+        if (k == 0) li[t] = (uint16_t)(cur_row << 8);
+        if (head[e] >= 0) li[t] |= (uint16_t)(1u << k);
+      }
+    }
+    bool dict = false;
+    if (code > 0 && ne >= 32 && krca::tuning().ppr_dict) {
+      uniq.assign(col + e0, col + e1);
+      std::sort(uniq.begin(), uniq.end());
+      uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+      const int64_t nu = (int64_t)uniq.size();
+      const int64_t dw = ((e0 + nu + 3) & ~int64_t(3)) - e0;  // slot words start 16-byte aligned
+      dict = dw + 4 * krca::ceil_div(ne, SEG) <= ne;          // the lanes' 16-byte slot loads stay inside
+      if (dict) {
+        for (int64_t u = 0; u < nu; ++u) pk[e0 + u] = remap(uniq[u]);
+        for (int64_t u = nu; u < dw; ++u) pk[e0 + u] = 0;
+        slot.assign(krca::ceil_div(ne, SEG) * SEG, 0);
+        for (int64_t e = 0; e < ne; ++e)
+          slot[e] = (uint16_t)(std::lower_bound(uniq.begin(), uniq.end(), col[e0 + e]) - uniq.begin());
+        uint32_t* words = reinterpret_cast<uint32_t*>(pk + e0 + dw);
+        for (int64_t i = 0; i < (int64_t)slot.size() / 2; ++i)
+          words[i] = (uint32_t)slot[2 * i] | ((uint32_t)slot[2 * i + 1] << 16);
+        for (int64_t e = dw + (int64_t)slot.size() / 2; e < ne; ++e) pk[e0 + e] = 0;
+        plan[p] = rb | (nu << 32);
+        ++ndict;
+      }
+    }
+    if (!dict)
+      for (int64_t e = e0; e < e1; ++e) pk[e] = remap(col[e]);
+  }
+  return ndict;
+}
+
 unsigned grid_for(int64_t n, int64_t cap = 2048) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), cap));
 }
@@ -409,6 +576,21 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host, in
   KRCA_CHECK_ARG(plan_len == need, "krca_ppr_plan: plan_len %lld != %lld", (long long)plan_len, (long long)need);
   build_plan(row_ptr_host, N, plan_host);
   return KRCA_OK;
+}
+
+int64_t krca_ppr_lane_size(int64_t plan_len) { return plan_len / 4 * TPB; }
+
+int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
+                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host) {
+  KRCA_CHECK_ARG(row_ptr_host && plan_host && pk_host && lane_host && N > 0 && N < INT32_MAX && n_max > 0,
+                 "krca_ppr_pack: bad arguments");
+  const int64_t E = row_ptr_host[N];
+  KRCA_CHECK_ARG(E == 0 || col_host, "krca_ppr_pack: null col");
+  int rc = krca_ppr_plan(row_ptr_host, N, plan_host, plan_len);
+  if (rc) return rc;
+  for (int64_t e = 0; e < E; ++e)
+    KRCA_CHECK_ARG(col_host[e] >= 0, "krca_ppr_pack: negative column at edge %lld", (long long)e);
+  return pack_blocks(row_ptr_host, col_host, N, n_max, plan_host, plan_len, pk_host, lane_host);
 }
 
 int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 16 * std::max<int64_t>(n_local, 1); }
@@ -456,13 +638,13 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
 }
 
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
-                        const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
-                        int64_t n_max, int64_t N, double alpha, int64_t* r_local, int64_t* send, void* ctl,
-                        void* stream) {
+                        const uint16_t* lane, const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
+                        int64_t n_max, int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send,
+                        void* ctl, void* stream) {
   KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 4 == 0 && n_local >= 0 && n_local <= n_max && N > 0,
                  "krca_ppr_shard_step: bad sizes");
   if (plan_len == 0) return KRCA_OK;
-  KRCA_CHECK_ARG(row_ptr && col && plan && w_all && outdeg && q_local && r_local && send && ctl,
+  KRCA_CHECK_ARG(row_ptr && col && plan && lane && w_all && outdeg && q_local && r_local && send && ctl,
                  "krca_ppr_shard_step: null pointer");
   KRCA_CHECK_ARG(w_all != send, "krca_ppr_shard_step: w_all and send must be distinct buffers (ping-pong)");
   const int64_t nblk = plan_len / 4;
@@ -471,14 +653,16 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&ppr_step), TPB, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&ppr_step<0>), TPB, 0) !=
             hipSuccess || per_cu < 1)
       per_cu = 4;
     return (int64_t)cus * per_cu;
   }();
   const int64_t resident = krca::tuning().ppr_grid > 0 ? (int64_t)krca::tuning().ppr_grid : occupancy;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nblk, resident));
-  hipLaunchKernelGGL(ppr_step, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, nblk,
+  auto kern = (flags & KRCA_PPR_RESIDUAL) ? ppr_step<PPR_RESIDUAL | PPR_WRITE_R>
+               : (flags & KRCA_PPR_WRITE_R) ? ppr_step<PPR_WRITE_R> : ppr_step<0>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, lane, nblk,
                      w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
@@ -528,10 +712,10 @@ int64_t krca_ppr_workspace_size(int64_t N) {
 }
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int64_t* plan,
-             int64_t plan_len, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
+             int64_t plan_len, const uint16_t* lane, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
              void* workspace, float* r_out, int64_t* r_fixed, int64_t* q_out, int32_t* iters_host, void* stream) {
   KRCA_CHECK_ARG(N > 0 && N < INT32_MAX, "krca_ppr: N=%lld out of range", (long long)N);
-  KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && seed && workspace && r_out, "krca_ppr: null pointer");
+  KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && lane && seed && workspace && r_out, "krca_ppr: null pointer");
   KRCA_CHECK_ARG(plan_len > 0 && plan_len % 4 == 0, "krca_ppr: bad plan");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0 && max_iter > 0, "krca_ppr: alpha in (0,1), max_iter > 0");
   char* ctl = reinterpret_cast<char*>(workspace);
@@ -549,8 +733,9 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   int32_t iters = 0, conv = 0;
   int cur = 0;  // w buffer the next step gathers from
   for (int it = 0; it < max_iter; ++it) {
-    if ((rc = krca_ppr_shard_step(row_ptr, col, plan, plan_len, wb[cur], outdeg, q, N, N, N, alpha, r, wb[cur ^ 1],
-                                  ctl, stream)))
+    const int32_t flags = tol > 0.0 ? (KRCA_PPR_RESIDUAL | KRCA_PPR_WRITE_R) : (it + 1 == max_iter ? KRCA_PPR_WRITE_R : 0);
+    if ((rc = krca_ppr_shard_step(row_ptr, col, plan, plan_len, lane, wb[cur], outdeg, q, N, N, N, alpha, flags, r,
+                                  wb[cur ^ 1], ctl, stream)))
       return rc;
     cur ^= 1;
     if ((rc = krca_ppr_shard_reduce(wb[cur], 1, N, N, alpha, tol, 0, ctl, wb[cur ^ 1], stream))) return rc;
@@ -569,4 +754,14 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   return KRCA_OK;
 }
 
+#ifdef PPR_TIMING
+int krca_ppr_debug_timing(unsigned long long* host, int reset) {
+  KRCA_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ppr_timing), sizeof(g_ppr_timing)));
+  if (reset) {
+    static unsigned long long zero[4096 * 5];
+    KRCA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ppr_timing), zero, sizeof(zero)));
+  }
+  return KRCA_OK;
+}
+#endif
 }  // extern "C"

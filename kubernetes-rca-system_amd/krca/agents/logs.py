@@ -40,6 +40,21 @@ class LogsAgent(BaseAgent):
         super().__init__(k8s_client, engine)
         self.error_patterns = dict(P.ERROR_PATTERNS)  # public attribute of the reference (:20)
 
+    def _check_patterns_compiled(self):
+        """The device matcher is compiled from krca/patterns.py (csrc/gen_log_dfa.py); the reference
+        matches whatever self.error_patterns holds (ref:agents/logs_agent.py:20,147-149).  An edited
+        dict would silently give different histograms, so it is refused instead."""
+        ident = getattr(self.engine, "log_dfa_identity", None)
+        if ident is not None and ident()[1] != P.pattern_digest():
+            raise P.PatternsChanged("krca/patterns.py and the compiled matcher (libkrca.so) disagree: "
+                                    "regenerate csrc/log_dfa_tables.h and rebuild")
+        if list(self.error_patterns.items()) == list(P.ERROR_PATTERNS):
+            return
+        raise P.PatternsChanged(
+            "LogsAgent.error_patterns differs from the patterns the device matcher was compiled from "
+            "(krca/patterns.py); edit krca/patterns.py and regenerate csrc/log_dfa_tables.h with "
+            "csrc/gen_log_dfa.py")
+
     def analyze(self, namespace, context=None, **kwargs):
         self.reset()
         try:
@@ -72,6 +87,8 @@ class LogsAgent(BaseAgent):
                 deferred = e
 
             # (2) one device pass over all containers
+            if docs:
+                self._check_patterns_compiled()
             scan = self.engine.log_scan(*pack_documents([d[3] for d in docs])) if docs else None
 
             # (3) findings in the reference's order: per container, log findings then status

@@ -31,6 +31,8 @@ SIGNATURES = {
     "krca_stream_state_size": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
     "krca_stream_score": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_vp]),
+    "krca_log_dfa_unicode": (ctypes.c_char_p, []),
+    "krca_log_dfa_digest": (ctypes.c_uint64, []),
     "krca_log_index_size": (c_i64, [c_i64]),
     "krca_log_index": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "krca_log_match": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -60,16 +62,18 @@ SIGNATURES = {
     "krca_ppr_plan_size": (c_i64, [c_vp, c_i64]),
     "krca_ppr_plan": (c_i32, [c_vp, c_i64, c_vp, c_i64]),
     "krca_ppr_workspace_size": (c_i64, [c_i64]),
-    "krca_ppr": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_f32, c_f64, c_i32, c_f64, c_vp, c_vp, c_vp,
-                         c_vp, ctypes.POINTER(c_i32), c_vp]),
+    "krca_ppr": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_f64, c_i32, c_f64, c_vp, c_vp,
+                         c_vp, c_vp, ctypes.POINTER(c_i32), c_vp]),
     "krca_ppr_nslot": (c_i32, []),
     "krca_ppr_ctl_size": (c_i64, [c_i64]),
     "krca_ppr_remap_cols": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "krca_ppr_shard_init": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_ppr_shard_init_warm": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp,
                                          c_vp]),
-    "krca_ppr_shard_step": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp,
-                                    c_vp, c_vp]),
+    "krca_ppr_shard_step": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f64, c_i32,
+                                    c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_lane_size": (c_i64, [c_i64]),
+    "krca_ppr_pack": (c_i64, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_shard_reduce": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp]),
     "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
@@ -91,6 +95,7 @@ SIGNATURES = {
 }
 
 KRCA_ENOTCONV = -70
+PPR_RESIDUAL, PPR_WRITE_R = 1, 2  # krca_ppr_shard_step flags
 SCORE_VARIANTS = {0: "pipe", 1: "ring", 2: "ring_buf", 3: "reread", 4: "pipe_rows"}  # krca_rolling_score_variant
 
 
@@ -395,6 +400,22 @@ class NativeEngine:
         return idx.cpu().numpy(), val.cpu().numpy()
 
     # -- a12 ---------------------------------------------------------------------------------
+    def log_dfa_identity(self):
+        """(Unicode version, pattern digest) the device matcher was compiled for."""
+        return self.lib.krca_log_dfa_unicode().decode(), int(self.lib.krca_log_dfa_digest())
+
+    def check_log_unicode(self, blob):
+        """Non-ASCII text matches the reference's re semantics only under the Unicode version the
+        DFA was generated with (IGNORECASE folds, \\d classes, separators); ASCII text under any.
+        Raises when the running interpreter differs and the text holds a byte >= 0x80."""
+        import unicodedata
+        want = self.lib.krca_log_dfa_unicode().decode()
+        if unicodedata.unidata_version != want and len(blob) and \
+                int(np.frombuffer(memoryview(blob), np.uint8).max()) >= 0x80:
+            raise KrcaError(f"log matcher compiled for Unicode {want}, interpreter has "
+                            f"{unicodedata.unidata_version}: regenerate csrc/log_dfa_tables.h "
+                            f"(csrc/gen_log_dfa.py) for non-ASCII logs")
+
     def log_scan_device(self, text, doc_off, validate=True):
         """text uint8 device tensor (16-byte aligned), doc_off int64 device tensor [D+1].
         validate: check the doc_off contract on the device first (one stream sync); pass False only
@@ -524,6 +545,7 @@ class NativeEngine:
         torch = self.torch
         doc_off = np.asarray(doc_off, dtype=np.int64)
         check_doc_off(doc_off, len(blob))
+        self.check_log_unicode(blob)
         text = self.upload_blob(blob)
         off = self._dev(doc_off)
         r = self.log_scan_device(text, off, validate=False)
@@ -539,6 +561,22 @@ class NativeEngine:
         return LogScan(blob, r["doc_lines"].cpu().numpy(), r["hist"].cpu().numpy(), ex, starts, ends)
 
     # -- a10 ---------------------------------------------------------------------------------
+    def ppr_pack(self, row_ptr_host, col_host, n_max=None):
+        """Host-built plan + packed columns + lane info (krca_ppr_pack), uploaded:
+        (plan, plan_len, pk, lane, n_dict)."""
+        rp = np.ascontiguousarray(row_ptr_host, dtype=np.int64)
+        cl = np.ascontiguousarray(col_host, dtype=np.int32)
+        N = len(rp) - 1
+        n = self.lib.krca_ppr_plan_size(rp.ctypes.data_as(c_vp), N)
+        plan = np.zeros(max(n, 4), dtype=np.int64)
+        pk = np.zeros(len(cl) + 64, dtype=np.int32)  # the step's clamped loads stay inside the padding
+        lane = np.zeros(max(self.lib.krca_ppr_lane_size(n), 1), dtype=np.uint16)
+        nd = self.lib.krca_ppr_pack(rp.ctypes.data_as(c_vp), cl.ctypes.data_as(c_vp), N, int(n_max or N),
+                                    plan.ctypes.data_as(c_vp), n, pk.ctypes.data_as(c_vp), lane.ctypes.data_as(c_vp))
+        if nd < 0:
+            _check(int(nd), "krca_ppr_pack", self.lib)
+        return self._dev(plan), n, self._dev(pk), self._dev(lane.view(np.int16)), int(nd)
+
     def ppr_plan(self, row_ptr_host):
         rp = np.ascontiguousarray(row_ptr_host, dtype=np.int64)
         N = len(rp) - 1
@@ -547,7 +585,7 @@ class NativeEngine:
         _check(self.lib.krca_ppr_plan(rp.ctypes.data_as(c_vp), N, plan.ctypes.data_as(c_vp), n), "krca_ppr_plan")
         return self._dev(plan), n
 
-    def ppr_device(self, row_ptr, col, outdeg, plan, plan_len, seed, alpha=0.85, max_iter=100, tol=1e-6,
+    def ppr_device(self, row_ptr, col, outdeg, plan, plan_len, lane, seed, alpha=0.85, max_iter=100, tol=1e-6,
                    seed_floor=0.0, allow_nonconv=False):
         """Single-device PageRank (krca_ppr).  Returns (r float32, r_fixed int64, q int64, iters)."""
         torch = self.torch
@@ -558,7 +596,7 @@ class NativeEngine:
         q = torch.empty(N, dtype=torch.int64, device=self.device)
         iters = c_i32(0)
         rc = self.lib.krca_ppr(self.ptr(row_ptr), self.ptr(col), self.ptr(outdeg), N, self.ptr(plan), plan_len,
-                               self.ptr(seed), float(seed_floor), float(alpha), int(max_iter), float(tol),
+                               self.ptr(lane), self.ptr(seed), float(seed_floor), float(alpha), int(max_iter), float(tol),
                                self.ptr(ws), self.ptr(r_out), self.ptr(r_fixed), self.ptr(q), ctypes.byref(iters),
                                self._stream())
         if not (allow_nonconv and rc == KRCA_ENOTCONV):
@@ -593,10 +631,10 @@ class NativeEngine:
     def _ppr_full(self, row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor):
         torch = self.torch
         rp_host = np.asarray(row_ptr, dtype=np.int64)
-        plan, n = self.ppr_plan(rp_host)
+        plan, n, pk, lane, _ = self.ppr_pack(rp_host, col)
         sd = self._dev(seed, torch.float32) if isinstance(seed, torch.Tensor) else self._dev(np.asarray(seed, np.float32))
-        return self.ppr_device(self._dev(rp_host), self._dev(np.asarray(col, np.int32)),
-                               self._dev(np.asarray(outdeg, np.int32)), plan, n, sd, alpha, max_iter, tol, seed_floor)
+        return self.ppr_device(self._dev(rp_host), pk, self._dev(np.asarray(outdeg, np.int32)), plan, n, lane, sd, alpha,
+                               max_iter, tol, seed_floor)
 
 
 _default = None

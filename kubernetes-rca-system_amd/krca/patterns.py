@@ -63,3 +63,17 @@ RECOMMENDATIONS = {
 
 def recommendation(category):
     return RECOMMENDATIONS.get(category, "Investigate the logs in detail to identify the root cause")
+
+
+class PatternsChanged(ValueError):
+    """LogsAgent.error_patterns no longer matches the compiled device matcher."""
+
+
+def pattern_digest(patterns=ERROR_PATTERNS):
+    """FNV-1a 64 over the (name, pattern) pairs in order, NUL-separated: the identity of a
+    compiled pattern set (KRCA_DFA_DIGEST in csrc/log_dfa_tables.h, krca_log_dfa_digest())."""
+    h = 0xcbf29ce484222325
+    for name, pat in patterns:
+        for c in name.encode() + b"\0" + pat.encode() + b"\0":
+            h = ((h ^ c) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h

@@ -78,6 +78,12 @@ class Config:
 RANKING = Config()
 
 
+def step_flags(tol, last):
+    """krca_ppr_shard_step flags: under a tolerance every iteration needs the residual and the
+    stored ranks; a fixed-iteration solve stores the ranks on its last iteration only."""
+    return 3 if tol > 0 else (2 if last else 0)
+
+
 class Comm:
     """All-gather over torch.distributed (nccl == RCCL on ROCm; gloo in CPU tests)."""
 
@@ -121,13 +127,10 @@ class DeviceShard:
         self.N, self.n_max, self.world = N, n_max, world
         self.x = x_local
         self.n = int(outdeg_local.shape[0])
-        self.plan, self.plan_len = (engine.ppr_plan(row_ptr_local) if self.n else (None, 0))
+        # plan + packed columns (remapped to the exchange layout, dictionary blocks where they pay)
+        self.plan, self.plan_len, self.col, self.lane, self.n_dict = (
+            engine.ppr_pack(row_ptr_local, col_local, n_max) if self.n else (None, 0, None, None, 0))
         self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr_local)).to(dev)
-        col = torch.from_numpy(np.ascontiguousarray(col_local, dtype=np.int32)).to(dev)
-        self.col = torch.empty_like(col)
-        self._chk(lib.krca_ppr_remap_cols(engine.ptr(col), col.numel(), n_max, engine.ptr(self.col), engine._stream()),
-                  "krca_ppr_remap_cols")
-        del col
         self.outdeg = torch.from_numpy(np.ascontiguousarray(outdeg_local)).to(dev)
         i64 = dict(dtype=torch.int64, device=dev)
         self.q = torch.zeros(max(self.n, 1), **i64)
@@ -153,13 +156,14 @@ class DeviceShard:
                                             self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
                                             p(self.send), e._stream()), "krca_ppr_shard_init")
 
-    def step(self, alpha):
+    def step(self, alpha, flags=3):
+        """flags: krca_ppr_shard_step's KRCA_PPR_RESIDUAL (1) | KRCA_PPR_WRITE_R (2)."""
         e, p = self.eng, self.eng.ptr
         if self.plan_len:
             self._chk(e.lib.krca_ppr_shard_step(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len,
-                                                p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
-                                                float(alpha), p(self.r), p(self.send), p(self.ctl), e._stream()),
-                      "krca_ppr_shard_step")
+                                                p(self.lane), p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
+                                                float(alpha), int(flags), p(self.r), p(self.send), p(self.ctl),
+                                                e._stream()), "krca_ppr_shard_step")
 
     def reduce(self, alpha, tol, first):
         e, p = self.eng, self.eng.ptr
@@ -188,8 +192,8 @@ class RcaStep:
         s.init(cfg.alpha, cfg.seed_floor)
         c.exchange(s)
         s.reduce(cfg.alpha, cfg.tol, 1)
-        for _ in range(cfg.iters):
-            s.step(cfg.alpha)
+        for it in range(cfg.iters):
+            s.step(cfg.alpha, step_flags(cfg.tol, it + 1 == cfg.iters))
             c.exchange(s)
             s.reduce(cfg.alpha, cfg.tol, 0)
 

@@ -80,7 +80,7 @@ class StreamingRCA:
         s.reduce(cfg.alpha, self.tol, 1)
         it_host, conv = ctypes.c_int32(0), ctypes.c_int32(0)
         for it in range(self.max_iter):
-            s.step(cfg.alpha)
+            s.step(cfg.alpha, 3)  # tol > 0: residual + ranks every iteration
             self.rca.comm.exchange(s)
             s.reduce(cfg.alpha, self.tol, 0)
             if (it + 1) % self.check_every == 0 and it + 1 < self.max_iter:

@@ -55,7 +55,7 @@ class NumpyShard:
         snd[self.n_max + 2 * NSPREAD] = int(self.q.sum())
         self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
 
-    def step(self, alpha):
+    def step(self, alpha, flags=3):
         """Pull SpMV fused with the update: reads w_all, writes r and send (krca_ppr_shard_step)."""
         if self.ctl["converged"]:
             return

@@ -13,7 +13,7 @@ from krca import native
 def header_symbols():
     with open(os.path.join(ROOT, "include", "krca.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|float|const char\*)\s+(krca_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|uint64_t|float|const char\*)\s+(krca_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol():
@@ -104,3 +104,62 @@ def test_tuning_knobs_and_score_variant():
     with native.tune(lib, KRCA_SCORE_IMPL=4):
         assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 1440, 60)] == "pipe_rows"
     assert lib.krca_tune_get(b"KRCA_SCORE_IMPL", ctypes.byref(v)) == 0 and v.value == 0  # restored
+
+
+def test_ppr_pack_decodes_to_the_remapped_columns():
+    """krca_ppr_pack (host): every edge of every block decodes to its remapped column, through the
+    block's sorted distinct-column list (dictionary blocks) or directly (direct / long-row blocks)."""
+    from krca import synth
+    from krca.rca import NSLOT
+    lib = native.load_library()
+    vp = ctypes.c_void_p
+    m = synth.make_graph(6000, n_edges=120_000, seed=2)
+    rp, col = m.row_ptr.copy(), m.col.copy()
+    # a long row (> 2048 callers) and a row with many distinct callers
+    for n_max in (6000, 2500):
+        n = lib.krca_ppr_plan_size(rp.ctypes.data_as(vp), len(rp) - 1)
+        plan = np.zeros(n, np.int64)
+        pk = np.zeros(len(col), np.int32)
+        lane = np.zeros(lib.krca_ppr_lane_size(n), np.uint16)
+        nd = lib.krca_ppr_pack(rp.ctypes.data_as(vp), col.ctypes.data_as(vp), len(rp) - 1, n_max,
+                               plan.ctypes.data_as(vp), n, pk.ctypes.data_as(vp), lane.ctypes.data_as(vp))
+        assert nd > 0.5 * (n // 4), nd  # most blocks of a service mesh are dictionary blocks
+        want = col.astype(np.int64) + NSLOT * (col.astype(np.int64) // n_max)
+        got = np.full(len(col), -1, np.int64)
+        for bi, (h, code, e0, e1) in enumerate(plan.reshape(-1, 4)):
+            nu = int(h) >> 32
+            if code > 0:  # lane info: row holding edge 8t, head bits of edges 8t .. 8t+7
+                rb = int(h) & 0xFFFFFFFF
+                rows = np.arange(rb, code)
+                starts = rp[rows] - e0
+                nonempty = rp[rows + 1] > rp[rows]
+                for t in range(0, (e1 - e0 + 7) // 8):
+                    li = int(lane[bi * 256 + t])
+                    a = 8 * t
+                    hold = rows[nonempty & (starts <= a)].max() - rb
+                    assert li >> 8 == hold
+                    heads = set((starts[nonempty] - a).tolist()) & set(range(8))
+                    assert li & 0xFF == sum(1 << k for k in heads if a + k < e1 - e0)
+            if nu == 0:
+                got[e0:e1] = pk[e0:e1]
+                continue
+            assert code > 0
+            uniq = pk[e0:e0 + nu].astype(np.int64)
+            assert np.all(np.diff(uniq) > 0)
+            dw = ((e0 + nu + 3) & ~3) - e0
+            words = pk[e0 + dw:e1].view(np.uint32)
+            slots = np.stack([words & 0xFFFF, words >> 16], 1).reshape(-1)[:e1 - e0]
+            assert slots.max() < nu
+            got[e0:e1] = uniq[slots]
+        assert np.array_equal(got, want)
+
+
+def test_log_matcher_identity_matches_this_interpreter():
+    """The DFA tables record the Unicode version they were generated under and the digest of the
+    13 patterns; both must match this interpreter and krca/patterns.py (the reference declares
+    Python >= 3.11, whose Unicode 14/15 tables may fold or classify non-ASCII differently)."""
+    import unicodedata
+    from krca import patterns
+    lib = native.load_library()
+    assert lib.krca_log_dfa_unicode().decode() == unicodedata.unidata_version
+    assert int(lib.krca_log_dfa_digest()) == patterns.pattern_digest()

@@ -146,3 +146,17 @@ def test_topology_cycles_valid():
                 assert nodes[0] == nodes[-1]
                 for u, v in zip(nodes, nodes[1:]):
                     assert agent.service_graph.has_edge(u, v), (name, u, v)
+
+
+def test_logs_agent_refuses_edited_error_patterns():
+    """The reference matches whatever LogsAgent.error_patterns holds (ref:agents/logs_agent.py:20,
+    147-149); the device matcher is compiled, so an edited dict is refused through the agent's
+    error contract instead of giving silently different histograms."""
+    agent = A.LogsAgent(A.Shim(), engine=ENG)
+    ok = agent.analyze(A.NS)
+    assert "error" not in ok
+    agent.error_patterns["timeout"] = r"(deadline)"
+    res = agent.analyze(A.NS)
+    assert "error_patterns differs" in res.get("error", "")
+    del agent.error_patterns["timeout"]
+    assert "error_patterns differs" in agent.analyze(A.NS).get("error", "")
