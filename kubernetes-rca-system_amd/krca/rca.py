@@ -144,7 +144,45 @@ class DeviceShard:
 
     def _chk(self, rc, what):
         from .native import _check
-        _check(rc, what)
+        _check(rc, what, self.eng.lib)
+
+    # -- streaming (krca/stream.py): rolling state of this rank's pods, warm-started ranks ------
+    def stream_score(self, x_new, t0, horizon):
+        """x_new float32 [delta, n_local, M] (device, time-major): carry the rank's rolling state
+        forward by delta steps (krca_stream_score); outputs as the batch scorer over the series so far."""
+        torch, e, p = self.torch, self.eng, self.eng.ptr
+        d, P, M = x_new.shape
+        if P != self.n:
+            raise ValueError(f"stream window has {P} pods, the shard owns {self.n}")
+        if getattr(self, "_stream_state", None) is None:
+            nbytes = e.lib.krca_stream_state_size(P, M, self.cfg.window, horizon)
+            dev = e.device
+            self._stream_state = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+            self.score_out = dict(z_last=torch.empty((max(P, 1), M), dtype=torch.float32, device=dev),
+                                  score=torch.empty(max(P, 1), dtype=torch.float32, device=dev),
+                                  n_exceed=torch.empty(max(P, 1), dtype=torch.int32, device=dev),
+                                  flags=torch.empty(max(P, 1), dtype=torch.uint8, device=dev))
+        o = self.score_out
+        self._chk(e.lib.krca_stream_score(p(x_new), P, M, int(d), int(t0), self.cfg.window, int(horizon),
+                                          float(self.cfg.z_threshold), p(self._stream_state), p(o["z_last"]), p(o["score"]),
+                                          p(o["n_exceed"]), p(o["flags"]), e._stream()), "krca_stream_score")
+        return o
+
+    def init_warm(self, alpha, seed_floor):
+        """Re-seed from the current scores, start from the ranks of the previous solve."""
+        e, p = self.eng, self.eng.ptr
+        self._chk(e.lib.krca_ppr_shard_init_warm(p(self.score_out["score"]), float(seed_floor), p(self.outdeg), self.n,
+                                                 self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
+                                                 p(self.send), e._stream()), "krca_ppr_shard_init_warm")
+
+    def ctl_read(self):
+        """(iterations done, converged) of the solve in flight (synchronises the stream)."""
+        import ctypes
+        e, p = self.eng, self.eng.ptr
+        it, conv = ctypes.c_int32(0), ctypes.c_int32(0)
+        self._chk(e.lib.krca_ppr_ctl_read(p(self.ctl), ctypes.byref(it), ctypes.byref(conv), e._stream()),
+                  "krca_ppr_ctl_read")
+        return int(it.value), bool(conv.value)
 
     def score(self):
         self.score_out = self.eng.rolling_score_device(self.x, self.cfg.window, self.cfg.z_threshold, self.score_out)

@@ -93,3 +93,37 @@ class NumpyShard:
     def local_topk(self, k):
         key = (self.r.astype(np.float64) * self.q.astype(np.float64)).view(np.int64)
         return oracle.topk_ref(key, min(k, self.n))
+
+    # -- streaming (krca/stream.py): the batch oracle over the series so far ---------------------
+    def stream_score(self, x_new, t0, horizon):
+        """krca_stream_score's contract restated: outputs of the batch scorer over the whole series
+        so far, n_exceed over the last `horizon` evaluated steps (a difference of prefix counts)."""
+        x_new = np.asarray(x_new.cpu() if hasattr(x_new, "cpu") else x_new, np.float32)
+        hist = getattr(self, "_hist", None)
+        self._hist = x_new if hist is None else np.concatenate([hist, x_new])
+        assert len(self._hist) == t0 + len(x_new)
+        W = self.cfg.window
+        t = len(self._hist)
+
+        def prefix(tt):
+            return oracle.c_rolling_score(self._hist[:tt], W)["n_exceed"] if tt > W else np.zeros(self.n, np.int32)
+        out = oracle.c_rolling_score(self._hist, W)  # t <= W: z = 0, no exceedance
+        out["n_exceed"] = prefix(t) - prefix(t - horizon) if t - horizon > W else prefix(t)
+        self.score_out = out
+        return out
+
+    def init_warm(self, alpha, floor):
+        """krca_ppr_shard_init_warm: new seeds, w and dangling mass from the kept ranks."""
+        s = self.score_out["score"]
+        v = s.astype(np.float64) - np.float64(np.float32(floor))
+        self.q = np.where(v > 0, (np.maximum(v, 0) * 4294967296.0).astype(np.int64), 0)
+        snd = self.send.numpy()
+        snd[self.n_max:] = 0
+        snd[:self.n] = _w(self.r, self.deg, alpha)
+        snd[self.n_max + NSPREAD] = int(self.r[self.deg == 0].sum())
+        snd[self.n_max + 2 * NSPREAD] = int(self.q.sum())
+        self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
+
+    def ctl_read(self):
+        c = self.ctl
+        return (c["converged"] or c["iter"]), bool(c["converged"])

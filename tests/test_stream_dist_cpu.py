@@ -1,0 +1,95 @@
+"""The C5 streaming replay (krca/stream.py) pod-sharded over gloo on CPU, world sizes 1-3.
+
+Each rank owns a pod range: its rolling state, its rows of the pull-CSR; every re-ranking
+iteration is one all-gather.  After every window the sharded ranks, iteration counts and merged
+top-10 must equal the single-process oracle chain (oracle.c_ppr_warm from the previous window's
+ranks; scores = the batch C scorer over the series so far), bit for bit, for any number of ranks.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+N, M, W, H = 2500, 8, 30, 90
+WINDOWS = [W + 40, 5, 1, 1, 17, 1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mesh():
+    from krca import synth
+    m = synth.make_graph(N, n_edges=15 * N, seed=8)
+    x = synth.make_metrics(N, M, sum(WINDOWS), window=W, seed=10, roots=m.roots,
+                           hop_sets=synth.caller_hops(m, m.roots)).numpy()
+    return m, x
+
+
+def _worker(rank, world, port, out_q):
+    sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"),
+                    os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from krca.rca import Comm, Config, shard_graph, shard_range
+    from krca.stream import StreamingRCA
+    from numpy_shard import NumpyShard
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, x = _mesh()
+    cfg = Config(window=W)
+    lo, hi, n_max = shard_range(N, world, rank)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
+    shard = NumpyShard(np.zeros((0, hi - lo, M), np.float32), rp, col, od, N, n_max, world, cfg)
+    s = StreamingRCA(None, m.row_ptr, m.col, m.outdeg, M, cfg, horizon=H, tol=1e-9, max_iter=60,
+                     comm=Comm(world, rank), shard=shard)
+    t, rows = 0, []
+    for d in WINDOWS:
+        out = s.window(x[t:t + d, lo:hi, :])
+        t += d
+        rows.append((shard.r.copy(), out["iters"], [int(i) for i in out["top"][0]],
+                     np.asarray(out["scores"]["n_exceed"]).copy()))
+    out_q.put((rank, rows))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_stream_matches_oracle_chain(world):
+    import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, x = _mesh()
+    r_ref, t = None, 0
+    for wi, d in enumerate(WINDOWS):
+        t += d
+        score = oracle.c_rolling_score(x[:t], W)["score"]
+        if r_ref is None:
+            _, r_ref, it = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, 4.0)
+            q_ = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, 4.0, return_q=True)[3]
+        else:
+            r_ref, it, q_ = oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, score, r_ref, 0.5, 60, 1e-9, 4.0)
+        top = oracle.topk_ref(oracle.c_rca_key(r_ref, q_), 10)[0].tolist()
+        r_sh = np.concatenate([res[g][wi][0] for g in range(world)])
+        assert np.array_equal(r_sh, r_ref), (world, wi)
+        for g in range(world):
+            assert res[g][wi][1] == it, (world, wi, res[g][wi][1], it)
+            assert res[g][wi][2] == top, (world, wi)
