@@ -114,14 +114,17 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
  * krca_template_hash: hash[l] for every line of krca_log_match.
  * krca_template_hist: per container d, the distinct hashes of its lines in ascending order and
  *   their counts, written to out_hash/out_count at the container's own line range
- *   [doc_line0[d], doc_line0[d] + n_templates[d]); sort-based and atomics-free.  Containers with
- *   more than 64 lines are listed (host) in big_docs_host (staged through big_docs_dev); at most
- *   krca_template_max_lines() lines per container (beyond: krca_template_hist_huge). */
+ *   [doc_line0[d], doc_line0[d] + n_templates[d]); sort-based.  Containers of <= 8 lines are sorted
+ *   in one lane's registers, <= 64 by a wave, <= krca_template_max_lines() by a workgroup, all on
+ *   device lists (no host round trip).  workspace: krca_template_hist_ws_size(ndocs) bytes, int32
+ *   {mid, big, huge counts, 0 | mid list [D] | big list [D] | huge list [D]}: containers above
+ *   krca_template_max_lines() lines are only LISTED (count at int32 [2], ids from int32 [4 + 2D]);
+ *   the caller runs krca_template_hist_huge on each. */
 int krca_template_hash(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int64_t* line_end,
                        int64_t n_lines, uint64_t* hash, void* stream);
+int64_t krca_template_hist_ws_size(int64_t ndocs);
 int krca_template_hist(const uint64_t* hash, const int32_t* doc_lines, const int64_t* doc_line0, int64_t ndocs,
-                       const int32_t* big_docs_host, int32_t n_big, int32_t* big_docs_dev, uint64_t* out_hash,
-                       int32_t* out_count, int32_t* n_templates, void* stream);
+                       void* workspace, uint64_t* out_hash, int32_t* out_count, int32_t* n_templates, void* stream);
 int32_t krca_template_max_lines(void);
 /* containers with more than krca_template_max_lines() lines, one call each: the same output for
  * the container's n_lines hashes (hash, out_hash, out_count already offset to its doc_line0),

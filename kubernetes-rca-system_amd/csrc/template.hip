@@ -9,9 +9,9 @@
 //                    prime 0x100000001b3);
 //   per container  = the distinct h of its lines in ascending order with their line counts.
 //
-// krca_template_hash: one lane per line (lines from krca_log_match), bytes through the same
-//   16-byte register window as the log scanner; word bytes are hashed once the word's fate is
-//   known (the word is re-read from L1/L2, never from HBM twice in practice).
+// krca_template_hash: one lane per line (lines from krca_log_match), the workgroup's span of text
+//   staged in LDS (coalesced, once); word bytes are hashed once the word's fate is known (the word
+//   is re-read from LDS).
 // krca_template_hist: sort-based, atomics-free.  Containers with <= 64 lines: one wave, bitonic
 //   sort of 64-bit keys across lanes (shuffles), run heads by ballot, counts by ballot distance.
 //   <= 4096 lines: one workgroup, bitonic sort in LDS, run compaction by a block scan.
@@ -27,41 +27,6 @@ constexpr int BIG = 4096;  // max lines per container handled by the LDS path
 constexpr uint64_t kFnvOff = 0xcbf29ce484222325ull;
 constexpr uint64_t kFnvPrime = 0x100000001b3ull;
 
-struct Bytes16 {  // 16-byte register window over the text (as in logscan.hip)
-  const uint8_t* t;
-  int64_t n, base;
-  uint32_t w0, w1, w2, w3;
-  __device__ void init(const uint8_t* text, int64_t nbytes) {
-    t = text;
-    n = nbytes;
-    base = -1;
-  }
-  __device__ __forceinline__ uint32_t at(int64_t p) {
-    const int64_t b = p & ~(int64_t)15;
-    if (b != base) {
-      base = b;
-      if (b + 16 <= n) {
-        const uint4 v = *reinterpret_cast<const uint4*>(t + b);
-        w0 = v.x;
-        w1 = v.y;
-        w2 = v.z;
-        w3 = v.w;
-      } else {
-        uint32_t ww[4] = {0, 0, 0, 0};
-        for (int k = 0; k < 16; ++k)
-          if (b + k < n) ww[k >> 2] |= (uint32_t)t[b + k] << (8 * (k & 3));
-        w0 = ww[0];
-        w1 = ww[1];
-        w2 = ww[2];
-        w3 = ww[3];
-      }
-    }
-    const int q = (int)((p >> 2) & 3);
-    const uint32_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
-    return (w >> (8 * (int)(p & 3))) & 0xFFu;
-  }
-};
-
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t b) { return (h ^ b) * kFnvPrime; }
 __device__ __forceinline__ bool is_word(uint32_t b) {
   return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
@@ -70,40 +35,96 @@ __device__ __forceinline__ bool is_hex(uint32_t b) {
   return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'F') || (b >= 'a' && b <= 'f');
 }
 
+// The template hash of one line in ONE pass, 4 bytes per read (`word_at(q)`: the aligned
+// little-endian dword at byte q).  FNV-1a runs through word bytes as if they stayed; the hash at the
+// word's start is kept, and a word that turns out masked (a digit, or >= 8 hex digits) is replaced
+// by "<*>" from that saved state when it ends — so a word is never re-read, and every lane runs
+// the same select-only instruction stream (no divergence inside the line).
+__device__ __forceinline__ uint64_t fnv3_mask(uint64_t h) { return fnv(fnv(fnv(h, '<'), '*'), '>'); }
+
+template <class WordAt>
+__device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& word_at) {
+  uint64_t h = kFnvOff, hb = 0;
+  bool inword = false, digit = false, hex = true;
+  int wl = 0;
+  for (int64_t q = s & ~(int64_t)3; q < e; q += 4) {
+    const uint32_t wv = word_at(q);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // straight-line selects; only the rare masked-word end branches
+      const int64_t p = q + k;
+      const bool in = (p >= s) & (p < e);
+      const uint32_t b = (wv >> (8 * k)) & 0xFFu;
+      const bool wc = in & is_word(b);
+      if (in & !wc & inword & (digit | (hex & (wl >= 8)))) h = fnv3_mask(hb);  // a masked word ends
+      const bool start = wc & !inword;
+      hb = start ? h : hb;
+      h = in ? fnv(h, b) : h;
+      digit = (digit & !start) | (wc & (b >= '0') & (b <= '9'));
+      hex = wc ? ((hex | start) & is_hex(b)) : hex;
+      wl = start ? 1 : (wc ? wl + 1 : wl);
+      inword = in ? wc : inword;
+    }
+  }
+  if (inword & (digit | (hex & (wl >= 8)))) h = fnv3_mask(hb);  // a trailing masked word
+  return h;
+}
+
+// Workgroup per 256 consecutive lines.  Lines are contiguous in the text, so the workgroup first
+// copies the bytes its lines span into LDS (16 B per lane, coalesced: every text byte crosses HBM
+// once) and every lane then hashes its line from LDS.  A lane whose line reaches past the staged
+// span (a line or a run of lines longer than SPAN bytes) reads through the global 16-byte window
+// instead.  (Round 1 read every line through that window: each window refill was a dependent
+// global load, and with 64 lanes at random phases nearly every byte step of a wave waited on one:
+// 1.63 ms for the 2.5M-line C5 window.)
+constexpr int SPAN = 24 * 1024;  // a multiple of 16 * TPB
 __global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restrict__ text, int64_t nbytes,
                                                         const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
                                                         int64_t L, uint64_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (i >= L) return;
-  Bytes16 B;
-  B.init(text, nbytes);
-  const int64_t s = ls[i], e = le[i];
-  uint64_t h = kFnvOff;
-  int64_t w0 = -1;  // start of the current word
-  bool digit = false, hex = true;
-  for (int64_t p = s; p <= e; ++p) {
-    const uint32_t b = p < e ? B.at(p) : 0u;  // sentinel closes a trailing word
-    if (p < e && is_word(b)) {
-      if (w0 < 0) {
-        w0 = p;
-        digit = false;
-        hex = true;
-      }
-      digit |= (b >= '0' && b <= '9');
-      hex &= is_hex(b);
-      continue;
-    }
-    if (w0 >= 0) {  // the word [w0, p) ends here
-      if (digit || (hex && p - w0 >= 8)) {
-        h = fnv(fnv(fnv(h, '<'), '*'), '>');
-      } else {
-        for (int64_t q = w0; q < p; ++q) h = fnv(h, B.at(q));
-      }
-      w0 = -1;
-    }
-    if (p < e) h = fnv(h, b);
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[SPAN];
+  const int64_t l0 = (int64_t)blockIdx.x * TPB;
+  const int64_t i = l0 + threadIdx.x;
+  const int64_t l1 = min(l0 + TPB, L);
+  const int64_t a0 = ls[l0] & ~(int64_t)15;
+  const int64_t a1 = min(min(le[l1 - 1], nbytes), a0 + SPAN - 4);  // dword reads may touch 3 bytes past
+  // every staging load is issued before the first LDS write (one latency per workgroup, not one
+  // per 4 KiB); a bounds-checked buffer descriptor over [a0, nbytes) returns zeros past the text
+  constexpr int NST = SPAN / (16 * TPB);
+  const int64_t rem = nbytes - a0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(text + a0), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
+  uint4 st[NST];
+#pragma unroll
+  for (int j = 0; j < NST; ++j) {
+    const int off = 16 * (threadIdx.x + j * TPB);
+    st[j] = off < a1 + 4 - a0 ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0))
+                              : make_uint4(0u, 0u, 0u, 0u);
   }
-  out[i] = h;
+#pragma unroll
+  for (int j = 0; j < NST; ++j) {
+    const int off = 16 * (threadIdx.x + j * TPB);
+    if (off < rem && off + 16 > rem) {  // the text's last partial piece (a straddling buffer load reads as 0)
+      uint32_t ww[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (off + k < rem) ww[k >> 2] |= (uint32_t)text[a0 + off + k] << (8 * (k & 3));
+      st[j] = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+    }
+    reinterpret_cast<uint4*>(sbuf)[threadIdx.x + j * TPB] = st[j];
+  }
+  __syncthreads();
+  if (i >= L) return;
+  const int64_t s = ls[i], e = le[i];
+  if (e <= a1) {
+    out[i] = line_hash(s, e, [&](int64_t q) -> uint32_t { return *reinterpret_cast<const uint32_t*>(sbuf + (q - a0)); });
+  } else {  // past the staged span: aligned dwords from the text (the last one may be partial)
+    out[i] = line_hash(s, e, [&](int64_t q) -> uint32_t {
+      if (q + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(text + q);
+      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k)
+        if (q + k < nbytes) v |= (uint32_t)text[q + k] << (8 * k);
+      return v;
+    });
+  }
 }
 
 // ---- per-container histograms ----------------------------------------------------------------
@@ -111,17 +132,79 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   return (uint64_t)__shfl_xor((long long)v, m, 64);
 }
 
-// wave per container with <= 64 lines
+// Containers by size, one lane each (a C5 container holds ~2.5 lines): up to LANE_MAX lines are
+// sorted in the lane's registers (odd-even transposition network, static indices) and emitted
+// here; larger ones are appended to the mid (<= 64), big (<= BIG) or huge lists of the workspace,
+// one atomic per wave and list.  (Round 1 gave every container a whole wave: 1M mostly idle waves,
+// 0.5 ms per C5 window.)
+constexpr int LANE_MAX = 8;
+constexpr int MID_MAX = 64;
+__device__ __forceinline__ void wave_append(bool take, int32_t d, int32_t* cnt, int32_t* list) {
+  const uint64_t m = __ballot(take);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  int32_t base = 0;
+  if (lane == leader) base = atomicAdd(cnt, __popcll(m));
+  base = __shfl(base, leader, 64);
+  if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = d;
+}
+
+__global__ __launch_bounds__(TPB) void tmpl_hist_lane(const uint64_t* __restrict__ hash,
+                                                      const int32_t* __restrict__ doc_lines,
+                                                      const int64_t* __restrict__ doc_line0, int64_t D,
+                                                      uint64_t* __restrict__ out_hash, int32_t* __restrict__ out_cnt,
+                                                      int32_t* __restrict__ n_tmpl, int32_t* __restrict__ ws) {
+  const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int n = d < D ? doc_lines[d] : 0;
+  int32_t* cnt = ws;
+  int32_t* lists = ws + 4;
+  wave_append(d < D && n > LANE_MAX && n <= MID_MAX, (int32_t)d, cnt + 0, lists);
+  wave_append(d < D && n > MID_MAX && n <= BIG, (int32_t)d, cnt + 1, lists + D);
+  wave_append(d < D && n > BIG, (int32_t)d, cnt + 2, lists + 2 * D);
+  if (d >= D || n > LANE_MAX) return;
+  const int64_t lo = doc_line0[d];
+  uint64_t v[LANE_MAX];
+#pragma unroll
+  for (int j = 0; j < LANE_MAX; ++j) v[j] = j < n ? hash[lo + j] : ~0ull;
+#pragma unroll
+  for (int r = 0; r < LANE_MAX; ++r)
+#pragma unroll
+    for (int j = r & 1; j + 1 < LANE_MAX; j += 2) {
+      const uint64_t a = v[j], b = v[j + 1];
+      v[j] = a < b ? a : b;
+      v[j + 1] = a < b ? b : a;
+    }
+  int k = 0, run = 0;
+#pragma unroll
+  for (int j = 0; j < LANE_MAX; ++j) {  // runs of equal keys among the first n
+    if (j < n) {
+      ++run;
+      if (j + 1 == n || v[j + 1] != v[j]) {
+        out_hash[lo + k] = v[j];
+        out_cnt[lo + k] = run;
+        ++k;
+        run = 0;
+      }
+    }
+  }
+  n_tmpl[d] = k;
+}
+
+// persistent waves over the mid list (LANE_MAX < lines <= 64): a wave per container, bitonic sort
+// of 64-bit keys across lanes (shuffles), run heads by ballot, counts by ballot distance
 __global__ __launch_bounds__(TPB) void tmpl_hist_small(const uint64_t* __restrict__ hash,
                                                        const int32_t* __restrict__ doc_lines,
                                                        const int64_t* __restrict__ doc_line0, int64_t D,
+                                                       const int32_t* __restrict__ ws,
                                                        uint64_t* __restrict__ out_hash, int32_t* __restrict__ out_cnt,
                                                        int32_t* __restrict__ n_tmpl) {
-  const int64_t d = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (d >= D) return;
+  const int32_t nmid = ws[0];
+  for (int64_t wv = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6); wv < nmid;
+       wv += (int64_t)gridDim.x * (TPB / 64)) {
+  const int64_t d = ws[4 + wv];
   const int n = doc_lines[d];
-  if (n > 64) return;  // handled by tmpl_hist_big
   const int64_t lo = doc_line0[d];
   uint64_t v = lane < n ? hash[lo + lane] : ~0ull;
   // bitonic sort ascending across the 64 lanes
@@ -146,21 +229,23 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_small(const uint64_t* __restric
     out_cnt[lo + idx] = next - lane;
   }
   if (lane == 0) n_tmpl[d] = __popcll(heads);
+  }
 }
 
 // workgroup per container with 64 < lines <= 4096
 __global__ __launch_bounds__(TPB) void tmpl_hist_big(const uint64_t* __restrict__ hash,
                                                      const int32_t* __restrict__ doc_lines,
-                                                     const int64_t* __restrict__ doc_line0,
-                                                     const int32_t* __restrict__ big_docs, int32_t n_big,
+                                                     const int64_t* __restrict__ doc_line0, int64_t D,
+                                                     const int32_t* __restrict__ ws,
                                                      uint64_t* __restrict__ out_hash, int32_t* __restrict__ out_cnt,
                                                      int32_t* __restrict__ n_tmpl) {
   __shared__ uint64_t key[BIG];
   __shared__ int32_t pos[BIG];
   __shared__ int32_t wsum[TPB / 64];
-  const int b = blockIdx.x;
-  if (b >= n_big) return;
-  const int64_t d = big_docs[b];
+  const int32_t n_big = ws[1];
+  for (int64_t b = blockIdx.x; b < n_big; b += gridDim.x) {
+  __syncthreads();  // key / pos / wsum of the previous container
+  const int64_t d = ws[4 + D + b];
   const int n = doc_lines[d];
   const int64_t lo = doc_line0[d];
   int np = 64;
@@ -209,6 +294,7 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_big(const uint64_t* __restrict_
     out_cnt[lo + r] = next - i;
   }
   if (threadIdx.x == 0) n_tmpl[d] = carry;
+  }
 }
 
 // ---- containers with more than BIG lines -----------------------------------------------------
@@ -413,23 +499,26 @@ int krca_template_hash(const uint8_t* text, int64_t nbytes, const int64_t* line_
   return KRCA_OK;
 }
 
+int64_t krca_template_hist_ws_size(int64_t ndocs) { return 16 + 12 * std::max<int64_t>(ndocs, 1); }
+
 int krca_template_hist(const uint64_t* hash, const int32_t* doc_lines, const int64_t* doc_line0, int64_t ndocs,
-                       const int32_t* big_docs_host, int32_t n_big, int32_t* big_docs_dev, uint64_t* out_hash,
-                       int32_t* out_count, int32_t* n_templates, void* stream) {
-  KRCA_CHECK_ARG(ndocs >= 0 && n_big >= 0, "krca_template_hist: bad sizes");
+                       void* workspace, uint64_t* out_hash, int32_t* out_count, int32_t* n_templates, void* stream) {
+  KRCA_CHECK_ARG(ndocs >= 0 && ndocs < INT32_MAX, "krca_template_hist: bad sizes");
   if (ndocs == 0) return KRCA_OK;
-  KRCA_CHECK_ARG(doc_lines && doc_line0 && n_templates && out_hash && out_count, "krca_template_hist: null pointer");
+  KRCA_CHECK_ARG(doc_lines && doc_line0 && n_templates && out_hash && out_count && workspace,
+                 "krca_template_hist: null pointer");
   hipStream_t st = krca::as_stream(stream);
-  hipLaunchKernelGGL(tmpl_hist_small, dim3((unsigned)krca::ceil_div(ndocs, TPB / 64)), dim3(TPB), 0, st, hash,
-                     doc_lines, doc_line0, ndocs, out_hash, out_count, n_templates);
+  int32_t* ws = static_cast<int32_t*>(workspace);
+  KRCA_HIP(hipMemsetAsync(ws, 0, 16, st));
+  hipLaunchKernelGGL(tmpl_hist_lane, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, hash, doc_lines,
+                     doc_line0, ndocs, out_hash, out_count, n_templates, ws);
   KRCA_LAUNCH_CHECK();
-  if (n_big > 0) {
-    KRCA_CHECK_ARG(big_docs_host && big_docs_dev, "krca_template_hist: null big-doc list");
-    KRCA_HIP(hipMemcpyAsync(big_docs_dev, big_docs_host, n_big * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(tmpl_hist_big, dim3((unsigned)n_big), dim3(TPB), 0, st, hash, doc_lines, doc_line0, big_docs_dev,
-                       n_big, out_hash, out_count, n_templates);
-    KRCA_LAUNCH_CHECK();
-  }
+  hipLaunchKernelGGL(tmpl_hist_small, dim3(1024), dim3(TPB), 0, st, hash, doc_lines, doc_line0, ndocs,
+                     (const int32_t*)ws, out_hash, out_count, n_templates);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(tmpl_hist_big, dim3(512), dim3(TPB), 0, st, hash, doc_lines, doc_line0, ndocs,
+                     (const int32_t*)ws, out_hash, out_count, n_templates);
+  KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
 

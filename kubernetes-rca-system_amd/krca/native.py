@@ -38,7 +38,8 @@ SIGNATURES = {
     "krca_log_match": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),
     "krca_template_hash": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
-    "krca_template_hist": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_template_hist_ws_size": (c_i64, [c_i64]),
+    "krca_template_hist": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_template_max_lines": (c_i32, []),
     "krca_template_huge_ws_size": (c_i64, [c_i64]),
     "krca_template_hist_huge": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -460,27 +461,25 @@ class NativeEngine:
         _check(self.lib.krca_template_hash(self.ptr(scan["text"]), scan["text"].numel(), self.ptr(scan["line_start"]),
                                            self.ptr(scan["line_end"]), L, self.ptr(h), self._stream()),
                "krca_template_hash")
-        dl = scan["doc_lines"].cpu().numpy()
-        cap = self.lib.krca_template_max_lines()
-        big = np.nonzero((dl > 64) & (dl <= cap))[0].astype(np.int32)
-        huge = np.nonzero(dl > cap)[0]
-        bigd = torch.empty(max(len(big), 1), dtype=torch.int32, device=self.device)
+        ws = self._workspace("tmpl_hist", self.lib.krca_template_hist_ws_size(D)).view(torch.int32)
         _check(self.lib.krca_template_hist(self.ptr(h), self.ptr(scan["doc_lines"]), self.ptr(scan["doc_line0"]), D,
-                                           big.ctypes.data_as(c_vp), len(big), self.ptr(bigd), self.ptr(oh),
-                                           self.ptr(oc), self.ptr(nt), self._stream()), "krca_template_hist")
-        if len(huge):  # > cap lines: a distinct-hash table + bucketed sorts per container
+                                           self.ptr(ws), self.ptr(oh), self.ptr(oc), self.ptr(nt), self._stream()),
+               "krca_template_hist")
+        n_huge = int(ws[2].item())  # containers above krca_template_max_lines() (a 4-byte read)
+        if n_huge:  # a distinct-hash table + bucketed sorts per container
+            huge = np.sort(ws[4 + 2 * D:4 + 2 * D + n_huge].cpu().numpy())
+            dl = scan["doc_lines"].cpu().numpy()
             d0 = scan["doc_line0"].cpu().numpy()
             flag = torch.zeros(len(huge), dtype=torch.int32, device=self.device)
             for i, d in enumerate(huge.tolist()):
                 n, lo = int(dl[d]), int(d0[d])
-                ws = self._workspace("tmpl_huge", self.lib.krca_template_huge_ws_size(n) + 16)
-                _check(self.lib.krca_template_hist_huge(c_vp(h.data_ptr() + 8 * lo), n, self.ptr(ws),
+                wsh = self._workspace("tmpl_huge", self.lib.krca_template_huge_ws_size(n) + 16)
+                _check(self.lib.krca_template_hist_huge(c_vp(h.data_ptr() + 8 * lo), n, self.ptr(wsh),
                                                         c_vp(oh.data_ptr() + 8 * lo), c_vp(oc.data_ptr() + 4 * lo),
                                                         c_vp(nt.data_ptr() + 4 * d), c_vp(flag.data_ptr() + 4 * i),
                                                         self._stream()), "krca_template_hist_huge")
             if int(flag.max().item()):
                 raise KrcaError("template histogram: a hash bucket overflowed (not expected for 64-bit hashes)")
-        torch.cuda.current_stream(self.device).synchronize()  # big-doc list lives on the host
         return dict(hash=h[:L], tmpl_hash=oh[:L], tmpl_count=oc[:L], n_templates=nt)
 
     def template_hist(self, blob, doc_off):

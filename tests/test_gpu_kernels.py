@@ -334,6 +334,15 @@ def test_template_hist_vs_oracle(eng):
     docs += synth.make_log_corpus(5000, lines_per_doc=4, seed=11, hazard_rate=0.02)
     docs += ["", "\n", "id=deadbeefcafe x", "user_42 7f9c4 0xFF", "a" * 5000 + " 123", "été 42 café"]
     docs.append("\n".join("req %d from 10.0.%d.%d took %dms" % (i, i % 7, i % 250, i) for i in range(3000)))
+    # workgroups whose 256 lines span more than the LDS-staged 24 KiB (the rest go through global
+    # dwords), a 30 KB line, masked / unmasked hex lengths, words across dword boundaries, no final \n
+    docs.append("\n".join("y" * (150 + i % 7) + " w%d deadbeef deadbee _9 a_b ABCDEF12 abcdefg" % i for i in range(700)))
+    docs.append("z" * 15000 + " 42 " + "q" * 15000 + " cafebabe1 end")
+    docs += ["deadbeef", "deadbee", "x_", "_", "9", "a9b c", "ab\u00e9cd 12\u00e912"]
+    for tail in range(1, 20):  # the text's last bytes in every position of a 16-byte piece
+        got = eng.template_hist(*pack_documents(["w" * tail + " 1 tail" + "z" * (tail % 5), "end" * tail]))
+        assert got == [oracle.template_hist("w" * tail + " 1 tail" + "z" * (tail % 5)),
+                       oracle.template_hist("end" * tail)], tail
     got = eng.template_hist(*pack_documents(docs))
     for d, text in enumerate(docs):
         assert got[d] == oracle.template_hist(text), d
