@@ -150,8 +150,37 @@ def build():
         trans.append(row)
         k += 1
     outs = [out(s) for s in order]
-    return dict(nsym=nsym, nstate=len(order), ascii_sym=ascii_sym, ranges=ranges, trans=trans,
+    trans, outs = minimize(trans, outs)
+    return dict(nsym=nsym, nstate=len(trans), ascii_sym=ascii_sym, ranges=ranges, trans=trans,
                 out=outs, SEP=SEP, OTHER=OTHER, ncat=len(pats))
+
+
+def minimize(trans, outs):
+    """Moore partition refinement (states equivalent iff same output mask now and after every
+    symbol string), then breadth-first renumbering from the start state (0 stays 0).  The
+    subset construction's 502 states fold to 394: a smaller LDS table for the device walk."""
+    n, nsym = len(trans), len(trans[0])
+    part = list(outs)
+    while True:
+        keys = {}
+        new = [keys.setdefault((part[s],) + tuple(part[trans[s][a]] for a in range(nsym)), len(keys))
+               for s in range(n)]
+        if len(keys) == len(set(part)):
+            break
+        part = new
+    rep = {}
+    for s in range(n):
+        rep.setdefault(part[s], s)
+    ids, order, k = {part[0]: 0}, [part[0]], 0
+    while k < len(order):
+        r = rep[order[k]]
+        for a in range(nsym):
+            c = part[trans[r][a]]
+            if c not in ids:
+                ids[c] = len(order)
+                order.append(c)
+        k += 1
+    return ([[ids[part[trans[rep[c]][a]]] for a in range(nsym)] for c in order], [outs[rep[c]] for c in order])
 
 
 def simulate(tables, line):

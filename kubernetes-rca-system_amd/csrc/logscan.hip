@@ -658,7 +658,7 @@ __device__ __forceinline__ void dfa_load(DfaLds& dfa) {
 // SIMD to hide the walk's dependent LDS round trips (256-lane groups left it at 4).
 constexpr int DFA_TPB = 512;
 
-__global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
+__global__ __launch_bounds__(DFA_TPB) void log_dfa_window(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
                                                    const int64_t* __restrict__ line_start,
                                                    const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
                                                    int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
@@ -693,6 +693,194 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
       }
     }
     line_mask[l] = mask;
+  }
+}
+
+// ---- log_dfa: the walk, four bytes per word and sixteen per block --------------------------
+// The round-1 walk (log_dfa_window, kept for A/B) spent ~20 instructions per byte on the 16-byte
+// window bookkeeping, the UTF-8 decode branches and the accept test, with a dependent global
+// refill every 16 bytes at a different iteration in each lane (the memory counter being per
+// wave, nearly every step of a wave waited on one).  This walk:
+//  * moves every lane of a wave through its line in lockstep blocks of 16 bytes (starting at the
+//    line's 4-byte-aligned start): one buffer load per block per lane, issued a block ahead into
+//    the other half of a register ping-pong, so a wave's loads are issued together and each
+//    wait covers a load issued 16 transitions earlier;
+//  * maps bytes to symbols with one LDS byte table (bytes outside the line map to NOP, an
+//    identity column), no decode, when the block's line bytes are all ASCII; blocks holding a
+//    non-ASCII byte (or a code point continuing from the previous block) take the exact
+//    code-point path of the reference (decode, range table);
+//  * keeps a 32-bit entry per (state, symbol): the target's row offset (low half) and its
+//    category mask (high half), so the accept test is one OR per byte.
+// Per byte: a byte-table read, a 16-bit add, a table read and an OR.
+constexpr int DFA_RS = 32;  // u32 entries per state row: the symbols, then NOP
+constexpr uint32_t NOP_SYM = DFA_RS - 1;
+static_assert(KRCA_DFA_NSYM <= (int)NOP_SYM, "no room for the NOP column");
+static_assert(KRCA_DFA_NSTATE * DFA_RS * 4 <= 65536, "row byte offsets must fit 16 bits");
+static_assert(KRCA_NCAT <= 16, "category masks must fit 16 bits");
+
+struct DfaLds4 {
+  uint32_t trans[KRCA_DFA_NSTATE * DFA_RS];  // (out[target] << 16) | target * DFA_RS * 4
+  uint8_t sym[256];                          // byte -> symbol * 4 (bytes >= 0x80 -> NOP)
+};
+
+__device__ __forceinline__ void dfa4_load(DfaLds4& d) {
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * DFA_RS; i += blockDim.x) {
+    const int st = i / DFA_RS, c = i % DFA_RS;
+    const uint32_t t = c < KRCA_DFA_NSYM ? krca_dfa_trans[st * KRCA_DFA_NSYM + c] : (uint32_t)st;
+    d.trans[i] = ((uint32_t)krca_dfa_out[t] << 16) | (t * DFA_RS * 4);
+  }
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    const uint32_t sy = i < 128 ? krca_dfa_ascii_sym[i] : NOP_SYM;
+    d.sym[i] = (uint8_t)((sy == KRCA_DFA_SEP ? NOP_SYM : sy) * 4);  // no separator inside a line
+  }
+  __syncthreads();
+}
+
+// the entry at byte offset (row + symoff) mod 2^16 of the table: the row offset sits in the low
+// half of the previous entry, a 16-bit add drops the category bits above it
+__device__ __forceinline__ uint32_t dfa4_step(const DfaLds4& d, uint32_t row, uint32_t symoff) {
+  uint32_t a;  // (row + symoff) & 0xFFFF in one VALU op (SDWA: low word, upper bits zeroed)
+  asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
+      : "=v"(a)
+      : "v"(row), "v"(symoff));
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(d.trans) + a);
+}
+
+// Line bytes of a block, four at a time: byte k of word j (block index i = 4j + k) is in the line
+// iff lo <= i < hi (lo = s - P clamped to [0, 16], hi = e - P clamped to [0, 16], broadcast to
+// the four bytes as lo4 / hi4 | 0x80808080).  SWAR on bytes < 0x80, no borrows: bit 7 of each
+// byte of the result is set iff the byte is in the line.
+__device__ __forceinline__ uint32_t word_in_line(int j, uint32_t lo4, uint32_t hi4x) {
+  const uint32_t idx = 0x03020100u + 0x04040404u * (uint32_t)j;
+  return ((idx | 0x80808080u) - lo4) & (hi4x - idx) & 0x80808080u;
+}
+
+__global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
+                                                   const int64_t* __restrict__ line_start,
+                                                   const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
+                                                   int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
+  __shared__ DfaLds4 d;
+  dfa4_load(d);
+  for (int64_t l0 = (int64_t)blockIdx.x * DFA_TPB; l0 < L; l0 += (int64_t)gridDim.x * DFA_TPB) {
+    // buffer resource at the group's first line: offsets stay 32-bit (the group's short lines
+    // span < 1 MiB), reads past the text return 0 and never fault
+    const int64_t base = line_start[l0] & ~(int64_t)15;
+    const int64_t rem = nbytes - base;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(text + base), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
+    const int64_t l = l0 + threadIdx.x;
+    if (l >= L) continue;
+    const int64_t s = line_start[l], e = line_end[l];
+    if (e - s > LONG_LINE) {
+      long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // a wave per long line (log_dfa_long)
+      continue;
+    }
+    uint32_t row = 0, acc = 0;
+    int off = (int)((s & ~(int64_t)3) - base);  // this block's first byte, from base
+    int rs_ = (int)(s & 3);                      // s - P: 0..3 at the first block, then negative
+    int re_ = (int)(e - (s & ~(int64_t)3));      // e - P
+    int ncp = rs_;                               // next code point start - P
+    const int end_off = (int)min(rem, (int64_t)INT32_MAX);
+    auto load = [&](int q) -> uint4 {
+      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, q, 0, 0));
+    };
+    // one block: cur holds bytes off .. off+15; the next block is loaded into nxt first (every
+    // lane, every block: the wait on cur is then never a wait on the load just issued)
+    auto block = [&](uint4& cur, uint4& nxt) -> bool {
+      nxt = load(off + 16);
+      uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+      if (off + 16 > end_off) {  // the text's last bytes (a buffer load straddling the end reads 0)
+#pragma unroll 1
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t b = off + k < end_off ? (uint32_t)text[base + off + k] : 0u;
+          w[k >> 2] = (w[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (b << (8 * (k & 3)));
+        }
+      }
+      const int lo = max(rs_, 0), hi = min(re_, 16);
+      const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = ((uint32_t)hi * 0x01010101u) | 0x80808080u;
+      uint32_t in[4], hib = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        in[j] = word_in_line(j, lo4, hi4x);
+        hib |= w[j] & in[j];
+      }
+      // all-ASCII line bytes and no code point running in from the last block (always so for
+      // valid UTF-8, whose continuation bytes are >= 0x80): byte table, no decode
+      if (!hib && ncp <= lo) {
+        uint32_t so[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = w[j] | (in[j] ^ 0x80808080u);  // outside the line: >= 0x80, NOP
+#pragma unroll
+          for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t t = dfa4_step(d, row, so[k]);
+          row = t;
+          acc |= t;
+        }
+        ncp = 16;
+      } else {  // code points, as the reference decodes them (rare: non-ASCII text)
+#pragma unroll 1
+        for (int k = 0; k < 16; ++k) {
+          if (k < ncp || k < lo || k >= hi) continue;
+          auto at = [&](int r) -> uint32_t {
+            if (r < 16) return (w[r >> 2] >> (8 * (r & 3))) & 0xFFu;
+            return off + r < end_off ? (uint32_t)text[base + off + r] : 0u;
+          };
+          uint32_t cp;
+          const uint32_t b = at(k);
+          int len;
+          if (b < 0x80) {
+            cp = b;
+            len = 1;
+          } else if (b < 0xE0) {
+            cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
+            len = 2;
+          } else if (b < 0xF0) {
+            cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
+            len = 3;
+          } else {
+            cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
+            len = 4;
+          }
+          uint32_t sy;
+          if (cp < 128) {
+            sy = d.sym[cp];
+          } else {
+            sy = KRCA_DFA_OTHER;
+            int a = 0, z = KRCA_DFA_NRANGE - 1;
+            while (a <= z) {
+              const int mid = (a + z) >> 1;
+              if (cp < krca_dfa_ranges[mid][0]) z = mid - 1;
+              else if (cp > krca_dfa_ranges[mid][1]) a = mid + 1;
+              else {
+                sy = krca_dfa_ranges[mid][2];
+                break;
+              }
+            }
+            sy *= 4;
+          }
+          const uint32_t t = dfa4_step(d, row, sy);
+          row = t;
+          acc |= t;
+          ncp = k + len;
+        }
+      }
+      const bool more = re_ > 16;
+      off += 16;
+      rs_ -= 16;
+      re_ -= 16;
+      ncp -= 16;
+      return more;
+    };
+    if (s < e) {
+      uint4 A = load(off), B;
+      while (block(A, B) && block(B, A)) {
+      }
+    }
+    line_mask[l] = acc >> 16;
   }
 }
 
@@ -948,9 +1136,15 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, n_lines, line_end);
     KRCA_LAUNCH_CHECK();
-    const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, DFA_TPB), 256 * 4);
-    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, n_lines,
-                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    if (impl == 2) {  // A/B: the round-1 walk (16-byte window, code point per step)
+      const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, DFA_TPB), 256 * 4);
+      hipLaunchKernelGGL(log_dfa_window, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, n_lines,
+                         (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    } else {  // persistent: the 50 KB table is filled once per workgroup, 3 workgroups per CU
+      const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, DFA_TPB), 256 * 3);
+      hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, n_lines,
+                         (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    }
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,
                        (const int64_t*)line_end, line_mask, (const int32_t*)long_q, (const int32_t*)n_long);

@@ -197,14 +197,32 @@ def test_log_scan_impls_identical(eng, monkeypatch):
     blob, off = pack_documents(docs)
     tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
     out = {}
-    for impl in ("0", "1"):
+    for impl in ("0", "1", "2"):
         with native.tune(eng.lib, KRCA_LOG_IMPL=int(impl)):
             r = eng.log_scan_device(tb, toff)
             out[impl] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
-    assert out["0"].keys() == out["1"].keys()
-    for k in out["0"]:
-        assert np.array_equal(out["0"][k], out["1"][k]), k
+    for other in ("1", "2"):
+        assert out["0"].keys() == out[other].keys()
+        for k in out["0"]:
+            assert np.array_equal(out["0"][k], out[other][k]), (other, k)
     _check_docs(eng, docs)
+
+
+def test_log_scan_block_edges(eng):
+    """log_dfa walks 16-byte blocks from each line's 4-byte-aligned start: lines starting at every
+    offset mod 16, multi-byte code points (2, 3 and 4 bytes, case folds) straddling block and word
+    edges, matches ending on the last byte of a block, and texts ending at every offset mod 16
+    (the buffer load straddling the text's end)."""
+    docs = []
+    for k in range(20):
+        for cp in ("é", "€", "\U0001d400", "\u212a", "ſ"):
+            docs.append("a" * k + cp + "Error" + "\n" + "b" * (k % 7) + "Killed" + cp * 3)
+        docs.append("c" * k + "timeout")  # a match ending at every offset
+        docs.append(" " * (k % 5) + "\u212aILLED " + "x" * k + "secret not found")
+    _check_docs(eng, docs)
+    for tail in range(17):
+        _check_docs(eng, ["z" * 11 + "\n" + "Error" * 3 + "q" * tail])
+        _check_docs(eng, ["y" * (37 + tail) + "é" + "panic:"])
 
 
 def test_log_scan_synthetic_large(eng):
