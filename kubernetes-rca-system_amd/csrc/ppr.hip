@@ -11,11 +11,19 @@
 // so the result does not depend on the summation order, on atomics or on the number of GPUs,
 // and is bit-identical to oracle/krca_oracle.c.
 //
+// Gathered weights: w_j = floor(r_j * alpha / outdeg_j) is stored as a 32-bit code (wenc: 26
+// significant bits and a 6-bit shift, truncating; wdec restores the int64 it stands for), so the
+// table every row gathers from is 4 bytes per node: at C4 (1M pods) 4 MB, the size of one XCD's
+// L2, instead of 8 MB.  The rank update still sums int64 (the decoded codes), so sums stay exact
+// and order-free; oracle/krca_oracle.c applies the same code.  Relative rounding <= 2^-25 per
+// weight (networkx parity is asserted at 1e-5).
+//
 // Sharding: rank g of G owns the contiguous node range [g*n_max, ...) and the
-// pull-CSR rows of those nodes.  Each iteration ends with ONE exchange: every rank's slice
-// [w_local (n_max int64) | NSLOT partial-sum slots] is all-gathered (RCCL over xGMI, driven by
-// the host: krca/rca.py) into w_all[G][n_max+NSLOT]; the column indices are pre-remapped to that
-// layout (col' = j + NSLOT*(j / n_max)), so the step kernel gathers directly.  At G = 1 the
+// pull-CSR rows of those nodes.  Each iteration ends with ONE exchange: every rank's slice of
+// krca_ppr_slice_words(n_max) int64 words — [codes (n_max uint32, padded to 8 bytes) | NSLOT
+// partial-sum slots] — is all-gathered (RCCL over xGMI, driven by the host: krca/rca.py) into
+// w_all[G][slice]; the column indices are pre-remapped to that layout in uint32 units (col' = j +
+// (j / n_max) * (2 * slice - n_max)), so the step kernel gathers directly.  At G = 1 the
 // "exchange" is a swap of two such buffers (ping-pong), no copy.
 //
 // One iteration = ppr_step (pull SpMV fused with the rank update) + ppr_reduce (one block).
@@ -90,6 +98,24 @@ __device__ __forceinline__ int64_t edge_weight(int64_t rj, int32_t deg, double a
   return (int64_t)((double)rj * coef);
 }
 
+// 32-bit weight code: w < 2^26 as is; above, the top 26 bits (bit 25 set) and the shift in the top
+// 6 bits (w < 2^61, so the shift is <= 35).  Decoding is one mask and one 64-bit shift.
+__host__ __device__ __forceinline__ uint32_t wenc(int64_t w) {
+  if (w < ((int64_t)1 << 26)) return (uint32_t)w;
+  const int sh = 63 - __builtin_clzll((unsigned long long)w) - 25;
+  return ((uint32_t)sh << 26) | (uint32_t)(w >> sh);
+}
+__host__ __device__ __forceinline__ int64_t wdec(uint32_t c) { return (int64_t)(c & 0x3FFFFFFu) << (c >> 26); }
+
+// one rank's exchange slice in int64 words: the n_max codes (uint32, padded to 8 bytes), then the
+// NSLOT partial-sum slots at int64 offset wslots(n_max)
+__host__ __device__ __forceinline__ int64_t wslots(int64_t n_max) { return (n_max + 1) / 2; }
+__host__ __device__ __forceinline__ int64_t slice_words(int64_t n_max) { return wslots(n_max) + NSLOT; }
+// uint32 index of node j's code in w_all
+__host__ __device__ __forceinline__ int64_t remap_col(int64_t j, int64_t n_max) {
+  return j + (j / n_max) * (2 * slice_words(n_max) - n_max);
+}
+
 __device__ __forceinline__ int64_t quantise(float s, float floor_) {
   const double v = (double)s - (double)floor_;
   return v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
@@ -109,14 +135,14 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
     q[i] = qi;
     qs += qi;
     r[i] = r0;
-    send[i] = edge_weight(r0, deg, alpha);
+    reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(r0, deg, alpha));
     if (deg == 0) dang += r0;
   }
   dang = block_sum_i64(dang, red);
   qs = block_sum_i64(qs, red);
   if (threadIdx.x == 0) {
-    add_slot(send + n_max + NSPREAD, dang);
-    add_slot(send + n_max + 2 * NSPREAD, qs);
+    add_slot(send + wslots(n_max) + NSPREAD, dang);
+    add_slot(send + wslots(n_max) + 2 * NSPREAD, qs);
   }
 }
 
@@ -134,14 +160,14 @@ __global__ __launch_bounds__(TPB) void ppr_init_warm(const float* __restrict__ s
     q[i] = qi;
     qs += qi;
     const int64_t ri = r[i];
-    send[i] = edge_weight(ri, deg, alpha);
+    reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(ri, deg, alpha));
     if (deg == 0) dang += ri;
   }
   dang = block_sum_i64(dang, red);
   qs = block_sum_i64(qs, red);
   if (threadIdx.x == 0) {
-    add_slot(send + n_max + NSPREAD, dang);
-    add_slot(send + n_max + 2 * NSPREAD, qs);
+    add_slot(send + wslots(n_max) + NSPREAD, dang);
+    add_slot(send + wslots(n_max) + 2 * NSPREAD, qs);
   }
 }
 
@@ -164,7 +190,7 @@ __device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi
   if (FLAGS & PPR_WRITE_R) r[i] = rn;
   if (FLAGS & PPR_RESIDUAL) err += rn > ro ? rn - ro : ro - rn;
   if (deg == 0) dang += rn;
-  send[i] = edge_weight(rn, deg, k.alpha);
+  reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(rn, deg, k.alpha));
 }
 
 // One plan entry, loaded in two parts so that a prefetched value is never copied or computed on
@@ -239,7 +265,7 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
   R.ix = *reinterpret_cast<const uint4*>(pk + wb + (tid * SEG < m.e1 - m.e0 ? tid * (SEG / 2) : 0));
 }
 
-__device__ __forceinline__ void gather(const Head& H, const int64_t* __restrict__ w, int64_t (&v)[SEG]) {
+__device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict__ w, uint32_t (&v)[SEG]) {
   const int64_t lim = H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0;
 #pragma unroll
   for (int j = 0; j < SEG; ++j) v[j] = threadIdx.x + j * TPB < lim ? w[H.c[j]] : 0;
@@ -268,10 +294,10 @@ __device__ unsigned long long g_ppr_timing[4096 * 5];  // per workgroup: stage, 
 template <int FLAGS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 8))) void ppr_step(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
-    const uint16_t* __restrict__ lane_info, int64_t nblk, const int64_t* __restrict__ w,
+    const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
     int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
-  __shared__ int64_t vals[EDGE_BUDGET];  // staged values: edge (direct) or slot (dictionary) i
+  __shared__ uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
   __shared__ __attribute__((aligned(16))) uint8_t headrow[EDGE_BUDGET];  // at a row's first edge: its row
   __shared__ unsigned long long rowsum[ROW_BUDGET];
   __shared__ int64_t red[TPB / 64];
@@ -289,7 +315,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   Head H0, H1;
   Rows R0, R1;
   load_head(plan, b, pk, H0);
-  int64_t v[SEG];
+  uint32_t v[SEG];  // codes: decoded where summed (a prefetched register is never computed on early)
   gather(H0, w, v);
   load_rows<FLAGS>(H0.m, b, lane_info, row_ptr, pk, outdeg, q, r, R0);
   Meta cur = H0.m;
@@ -323,7 +349,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       rowsum[tid] = 0ull;
     } else {
 #pragma unroll
-      for (int j = 0; j < SEG; ++j) sacc_long += v[j];
+      for (int j = 0; j < SEG; ++j) sacc_long += wdec(v[j]);
     }
     // v is free: gathers and rows of the next entry, head of the one after
     const int64_t b2 = b1 + gridDim.x;
@@ -348,7 +374,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
         for (int kk = 0; kk < SEG; ++kk) {
           const uint32_t wd = kk < 2 ? sx.x : kk < 4 ? sx.y : kk < 6 ? sx.z : sx.w;
           const int sl = dict ? (int)((wd >> (16 * (kk & 1))) & 0xFFFFu) : a + kk;
-          x[kk] = a + kk < ne ? vals[sl] : 0;
+          x[kk] = a + kk < ne ? wdec(vals[sl]) : 0;
         }
         int64_t sacc = 0;
 #pragma unroll
@@ -406,8 +432,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   err = block_sum_i64(err, red);
   dang = block_sum_i64(dang, red);
   if (tid == 0) {
-    add_slot(send + n_max, err);
-    add_slot(send + n_max + NSPREAD, dang);
+    add_slot(send + wslots(n_max), err);
+    add_slot(send + wslots(n_max) + NSPREAD, dang);
   }
 }
 
@@ -419,7 +445,7 @@ __global__ __launch_bounds__(TPB) void ppr_reduce(const int64_t* __restrict__ w_
   __shared__ int64_t red[TPB / 64];
   int64_t part[3] = {0, 0, 0};
   for (int i = threadIdx.x; i < G * NSPREAD; i += TPB) {
-    const int64_t* s = w_all + (int64_t)(i / NSPREAD) * (n_max + NSLOT) + n_max + (i % NSPREAD);
+    const int64_t* s = w_all + (int64_t)(i / NSPREAD) * slice_words(n_max) + wslots(n_max) + (i % NSPREAD);
     part[0] += s[0];
     part[1] += s[NSPREAD];
     part[2] += s[2 * NSPREAD];
@@ -428,7 +454,7 @@ __global__ __launch_bounds__(TPB) void ppr_reduce(const int64_t* __restrict__ w_
   const int64_t dang = block_sum_i64(part[1], red);
   const int64_t qs = block_sum_i64(part[2], red);
   __syncthreads();
-  if (threadIdx.x < NSLOT) send_next[n_max + threadIdx.x] = 0;
+  if (threadIdx.x < NSLOT) send_next[wslots(n_max) + threadIdx.x] = 0;
   if (threadIdx.x != 0 || ctl->converged) return;
   if (first) {
     ctl->q_total = qs;
@@ -460,7 +486,7 @@ __global__ __launch_bounds__(TPB) void remap_cols(const int32_t* __restrict__ co
                                                   int32_t* __restrict__ out) {
   for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < E; e += (int64_t)gridDim.x * TPB) {
     const int64_t j = col[e];
-    out[e] = (int32_t)(j + NSLOT * (j / n_max));
+    out[e] = (int32_t)remap_col(j, n_max);
   }
 }
 
@@ -498,12 +524,12 @@ int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out) {
 }
 
 // host: the plan of build_plan plus the packed column array pk[E] (include/krca.h krca_ppr_pack):
-// columns remapped to the [G][n_max + NSLOT] exchange layout; a short-row block whose distinct
+// columns remapped to the [G][slice] exchange layout (uint32 units); a short-row block whose distinct
 // columns fit becomes a dictionary block (sorted distinct columns, then uint16 slots per edge),
 // every other block stays direct.  Returns the number of dictionary blocks.
 int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_max, int64_t* plan, int64_t plan_len,
                     int32_t* pk, uint16_t* lane) {
-  auto remap = [n_max](int64_t j) { return (int32_t)(j + NSLOT * (j / n_max)); };
+  auto remap = [n_max](int64_t j) { return (int32_t)remap_col(j, n_max); };
   std::vector<int32_t> uniq;
   std::vector<uint16_t> slot;
   std::vector<int16_t> head;  // block-relative row starting at each edge (-1: none)
@@ -562,6 +588,7 @@ unsigned grid_for(int64_t n, int64_t cap = 2048) {
 extern "C" {
 
 int32_t krca_ppr_nslot(void) { return NSLOT; }
+int64_t krca_ppr_slice_words(int64_t n_max) { return n_max > 0 ? slice_words(n_max) : 0; }
 
 int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N) {
   if (!row_ptr_host || N <= 0) return 0;
@@ -612,7 +639,7 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
   KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)), "krca_ppr_shard_init: null pointer");
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
-  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
+  KRCA_HIP(hipMemsetAsync(send + wslots(n_max), 0, NSLOT * sizeof(int64_t), st));
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N,
                        alpha, q_local, r_local, send, n_max);
@@ -629,7 +656,7 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
                  "krca_ppr_shard_init_warm: null pointer");
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
-  KRCA_HIP(hipMemsetAsync(send + n_max, 0, NSLOT * sizeof(int64_t), st));
+  KRCA_HIP(hipMemsetAsync(send + wslots(n_max), 0, NSLOT * sizeof(int64_t), st));
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init_warm, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local,
                        alpha, q_local, r_local, send, n_max);
@@ -663,7 +690,7 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
   auto kern = (flags & KRCA_PPR_RESIDUAL) ? ppr_step<PPR_RESIDUAL | PPR_WRITE_R>
                : (flags & KRCA_PPR_WRITE_R) ? ppr_step<PPR_WRITE_R> : ppr_step<0>;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, lane, nblk,
-                     w_all, outdeg, q_local, n_local, N, alpha, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
+                     reinterpret_cast<const uint32_t*>(w_all), outdeg, q_local, n_local, N, alpha, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -706,9 +733,9 @@ int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key
   return KRCA_OK;
 }
 
-// workspace: ctl (krca_ppr_ctl_size(N), zeroed here once) | q[N] | w0[N+NSLOT] | w1[N+NSLOT] | r[N]
+// workspace: ctl (krca_ppr_ctl_size(N), zeroed here once) | q[N] | w0[slice(N)] | w1[slice(N)] | r[N]
 int64_t krca_ppr_workspace_size(int64_t N) {
-  return krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256 + (4 * N + 2 * NSLOT) * 8 + 256;
+  return krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256 + (2 * N + 2 * slice_words(N)) * 8 + 256;
 }
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int64_t* plan,
@@ -722,8 +749,8 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   const int64_t ctl_bytes = krca::ceil_div(krca_ppr_ctl_size(N), 256) * 256;
   char* p = ctl + ctl_bytes;
   int64_t* q = q_out ? q_out : reinterpret_cast<int64_t*>(p);
-  int64_t* wb[2] = {reinterpret_cast<int64_t*>(p + N * 8), reinterpret_cast<int64_t*>(p + (2 * N + NSLOT) * 8)};
-  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + (3 * N + 2 * NSLOT) * 8);
+  int64_t* wb[2] = {reinterpret_cast<int64_t*>(p + N * 8), reinterpret_cast<int64_t*>(p + (N + slice_words(N)) * 8)};
+  int64_t* r = r_fixed ? r_fixed : reinterpret_cast<int64_t*>(p + (N + 2 * slice_words(N)) * 8);
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
   int rc = krca_ppr_shard_init(seed, seed_floor, outdeg, N, N, N, alpha, ctl, q, r, wb[0], stream);

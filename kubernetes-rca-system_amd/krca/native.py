@@ -66,6 +66,7 @@ SIGNATURES = {
     "krca_ppr": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_f64, c_i32, c_f64, c_vp, c_vp,
                          c_vp, c_vp, ctypes.POINTER(c_i32), c_vp]),
     "krca_ppr_nslot": (c_i32, []),
+    "krca_ppr_slice_words": (c_i64, [c_i64]),
     "krca_ppr_ctl_size": (c_i64, [c_i64]),
     "krca_ppr_remap_cols": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "krca_ppr_shard_init": (c_i32, [c_vp, c_f32, c_vp, c_i64, c_i64, c_i64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -9,8 +9,8 @@ and ranks pods by propagated mass x own anomaly (krca_ppr_rca_key + krca_topk_i6
 Multi-GPU: one process per GPU; rank g owns pods [g*n_max, (g+1)*n_max): its
 slice of the metric tensor and its rows of the pull-CSR.  Scoring needs no communication.  Each
 PageRank iteration ends with ONE all-gather over RCCL/xGMI of every rank's
-[w_local | partial-sum slots] slice (n_max + NSLOT int64: residual, dangling mass and seed total,
-NSPREAD slots each); the partial sums ride in the same payload and every rank reduces them
+[weight codes | partial-sum slots] slice (slice_words(n_max) int64: the n_max 32-bit weight codes,
+then residual, dangling mass and seed total, NSPREAD slots each); the partial sums ride in the same payload and every rank reduces them
 identically, so no extra collective or broadcast is needed.  With one rank the exchange is a swap
 of two buffers (the step kernel reads one and writes the other).  Arithmetic is integer fixed
 point: the result is bit-identical for any G and to oracle/krca_oracle.c.  The final top-k merges G x k candidates.
@@ -25,6 +25,22 @@ import numpy as np
 
 NSPREAD = 32
 NSLOT = 3 * NSPREAD  # == krca_ppr_nslot()
+
+
+def wslots(n_max):
+    """int64 offset of the partial-sum slots in a rank's exchange slice (after n_max uint32 codes)."""
+    return (n_max + 1) // 2
+
+
+def slice_words(n_max):
+    """int64 words of one rank's exchange slice (== krca_ppr_slice_words)."""
+    return wslots(n_max) + NSLOT
+
+
+def remap_cols(col, n_max):
+    """uint32 index of node j's weight code in w_all[G][slice] (csrc/ppr.hip remap_col)."""
+    col = np.asarray(col, np.int64)
+    return col + (col // n_max) * (2 * slice_words(n_max) - n_max)
 
 
 def shard_range(N, world, rank):
@@ -136,9 +152,9 @@ class DeviceShard:
         self.q = torch.zeros(max(self.n, 1), **i64)
         self.r = torch.zeros(max(self.n, 1), **i64)
         self.key = torch.zeros(max(self.n, 1), **i64)
-        self.send = torch.zeros(n_max + NSLOT, **i64)
+        self.send = torch.zeros(slice_words(n_max), **i64)
         # G = 1: ping-pong pair (the step reads w_all, writes send; the exchange swaps them)
-        self.w_all = torch.zeros((1 if world == 1 else world) * (n_max + NSLOT), **i64)
+        self.w_all = torch.zeros((1 if world == 1 else world) * slice_words(n_max), **i64)
         self.ctl = torch.zeros(lib.krca_ppr_ctl_size(self.n), dtype=torch.uint8, device=dev)
         self.score_out = None
 

@@ -88,12 +88,21 @@ static int64_t edge_weight(int64_t rj, int32_t deg, double alpha) {
   return (int64_t)((double)rj * coef);
 }
 
+/* the 32-bit weight code the rows gather (csrc/ppr.hip wenc / wdec): w < 2^26 as is, above that
+ * the top 26 bits and the shift in the top 6 bits (truncating) */
+static uint32_t wenc(int64_t w) {
+  if (w < ((int64_t)1 << 26)) return (uint32_t)w;
+  const int sh = 63 - __builtin_clzll((unsigned long long)w) - 25;
+  return ((uint32_t)sh << 26) | (uint32_t)(w >> sh);
+}
+static int64_t wdec(uint32_t c) { return (int64_t)(c & 0x3FFFFFFu) << (c >> 26); }
+
 /* Pull-CSR personalized PageRank; returns iterations (negative if no convergence).
  * warm != 0: r holds the start vector on entry (krca_ppr_shard_init_warm), else r0 = 2^60/N. */
 int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
                        const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r,
                        float* r_out, int64_t* q, int warm) {
-  int64_t* w = (int64_t*)malloc(sizeof(int64_t) * N);
+  uint32_t* w = (uint32_t*)malloc(sizeof(uint32_t) * N);
   int64_t qtot = 0, dang = 0;
   const int64_t r0 = (int64_t)(kFix / (double)N);
   for (int64_t i = 0; i < N; ++i) {
@@ -101,7 +110,7 @@ int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t
     q[i] = v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
     qtot += q[i];
     if (!warm) r[i] = r0;
-    w[i] = edge_weight(r[i], outdeg[i], alpha);
+    w[i] = wenc(edge_weight(r[i], outdeg[i], alpha));
     if (outdeg[i] == 0) dang += r[i];
   }
   const double err_limit = tol > 0.0 ? (double)N * tol * kFix : 0.0;
@@ -112,7 +121,7 @@ int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t
 #pragma omp parallel for schedule(dynamic, 1024)
     for (int64_t i = 0; i < N; ++i) {
       int64_t s = 0;
-      for (int64_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) s += w[col[e]];
+      for (int64_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) s += wdec(w[col[e]]);
       acc[i] = s;
     }
     int64_t err = 0, dn = 0;
@@ -126,7 +135,7 @@ int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t
       r[i] = rn;
       err += rn > ro ? rn - ro : ro - rn;
       if (outdeg[i] == 0) dn += rn;
-      w[i] = edge_weight(rn, outdeg[i], alpha);
+      w[i] = wenc(edge_weight(rn, outdeg[i], alpha));
     }
     ++it;
     if (err_limit > 0.0 && (double)err < err_limit) {

@@ -11,17 +11,31 @@ import numpy as np
 import torch
 
 import oracle
-from krca.rca import NSLOT, NSPREAD
+from krca.rca import NSPREAD, remap_cols, slice_words, wslots
 
 FIX = 1152921504606846976.0
 
 
 def _w(r, deg, alpha):
-    out = np.zeros(len(r), np.int64)
+    """Weight codes (csrc/ppr.hip wenc) of floor(r * alpha / deg)."""
+    w = np.zeros(len(r), np.int64)
     nz = deg > 0
     coef = alpha / deg[nz].astype(np.float64)
-    out[nz] = (r[nz].astype(np.float64) * coef).astype(np.int64)
+    w[nz] = (r[nz].astype(np.float64) * coef).astype(np.int64)
+    out = w.astype(np.uint32)
+    big = w >= (1 << 26)
+    sh = np.zeros(len(w), np.int64)
+    sh[big] = np.floor(np.log2(w[big].astype(np.float64))).astype(np.int64) - 25
+    # log2 of a float64 can land one off near powers of two: fix up with exact integer tests
+    sh[big] += (w[big] >> (sh[big] + 25)) >= 2
+    sh[big] -= (w[big] >> (sh[big] + 25)) < 1
+    out[big] = ((sh[big] << 26) | (w[big] >> sh[big])).astype(np.uint32)
     return out
+
+
+def _wdec(c):
+    c = c.astype(np.int64)
+    return (c & 0x3FFFFFF) << (c >> 26)
 
 
 class NumpyShard:
@@ -30,12 +44,13 @@ class NumpyShard:
         self.x = np.asarray(x_local, np.float32)
         self.rp = np.asarray(row_ptr_local, np.int64)
         c = np.asarray(col_local, np.int64)
-        self.col = c + NSLOT * (c // n_max)
+        self.col = remap_cols(c, n_max)
         self.deg = np.asarray(outdeg_local, np.int32)
         self.n = len(self.deg)
         self.rows = np.repeat(np.arange(self.n), np.diff(self.rp))
-        self.send = torch.zeros(n_max + NSLOT, dtype=torch.int64)
-        self.w_all = torch.zeros((1 if world == 1 else world) * (n_max + NSLOT), dtype=torch.int64)
+        self.ws = wslots(n_max)
+        self.send = torch.zeros(slice_words(n_max), dtype=torch.int64)
+        self.w_all = torch.zeros((1 if world == 1 else world) * slice_words(n_max), dtype=torch.int64)
         self.ctl = {}
 
     def score(self):
@@ -49,19 +64,19 @@ class NumpyShard:
         r0 = np.int64(FIX / float(self.N))
         self.r = np.full(self.n, r0, np.int64)
         snd = self.send.numpy()
-        snd[self.n_max:] = 0
-        snd[:self.n] = _w(self.r, self.deg, alpha)
-        snd[self.n_max + NSPREAD] = int(self.r[self.deg == 0].sum())
-        snd[self.n_max + 2 * NSPREAD] = int(self.q.sum())
+        snd[self.ws:] = 0
+        snd.view(np.uint32)[:self.n] = _w(self.r, self.deg, alpha)
+        snd[self.ws + NSPREAD] = int(self.r[self.deg == 0].sum())
+        snd[self.ws + 2 * NSPREAD] = int(self.q.sum())
         self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
 
     def step(self, alpha, flags=3):
         """Pull SpMV fused with the update: reads w_all, writes r and send (krca_ppr_shard_step)."""
         if self.ctl["converged"]:
             return
-        w = self.w_all.numpy()
+        w = self.w_all.numpy().view(np.uint32)
         acc = np.zeros(self.n, np.int64)
-        np.add.at(acc, self.rows, w[self.col])
+        np.add.at(acc, self.rows, _wdec(w[self.col]))
         qt = self.ctl["q_total"]
         pd = self.q.astype(np.float64) / float(qt) if qt > 0 else np.full(self.n, 1.0 / float(self.N))
         t = (pd * self.ctl["tele"]).astype(np.int64)
@@ -69,14 +84,14 @@ class NumpyShard:
         err = int(np.abs(rn - self.r).sum())
         self.r = rn
         snd = self.send.numpy()
-        snd[:self.n] = _w(rn, self.deg, alpha)
-        snd[self.n_max] += err
-        snd[self.n_max + NSPREAD] += int(rn[self.deg == 0].sum())
+        snd.view(np.uint32)[:self.n] = _w(rn, self.deg, alpha)
+        snd[self.ws] += err
+        snd[self.ws + NSPREAD] += int(rn[self.deg == 0].sum())
 
     def reduce(self, alpha, tol, first):
-        w = self.w_all.numpy().reshape(self.world, self.n_max + NSLOT)[:, self.n_max:]
+        w = self.w_all.numpy().reshape(self.world, slice_words(self.n_max))[:, self.ws:]
         err, dang, qs = (int(w[:, i * NSPREAD:(i + 1) * NSPREAD].sum()) for i in range(3))
-        self.send.numpy()[self.n_max:] = 0
+        self.send.numpy()[self.ws:] = 0
         c = self.ctl
         if c["converged"]:
             return
@@ -118,10 +133,10 @@ class NumpyShard:
         v = s.astype(np.float64) - np.float64(np.float32(floor))
         self.q = np.where(v > 0, (np.maximum(v, 0) * 4294967296.0).astype(np.int64), 0)
         snd = self.send.numpy()
-        snd[self.n_max:] = 0
-        snd[:self.n] = _w(self.r, self.deg, alpha)
-        snd[self.n_max + NSPREAD] = int(self.r[self.deg == 0].sum())
-        snd[self.n_max + 2 * NSPREAD] = int(self.q.sum())
+        snd[self.ws:] = 0
+        snd.view(np.uint32)[:self.n] = _w(self.r, self.deg, alpha)
+        snd[self.ws + NSPREAD] = int(self.r[self.deg == 0].sum())
+        snd[self.ws + 2 * NSPREAD] = int(self.q.sum())
         self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
 
     def ctl_read(self):

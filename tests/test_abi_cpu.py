@@ -32,8 +32,10 @@ def test_version_and_host_helpers():
     assert lib.krca_log_index_size(1 << 30) > lib.krca_log_index_size(1 << 20)
     assert lib.krca_topk_workspace_size(1 << 20, 10) > 0
     assert lib.krca_ppr_workspace_size(1000) >= 4 * 1000 * 8
-    from krca.rca import NSLOT
+    from krca.rca import NSLOT, slice_words
     assert lib.krca_ppr_nslot() == NSLOT  # send-slice layout shared by the kernels and krca/rca.py
+    for n_max in (1, 2, 7, 1000, 999999):
+        assert lib.krca_ppr_slice_words(n_max) == slice_words(n_max)
     assert lib.krca_ppr_ctl_size(1000) >= 12 * 1000  # long-row accumulators + tickets
     assert lib.krca_group_max_rank() == 6  # 64-byte slot records: first, counts, 6 ranks
     assert lib.krca_template_huge_ws_size(5000) >= 2 * 5000 * 12  # distinct-hash table of >= 2n slots
@@ -110,7 +112,7 @@ def test_ppr_pack_decodes_to_the_remapped_columns():
     """krca_ppr_pack (host): every edge of every block decodes to its remapped column, through the
     block's sorted distinct-column list (dictionary blocks) or directly (direct / long-row blocks)."""
     from krca import synth
-    from krca.rca import NSLOT
+    from krca.rca import remap_cols
     lib = native.load_library()
     vp = ctypes.c_void_p
     m = synth.make_graph(6000, n_edges=120_000, seed=2)
@@ -124,7 +126,7 @@ def test_ppr_pack_decodes_to_the_remapped_columns():
         nd = lib.krca_ppr_pack(rp.ctypes.data_as(vp), col.ctypes.data_as(vp), len(rp) - 1, n_max,
                                plan.ctypes.data_as(vp), n, pk.ctypes.data_as(vp), lane.ctypes.data_as(vp))
         assert nd > 0.5 * (n // 4), nd  # most blocks of a service mesh are dictionary blocks
-        want = col.astype(np.int64) + NSLOT * (col.astype(np.int64) // n_max)
+        want = remap_cols(col, n_max)
         got = np.full(len(col), -1, np.int64)
         for bi, (h, code, e0, e1) in enumerate(plan.reshape(-1, 4)):
             nu = int(h) >> 32

@@ -55,13 +55,18 @@ def main():
     ne = plan[:, 3] - plan[:, 2]
     d = nu > 0
     edge_bytes = int(4 * nu[d].sum() + 2 * ne[d].sum() + 4 * ne[~d].sum())
-    # algorithmic bytes per iteration: plan + packed columns + row offsets +
-    # q, outdeg read + w written + w gathered once (compulsory); r is written on the last iteration
-    per_iter = 32 * len(plan) + edge_bytes + 8 * N + 8 * N + 4 * N + 8 * N + 8 * N
+    # algorithmic bytes per iteration: plan + lane info + packed columns + row
+    # offsets + q, outdeg read + weight codes written + codes gathered once (compulsory); r is
+    # written on the last iteration.  fabric_bytes_per_iter prices the gathered table once per XCD
+    # instead (8 XCDs, each with its own L2: the least an L2-miss counter can show for a table
+    # that every XCD's rows gather from at random).
+    base = 32 * len(plan) + 2 * 256 * len(plan) + edge_bytes + 8 * N + 8 * N + 4 * N + 4 * N
+    per_iter = base + 4 * N
+    fabric_per_iter = base + 8 * 4 * N
     out = dict(kernel="ppr propagate (init + 30 x (step + reduce))", dict=a.dict, pods=N, edges=E,
                dict_blocks=int(d.sum()), blocks=len(plan), gathers=int(nu[d].sum() + ne[~d].sum()),
                ms=ms, ms_median=float(np.median(ms)), us_per_iter=float(np.median(ms)) * 1e3 / cfg.iters,
-               bytes_per_iter=per_iter)
+               bytes_per_iter=per_iter, fabric_bytes_per_iter=fabric_per_iter)
     if a.check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
