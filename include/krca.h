@@ -140,9 +140,12 @@ int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspa
  * r(p,q) = Pearson over the T samples of metric channel `channel` of x[T][P][M] (population
  * std; a flat series correlates 0 with everything).  Per pod p: the k partners with the largest
  * |r| (self excluded, ties -> lower index) with r re-scored exactly (float64 over fp32 z), the
- * count of partners with |r| > tau taken on the fp16 MFMA screening product (within
- * krca_corr_eps(T) of exact), and cert[p] > 0 iff the reported set is provably the exact top-k
- * (csrc/corr.hip).  Buffers: mean/scale [P]; z32 [P*T]; zh [krca_corr_pad_rows(P) *
+ * exact count of partners with |r| > tau (the fp16 MFMA screening product decides every pair
+ * farther than krca_corr_eps(T) from tau; the pairs within it are re-scored in float64: fails with
+ * KRCA_EINVAL if more than 256*P + 2^20 pairs fall there, i.e. tau sits in the bulk of |r|), and
+ * cert[p] > 0 iff the reported set is provably the exact top-k (pods whose first merge cannot
+ * prove it have all their candidates re-scored; only a pod whose candidate buffer overflows twice
+ * reports -1) (csrc/corr.hip).  Buffers: mean/scale [P]; z32 [P*T]; zh [krca_corr_pad_rows(P) *
  * krca_corr_pad_steps(T)] (fp16 bits); cand [krca_corr_cand_size(P, T, k) 4-byte words]; count [P];
  * out_idx/out_val [P*k]; cert [P].  k <= krca_corr_max_k(), 2 <= P <= 2^22.  krca_corr_topk
  * synchronises the stream once (it reads how many candidate buffers overflowed to decide on the
@@ -164,8 +167,8 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
 int64_t krca_corr_shard_ws_size(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G);
 int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, int64_t lo, int64_t n_loc,
                            int32_t G, void* ws, float* phi, void* stream);
-int krca_corr_shard_tiles(const uint16_t* zh, int64_t P, int32_t T, int32_t k, float tau, int32_t G, int32_t g,
-                          const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt,
+int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, int32_t G,
+                          int32_t g, const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt,
                           void* stream);
 int krca_corr_shard_pack_sizes(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t n_max, void* ws,
                                int64_t* tot_host /*[G], synchronous*/, void* stream);

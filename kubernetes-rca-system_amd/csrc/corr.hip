@@ -30,9 +30,16 @@
 //
 // Error bound of the screening product (eps, host-computed): fp16 rounding of unit-norm rows
 // moves a dot product by <= 2^-10 (+ 2^-24 sqrt(T) from subnormals), fp32 accumulation of T
-// terms of a unit-norm product by <= T 2^-24.  It bounds the candidate pool and the |r| > tau
-// counts (pairs within eps of tau may land on either side); reported r values are exact.  The
-// sample and main passes run the same K loop, so a pair's screening value is the same bits in both.
+// terms of a unit-norm product by <= T 2^-24.  It bounds the candidate pool.  |r| > tau counts
+// are exact: a screening value above tau + eps counts at once, one within eps of tau is appended
+// to the AMBIGUOUS list and re-scored in float64 (corr_amb_rescore), one below tau - eps cannot
+// count.  Reported r values are exact.  The sample and main passes run the same K loop, so a
+// pair's screening value is the same bits in both.
+//
+//   deep merge         a pod whose certificate is <= 0 after the merge (near-ties around its k-th
+//                      partner) has ALL its candidates re-scored in float64 (corr_merge_deep):
+//                      everything outside the buffer is below phi, so the certificate becomes
+//                      (k-th exact |r|) - phi - eps > 0.
 #include <cmath>
 #include <cstdlib>
 #include <vector>
@@ -50,6 +57,11 @@ constexpr int KMAX = 16;  // largest k served
 constexpr int NSB = 16;   // 128-pod column blocks in the threshold sample (2048 pods)
 constexpr int NSL = NSB + 2;  // sample lists per pod: NSB sample blocks + the pod's own 256-block
 constexpr int CAPC = 1024;    // candidate buffer per pod (main pass appends)
+// ambiguous |r| ~ tau pairs re-scored for exact counts: capacity of the list (int2 entries)
+// (C3's random-walk series put ~130 partners per pod within eps of tau = 0.5: ~13M pairs at 100k,
+// ~170 in every 256 x 256 tile)
+__host__ __device__ inline int64_t amb_cap(int64_t P) { return 256 * P + (1 << 20); }
+constexpr int32_t AMB_BOTH = 1 << 30;  // entry.y flag: credit the partner's count as well
 // KC = candidates kept per (pod, sample block) in the sample pass: a template parameter >= k
 // (8, 12 or 16), so the k best sampled partners of a pod survive their blocks' cuts
 
@@ -192,7 +204,8 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
                                                  int32_t* __restrict__ samp_i, float* __restrict__ selfd,
                                                  int2* __restrict__ buf, int32_t* __restrict__ cnt,
                                                  int32_t* __restrict__ count, const int32_t* __restrict__ rect_pods,
-                                                 int64_t n_rect, Shard sh, int debug) {
+                                                 int64_t n_rect, Shard sh, int debug, float tau_lo,
+                                                 int2* __restrict__ amb, int32_t* __restrict__ amb_n) {
   constexpr bool SAMPLE = MODE == MODE_SAMPLE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t I, J;
@@ -339,6 +352,8 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     int* sccnt = srcnt + TB;
     int* spod = sccnt + TB;  // row pod ids
     int* wcount = spod + TB;  // candidate-list length per wave
+    int* wamb = wcount + 8;   // ambiguous entries in each wave's list
+    int* wbase = wamb + 8;    // their first slot in the ambiguous-pair list (-1: list full)
     {
       const int q = tid & (TB - 1);
       (tid < TB ? sphr : sphc)[q] = my_phi;
@@ -359,23 +374,44 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     // atomics, no waiting); past CAPW entries a hit goes to the global buffer directly (rare)
     int4* wlist = reinterpret_cast<int4*>(smem + EPI_LIST_OFF) + w * CAPW;
     int nlist = 0;  // wave-uniform
-    auto push = [&](bool hit, uint64_t m, int pod, int partner, float v) {
+    int namb = 0;   // wave-uniform: ambiguous entries in this wave's list
+    // entry tag: bit 0 = a candidate of `pod`; bit 1 / bit 2 = an ambiguous pair for the count
+    // (bit 1: credit both pods, bit 2: the row pod only, a diagonal tile holding both orders);
+    // bits 3.. = its rank among the wave's listed ambiguous pairs.  A tile's ambiguous pairs take
+    // ONE contiguous range of the global list (one atomic per workgroup: ~170 pairs per C3 tile,
+    // so a per-pair atomic on one counter would serialise), in the XCD-aware tile order that
+    // corr_amb_rescore then walks (rows of neighbouring tiles shared through the caches).  A pair
+    // past a full wave list (rare) takes a slot of its own.
+    auto amb_one = [&](int4 ent) {
+      const int slot = atomicAdd(amb_n, 1);
+      if (slot < amb_cap(P)) amb[slot] = make_int2(ent.x, ent.y | ((ent.w & 2) ? AMB_BOTH : 0));
+    };
+    auto flush_one = [&](int4 ent) {
+      if (ent.w & 6) amb_one(ent);
+      if (ent.w & 1) {
+        const int64_t lp = RECT ? ent.x - sh.lo : ent.x;
+        const int gs = atomicAdd(&cnt[lp], 1);
+        if (gs < CAPC) buf[lp * CAPC + gs] = make_int2(ent.z, ent.y);
+      }
+    };
+    auto push = [&](bool hit, uint64_t m, int pod, int partner, float v, int tag) {
       const int slot = nlist + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      const bool inl = hit && slot < CAPW;
+      const uint64_t mam = RECT ? 0ull : __ballot(inl && (tag & 6));
       if (hit) {
-        if (slot < CAPW) {
-          wlist[slot] = make_int4(pod, partner, __float_as_int(v), 0);
-        } else {
-          const int64_t lp = RECT ? pod - sh.lo : pod;
-          const int gs = atomicAdd(&cnt[lp], 1);
-          if (gs < CAPC) buf[lp * CAPC + gs] = make_int2(__float_as_int(v), partner);
-        }
+        const int ar = namb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mam >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)mam, 0u));
+        const int4 ent = make_int4(pod, partner, __float_as_int(v), tag | (inl && (tag & 6) ? ar << 3 : 0));
+        if (inl) wlist[slot] = ent;
+        else flush_one(ent);
       }
+      namb += __builtin_popcountll(mam);
       nlist += __builtin_popcountll(m);
     };
     int rcl0 = 0, rcl1 = 0;  // lane L collects the row counts of (i, e) = (L >> 4, L & 15)
     int colcnt[2] = {0, 0};
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int i = 0; i < 4; ++i) {
       float pr[16];
 #pragma unroll
@@ -398,14 +434,16 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const float a = fabsf(acc[i][j][e]);
-          if (!RECT) {
+          if (!RECT) {  // tau: the screening threshold tau + eps (certain hits)
             const bool hit = a > tau;
             const uint64_t m = __ballot(hit);
             rc[e][0] += __builtin_popcount((uint32_t)m);
             rc[e][1] += __builtin_popcount((uint32_t)(m >> 32));
             colcnt[j] += hit ? 1 : 0;
           }
-          me[e] = __ballot(a > fminf(pr[e], pc));
+          // a candidate of the row or column pod, or (main pass) within eps of the caller's tau
+          // a candidate of the row or column pod, or (main pass) within eps of the caller's tau
+          me[e] = __ballot(a > fminf(pr[e], pc) || (!RECT && a > tau_lo && a <= tau));
           any |= me[e];
         }
         // slow path, only for the value slots that hold a candidate: at C3 densities nearly every
@@ -421,10 +459,14 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
             const int gr = RECT ? spod[row] : (int)(rowA + row);
             const bool hr = a > pr[e] && gc < P && gc != gr;  // padding partners / zeroed self: r = 0
             const bool hc = a > pc && rowA + row < P;
-            const uint64_t mr = __ballot(hr);
-            if (mr) push(hr, mr, gr, gc, v);
+            // ambiguous for the count (main pass; padding and self excluded): rides the row entry
+            const bool am = !RECT && a > tau_lo && a <= tau && gc < P && rowA + row < P && gc != gr;
+            const bool hra = hr || am;
+            const uint64_t mr = __ballot(hra);
+            if (mr) push(hra, mr, gr, gc, v, (hr ? 1 : 0) | (am ? (diag ? 4 : 2) : 0));
             const uint64_t mc = __ballot(hc);
-            if (mc) push(hc, mc, gc, gr, v);
+            if (mc) push(hc, mc, gc, gr, v, 1);
+
           }
         }
       }
@@ -437,7 +479,10 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
       }
     }
     // reserve the buffer slots of every listed candidate at once (independent atomics in flight)
-    if (lane == 0) wcount[w] = nlist < CAPW ? nlist : CAPW;
+    if (lane == 0) {
+      wcount[w] = nlist < CAPW ? nlist : CAPW;
+      wamb[w] = namb;
+    }
     if (!RECT) {  // |r| > tau: one LDS add per row / column and wave
       const int li = lane >> 4, le = lane & 15;
       const int rbase = wr * 128 + li * 32 + (le & 3) + 8 * (le >> 2);
@@ -449,6 +494,20 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
           const int c = colcnt[j] + __shfl_xor(colcnt[j], 32, 64);
           if (h == 0 && c) atomicAdd(&sccnt[wc * 64 + j * 32 + r32], c);
         }
+      }
+    }
+    __syncthreads();
+    if (!RECT && tid == 0) {  // the tile's listed ambiguous pairs: one contiguous range
+      int tot = 0;
+      for (int u = 0; u < 8; ++u) tot += wamb[u];
+      int base = -1;
+      if (tot) {
+        base = atomicAdd(amb_n, tot);
+        if ((int64_t)base + tot > amb_cap(P)) base = -1;  // the list is full: the host reports it
+      }
+      for (int u = 0; u < 8; ++u) {
+        wbase[u] = base;
+        if (base >= 0) base += wamb[u];
       }
     }
     __syncthreads();
@@ -474,8 +533,11 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
             const bool ok = q < wcount[u0 + u];
             more = more || base + NT < wcount[u0 + u];
             ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(-1, 0, 0, 0);
+            const bool cand = ok && (ent[u].w & 1);
+            if (!RECT && ok && (ent[u].w & 6) && wbase[u0 + u] >= 0)  // an ambiguous pair
+              amb[wbase[u0 + u] + (ent[u].w >> 3)] = make_int2(ent[u].x, ent[u].y | ((ent[u].w & 2) ? AMB_BOTH : 0));
             if (RECT && ok) ent[u].x -= (int)sh.lo;  // rect pass: the rank's local buffers
-            gs[u] = ok ? atomicAdd(&cnt[ent[u].x], 1) : CAPC;
+            gs[u] = cand ? atomicAdd(&cnt[ent[u].x], 1) : CAPC;
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
@@ -588,6 +650,39 @@ __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, 
   if (lane == 0) phi[g] = selfd[g] < 0.25f ? 3.f : (kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f);
 }
 
+// ---- exact |r| > tau counts: the ambiguous pairs in list order, 16 lanes each (float4 loads of
+// the pair's two rows of z32), float64 accumulation, persistent over the device-held list length
+__global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__ amb, const int32_t* __restrict__ amb_n,
+                                                        int64_t P, const float* __restrict__ z32, int T, float tau,
+                                                        int32_t* __restrict__ count) {
+  const int sub = threadIdx.x & 15;
+  const int64_t n = min((int64_t)*amb_n, amb_cap(P));
+  const bool vec = (T & 3) == 0;
+  for (int64_t q = (int64_t)blockIdx.x * (TPB / 16) + (threadIdx.x >> 4); q < n; q += (int64_t)gridDim.x * (TPB / 16)) {
+    const int2 e = amb[q];
+    const int64_t a = e.x, b = e.y & (AMB_BOTH - 1);
+    const float* za = z32 + a * T;
+    const float* zb = z32 + b * T;
+    double acc = 0.0;
+    if (vec) {
+      const float4* va = reinterpret_cast<const float4*>(za);
+      const float4* vb = reinterpret_cast<const float4*>(zb);
+      for (int t = sub; t < T / 4; t += 16) {
+        const float4 x = va[t], y = vb[t];
+        acc += (double)x.x * (double)y.x + (double)x.y * (double)y.y + (double)x.z * (double)y.z +
+               (double)x.w * (double)y.w;
+      }
+    } else {
+      for (int t = sub; t < T; t += 16) acc += (double)za[t] * (double)zb[t];
+    }
+    for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+    if (sub == 0 && fabs(acc) > (double)tau) {
+      atomicAdd(&count[a], 1);
+      if (e.y & AMB_BOTH) atomicAdd(&count[b], 1);
+    }
+  }
+}
+
 // ---- merge + exact re-scoring ------------------------------------------------------------------
 __device__ __forceinline__ bool cbetter(float a, int32_t ia, float b, int32_t ib) {
   if (ib < 0) return ia >= 0;
@@ -614,7 +709,8 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
                                                   int64_t P, int T, int k, float eps, int pass,
                                                   const int32_t* __restrict__ pods, float* __restrict__ phi2,
                                                   int32_t* __restrict__ over, int32_t* __restrict__ out_i,
-                                                  float* __restrict__ out_v, float* __restrict__ cert, int64_t lo) {
+                                                  float* __restrict__ out_v, float* __restrict__ cert, int64_t lo,
+                                                  int32_t* __restrict__ deep) {
   __shared__ float cv[CAPC];
   __shared__ int32_t ci[CAPC];
   __shared__ float top_v[KM + 1];
@@ -729,8 +825,77 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
   if (tid == 0) {
     // everything not re-scored has a screening |r| <= max(phi, the first un-re-scored candidate)
     const float dropped = fmaxf(ph, top_i[km] >= 0 ? fabsf(top_v[km]) : 0.f);
-    cert[gl] = flat ? 1.f
-                   : overflow ? -1.f : (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
+    const float c = flat ? 1.f
+                         : overflow ? -1.f : (float)(fabs(exact[ord[k - 1]]) - (double)dropped - (double)eps);
+    cert[gl] = c;
+    // near-ties around the k-th: re-score every candidate (corr_merge_deep)
+    if (!(c > 0.f) && !flat && !overflow && n >= k) deep[1 + atomicAdd(&deep[0], 1)] = (int32_t)g;
+  }
+}
+
+// one workgroup per listed pod (its merge left cert <= 0): every buffered candidate re-scored in
+// float64 (one wave per candidate, the merge's fixed-order reduction), sorted by (|r| desc, index
+// asc), top k written.  Partners outside the buffer have a screening |r| <= phi, so the k-th exact
+// |r| minus phi minus eps certifies the set (> 0 whenever the buffer holds the k sampled partners).
+__global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ buf, const int32_t* __restrict__ cnt,
+                                                       const float* __restrict__ phi, const float* __restrict__ phi2,
+                                                       const float* __restrict__ z32,
+                                                       int T, int k, float eps, const int32_t* __restrict__ pods,
+                                                       int32_t* __restrict__ out_i, float* __restrict__ out_v,
+                                                       float* __restrict__ cert, int64_t lo) {
+  __shared__ double ex[CAPC];
+  __shared__ int32_t ci[CAPC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nd = pods[0];  // list length first (device-held: no host round trip)
+  for (int b = blockIdx.x; b < nd; b += gridDim.x) {
+  __syncthreads();  // ex / ci of the previous pod
+  const int64_t g = pods[1 + b];
+  const int64_t gl = g - lo;
+  const int n = min(cnt[gl], CAPC);
+  int np = 32;
+  while (np < n) np <<= 1;
+  for (int i = tid; i < np; i += TPB) ci[i] = i < n ? buf[gl * CAPC + i].y : -1;
+  __syncthreads();
+  const float* zg = z32 + g * T;
+  for (int c = w; c < np; c += TPB / 64) {
+    const int32_t j = ci[c];
+    double acc = 0.0;
+    if (j >= 0) {
+      const float* zj = z32 + (int64_t)j * T;
+      for (int t = lane; t < T; t += 64) acc += (double)zg[t] * (double)zj[t];
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    }
+    if (lane == 0) ex[c] = acc;
+  }
+  __syncthreads();
+  for (int kk = 2; kk <= np; kk <<= 1) {  // bitonic: |r| desc, index asc, empties last
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np; i += TPB) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool desc = (i & kk) == 0;
+          const double fa = fabs(ex[l]), fb = fabs(ex[i]);
+          const int32_t ia = ci[l], ib = ci[i];
+          const bool better = ib < 0 ? ia >= 0 : (ia >= 0 && (fa > fb || (fa == fb && ia < ib)));
+          if (better == desc) {
+            const double tv = ex[i];
+            ex[i] = ex[l];
+            ex[l] = tv;
+            ci[i] = ia;
+            ci[l] = ib;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int q = tid; q < k; q += TPB) {
+    out_i[gl * k + q] = ci[q];
+    out_v[gl * k + q] = (float)ex[q];
+  }
+  // the bound of the buffer: phi2 for a pod refilled by the rectangle pass (3 = not refilled)
+  const float ph = phi2[g] < 2.5f ? phi2[g] : phi[g];
+  if (tid == 0) cert[gl] = (float)(fabs(ex[k - 1]) - (double)ph - (double)eps);
   }
 }
 
@@ -787,6 +952,9 @@ struct CorrWs {  // views into a caller's candidate workspace
   int32_t* samp_i;
   float *selfd, *phi2;  // [P]
   int32_t* over;        // [n_loc + 1]
+  int32_t* deep;        // [n_loc + 1]: pods for corr_merge_deep (count first)
+  int2* amb;            // [amb_cap(P)] ambiguous pairs of the main pass (contiguous per tile)
+  int32_t* amb_n;       // [4]: their count (past the capacity: an error)
   uint16_t* zs;         // [RECT_ROWS][Tp]
   int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
   int32_t* fill;        // sharded: [n_loc]
@@ -809,6 +977,9 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   w.selfd = reinterpret_cast<float*>(take(P));
   w.phi2 = reinterpret_cast<float*>(take(P));
   w.over = reinterpret_cast<int32_t*>(take(n_loc + 1));
+  w.deep = reinterpret_cast<int32_t*>(take(n_loc + 1));
+  w.amb = reinterpret_cast<int2*>(take(2 * amb_cap(P)));
+  w.amb_n = reinterpret_cast<int32_t*>(take(4));
   w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
   if (G > 0) {
     w.lbuf = reinterpret_cast<int2*>(take(2 * n_loc * CAPC));
@@ -865,7 +1036,7 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES, st,
                      zh, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau, (const float*)nullptr, ws.samp_v, ws.samp_i,
                      ws.selfd, (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
-                     (int64_t)0, sh, 0);
+                     (int64_t)0, sh, 0, 2.f, (int2*)nullptr, (int32_t*)nullptr);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
                      ws.samp_i, ws.selfd, lo, lo + n, d.nsb, d.k, d.eps, phi);
@@ -875,21 +1046,29 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
 
 // 2. upper-triangle tiles (every G-th super-tile from g): appends into ws.buf, tau counts
 template <int KC>
-int stage_tiles(const uint16_t* zh, const Dims& d, int G, int g, const float* phi, const CorrWs& ws, int32_t* count,
-                int dbg, hipStream_t st) {
+int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int g, const float* phi, const CorrWs& ws,
+                int32_t* count, int dbg, hipStream_t st) {
   if (int rc = set_lds_attr<KC>()) return rc;
   KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetAsync(ws.amb_n, 0, 4 * sizeof(int32_t), st));
   const int64_t ns = (d.nb2 + SUPER - 1) / SUPER;
   const int64_t n_st = ns * (ns + 1) / 2;
   const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
   if (n_mine == 0) return KRCA_OK;
   const int64_t per_xcd = (n_mine * SUPER * SUPER + 7) / 8;
   const Shard sh{0, G, g, 0};
+  // screening counts: certain above tau + eps, re-scored within eps of tau (exact counts)
   hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, zh, d.P,
-                     d.Tp, d.nb2, per_xcd, d.nsb, d.tau, phi, (float*)nullptr, (int32_t*)nullptr, (float*)nullptr,
-                     ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, sh, dbg);
+                     d.Tp, d.nb2, per_xcd, d.nsb, d.tau + d.eps, phi, (float*)nullptr, (int32_t*)nullptr,
+                     (float*)nullptr, ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, sh, dbg,
+                     d.tau - d.eps, ws.amb, ws.amb_n);
   KRCA_LAUNCH_CHECK();
+  if (dbg == 0) {
+    hipLaunchKernelGGL(corr_amb_rescore, dim3(4096), dim3(TPB), 0, st, (const int2*)ws.amb, (const int32_t*)ws.amb_n,
+                       d.P, z32, d.T, d.tau, count);
+    KRCA_LAUNCH_CHECK();
+  }
   return KRCA_OK;
 }
 
@@ -903,14 +1082,31 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
   if (n == 0) return KRCA_OK;
   if (int rc = set_lds_attr<KC>()) return rc;
   KRCA_HIP(hipMemsetAsync(ws.over, 0, sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetAsync(ws.deep, 0, sizeof(int32_t), st));
   KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.phi2), 0x40400000 /* 3.0f */, (size_t)d.P, st));
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n), dim3(TPB), 0, st, (const int2*)lbuf, lcnt, phi, z32, d.P, d.T,
-                     d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo);
+                     d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo, ws.deep);
   KRCA_LAUNCH_CHECK();
-  int32_t n_over = 0;
+  int32_t n_over = 0, n_amb[4] = {0, 0, 0, 0};
   KRCA_HIP(hipMemcpyAsync(&n_over, ws.over, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  KRCA_HIP(hipMemcpyAsync(n_amb, ws.amb_n, sizeof(n_amb), hipMemcpyDeviceToHost, st));
   KRCA_HIP(hipStreamSynchronize(st));
-  if (n_over == 0 || dbg != 0) return KRCA_OK;
+  if (dbg == 0 && n_amb[0] > amb_cap(d.P)) {
+    krca::set_error("krca_corr: %d pairs have a screening |r| within eps = %.3g of tau = %g (capacity %lld): the "
+                    "|r| > tau counts cannot be made exact; use a tau farther from the bulk of |r|",
+                    n_amb[0], (double)d.eps, (double)d.tau, (long long)amb_cap(d.P));
+    return KRCA_EINVAL;
+  }
+  auto deep_pass = [&]() -> int {  // pods whose merge left cert <= 0 (device-held list)
+    hipLaunchKernelGGL(corr_merge_deep, dim3((unsigned)std::min<int64_t>(n, 2048)), dim3(TPB), 0, st,
+                       (const int2*)lbuf, (const int32_t*)lcnt, phi, (const float*)ws.phi2, z32, d.T, d.k, d.eps,
+                       (const int32_t*)ws.deep,
+                       out_idx, out_val, cert, lo);
+    KRCA_LAUNCH_CHECK();
+    return KRCA_OK;
+  };
+  if (dbg != 0) return KRCA_OK;
+  if (n_over == 0) return deep_pass();
   const Shard sh{lo, 1, 0, 0};
   for (int64_t r0 = 0; r0 < n_over; r0 += RECT_ROWS) {
     const int64_t nr = std::min<int64_t>(RECT_ROWS, n_over - r0);
@@ -921,14 +1117,15 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
     hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * d.nb2)), dim3(NT), LDS_BYTES, st,
                        (const uint16_t*)ws.zs, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau,
                        (const float*)ws.phi2, (float*)nullptr, (int32_t*)nullptr, (float*)nullptr, lbuf, lcnt,
-                       (int32_t*)nullptr, (const int32_t*)(ws.over + 1 + r0), nr, sh, 0);
+                       (int32_t*)nullptr, (const int32_t*)(ws.over + 1 + r0), nr, sh, 0, 2.f, (int2*)nullptr,
+                       (int32_t*)nullptr);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,
                      (const float*)ws.phi2, z32, d.P, d.T, d.k, d.eps, 1, (const int32_t*)(ws.over + 1), ws.phi2,
-                     ws.over, out_idx, out_val, cert, lo);
+                     ws.over, out_idx, out_val, cert, lo, ws.deep);
   KRCA_LAUNCH_CHECK();
-  return KRCA_OK;
+  return deep_pass();
 }
 
 template <int KC>
@@ -940,7 +1137,7 @@ int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, 
   float* phi = reinterpret_cast<float*>(cand + 4 * head);  // one more [P] after the layout
   const int dbg = debug_mode();
   if (int rc = stage_sample<KC>(zh, d, 0, d.P, ws, phi, st)) return rc;
-  if (int rc = stage_tiles<KC>(zh, d, 1, 0, phi, ws, count, dbg, st)) return rc;
+  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, st)) return rc;
   return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
 }
 
@@ -1023,16 +1220,18 @@ int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, 
   }
 }
 
-int krca_corr_shard_tiles(const uint16_t* zh, int64_t P, int32_t T, int32_t k, float tau, int32_t G, int32_t g,
-                          const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt, void* stream) {
+int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, int32_t G,
+                          int32_t g, const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt,
+                          void* stream) {
   KRCA_CORR_SHARD_ARGS("krca_corr_shard_tiles")
-  KRCA_CHECK_ARG(zh && phi && count && raw_cnt && g >= 0 && g < G && tau >= 0.f, "krca_corr_shard_tiles: bad args");
+  KRCA_CHECK_ARG(zh && z32 && phi && count && raw_cnt && g >= 0 && g < G && tau >= 0.f,
+                 "krca_corr_shard_tiles: bad args");
   const Dims d = dims_of(P, T, k, tau);
   int rc;
   switch (kc_for(k)) {
-    case 8: rc = stage_tiles<8>(zh, d, G, g, phi, w, count, 0, st); break;
-    case 12: rc = stage_tiles<12>(zh, d, G, g, phi, w, count, 0, st); break;
-    default: rc = stage_tiles<16>(zh, d, G, g, phi, w, count, 0, st);
+    case 8: rc = stage_tiles<8>(zh, z32, d, G, g, phi, w, count, 0, st); break;
+    case 12: rc = stage_tiles<12>(zh, z32, d, G, g, phi, w, count, 0, st); break;
+    default: rc = stage_tiles<16>(zh, z32, d, G, g, phi, w, count, 0, st);
   }
   if (rc) return rc;
   KRCA_HIP(hipMemcpyAsync(raw_cnt, w.cnt, (size_t)P * sizeof(int32_t), hipMemcpyDeviceToDevice, st));

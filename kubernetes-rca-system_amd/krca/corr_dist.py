@@ -110,7 +110,7 @@ class CorrShard:
     # -- phase 3: this rank's share of the upper triangle -----------------------------------------
     def tiles(self):
         e, p = self.eng, self.eng.ptr
-        self._chk(self.lib.krca_corr_shard_tiles(p(self.zh), self.P, self.T, self.k, self.tau, self.world, self.rank,
+        self._chk(self.lib.krca_corr_shard_tiles(p(self.zh), p(self.z32), self.P, self.T, self.k, self.tau, self.world, self.rank,
                                                  p(self.phi), self.n_loc, p(self.ws), p(self.count), p(self.raw),
                                                  e._stream()), "krca_corr_shard_tiles")
 

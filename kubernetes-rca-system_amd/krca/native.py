@@ -52,7 +52,7 @@ SIGNATURES = {
     "krca_corr_topk": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_corr_shard_ws_size": (c_i64, [c_i64, c_i32, c_i32, c_i64, c_i32]),
     "krca_corr_shard_sample": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
-    "krca_corr_shard_tiles": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_f32, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
+    "krca_corr_shard_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
                                       c_vp]),
     "krca_corr_shard_pack_sizes": (c_i32, [c_i64, c_i32, c_i32, c_i64, c_i32, c_i64, c_vp, ctypes.POINTER(c_i64),
                                            c_vp]),

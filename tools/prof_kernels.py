@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--docs", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tsteps", type=int, default=1440)
+    ap.add_argument("--tau", type=float, default=0.5)
     a = ap.parse_args()
     import torch
     from krca import native, synth
@@ -64,9 +65,9 @@ def main():
     elif a.what == "corr":
         x = synth.make_metrics(a.pods, 1, a.tsteps, device="cuda", group_size=20)
         z = eng.corr_prepare_device(x)
-        r = eng.corr_topk_device(z, 10, 0.5)
+        r = eng.corr_topk_device(z, 10, a.tau)
         ms_prep = timed(torch, lambda: eng.corr_prepare_device(x), a.reps)
-        ms = timed(torch, lambda: eng.corr_topk_device(z, 10, 0.5, out=r), a.reps)
+        ms = timed(torch, lambda: eng.corr_topk_device(z, 10, a.tau, out=r), a.reps)
         P, T = a.pods, a.tsteps
         flops = P * (P + 1) * T  # upper triangle incl. diagonal, 2 flops per MAC
         ws = eng._ws["corr_cand"].view(torch.int32)
