@@ -40,6 +40,7 @@ const NamedKnob* find_knob(const char* name) {
 }  // namespace
 
 const Tuning& tuning() { return g_tune; }
+int tuning_ppr_dict() { return g_tune.ppr_dict; }  // for the plain-C++ host units (ppr_pack.cpp)
 
 void set_error(const char* fmt, ...) {
   va_list ap;

@@ -54,5 +54,6 @@ struct Tuning {
   int corr_debug;   // KRCA_CORR_DEBUG: profiling aid (results wrong when != 0)
 };
 const Tuning& tuning();
+int tuning_ppr_dict();
 
 }  // namespace krca

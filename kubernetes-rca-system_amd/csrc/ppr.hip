@@ -42,17 +42,13 @@
 #include <vector>
 
 #include "krca_common.h"
+#include "ppr_layout.h"
 
 #pragma clang fp contract(off)
 
 namespace {
+using namespace pprl;
 
-constexpr int TPB = 256;
-constexpr int EDGE_BUDGET = 2048;       // edges per short block == LDS slots
-constexpr int ROW_BUDGET = TPB;         // rows per short block (one updating lane per row)
-constexpr int SEG = EDGE_BUDGET / TPB;  // edges per lane: gathered lane-strided, summed contiguous
-constexpr int NSPREAD = 32;             // partial-sum slots per quantity (spreads the atomics)
-constexpr int NSLOT = 3 * NSPREAD;      // send tail: residual[32] | dangling[32] | seed total[32]
 constexpr int PPR_RESIDUAL = KRCA_PPR_RESIDUAL;
 constexpr int PPR_WRITE_R = KRCA_PPR_WRITE_R;
 
@@ -64,7 +60,6 @@ struct Ctl {          // device control block (header of the ctl buffer)
 };
 // ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n].  The long-row
 // accumulators and tickets are zero when allocated and reset by the last chunk of each row.
-constexpr int CTL_BYTES = 256;
 
 __device__ __forceinline__ int64_t* acc_long_of(Ctl* ctl) {
   return reinterpret_cast<int64_t*>(reinterpret_cast<char*>(ctl) + CTL_BYTES);
@@ -98,23 +93,6 @@ __device__ __forceinline__ int64_t edge_weight(int64_t rj, int32_t deg, double a
   return (int64_t)((double)rj * coef);
 }
 
-// 32-bit weight code: w < 2^26 as is; above, the top 26 bits (bit 25 set) and the shift in the top
-// 6 bits (w < 2^61, so the shift is <= 35).  Decoding is one mask and one 64-bit shift.
-__host__ __device__ __forceinline__ uint32_t wenc(int64_t w) {
-  if (w < ((int64_t)1 << 26)) return (uint32_t)w;
-  const int sh = 63 - __builtin_clzll((unsigned long long)w) - 25;
-  return ((uint32_t)sh << 26) | (uint32_t)(w >> sh);
-}
-__host__ __device__ __forceinline__ int64_t wdec(uint32_t c) { return (int64_t)(c & 0x3FFFFFFu) << (c >> 26); }
-
-// one rank's exchange slice in int64 words: the n_max codes (uint32, padded to 8 bytes), then the
-// NSLOT partial-sum slots at int64 offset wslots(n_max)
-__host__ __device__ __forceinline__ int64_t wslots(int64_t n_max) { return (n_max + 1) / 2; }
-__host__ __device__ __forceinline__ int64_t slice_words(int64_t n_max) { return wslots(n_max) + NSLOT; }
-// uint32 index of node j's code in w_all
-__host__ __device__ __forceinline__ int64_t remap_col(int64_t j, int64_t n_max) {
-  return j + (j / n_max) * (2 * slice_words(n_max) - n_max);
-}
 
 __device__ __forceinline__ int64_t quantise(float s, float floor_) {
   const double v = (double)s - (double)floor_;
@@ -490,95 +468,6 @@ __global__ __launch_bounds__(TPB) void remap_cols(const int32_t* __restrict__ co
   }
 }
 
-// host: CSR-adaptive row blocks {rb, code, e0, e1} (code > 0: short rows [rb, code); code <= 0:
-// chunk -code of long row rb); returns the number of int64 entries (4 per block)
-int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out) {
-  int64_t n = 0;
-  int64_t r = 0;
-  auto put = [&](int64_t rb, int64_t code, int64_t e0, int64_t e1) {
-    if (out) {
-      out[n] = rb;
-      out[n + 1] = code;
-      out[n + 2] = e0;
-      out[n + 3] = e1;
-    }
-    n += 4;
-  };
-  while (r < N) {
-    const int64_t deg = rp[r + 1] - rp[r];
-    if (deg > EDGE_BUDGET) {
-      const int64_t chunks = krca::ceil_div(deg, EDGE_BUDGET);
-      for (int64_t c = 0; c < chunks; ++c) {
-        const int64_t e0 = rp[r] + c * EDGE_BUDGET;
-        put(r, -c, e0, std::min<int64_t>(rp[r + 1], e0 + EDGE_BUDGET));  // chunk 0 encodes as 0
-      }
-      r += 1;
-      continue;
-    }
-    int64_t re = r + 1;
-    while (re < N && re - r < ROW_BUDGET && rp[re + 1] - rp[r] <= EDGE_BUDGET) ++re;
-    put(r, re, rp[r], rp[re]);
-    r = re;
-  }
-  return n;
-}
-
-// host: the plan of build_plan plus the packed column array pk[E] (include/krca.h krca_ppr_pack):
-// columns remapped to the [G][slice] exchange layout (uint32 units); a short-row block whose distinct
-// columns fit becomes a dictionary block (sorted distinct columns, then uint16 slots per edge),
-// every other block stays direct.  Returns the number of dictionary blocks.
-int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_max, int64_t* plan, int64_t plan_len,
-                    int32_t* pk, uint16_t* lane) {
-  auto remap = [n_max](int64_t j) { return (int32_t)remap_col(j, n_max); };
-  std::vector<int32_t> uniq;
-  std::vector<uint16_t> slot;
-  std::vector<int16_t> head;  // block-relative row starting at each edge (-1: none)
-  int64_t ndict = 0;
-  for (int64_t p = 0; p < plan_len; p += 4) {
-    const int64_t rb = plan[p], code = plan[p + 1], e0 = plan[p + 2], e1 = plan[p + 3];
-    const int64_t ne = e1 - e0;
-    uint16_t* li = lane + (p / 4) * TPB;
-    for (int t = 0; t < TPB; ++t) li[t] = 0;
-    if (code > 0) {  // lane t: (row holding edge 8t) << 8 | head bits of its edges 8t .. 8t+7
-      head.assign(ne, -1);
-      for (int64_t rr = rb; rr < code; ++rr)
-        if (rp[rr + 1] > rp[rr]) head[rp[rr] - e0] = (int16_t)(rr - rb);
-      int cur_row = 0;
-      for (int64_t e = 0; e < ne; ++e) {
-        if (head[e] >= 0) cur_row = head[e];
-        const int t = (int)(e / SEG), k = (int)(e % SEG);
-        if (k == 0) li[t] = (uint16_t)(cur_row << 8);
-        if (head[e] >= 0) li[t] |= (uint16_t)(1u << k);
-      }
-    }
-    bool dict = false;
-    if (code > 0 && ne >= 32 && krca::tuning().ppr_dict) {
-      uniq.assign(col + e0, col + e1);
-      std::sort(uniq.begin(), uniq.end());
-      uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-      const int64_t nu = (int64_t)uniq.size();
-      const int64_t dw = ((e0 + nu + 3) & ~int64_t(3)) - e0;  // slot words start 16-byte aligned
-      dict = dw + 4 * krca::ceil_div(ne, SEG) <= ne;          // the lanes' 16-byte slot loads stay inside
-      if (dict) {
-        for (int64_t u = 0; u < nu; ++u) pk[e0 + u] = remap(uniq[u]);
-        for (int64_t u = nu; u < dw; ++u) pk[e0 + u] = 0;
-        slot.assign(krca::ceil_div(ne, SEG) * SEG, 0);
-        for (int64_t e = 0; e < ne; ++e)
-          slot[e] = (uint16_t)(std::lower_bound(uniq.begin(), uniq.end(), col[e0 + e]) - uniq.begin());
-        uint32_t* words = reinterpret_cast<uint32_t*>(pk + e0 + dw);
-        for (int64_t i = 0; i < (int64_t)slot.size() / 2; ++i)
-          words[i] = (uint32_t)slot[2 * i] | ((uint32_t)slot[2 * i + 1] << 16);
-        for (int64_t e = dw + (int64_t)slot.size() / 2; e < ne; ++e) pk[e0 + e] = 0;
-        plan[p] = rb | (nu << 32);
-        ++ndict;
-      }
-    }
-    if (!dict)
-      for (int64_t e = e0; e < e1; ++e) pk[e] = remap(col[e]);
-  }
-  return ndict;
-}
-
 unsigned grid_for(int64_t n, int64_t cap = 2048) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), cap));
 }
@@ -587,38 +476,6 @@ unsigned grid_for(int64_t n, int64_t cap = 2048) {
 
 extern "C" {
 
-int32_t krca_ppr_nslot(void) { return NSLOT; }
-int64_t krca_ppr_slice_words(int64_t n_max) { return n_max > 0 ? slice_words(n_max) : 0; }
-
-int64_t krca_ppr_plan_size(const int64_t* row_ptr_host, int64_t N) {
-  if (!row_ptr_host || N <= 0) return 0;
-  return build_plan(row_ptr_host, N, nullptr);
-}
-
-int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host, int64_t plan_len) {
-  KRCA_CHECK_ARG(row_ptr_host && plan_host && N > 0 && N < INT32_MAX, "krca_ppr_plan: bad arguments");
-  for (int64_t i = 0; i < N; ++i)
-    KRCA_CHECK_ARG(row_ptr_host[i + 1] >= row_ptr_host[i], "krca_ppr_plan: row_ptr not monotone at %lld", (long long)i);
-  const int64_t need = build_plan(row_ptr_host, N, nullptr);
-  KRCA_CHECK_ARG(plan_len == need, "krca_ppr_plan: plan_len %lld != %lld", (long long)plan_len, (long long)need);
-  build_plan(row_ptr_host, N, plan_host);
-  return KRCA_OK;
-}
-
-int64_t krca_ppr_lane_size(int64_t plan_len) { return plan_len / 4 * TPB; }
-
-int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
-                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host) {
-  KRCA_CHECK_ARG(row_ptr_host && plan_host && pk_host && lane_host && N > 0 && N < INT32_MAX && n_max > 0,
-                 "krca_ppr_pack: bad arguments");
-  const int64_t E = row_ptr_host[N];
-  KRCA_CHECK_ARG(E == 0 || col_host, "krca_ppr_pack: null col");
-  int rc = krca_ppr_plan(row_ptr_host, N, plan_host, plan_len);
-  if (rc) return rc;
-  for (int64_t e = 0; e < E; ++e)
-    KRCA_CHECK_ARG(col_host[e] >= 0, "krca_ppr_pack: negative column at edge %lld", (long long)e);
-  return pack_blocks(row_ptr_host, col_host, N, n_max, plan_host, plan_len, pk_host, lane_host);
-}
 
 int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 16 * std::max<int64_t>(n_local, 1); }
 

@@ -390,7 +390,8 @@ def c_lib():
     global _c
     if _c is not None:
         return _c
-    path = os.path.join(HERE, "_build", "libkrca_oracle.so")
+    # KRCA_ORACLE_LIB: the AddressSanitizer build of the same source (tests/test_host_asan_cpu.py)
+    path = os.environ.get("KRCA_ORACLE_LIB") or os.path.join(HERE, "_build", "libkrca_oracle.so")
     if not os.path.exists(path):
         subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
     lib = ctypes.CDLL(path)

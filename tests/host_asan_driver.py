@@ -1,0 +1,81 @@
+"""Exercises the host-only code of libkrca (api.cpp, ppr_pack.cpp) and the C oracle under
+AddressSanitizer — TEST INFRASTRUCTURE, run by tests/test_host_asan_cpu.py in a subprocess with
+the clang ASan runtime preloaded (LD_PRELOAD) and KRCA_ORACLE_LIB pointing at the ASan oracle.
+Exits non-zero (ASan aborts) on any heap / stack / global overflow or use-after-free."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle")]
+
+vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+lib = ctypes.CDLL(sys.argv[1])
+lib.krca_last_error.restype = ctypes.c_char_p
+lib.krca_tune_set.argtypes = [ctypes.c_char_p, i32]
+lib.krca_tune_get.argtypes = [ctypes.c_char_p, ctypes.POINTER(i32)]
+lib.krca_ppr_plan_size.restype = i64
+lib.krca_ppr_plan_size.argtypes = [vp, i64]
+lib.krca_ppr_plan.argtypes = [vp, i64, vp, i64]
+lib.krca_ppr_lane_size.restype = i64
+lib.krca_ppr_lane_size.argtypes = [i64]
+lib.krca_ppr_pack.restype = i64
+lib.krca_ppr_pack.argtypes = [vp, vp, i64, i64, vp, i64, vp, vp]
+lib.krca_ppr_slice_words.restype = i64
+lib.krca_ppr_slice_words.argtypes = [i64]
+lib.krca_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+
+# api.cpp: knobs, error strings (a name long enough to be truncated), device query error path
+v = i32()
+assert lib.krca_tune_set(b"KRCA_PPR_DICT", 1) == 0 and lib.krca_tune_get(b"KRCA_PPR_DICT", ctypes.byref(v)) == 0
+assert lib.krca_tune_set(b"X" * 4000, 1) != 0 and len(lib.krca_last_error()) < 1024
+assert lib.krca_tune_get(None, None) != 0
+n = ctypes.c_int(-1)
+lib.krca_device_count(ctypes.byref(n))
+
+# ppr_pack.cpp: plans and packed columns of meshes with empty rows, hub rows (> 2048 callers),
+# dictionary and direct blocks, for several exchange layouts
+from krca import synth  # noqa: E402
+rng = np.random.default_rng(0)
+cases = [synth.make_graph(3000, n_edges=60_000, seed=1)]
+N = 4000
+deg = rng.integers(0, 6, N)
+deg[7] = 5000
+deg[100:140] = 0
+src = np.concatenate([rng.integers(0, N, d) for d in deg])
+rp = np.zeros(N + 1, np.int64)
+np.cumsum(deg, out=rp[1:])
+cases.append(synth.Mesh(N, rp, src.astype(np.int32), np.bincount(src, minlength=N).astype(np.int32), np.arange(3)))
+for m in cases:
+    rp, col = np.ascontiguousarray(m.row_ptr), np.ascontiguousarray(m.col)
+    Nn = len(rp) - 1
+    for dict_on in (1, 0):
+        lib.krca_tune_set(b"KRCA_PPR_DICT", dict_on)
+        for n_max in (Nn, (Nn + 1) // 2, 333):
+            pl = lib.krca_ppr_plan_size(rp.ctypes.data, Nn)
+            plan = np.zeros(pl, np.int64)
+            pk = np.zeros(len(col), np.int32)
+            lane = np.zeros(lib.krca_ppr_lane_size(pl), np.uint16)
+            nd = lib.krca_ppr_pack(rp.ctypes.data, col.ctypes.data, Nn, n_max, plan.ctypes.data, pl, pk.ctypes.data,
+                                   lane.ctypes.data)
+            assert nd >= 0, lib.krca_last_error()
+            assert lib.krca_ppr_slice_words(n_max) > 0
+    bad = plan.copy()
+    assert lib.krca_ppr_plan(rp.ctypes.data, Nn, bad.ctypes.data, len(bad) - 4) != 0  # wrong length: refused
+lib.krca_tune_set(b"KRCA_PPR_DICT", 1)
+
+# the C oracle (KRCA_ORACLE_LIB): scoring, PageRank (cold and warm), key
+import oracle  # noqa: E402
+x = rng.normal(50, 5, (200, 300, 2)).astype(np.float32)
+oracle.c_rolling_score(x, 60)
+oracle.c_rolling_score(x[:30], 60)  # shorter than the window
+m = cases[0]
+seed = rng.random(m.n_pods).astype(np.float32)
+rf, r, it, q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, 40, 1e-9, 0.1, return_q=True)
+oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, seed, r, 0.85, 40, 1e-9, 0.1)
+oracle.c_rca_key(r, q)
+oracle.c_usage_flags(rng.random((100, 2)).astype(np.float32) * 100)
+print("host-asan-ok")
