@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Root-cause ranking definitions compared on planted faults — TEST INFRASTRUCTURE (CPU, the C
+oracle; DESIGN.md §3.2 "Ranking").  For seeded C2-shaped meshes (10k pods / 200k edges, 8 metrics
+x 1440 steps) with 10 planted root pods and their callers perturbed hop by hop (krca/synth.py),
+reports the recall@10 of the planted roots for PageRank damping alpha, seed floor and ranking key
+(r = propagated mass alone, r*q = mass times own anomaly, q = anomaly alone).
+
+  python tests/ranking_ablation.py [--seeds 3] [--out profiles/r2/ranking_ablation.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle")]
+import oracle  # noqa: E402
+from krca import synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seeds", type=int, default=3)
+    ap.add_argument("--pods", type=int, default=10_000)
+    ap.add_argument("--edges", type=int, default=200_000)
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0) for key in ("r", "rq")] + [(None, None, "q")]
+    hits = {d: [] for d in defs}
+    for seed in range(a.seeds):
+        m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)
+        hops = synth.caller_hops(m, m.roots)
+        x = synth.make_metrics(a.pods, 8, 1440, seed=seed, roots=m.roots, hop_sets=hops).numpy()
+        s = oracle.c_rolling_score(x, 60)["score"]
+        roots = set(m.roots.tolist())
+        for al, fl, key in defs:
+            if key == "q":
+                idx, _ = oracle.topk_ref(s.astype(np.float64), 10)
+            else:
+                _, r, _, q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, s, al, 30, 0.0, fl, return_q=True)
+                kv = oracle.c_rca_key(r, q) if key == "rq" else r
+                idx, _ = oracle.topk_ref(kv, 10)
+            hits[(al, fl, key)].append(len(roots & set(int(i) for i in idx)) / len(roots))
+    rows = [dict(alpha=al, seed_floor=fl, key=key, recall_at_10=float(np.mean(v)), per_seed=v)
+            for (al, fl, key), v in hits.items()]
+    txt = json.dumps(dict(config=vars(a), rows=rows), indent=1)
+    if a.out:
+        open(a.out, "w").write(txt + "\n")
+    for r in rows:
+        print(f"alpha={r['alpha']} floor={r['seed_floor']} key={r['key']:3s} recall@10={r['recall_at_10']:.2f} {r['per_seed']}")
+
+
+if __name__ == "__main__":
+    main()
