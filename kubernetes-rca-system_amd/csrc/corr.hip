@@ -195,6 +195,9 @@ struct Shard {
   int64_t lo;
   int G, g;
   int64_t I0;
+  int j0 = 0;        // SAMPLE: first 256-column block of this chunk of the sample
+  int own = 0;       // SAMPLE: this chunk also runs each row block's own 256-block
+  int nsb2_all = 0;  // SAMPLE: 256-blocks of the whole sample (an own block inside it is skipped)
 };
 
 template <int KC, int MODE>
@@ -214,13 +217,15 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     I = blockIdx.x / nb2;
     J = blockIdx.x % nb2;
   } else if (SAMPLE) {
-    const int nsb2 = (nsb + 1) / 2;
+    const int nsb2 = (nsb + 1) / 2;  // this chunk's 256-blocks
     I = sh.I0 + blockIdx.x / (nsb2 + 1);
     J = blockIdx.x % (nsb2 + 1);
     if (J == nsb2) {  // the row block's own 256-block, unless it is already a sample block
-      if (I < nsb2) return;
+      if (!sh.own || I < sh.nsb2_all) return;
       J = I;
       own = true;
+    } else {
+      J += sh.j0;
     }
   } else {
     // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so slot
@@ -568,7 +573,7 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     if (tid < 256) {  // row scan: pod rowA + half*128 + r against 128 columns of block 2J + ch
       const int r = tid & 127, ch = tid >> 7;
       const int64_t g = rowA + half * BM + r;
-      const int jb = 2 * (int)J + ch;
+      const int jb = 2 * (int)(J - sh.j0) + ch;  // list slot of this chunk
       const int64_t c0 = rowB + ch * BM;
       if (g < P && (own || jb < nsb)) {
         Cand<KC> cd;
@@ -604,33 +609,40 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
   }
 }
 
-// phi[g] = (k-th best |r| of g among the sampled partners) - 2 eps (-1 if fewer than k): every
-// member of g's exact top-k has a screening |r| above it (exact k-th >= sampled k-th - eps).
-// A flat pod (self product 0: z = 0) gets phi = 3 (never a candidate owner; handled exactly).
+// The threshold sample runs in chunks of NSB 128-pod column blocks (its size grows with P, the
+// lists of one chunk are [P][NSL][KC]).  After each chunk, one wave per pod merges the chunk's lists
+// into the pod's running top-k |r| VALUES (chunks hold disjoint partners, so the k-th best of the
+// whole sample is the k-th best of the running values and the chunk's); after the last chunk,
+// phi[g] = (k-th best sampled |r|) - 2 eps (-1 if fewer than k): every member of g's exact top-k
+// has a screening |r| above it (exact k-th >= sampled k-th - eps).  A flat pod (self product 0:
+// z = 0) gets phi = 3 (never a candidate owner; handled exactly).
 template <int KC>
 __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, const int32_t* __restrict__ si,
                                                   const float* __restrict__ selfd, int64_t g0, int64_t g1, int nsb,
-                                                  int k, float eps, float* __restrict__ phi) {
+                                                  int k, float eps, float* __restrict__ run, int first, int last,
+                                                  float* __restrict__ phi) {
   const int64_t g = g0 + (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= g1) return;
-  constexpr int PER = (NSL * KC + 63) / 64;
+  constexpr int PER = (NSL * KC + 63) / 64 + 1;  // + the running values (lanes < k of the last slot)
   float a[PER];
 #pragma unroll
-  for (int u = 0; u < PER; ++u) {
+  for (int u = 0; u < PER - 1; ++u) {
     const int q = lane + 64 * u;
     const int lst = q / KC;
     const int64_t e = g * NSL * KC + q;
     const bool used = q < NSL * KC && (lst < nsb || lst >= NSB);
     a[u] = (used && si[e] >= 0) ? fabsf(sv[e]) : -1.f;
   }
-  float kth = -1.f;
+  a[PER - 1] = (!first && lane < k) ? run[g * KMAX + lane] : -1.f;
+  float kth = -1.f, keep = -1.f;
   for (int r = 0; r < k; ++r) {
     float m = a[0];
 #pragma unroll
     for (int u = 1; u < PER; ++u) m = fmaxf(m, a[u]);
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
     kth = m;
+    if (lane == r) keep = m;
     if (m < 0.f) break;
     // remove one instance of m: the lowest lane holding it, its first slot
     bool has = false;
@@ -647,7 +659,8 @@ __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, 
         }
     }
   }
-  if (lane == 0) phi[g] = selfd[g] < 0.25f ? 3.f : (kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f);
+  if (lane < k) run[g * KMAX + lane] = keep;
+  if (last && lane == 0) phi[g] = selfd[g] < 0.25f ? 3.f : (kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f);
 }
 
 // ---- exact |r| > tau counts: the ambiguous pairs in list order, 16 lanes each (float4 loads of
@@ -951,6 +964,7 @@ struct CorrWs {  // views into a caller's candidate workspace
   float* samp_v;  // [P][NSL][KC]
   int32_t* samp_i;
   float *selfd, *phi2;  // [P]
+  float* run;           // [P][KMAX] running top-k |r| of the threshold sample
   int32_t* over;        // [n_loc + 1]
   int32_t* deep;        // [n_loc + 1]: pods for corr_merge_deep (count first)
   int2* amb;            // [amb_cap(P)] ambiguous pairs of the main pass (contiguous per tile)
@@ -975,6 +989,7 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   w.samp_v = reinterpret_cast<float*>(take(P * NSL * KC));
   w.samp_i = reinterpret_cast<int32_t*>(take(P * NSL * KC));
   w.selfd = reinterpret_cast<float*>(take(P));
+  w.run = reinterpret_cast<float*>(take(P * KMAX));
   w.phi2 = reinterpret_cast<float*>(take(P));
   w.over = reinterpret_cast<int32_t*>(take(n_loc + 1));
   w.deep = reinterpret_cast<int32_t*>(take(n_loc + 1));
@@ -1017,7 +1032,9 @@ Dims dims_of(int64_t P, int T, int k, float tau) {
   d.T = T;
   d.Tp = (int)krca::ceil_div(T, BK) * BK;
   d.nb2 = (int)krca::ceil_div(P, TB);
-  d.nsb = std::min(2 * d.nb2, NSB);
+  // threshold sample: ~P*k/500 pods (>= NSB blocks of 128), so that about 500 partners per pod clear
+  // phi at any P (2,048 at C3; a fixed 2,048 at 1M pods let ~0.4 % of a million partners through)
+  d.nsb = (int)std::min<int64_t>(2 * d.nb2, std::max<int64_t>(NSB, krca::ceil_div(P * k, 500 * 128)));
   d.k = k;
   d.tau = tau;
   d.eps = (float)(std::ldexp(1.0, -10) * 1.001 + std::ldexp((double)T, -24) + std::ldexp(std::sqrt((double)T), -23));
@@ -1030,17 +1047,25 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
                  hipStream_t st) {
   if (int rc = set_lds_attr<KC>()) return rc;
   const int64_t I0 = lo / TB, I1 = krca::ceil_div(lo + n, TB);
-  const int nsb2 = (d.nsb + 1) / 2;
-  KRCA_HIP(hipMemsetAsync(ws.samp_i + lo * NSL * KC, 0xff, (size_t)n * NSL * KC * sizeof(int32_t), st));
-  const Shard sh{0, 1, 0, I0};
-  hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES, st,
-                     zh, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau, (const float*)nullptr, ws.samp_v, ws.samp_i,
-                     ws.selfd, (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
-                     (int64_t)0, sh, 0, 2.f, (int2*)nullptr, (int32_t*)nullptr);
-  KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
-                     ws.samp_i, ws.selfd, lo, lo + n, d.nsb, d.k, d.eps, phi);
-  KRCA_LAUNCH_CHECK();
+  const int nsb2_all = (d.nsb + 1) / 2;
+  for (int c0 = 0; c0 < nsb2_all; c0 += NSB / 2) {  // chunks of NSB 128-blocks
+    const int nsb_c = std::min(NSB, d.nsb - 2 * c0);
+    const int nsb2 = (nsb_c + 1) / 2;
+    KRCA_HIP(hipMemsetAsync(ws.samp_i + lo * NSL * KC, 0xff, (size_t)n * NSL * KC * sizeof(int32_t), st));
+    Shard sh{0, 1, 0, I0};
+    sh.j0 = c0;
+    sh.own = c0 == 0;
+    sh.nsb2_all = nsb2_all;
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES,
+                       st, zh, zh, d.P, d.Tp, d.nb2, (int64_t)0, nsb_c, d.tau, (const float*)nullptr, ws.samp_v,
+                       ws.samp_i, ws.selfd, (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                       (const int32_t*)nullptr, (int64_t)0, sh, 0, 2.f, (int2*)nullptr, (int32_t*)nullptr);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
+                       ws.samp_i, ws.selfd, lo, lo + n, nsb_c, d.k, d.eps, ws.run, (int)(c0 == 0),
+                       (int)(c0 + NSB / 2 >= nsb2_all), phi);
+    KRCA_LAUNCH_CHECK();
+  }
   return KRCA_OK;
 }
 

@@ -112,6 +112,33 @@ def test_corr_c3_every_row(eng):
     assert bad_cnt == 0 and bad_set == 0, (bad_cnt, bad_set)
 
 
+def test_corr_sample_in_chunks(eng):
+    """P * k past 16 * 64,000 grows the threshold sample beyond one chunk of 16 column blocks (the
+    running top-k merge of corr_theta): every row still exact against a float64 device reference."""
+    P, T, k = 140_000, 256, 10
+    x = synth.make_metrics(P, 1, T, seed=4, group_size=20, device="cuda")
+    res = eng.corr_topk(x, k=k, tau=TAU)
+    z = torch.from_numpy(oracle.corr_standardize(x.cpu().numpy(), 0)).cuda()
+    assert (res["cert"] > 0).all()
+    gi = torch.from_numpy(res["idx"]).cuda().long()
+    bad = 0
+    for r0 in range(0, P, 4096):
+        r1 = min(P, r0 + 4096)
+        a = (z[r0:r1] @ z.T).abs()
+        rr = torch.arange(r0, r1, device="cuda")
+        a[rr - r0, rr] = -1.0
+        top = torch.topk(a, k + 1, dim=1)
+        gap = top.values[:, k - 1] - top.values[:, k]
+        want = torch.sort(top.indices[:, :k], dim=1).values
+        got = torch.sort(gi[r0:r1], dim=1).values
+        bad += int(((want != got).any(1) & (gap > 1e-6)).sum())
+        cnt = torch.from_numpy(res["count"][r0:r1]).cuda()
+        a[rr - r0, rr] = 0.0
+        lo, hi = (a > TAU + 1e-6).sum(1), (a > TAU - 1e-6).sum(1)
+        bad += int(((cnt < lo) | (cnt > hi)).sum())
+    assert bad == 0
+
+
 def test_corr_rejects_bad_k(eng):
     x = torch.rand(50, 10, 1)
     with pytest.raises(native.KrcaError):
