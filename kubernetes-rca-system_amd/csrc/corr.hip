@@ -208,7 +208,8 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
                                                  int2* __restrict__ buf, int32_t* __restrict__ cnt,
                                                  int32_t* __restrict__ count, const int32_t* __restrict__ rect_pods,
                                                  int64_t n_rect, Shard sh, int debug, float tau_lo,
-                                                 int2* __restrict__ amb, int32_t* __restrict__ amb_n) {
+                                                 int2* __restrict__ amb, int32_t* __restrict__ amb_n,
+                                                 float* __restrict__ ambv) {
   constexpr bool SAMPLE = MODE == MODE_SAMPLE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t I, J;
@@ -389,7 +390,10 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     // past a full wave list (rare) takes a slot of its own.
     auto amb_one = [&](int4 ent) {
       const int slot = atomicAdd(amb_n, 1);
-      if (slot < amb_cap(P)) amb[slot] = make_int2(ent.x, ent.y | ((ent.w & 2) ? AMB_BOTH : 0));
+      if (slot < amb_cap(P)) {
+        amb[slot] = make_int2(ent.x, ent.y | ((ent.w & 2) ? AMB_BOTH : 0));
+        ambv[slot] = __int_as_float(ent.z);
+      }
     };
     auto flush_one = [&](int4 ent) {
       if (ent.w & 6) amb_one(ent);
@@ -539,8 +543,11 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
             more = more || base + NT < wcount[u0 + u];
             ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(-1, 0, 0, 0);
             const bool cand = ok && (ent[u].w & 1);
-            if (!RECT && ok && (ent[u].w & 6) && wbase[u0 + u] >= 0)  // an ambiguous pair
-              amb[wbase[u0 + u] + (ent[u].w >> 3)] = make_int2(ent[u].x, ent[u].y | ((ent[u].w & 2) ? AMB_BOTH : 0));
+            if (!RECT && ok && (ent[u].w & 6) && wbase[u0 + u] >= 0) {  // an ambiguous pair
+              const int slot = wbase[u0 + u] + (ent[u].w >> 3);
+              amb[slot] = make_int2(ent[u].x, ent[u].y | ((ent[u].w & 2) ? AMB_BOTH : 0));
+              ambv[slot] = __int_as_float(ent[u].z);
+            }
             if (RECT && ok) ent[u].x -= (int)sh.lo;  // rect pass: the rank's local buffers
             gs[u] = cand ? atomicAdd(&cnt[ent[u].x], 1) : CAPC;
           }
@@ -663,33 +670,67 @@ __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, 
   if (last && lane == 0) phi[g] = selfd[g] < 0.25f ? 3.f : (kth < 0.f ? -1.f : kth - 2.f * eps - 1e-6f);
 }
 
-// ---- exact |r| > tau counts: the ambiguous pairs in list order, 16 lanes each (float4 loads of
-// the pair's two rows of z32), float64 accumulation, persistent over the device-held list length
-__global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__ amb, const int32_t* __restrict__ amb_n,
-                                                        int64_t P, const float* __restrict__ z32, int T, float tau,
-                                                        int32_t* __restrict__ count) {
+// ---- exact |r| > tau counts -------------------------------------------------------------------
+// dn[p] = || z32[p] - fp16(z32[p]) ||, the fp16 rounding error of row p (float64, rounded up): the
+// screening product of a pair then differs from the exact one by at most
+//   |h_a.d_b| + |d_a.h_b| + |d_a.d_b| + acc <= dn_a + dn_b + 3 dn_a dn_b + acc
+// (||h|| <= 1 + dn, unit-norm rows, acc = the fp32 accumulation terms of eps), typically ~60 % of the
+// worst-case eps: most listed pairs are decided from their screening value without reading a row.
+__global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32, const uint16_t* __restrict__ zh,
+                                                  int64_t P, int T, int Tp, float* __restrict__ dn) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  if (p >= P) return;
+  double s2 = 0.0;
+  for (int t = lane; t < T; t += 64) {
+    const float z = z32[p * T + t];
+    const double d = (double)z - (double)(float)__builtin_bit_cast(_Float16, zh[p * Tp + t]);
+    s2 += d * d;
+  }
+  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off, 64);
+  if (lane == 0) dn[p] = (float)(sqrt(s2) * (1.0 + 1e-6)) + 1e-12f;
+}
+
+// the ambiguous pairs in list order, 16 lanes each: decided from the screening value and the two
+// rows' rounding-error norms when that suffices, else re-scored (float4 loads of the pair's rows of
+// z32, float64 accumulation); persistent over the device-held list length
+__global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__ amb, const float* __restrict__ ambv,
+                                                        const int32_t* __restrict__ amb_n, int64_t P,
+                                                        const float* __restrict__ z32, const float* __restrict__ dn,
+                                                        int T, float tau, float acc_err, int32_t* __restrict__ count) {
   const int sub = threadIdx.x & 15;
   const int64_t n = min((int64_t)*amb_n, amb_cap(P));
   const bool vec = (T & 3) == 0;
   for (int64_t q = (int64_t)blockIdx.x * (TPB / 16) + (threadIdx.x >> 4); q < n; q += (int64_t)gridDim.x * (TPB / 16)) {
     const int2 e = amb[q];
     const int64_t a = e.x, b = e.y & (AMB_BOTH - 1);
-    const float* za = z32 + a * T;
-    const float* zb = z32 + b * T;
-    double acc = 0.0;
-    if (vec) {
-      const float4* va = reinterpret_cast<const float4*>(za);
-      const float4* vb = reinterpret_cast<const float4*>(zb);
-      for (int t = sub; t < T / 4; t += 16) {
-        const float4 x = va[t], y = vb[t];
-        acc += (double)x.x * (double)y.x + (double)x.y * (double)y.y + (double)x.z * (double)y.z +
-               (double)x.w * (double)y.w;
+    const double sa = (double)dn[a], sb = (double)dn[b];
+    const double band = sa + sb + 3.0 * sa * sb + (double)acc_err + 1e-9;
+    const double v = fabs((double)ambv[q]);
+    int hit;
+    if (v > (double)tau + band) {
+      hit = 1;
+    } else if (v <= (double)tau - band) {
+      hit = 0;
+    } else {  // too close to call from the screening value: float64 from the rows
+      const float* za = z32 + a * T;
+      const float* zb = z32 + b * T;
+      double acc = 0.0;
+      if (vec) {
+        const float4* va = reinterpret_cast<const float4*>(za);
+        const float4* vb = reinterpret_cast<const float4*>(zb);
+        for (int t = sub; t < T / 4; t += 16) {
+          const float4 x = va[t], y = vb[t];
+          acc += (double)x.x * (double)y.x + (double)x.y * (double)y.y + (double)x.z * (double)y.z +
+                 (double)x.w * (double)y.w;
+        }
+      } else {
+        for (int t = sub; t < T; t += 16) acc += (double)za[t] * (double)zb[t];
       }
-    } else {
-      for (int t = sub; t < T; t += 16) acc += (double)za[t] * (double)zb[t];
+      for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+      hit = fabs(acc) > (double)tau;
     }
-    for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
-    if (sub == 0 && fabs(acc) > (double)tau) {
+    if (sub == 0 && hit) {
       atomicAdd(&count[a], 1);
       if (e.y & AMB_BOTH) atomicAdd(&count[b], 1);
     }
@@ -968,6 +1009,8 @@ struct CorrWs {  // views into a caller's candidate workspace
   int32_t* over;        // [n_loc + 1]
   int32_t* deep;        // [n_loc + 1]: pods for corr_merge_deep (count first)
   int2* amb;            // [amb_cap(P)] ambiguous pairs of the main pass (contiguous per tile)
+  float* ambv;          // [amb_cap(P)] their screening values
+  float* dn;            // [P] fp16 rounding-error norm of each row
   int32_t* amb_n;       // [4]: their count (past the capacity: an error)
   uint16_t* zs;         // [RECT_ROWS][Tp]
   int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
@@ -994,6 +1037,8 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   w.over = reinterpret_cast<int32_t*>(take(n_loc + 1));
   w.deep = reinterpret_cast<int32_t*>(take(n_loc + 1));
   w.amb = reinterpret_cast<int2*>(take(2 * amb_cap(P)));
+  w.ambv = reinterpret_cast<float*>(take(amb_cap(P)));
+  w.dn = reinterpret_cast<float*>(take(P));
   w.amb_n = reinterpret_cast<int32_t*>(take(4));
   w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
   if (G > 0) {
@@ -1059,7 +1104,8 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
     hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES,
                        st, zh, zh, d.P, d.Tp, d.nb2, (int64_t)0, nsb_c, d.tau, (const float*)nullptr, ws.samp_v,
                        ws.samp_i, ws.selfd, (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
-                       (const int32_t*)nullptr, (int64_t)0, sh, 0, 2.f, (int2*)nullptr, (int32_t*)nullptr);
+                       (const int32_t*)nullptr, (int64_t)0, sh, 0, 2.f, (int2*)nullptr, (int32_t*)nullptr,
+                       (float*)nullptr);
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
                        ws.samp_i, ws.selfd, lo, lo + n, nsb_c, d.k, d.eps, ws.run, (int)(c0 == 0),
@@ -1087,11 +1133,15 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, zh, d.P,
                      d.Tp, d.nb2, per_xcd, d.nsb, d.tau + d.eps, phi, (float*)nullptr, (int32_t*)nullptr,
                      (float*)nullptr, ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, sh, dbg,
-                     d.tau - d.eps, ws.amb, ws.amb_n);
+                     d.tau - d.eps, ws.amb, ws.amb_n, ws.ambv);
   KRCA_LAUNCH_CHECK();
   if (dbg == 0) {
-    hipLaunchKernelGGL(corr_amb_rescore, dim3(4096), dim3(TPB), 0, st, (const int2*)ws.amb, (const int32_t*)ws.amb_n,
-                       d.P, z32, d.T, d.tau, count);
+    hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
+                       d.Tp, ws.dn);
+    KRCA_LAUNCH_CHECK();
+    const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
+    hipLaunchKernelGGL(corr_amb_rescore, dim3(4096), dim3(TPB), 0, st, (const int2*)ws.amb, (const float*)ws.ambv,
+                       (const int32_t*)ws.amb_n, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
     KRCA_LAUNCH_CHECK();
   }
   return KRCA_OK;
@@ -1143,7 +1193,7 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
                        (const uint16_t*)ws.zs, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau,
                        (const float*)ws.phi2, (float*)nullptr, (int32_t*)nullptr, (float*)nullptr, lbuf, lcnt,
                        (int32_t*)nullptr, (const int32_t*)(ws.over + 1 + r0), nr, sh, 0, 2.f, (int2*)nullptr,
-                       (int32_t*)nullptr);
+                       (int32_t*)nullptr, (float*)nullptr);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,
