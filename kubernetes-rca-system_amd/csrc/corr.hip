@@ -186,7 +186,10 @@ __device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ 
 //              only (sample slots NSB, NSB+1 = own block), and each pod's self product.
 // MODE_RECT:   the gathered rows zA = zh[rect_pods] x every column block (second pass of the pods
 //              whose buffer overflowed): row-side appends only, against phi = phi2.
-constexpr int MODE_MAIN = 0, MODE_SAMPLE = 1, MODE_RECT = 2;
+// MODE_REFILL: the main-pass tiles whose candidate lists overflowed LDS (rare: a wave's list holds
+//              CAPW entries), recomputed with every entry past the list appended to the global
+//              buffers at once; their counts were already added by the main pass.
+constexpr int MODE_MAIN = 0, MODE_SAMPLE = 1, MODE_RECT = 2, MODE_REFILL = 3;
 
 // Pod-sharded runs: rank g of G takes every G-th super-tile of the upper triangle
 // (MAIN), the row blocks [I0, ...) of its own pods (SAMPLE), and appends the candidates of its own
@@ -200,69 +203,67 @@ struct Shard {
   int nsb2_all = 0;  // SAMPLE: 256-blocks of the whole sample (an own block inside it is skipped)
 };
 
-template <int KC, int MODE>
-__global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA, const uint16_t* __restrict__ zh,
-                                                 int64_t P, int Tp, int nb2, int64_t per_xcd, int nsb, float tau,
-                                                 const float* __restrict__ phi, float* __restrict__ samp_v,
-                                                 int32_t* __restrict__ samp_i, float* __restrict__ selfd,
-                                                 int2* __restrict__ buf, int32_t* __restrict__ cnt,
-                                                 int32_t* __restrict__ count, const int32_t* __restrict__ rect_pods,
-                                                 int64_t n_rect, Shard sh, int debug, float tau_lo,
-                                                 int2* __restrict__ amb, int32_t* __restrict__ amb_n,
-                                                 float* __restrict__ ambv) {
+struct TileArgs {
+  const uint16_t* zA;  // row operand: zh, or the gathered rows of a rect pass
+  const uint16_t* zh;
+  int64_t P;
+  int Tp, nb2;
+  int64_t per_xcd;
+  int nsb;
+  float tau_hi;   // MAIN: tau + eps, every screening |r| above it is a hit
+  float tau_lo;   // MAIN: tau - eps, none at or below it is
+  float tau;      // MAIN: the caller's tau (the per-pair band in between)
+  float acc_err;  // MAIN: the fp32 accumulation terms of eps
+  const float* phi;  // MAIN: candidate bound per pod; RECT: phi2
+  float* samp_v;
+  int32_t* samp_i;
+  float* selfd;
+  int2* buf;
+  int32_t* cnt;
+  int32_t* count;
+  const int32_t* rect_pods;
+  int64_t n_rect;
+  Shard sh;
+  int debug;
+  int2* amb;
+  int32_t* amb_n;
+  float* ambv;
+  const float* dn;  // MAIN: fp16 rounding-error norm per pod (corr_dnorm)
+  int32_t* ovt;     // MAIN / REFILL: [0] overflowed tiles, then I * nb2 + J each
+};
+
+// One 256 x 256 tile (I, J).  DIRECT: list entries past CAPW go to the global buffers at once (rect
+// and refill passes); otherwise a full list marks the tile for the refill pass.
+template <int KC, int MODE, bool DIRECT>
+__device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, const int64_t J, const bool own) {
   constexpr bool SAMPLE = MODE == MODE_SAMPLE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int64_t I, J;
-  bool own = false;
-  if (MODE == MODE_RECT) {
-    I = blockIdx.x / nb2;
-    J = blockIdx.x % nb2;
-  } else if (SAMPLE) {
-    const int nsb2 = (nsb + 1) / 2;  // this chunk's 256-blocks
-    I = sh.I0 + blockIdx.x / (nsb2 + 1);
-    J = blockIdx.x % (nsb2 + 1);
-    if (J == nsb2) {  // the row block's own 256-block, unless it is already a sample block
-      if (!sh.own || I < sh.nsb2_all) return;
-      J = I;
-      own = true;
-    } else {
-      J += sh.j0;
-    }
-  } else {
-    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so slot
-    // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the
-    // upper triangle in SUPER x SUPER super-tiles, so the tiles an XCD has in flight share 2*SUPER
-    // row blocks through its L2.  Slots below the diagonal or past nb2 exit at once.
-    const int64_t b = blockIdx.x;
-    const int64_t L = (b & 7) * per_xcd + (b >> 3);
-    const int64_t ns = (nb2 + SUPER - 1) / SUPER;
-    const int64_t st = (L / (SUPER * SUPER)) * sh.G + sh.g;  // this rank's super-tiles
-    if (st >= ns * (ns + 1) / 2) return;
-    int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
-    while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
-    while (SJ * (SJ + 1) / 2 > st) --SJ;
-    const int64_t SI = st - SJ * (SJ + 1) / 2;
-    const int64_t in = L % (SUPER * SUPER);
-    I = SI * SUPER + in / SUPER;
-    J = SJ * SUPER + in % SUPER;
-    if (I > J || J >= nb2) return;
-  }
+  const int64_t P = A.P;
+  const int Tp = A.Tp;
+  const Shard& sh = A.sh;
+  const int debug = A.debug;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 2, wc = w & 3;
   const int64_t rowA = I * TB, rowB = J * TB;
   // main / rect epilogue operands, loaded now so their latency hides behind the K loop: thread
-  // tid < 256 holds row pod tid of the tile and its phi, thread tid >= 256 column pod tid - 256
+  // tid < 256 holds row pod tid of the tile, its phi and rounding-error norm, thread tid >= 256
+  // column pod tid - 256
   int my_pod = -1;
   float my_phi = 4.f;  // 4 = never a candidate owner (padding, or column side of a rect pass)
+  float my_dn = 0.f;
   if (!SAMPLE) {
     const int q = tid & (TB - 1);
     if (tid < TB) {
-      const int64_t g = MODE == MODE_RECT ? (rowA + q < n_rect ? rect_pods[rowA + q] : -1) : (rowA + q < P ? rowA + q : -1);
+      const int64_t g = MODE == MODE_RECT ? (rowA + q < A.n_rect ? A.rect_pods[rowA + q] : -1) : (rowA + q < P ? rowA + q : -1);
       my_pod = (int)g;
-      if (g >= 0) my_phi = phi[g];
+      if (g >= 0) {
+        my_phi = A.phi[g];
+        if (MODE == MODE_MAIN) my_dn = A.dn[g];
+      }
     } else if (MODE == MODE_MAIN && rowB + q < P) {
       my_pod = (int)(rowB + q);
-      my_phi = phi[rowB + q];
+      my_phi = A.phi[rowB + q];
+      my_dn = A.dn[rowB + q];
     }
   }
 
@@ -278,8 +279,8 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
   // instruction writes a lane-linear 1 KiB piece = 8 rows of 128 B; lane l lands on row l/8,
   // slot l%8, so it fetches the global chunk (l%8) ^ key(row): the XOR swizzle is applied on the
   // SOURCE address.  64 pieces per K step (32 A + 32 B), 8 per wave.
-  const uint16_t* gA = zA + rowA * Tp;
-  const uint16_t* gB = zh + rowB * Tp;
+  const uint16_t* gA = A.zA + rowA * Tp;
+  const uint16_t* gB = A.zh + rowB * Tp;
   const int prow = lane >> 3, pslot = lane & 7;
 #define CORR_GLDS(BUF, K0)                                                                             \
   _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                      \
@@ -292,22 +293,26 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
                                      16, 0, 0);                                                       \
   }
   const int r32 = lane & 31, h = lane >> 5;
-#define CORR_COMPUTE(BUF)                                                                         \
-  {                                                                                                \
-    const char* sA = smem + (BUF) * STAGE_BYTES;                                                   \
-    const char* sB = sA + TB * BK * 2;                                                             \
-    _Pragma("unroll") for (int ks = 0; ks < BK / 16; ++ks) {                                       \
-      const int c = ks * 2 + h;                                                                    \
-      halfx8 fa[4], fb[2];                                                                         \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
-        fa[i] = *reinterpret_cast<const halfx8*>(sA + chunk_off(wr * 128 + i * 32 + r32, c));      \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
-        fb[j] = *reinterpret_cast<const halfx8*>(sB + chunk_off(wc * 64 + j * 32 + r32, c));       \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);    \
-    }                                                                                              \
-  }
+  // Fragments in two register sets: the 6 fragments of 16-deep slice ks+1 are read while the 8 MFMAs
+  // of slice ks run, and slice 0 of step s+1 right after the step's barrier, beside slice 3's MFMAs,
+  // so no MFMA waits on a just-issued LDS read.
+  halfx8 fa[2][4], fb[2][2];
+  auto frag_load = [&](int buf, int ks, int set) {
+    const char* sA = smem + buf * STAGE_BYTES;
+    const char* sB = sA + TB * BK * 2;
+    const int c = ks * 2 + h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[set][i] = *reinterpret_cast<const halfx8*>(sA + chunk_off(wr * 128 + i * 32 + r32, c));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[set][j] = *reinterpret_cast<const halfx8*>(sB + chunk_off(wc * 64 + j * 32 + r32, c));
+  };
+  auto frag_mfma = [&](int set) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+  };
   // L2 prefetch of K step s+2 while step s+1 streams into LDS: one 4-byte LDS-DMA per 128-B line
   // (lane tid < 256: A row tid, else B row tid-256) into a junk LDS slot, so no VGPR is tied up;
   // step s+2's 16-byte loads then hit L2 instead of paying the HBM/MALL latency inside one
@@ -320,10 +325,13 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
   CORR_GLDS(0, 0)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  frag_load(0, 0, 0);
   for (int s = 0; s < nk; ++s) {
-    // stage (s+1)&1 was last read in step s-1, which every wave finished before the barrier
+    const int buf = s & 1;
+    // stage buf ^ 1 was last read in step s-1; every wave retired those reads (lgkmcnt(0)) before
+    // the barrier that ended it
     if (s + 1 < nk) {
-      CORR_GLDS((s + 1) & 1, (s + 1) * BK)
+      CORR_GLDS(buf ^ 1, (s + 1) * BK)
     }
     if (s + 2 < nk) {
       CORR_L2PF((s + 2) * BK)
@@ -331,9 +339,28 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
       CORR_L2PF(0)  // keeps the count of outstanding loads uniform (re-touches a resident line)
     }
     __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs, not after
-    CORR_COMPUTE(s & 1)
-    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    // each phase: the 8 MFMAs of one slice with the 6 reads of the next one between them (pinned:
+    // left alone, the scheduler sinks every read to its first use and waits on it there)
+#define CORR_PHASE(RB, RKS, RSET, MSET)                                              \
+    frag_load(RB, RKS, RSET);                                                        \
+    frag_mfma(MSET);                                                                 \
+    _Pragma("unroll") for (int q = 0; q < 6; ++q) {                                  \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                             \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                             \
+    }                                                                                \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                               \
+    __builtin_amdgcn_sched_barrier(0);
+    CORR_PHASE(buf, 1, 1, 0)
+    CORR_PHASE(buf, 2, 0, 1)
+    CORR_PHASE(buf, 3, 1, 0)
+    // stage buf ^ 1 has landed for this wave (only the L2 prefetch may be outstanding) and this
+    // wave's reads of stage buf are retired; after the barrier, for every wave.  The last step
+    // reads stage buf ^ 1 as well (stale bytes, never used): no branch in the loop.
+    asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    CORR_PHASE(buf ^ 1, 0, 0, 1)
+#undef CORR_PHASE
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -341,8 +368,8 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
 #undef CORR_COMPUTE
 #undef CORR_L2PF
   const bool diag = MODE != MODE_RECT && I == J;
-  if (debug == 1) {  // profiling aid (KRCA_CORR_DEBUG=1): product only, no epilogue
-    if (tid == 0 && acc[0][0][0] == 12345.f) count[0] = 1;
+  if (debug == 1 || debug == 4) {  // profiling aid (KRCA_CORR_DEBUG=1 / 4): product only, no epilogue
+    if (tid == 0 && acc[0][0][0] == 12345.f) A.count[0] = 1;
     return;
   }
   if (!SAMPLE) {
@@ -350,21 +377,28 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
     // lane holds rows wr*128 + i*32 + (e&3) + 8*(e>>2) + 4*h and columns wc*64 + j*32 + r32.
     // Padding rows / columns have z = 0 (r = 0: never above tau >= 0) and phi = 4 (never a
     // candidate); the self products of a diagonal tile are zeroed first.  The common case costs
-    // ~4 vector ops per value; only a 16-value group with a candidate takes the slow path.
+    // a few vector ops per value; only a value slot with a candidate or a screening |r| within eps
+    // of tau in some lane takes the slow path.
     constexpr bool RECT = MODE == MODE_RECT;
+    constexpr bool COUNTS = MODE == MODE_MAIN && !DIRECT;  // a refill pass re-lists only
     float* sphr = reinterpret_cast<float*>(smem);  // phi of the 256 row pods
     float* sphc = sphr + TB;                        // phi of the 256 column pods
     int* srcnt = reinterpret_cast<int*>(sphc + TB);  // |r| > tau counts per row / column
     int* sccnt = srcnt + TB;
-    int* spod = sccnt + TB;  // row pod ids
-    int* wcount = spod + TB;  // candidate-list length per wave
+    int* spod = sccnt + TB;    // row pod ids
+    float* sdnr = reinterpret_cast<float*>(spod + TB);  // rounding-error norms of the rows / columns
+    float* sdnc = sdnr + TB;
+    int* wcount = reinterpret_cast<int*>(sdnc + TB);  // candidate-list length per wave
     int* wamb = wcount + 8;   // ambiguous entries in each wave's list
     int* wbase = wamb + 8;    // their first slot in the ambiguous-pair list (-1: list full)
+    int* sflag = wbase + 8;   // a wave's list overflowed
     {
       const int q = tid & (TB - 1);
       (tid < TB ? sphr : sphc)[q] = my_phi;
       (tid < TB ? srcnt : sccnt)[q] = 0;
+      (tid < TB ? sdnr : sdnc)[q] = my_dn;
       if (tid < TB) spod[q] = my_pod;
+      if (tid == 0) *sflag = 0;
     }
     __syncthreads();
     if (diag) {
@@ -376,47 +410,31 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
           for (int e = 0; e < 16; ++e)
             if (wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h == wc * 64 + j * 32 + r32) acc[i][j][e] = 0.f;
     }
-    // per-wave candidate list in LDS {pod, partner, r bits}, compacted by ballot + mbcnt (no
-    // atomics, no waiting); past CAPW entries a hit goes to the global buffer directly (rare)
+    // per-wave list in LDS, one entry per (row, column) pair that needs anything, compacted by
+    // ballot + mbcnt (no atomics, no waiting): {row pod, column pod, r bits, tag}.  Tag bit 0: a
+    // candidate of the row pod, bit 1: of the column pod, bit 2 / 3: an ambiguous pair for the
+    // count (bit 2: credit both pods, bit 3: the row pod only, a diagonal tile holding both
+    // orders); bits 4..: its rank among the wave's listed ambiguous pairs.  A tile's ambiguous pairs
+    // take ONE contiguous range of the global list (one atomic per workgroup), in the XCD-aware tile
+    // order that corr_amb_rescore then walks.
     int4* wlist = reinterpret_cast<int4*>(smem + EPI_LIST_OFF) + w * CAPW;
     int nlist = 0;  // wave-uniform
     int namb = 0;   // wave-uniform: ambiguous entries in this wave's list
-    // entry tag: bit 0 = a candidate of `pod`; bit 1 / bit 2 = an ambiguous pair for the count
-    // (bit 1: credit both pods, bit 2: the row pod only, a diagonal tile holding both orders);
-    // bits 3.. = its rank among the wave's listed ambiguous pairs.  A tile's ambiguous pairs take
-    // ONE contiguous range of the global list (one atomic per workgroup: ~170 pairs per C3 tile,
-    // so a per-pair atomic on one counter would serialise), in the XCD-aware tile order that
-    // corr_amb_rescore then walks (rows of neighbouring tiles shared through the caches).  A pair
-    // past a full wave list (rare) takes a slot of its own.
-    auto amb_one = [&](int4 ent) {
-      const int slot = atomicAdd(amb_n, 1);
-      if (slot < amb_cap(P)) {
-        amb[slot] = make_int2(ent.x, ent.y | ((ent.w & 2) ? AMB_BOTH : 0));
-        ambv[slot] = __int_as_float(ent.z);
-      }
+    auto append = [&](int pod, int partner, int vbits) {  // candidate of pod (rect: local buffers)
+      const int64_t lp = RECT ? pod - sh.lo : pod;
+      const int gs = atomicAdd(&A.cnt[lp], 1);
+      if (gs < CAPC) A.buf[lp * CAPC + gs] = make_int2(vbits, partner);
     };
-    auto flush_one = [&](int4 ent) {
-      if (ent.w & 6) amb_one(ent);
-      if (ent.w & 1) {
-        const int64_t lp = RECT ? ent.x - sh.lo : ent.x;
-        const int gs = atomicAdd(&cnt[lp], 1);
-        if (gs < CAPC) buf[lp * CAPC + gs] = make_int2(ent.z, ent.y);
+    auto flush_direct = [&](int4 ent) {  // DIRECT passes only: an entry past the wave's list
+      if (ent.w & 12) {
+        const int slot = atomicAdd(A.amb_n, 1);
+        if (slot < amb_cap(P)) {
+          A.amb[slot] = make_int2(ent.x, ent.y | ((ent.w & 4) ? AMB_BOTH : 0));
+          A.ambv[slot] = __int_as_float(ent.z);
+        }
       }
-    };
-    auto push = [&](bool hit, uint64_t m, int pod, int partner, float v, int tag) {
-      const int slot = nlist + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      const bool inl = hit && slot < CAPW;
-      const uint64_t mam = RECT ? 0ull : __ballot(inl && (tag & 6));
-      if (hit) {
-        const int ar = namb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mam >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)mam, 0u));
-        const int4 ent = make_int4(pod, partner, __float_as_int(v), tag | (inl && (tag & 6) ? ar << 3 : 0));
-        if (inl) wlist[slot] = ent;
-        else flush_one(ent);
-      }
-      namb += __builtin_popcountll(mam);
-      nlist += __builtin_popcountll(m);
+      if (ent.w & 1) append(ent.x, ent.y, ent.z);
+      if (ent.w & 2) append(ent.y, ent.x, ent.z);
     };
     int rcl0 = 0, rcl1 = 0;  // lane L collects the row counts of (i, e) = (L >> 4, L & 15)
     int colcnt[2] = {0, 0};
@@ -431,68 +449,103 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
         pr[4 * e4 + 2] = q.z;
         pr[4 * e4 + 3] = q.w;
       }
-      int rc[16][2];  // wave-uniform row counts of this i, [e][h]
+      float pc[2];  // diagonal tile: both orders present, candidates on the row side only
 #pragma unroll
-      for (int e = 0; e < 16; ++e) rc[e][0] = rc[e][1] = 0;
+      for (int j = 0; j < 2; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 32 + r32];
+      // hot part, both column blocks of a row slot together: |r| > tau + eps counted at once (row
+      // counts by ballot + popcount into lane i*16+e, column counts per lane); the value slots with
+      // a candidate or a value within eps of tau marked per lane (bit e) for the slow part
+      uint32_t lm[2] = {0u, 0u};
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wc * 64 + j * 32 + r32;
-        const float pc = diag ? 4.f : sphc[col];  // diagonal tile: both orders present, rows only
-        uint64_t me[16];  // per value slot: the lanes holding a candidate of the row or column pod
-        uint64_t any = 0;
+      for (int e = 0; e < 16; ++e) {
+        int c0 = 0, c1 = 0;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
+        for (int j = 0; j < 2; ++j) {
           const float a = fabsf(acc[i][j][e]);
-          if (!RECT) {  // tau: the screening threshold tau + eps (certain hits)
-            const bool hit = a > tau;
+          if (COUNTS) {
+            const bool hit = a > A.tau_hi;
             const uint64_t m = __ballot(hit);
-            rc[e][0] += __builtin_popcount((uint32_t)m);
-            rc[e][1] += __builtin_popcount((uint32_t)(m >> 32));
+            c0 += __builtin_popcount((uint32_t)m);
+            c1 += __builtin_popcount((uint32_t)(m >> 32));
             colcnt[j] += hit ? 1 : 0;
           }
-          // a candidate of the row or column pod, or (main pass) within eps of the caller's tau
-          // a candidate of the row or column pod, or (main pass) within eps of the caller's tau
-          me[e] = __ballot(a > fminf(pr[e], pc) || (!RECT && a > tau_lo && a <= tau));
-          any |= me[e];
+          const bool cond = a > fminf(pr[e], pc[j]) || (!RECT && a > A.tau_lo && a <= A.tau_hi);
+          lm[j] |= cond ? (1u << e) : 0u;
         }
-        // slow path, only for the value slots that hold a candidate: at C3 densities nearly every
-        // 16-slot group has one, but only ~5 of its 16 slots do
-        if (any && debug != 3) {
-          const int gc = (int)(rowB + col);
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            if (!me[e]) continue;  // wave-uniform
-            const float v = acc[i][j][e];
-            const float a = fabsf(v);
-            const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int gr = RECT ? spod[row] : (int)(rowA + row);
-            const bool hr = a > pr[e] && gc < P && gc != gr;  // padding partners / zeroed self: r = 0
-            const bool hc = a > pc && rowA + row < P;
-            // ambiguous for the count (main pass; padding and self excluded): rides the row entry
-            const bool am = !RECT && a > tau_lo && a <= tau && gc < P && rowA + row < P && gc != gr;
-            const bool hra = hr || am;
-            const uint64_t mr = __ballot(hra);
-            if (mr) push(hra, mr, gr, gc, v, (hr ? 1 : 0) | (am ? (diag ? 4 : 2) : 0));
-            const uint64_t mc = __ballot(hc);
-            if (mc) push(hc, mc, gc, gr, v, 1);
-
-          }
+        if (COUNTS) {
+          rcl0 = lane == i * 16 + e ? c0 : rcl0;
+          rcl1 = lane == i * 16 + e ? c1 : rcl1;
         }
       }
-      if (!RECT) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (!__ballot(lm[j] != 0u) || debug == 7) continue;  // wave-uniform
+        const int col = wc * 64 + j * 32 + r32;
+        const int gc = (int)(rowB + col);
+        const double dc = RECT ? 0.0 : (double)sdnc[col];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          rcl0 = lane == i * 16 + e ? rc[e][0] : rcl0;
-          rcl1 = lane == i * 16 + e ? rc[e][1] : rcl1;
+          if (!__ballot((lm[j] >> e) & 1u)) continue;  // wave-uniform
+          const float v = acc[i][j][e];
+          const float a = fabsf(v);
+          const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int gr = RECT ? spod[row] : (int)(rowA + row);
+          const bool hr = a > pr[e] && gc < P && gc != gr;  // padding partners / zeroed self: r = 0
+          const bool hc = a > pc[j] && rowA + row < P;
+          bool am = false, settled = false;
+          if (!RECT && a > A.tau_lo && a <= A.tau_hi && gc < P && rowA + row < P && gc != gr) {
+            // within eps of tau: the pair's own bound from the rows' rounding-error norms
+            // (corr_dnorm) often settles it; otherwise it is listed for float64 re-scoring
+            const double dr = (double)sdnr[row];
+            const double band = dr + dc + 3.0 * dr * dc + (double)A.acc_err + 1e-9;
+            if ((double)a > (double)A.tau + band) {
+              settled = true;
+            } else if ((double)a > (double)A.tau - band) {
+              am = true;
+            }
+          }
+          if (COUNTS) {
+            const uint64_t ms = __ballot(settled);
+            if (ms) {
+              rcl0 = lane == i * 16 + e ? rcl0 + __builtin_popcount((uint32_t)ms) : rcl0;
+              rcl1 = lane == i * 16 + e ? rcl1 + __builtin_popcount((uint32_t)(ms >> 32)) : rcl1;
+              colcnt[j] += settled ? 1 : 0;
+            }
+          }
+          const bool need = hr || hc || am;
+          const uint64_t m = __ballot(need);
+          if (m) {  // wave-uniform
+            const int slot = nlist + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const bool inl = slot < CAPW;
+            const uint64_t mam = __ballot(am && inl);
+            if (need) {
+              const int ar = namb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mam >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mam, 0u));
+              const int tag = (hr ? 1 : 0) | (hc ? 2 : 0) | (am ? (diag ? 8 : 4) : 0);
+              const int4 ent = make_int4(gr, gc, __float_as_int(v), tag | (am && inl ? ar << 4 : 0));
+              if (inl) {
+                wlist[slot] = ent;
+              } else if (DIRECT) {
+                flush_direct(ent);
+              }
+            }
+            namb += __builtin_popcountll(mam);
+            nlist += __builtin_popcountll(m);
+          }
         }
       }
     }
-    // reserve the buffer slots of every listed candidate at once (independent atomics in flight)
+    if (debug == 6) {  // profiling aid: epilogue loops only
+      if (nlist == 12345) A.count[0] = rcl0 + rcl1 + colcnt[0] + colcnt[1] + namb;
+      return;
+    }
     if (lane == 0) {
       wcount[w] = nlist < CAPW ? nlist : CAPW;
       wamb[w] = namb;
+      if (!DIRECT && nlist > CAPW) *sflag = 1;  // this tile's lists are incomplete: refill pass
     }
-    if (!RECT) {  // |r| > tau: one LDS add per row / column and wave
+    if (COUNTS) {  // |r| > tau: one LDS add per row / column and wave
       const int li = lane >> 4, le = lane & 15;
       const int rbase = wr * 128 + li * 32 + (le & 3) + 8 * (le >> 2);
       if (rcl0) atomicAdd(&srcnt[rbase], rcl0);
@@ -506,57 +559,66 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
       }
     }
     __syncthreads();
-    if (!RECT && tid == 0) {  // the tile's listed ambiguous pairs: one contiguous range
-      int tot = 0;
-      for (int u = 0; u < 8; ++u) tot += wamb[u];
-      int base = -1;
-      if (tot) {
-        base = atomicAdd(amb_n, tot);
-        if ((int64_t)base + tot > amb_cap(P)) base = -1;  // the list is full: the host reports it
+    const bool overflowed = !DIRECT && *sflag;
+    if (!RECT && tid == 0) {
+      if (overflowed) {  // nothing listed is committed; the refill pass recomputes the tile
+        const int slot = atomicAdd(&A.ovt[0], 1);
+        A.ovt[1 + slot] = (int32_t)(I * A.nb2 + J);
+      } else {  // the tile's listed ambiguous pairs: one contiguous range
+        int tot = 0;
+        for (int u = 0; u < 8; ++u) tot += wamb[u];
+        int base = -1;
+        if (tot) {
+          base = atomicAdd(A.amb_n, tot);
+          if ((int64_t)base + tot > amb_cap(P)) base = -1;  // the list is full: the host reports it
+        }
+        for (int u = 0; u < 8; ++u) {
+          wbase[u] = base;
+          if (base >= 0) base += wamb[u];
+        }
       }
-      for (int u = 0; u < 8; ++u) {
-        wbase[u] = base;
-        if (base >= 0) base += wamb[u];
+    }
+    if (COUNTS) {  // one global add per row / column of the tile
+      const int q = tid & (TB - 1);
+      if (tid < TB) {
+        if (srcnt[q]) atomicAdd(&A.count[rowA + q], srcnt[q]);
+      } else if (!diag && sccnt[q]) {
+        atomicAdd(&A.count[rowB + q], sccnt[q]);
       }
     }
     __syncthreads();
-    if (!RECT) {  // one global add per row / column of the tile
-      const int q = tid & (TB - 1);
-      if (tid < TB) {
-        if (srcnt[q]) atomicAdd(&count[rowA + q], srcnt[q]);
-      } else if (!diag && sccnt[q]) {
-        atomicAdd(&count[rowB + q], sccnt[q]);
-      }
-    }
-    if (debug < 2) {
-      const int4* lists = reinterpret_cast<const int4*>(smem + EPI_LIST_OFF);
-      for (int base = 0;; base += NT) {
-        bool more = false;
+    if (overflowed || debug == 5) return;
+    const int4* lists = reinterpret_cast<const int4*>(smem + EPI_LIST_OFF);
+    for (int base = 0;; base += NT) {
+      bool more = false;
 #pragma unroll
-        for (int u0 = 0; u0 < 8; u0 += 4) {
-          int4 ent[4];
-          int gs[4];
+      for (int u0 = 0; u0 < 8; u0 += 4) {
+        int4 ent[4];
+        int gs[4], gt[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int q = base + tid;
-            const bool ok = q < wcount[u0 + u];
-            more = more || base + NT < wcount[u0 + u];
-            ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(-1, 0, 0, 0);
-            const bool cand = ok && (ent[u].w & 1);
-            if (!RECT && ok && (ent[u].w & 6) && wbase[u0 + u] >= 0) {  // an ambiguous pair
-              const int slot = wbase[u0 + u] + (ent[u].w >> 3);
-              amb[slot] = make_int2(ent[u].x, ent[u].y | ((ent[u].w & 2) ? AMB_BOTH : 0));
-              ambv[slot] = __int_as_float(ent[u].z);
-            }
-            if (RECT && ok) ent[u].x -= (int)sh.lo;  // rect pass: the rank's local buffers
-            gs[u] = cand ? atomicAdd(&cnt[ent[u].x], 1) : CAPC;
+        for (int u = 0; u < 4; ++u) {
+          const int q = base + tid;
+          const bool ok = q < wcount[u0 + u];
+          more = more || base + NT < wcount[u0 + u];
+          ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(0, 0, 0, 0);
+          if (!RECT && (ent[u].w & 12) && wbase[u0 + u] >= 0) {  // an ambiguous pair
+            const int slot = wbase[u0 + u] + (ent[u].w >> 4);
+            A.amb[slot] = make_int2(ent[u].x, ent[u].y | ((ent[u].w & 4) ? AMB_BOTH : 0));
+            A.ambv[slot] = __int_as_float(ent[u].z);
           }
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (gs[u] < CAPC) buf[(int64_t)ent[u].x * CAPC + gs[u]] = make_int2(ent[u].z, ent[u].y);
+          if (RECT) {  // rect pass: the rank's local buffers
+            ent[u].x -= (int)sh.lo;
+          }
+          gs[u] = (ent[u].w & 1) ? atomicAdd(&A.cnt[ent[u].x], 1) : CAPC;
+          gt[u] = (ent[u].w & 2) ? atomicAdd(&A.cnt[ent[u].y], 1) : CAPC;
         }
-        if (!more) break;  // wave-uniform: every lane reads the same wcount[]
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (gs[u] < CAPC) A.buf[(int64_t)ent[u].x * CAPC + gs[u]] = make_int2(ent[u].z, ent[u].y);
+          if (gt[u] < CAPC) A.buf[(int64_t)ent[u].y * CAPC + gt[u]] = make_int2(ent[u].z, ent[u].x);
+        }
       }
+      if (!more) break;  // wave-uniform: every lane reads the same wcount[]
     }
     return;
   }
@@ -582,14 +644,14 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
       const int64_t g = rowA + half * BM + r;
       const int jb = 2 * (int)(J - sh.j0) + ch;  // list slot of this chunk
       const int64_t c0 = rowB + ch * BM;
-      if (g < P && (own || jb < nsb)) {
+      if (g < P && (own || jb < A.nsb)) {
         Cand<KC> cd;
         cd.init();
         const int64_t slot = g * NSL + (own ? NSB + ch : jb);
         const int cend = (int)std::min<int64_t>(BM, P - c0);
         const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
         const float* rowp = tile + r * EPI_LD + ch * BM;
-        if (self >= 0) selfd[g] = rowp[self];
+        if (self >= 0) A.selfd[g] = rowp[self];
         float lim = -1.f;
         for (int c4 = 0; c4 < cend; c4 += 4) {
           const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
@@ -603,8 +665,8 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
             }
           }
         }
-        float* ov = samp_v + slot * KC;
-        int32_t* oi = samp_i + slot * KC;
+        float* ov = A.samp_v + slot * KC;
+        int32_t* oi = A.samp_i + slot * KC;
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
           ov[q] = cd.v[q];
@@ -613,6 +675,54 @@ __global__ __launch_bounds__(NT) void corr_tiles(const uint16_t* __restrict__ zA
       }
     }
     __syncthreads();  // the next half overwrites the tile
+  }
+}
+
+
+template <int KC, int MODE>
+__global__ __launch_bounds__(NT) void corr_tiles(TileArgs A) {
+  if (MODE == MODE_RECT) {
+    tile_body<KC, MODE_RECT, true>(A, blockIdx.x / A.nb2, blockIdx.x % A.nb2, false);
+  } else if (MODE == MODE_SAMPLE) {
+    const int nsb2 = (A.nsb + 1) / 2;  // this chunk's 256-blocks
+    const int64_t I = A.sh.I0 + blockIdx.x / (nsb2 + 1);
+    int64_t J = blockIdx.x % (nsb2 + 1);
+    bool own = false;
+    if (J == nsb2) {  // the row block's own 256-block, unless it is already a sample block
+      if (!A.sh.own || I < A.sh.nsb2_all) return;
+      J = I;
+      own = true;
+    } else {
+      J += A.sh.j0;
+    }
+    tile_body<KC, MODE_SAMPLE, false>(A, I, J, own);
+  } else if (MODE == MODE_MAIN) {
+    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so slot
+    // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the
+    // upper triangle in SUPER x SUPER super-tiles, so the tiles an XCD has in flight share 2*SUPER
+    // row blocks through its L2.  Slots below the diagonal or past nb2 exit at once.
+    const int64_t b = blockIdx.x;
+    const int64_t L = (b & 7) * A.per_xcd + (b >> 3);
+    const int64_t ns = (A.nb2 + SUPER - 1) / SUPER;
+    const int64_t st = (L / (SUPER * SUPER)) * A.sh.G + A.sh.g;  // this rank's super-tiles
+    if (st >= ns * (ns + 1) / 2) return;
+    int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
+    while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
+    while (SJ * (SJ + 1) / 2 > st) --SJ;
+    const int64_t SI = st - SJ * (SJ + 1) / 2;
+    const int64_t in = L % (SUPER * SUPER);
+    int64_t I = SI * SUPER + in / SUPER;
+    int64_t J = SJ * SUPER + in % SUPER;
+    if (I > J || J >= A.nb2) return;
+    if (A.debug == 4) I = J = (blockIdx.x & 7);  // profiling aid: product only, operands L2-resident
+    tile_body<KC, MODE_MAIN, false>(A, I, J, false);
+  } else {  // MODE_REFILL: persistent over the device-held list of overflowed tiles
+    const int n = A.ovt[0];
+    for (int t = blockIdx.x; t < n; t += gridDim.x) {
+      const int32_t code = A.ovt[1 + t];
+      __syncthreads();  // the previous tile's LDS is free
+      tile_body<KC, MODE_MAIN, true>(A, code / A.nb2, code % A.nb2, false);
+    }
   }
 }
 
@@ -953,8 +1063,9 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
   }
 }
 
-// profiling aid, KRCA_CORR_DEBUG (results are wrong when set): 1 = product only, 2 = no global
-// candidate appends, 3 = no candidate slow path either
+// profiling aid, KRCA_CORR_DEBUG (results are wrong when set): 1 = product only, 4 = product only
+// with every tile reading the same few row blocks (operands L2-resident), 5 = no list flush, 6 = the
+// epilogue loops only (no counts, no lists committed), 7 = no slow path
 int debug_mode() { return krca::tuning().corr_debug; }
 
 constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
@@ -1012,6 +1123,7 @@ struct CorrWs {  // views into a caller's candidate workspace
   float* ambv;          // [amb_cap(P)] their screening values
   float* dn;            // [P] fp16 rounding-error norm of each row
   int32_t* amb_n;       // [4]: their count (past the capacity: an error)
+  int32_t* ovt;         // [1 + tiles]: main-pass tiles whose candidate lists overflowed LDS
   uint16_t* zs;         // [RECT_ROWS][Tp]
   int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
   int32_t* fill;        // sharded: [n_loc]
@@ -1040,6 +1152,10 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   w.ambv = reinterpret_cast<float*>(take(amb_cap(P)));
   w.dn = reinterpret_cast<float*>(take(P));
   w.amb_n = reinterpret_cast<int32_t*>(take(4));
+  {
+    const int64_t nb2 = krca::ceil_div(P, TB);
+    w.ovt = reinterpret_cast<int32_t*>(take(1 + nb2 * (nb2 + 1) / 2));
+  }
   w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
   if (G > 0) {
     w.lbuf = reinterpret_cast<int2*>(take(2 * n_loc * CAPC));
@@ -1059,6 +1175,8 @@ int set_lds_attr() {
     KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_SAMPLE>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
     KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_RECT>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_REFILL>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
     done = true;
   }
@@ -1101,11 +1219,19 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
     sh.j0 = c0;
     sh.own = c0 == 0;
     sh.nsb2_all = nsb2_all;
+    TileArgs ta{};
+    ta.zA = zh;
+    ta.zh = zh;
+    ta.P = d.P;
+    ta.Tp = d.Tp;
+    ta.nb2 = d.nb2;
+    ta.nsb = nsb_c;
+    ta.samp_v = ws.samp_v;
+    ta.samp_i = ws.samp_i;
+    ta.selfd = ws.selfd;
+    ta.sh = sh;
     hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES,
-                       st, zh, zh, d.P, d.Tp, d.nb2, (int64_t)0, nsb_c, d.tau, (const float*)nullptr, ws.samp_v,
-                       ws.samp_i, ws.selfd, (int2*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
-                       (const int32_t*)nullptr, (int64_t)0, sh, 0, 2.f, (int2*)nullptr, (int32_t*)nullptr,
-                       (float*)nullptr);
+                       st, ta);
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
                        ws.samp_i, ws.selfd, lo, lo + n, nsb_c, d.k, d.eps, ws.run, (int)(c0 == 0),
@@ -1123,23 +1249,49 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(ws.amb_n, 0, 4 * sizeof(int32_t), st));
+  KRCA_HIP(hipMemsetAsync(ws.ovt, 0, sizeof(int32_t), st));
   const int64_t ns = (d.nb2 + SUPER - 1) / SUPER;
   const int64_t n_st = ns * (ns + 1) / 2;
   const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
   if (n_mine == 0) return KRCA_OK;
   const int64_t per_xcd = (n_mine * SUPER * SUPER + 7) / 8;
   const Shard sh{0, G, g, 0};
-  // screening counts: certain above tau + eps, re-scored within eps of tau (exact counts)
-  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, zh, zh, d.P,
-                     d.Tp, d.nb2, per_xcd, d.nsb, d.tau + d.eps, phi, (float*)nullptr, (int32_t*)nullptr,
-                     (float*)nullptr, ws.buf, ws.cnt, count, (const int32_t*)nullptr, (int64_t)0, sh, dbg,
-                     d.tau - d.eps, ws.amb, ws.amb_n, ws.ambv);
+  hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
+                     d.Tp, ws.dn);
+  KRCA_LAUNCH_CHECK();
+  const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
+  // screening counts: certain above tau + eps, decided in the tile by the pair's own bound or
+  // re-scored within it (exact counts)
+  TileArgs ta{};
+  ta.zA = zh;
+  ta.zh = zh;
+  ta.P = d.P;
+  ta.Tp = d.Tp;
+  ta.nb2 = d.nb2;
+  ta.per_xcd = per_xcd;
+  ta.nsb = d.nsb;
+  ta.tau_hi = d.tau + d.eps;
+  ta.tau_lo = d.tau - d.eps;
+  ta.tau = d.tau;
+  ta.acc_err = acc_err;
+  ta.phi = phi;
+  ta.buf = ws.buf;
+  ta.cnt = ws.cnt;
+  ta.count = count;
+  ta.sh = sh;
+  ta.debug = dbg;
+  ta.amb = ws.amb;
+  ta.amb_n = ws.amb_n;
+  ta.ambv = ws.ambv;
+  ta.dn = ws.dn;
+  ta.ovt = ws.ovt;
+  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, ta);
   KRCA_LAUNCH_CHECK();
   if (dbg == 0) {
-    hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
-                       d.Tp, ws.dn);
+    // tiles whose lists overflowed (device-held count; usually none: the workgroups exit at once)
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_REFILL>), dim3((unsigned)std::min<int64_t>(1024, n_mine * SUPER * SUPER)),
+                       dim3(NT), LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
-    const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
     hipLaunchKernelGGL(corr_amb_rescore, dim3(4096), dim3(TPB), 0, st, (const int2*)ws.amb, (const float*)ws.ambv,
                        (const int32_t*)ws.amb_n, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
     KRCA_LAUNCH_CHECK();
@@ -1189,11 +1341,20 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
     hipLaunchKernelGGL(corr_gather_rows, dim3((unsigned)npad), dim3(TPB), 0, st, zh, d.Tp,
                        (const int32_t*)(ws.over + 1 + r0), nr, ws.zs);
     KRCA_LAUNCH_CHECK();
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * d.nb2)), dim3(NT), LDS_BYTES, st,
-                       (const uint16_t*)ws.zs, zh, d.P, d.Tp, d.nb2, (int64_t)0, d.nsb, d.tau,
-                       (const float*)ws.phi2, (float*)nullptr, (int32_t*)nullptr, (float*)nullptr, lbuf, lcnt,
-                       (int32_t*)nullptr, (const int32_t*)(ws.over + 1 + r0), nr, sh, 0, 2.f, (int2*)nullptr,
-                       (int32_t*)nullptr, (float*)nullptr);
+    TileArgs ta{};
+    ta.zA = ws.zs;
+    ta.zh = zh;
+    ta.P = d.P;
+    ta.Tp = d.Tp;
+    ta.nb2 = d.nb2;
+    ta.nsb = d.nsb;
+    ta.phi = ws.phi2;
+    ta.buf = lbuf;
+    ta.cnt = lcnt;
+    ta.rect_pods = ws.over + 1 + r0;
+    ta.n_rect = nr;
+    ta.sh = sh;
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * d.nb2)), dim3(NT), LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,

@@ -139,6 +139,27 @@ def test_corr_sample_in_chunks(eng):
     assert bad == 0
 
 
+def test_corr_list_overflow_refill(eng):
+    """Two groups of 600 identical series: every in-group pair is a candidate of both pods, so the
+    LDS candidate lists of the in-group tiles overflow and the refill pass recomputes those tiles
+    with direct appends.  Every row equals the oracle (ties at r = 1 go to the lower index)."""
+    P, T, k = 1800, 256, 10
+    base = synth.make_metrics(P, 1, T, seed=11, group_size=0)
+    x = base.clone()
+    for g0 in (0, 600):
+        x[:, g0:g0 + 600, 0] = base[:, g0:g0 + 1, 0]
+    res = eng.corr_topk(x, k=k, tau=TAU)
+    z = oracle.corr_standardize(x.numpy(), 0)
+    check_rows(res, z, np.arange(P), k)
+    # in-group pairs tie exactly (identical rows; the float64 oracle's BLAS breaks them by rounding
+    # noise): the device keeps the k lowest indices of the group
+    for p in range(1200):
+        g0 = p // 600 * 600
+        want = [q for q in range(g0, g0 + 600) if q != p][:k]
+        assert res["idx"][p].tolist() == want, (p, res["idx"][p])
+    assert np.all(res["count"][:1200] >= 599)
+
+
 def test_corr_rejects_bad_k(eng):
     x = torch.rand(50, 10, 1)
     with pytest.raises(native.KrcaError):
