@@ -42,6 +42,8 @@
 //                      (k-th exact |r|) - phi - eps > 0.
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "krca_common.h"
@@ -72,6 +74,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 str
 __device__ __forceinline__ uint16_t f16_bits(float f) {
   const _Float16 h = (_Float16)f;  // round to nearest even
   return __builtin_bit_cast(uint16_t, h);
+}
+
+template <int... Is, class F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {  // f(integral_constant<int, k>) for k = 0 .. N-1
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
 // ---- prepare -------------------------------------------------------------------------------
@@ -159,37 +170,53 @@ struct Cand {
   }
 };
 
-// Tile kernel: 256 x 256 pods per workgroup (8 waves = 2 row halves x 4 column quarters, a
-// 128 x 64 wave tile = 4 x 2 MFMA 32x32 blocks), K steps of 64 through a double-buffered LDS
-// stage (A and B 256 x 64 fp16 each) fed by direct global->LDS loads.  Sample-pass lists keep a
-// 128-pod block granularity (a row's list covers one 128-column half of the tile).
-constexpr int TB = 256;                                // tile edge (pods)
-constexpr int NT = 512;                                // threads per tile workgroup
-constexpr int STAGE_BYTES = 2 * TB * BK * 2;           // A and B, fp16
-constexpr int LDS_STAGE = 2 * STAGE_BYTES;             // double buffered: 128 KB
-constexpr int EPI_LD = TB + 4;  // padded row of the epilogue half tile (16-B rows; conflict-free b128 row reads)
-constexpr int LDS_EPI = BM * EPI_LD * 4;               // 128 rows x 256 columns fp32
-constexpr int LDS_MAIN = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
-constexpr int LDS_JUNK = NT * 4;                       // landing slots of the L2 prefetch loads
-constexpr int LDS_BYTES = LDS_MAIN + LDS_JUNK;
-constexpr int EPI_LIST_OFF = 8192;                     // main-pass epilogue: per-wave candidate lists
-constexpr int CAPW = (LDS_MAIN - EPI_LIST_OFF) / (8 * 16);
+// Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh.  A wave holds a 128 x 64
+// tile = 4 x 2 MFMA 32x32 blocks; K steps run through a double-buffered LDS stage fed by direct
+// global->LDS loads.
+//   TC = 256: 8 waves (2 row halves x 4 column quarters), K steps of 64, 130 KB of LDS: one
+//             workgroup per CU (every pass).
+//   TC = 128: 4 waves (2 x 2), K steps of 32, 49 KB of LDS: two workgroups share a CU, so one's
+//             epilogue runs beside the other's MFMAs (the main pass under KRCA_CORR_TC=128; its
+//             product runs 1.6x slower: at 1.5x the staged bytes per flop, the per-CU L2 -> LDS
+//             delivery is the bound).
+// Every output accumulates its 16-deep K slices in ascending order in both geometries, so a pair's
+// screening value is the same bits in every pass.  Sample-pass lists keep a 128-pod block
+// granularity (a row's list covers one 128-column half of a 256-column tile).
+constexpr int TB = 256;                  // row block (pods); the unit of the upper-triangle order
+constexpr int EPI_LD = TB + 4;           // padded row of the sample pass's parked half tile (16-B rows)
+constexpr int EPI_LIST_OFF = 8192;       // main-pass epilogue: per-wave candidate lists start here
+template <int TC>
+struct Geo {
+  static constexpr int NWC = TC / 64;                     // wave columns
+  static constexpr int NW = 2 * NWC;                      // waves
+  static constexpr int NTH = 64 * NW;                     // threads
+  static constexpr int BKS = TC == 256 ? 64 : 32;         // K step (time samples)
+  static constexpr int KS = BKS / 16;                     // MFMA slices per K step
+  static constexpr int ROWB = BKS * 2;                    // bytes of one staged row (fp16)
+  static constexpr int CPR = ROWB / 16;                   // 16-byte chunks per staged row
+  static constexpr int RPP = 1024 / ROWB;                 // rows per 1 KiB LDS-DMA piece
+  static constexpr int NPA = TB / RPP / NW, NPB = TC / RPP / NW;  // pieces per wave and K step
+  static constexpr int STAGE = (TB + TC) * ROWB;          // A and B
+  static constexpr int LDS_STAGE = 2 * STAGE;             // double buffered
+  static constexpr int LDS_EPI = TC == 256 ? BM * EPI_LD * 4 : 0;  // sample pass: 128 x 256 fp32
+  static constexpr int LDS_MAIN = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
+  static constexpr int LDS_BYTES = LDS_MAIN + NTH * 4;    // + landing slots of the L2 prefetch loads
+  static constexpr int PFD = TC == 256 ? 2 : 4;           // L2 prefetch distance (K steps)
+  static constexpr int CAPL = (LDS_MAIN - EPI_LIST_OFF) / (NW * 8);  // epilogue list entries per wave
+  // 16-byte chunk c of staged row r, XOR-swizzled: the 256/ROWB rows of one 256-B bank row sit in
+  // distinct granule groups and the key (r / (256/ROWB)) % CPR spreads the rest, so every 16-lane
+  // ds_read_b128 phase of 16 rows hits 16 distinct 4-bank granules
+  __device__ static __forceinline__ int key(int r) { return (r / (256 / ROWB)) & (CPR - 1); }
+  __device__ static __forceinline__ int chunk_off(int r, int c) { return r * ROWB + ((c ^ key(r)) << 4); }
+};
 
-// 16-byte chunk c (0..7) of row r of a [rows][64] fp16 stage, XOR-swizzled against bank conflicts
-// (the XOR key (r >> 1) & 7 makes every 16-lane ds_read_b128 phase of 16 rows hit 16 distinct
-// 4-bank granules: row parity picks the 32-bank half, the key the granule inside it)
-__device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
-
-// MODE_MAIN:   the upper triangle of 256-blocks (all pairs); hits above phi appended to the
-//              per-pod candidate buffers (row and column side), |r| > tau counted.
+// MODE_MAIN:   the upper triangle of 256-blocks (all pairs), in TC-column tiles; hits above phi
+//              appended to the per-pod candidate buffers (row and column side), |r| > tau counted.
 // MODE_SAMPLE: rows x (the first nsb 128-column blocks, then the row's own 256-block): row lists
 //              only (sample slots NSB, NSB+1 = own block), and each pod's self product.
 // MODE_RECT:   the gathered rows zA = zh[rect_pods] x every column block (second pass of the pods
 //              whose buffer overflowed): row-side appends only, against phi = phi2.
-// MODE_REFILL: the main-pass tiles whose candidate lists overflowed LDS (rare: a wave's list holds
-//              CAPW entries), recomputed with every entry past the list appended to the global
-//              buffers at once; their counts were already added by the main pass.
-constexpr int MODE_MAIN = 0, MODE_SAMPLE = 1, MODE_RECT = 2, MODE_REFILL = 3;
+constexpr int MODE_MAIN = 0, MODE_SAMPLE = 1, MODE_RECT = 2;
 
 // Pod-sharded runs: rank g of G takes every G-th super-tile of the upper triangle
 // (MAIN), the row blocks [I0, ...) of its own pods (SAMPLE), and appends the candidates of its own
@@ -208,7 +235,7 @@ struct TileArgs {
   const uint16_t* zh;
   int64_t P;
   int Tp, nb2;
-  int64_t per_xcd;
+  int64_t per_xcd;     // MAIN: workgroup slots per XCD
   int nsb;
   float tau_hi;   // MAIN: tau + eps, every screening |r| above it is a hit
   float tau_lo;   // MAIN: tau - eps, none at or below it is
@@ -229,41 +256,46 @@ struct TileArgs {
   int32_t* amb_n;
   float* ambv;
   const float* dn;  // MAIN: fp16 rounding-error norm per pod (corr_dnorm)
-  int32_t* ovt;     // MAIN / REFILL: [0] overflowed tiles, then I * nb2 + J each
 };
 
-// One 256 x 256 tile (I, J).  DIRECT: list entries past CAPW go to the global buffers at once (rect
-// and refill passes); otherwise a full list marks the tile for the refill pass.
-template <int KC, int MODE, bool DIRECT>
-__device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, const int64_t J, const bool own) {
+// One tile: row block I (256 pods), column block J (TC pods).  Main / rect passes: the epilogue takes
+// the flagged values of list slots [win, win + CAPL) of each wave; returns whether some wave has
+// more (rare: the caller runs the tile again for the next window; the counts of |r| > tau + eps are
+// taken in window 0 only).
+template <int KC, int MODE, int TC>
+__device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, const int64_t J, const bool own,
+                                          const int win) {
+  using G = Geo<TC>;
   constexpr bool SAMPLE = MODE == MODE_SAMPLE;
+  static_assert(!SAMPLE || TC == 256, "the sample pass parks 256-column tiles");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t P = A.P;
   const int Tp = A.Tp;
   const Shard& sh = A.sh;
   const int debug = A.debug;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 2, wc = w & 3;
-  const int64_t rowA = I * TB, rowB = J * TB;
-  // main / rect epilogue operands, loaded now so their latency hides behind the K loop: thread
-  // tid < 256 holds row pod tid of the tile, its phi and rounding-error norm, thread tid >= 256
-  // column pod tid - 256
-  int my_pod = -1;
-  float my_phi = 4.f;  // 4 = never a candidate owner (padding, or column side of a rect pass)
-  float my_dn = 0.f;
+  const int wr = w / G::NWC, wc = w % G::NWC;
+  const int64_t rowA = I * TB, rowB = J * TC;
+  // main / rect epilogue operands, loaded now so their latency hides behind the K loop: thread rq
+  // (< 256) holds row pod rq of the tile, its phi and rounding-error norm; thread cq (in [0, TC))
+  // column pod cq
+  const int rq = tid;
+  const int cq = G::NTH == 2 * TB ? tid - TB : tid;
+  int r_pod = -1;
+  float r_phi = 4.f, c_phi = 4.f;  // 4 = never a candidate owner (padding, or column side of a rect pass)
+  float r_dn = 0.f, c_dn = 0.f;
   if (!SAMPLE) {
-    const int q = tid & (TB - 1);
-    if (tid < TB) {
-      const int64_t g = MODE == MODE_RECT ? (rowA + q < A.n_rect ? A.rect_pods[rowA + q] : -1) : (rowA + q < P ? rowA + q : -1);
-      my_pod = (int)g;
+    if (rq < TB) {
+      const int64_t g = MODE == MODE_RECT ? (rowA + rq < A.n_rect ? A.rect_pods[rowA + rq] : -1) : (rowA + rq < P ? rowA + rq : -1);
+      r_pod = (int)g;
       if (g >= 0) {
-        my_phi = A.phi[g];
-        if (MODE == MODE_MAIN) my_dn = A.dn[g];
+        r_phi = A.phi[g];
+        if (MODE == MODE_MAIN) r_dn = A.dn[g];
       }
-    } else if (MODE == MODE_MAIN && rowB + q < P) {
-      my_pod = (int)(rowB + q);
-      my_phi = A.phi[rowB + q];
-      my_dn = A.dn[rowB + q];
+    }
+    if (MODE == MODE_MAIN && cq >= 0 && cq < TC && rowB + cq < P) {
+      c_phi = A.phi[rowB + cq];
+      c_dn = A.dn[rowB + cq];
     }
   }
 
@@ -276,35 +308,43 @@ __device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, co
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   // Staging: global -> LDS direct (global_load_lds_dwordx4, no VGPR round trip).  One wave
-  // instruction writes a lane-linear 1 KiB piece = 8 rows of 128 B; lane l lands on row l/8,
-  // slot l%8, so it fetches the global chunk (l%8) ^ key(row): the XOR swizzle is applied on the
-  // SOURCE address.  64 pieces per K step (32 A + 32 B), 8 per wave.
+  // instruction writes a lane-linear 1 KiB piece = RPP rows; lane l lands on row l / CPR, slot
+  // l % CPR, so it fetches the global chunk (l % CPR) ^ key(row): the XOR swizzle is applied on the
+  // SOURCE address.
   const uint16_t* gA = A.zA + rowA * Tp;
   const uint16_t* gB = A.zh + rowB * Tp;
-  const int prow = lane >> 3, pslot = lane & 7;
-#define CORR_GLDS(BUF, K0)                                                                             \
-  _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                      \
-    const int piece = w + 8 * q;      /* rows 8*piece .. +7 */                                         \
-    const int row = 8 * piece + prow;                                                                  \
-    const int64_t src = (int64_t)row * Tp + (K0) + ((pslot ^ ((row >> 1) & 7)) << 3);                 \
-    char* dA = smem + (BUF) * STAGE_BYTES + piece * 1024;                                              \
-    __builtin_amdgcn_global_load_lds(gA + src, (__attribute__((address_space(3))) void*)dA, 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds(gB + src, (__attribute__((address_space(3))) void*)(dA + TB * BK * 2), \
-                                     16, 0, 0);                                                       \
-  }
+  const int prow = lane / G::CPR, pslot = lane % G::CPR;
+  auto glds = [&](int buf, int k0) {
+    char* sbase = smem + buf * G::STAGE;
+#pragma unroll
+    for (int q = 0; q < G::NPA; ++q) {
+      const int piece = w + G::NW * q;
+      const int row = G::RPP * piece + prow;
+      __builtin_amdgcn_global_load_lds(gA + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
+                                       (__attribute__((address_space(3))) void*)(sbase + piece * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < G::NPB; ++q) {
+      const int piece = w + G::NW * q;
+      const int row = G::RPP * piece + prow;
+      __builtin_amdgcn_global_load_lds(gB + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
+                                       (__attribute__((address_space(3))) void*)(sbase + TB * G::ROWB + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
   const int r32 = lane & 31, h = lane >> 5;
   // Fragments in two register sets: the 6 fragments of 16-deep slice ks+1 are read while the 8 MFMAs
-  // of slice ks run, and slice 0 of step s+1 right after the step's barrier, beside slice 3's MFMAs,
-  // so no MFMA waits on a just-issued LDS read.
+  // of slice ks run, and slice 0 of step s+1 right after the step's barrier, beside the last slice's
+  // MFMAs, so no MFMA waits on a just-issued LDS read.
   halfx8 fa[2][4], fb[2][2];
   auto frag_load = [&](int buf, int ks, int set) {
-    const char* sA = smem + buf * STAGE_BYTES;
-    const char* sB = sA + TB * BK * 2;
+    const char* sA = smem + buf * G::STAGE;
+    const char* sB = sA + TB * G::ROWB;
     const int c = ks * 2 + h;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[set][i] = *reinterpret_cast<const halfx8*>(sA + chunk_off(wr * 128 + i * 32 + r32, c));
+    for (int i = 0; i < 4; ++i) fa[set][i] = *reinterpret_cast<const halfx8*>(sA + G::chunk_off(wr * 128 + i * 32 + r32, c));
 #pragma unroll
-    for (int j = 0; j < 2; ++j) fb[set][j] = *reinterpret_cast<const halfx8*>(sB + chunk_off(wc * 64 + j * 32 + r32, c));
+    for (int j = 0; j < 2; ++j) fb[set][j] = *reinterpret_cast<const halfx8*>(sB + G::chunk_off(wc * 64 + j * 32 + r32, c));
   };
   auto frag_mfma = [&](int set) {
 #pragma unroll
@@ -313,16 +353,23 @@ __device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, co
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
   };
-  // L2 prefetch of K step s+2 while step s+1 streams into LDS: one 4-byte LDS-DMA per 128-B line
-  // (lane tid < 256: A row tid, else B row tid-256) into a junk LDS slot, so no VGPR is tied up;
-  // step s+2's 16-byte loads then hit L2 instead of paying the HBM/MALL latency inside one
-  // K step's compute.  The barrier waits vmcnt(1): the stage loads, issued before it, are done.
-  const uint16_t* gP = (tid < TB ? gA + (int64_t)tid * Tp : gB + (int64_t)(tid - TB) * Tp);
-  char* junk = smem + LDS_MAIN + w * 256;
-#define CORR_L2PF(K0) \
-  __builtin_amdgcn_global_load_lds(gP + (K0), (__attribute__((address_space(3))) void*)junk, 4, 0, 0);
-  const int nk = Tp / BK;
-  CORR_GLDS(0, 0)
+  // L2 prefetch of K step s+PFD while step s+1 streams into LDS: one 4-byte LDS-DMA per 128-B line
+  // into a junk LDS slot, so no VGPR is tied up; those steps' 16-byte loads then hit L2 instead of
+  // paying the HBM/MALL latency inside one K step's compute.  TC = 256: thread tid < 256 takes A
+  // row tid, else B row tid - 256, every step.  TC = 128 (a line spans two 32-deep steps): A row tid
+  // on even steps, B row tid (tid < 128) on odd ones.  One load per thread and step, so the
+  // barrier's vmcnt(1) leaves exactly it outstanding.
+  const int nk = Tp / G::BKS;
+  const uint16_t* gP = TC == 256 ? (tid < TB ? gA + (int64_t)tid * Tp : gB + (int64_t)(tid - TB) * Tp)
+                                 : gA + (int64_t)tid * Tp;
+  const uint16_t* gPB = gB + (int64_t)(tid & (TC - 1)) * Tp;
+  char* junk = smem + G::LDS_MAIN + w * 256;
+  auto l2pf = [&](int s) {
+    const int sp = s + G::PFD < nk ? s + G::PFD : 0;  // past the end: re-touches a resident line
+    const uint16_t* src = (TC == 128 && (s & 1) && tid < TC) ? gPB : gP;
+    __builtin_amdgcn_global_load_lds(src + sp * G::BKS, (__attribute__((address_space(3))) void*)junk, 4, 0, 0);
+  };
+  glds(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   frag_load(0, 0, 0);
@@ -330,14 +377,8 @@ __device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, co
     const int buf = s & 1;
     // stage buf ^ 1 was last read in step s-1; every wave retired those reads (lgkmcnt(0)) before
     // the barrier that ended it
-    if (s + 1 < nk) {
-      CORR_GLDS(buf ^ 1, (s + 1) * BK)
-    }
-    if (s + 2 < nk) {
-      CORR_L2PF((s + 2) * BK)
-    } else {
-      CORR_L2PF(0)  // keeps the count of outstanding loads uniform (re-touches a resident line)
-    }
+    if (s + 1 < nk) glds(buf ^ 1, (s + 1) * G::BKS);
+    l2pf(s);
     __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs, not after
     // each phase: the 8 MFMAs of one slice with the 6 reads of the next one between them (pinned:
     // left alone, the scheduler sinks every read to its first use and waits on it there)
@@ -351,8 +392,10 @@ __device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, co
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                               \
     __builtin_amdgcn_sched_barrier(0);
     CORR_PHASE(buf, 1, 1, 0)
-    CORR_PHASE(buf, 2, 0, 1)
-    CORR_PHASE(buf, 3, 1, 0)
+    if constexpr (G::KS == 4) {
+      CORR_PHASE(buf, 2, 0, 1)
+      CORR_PHASE(buf, 3, 1, 0)
+    }
     // stage buf ^ 1 has landed for this wave (only the L2 prefetch may be outstanding) and this
     // wave's reads of stage buf are retired; after the barrier, for every wave.  The last step
     // reads stage buf ^ 1 as well (stale bytes, never used): no branch in the loop.
@@ -364,326 +407,334 @@ __device__ __forceinline__ void tile_body(const TileArgs& A, const int64_t I, co
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-#undef CORR_GLDS
-#undef CORR_COMPUTE
-#undef CORR_L2PF
-  const bool diag = MODE != MODE_RECT && I == J;
+  // a diagonal 256-block: its tiles hold both orders of every pair (across the TC-column tiles of
+  // the block), so counts and candidates go to the row side only
+  const bool diag = MODE != MODE_RECT && rowB / TB == I;
   if (debug == 1 || debug == 4) {  // profiling aid (KRCA_CORR_DEBUG=1 / 4): product only, no epilogue
     if (tid == 0 && acc[0][0][0] == 12345.f) A.count[0] = 1;
-    return;
+    return false;
   }
-  if (!SAMPLE) {
-    // ---- main / rect pass: epilogue straight from the accumulators -------------------------
+  if constexpr (!SAMPLE) {
+    // ---- main / rect epilogue, straight from the accumulators ---------------------------
     // lane holds rows wr*128 + i*32 + (e&3) + 8*(e>>2) + 4*h and columns wc*64 + j*32 + r32.
     // Padding rows / columns have z = 0 (r = 0: never above tau >= 0) and phi = 4 (never a
-    // candidate); the self products of a diagonal tile are zeroed first.  The common case costs
-    // a few vector ops per value; only a value slot with a candidate or a screening |r| within eps
-    // of tau in some lane takes the slow path.
+    // candidate); the self products of a diagonal tile are zeroed first.
+    //   1. per wave, branch-free over a lane's 128 values: |r| > tau + eps counted (row counts by
+    //      ballot + popcount, kept in lane (i, e); column counts per lane), and each
+    //      value that may need anything (above phi of its row or column pod, or within eps of tau)
+    //      appended RAW to the wave's LDS list {row | col << 8, r bits} (ballot + mbcnt, only when
+    //      some lane has one: they are sparse)
+    //   2. every thread takes list entries: classified (candidate of the row / column pod; within eps
+    //      of tau: settled by the pair's own rounding-error bound, or ambiguous), settled pairs
+    //      counted in LDS, ambiguous pairs ranked in the tile (one LDS atomic per wave and round)
+    //   3. counts committed (one global add per row / column), ONE global atomic reserves the tile's
+    //      range of the ambiguous-pair list, then the entries are written out (ambiguous list,
+    //      candidate buffers)
     constexpr bool RECT = MODE == MODE_RECT;
-    constexpr bool COUNTS = MODE == MODE_MAIN && !DIRECT;  // a refill pass re-lists only
+    constexpr bool HITS = MODE == MODE_MAIN;    // |r| > tau + eps counted in step 1 (first window)
+    constexpr bool SETTLE = MODE == MODE_MAIN;  // pairs settled by their bound counted in step 2
+    constexpr int CAPL = G::CAPL;
+    constexpr int RANKS = 1 << 13;  // ambiguous pairs ranked per tile (the rest: one global atomic each)
     float* sphr = reinterpret_cast<float*>(smem);  // phi of the 256 row pods
-    float* sphc = sphr + TB;                        // phi of the 256 column pods
-    int* srcnt = reinterpret_cast<int*>(sphc + TB);  // |r| > tau counts per row / column
+    float* sphc = sphr + TB;                        // phi of the TC column pods
+    int* srcnt = reinterpret_cast<int*>(sphc + TC);  // |r| > tau counts per row / column
     int* sccnt = srcnt + TB;
-    int* spod = sccnt + TB;    // row pod ids
+    int* spod = sccnt + TC;    // row pod ids
     float* sdnr = reinterpret_cast<float*>(spod + TB);  // rounding-error norms of the rows / columns
     float* sdnc = sdnr + TB;
-    int* wcount = reinterpret_cast<int*>(sdnc + TB);  // candidate-list length per wave
-    int* wamb = wcount + 8;   // ambiguous entries in each wave's list
-    int* wbase = wamb + 8;    // their first slot in the ambiguous-pair list (-1: list full)
-    int* sflag = wbase + 8;   // a wave's list overflowed
+    int* wcount = reinterpret_cast<int*>(sdnc + TC);  // list length per wave
+    int* sflag = wcount + G::NW;  // [0] a list passed its window, [1] ranked ambiguous pairs, [2] their base
+    int2* lists = reinterpret_cast<int2*>(smem + EPI_LIST_OFF);
     {
-      const int q = tid & (TB - 1);
-      (tid < TB ? sphr : sphc)[q] = my_phi;
-      (tid < TB ? srcnt : sccnt)[q] = 0;
-      (tid < TB ? sdnr : sdnc)[q] = my_dn;
-      if (tid < TB) spod[q] = my_pod;
-      if (tid == 0) *sflag = 0;
+      if (rq < TB) {
+        sphr[rq] = r_phi;
+        srcnt[rq] = 0;
+        sdnr[rq] = r_dn;
+        spod[rq] = r_pod;
+      }
+      if (cq >= 0 && cq < TC) {
+        sphc[cq] = c_phi;
+        sccnt[cq] = 0;
+        sdnc[cq] = c_dn;
+      }
+      if (tid == 0) {
+        sflag[0] = 0;
+        sflag[1] = 0;
+      }
     }
     __syncthreads();
     if (diag) {
+      const int doff = (int)(rowB - rowA);  // global row == global column <=> row - col == doff
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int e = 0; e < 16; ++e)
-            if (wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h == wc * 64 + j * 32 + r32) acc[i][j][e] = 0.f;
+            if (wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h == wc * 64 + j * 32 + r32 + doff) acc[i][j][e] = 0.f;
     }
-    // per-wave list in LDS, one entry per (row, column) pair that needs anything, compacted by
-    // ballot + mbcnt (no atomics, no waiting): {row pod, column pod, r bits, tag}.  Tag bit 0: a
-    // candidate of the row pod, bit 1: of the column pod, bit 2 / 3: an ambiguous pair for the
-    // count (bit 2: credit both pods, bit 3: the row pod only, a diagonal tile holding both
-    // orders); bits 4..: its rank among the wave's listed ambiguous pairs.  A tile's ambiguous pairs
-    // take ONE contiguous range of the global list (one atomic per workgroup), in the XCD-aware tile
-    // order that corr_amb_rescore then walks.
-    int4* wlist = reinterpret_cast<int4*>(smem + EPI_LIST_OFF) + w * CAPW;
-    int nlist = 0;  // wave-uniform
-    int namb = 0;   // wave-uniform: ambiguous entries in this wave's list
     auto append = [&](int pod, int partner, int vbits) {  // candidate of pod (rect: local buffers)
       const int64_t lp = RECT ? pod - sh.lo : pod;
       const int gs = atomicAdd(&A.cnt[lp], 1);
       if (gs < CAPC) A.buf[lp * CAPC + gs] = make_int2(vbits, partner);
     };
-    auto flush_direct = [&](int4 ent) {  // DIRECT passes only: an entry past the wave's list
-      if (ent.w & 12) {
-        const int slot = atomicAdd(A.amb_n, 1);
-        if (slot < amb_cap(P)) {
-          A.amb[slot] = make_int2(ent.x, ent.y | ((ent.w & 4) ? AMB_BOTH : 0));
-          A.ambv[slot] = __int_as_float(ent.z);
+    // classification of one flagged value: bit 0 candidate of the row pod, bit 1 of the column pod
+    // (never in a diagonal tile: both orders are present), bit 2 ambiguous, bit 3 settled above tau
+    auto classify = [&](int row, int col, float v) -> int {
+      const float a = fabsf(v);
+      const int gr = RECT ? spod[row] : (int)(rowA + row);
+      const int gc = (int)(rowB + col);
+      const bool pair = gc < P && gc != gr;  // padding partners / zeroed self: r = 0
+      int tag = (a > sphr[row] && pair) ? 1 : 0;
+      if (!RECT && !diag && a > sphc[col] && rowA + row < P) tag |= 2;
+      if (!RECT && a > A.tau_lo && a <= A.tau_hi && pair && rowA + row < P) {
+        // within eps of tau: the pair's own bound from the rows' rounding-error norms (corr_dnorm)
+        // often settles it; otherwise it is listed for float64 re-scoring
+        const double dr = (double)sdnr[row], dc = (double)sdnc[col];
+        const double band = dr + dc + 3.0 * dr * dc + (double)A.acc_err + 1e-9;
+        if ((double)a > (double)A.tau + band) {
+          tag |= 8;
+        } else if ((double)a > (double)A.tau - band) {
+          tag |= 4;
         }
       }
-      if (ent.w & 1) append(ent.x, ent.y, ent.z);
-      if (ent.w & 2) append(ent.y, ent.x, ent.z);
+      return tag;
     };
-    int rcl0 = 0, rcl1 = 0;  // lane L collects the row counts of (i, e) = (L >> 4, L & 15)
-    int colcnt[2] = {0, 0};
-#pragma clang loop unroll(full)
-    for (int i = 0; i < 4; ++i) {
-      float pr[16];
-#pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4) {
-        const float4 q = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 32 + 8 * e4 + 4 * h);
-        pr[4 * e4] = q.x;
-        pr[4 * e4 + 1] = q.y;
-        pr[4 * e4 + 2] = q.z;
-        pr[4 * e4 + 3] = q.w;
+    auto amb_direct = [&](int gr, int gc, float v) {  // an ambiguous pair outside the tile's range
+      const int slot = atomicAdd(A.amb_n, 1);
+      if (slot < amb_cap(P)) {
+        A.amb[slot] = make_int2(gr, gc | (diag ? 0 : AMB_BOTH));
+        A.ambv[slot] = v;
       }
-      float pc[2];  // diagonal tile: both orders present, candidates on the row side only
+    };
+    // ---- 1. counts and raw lists (this window's CAPL slots per wave) --------------------------
+    int2* wlist = lists + w * CAPL;
+    const float tau_hi = A.tau_hi, tau_lo = A.tau_lo;
+    {
+      int nlist = 0;  // wave-uniform
+      int rcl0 = 0, rcl1 = 0;  // lane L holds the row counts of (i, e) = (L >> 4, L & 15)
+      int colcnt[2] = {0, 0};
+      const bool hits = HITS && win == 0;
+      static_for<4>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        float pr[16];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 32 + r32];
-      // hot part, both column blocks of a row slot together: |r| > tau + eps counted at once (row
-      // counts by ballot + popcount into lane i*16+e, column counts per lane); the value slots with
-      // a candidate or a value within eps of tau marked per lane (bit e) for the slow part
-      uint32_t lm[2] = {0u, 0u};
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        int c0 = 0, c1 = 0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const float a = fabsf(acc[i][j][e]);
-          if (COUNTS) {
-            const bool hit = a > A.tau_hi;
-            const uint64_t m = __ballot(hit);
-            c0 += __builtin_popcount((uint32_t)m);
-            c1 += __builtin_popcount((uint32_t)(m >> 32));
-            colcnt[j] += hit ? 1 : 0;
-          }
-          const bool cond = a > fminf(pr[e], pc[j]) || (!RECT && a > A.tau_lo && a <= A.tau_hi);
-          lm[j] |= cond ? (1u << e) : 0u;
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const float4 q = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 32 + 8 * e4 + 4 * h);
+          pr[4 * e4] = q.x;
+          pr[4 * e4 + 1] = q.y;
+          pr[4 * e4 + 2] = q.z;
+          pr[4 * e4 + 3] = q.w;
         }
-        if (COUNTS) {
-          rcl0 = lane == i * 16 + e ? c0 : rcl0;
-          rcl1 = lane == i * 16 + e ? c1 : rcl1;
-        }
-      }
+        float pc[2];  // diagonal tile: both orders present, candidates on the row side only
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (!__ballot(lm[j] != 0u) || debug == 7) continue;  // wave-uniform
-        const int col = wc * 64 + j * 32 + r32;
-        const int gc = (int)(rowB + col);
-        const double dc = RECT ? 0.0 : (double)sdnc[col];
+        for (int j = 0; j < 2; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 32 + r32];
+        static_for<16>([&](auto ec) {
+          constexpr int e = decltype(ec)::value;
+          int c0 = 0, c1 = 0;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          if (!__ballot((lm[j] >> e) & 1u)) continue;  // wave-uniform
-          const float v = acc[i][j][e];
-          const float a = fabsf(v);
-          const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          const int gr = RECT ? spod[row] : (int)(rowA + row);
-          const bool hr = a > pr[e] && gc < P && gc != gr;  // padding partners / zeroed self: r = 0
-          const bool hc = a > pc[j] && rowA + row < P;
-          bool am = false, settled = false;
-          if (!RECT && a > A.tau_lo && a <= A.tau_hi && gc < P && rowA + row < P && gc != gr) {
-            // within eps of tau: the pair's own bound from the rows' rounding-error norms
-            // (corr_dnorm) often settles it; otherwise it is listed for float64 re-scoring
-            const double dr = (double)sdnr[row];
-            const double band = dr + dc + 3.0 * dr * dc + (double)A.acc_err + 1e-9;
-            if ((double)a > (double)A.tau + band) {
-              settled = true;
-            } else if ((double)a > (double)A.tau - band) {
-              am = true;
+          for (int j = 0; j < 2; ++j) {
+            const float v = acc[i][j][e];
+            const float a = fabsf(v);
+            const bool hit = a > tau_hi;
+            if (hits) {
+              const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
+              c0 += __builtin_popcount((uint32_t)m);
+              c1 += __builtin_popcount((uint32_t)(m >> 32));
+              int cc = colcnt[j] + (hit ? 1 : 0);
+              asm volatile("" : "+s"(c0), "+s"(c1));  // counted here: no mask held across the branch below
+              asm volatile("" : "+v"(cc));
+              colcnt[j] = cc;
             }
-          }
-          if (COUNTS) {
-            const uint64_t ms = __ballot(settled);
-            if (ms) {
-              rcl0 = lane == i * 16 + e ? rcl0 + __builtin_popcount((uint32_t)ms) : rcl0;
-              rcl1 = lane == i * 16 + e ? rcl1 + __builtin_popcount((uint32_t)(ms >> 32)) : rcl1;
-              colcnt[j] += settled ? 1 : 0;
-            }
-          }
-          const bool need = hr || hc || am;
-          const uint64_t m = __ballot(need);
-          if (m) {  // wave-uniform
-            const int slot = nlist + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const bool inl = slot < CAPW;
-            const uint64_t mam = __ballot(am && inl);
-            if (need) {
-              const int ar = namb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mam >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mam, 0u));
-              const int tag = (hr ? 1 : 0) | (hc ? 2 : 0) | (am ? (diag ? 8 : 4) : 0);
-              const int4 ent = make_int4(gr, gc, __float_as_int(v), tag | (am && inl ? ar << 4 : 0));
-              if (inl) {
-                wlist[slot] = ent;
-              } else if (DIRECT) {
-                flush_direct(ent);
+            bool flag = (a > pr[e]) | (a > pc[j]);  // phi is never NaN: no fminf canonicalisation
+            if (!RECT) flag = flag | ((a > tau_lo) & !hit);
+            const uint64_t fm = __builtin_amdgcn_ballot_w64(flag);
+            if (fm && debug != 7) {  // wave-uniform, rare
+              const int slot = nlist - win + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+              if (flag && slot >= 0 && slot < CAPL) {
+                const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int col = wc * 64 + j * 32 + r32;
+                wlist[slot] = make_int2(row | (col << 8), __float_as_int(v));
               }
+              nlist += __builtin_popcountll(fm);
             }
-            namb += __builtin_popcountll(mam);
-            nlist += __builtin_popcountll(m);
+          }
+          if (hits) {  // row (i, e) counts into lane i*16 + e (immediate lane: no lane masks held)
+            int t0 = rcl0, t1 = rcl1;  // (asm operands cannot name the enclosing function's locals)
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(t0) : "s"(c0), "n"(i * 16 + e));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(t1) : "s"(c1), "n"(i * 16 + e));
+            rcl0 = t0;
+            rcl1 = t1;
+          }
+        });
+      });
+      if (debug == 6) {  // profiling aid: step 1 only
+        if (nlist == 12345) A.count[0] = rcl0 + rcl1 + colcnt[0] + colcnt[1];
+        return false;
+      }
+      if (lane == 0) {
+        wcount[w] = min(max(nlist - win, 0), CAPL);
+        if (nlist > win + CAPL) sflag[0] = 1;  // another window follows
+      }
+      if (hits) {  // |r| > tau: one LDS add per row / column and wave
+        const int li = lane >> 4, le = lane & 15;
+        const int rbase = wr * 128 + li * 32 + (le & 3) + 8 * (le >> 2);
+        if (rcl0) atomicAdd(&srcnt[rbase], rcl0);
+        if (rcl1) atomicAdd(&srcnt[rbase + 4], rcl1);
+        if (!diag) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int c = colcnt[j] + __shfl_xor(colcnt[j], 32, 64);
+            if (h == 0 && c) atomicAdd(&sccnt[wc * 64 + j * 32 + r32], c);
           }
         }
       }
-    }
-    if (debug == 6) {  // profiling aid: epilogue loops only
-      if (nlist == 12345) A.count[0] = rcl0 + rcl1 + colcnt[0] + colcnt[1] + namb;
-      return;
-    }
-    if (lane == 0) {
-      wcount[w] = nlist < CAPW ? nlist : CAPW;
-      wamb[w] = namb;
-      if (!DIRECT && nlist > CAPW) *sflag = 1;  // this tile's lists are incomplete: refill pass
-    }
-    if (COUNTS) {  // |r| > tau: one LDS add per row / column and wave
-      const int li = lane >> 4, le = lane & 15;
-      const int rbase = wr * 128 + li * 32 + (le & 3) + 8 * (le >> 2);
-      if (rcl0) atomicAdd(&srcnt[rbase], rcl0);
-      if (rcl1) atomicAdd(&srcnt[rbase + 4], rcl1);
-      if (!diag) {
+      __syncthreads();
+      // the waves' lists as one sequence: entry q of wave u is at lists[u * CAPL + q - off(u)]
+      int woff[G::NW + 1];
+      woff[0] = 0;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int c = colcnt[j] + __shfl_xor(colcnt[j], 32, 64);
-          if (h == 0 && c) atomicAdd(&sccnt[wc * 64 + j * 32 + r32], c);
+      for (int u = 0; u < G::NW; ++u) woff[u + 1] = woff[u] + wcount[u];
+      const int ntot = woff[G::NW];
+      auto entry_at = [&](int q) -> int2* {
+        int u = 0;
+#pragma unroll
+        for (int k = 1; k < G::NW; ++k) u += q >= woff[k] ? 1 : 0;
+        return lists + u * CAPL + (q - woff[u]);
+      };
+      const bool more = sflag[0] != 0;
+      // ---- 2. classification -----------------------------------------------------------------
+      for (int q = tid; q < ntot; q += G::NTH) {
+        int2* ep = entry_at(q);
+        const int2 ent = *ep;
+        const int row = ent.x & 255, col = (ent.x >> 8) & 255;
+        const float v = __int_as_float(ent.y);
+        int tag = classify(row, col, v);
+        if (SETTLE && (tag & 8)) {
+          atomicAdd(&srcnt[row], 1);
+          if (!diag) atomicAdd(&sccnt[col], 1);
         }
+        int rank = 0;
+        const uint64_t mam = __ballot((tag & 4) != 0);
+        if (mam) {
+          const int leader = __builtin_ctzll(mam);
+          int base = 0;
+          if (lane == leader) base = atomicAdd(&sflag[1], __builtin_popcountll(mam));
+          base = __shfl(base, leader, 64);
+          rank = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mam >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mam, 0u));
+        }
+        if ((tag & 4) && rank >= RANKS - 1) {  // past the tile's ranks: its own slot
+          amb_direct(RECT ? spod[row] : (int)(rowA + row), (int)(rowB + col), v);
+          tag &= ~4;
+        }
+        *ep = make_int2((ent.x & 0xffff) | ((tag & 7) << 16) | ((tag & 4) ? rank << 19 : 0), ent.y);
       }
-    }
-    __syncthreads();
-    const bool overflowed = !DIRECT && *sflag;
-    if (!RECT && tid == 0) {
-      if (overflowed) {  // nothing listed is committed; the refill pass recomputes the tile
-        const int slot = atomicAdd(&A.ovt[0], 1);
-        A.ovt[1 + slot] = (int32_t)(I * A.nb2 + J);
-      } else {  // the tile's listed ambiguous pairs: one contiguous range
-        int tot = 0;
-        for (int u = 0; u < 8; ++u) tot += wamb[u];
+      __syncthreads();
+      // ---- 3. counts, the window's ambiguous range, entries out --------------------------------
+      if (SETTLE) {  // one global add per row / column of the tile
+        if (rq < TB && srcnt[rq]) atomicAdd(&A.count[rowA + rq], srcnt[rq]);
+        if (!diag && cq >= 0 && cq < TC && sccnt[cq]) atomicAdd(&A.count[rowB + cq], sccnt[cq]);
+      }
+      if (!RECT && tid == 0) {
+        const int tot = min(sflag[1], RANKS - 1);
         int base = -1;
         if (tot) {
           base = atomicAdd(A.amb_n, tot);
           if ((int64_t)base + tot > amb_cap(P)) base = -1;  // the list is full: the host reports it
         }
-        for (int u = 0; u < 8; ++u) {
-          wbase[u] = base;
-          if (base >= 0) base += wamb[u];
-        }
+        sflag[2] = base;
       }
-    }
-    if (COUNTS) {  // one global add per row / column of the tile
-      const int q = tid & (TB - 1);
-      if (tid < TB) {
-        if (srcnt[q]) atomicAdd(&A.count[rowA + q], srcnt[q]);
-      } else if (!diag && sccnt[q]) {
-        atomicAdd(&A.count[rowB + q], sccnt[q]);
-      }
-    }
-    __syncthreads();
-    if (overflowed || debug == 5) return;
-    const int4* lists = reinterpret_cast<const int4*>(smem + EPI_LIST_OFF);
-    for (int base = 0;; base += NT) {
-      bool more = false;
-#pragma unroll
-      for (int u0 = 0; u0 < 8; u0 += 4) {
-        int4 ent[4];
-        int gs[4], gt[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int q = base + tid;
-          const bool ok = q < wcount[u0 + u];
-          more = more || base + NT < wcount[u0 + u];
-          ent[u] = ok ? lists[(u0 + u) * CAPW + q] : make_int4(0, 0, 0, 0);
-          if (!RECT && (ent[u].w & 12) && wbase[u0 + u] >= 0) {  // an ambiguous pair
-            const int slot = wbase[u0 + u] + (ent[u].w >> 4);
-            A.amb[slot] = make_int2(ent[u].x, ent[u].y | ((ent[u].w & 4) ? AMB_BOTH : 0));
-            A.ambv[slot] = __int_as_float(ent[u].z);
-          }
-          if (RECT) {  // rect pass: the rank's local buffers
-            ent[u].x -= (int)sh.lo;
-          }
-          gs[u] = (ent[u].w & 1) ? atomicAdd(&A.cnt[ent[u].x], 1) : CAPC;
-          gt[u] = (ent[u].w & 2) ? atomicAdd(&A.cnt[ent[u].y], 1) : CAPC;
+      if (debug == 5) return false;
+      __syncthreads();
+      const int abase = RECT ? -1 : sflag[2];
+      for (int q = tid; q < ntot; q += G::NTH) {
+        const int2 ent = *entry_at(q);
+        const int row = ent.x & 255, col = (ent.x >> 8) & 255, tag = (ent.x >> 16) & 7;
+        const int gr = RECT ? spod[row] : (int)(rowA + row);
+        const int gc = (int)(rowB + col);
+        if ((tag & 4) && abase >= 0) {
+          const int slot = abase + ((uint32_t)ent.x >> 19);
+          A.amb[slot] = make_int2(gr, gc | (diag ? 0 : AMB_BOTH));
+          A.ambv[slot] = __int_as_float(ent.y);
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (gs[u] < CAPC) A.buf[(int64_t)ent[u].x * CAPC + gs[u]] = make_int2(ent[u].z, ent[u].y);
-          if (gt[u] < CAPC) A.buf[(int64_t)ent[u].y * CAPC + gt[u]] = make_int2(ent[u].z, ent[u].x);
-        }
+        if (tag & 1) append(gr, gc, ent.y);
+        if (tag & 2) append(gc, gr, ent.y);
       }
-      if (!more) break;  // wave-uniform: every lane reads the same wcount[]
+      return more;
     }
-    return;
-  }
-  // ---- sample pass: park each 128-row half in LDS, one lane per (row, 128-column half) --------
-  float* tile = reinterpret_cast<float*>(smem);
+  } else {
+    // ---- sample pass: park each 128-row half in LDS, one lane per (row, 128-column half) --------
+    float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (wr == half) {
+    for (int half = 0; half < 2; ++half) {
+      if (wr == half) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int row = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int col = wc * 64 + j * 32 + r32;
-            tile[row * EPI_LD + col] = acc[i][j][e];
-          }
-    }
-    __syncthreads();
-    if (tid < 256) {  // row scan: pod rowA + half*128 + r against 128 columns of block 2J + ch
-      const int r = tid & 127, ch = tid >> 7;
-      const int64_t g = rowA + half * BM + r;
-      const int jb = 2 * (int)(J - sh.j0) + ch;  // list slot of this chunk
-      const int64_t c0 = rowB + ch * BM;
-      if (g < P && (own || jb < A.nsb)) {
-        Cand<KC> cd;
-        cd.init();
-        const int64_t slot = g * NSL + (own ? NSB + ch : jb);
-        const int cend = (int)std::min<int64_t>(BM, P - c0);
-        const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
-        const float* rowp = tile + r * EPI_LD + ch * BM;
-        if (self >= 0) A.selfd[g] = rowp[self];
-        float lim = -1.f;
-        for (int c4 = 0; c4 < cend; c4 += 4) {
-          const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
+            for (int e = 0; e < 16; ++e) {
+              const int row = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+              const int col = wc * 64 + j * 32 + r32;
+              tile[row * EPI_LD + col] = acc[i][j][e];
+            }
+      }
+      __syncthreads();
+      if (tid < 256) {  // row scan: pod rowA + half*128 + r against 128 columns of block 2J + ch
+        const int r = tid & 127, ch = tid >> 7;
+        const int64_t g = rowA + half * BM + r;
+        const int jb = 2 * (int)(J - sh.j0) + ch;  // list slot of this chunk
+        const int64_t c0 = rowB + ch * BM;
+        if (g < P && (own || jb < A.nsb)) {
+          Cand<KC> cd;
+          cd.init();
+          const int64_t slot = g * NSL + (own ? NSB + ch : jb);
+          const int cend = (int)std::min<int64_t>(BM, P - c0);
+          const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
+          const float* rowp = tile + r * EPI_LD + ch * BM;
+          if (self >= 0) A.selfd[g] = rowp[self];
+          float lim = -1.f;
+          for (int c4 = 0; c4 < cend; c4 += 4) {
+            const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int c = c4 + u;
-            const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
-            if (c < cend && c != self && fabsf(vu) > lim) {
-              cd.insert(vu, (int32_t)(c0 + c));
-              lim = cd.thr;
+            for (int u = 0; u < 4; ++u) {
+              const int c = c4 + u;
+              const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
+              if (c < cend && c != self && fabsf(vu) > lim) {
+                cd.insert(vu, (int32_t)(c0 + c));
+                lim = cd.thr;
+              }
             }
           }
-        }
-        float* ov = A.samp_v + slot * KC;
-        int32_t* oi = A.samp_i + slot * KC;
+          float* ov = A.samp_v + slot * KC;
+          int32_t* oi = A.samp_i + slot * KC;
 #pragma unroll
-        for (int q = 0; q < KC; ++q) {
-          ov[q] = cd.v[q];
-          oi[q] = cd.i[q];
+          for (int q = 0; q < KC; ++q) {
+            ov[q] = cd.v[q];
+            oi[q] = cd.i[q];
+          }
         }
       }
+      __syncthreads();  // the next half overwrites the tile
     }
-    __syncthreads();  // the next half overwrites the tile
+    return false;
   }
 }
 
-
-template <int KC, int MODE>
-__global__ __launch_bounds__(NT) void corr_tiles(TileArgs A) {
-  if (MODE == MODE_RECT) {
-    tile_body<KC, MODE_RECT, true>(A, blockIdx.x / A.nb2, blockIdx.x % A.nb2, false);
-  } else if (MODE == MODE_SAMPLE) {
+// TC: the main pass's column-tile width (256 for the other modes).  Two workgroups
+// per CU for TC = 128 (<= 256 registers per lane).
+template <int KC, int MODE, int TC>
+__global__ __launch_bounds__(Geo<TC>::NTH) __attribute__((amdgpu_waves_per_eu(2))) void corr_tiles(TileArgs A) {
+  if constexpr (MODE == MODE_RECT) {
+    const int64_t I = blockIdx.x / A.nb2, J = blockIdx.x % A.nb2;
+    if (tile_body<KC, MODE_RECT, TC>(A, I, J, false, 0)) {  // window 0 outside the loop (as MODE_MAIN)
+      for (int win = Geo<TC>::CAPL;; win += Geo<TC>::CAPL) {
+        __syncthreads();  // the next window reuses the LDS
+        if (!tile_body<KC, MODE_RECT, TC>(A, I, J, false, win)) break;
+      }
+    }
+  } else if constexpr (MODE == MODE_SAMPLE) {
     const int nsb2 = (A.nsb + 1) / 2;  // this chunk's 256-blocks
     const int64_t I = A.sh.I0 + blockIdx.x / (nsb2 + 1);
     int64_t J = blockIdx.x % (nsb2 + 1);
@@ -695,14 +746,18 @@ __global__ __launch_bounds__(NT) void corr_tiles(TileArgs A) {
     } else {
       J += A.sh.j0;
     }
-    tile_body<KC, MODE_SAMPLE, false>(A, I, J, own);
-  } else if (MODE == MODE_MAIN) {
+    tile_body<KC, MODE_SAMPLE, TC>(A, I, J, own, 0);
+  } else {  // MODE_MAIN
     // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so slot
-    // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; slots walk the
-    // upper triangle in SUPER x SUPER super-tiles, so the tiles an XCD has in flight share 2*SUPER
-    // row blocks through its L2.  Slots below the diagonal or past nb2 exit at once.
+    // L = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; SPLIT consecutive
+    // slots are the column tiles of one 256 x 256 block pair, and the pairs walk the upper triangle
+    // in SUPER x SUPER super-tiles, so the tiles an XCD has in flight share 2*SUPER row blocks
+    // through its L2.  Slots below the diagonal or past nb2 exit at once.
+    constexpr int SPLIT = TB / TC;
     const int64_t b = blockIdx.x;
-    const int64_t L = (b & 7) * A.per_xcd + (b >> 3);
+    const int64_t L2 = (b & 7) * A.per_xcd + (b >> 3);
+    const int64_t L = L2 / SPLIT;
+    const int part = (int)(L2 % SPLIT);
     const int64_t ns = (A.nb2 + SUPER - 1) / SUPER;
     const int64_t st = (L / (SUPER * SUPER)) * A.sh.G + A.sh.g;  // this rank's super-tiles
     if (st >= ns * (ns + 1) / 2) return;
@@ -715,13 +770,13 @@ __global__ __launch_bounds__(NT) void corr_tiles(TileArgs A) {
     int64_t J = SJ * SUPER + in % SUPER;
     if (I > J || J >= A.nb2) return;
     if (A.debug == 4) I = J = (blockIdx.x & 7);  // profiling aid: product only, operands L2-resident
-    tile_body<KC, MODE_MAIN, false>(A, I, J, false);
-  } else {  // MODE_REFILL: persistent over the device-held list of overflowed tiles
-    const int n = A.ovt[0];
-    for (int t = blockIdx.x; t < n; t += gridDim.x) {
-      const int32_t code = A.ovt[1 + t];
-      __syncthreads();  // the previous tile's LDS is free
-      tile_body<KC, MODE_MAIN, true>(A, code / A.nb2, code % A.nb2, false);
+    // window 0 outside the loop: the loop's copy may hold more registers (values kept across its
+    // iterations); it runs only for a tile whose lists pass CAPL entries in some wave
+    if (tile_body<KC, MODE_MAIN, TC>(A, I, J * SPLIT + part, false, 0)) {
+      for (int win = Geo<TC>::CAPL;; win += Geo<TC>::CAPL) {
+        __syncthreads();  // the next window reuses the LDS
+        if (!tile_body<KC, MODE_MAIN, TC>(A, I, J * SPLIT + part, false, win)) break;
+      }
     }
   }
 }
@@ -1064,8 +1119,8 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
 }
 
 // profiling aid, KRCA_CORR_DEBUG (results are wrong when set): 1 = product only, 4 = product only
-// with every tile reading the same few row blocks (operands L2-resident), 5 = no list flush, 6 = the
-// epilogue loops only (no counts, no lists committed), 7 = no slow path
+// with every tile reading the same few row blocks (operands L2-resident), 5 = no entries written out,
+// 6 = the epilogue's first step only (counts and raw lists, nothing committed), 7 = no lists
 int debug_mode() { return krca::tuning().corr_debug; }
 
 constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
@@ -1123,7 +1178,6 @@ struct CorrWs {  // views into a caller's candidate workspace
   float* ambv;          // [amb_cap(P)] their screening values
   float* dn;            // [P] fp16 rounding-error norm of each row
   int32_t* amb_n;       // [4]: their count (past the capacity: an error)
-  int32_t* ovt;         // [1 + tiles]: main-pass tiles whose candidate lists overflowed LDS
   uint16_t* zs;         // [RECT_ROWS][Tp]
   int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
   int32_t* fill;        // sharded: [n_loc]
@@ -1152,10 +1206,6 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   w.ambv = reinterpret_cast<float*>(take(amb_cap(P)));
   w.dn = reinterpret_cast<float*>(take(P));
   w.amb_n = reinterpret_cast<int32_t*>(take(4));
-  {
-    const int64_t nb2 = krca::ceil_div(P, TB);
-    w.ovt = reinterpret_cast<int32_t*>(take(1 + nb2 * (nb2 + 1) / 2));
-  }
   w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
   if (G > 0) {
     w.lbuf = reinterpret_cast<int2*>(take(2 * n_loc * CAPC));
@@ -1166,21 +1216,23 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   return o;
 }
 
-template <int KC>
-int set_lds_attr() {
+template <int KC, int MODE, int TC>
+int set_lds_attr1() {
   static bool done = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
   if (!done) {
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_MAIN>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_SAMPLE>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_RECT>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE_REFILL>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_tiles<KC, MODE, TC>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, Geo<TC>::LDS_BYTES));
     done = true;
   }
   return KRCA_OK;
+}
+template <int KC>
+int set_lds_attr() {
+  int rc = set_lds_attr1<KC, MODE_MAIN, 128>();
+  if (!rc) rc = set_lds_attr1<KC, MODE_MAIN, 256>();
+  if (!rc) rc = set_lds_attr1<KC, MODE_SAMPLE, 256>();
+  if (!rc) rc = set_lds_attr1<KC, MODE_RECT, 256>();
+  return rc;
 }
 
 struct Dims {
@@ -1230,8 +1282,8 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
     ta.samp_i = ws.samp_i;
     ta.selfd = ws.selfd;
     ta.sh = sh;
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))), dim3(NT), LDS_BYTES,
-                       st, ta);
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE, 256>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))),
+                       dim3(Geo<256>::NTH), Geo<256>::LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
                        ws.samp_i, ws.selfd, lo, lo + n, nsb_c, d.k, d.eps, ws.run, (int)(c0 == 0),
@@ -1249,12 +1301,10 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(ws.amb_n, 0, 4 * sizeof(int32_t), st));
-  KRCA_HIP(hipMemsetAsync(ws.ovt, 0, sizeof(int32_t), st));
   const int64_t ns = (d.nb2 + SUPER - 1) / SUPER;
   const int64_t n_st = ns * (ns + 1) / 2;
   const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
   if (n_mine == 0) return KRCA_OK;
-  const int64_t per_xcd = (n_mine * SUPER * SUPER + 7) / 8;
   const Shard sh{0, G, g, 0};
   hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
                      d.Tp, ws.dn);
@@ -1268,7 +1318,6 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.P = d.P;
   ta.Tp = d.Tp;
   ta.nb2 = d.nb2;
-  ta.per_xcd = per_xcd;
   ta.nsb = d.nsb;
   ta.tau_hi = d.tau + d.eps;
   ta.tau_lo = d.tau - d.eps;
@@ -1284,14 +1333,20 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.amb_n = ws.amb_n;
   ta.ambv = ws.ambv;
   ta.dn = ws.dn;
-  ta.ovt = ws.ovt;
-  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN>), dim3((unsigned)(8 * per_xcd)), dim3(NT), LDS_BYTES, st, ta);
-  KRCA_LAUNCH_CHECK();
-  if (dbg == 0) {
-    // tiles whose lists overflowed (device-held count; usually none: the workgroups exit at once)
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_REFILL>), dim3((unsigned)std::min<int64_t>(1024, n_mine * SUPER * SUPER)),
-                       dim3(NT), LDS_BYTES, st, ta);
+  // main pass: 256 x 256 tiles (KRCA_CORR_TC = 128: 256 x 128 tiles, two workgroups per CU)
+  auto launch = [&](auto tc) -> int {
+    constexpr int TC = decltype(tc)::value;
+    constexpr int SPLIT = TB / TC;
+    ta.per_xcd = (n_mine * SUPER * SUPER * SPLIT + 7) / 8;
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, TC>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<TC>::NTH),
+                       Geo<TC>::LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
+    return KRCA_OK;
+  };
+  const int rc = krca::tuning().corr_tc == 128 ? launch(std::integral_constant<int, 128>{})
+                                               : launch(std::integral_constant<int, 256>{});
+  if (rc) return rc;
+  if (dbg == 0) {
     hipLaunchKernelGGL(corr_amb_rescore, dim3(4096), dim3(TPB), 0, st, (const int2*)ws.amb, (const float*)ws.ambv,
                        (const int32_t*)ws.amb_n, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
     KRCA_LAUNCH_CHECK();
@@ -1354,7 +1409,8 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
     ta.rect_pods = ws.over + 1 + r0;
     ta.n_rect = nr;
     ta.sh = sh;
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT>), dim3((unsigned)(npad / TB * d.nb2)), dim3(NT), LDS_BYTES, st, ta);
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT, 256>), dim3((unsigned)(npad / TB * d.nb2)), dim3(Geo<256>::NTH),
+                       Geo<256>::LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,

@@ -141,8 +141,8 @@ def test_corr_sample_in_chunks(eng):
 
 def test_corr_list_overflow_refill(eng):
     """Two groups of 600 identical series: every in-group pair is a candidate of both pods, so the
-    LDS candidate lists of the in-group tiles overflow and the refill pass recomputes those tiles
-    with direct appends.  Every row equals the oracle (ties at r = 1 go to the lower index)."""
+    LDS lists of the in-group tiles pass their capacity and those tiles run again for the next
+    windows of list slots.  Every row equals the oracle (ties at r = 1 go to the lower index)."""
     P, T, k = 1800, 256, 10
     base = synth.make_metrics(P, 1, T, seed=11, group_size=0)
     x = base.clone()
@@ -158,6 +158,26 @@ def test_corr_list_overflow_refill(eng):
         want = [q for q in range(g0, g0 + 600) if q != p][:k]
         assert res["idx"][p].tolist() == want, (p, res["idx"][p])
     assert np.all(res["count"][:1200] >= 599)
+
+
+def test_corr_every_pair_at_tau(eng):
+    """600 series x_i = u + v_i from orthogonal Hadamard rows: every in-group pair has r = 0.5 = tau
+    exactly, so each in-group tile lists 65,536 pairs within eps of tau (past the 8,191 a tile ranks:
+    the rest take one global slot each) and the lists pass their capacity.  Counts of the other pairs
+    exact, in-group pairs (within 1e-6 of tau) on either side; every row certified."""
+    T, G, R = 1024, 600, 100
+    H = np.array([[1.0]])
+    while H.shape[0] < T:
+        H = np.block([[H, H], [H, -H]])
+    rng = np.random.default_rng(5)
+    x = np.empty((T, G + R, 1), np.float32)
+    x[:, :G, 0] = (H[1][:, None] + H[2:G + 2].T) * 3.0 + 10.0
+    x[:, G:, 0] = np.cumsum(rng.standard_normal((T, R)), axis=0)
+    x = torch.from_numpy(x)
+    res = eng.corr_topk(x, k=10, tau=TAU)
+    z = oracle.corr_standardize(x.numpy(), 0)
+    check_rows(res, z, np.arange(G + R), 10)
+    assert np.all(res["count"][:G] <= G - 1 + R)
 
 
 def test_corr_rejects_bad_k(eng):
