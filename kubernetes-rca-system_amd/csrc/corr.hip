@@ -536,23 +536,23 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
           for (int j = 0; j < 2; ++j) {
             const float v = acc[i][j][e];
             const float a = fabsf(v);
-            const bool hit = a > tau_hi;
+            // the masks straight from the compares (no boolean round trip through a VGPR)
+            const uint64_t mh = __builtin_amdgcn_ballot_w64(a > tau_hi);
             if (hits) {
-              const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
-              c0 += __builtin_popcount((uint32_t)m);
-              c1 += __builtin_popcount((uint32_t)(m >> 32));
-              int cc = colcnt[j] + (hit ? 1 : 0);
+              c0 += __builtin_popcount((uint32_t)mh);
+              c1 += __builtin_popcount((uint32_t)(mh >> 32));
               asm volatile("" : "+s"(c0), "+s"(c1));  // counted here: no mask held across the branch below
-              asm volatile("" : "+v"(cc));
+              int cc = colcnt[j];
+              uint64_t co;
+              asm volatile("v_addc_co_u32_e64 %0, %1, 0, %0, %2" : "+v"(cc), "=s"(co) : "s"(mh));  // += own hit bit
               colcnt[j] = cc;
             }
-            bool flag = (a > pr[e]) | (a > pc[j]);  // phi is never NaN: no fminf canonicalisation
-            if (!RECT) flag = flag | ((a > tau_lo) & !hit);
-            const uint64_t fm = __builtin_amdgcn_ballot_w64(flag);
-            if (fm && debug != 7) {  // wave-uniform, rare
+            uint64_t fm = __builtin_amdgcn_ballot_w64(a > pr[e]) | __builtin_amdgcn_ballot_w64(a > pc[j]);
+            if (!RECT) fm |= __builtin_amdgcn_ballot_w64(a > tau_lo) & ~mh;
+            if (fm) {  // wave-uniform, rare
               const int slot = nlist - win + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-              if (flag && slot >= 0 && slot < CAPL) {
+              if (((fm >> lane) & 1) && slot >= 0 && slot < CAPL) {
                 const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 const int col = wc * 64 + j * 32 + r32;
                 wlist[slot] = make_int2(row | (col << 8), __float_as_int(v));
@@ -866,7 +866,13 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__
   const int sub = threadIdx.x & 15;
   const int64_t n = min((int64_t)*amb_n, amb_cap(P));
   const bool vec = (T & 3) == 0;
-  for (int64_t q = (int64_t)blockIdx.x * (TPB / 16) + (threadIdx.x >> 4); q < n; q += (int64_t)gridDim.x * (TPB / 16)) {
+  // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs; XCD x takes the contiguous
+  // eighth [x n / 8, (x + 1) n / 8) of the list (which runs tile by tile), so the rows of a tile's
+  // pairs are fetched into one L2
+  const int xcd = blockIdx.x & 7, nb = gridDim.x >> 3;  // gridDim.x: a multiple of 8
+  const int64_t q0 = n * xcd / 8, q1 = n * (xcd + 1) / 8;
+  for (int64_t q = q0 + (int64_t)(blockIdx.x >> 3) * (TPB / 16) + (threadIdx.x >> 4); q < q1;
+       q += (int64_t)nb * (TPB / 16)) {
     const int2 e = amb[q];
     const int64_t a = e.x, b = e.y & (AMB_BOTH - 1);
     const double sa = (double)dn[a], sb = (double)dn[b];
@@ -1120,7 +1126,7 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
 
 // profiling aid, KRCA_CORR_DEBUG (results are wrong when set): 1 = product only, 4 = product only
 // with every tile reading the same few row blocks (operands L2-resident), 5 = no entries written out,
-// 6 = the epilogue's first step only (counts and raw lists, nothing committed), 7 = no lists
+// 6 = the epilogue's first step only (counts and raw lists, nothing committed)
 int debug_mode() { return krca::tuning().corr_debug; }
 
 constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
@@ -1347,7 +1353,7 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
                                                : launch(std::integral_constant<int, 256>{});
   if (rc) return rc;
   if (dbg == 0) {
-    hipLaunchKernelGGL(corr_amb_rescore, dim3(4096), dim3(TPB), 0, st, (const int2*)ws.amb, (const float*)ws.ambv,
+    hipLaunchKernelGGL(corr_amb_rescore, dim3((unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7)), dim3(TPB), 0, st, (const int2*)ws.amb, (const float*)ws.ambv,
                        (const int32_t*)ws.amb_n, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
     KRCA_LAUNCH_CHECK();
   }

@@ -12,13 +12,16 @@ if [ "${TESTS:-1}" = 1 ]; then
   rc=$?; echo "tests EXIT=$rc" >> $O/status; tail -3 $O/tests.log
   [ $rc -eq 0 ] || { tail -40 $O/tests.log; exit $rc; }
 fi
+for rsg in ${RSGS:-4096}; do
 for tc in ${TCS:-128 256}; do
 for m in ${MODES:-0 1}; do
-  KRCA_CORR_TC=$tc KRCA_CORR_DEBUG=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t${tc}m$m -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps 3 > $O/t${tc}m$m.log 2>&1
-  rc=$?; echo "t${tc}m$m EXIT=$rc" >> $O/status
-  [ $rc -eq 0 ] || { tail -5 $O/t${tc}m$m.log; exit $rc; }
-  find $O/t${tc}m$m -name '*.db' -delete
-  echo "tc $tc mode $m $(grep '^{' $O/t${tc}m$m.log | cut -c1-120)"
-  python3 -c "import csv;[print('   ', r['Name'][32:62], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us') for r in csv.DictReader(open('$O/t${tc}m$m/run_kernel_stats.csv')) if 'corr_tiles' in r['Name'] or 'amb' in r['Name']]"
+  D=t${tc}m${m}g$rsg
+  KRCA_CORR_RS_GRID=$rsg KRCA_CORR_TC=$tc KRCA_CORR_DEBUG=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t${tc}m${m}g$rsg -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps 3 > $O/t${tc}m${m}g$rsg.log 2>&1
+  rc=$?; echo "$D EXIT=$rc" >> $O/status
+  [ $rc -eq 0 ] || { tail -5 $O/$D.log; exit $rc; }
+  find $O/$D -name '*.db' -delete
+  echo "tc $tc mode $m rsg $rsg $(grep '^{' $O/$D.log | cut -c1-100)"
+  python3 -c "import csv;[print('   ', r['Name'][32:62], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us') for r in csv.DictReader(open('$O/$D/run_kernel_stats.csv')) if 'corr_tiles<' in r['Name'] or 'rescore' in r['Name']]"
+done
 done
 done

@@ -5,6 +5,9 @@
   python tools/prof_kernels.py ppr    [--pods 1000000] [--reps 3]
   python tools/prof_kernels.py logs   [--docs 1000000] [--reps 3]
   python tools/prof_kernels.py corr   [--pods 100000] [--reps 3]
+  python tools/prof_kernels.py tmpl   [--docs 1000000] [--reps 3]   (a13 template hashing + histograms)
+  python tools/prof_kernels.py f2     [--pods 1000000] [--reps 3]   (selector bit matrix + env DNS matches)
+  python tools/prof_kernels.py bc     [--pods 20000]  [--reps 1]    (f3 betweenness)
 Prints per-kernel event-timed averages and the algorithmic bytes.
 """
 import argparse
@@ -31,7 +34,7 @@ def timed(torch, fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods", "bc", "events"])
+    ap.add_argument("what", choices=["score", "ppr", "logs", "corr", "pods", "bc", "events", "tmpl", "f2"])
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--docs", type=int, default=1_000_000)
@@ -121,6 +124,47 @@ def main():
         nbytes = P * (1 + 8 + 2) + 8 + 2 * len(cc)
         out = dict(kernel="krca_pod_classify", pods=P, containers=len(cc), ms=ms, bytes=nbytes,
                    gbs=nbytes / (min(ms) * 1e-3) / 1e9)
+    elif a.what == "tmpl":
+        from krca.agents.logs import pack_documents
+        docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
+        blob, off = pack_documents(docs)
+        scan = eng.log_scan_device(eng.upload_blob(blob), torch.from_numpy(off).cuda())
+        eng.template_hist_device(scan)
+        ms = timed(torch, lambda: eng.template_hist_device(scan), a.reps)
+        L = scan["n_lines_total"]
+        # text once, line offsets (16 B) read, hashes (8 B) written, histogram pass (8 B in, 12 B out)
+        nbytes = len(blob) + 16 * L + 8 * L + 20 * L
+        out = dict(kernel="template hash + histograms", ms=ms, lines=L, docs=a.docs, bytes=nbytes,
+                   gbs=nbytes / (min(ms) * 1e-3) / 1e9)
+    elif a.what == "f2":
+        # selector test: D objects with 6 label items each (interned ids from 4096), S = 256 selectors
+        # of 1-3 items; env DNS inference: V env values (~48 B) against the 4 DNS keys of 2,000 services
+        rng = np.random.default_rng(0)
+        D, S = a.pods, 256
+        lab = np.sort(rng.integers(0, 4096, (D, 6)), axis=1).astype(np.int32).ravel()
+        lab_off = np.arange(0, 6 * D + 1, 6, dtype=np.int64)
+        sl = rng.integers(1, 4, S)
+        sel = np.concatenate([np.sort(rng.choice(4096, k, replace=False)) for k in sl]).astype(np.int32)
+        sel_off = np.concatenate([[0], np.cumsum(sl)]).astype(np.int64)
+        eng.selector_match(lab, lab_off, sel, sel_off)
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            bits = eng.selector_match(lab, lab_off, sel, sel_off)
+        sel_s = (time.perf_counter() - t0) / a.reps
+        names = [f"svc-{i:04d}" for i in range(2000)]
+        keys = [f"{n}{suf}" for n in names for suf in ("", ".default", ".default.svc", ".default.svc.cluster.local")]
+        V = a.pods // 10
+        vals = [f"http://{names[rng.integers(2000)]}.default.svc:8080/api/v{i % 7}" if i % 3 else f"value-{i}"
+                for i in range(V)]
+        from krca import topograph
+        eng.substr_match(*topograph.pack_strings(vals), *topograph.pack_strings(keys))
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            pairs = eng.substr_match(*topograph.pack_strings(vals), *topograph.pack_strings(keys))
+        sub_s = (time.perf_counter() - t0) / a.reps
+        out = dict(kernel="f2 selector + substring", objects=D, selectors=S, selector_s=sel_s,
+                   hits=int(np.unpackbits(bits.view(np.uint8)).sum()), env_values=V, keys=len(keys), substr_s=sub_s,
+                   pairs=len(pairs))
     else:
         from krca.agents.logs import pack_documents
         docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
