@@ -50,6 +50,16 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+hipStream_t side_stream() {
+  // one per thread and device, never destroyed (a thread-exit destructor could run after the HIP
+  // runtime's own teardown at process exit); the fork / join events order it, so the null stream
+  // is a correct (serialising) fallback
+  static thread_local hipStream_t side[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!side[dev] && hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess) side[dev] = nullptr;
+  return side[dev];
+}
 }  // namespace krca
 
 extern "C" {

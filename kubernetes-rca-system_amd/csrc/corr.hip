@@ -1299,10 +1299,20 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   return KRCA_OK;
 }
 
+// exact |r| > tau counts of the listed ambiguous pairs (float64 from z32), added to count
+int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int32_t* count, hipStream_t st) {
+  const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
+  hipLaunchKernelGGL(corr_amb_rescore, dim3((unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7)), dim3(TPB), 0, st,
+                     (const int2*)ws.amb, (const float*)ws.ambv, (const int32_t*)ws.amb_n, d.P, z32,
+                     (const float*)ws.dn, d.T, d.tau, acc_err, count);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
 // 2. upper-triangle tiles (every G-th super-tile from g): appends into ws.buf, tau counts
 template <int KC>
 int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int g, const float* phi, const CorrWs& ws,
-                int32_t* count, int dbg, hipStream_t st) {
+                int32_t* count, int dbg, hipStream_t st, bool rescore = true) {
   if (int rc = set_lds_attr<KC>()) return rc;
   KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
@@ -1352,11 +1362,7 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   const int rc = krca::tuning().corr_tc == 128 ? launch(std::integral_constant<int, 128>{})
                                                : launch(std::integral_constant<int, 256>{});
   if (rc) return rc;
-  if (dbg == 0) {
-    hipLaunchKernelGGL(corr_amb_rescore, dim3((unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7)), dim3(TPB), 0, st, (const int2*)ws.amb, (const float*)ws.ambv,
-                       (const int32_t*)ws.amb_n, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
-    KRCA_LAUNCH_CHECK();
-  }
+  if (dbg == 0 && rescore) return launch_rescore(z32, d, ws, count, st);
   return KRCA_OK;
 }
 
@@ -1435,8 +1441,24 @@ int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, 
   float* phi = reinterpret_cast<float*>(cand + 4 * head);  // one more [P] after the layout
   const int dbg = debug_mode();
   if (int rc = stage_sample<KC>(zh, d, 0, d.P, ws, phi, st)) return rc;
-  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, st)) return rc;
-  return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
+  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, st, /*rescore=*/false)) return rc;
+  if (dbg != 0) return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
+  // the exact-count re-score (memory-bound, writes count only) and the merge chain (sort, float64
+  // top-k re-scoring, rectangle and deep passes: candidate buffers and outputs only) are
+  // independent: the re-score runs on a side stream forked from and joined back into st
+  hipStream_t side = krca::side_stream();
+  hipEvent_t fork, join;
+  KRCA_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  KRCA_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  KRCA_HIP(hipEventRecord(fork, st));
+  KRCA_HIP(hipStreamWaitEvent(side, fork, 0));
+  int rc = launch_rescore(z32, d, ws, count, side);
+  KRCA_HIP(hipEventRecord(join, side));
+  if (!rc) rc = stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
+  KRCA_HIP(hipStreamWaitEvent(st, join, 0));  // joined on every path: count is final on st
+  KRCA_HIP(hipEventDestroy(fork));
+  KRCA_HIP(hipEventDestroy(join));
+  return rc;
 }
 
 int kc_for(int32_t k) { return k <= 4 ? 8 : k <= 8 ? 12 : 16; }

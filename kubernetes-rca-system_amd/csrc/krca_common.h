@@ -32,6 +32,9 @@ void set_error(const char* fmt, ...);
 #define KRCA_LAUNCH_CHECK() KRCA_HIP(hipGetLastError())
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+// a non-blocking stream of the calling thread's current device for work a launcher forks off its
+// caller's stream (and joins back with events before returning); created once per thread and device
+hipStream_t side_stream();
 
 constexpr int kWave = 64;
 
