@@ -25,14 +25,13 @@ const NamedKnob kKnobs[] = {
     {"KRCA_SCORE_NT", &Tuning::score_nt},     {"KRCA_PPR_GRID", &Tuning::ppr_grid},
     {"KRCA_PPR_DICT", &Tuning::ppr_dict},
     {"KRCA_LOG_IMPL", &Tuning::log_impl},     {"KRCA_GROUP_IMPL", &Tuning::group_impl},
-    {"KRCA_CORR_DEBUG", &Tuning::corr_debug}, {"KRCA_CORR_TC", &Tuning::corr_tc},
+    {"KRCA_CORR_DEBUG", &Tuning::corr_debug},
     {"KRCA_CORR_RS_GRID", &Tuning::corr_rs_grid},
 };
 Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20), env_int("KRCA_SCORE_NT", 1),
                  env_int("KRCA_PPR_GRID", 0),   env_int("KRCA_PPR_DICT", 1),     env_int("KRCA_LOG_IMPL", 0),
                  env_int("KRCA_GROUP_IMPL", 0),
-                 env_int("KRCA_CORR_DEBUG", 0), env_int("KRCA_CORR_RS_GRID", 1024),
-                 env_int("KRCA_CORR_TC", 256)};
+                 env_int("KRCA_CORR_DEBUG", 0), env_int("KRCA_CORR_RS_GRID", 1024)};
 const NamedKnob* find_knob(const char* name) {
   if (!name) return nullptr;
   for (const NamedKnob& k : kKnobs)

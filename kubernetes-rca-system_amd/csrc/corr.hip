@@ -68,7 +68,7 @@ constexpr int32_t AMB_BOTH = 1 << 30;  // entry.y flag: credit the partner's cou
 // (8, 12 or 16), so the k best sampled partners of a pod survive their blocks' cuts
 
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct defeats SROA)
 
 __device__ __forceinline__ uint16_t f16_bits(float f) {
@@ -170,18 +170,14 @@ struct Cand {
   }
 };
 
-// Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh.  A wave holds a 128 x 64
-// tile = 4 x 2 MFMA 32x32 blocks; K steps run through a double-buffered LDS stage fed by direct
-// global->LDS loads.
-//   TC = 256: 8 waves (2 row halves x 4 column quarters), K steps of 64, 130 KB of LDS: one
-//             workgroup per CU (every pass).
-//   TC = 128: 4 waves (2 x 2), K steps of 32, 49 KB of LDS: two workgroups share a CU, so one's
-//             epilogue runs beside the other's MFMAs (the main pass under KRCA_CORR_TC=128; its
-//             product runs 1.6x slower: at 1.5x the staged bytes per flop, the per-CU L2 -> LDS
-//             delivery is the bound).
-// Every output accumulates its 16-deep K slices in ascending order in both geometries, so a pair's
-// screening value is the same bits in every pass.  Sample-pass lists keep a 128-pod block
-// granularity (a row's list covers one 128-column half of a 256-column tile).
+// Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh (TC = 256 in every pass):
+// 8 waves (2 row halves x 4 column quarters), each a 128 x 64 tile = 8 x 4 MFMA 16x16 blocks, K
+// steps of 64 through a double-buffered LDS stage (130 KB with the sample pass's parking area: one
+// workgroup per CU) fed by direct global->LDS loads.  (Measured and dropped: 256 x 128 tiles with
+// 4 waves and two workgroups per CU hide most of the epilogue but stage 1.5x the bytes per flop;
+// their product ran 1.57x slower.)  Every output accumulates its 32-deep K slices in ascending
+// order, so a pair's screening value is the same bits in every pass.  Sample-pass lists keep a
+// 128-pod block granularity (a row's list covers one 128-column half of a 256-column tile).
 constexpr int TB = 256;                  // row block (pods); the unit of the upper-triangle order
 constexpr int EPI_LD = TB + 4;           // padded row of the sample pass's parked half tile (16-B rows)
 constexpr int EPI_LIST_OFF = 8192;       // main-pass epilogue: per-wave candidate lists start here
@@ -299,13 +295,18 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     }
   }
 
-  floatx16 acc[4][2];
+  // 16x16x32 MFMA blocks: acc[i][j][e] = row wr*128 + i*16 + 4*(lane >> 4) + e, column
+  // wc*64 + j*16 + (lane & 15) of the tile.  (The 32x32x16 form ran the same MACs in the same
+  // cycles, 7-9 % slower in wall time: the chip holds a lower clock on it, MI355X_MICROARCH.md
+  // 'DVFS give-back' item 7.)
+  static_assert(G::BKS == 64, "the K loop runs two 32-deep sub-steps per stage");
+  floatx4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
 
   // Staging: global -> LDS direct (global_load_lds_dwordx4, no VGPR round trip).  One wave
   // instruction writes a lane-linear 1 KiB piece = RPP rows; lane l lands on row l / CPR, slot
@@ -332,26 +333,44 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
                                        16, 0, 0);
     }
   };
-  const int r32 = lane & 31, h = lane >> 5;
-  // Fragments in two register sets: the 6 fragments of 16-deep slice ks+1 are read while the 8 MFMAs
-  // of slice ks run, and slice 0 of step s+1 right after the step's barrier, beside the last slice's
-  // MFMAs, so no MFMA waits on a just-issued LDS read.
-  halfx8 fa[2][4], fb[2][2];
-  auto frag_load = [&](int buf, int ks, int set) {
+  const int r16 = lane & 15, g4 = lane >> 4;
+  // Fragments (16x16x32: lane l holds A[row l & 15][k = 8 (l >> 4) .. + 7] of a 16-row block, B the
+  // same of a 16-column block): A row blocks 0-3 (alo) and 4-7 (ahi), B in two sets (one per
+  // 32-deep sub-step).  Each phase runs 16 MFMAs with the reads of the next phase's operands pinned
+  // between them, so no MFMA waits on a just-issued LDS read.
+  halfx8 alo[4], ahi[4], bfr[2][4];
+  auto chunk = [&](int kk) { return 4 * kk + g4; };
+  auto ld_alo = [&](int buf, int kk) {
     const char* sA = smem + buf * G::STAGE;
-    const char* sB = sA + TB * G::ROWB;
-    const int c = ks * 2 + h;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[set][i] = *reinterpret_cast<const halfx8*>(sA + G::chunk_off(wr * 128 + i * 32 + r32, c));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) fb[set][j] = *reinterpret_cast<const halfx8*>(sB + G::chunk_off(wc * 64 + j * 32 + r32, c));
+    for (int i = 0; i < 4; ++i)
+      alo[i] = *reinterpret_cast<const halfx8*>(sA + G::chunk_off(wr * 128 + i * 16 + r16, chunk(kk)));
   };
-  auto frag_mfma = [&](int set) {
+  auto ld_ahi = [&](int buf, int kk) {
+    const char* sA = smem + buf * G::STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      ahi[i] = *reinterpret_cast<const halfx8*>(sA + G::chunk_off(wr * 128 + (i + 4) * 16 + r16, chunk(kk)));
+  };
+  auto ld_b = [&](int set, int buf, int kk) {
+    const char* sB = smem + buf * G::STAGE + TB * G::ROWB;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfr[set][j] = *reinterpret_cast<const halfx8*>(sB + G::chunk_off(wc * 64 + j * 16 + r16, chunk(kk)));
+  };
+  auto mm_lo = [&](int set) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[i], bfr[set][j], acc[i][j], 0, 0, 0);
+  };
+  auto mm_hi = [&](int set) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i + 4][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[i], bfr[set][j], acc[i + 4][j], 0, 0, 0);
   };
   // L2 prefetch of K step s+PFD while step s+1 streams into LDS: one 4-byte LDS-DMA per 128-B line
   // into a junk LDS slot, so no VGPR is tied up; those steps' 16-byte loads then hit L2 instead of
@@ -372,7 +391,17 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   glds(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  frag_load(0, 0, 0);
+  ld_alo(0, 0);
+  ld_b(0, 0, 0);
+  // Per stage (64 deep = sub-steps 0 and 1): A(0) alo x b0 while reading ahi(0); B(0) ahi x b0 while
+  // reading alo(1), b1; A(1) alo x b1 while reading ahi(1); barrier; B(1) ahi x b1 while reading
+  // alo(0), b0 of the next stage.
+#define CORR_PIN(NM, ND)                                                                 \
+  _Pragma("unroll") for (int q = 0; q < 16 / (NM); ++q) {                                 \
+    __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);                                   \
+    __builtin_amdgcn_sched_group_barrier(0x100, ND, 0);                                   \
+  }                                                                                       \
+  __builtin_amdgcn_sched_barrier(0);
   for (int s = 0; s < nk; ++s) {
     const int buf = s & 1;
     // stage buf ^ 1 was last read in step s-1; every wave retired those reads (lgkmcnt(0)) before
@@ -380,31 +409,28 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     if (s + 1 < nk) glds(buf ^ 1, (s + 1) * G::BKS);
     l2pf(s);
     __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs, not after
-    // each phase: the 8 MFMAs of one slice with the 6 reads of the next one between them (pinned:
-    // left alone, the scheduler sinks every read to its first use and waits on it there)
-#define CORR_PHASE(RB, RKS, RSET, MSET)                                              \
-    frag_load(RB, RKS, RSET);                                                        \
-    frag_mfma(MSET);                                                                 \
-    _Pragma("unroll") for (int q = 0; q < 6; ++q) {                                  \
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                             \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                             \
-    }                                                                                \
-    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                               \
-    __builtin_amdgcn_sched_barrier(0);
-    CORR_PHASE(buf, 1, 1, 0)
-    if constexpr (G::KS == 4) {
-      CORR_PHASE(buf, 2, 0, 1)
-      CORR_PHASE(buf, 3, 1, 0)
-    }
+    ld_ahi(buf, 0);
+    mm_lo(0);
+    CORR_PIN(4, 1)
+    ld_alo(buf, 1);
+    ld_b(1, buf, 1);
+    mm_hi(0);
+    CORR_PIN(2, 1)
+    ld_ahi(buf, 1);
+    mm_lo(1);
+    CORR_PIN(4, 1)
     // stage buf ^ 1 has landed for this wave (only the L2 prefetch may be outstanding) and this
     // wave's reads of stage buf are retired; after the barrier, for every wave.  The last step
     // reads stage buf ^ 1 as well (stale bytes, never used): no branch in the loop.
     asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    CORR_PHASE(buf ^ 1, 0, 0, 1)
-#undef CORR_PHASE
+    ld_alo(buf ^ 1, 0);
+    ld_b(0, buf ^ 1, 0);
+    mm_hi(1);
+    CORR_PIN(2, 1)
   }
+#undef CORR_PIN
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // a diagonal 256-block: its tiles hold both orders of every pair (across the TC-column tiles of
@@ -416,11 +442,12 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   }
   if constexpr (!SAMPLE) {
     // ---- main / rect epilogue, straight from the accumulators ---------------------------
-    // lane holds rows wr*128 + i*32 + (e&3) + 8*(e>>2) + 4*h and columns wc*64 + j*32 + r32.
+    // lane holds rows wr*128 + i*16 + 4*(lane >> 4) + e and columns wc*64 + j*16 + (lane & 15).
     // Padding rows / columns have z = 0 (r = 0: never above tau >= 0) and phi = 4 (never a
     // candidate); the self products of a diagonal tile are zeroed first.
-    //   1. per wave, branch-free over a lane's 128 values: |r| > tau + eps counted (row counts by
-    //      ballot + popcount, kept in lane (i, e); column counts per lane), and each
+    //   1. per wave, branch-free over a lane's 128 values: |r| > tau + eps counted (a lane's own hit
+    //      bits added per row e into byte e of a packed counter, summed over the 16 lanes of its row
+    //      group per row block i; column counts per lane), and each
     //      value that may need anything (above phi of its row or column pod, or within eps of tau)
     //      appended RAW to the wave's LDS list {row | col << 8, r bits} (ballot + mbcnt, only when
     //      some lane has one: they are sparse)
@@ -466,12 +493,12 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     if (diag) {
       const int doff = (int)(rowB - rowA);  // global row == global column <=> row - col == doff
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int e = 0; e < 16; ++e)
-            if (wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h == wc * 64 + j * 32 + r32 + doff) acc[i][j][e] = 0.f;
+          for (int e = 0; e < 4; ++e)
+            if (wr * 128 + i * 16 + 4 * g4 + e == wc * 64 + j * 16 + r16 + doff) acc[i][j][e] = 0.f;
     }
     auto append = [&](int pod, int partner, int vbits) {  // candidate of pod (rect: local buffers)
       const int64_t lp = RECT ? pod - sh.lo : pod;
@@ -512,39 +539,30 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     const float tau_hi = A.tau_hi, tau_lo = A.tau_lo;
     {
       int nlist = 0;  // wave-uniform
-      int rcl0 = 0, rcl1 = 0;  // lane L holds the row counts of (i, e) = (L >> 4, L & 15)
-      int colcnt[2] = {0, 0};
+      int colcnt[4] = {0, 0, 0, 0};
       const bool hits = HITS && win == 0;
-      static_for<4>([&](auto ic) {
+      static_for<8>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        float pr[16];
+        const float4 prv = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 16 + 4 * g4);
+        const float pr[4] = {prv.x, prv.y, prv.z, prv.w};
+        float pc[4];  // diagonal tile: both orders present, candidates on the row side only
 #pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const float4 q = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 32 + 8 * e4 + 4 * h);
-          pr[4 * e4] = q.x;
-          pr[4 * e4 + 1] = q.y;
-          pr[4 * e4 + 2] = q.z;
-          pr[4 * e4 + 3] = q.w;
-        }
-        float pc[2];  // diagonal tile: both orders present, candidates on the row side only
-#pragma unroll
-        for (int j = 0; j < 2; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 32 + r32];
-        static_for<16>([&](auto ec) {
+        for (int j = 0; j < 4; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 16 + r16];
+        int rh[4] = {0, 0, 0, 0};  // this lane's hits in row e of block i (over its 4 columns)
+        static_for<4>([&](auto ec) {
           constexpr int e = decltype(ec)::value;
-          int c0 = 0, c1 = 0;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < 4; ++j) {
             const float v = acc[i][j][e];
             const float a = fabsf(v);
             // the masks straight from the compares (no boolean round trip through a VGPR)
             const uint64_t mh = __builtin_amdgcn_ballot_w64(a > tau_hi);
-            if (hits) {
-              c0 += __builtin_popcount((uint32_t)mh);
-              c1 += __builtin_popcount((uint32_t)(mh >> 32));
-              asm volatile("" : "+s"(c0), "+s"(c1));  // counted here: no mask held across the branch below
-              int cc = colcnt[j];
+            if (hits) {  // += own hit bit (v_addc on the mask), row and column counters
+              int cr = rh[e], cc = colcnt[j];
               uint64_t co;
-              asm volatile("v_addc_co_u32_e64 %0, %1, 0, %0, %2" : "+v"(cc), "=s"(co) : "s"(mh));  // += own hit bit
+              asm volatile("v_addc_co_u32_e64 %0, %1, 0, %0, %2" : "+v"(cr), "=s"(co) : "s"(mh));
+              asm volatile("v_addc_co_u32_e64 %0, %1, 0, %0, %2" : "+v"(cc), "=s"(co) : "s"(mh));
+              rh[e] = cr;
               colcnt[j] = cc;
             }
             uint64_t fm = __builtin_amdgcn_ballot_w64(a > pr[e]) | __builtin_amdgcn_ballot_w64(a > pc[j]);
@@ -553,41 +571,36 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
               const int slot = nlist - win + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
               if (((fm >> lane) & 1) && slot >= 0 && slot < CAPL) {
-                const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                const int col = wc * 64 + j * 32 + r32;
+                const int row = wr * 128 + i * 16 + 4 * g4 + e;
+                const int col = wc * 64 + j * 16 + r16;
                 wlist[slot] = make_int2(row | (col << 8), __float_as_int(v));
               }
               nlist += __builtin_popcountll(fm);
             }
           }
-          if (hits) {  // row (i, e) counts into lane i*16 + e (immediate lane: no lane masks held)
-            int t0 = rcl0, t1 = rcl1;  // (asm operands cannot name the enclosing function's locals)
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(t0) : "s"(c0), "n"(i * 16 + e));
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(t1) : "s"(c1), "n"(i * 16 + e));
-            rcl0 = t0;
-            rcl1 = t1;
-          }
         });
+        if (hits) {  // rows of block i: packed (byte e <= 64), summed over the 16 lanes of the row group
+          int pk = rh[0] | (rh[1] << 8) | (rh[2] << 16) | (rh[3] << 24);
+#pragma unroll
+          for (int d = 1; d < 16; d <<= 1) pk += __shfl_xor(pk, d, 16);
+          const int c = (pk >> (8 * (r16 & 3))) & 0xFF;
+          if (r16 < 4 && c) atomicAdd(&srcnt[wr * 128 + i * 16 + 4 * g4 + r16], c);
+        }
       });
       if (debug == 6) {  // profiling aid: step 1 only
-        if (nlist == 12345) A.count[0] = rcl0 + rcl1 + colcnt[0] + colcnt[1];
+        if (nlist == 12345) A.count[0] = colcnt[0] + colcnt[1] + colcnt[2] + colcnt[3];
         return false;
       }
       if (lane == 0) {
         wcount[w] = min(max(nlist - win, 0), CAPL);
         if (nlist > win + CAPL) sflag[0] = 1;  // another window follows
       }
-      if (hits) {  // |r| > tau: one LDS add per row / column and wave
-        const int li = lane >> 4, le = lane & 15;
-        const int rbase = wr * 128 + li * 32 + (le & 3) + 8 * (le >> 2);
-        if (rcl0) atomicAdd(&srcnt[rbase], rcl0);
-        if (rcl1) atomicAdd(&srcnt[rbase + 4], rcl1);
-        if (!diag) {
+      if (hits && !diag) {  // |r| > tau, columns: summed over the 4 row groups, one LDS add per column
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int c = colcnt[j] + __shfl_xor(colcnt[j], 32, 64);
-            if (h == 0 && c) atomicAdd(&sccnt[wc * 64 + j * 32 + r32], c);
-          }
+        for (int j = 0; j < 4; ++j) {
+          int c = colcnt[j] + __shfl_xor(colcnt[j], 16, 64);
+          c += __shfl_xor(c, 32, 64);
+          if (g4 == 0 && c) atomicAdd(&sccnt[wc * 64 + j * 16 + r16], c);
         }
       }
       __syncthreads();
@@ -670,13 +683,13 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     for (int half = 0; half < 2; ++half) {
       if (wr == half) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              const int row = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-              const int col = wc * 64 + j * 32 + r32;
+            for (int e = 0; e < 4; ++e) {
+              const int row = i * 16 + 4 * g4 + e;
+              const int col = wc * 64 + j * 16 + r16;
               tile[row * EPI_LD + col] = acc[i][j][e];
             }
       }
@@ -1234,8 +1247,7 @@ int set_lds_attr1() {
 }
 template <int KC>
 int set_lds_attr() {
-  int rc = set_lds_attr1<KC, MODE_MAIN, 128>();
-  if (!rc) rc = set_lds_attr1<KC, MODE_MAIN, 256>();
+  int rc = set_lds_attr1<KC, MODE_MAIN, 256>();
   if (!rc) rc = set_lds_attr1<KC, MODE_SAMPLE, 256>();
   if (!rc) rc = set_lds_attr1<KC, MODE_RECT, 256>();
   return rc;
@@ -1349,19 +1361,11 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.amb_n = ws.amb_n;
   ta.ambv = ws.ambv;
   ta.dn = ws.dn;
-  // main pass: 256 x 256 tiles (KRCA_CORR_TC = 128: 256 x 128 tiles, two workgroups per CU)
-  auto launch = [&](auto tc) -> int {
-    constexpr int TC = decltype(tc)::value;
-    constexpr int SPLIT = TB / TC;
-    ta.per_xcd = (n_mine * SUPER * SUPER * SPLIT + 7) / 8;
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, TC>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<TC>::NTH),
-                       Geo<TC>::LDS_BYTES, st, ta);
-    KRCA_LAUNCH_CHECK();
-    return KRCA_OK;
-  };
-  const int rc = krca::tuning().corr_tc == 128 ? launch(std::integral_constant<int, 128>{})
-                                               : launch(std::integral_constant<int, 256>{});
-  if (rc) return rc;
+  // main pass: 256 x 256 tiles, XCD-aware slots
+  ta.per_xcd = (n_mine * SUPER * SUPER + 7) / 8;
+  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, 256>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<256>::NTH),
+                     Geo<256>::LDS_BYTES, st, ta);
+  KRCA_LAUNCH_CHECK();
   if (dbg == 0 && rescore) return launch_rescore(z32, d, ws, count, st);
   return KRCA_OK;
 }

@@ -56,7 +56,6 @@ struct Tuning {
   int group_impl;   // KRCA_GROUP_IMPL: 0 peeled atomics, 1 one atomic per lane
   int corr_debug;   // KRCA_CORR_DEBUG: profiling aid (results wrong when != 0)
   int corr_rs_grid; // KRCA_CORR_RS_GRID: workgroups of the ambiguous-pair re-score (a multiple of 8)
-  int corr_tc;      // KRCA_CORR_TC: main-pass column tile, 256 or 128 (two workgroups per CU)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

@@ -13,7 +13,7 @@ if [ "${TESTS:-1}" = 1 ]; then
   [ $rc -eq 0 ] || { tail -40 $O/tests.log; exit $rc; }
 fi
 for rsg in ${RSGS:-4096}; do
-for tc in ${TCS:-128 256}; do
+for tc in ${TCS:-256}; do
 for m in ${MODES:-0 1}; do
   D=t${tc}m${m}g$rsg
   KRCA_CORR_RS_GRID=$rsg KRCA_CORR_TC=$tc KRCA_CORR_DEBUG=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t${tc}m${m}g$rsg -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps 3 > $O/t${tc}m${m}g$rsg.log 2>&1
