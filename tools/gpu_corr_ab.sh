@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU call: correlation GPU tests, then the main-pass tile kernel at C3 per KRCA_CORR_TC (A/B on
+# GPU call: correlation GPU tests, then the main-pass tile kernel at C3 per re-score grid (A/B on
 # one box) and per KRCA_CORR_DEBUG mode, kernel-traced.
 set -u
 TAG=${1:-corrab}
@@ -16,7 +16,7 @@ for rsg in ${RSGS:-4096}; do
 for tc in ${TCS:-256}; do
 for m in ${MODES:-0 1}; do
   D=t${tc}m${m}g$rsg
-  KRCA_CORR_RS_GRID=$rsg KRCA_CORR_TC=$tc KRCA_CORR_DEBUG=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t${tc}m${m}g$rsg -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps 3 > $O/t${tc}m${m}g$rsg.log 2>&1
+  KRCA_CORR_RS_GRID=$rsg KRCA_CORR_DEBUG=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t${tc}m${m}g$rsg -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps 3 > $O/t${tc}m${m}g$rsg.log 2>&1
   rc=$?; echo "$D EXIT=$rc" >> $O/status
   [ $rc -eq 0 ] || { tail -5 $O/$D.log; exit $rc; }
   find $O/$D -name '*.db' -delete
