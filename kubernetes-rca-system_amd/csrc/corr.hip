@@ -1029,11 +1029,25 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
       zj[u] = (q < km && top_i[q] >= 0) ? z32 + (int64_t)top_i[q] * T : nullptr;
       acc2[u] = 0.0;
     }
-    for (int t = lane; t < T; t += 64) {
-      const double a = (double)zg[t];
+    if ((T & 3) == 0) {  // rows are 16-B aligned: float4 loads (1 KiB per wave instruction)
+      const float4* g4 = reinterpret_cast<const float4*>(zg);
+      for (int t = lane; t < T / 4; t += 64) {
+        const float4 a = g4[t];
 #pragma unroll
-      for (int u = 0; u < PER; ++u)
-        if (zj[u]) acc2[u] += a * (double)zj[u][t];
+        for (int u = 0; u < PER; ++u)
+          if (zj[u]) {
+            const float4 b = reinterpret_cast<const float4*>(zj[u])[t];
+            acc2[u] += (double)a.x * (double)b.x + (double)a.y * (double)b.y + (double)a.z * (double)b.z +
+                       (double)a.w * (double)b.w;
+          }
+      }
+    } else {
+      for (int t = lane; t < T; t += 64) {
+        const double a = (double)zg[t];
+#pragma unroll
+        for (int u = 0; u < PER; ++u)
+          if (zj[u]) acc2[u] += a * (double)zj[u][t];
+      }
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -1095,15 +1109,44 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
   for (int i = tid; i < np; i += TPB) ci[i] = i < n ? buf[gl * CAPC + i].y : -1;
   __syncthreads();
   const float* zg = z32 + g * T;
-  for (int c = w; c < np; c += TPB / 64) {
-    const int32_t j = ci[c];
-    double acc = 0.0;
-    if (j >= 0) {
-      const float* zj = z32 + (int64_t)j * T;
-      for (int t = lane; t < T; t += 64) acc += (double)zg[t] * (double)zj[t];
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  // wave w re-scores candidates 4w .. 4w + 3, then 4w + 16 .., together (independent loads in flight;
+  // float4 loads when the rows are 16-B aligned)
+  constexpr int PD = 4;
+  for (int c0 = PD * w; c0 < np; c0 += PD * (TPB / 64)) {
+    const float* zj[PD];
+    double acc[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int32_t j = c0 + u < np ? ci[c0 + u] : -1;
+      zj[u] = j >= 0 ? z32 + (int64_t)j * T : nullptr;
+      acc[u] = 0.0;
     }
-    if (lane == 0) ex[c] = acc;
+    if ((T & 3) == 0) {
+      const float4* g4 = reinterpret_cast<const float4*>(zg);
+      for (int t = lane; t < T / 4; t += 64) {
+        const float4 a = g4[t];
+#pragma unroll
+        for (int u = 0; u < PD; ++u)
+          if (zj[u]) {
+            const float4 b = reinterpret_cast<const float4*>(zj[u])[t];
+            acc[u] += (double)a.x * (double)b.x + (double)a.y * (double)b.y + (double)a.z * (double)b.z +
+                      (double)a.w * (double)b.w;
+          }
+      }
+    } else {
+      for (int t = lane; t < T; t += 64) {
+        const double a = (double)zg[t];
+#pragma unroll
+        for (int u = 0; u < PD; ++u)
+          if (zj[u]) acc[u] += a * (double)zj[u][t];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      double v = acc[u];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0 && c0 + u < np) ex[c0 + u] = zj[u] ? v : 0.0;
+    }
   }
   __syncthreads();
   for (int kk = 2; kk <= np; kk <<= 1) {  // bitonic: |r| desc, index asc, empties last
