@@ -196,8 +196,7 @@ struct Geo {
   static constexpr int LDS_STAGE = 2 * STAGE;             // double buffered
   static constexpr int LDS_EPI = TC == 256 ? BM * EPI_LD * 4 : 0;  // sample pass: 128 x 256 fp32
   static constexpr int LDS_MAIN = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
-  static constexpr int LDS_BYTES = LDS_MAIN + NTH * 4;    // + landing slots of the L2 prefetch loads
-  static constexpr int PFD = TC == 256 ? 2 : 4;           // L2 prefetch distance (K steps)
+  static constexpr int LDS_BYTES = LDS_MAIN;
   static constexpr int CAPL = (LDS_MAIN - EPI_LIST_OFF) / (NW * 8);  // epilogue list entries per wave
   // 16-byte chunk c of staged row r, XOR-swizzled: the 256/ROWB rows of one 256-B bank row sit in
   // distinct granule groups and the key (r / (256/ROWB)) % CPR spreads the rest, so every 16-lane
@@ -315,7 +314,7 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   const uint16_t* gA = A.zA + rowA * Tp;
   const uint16_t* gB = A.zh + rowB * Tp;
   const int prow = lane / G::CPR, pslot = lane % G::CPR;
-  auto glds = [&](int buf, int k0) {
+  auto glds_a = [&](int buf, int k0) {
     char* sbase = smem + buf * G::STAGE;
 #pragma unroll
     for (int q = 0; q < G::NPA; ++q) {
@@ -324,6 +323,9 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       __builtin_amdgcn_global_load_lds(gA + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
                                        (__attribute__((address_space(3))) void*)(sbase + piece * 1024), 16, 0, 0);
     }
+  };
+  auto glds_b = [&](int buf, int k0) {
+    char* sbase = smem + buf * G::STAGE;
 #pragma unroll
     for (int q = 0; q < G::NPB; ++q) {
       const int piece = w + G::NW * q;
@@ -332,6 +334,10 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
                                        (__attribute__((address_space(3))) void*)(sbase + TB * G::ROWB + piece * 1024),
                                        16, 0, 0);
     }
+  };
+  auto glds = [&](int buf, int k0) {
+    glds_a(buf, k0);
+    glds_b(buf, k0);
   };
   const int r16 = lane & 15, g4 = lane >> 4;
   // Fragments (16x16x32: lane l holds A[row l & 15][k = 8 (l >> 4) .. + 7] of a 16-row block, B the
@@ -372,22 +378,7 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       for (int j = 0; j < 4; ++j)
         acc[i + 4][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[i], bfr[set][j], acc[i + 4][j], 0, 0, 0);
   };
-  // L2 prefetch of K step s+PFD while step s+1 streams into LDS: one 4-byte LDS-DMA per 128-B line
-  // into a junk LDS slot, so no VGPR is tied up; those steps' 16-byte loads then hit L2 instead of
-  // paying the HBM/MALL latency inside one K step's compute.  TC = 256: thread tid < 256 takes A
-  // row tid, else B row tid - 256, every step.  TC = 128 (a line spans two 32-deep steps): A row tid
-  // on even steps, B row tid (tid < 128) on odd ones.  One load per thread and step, so the
-  // barrier's vmcnt(1) leaves exactly it outstanding.
   const int nk = Tp / G::BKS;
-  const uint16_t* gP = TC == 256 ? (tid < TB ? gA + (int64_t)tid * Tp : gB + (int64_t)(tid - TB) * Tp)
-                                 : gA + (int64_t)tid * Tp;
-  const uint16_t* gPB = gB + (int64_t)(tid & (TC - 1)) * Tp;
-  char* junk = smem + G::LDS_MAIN + w * 256;
-  auto l2pf = [&](int s) {
-    const int sp = s + G::PFD < nk ? s + G::PFD : 0;  // past the end: re-touches a resident line
-    const uint16_t* src = (TC == 128 && (s & 1) && tid < TC) ? gPB : gP;
-    __builtin_amdgcn_global_load_lds(src + sp * G::BKS, (__attribute__((address_space(3))) void*)junk, 4, 0, 0);
-  };
   glds(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -405,13 +396,20 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   for (int s = 0; s < nk; ++s) {
     const int buf = s & 1;
     // stage buf ^ 1 was last read in step s-1; every wave retired those reads (lgkmcnt(0)) before
-    // the barrier that ended it
-    if (s + 1 < nk) glds(buf ^ 1, (s + 1) * G::BKS);
-    l2pf(s);
-    __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs, not after
+    // the barrier that ended it.  The next stage's A pieces go out before the first MFMA phase, its
+    // B pieces after it: issued together (or in three groups) they ran 4 % (2 %) slower.  The last
+    // step re-loads its own stage into the idle buffer (never read), so the loop has no branch.
+    // (An L2 prefetch of step s + 2 by 4-byte LDS-DMA loads, one per 128-B line, ran 7 % slower in
+    // the 16x16x32 form: its issue slots and a lower clock cost more than the latency it hid;
+    // without any staging in the loop the product ran 9.3 vs 12.8 ms, clock 1.97 vs 1.74 GHz.)
+    const int kn = (s + 1 < nk ? s + 1 : s) * G::BKS;
+    glds_a(buf ^ 1, kn);
+    __builtin_amdgcn_sched_barrier(0);
     ld_ahi(buf, 0);
     mm_lo(0);
     CORR_PIN(4, 1)
+    glds_b(buf ^ 1, kn);
+    __builtin_amdgcn_sched_barrier(0);
     ld_alo(buf, 1);
     ld_b(1, buf, 1);
     mm_hi(0);
@@ -419,10 +417,10 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     ld_ahi(buf, 1);
     mm_lo(1);
     CORR_PIN(4, 1)
-    // stage buf ^ 1 has landed for this wave (only the L2 prefetch may be outstanding) and this
+    // stage buf ^ 1 has landed for this wave and this
     // wave's reads of stage buf are retired; after the barrier, for every wave.  The last step
     // reads stage buf ^ 1 as well (stale bytes, never used): no branch in the loop.
-    asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     ld_alo(buf ^ 1, 0);
