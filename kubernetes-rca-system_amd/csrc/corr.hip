@@ -230,7 +230,8 @@ struct TileArgs {
   const uint16_t* zh;
   int64_t P;
   int Tp, nb2;
-  int64_t per_xcd;     // MAIN: workgroup slots per XCD
+  int64_t per_xcd;     // workgroup slots per XCD
+  int64_t n_tiles;     // RECT / SAMPLE: tiles of the launch (slots past it exit at once)
   int nsb;
   float tau_hi;   // MAIN: tau + eps, every screening |r| above it is a hit
   float tau_lo;   // MAIN: tau - eps, none at or below it is
@@ -741,8 +742,16 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
 // per CU for TC = 128 (<= 256 registers per lane).
 template <int KC, int MODE, int TC>
 __global__ __launch_bounds__(Geo<TC>::NTH) __attribute__((amdgpu_waves_per_eu(2))) void corr_tiles(TileArgs A) {
+  // RECT / SAMPLE: XCD-aware slots as in the main pass (L = (b % 8) * per_xcd + b / 8, each XCD a
+  // contiguous run), ordered so that the tiles sharing the operand fetched from beyond L2 run on one
+  // XCD together: rect, column-block-major (the gathered row blocks are few and stay cached); sample,
+  // row-block-major (the sample column blocks are shared by every tile).  Row-major over blockIdx
+  // spread each such panel over all 8 XCDs' L2s.
+  const int64_t L = (int64_t)(blockIdx.x & 7) * A.per_xcd + (blockIdx.x >> 3);
   if constexpr (MODE == MODE_RECT) {
-    const int64_t I = blockIdx.x / A.nb2, J = blockIdx.x % A.nb2;
+    if (L >= A.n_tiles) return;
+    const int64_t nri = A.n_tiles / A.nb2;  // gathered row blocks of this launch
+    const int64_t I = L % nri, J = L / nri;
     if (tile_body<KC, MODE_RECT, TC>(A, I, J, false, 0)) {  // window 0 outside the loop (as MODE_MAIN)
       for (int win = Geo<TC>::CAPL;; win += Geo<TC>::CAPL) {
         __syncthreads();  // the next window reuses the LDS
@@ -750,9 +759,10 @@ __global__ __launch_bounds__(Geo<TC>::NTH) __attribute__((amdgpu_waves_per_eu(2)
       }
     }
   } else if constexpr (MODE == MODE_SAMPLE) {
+    if (L >= A.n_tiles) return;
     const int nsb2 = (A.nsb + 1) / 2;  // this chunk's 256-blocks
-    const int64_t I = A.sh.I0 + blockIdx.x / (nsb2 + 1);
-    int64_t J = blockIdx.x % (nsb2 + 1);
+    const int64_t I = A.sh.I0 + L / (nsb2 + 1);
+    int64_t J = L % (nsb2 + 1);
     bool own = false;
     if (J == nsb2) {  // the row block's own 256-block, unless it is already a sample block
       if (!A.sh.own || I < A.sh.nsb2_all) return;
@@ -1345,7 +1355,10 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
     ta.samp_i = ws.samp_i;
     ta.selfd = ws.selfd;
     ta.sh = sh;
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE, 256>), dim3((unsigned)((I1 - I0) * (nsb2 + 1))),
+    ta.debug = debug_mode();
+    ta.n_tiles = (I1 - I0) * (nsb2 + 1);
+    ta.per_xcd = (ta.n_tiles + 7) / 8;
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_SAMPLE, 256>), dim3((unsigned)(8 * ta.per_xcd)),
                        dim3(Geo<256>::NTH), Geo<256>::LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(corr_theta<KC>, dim3((unsigned)krca::ceil_div(n, TPB / 64)), dim3(TPB), 0, st, ws.samp_v,
@@ -1470,7 +1483,9 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
     ta.rect_pods = ws.over + 1 + r0;
     ta.n_rect = nr;
     ta.sh = sh;
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT, 256>), dim3((unsigned)(npad / TB * d.nb2)), dim3(Geo<256>::NTH),
+    ta.n_tiles = npad / TB * d.nb2;
+    ta.per_xcd = (ta.n_tiles + 7) / 8;
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_RECT, 256>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<256>::NTH),
                        Geo<256>::LDS_BYTES, st, ta);
     KRCA_LAUNCH_CHECK();
   }

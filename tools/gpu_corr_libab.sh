@@ -19,7 +19,7 @@ fi
 for r in $(seq ${ROUNDS:-2}); do
 for v in ${VARIANTS:-base}; do
   D=$v-r$r
-  KRCA_LIB=$(lib $v) KRCA_CORR_DEBUG=${MODE:-0} timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$D -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps 3 > $O/$D.log 2>&1
+  KRCA_LIB=$(lib $v) KRCA_CORR_DEBUG=${MODE:-0} timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$D -o run -- python3 tools/prof_kernels.py corr --pods ${PODS:-100000} --reps ${REPS:-3} --tau ${TAU:-0.5} > $O/$D.log 2>&1
   rc=$?; echo "$D EXIT=$rc" >> $O/status
   [ $rc -eq 0 ] || { tail -5 $O/$D.log; exit $rc; }
   find $O/$D -name '*.db' -delete
