@@ -680,7 +680,7 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       return more;
     }
   } else {
-    // ---- sample pass: park each 128-row half in LDS, one lane per (row, 128-column half) --------
+    // ---- sample pass: park each 128-row half in LDS, two lanes per (row, 128-column half) -------
     float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -697,39 +697,69 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
             }
       }
       __syncthreads();
-      if (tid < 256) {  // row scan: pod rowA + half*128 + r against 128 columns of block 2J + ch
-        const int r = tid & 127, ch = tid >> 7;
-        const int64_t g = rowA + half * BM + r;
-        const int jb = 2 * (int)(J - sh.j0) + ch;  // list slot of this chunk
-        const int64_t c0 = rowB + ch * BM;
-        if (g < P && (own || jb < A.nsb)) {
-          Cand<KC> cd;
-          cd.init();
-          const int64_t slot = g * NSL + (own ? NSB + ch : jb);
-          const int cend = (int)std::min<int64_t>(BM, P - c0);
-          const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
-          const float* rowp = tile + r * EPI_LD + ch * BM;
-          if (self >= 0) A.selfd[g] = rowp[self];
-          float lim = -1.f;
-          for (int c4 = 0; c4 < cend; c4 += 4) {
-            const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
+      // row scan: pod rowA + half*128 + r against the 128 columns of block 2J + ch, two threads per
+      // row and block (part 0: columns 0-63, part 1: 64-127; the lanes of a wave scan different
+      // rows, so the insert network runs at every column where any lane inserts: halving the
+      // columns per thread halves that).  Part 1 leaves its sorted list in its own (scanned) columns
+      // of the parked row; part 0 inserts it after its own: part 1's columns are all higher, so the
+      // index tie rule of the ascending scan still holds and the list equals a single scan's.
+      const int r = tid & 127, ch = (tid >> 7) & 1, part = tid >> 8;
+      const int64_t g = rowA + half * BM + r;
+      const int jb = 2 * (int)(J - sh.j0) + ch;  // list slot of this chunk
+      const int64_t c0 = rowB + ch * BM;
+      const bool active = g < P && (own || jb < A.nsb);
+      float* rowp = tile + r * EPI_LD + ch * BM;
+      Cand<KC> cd;
+      cd.init();
+      if (active) {
+        const int cend = (int)std::min<int64_t>(BM, P - c0);
+        const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
+        if (self >= 0 && (self >= BM / 2) == (part == 1)) A.selfd[g] = rowp[self];  // before part 1's list lands
+        float lim = -1.f;
+        const int cb = part * (BM / 2), ce = std::min(cend, cb + BM / 2);
+        for (int c4 = cb; c4 < ce; c4 += 4) {
+          const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int c = c4 + u;
-              const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
-              if (c < cend && c != self && fabsf(vu) > lim) {
-                cd.insert(vu, (int32_t)(c0 + c));
-                lim = cd.thr;
-              }
+          for (int u = 0; u < 4; ++u) {
+            const int c = c4 + u;
+            const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
+            if (c < ce && c != self && fabsf(vu) > lim) {
+              cd.insert(vu, (int32_t)(c0 + c));
+              lim = cd.thr;
             }
           }
-          float* ov = A.samp_v + slot * KC;
-          int32_t* oi = A.samp_i + slot * KC;
+        }
+        if (part == 1) {
 #pragma unroll
           for (int q = 0; q < KC; ++q) {
-            ov[q] = cd.v[q];
-            oi[q] = cd.i[q];
+            rowp[BM / 2 + 2 * q] = cd.v[q];
+            rowp[BM / 2 + 2 * q + 1] = __int_as_float(cd.i[q]);
           }
+        }
+      }
+      static_assert(2 * KC <= BM / 2, "part 1's list fits in its columns");
+      __syncthreads();
+      if (active && part == 0) {
+        float lim = cd.thr;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+          const float vu = rowp[BM / 2 + 2 * q];
+          const int32_t iq = __float_as_int(rowp[BM / 2 + 2 * q + 1]);
+          if (iq >= 0 && fabsf(vu) > lim) {
+            cd.insert(vu, iq);
+            lim = cd.thr;
+          }
+        }
+        const int64_t slot = g * NSL + (own ? NSB + ch : jb);
+        // 16-byte stores (a list is KC * 4 bytes at a multiple of 16): a lane's dword stores to its
+        // own list went to 64 lines per wave instruction, KC of them per array
+        static_assert(KC % 4 == 0, "lists are whole 16-byte pieces");
+        float4* ov = reinterpret_cast<float4*>(A.samp_v + slot * KC);
+        int4* oi = reinterpret_cast<int4*>(A.samp_i + slot * KC);
+#pragma unroll
+        for (int q = 0; q < KC / 4; ++q) {
+          ov[q] = make_float4(cd.v[4 * q], cd.v[4 * q + 1], cd.v[4 * q + 2], cd.v[4 * q + 3]);
+          oi[q] = make_int4(cd.i[4 * q], cd.i[4 * q + 1], cd.i[4 * q + 2], cd.i[4 * q + 3]);
         }
       }
       __syncthreads();  // the next half overwrites the tile
