@@ -535,13 +535,16 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       int nlist = 0;  // wave-uniform
       int colcnt[4] = {0, 0, 0, 0};
       const bool hits = HITS && win == 0;
+      // the lane's 32 row bounds and 4 column bounds, read once (one LDS wait, not one per block)
+      float4 prall[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) prall[i] = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 16 + 4 * g4);
+      float pc[4];  // diagonal tile: both orders present, candidates on the row side only
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 16 + r16];
       static_for<8>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const float4 prv = *reinterpret_cast<const float4*>(sphr + wr * 128 + i * 16 + 4 * g4);
-        const float pr[4] = {prv.x, prv.y, prv.z, prv.w};
-        float pc[4];  // diagonal tile: both orders present, candidates on the row side only
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pc[j] = diag ? 4.f : sphc[wc * 64 + j * 16 + r16];
+        const float pr[4] = {prall[i].x, prall[i].y, prall[i].z, prall[i].w};
         int rh[4] = {0, 0, 0, 0};  // this lane's hits in row e of block i (over its 4 columns)
         static_for<4>([&](auto ec) {
           constexpr int e = decltype(ec)::value;
