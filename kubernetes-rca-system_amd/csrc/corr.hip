@@ -140,34 +140,40 @@ __global__ __launch_bounds__(TPB) void corr_transpose(const float* __restrict__ 
 // "better" is a strict |r| comparison and the index tie rule holds by construction.
 template <int KC>
 struct Cand {
-  float v[KC];  // signed r
-  int32_t i[KC];
-  float thr;    // |v[KC-1]| (-1 while the list is not full)
+  float k[KC];    // |r|, -1 = empty (below every |r|, so an empty slot takes any value)
+  int32_t c[KC];  // partner << 1 | sign of r, -1 = empty (partner < 2^30)
+  float thr;      // k[KC-1]: -1 while the list is not full
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      v[j] = 0.f;
-      i[j] = -1;
+      k[j] = -1.f;
+      c[j] = -1;
     }
     thr = -1.f;
   }
+  // one compare per slot (h[j] = the new value goes above slot j), then a shift of the slots below
+  // the insertion point: 2 selects per slot for the key and the packed partner
   __device__ __forceinline__ void insert(float nv, int32_t ni) {
     const float a = fabsf(nv);
+    const int32_t code = (ni << 1) | (int32_t)(__float_as_uint(nv) >> 31);
+    bool h[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) h[j] = a > k[j];
 #pragma unroll
     for (int j = KC - 1; j > 0; --j) {
-      const bool up = a > fabsf(v[j - 1]) || i[j - 1] < 0;  // shift v[j-1] down
-      const bool here = a > fabsf(v[j]) || i[j] < 0;
-      const float pv = v[j - 1];
-      const int32_t pi = i[j - 1];
-      v[j] = up ? pv : (here ? nv : v[j]);
-      i[j] = up ? pi : (here ? ni : i[j]);
+      k[j] = h[j - 1] ? k[j - 1] : (h[j] ? a : k[j]);
+      c[j] = h[j - 1] ? c[j - 1] : (h[j] ? code : c[j]);
     }
-    if (a > fabsf(v[0]) || i[0] < 0) {
-      v[0] = nv;
-      i[0] = ni;
+    if (h[0]) {
+      k[0] = a;
+      c[0] = code;
     }
-    thr = i[KC - 1] < 0 ? -1.f : fabsf(v[KC - 1]);
+    thr = k[KC - 1];
   }
+  __device__ __forceinline__ float value(int j) const {
+    return c[j] < 0 ? 0.f : ((c[j] & 1) ? -k[j] : k[j]);
+  }
+  __device__ __forceinline__ int32_t partner(int j) const { return c[j] < 0 ? -1 : c[j] >> 1; }
 };
 
 // Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh (TC = 256 in every pass):
@@ -735,8 +741,8 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         if (part == 1) {
 #pragma unroll
           for (int q = 0; q < KC; ++q) {
-            rowp[BM / 2 + 2 * q] = cd.v[q];
-            rowp[BM / 2 + 2 * q + 1] = __int_as_float(cd.i[q]);
+            rowp[BM / 2 + 2 * q] = cd.value(q);
+            rowp[BM / 2 + 2 * q + 1] = __int_as_float(cd.partner(q));
           }
         }
       }
@@ -761,8 +767,8 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         int4* oi = reinterpret_cast<int4*>(A.samp_i + slot * KC);
 #pragma unroll
         for (int q = 0; q < KC / 4; ++q) {
-          ov[q] = make_float4(cd.v[4 * q], cd.v[4 * q + 1], cd.v[4 * q + 2], cd.v[4 * q + 3]);
-          oi[q] = make_int4(cd.i[4 * q], cd.i[4 * q + 1], cd.i[4 * q + 2], cd.i[4 * q + 3]);
+          ov[q] = make_float4(cd.value(4 * q), cd.value(4 * q + 1), cd.value(4 * q + 2), cd.value(4 * q + 3));
+          oi[q] = make_int4(cd.partner(4 * q), cd.partner(4 * q + 1), cd.partner(4 * q + 2), cd.partner(4 * q + 3));
         }
       }
       __syncthreads();  // the next half overwrites the tile
@@ -1558,7 +1564,7 @@ int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, 
   return rc;
 }
 
-int kc_for(int32_t k) { return k <= 4 ? 8 : k <= 8 ? 12 : 16; }
+int kc_for(int32_t k) { return k <= 8 ? 8 : k <= 12 ? 12 : 16; }  // the smallest list size >= k
 
 }  // namespace
 

@@ -19,6 +19,6 @@ for mode in ${MODES:-1 4 0}; do
   done
 done
 find $O -name '*.db' -delete
-for mode in ${MODES:-1 4 0}; do echo "== mode $mode"; python3 tools/pmc_summary.py $O/m${mode}p1 "corr_tiles<16, 0, 256>"; python3 tools/pmc_summary.py $O/m${mode}p2 "corr_tiles<16, 0, 256>"; done > $O/summary.txt
+for mode in ${MODES:-1 4 0}; do echo "== mode $mode"; python3 tools/pmc_summary.py $O/m${mode}p1 "corr_tiles<12, 0, 256>"; python3 tools/pmc_summary.py $O/m${mode}p2 "corr_tiles<12, 0, 256>"; done > $O/summary.txt
 cat $O/summary.txt
 echo all-done >> $O/status
