@@ -1136,10 +1136,14 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
   }
 }
 
-// one workgroup per listed pod (its merge left cert <= 0): every buffered candidate re-scored in
-// float64 (one wave per candidate, the merge's fixed-order reduction), sorted by (|r| desc, index
-// asc), top k written.  Partners outside the buffer have a screening |r| <= phi, so the k-th exact
-// |r| minus phi minus eps certifies the set (> 0 whenever the buffer holds the k sampled partners).
+// one workgroup per listed pod (its merge left cert <= 0): buffered candidates re-scored in float64
+// (one wave per candidate, the merge's fixed-order reduction), sorted by (|r| desc, index asc), top k
+// written.  Pass 0 re-scores only the candidates whose screening |r| reaches the merge's k-th exact
+// value - 2 eps (near-ties around the k-th: usually a handful, not the whole buffer); the rest have
+// exact |r| <= their screening |r| + eps, so it certifies with that bound in place of phi when it
+// can.  Pass 1 (only if not) re-scores every candidate: partners outside the buffer have a screening
+// |r| <= phi, so the k-th exact |r| minus phi minus eps certifies the set (> 0 whenever the buffer
+// holds the k sampled partners).
 __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ buf, const int32_t* __restrict__ cnt,
                                                        const float* __restrict__ phi, const float* __restrict__ phi2,
                                                        const float* __restrict__ z32,
@@ -1148,16 +1152,34 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
                                                        float* __restrict__ cert, int64_t lo) {
   __shared__ double ex[CAPC];
   __shared__ int32_t ci[CAPC];
+  __shared__ int srest;  // pass 0: the largest screening |r| left out (float bits, >= 0), INT_MIN = none
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nd = pods[0];  // list length first (device-held: no host round trip)
   for (int b = blockIdx.x; b < nd; b += gridDim.x) {
-  __syncthreads();  // ex / ci of the previous pod
   const int64_t g = pods[1 + b];
   const int64_t gl = g - lo;
   const int n = min(cnt[gl], CAPC);
   int np = 32;
   while (np < n) np <<= 1;
-  for (int i = tid; i < np; i += TPB) ci[i] = i < n ? buf[gl * CAPC + i].y : -1;
+  // the merge's k-th exact |r| (its output row, written before it listed the pod)
+  const float thr = fabsf(out_v[gl * k + k - 1]) - 2.f * eps - 1e-6f;
+  for (int pass = 0; pass < 2; ++pass) {
+  __syncthreads();  // ex / ci / srest of the previous pod or pass
+  if (tid == 0) srest = INT_MIN;
+  __syncthreads();
+  for (int i = tid; i < np; i += TPB) {
+    int32_t c = -1;
+    if (i < n) {
+      const int2 e = buf[gl * CAPC + i];
+      const float a = fabsf(__int_as_float(e.x));
+      if (pass == 1 || a >= thr) {
+        c = e.y;
+      } else {
+        atomicMax(&srest, __float_as_int(a));
+      }
+    }
+    ci[i] = c;
+  }
   __syncthreads();
   const float* zg = z32 + g * T;
   // wave w re-scores candidates 4w .. 4w + 3, then 4w + 16 .., together (independent loads in flight;
@@ -1221,13 +1243,20 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
       __syncthreads();
     }
   }
-  for (int q = tid; q < k; q += TPB) {
-    out_i[gl * k + q] = ci[q];
-    out_v[gl * k + q] = (float)ex[q];
-  }
-  // the bound of the buffer: phi2 for a pod refilled by the rectangle pass (3 = not refilled)
+  // the bound of the buffer: phi2 for a pod refilled by the rectangle pass (3 = not refilled); in
+  // pass 0 also the screening |r| of the candidates left out
   const float ph = phi2[g] < 2.5f ? phi2[g] : phi[g];
-  if (tid == 0) cert[gl] = (float)(fabs(ex[k - 1]) - (double)ph - (double)eps);
+  const float bound = srest == INT_MIN ? ph : fmaxf(ph, __int_as_float(srest));
+  const float c = (float)(fabs(ex[k - 1]) - (double)bound - (double)eps);
+  if (pass == 1 || (ci[k - 1] >= 0 && c > 0.f)) {  // block-uniform
+    for (int q = tid; q < k; q += TPB) {
+      out_i[gl * k + q] = ci[q];
+      out_v[gl * k + q] = (float)ex[q];
+    }
+    if (tid == 0) cert[gl] = c;
+    break;
+  }
+  }
   }
 }
 
