@@ -7,9 +7,10 @@ the full RCA hot path (krca/rca.py): rolling z-scores of every pod -> seeded per
 PageRank (30 fixed-point iterations) -> root-cause top-10 on the host.  Inputs are resident in
 HBM before timing; nothing is cached across steps.
 
-Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`; the mesh is
-sharded by pod (strong scaling: the same 1M pods over N GPUs), one all-gather over RCCL per
-PageRank iteration.  Rank 0 prints ONE JSON line.
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (a `torch.distributed.run` child
+process, before anything touches the GPU); under an external launcher (WORLD_SIZE set) it must
+equal --gpus.  The mesh is sharded by pod (strong scaling: the same 1M pods over N GPUs), one
+all-gather over RCCL per PageRank iteration.  Rank 0 prints ONE JSON line.
 
 Steps are pipelined over two HIP streams (two shard states over the same resident metrics): step
 i+1's HBM-bound scoring runs while step i's latency-bound PageRank iterates (the scoring kernels
@@ -56,7 +57,24 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run steps back to back on one stream (default: two streams, step i+1's scoring "
                          "overlaps step i's PageRank)")
+    ap.add_argument("--profile", action="store_true",
+                    help="after the timed steps, one unpipelined step per rank with a HIP event around every "
+                         "launch (scoring, PageRank init / step / exchange / reduce, key + top-k) and roctx "
+                         "ranges for rocprofv3 --marker-trace; per-kernel times go to the JSON line's 'profile'")
     return ap.parse_args(argv)
+
+
+def launch_ranks(n, argv):
+    """Start n ranks of this script (one per GPU) with torch.distributed.run as a CHILD process —
+    nothing in this process has touched the GPU — and return rank 0's launcher exit status."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    log(f"bench: starting {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
 
 
 def cpu_model():
@@ -74,8 +92,66 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def profile_step(step, stream, world):
+    """One unpipelined RCA step with a HIP event pair around every launch on `stream` (and a roctx
+    range per phase): {phase: [ms per launch]} summarised as count / total / mean, plus the step."""
+    import torch
+    import torch.distributed as dist
+    try:
+        from torch.cuda import nvtx  # roctx on ROCm builds
+        push, pop = nvtx.range_push, nvtx.range_pop
+        push("krca.probe")
+        pop()
+    except Exception:  # noqa: BLE001
+        push = pop = lambda *a: None  # noqa: E731
+    s, c, cfg = step.s, step.comm, step.cfg
+    from krca.rca import step_flags
+    rec = []
+
+    def timed(name, fn):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        push(name)
+        a.record()
+        fn()
+        b.record()
+        pop()
+        rec.append((name, a, b))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        timed("krca_rolling_score", s.score)
+        timed("krca_ppr_shard_init", lambda: s.init(cfg.alpha, cfg.seed_floor))
+        timed("exchange", lambda: c.exchange(s))
+        timed("krca_ppr_shard_reduce", lambda: s.reduce(cfg.alpha, cfg.tol, 1))
+        for it in range(cfg.iters):
+            timed("krca_ppr_shard_step", lambda: s.step(cfg.alpha, step_flags(cfg.tol, it + 1 == cfg.iters)))
+            timed("exchange", lambda: c.exchange(s))
+            timed("krca_ppr_shard_reduce", lambda: s.reduce(cfg.alpha, cfg.tol, 0))
+        timed("key+topk", lambda: s.local_topk(cfg.k))
+        t1.record()
+    torch.cuda.synchronize()
+    out = {}
+    for name, a, b in rec:
+        out.setdefault(name, []).append(a.elapsed_time(b))
+    summ = {k: {"launches": len(v), "total_ms": float(np.sum(v)), "mean_ms": float(np.mean(v))} for k, v in out.items()}
+    summ["step_ms"] = t0.elapsed_time(t1)
+    summ["note"] = ("HIP events on the launch stream around each call (host launch gaps included in step_ms, "
+                    "not in the per-call times); 'exchange' is the all-gather at G > 1, a buffer swap at G = 1")
+    return summ
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        log(f"bench: WORLD_SIZE={os.environ.get('WORLD_SIZE')} but --gpus {args.gpus}")
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -192,6 +268,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         latency_ms = float(t.item())
     score_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    prof = profile_step(step, streams[0], world) if args.profile else None
 
     # ---- roofline of the dominant kernel (krca_rolling_score) ----------------------------
     n_loc = hi - lo
@@ -234,6 +311,7 @@ def main():
                          "solo_avg_launch_ms": solo_ms,
                          "solo_frac": bytes_score / (solo_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "rca_top10": [int(i) for i in top_idx],
+            "world_ranks": world, "backend": backend if world > 1 else None,
             "planted_root_recall": len(set(int(i) for i in top_idx) & set(mesh.roots.tolist())) / len(mesh.roots),
         }
 
@@ -299,6 +377,8 @@ def main():
                 "note": "the reference has no rolling scoring or PageRank; these are its per-pod threshold "
                         "loop, 13-regex line histogram, SPOF betweenness and C1 comprehensive analysis"}
 
+    if rank == 0 and prof is not None:
+        result["profile"] = prof
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -243,6 +243,14 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const
                         int32_t flags, int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
                           double tol, int32_t first, void* ctl, int64_t* send_next, void* stream);
+/* Single device (G = 1, n_max = N): krca_ppr_shard_step with the iteration's krca_ppr_shard_reduce
+ * (first = 0) done by the step's last workgroup — one launch per iteration instead of two.  Reads
+ * the codes of w, writes r and send, zeroes w's partial-sum slots (w is the next step's write
+ * target: the caller swaps w and send, exactly as around krca_ppr_shard_reduce). */
+int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const int64_t* plan, int64_t plan_len,
+                       const uint16_t* lane, int64_t* w /*[slice(N)]*/, const int32_t* outdeg, const int64_t* q,
+                       int64_t N, double alpha, int32_t flags, double tol, int64_t* r, int64_t* send /*!= w*/,
+                       void* ctl, void* stream);
 int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);
 int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream);
 /* root-cause key = bits of (double)r_i * (double)q_i: ranks pods by propagated mass times their

@@ -27,11 +27,14 @@ const NamedKnob kKnobs[] = {
     {"KRCA_LOG_IMPL", &Tuning::log_impl},     {"KRCA_GROUP_IMPL", &Tuning::group_impl},
     {"KRCA_CORR_DEBUG", &Tuning::corr_debug},
     {"KRCA_CORR_RS_GRID", &Tuning::corr_rs_grid},
+    {"KRCA_CORR_BATCH", &Tuning::corr_batch},
+    {"KRCA_CORR_AMB_TILE", &Tuning::corr_amb_tile},
 };
 Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20), env_int("KRCA_SCORE_NT", 1),
                  env_int("KRCA_PPR_GRID", 0),   env_int("KRCA_PPR_DICT", 1),     env_int("KRCA_LOG_IMPL", 0),
                  env_int("KRCA_GROUP_IMPL", 0),
-                 env_int("KRCA_CORR_DEBUG", 0), env_int("KRCA_CORR_RS_GRID", 1024)};
+                 env_int("KRCA_CORR_DEBUG", 0), env_int("KRCA_CORR_RS_GRID", 1024),
+                 env_int("KRCA_CORR_BATCH", 0),   env_int("KRCA_CORR_AMB_TILE", -1)};
 const NamedKnob* find_knob(const char* name) {
   if (!name) return nullptr;
   for (const NamedKnob& k : kKnobs)
@@ -49,14 +52,22 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
-hipStream_t side_stream() {
+hipStream_t side_stream(hipStream_t st) {
   // one per thread and device, never destroyed (a thread-exit destructor could run after the HIP
   // runtime's own teardown at process exit); the fork / join events order it, so the null stream
-  // is a correct (serialising) fallback
+  // is a correct (serialising) fallback.  Created on st's device, whatever device is current.
   static thread_local hipStream_t side[64] = {};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!side[dev] && hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess) side[dev] = nullptr;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (st && hipStreamGetDevice(st, &dev) != hipSuccess) return nullptr;
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!side[dev]) {
+    int cur = dev;
+    (void)hipGetDevice(&cur);
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess) side[dev] = nullptr;
+    if (cur != dev) (void)hipSetDevice(cur);
+  }
   return side[dev];
 }
 }  // namespace krca

@@ -59,10 +59,18 @@ constexpr int KMAX = 16;  // largest k served
 constexpr int NSB = 16;   // 128-pod column blocks in the threshold sample (2048 pods)
 constexpr int NSL = NSB + 2;  // sample lists per pod: NSB sample blocks + the pod's own 256-block
 constexpr int CAPC = 1024;    // candidate buffer per pod (main pass appends)
-// ambiguous |r| ~ tau pairs re-scored for exact counts: capacity of the list (int2 entries)
-// (C3's random-walk series put ~130 partners per pod within eps of tau = 0.5: ~13M pairs at 100k,
-// ~170 in every 256 x 256 tile)
-__host__ __device__ inline int64_t amb_cap(int64_t P) { return 256 * P + (1 << 20); }
+// Ambiguous |r| ~ tau pairs (screening value within eps of tau, not settled by the pair's own
+// bound) are re-scored in float64 for exact counts.  C3's random-walk series put ~130 partners per
+// pod within eps of tau = 0.5 (~170 in EVERY 256 x 256 tile, about half settled in the tile), so the
+// pairs scale with P^2: ~6.5M at 100k pods, ~6e8 at 1M.  The main pass therefore runs in batches of
+// SB super-tiles, each batch appending to one of two lists of a fixed capacity that the re-score
+// drains while the next batch runs; a tile that finds its batch's list full decides its ambiguous
+// pairs itself (float64 from z32, in the epilogue), so no valid tau ever fails.
+// (knobs KRCA_CORR_BATCH / KRCA_CORR_AMB_TILE, for tests: many batches, lists that fill early)
+inline int64_t sb_batch() { return krca::tuning().corr_batch > 0 ? krca::tuning().corr_batch : 2048; }
+inline int64_t amb_per_tile() {  // list budget per tile of a batch (C3 data: ~85 on average)
+  return krca::tuning().corr_amb_tile >= 0 ? krca::tuning().corr_amb_tile : 512;
+}
 constexpr int32_t AMB_BOTH = 1 << 30;  // entry.y flag: credit the partner's count as well
 // KC = candidates kept per (pod, sample block) in the sample pass: a template parameter >= k
 // (8, 12 or 16), so the k best sampled partners of a pod survive their blocks' cuts
@@ -176,6 +184,25 @@ struct Cand {
   __device__ __forceinline__ int32_t partner(int j) const { return c[j] < 0 ? -1 : c[j] >> 1; }
 };
 
+// float64 dot product of two fp32 rows by the 16 lanes of a group (sub = lane & 15; float4 loads
+// when the rows are 16-B aligned), reduced over the group: every lane gets the sum
+__device__ __forceinline__ double dot16_f64(const float* za, const float* zb, int T, int sub) {
+  double acc = 0.0;
+  if ((T & 3) == 0) {
+    const float4* va = reinterpret_cast<const float4*>(za);
+    const float4* vb = reinterpret_cast<const float4*>(zb);
+    for (int t = sub; t < T / 4; t += 16) {
+      const float4 x = va[t], y = vb[t];
+      acc += (double)x.x * (double)y.x + (double)x.y * (double)y.y + (double)x.z * (double)y.z +
+             (double)x.w * (double)y.w;
+    }
+  } else {
+    for (int t = sub; t < T; t += 16) acc += (double)za[t] * (double)zb[t];
+  }
+  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  return acc;
+}
+
 // Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh (TC = 256 in every pass):
 // 8 waves (2 row halves x 4 column quarters), each a 128 x 64 tile = 8 x 4 MFMA 16x16 blocks, K
 // steps of 64 through a double-buffered LDS stage (130 KB with the sample pass's parking area: one
@@ -254,10 +281,14 @@ struct TileArgs {
   int64_t n_rect;
   Shard sh;
   int debug;
-  int2* amb;
-  int32_t* amb_n;
+  int2* amb;                  // MAIN: this batch's ambiguous-pair list
+  unsigned long long* amb_n;  // MAIN: its fill (may pass amb_cap: the tiles past it decide in place)
+  int64_t amb_cap;
   float* ambv;
-  const float* dn;  // MAIN: fp16 rounding-error norm per pod (corr_dnorm)
+  const float* dn;   // MAIN: fp16 rounding-error norm per pod (corr_dnorm)
+  const float* z32;  // MAIN: fp32 rows for the in-tile re-score of a full list
+  int T;
+  int64_t st0, st_end;  // MAIN: this launch's batch [st0, st_end) of the rank's super-tiles
 };
 
 // One tile: row block I (256 pods), column block J (TC pods).  Main / rect passes: the epilogue takes
@@ -466,7 +497,8 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     constexpr bool HITS = MODE == MODE_MAIN;    // |r| > tau + eps counted in step 1 (first window)
     constexpr bool SETTLE = MODE == MODE_MAIN;  // pairs settled by their bound counted in step 2
     constexpr int CAPL = G::CAPL;
-    constexpr int RANKS = 1 << 13;  // ambiguous pairs ranked per tile (the rest: one global atomic each)
+    // an entry after classification: row | col << 8 | candidate bits << 16 | (ambiguous rank + 1) << 18
+    static_assert(G::NW * CAPL < (1 << 14) - 1, "ambiguous ranks of a window fit 14 bits");
     float* sphr = reinterpret_cast<float*>(smem);  // phi of the 256 row pods
     float* sphc = sphr + TB;                        // phi of the TC column pods
     int* srcnt = reinterpret_cast<int*>(sphc + TC);  // |r| > tau counts per row / column
@@ -475,7 +507,8 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     float* sdnr = reinterpret_cast<float*>(spod + TB);  // rounding-error norms of the rows / columns
     float* sdnc = sdnr + TB;
     int* wcount = reinterpret_cast<int*>(sdnc + TC);  // list length per wave
-    int* sflag = wcount + G::NW;  // [0] a list passed its window, [1] ranked ambiguous pairs, [2] their base
+    int* sflag = wcount + G::NW;  // [0] a list passed its window, [1] ranked ambiguous pairs
+    long long* sbase = reinterpret_cast<long long*>(sflag + 4);  // their base in the list (-1: decide here)
     int2* lists = reinterpret_cast<int2*>(smem + EPI_LIST_OFF);
     {
       if (rq < TB) {
@@ -526,13 +559,6 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         }
       }
       return tag;
-    };
-    auto amb_direct = [&](int gr, int gc, float v) {  // an ambiguous pair outside the tile's range
-      const int slot = atomicAdd(A.amb_n, 1);
-      if (slot < amb_cap(P)) {
-        A.amb[slot] = make_int2(gr, gc | (diag ? 0 : AMB_BOTH));
-        A.ambv[slot] = v;
-      }
     };
     // ---- 1. counts and raw lists (this window's CAPL slots per wave) --------------------------
     int2* wlist = lists + w * CAPL;
@@ -640,11 +666,9 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
           base = __shfl(base, leader, 64);
           rank = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mam >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mam, 0u));
         }
-        if ((tag & 4) && rank >= RANKS - 1) {  // past the tile's ranks: its own slot
-          amb_direct(RECT ? spod[row] : (int)(rowA + row), (int)(rowB + col), v);
-          tag &= ~4;
-        }
-        *ep = make_int2((ent.x & 0xffff) | ((tag & 7) << 16) | ((tag & 4) ? rank << 19 : 0), ent.y);
+        *ep = make_int2((int)(((uint32_t)ent.x & 0xffffu) | ((uint32_t)(tag & 3) << 16) |
+                              ((tag & 4) ? (uint32_t)(rank + 1) << 18 : 0u)),
+                        ent.y);
       }
       __syncthreads();
       // ---- 3. counts, the window's ambiguous range, entries out --------------------------------
@@ -654,15 +678,13 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       }
       // the ambiguous range's reservation, the candidates' slot reservations and the count adds are
       // all in flight together (the range first, then the candidates: 0.5 % slower main pass)
-      int abase_t = -1, atot = 0;
-      if (!RECT && tid == 0) {
-        atot = min(sflag[1], RANKS - 1);
-        if (atot) abase_t = atomicAdd(A.amb_n, atot);
-      }
+      long long abase_t = -1;
+      const int atot = RECT ? 0 : sflag[1];
+      if (!RECT && tid == 0 && atot) abase_t = (long long)atomicAdd(A.amb_n, (unsigned long long)atot);
       if (debug == 5) return false;
       for (int q = tid; q < ntot; q += G::NTH) {
         const int2 ent = *entry_at(q);
-        const int row = ent.x & 255, col = (ent.x >> 8) & 255, tag = (ent.x >> 16) & 7;
+        const int row = ent.x & 255, col = (ent.x >> 8) & 255, tag = (ent.x >> 16) & 3;
         const int gr = RECT ? spod[row] : (int)(rowA + row);
         const int gc = (int)(rowB + col);
         const int64_t lr = RECT ? gr - sh.lo : gr;  // rect: local buffers
@@ -671,17 +693,35 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         if (s1 < CAPC) A.buf[lr * CAPC + s1] = make_int2(ent.y, gc);
         if (s2 < CAPC) A.buf[(int64_t)gc * CAPC + s2] = make_int2(ent.y, gr);
       }
-      if (!RECT) {
-        if (tid == 0) sflag[2] = (atot && (int64_t)abase_t + atot <= amb_cap(P)) ? abase_t : -1;  // full: the host reports it
+      if (!RECT && atot) {  // block-uniform
+        if (tid == 0) *sbase = (abase_t >= 0 && abase_t + atot <= A.amb_cap) ? abase_t : -1;
         __syncthreads();
-        const int abase = sflag[2];
+        const long long abase = *sbase;
         if (abase >= 0) {
           for (int q = tid; q < ntot; q += G::NTH) {
             const int2 ent = *entry_at(q);
-            if ((ent.x >> 16) & 4) {
-              const int slot = abase + ((uint32_t)ent.x >> 19);
+            const uint32_t rk = (uint32_t)ent.x >> 18;
+            if (rk) {
+              const long long slot = abase + rk - 1;
               A.amb[slot] = make_int2((int)(rowA + (ent.x & 255)), (int)(rowB + ((ent.x >> 8) & 255)) | (diag ? 0 : AMB_BOTH));
               A.ambv[slot] = __int_as_float(ent.y);
+            }
+          }
+        } else {
+          // the batch's list is full (a tau inside the bulk of |r|): this tile's ambiguous pairs are
+          // decided here, 16 lanes per pair, float64 from the two fp32 rows (corr_amb_rescore's
+          // arithmetic)
+          const int sub = tid & 15;
+          for (int q0 = 0; q0 < ntot; q0 += G::NTH / 16) {
+            const int q = q0 + (tid >> 4);
+            const int2 ent = q < ntot ? *entry_at(q) : make_int2(0, 0);
+            if (q < ntot && ((uint32_t)ent.x >> 18) != 0) {  // uniform over the 16-lane group
+              const int64_t a = rowA + (ent.x & 255), b = rowB + ((ent.x >> 8) & 255);
+              const double acc = dot16_f64(A.z32 + a * A.T, A.z32 + b * A.T, A.T, sub);
+              if (sub == 0 && fabs(acc) > (double)A.tau) {
+                atomicAdd(&A.count[a], 1);
+                if (!diag) atomicAdd(&A.count[b], 1);
+              }
             }
           }
         }
@@ -823,7 +863,9 @@ __global__ __launch_bounds__(Geo<TC>::NTH) __attribute__((amdgpu_waves_per_eu(2)
     const int64_t L = L2 / SPLIT;
     const int part = (int)(L2 % SPLIT);
     const int64_t ns = (A.nb2 + SUPER - 1) / SUPER;
-    const int64_t st = (L / (SUPER * SUPER)) * A.sh.G + A.sh.g;  // this rank's super-tiles
+    const int64_t sl = A.st0 + L / (SUPER * SUPER);  // this batch's share of the rank's super-tiles
+    if (sl >= A.st_end) return;
+    const int64_t st = sl * A.sh.G + A.sh.g;
     if (st >= ns * (ns + 1) / 2) return;
     int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
     while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
@@ -924,12 +966,11 @@ __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32,
 // rows' rounding-error norms when that suffices, else re-scored (float4 loads of the pair's rows of
 // z32, float64 accumulation); persistent over the device-held list length
 __global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__ amb, const float* __restrict__ ambv,
-                                                        const int32_t* __restrict__ amb_n, int64_t P,
+                                                        const unsigned long long* __restrict__ amb_n, int64_t cap,
                                                         const float* __restrict__ z32, const float* __restrict__ dn,
                                                         int T, float tau, float acc_err, int32_t* __restrict__ count) {
   const int sub = threadIdx.x & 15;
-  const int64_t n = min((int64_t)*amb_n, amb_cap(P));
-  const bool vec = (T & 3) == 0;
+  const int64_t n = (int64_t)min(*amb_n, (unsigned long long)cap);  // entries past cap were decided in their tiles
   // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs; XCD x takes the contiguous
   // eighth [x n / 8, (x + 1) n / 8) of the list (which runs tile by tile), so the rows of a tile's
   // pairs are fetched into one L2
@@ -948,22 +989,7 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__
     } else if (v <= (double)tau - band) {
       hit = 0;
     } else {  // too close to call from the screening value: float64 from the rows
-      const float* za = z32 + a * T;
-      const float* zb = z32 + b * T;
-      double acc = 0.0;
-      if (vec) {
-        const float4* va = reinterpret_cast<const float4*>(za);
-        const float4* vb = reinterpret_cast<const float4*>(zb);
-        for (int t = sub; t < T / 4; t += 16) {
-          const float4 x = va[t], y = vb[t];
-          acc += (double)x.x * (double)y.x + (double)x.y * (double)y.y + (double)x.z * (double)y.z +
-                 (double)x.w * (double)y.w;
-        }
-      } else {
-        for (int t = sub; t < T; t += 16) acc += (double)za[t] * (double)zb[t];
-      }
-      for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
-      hit = fabs(acc) > (double)tau;
+      hit = fabs(dot16_f64(z32 + a * T, z32 + b * T, T, sub)) > (double)tau;
     }
     if (sub == 0 && hit) {
       atomicAdd(&count[a], 1);
@@ -1316,15 +1342,23 @@ struct CorrWs {  // views into a caller's candidate workspace
   float* run;           // [P][KMAX] running top-k |r| of the threshold sample
   int32_t* over;        // [n_loc + 1]
   int32_t* deep;        // [n_loc + 1]: pods for corr_merge_deep (count first)
-  int2* amb;            // [amb_cap(P)] ambiguous pairs of the main pass (contiguous per tile)
-  float* ambv;          // [amb_cap(P)] their screening values
+  int2* amb[2];         // [amb_cap] ambiguous pairs of a main-pass batch (contiguous per tile), two lists
+  float* ambv[2];       // [amb_cap] their screening values
+  int64_t amb_cap;
+  int nlist;            // lists in use (2 when the main pass runs in more than one batch)
   float* dn;            // [P] fp16 rounding-error norm of each row
-  int32_t* amb_n;       // [4]: their count (past the capacity: an error)
+  unsigned long long* amb_n;  // [2]: the lists' fill
   uint16_t* zs;         // [RECT_ROWS][Tp]
   int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
   int32_t* fill;        // sharded: [n_loc]
   unsigned long long* xc;  // sharded: tot[G] | off[G] | cursor[G]
 };
+
+// super-tiles of the upper triangle of nb2 256-blocks
+inline int64_t n_supertiles(int64_t nb2) {
+  const int64_t ns = (nb2 + SUPER - 1) / SUPER;
+  return ns * (ns + 1) / 2;
+}
 
 // layout in 4-byte words; sharded adds the local buffers and the exchange counters
 int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, CorrWs* ws) {
@@ -1344,10 +1378,16 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   w.phi2 = reinterpret_cast<float*>(take(P));
   w.over = reinterpret_cast<int32_t*>(take(n_loc + 1));
   w.deep = reinterpret_cast<int32_t*>(take(n_loc + 1));
-  w.amb = reinterpret_cast<int2*>(take(2 * amb_cap(P)));
-  w.ambv = reinterpret_cast<float*>(take(amb_cap(P)));
+  const int64_t n_st = n_supertiles(krca::ceil_div(P, TB));
+  const int64_t SB = sb_batch();
+  w.amb_cap = std::min(n_st, SB) * SUPER * SUPER * amb_per_tile();
+  w.nlist = n_st > SB ? 2 : 1;  // (a sharded rank runs a subset: at most as many batches)
+  for (int l = 0; l < 2; ++l) {
+    w.amb[l] = l < w.nlist ? reinterpret_cast<int2*>(take(2 * w.amb_cap)) : nullptr;
+    w.ambv[l] = l < w.nlist ? reinterpret_cast<float*>(take(w.amb_cap)) : nullptr;
+  }
   w.dn = reinterpret_cast<float*>(take(P));
-  w.amb_n = reinterpret_cast<int32_t*>(take(4));
+  w.amb_n = reinterpret_cast<unsigned long long*>(take(4));
   w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
   if (G > 0) {
     w.lbuf = reinterpret_cast<int2*>(take(2 * n_loc * CAPC));
@@ -1437,26 +1477,53 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   return KRCA_OK;
 }
 
-// exact |r| > tau counts of the listed ambiguous pairs (float64 from z32), added to count
-int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int32_t* count, hipStream_t st) {
+// exact |r| > tau counts of the ambiguous pairs in list l (float64 from z32), added to count
+int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int32_t* count, hipStream_t st) {
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   hipLaunchKernelGGL(corr_amb_rescore, dim3((unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7)), dim3(TPB), 0, st,
-                     (const int2*)ws.amb, (const float*)ws.ambv, (const int32_t*)ws.amb_n, d.P, z32,
-                     (const float*)ws.dn, d.T, d.tau, acc_err, count);
+                     (const int2*)ws.amb[l], (const float*)ws.ambv[l], (const unsigned long long*)(ws.amb_n + l),
+                     ws.amb_cap, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
 
-// 2. upper-triangle tiles (every G-th super-tile from g): appends into ws.buf, tau counts
+// Events of a fork from the caller's stream onto a side stream and the joins back; the destructor
+// joins every fork that was made and frees the events on every return path.
+struct SideWork {
+  hipStream_t st, side;
+  hipEvent_t ev[5] = {};  // 0, 1: batch b's list l filled (st); 2, 3: list l drained (side); 4: join
+  bool forked = false;
+  SideWork(hipStream_t s, hipStream_t sd) : st(s), side(sd) {}
+  int init() {
+    if (side == st) return KRCA_OK;
+    for (hipEvent_t& e : ev) KRCA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return KRCA_OK;
+  }
+  ~SideWork() {
+    if (side != st) {
+      if (forked && ev[4]) {
+        (void)hipEventRecord(ev[4], side);
+        (void)hipStreamWaitEvent(st, ev[4], 0);
+      }
+      for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    }
+  }
+};
+
+// 2. upper-triangle tiles (every G-th super-tile from g): appends into ws.buf, tau counts.  The
+//    main pass runs in batches of SB super-tiles; after batch b its ambiguous list (b & 1) is
+//    re-scored on `sw.side` (the caller's stream itself when no side stream is wanted) while batch
+//    b + 1 fills the other list.  count is final on sw.st once sw is destroyed (joined).
 template <int KC>
 int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int g, const float* phi, const CorrWs& ws,
-                int32_t* count, int dbg, hipStream_t st, bool rescore = true) {
+                int32_t* count, int dbg, SideWork& sw) {
+  hipStream_t st = sw.st;
   if (int rc = set_lds_attr<KC>()) return rc;
   KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
-  KRCA_HIP(hipMemsetAsync(ws.amb_n, 0, 4 * sizeof(int32_t), st));
-  const int64_t ns = (d.nb2 + SUPER - 1) / SUPER;
-  const int64_t n_st = ns * (ns + 1) / 2;
+  KRCA_HIP(hipMemsetAsync(ws.amb_n, 0, 2 * sizeof(unsigned long long), st));
+  const int64_t n_st = n_supertiles(d.nb2);
   const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
   if (n_mine == 0) return KRCA_OK;
   const Shard sh{0, G, g, 0};
@@ -1483,16 +1550,37 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.count = count;
   ta.sh = sh;
   ta.debug = dbg;
-  ta.amb = ws.amb;
-  ta.amb_n = ws.amb_n;
-  ta.ambv = ws.ambv;
+  ta.amb_cap = ws.amb_cap;
   ta.dn = ws.dn;
-  // main pass: 256 x 256 tiles, XCD-aware slots
-  ta.per_xcd = (n_mine * SUPER * SUPER + 7) / 8;
-  hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, 256>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<256>::NTH),
-                     Geo<256>::LDS_BYTES, st, ta);
-  KRCA_LAUNCH_CHECK();
-  if (dbg == 0 && rescore) return launch_rescore(z32, d, ws, count, st);
+  ta.z32 = z32;
+  ta.T = d.T;
+  const bool fork = sw.side != st;
+  const int64_t SB = sb_batch();
+  for (int64_t b = 0, s0 = 0; s0 < n_mine; ++b, s0 += SB) {
+    const int l = (int)(b & 1) % ws.nlist;
+    if (b >= 2 || (b >= 1 && ws.nlist == 1)) {  // list l was drained by the re-score of batch b - nlist
+      if (fork) KRCA_HIP(hipStreamWaitEvent(st, sw.ev[2 + l], 0));
+      KRCA_HIP(hipMemsetAsync(ws.amb_n + l, 0, sizeof(unsigned long long), st));
+    }
+    ta.amb = ws.amb[l];
+    ta.ambv = ws.ambv[l];
+    ta.amb_n = ws.amb_n + l;
+    ta.st0 = s0;
+    ta.st_end = std::min(n_mine, s0 + SB);
+    // 256 x 256 tiles, XCD-aware slots
+    ta.per_xcd = ((ta.st_end - s0) * SUPER * SUPER + 7) / 8;
+    hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, 256>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<256>::NTH),
+                       Geo<256>::LDS_BYTES, st, ta);
+    KRCA_LAUNCH_CHECK();
+    if (dbg != 0) continue;
+    if (fork) {
+      KRCA_HIP(hipEventRecord(sw.ev[l], st));
+      KRCA_HIP(hipStreamWaitEvent(sw.side, sw.ev[l], 0));
+      sw.forked = true;
+    }
+    if (int rc = launch_rescore(z32, d, ws, l, count, sw.side)) return rc;
+    if (fork) KRCA_HIP(hipEventRecord(sw.ev[2 + l], sw.side));
+  }
   return KRCA_OK;
 }
 
@@ -1511,16 +1599,9 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n), dim3(TPB), 0, st, (const int2*)lbuf, lcnt, phi, z32, d.P, d.T,
                      d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo, ws.deep);
   KRCA_LAUNCH_CHECK();
-  int32_t n_over = 0, n_amb[4] = {0, 0, 0, 0};
+  int32_t n_over = 0;
   KRCA_HIP(hipMemcpyAsync(&n_over, ws.over, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  KRCA_HIP(hipMemcpyAsync(n_amb, ws.amb_n, sizeof(n_amb), hipMemcpyDeviceToHost, st));
   KRCA_HIP(hipStreamSynchronize(st));
-  if (dbg == 0 && n_amb[0] > amb_cap(d.P)) {
-    krca::set_error("krca_corr: %d pairs have a screening |r| within eps = %.3g of tau = %g (capacity %lld): the "
-                    "|r| > tau counts cannot be made exact; use a tau farther from the bulk of |r|",
-                    n_amb[0], (double)d.eps, (double)d.tau, (long long)amb_cap(d.P));
-    return KRCA_EINVAL;
-  }
   auto deep_pass = [&]() -> int {  // pods whose merge left cert <= 0 (device-held list)
     hipLaunchKernelGGL(corr_merge_deep, dim3((unsigned)std::min<int64_t>(n, 2048)), dim3(TPB), 0, st,
                        (const int2*)lbuf, (const int32_t*)lcnt, phi, (const float*)ws.phi2, z32, d.T, d.k, d.eps,
@@ -1565,32 +1646,24 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
 }
 
 template <int KC>
-int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, float* phi_unused, int32_t* count,
-               int32_t* out_idx, float* out_val, float* cert, hipStream_t st) {
-  (void)phi_unused;
+int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, int32_t* count, int32_t* out_idx,
+               float* out_val, float* cert, hipStream_t st) {
   CorrWs ws;
   const int64_t head = ws_layout(d.P, d.Tp, KC, d.P, 0, cand, &ws);
   float* phi = reinterpret_cast<float*>(cand + 4 * head);  // one more [P] after the layout
   const int dbg = debug_mode();
+  // every launch below goes to st's device (the side stream is that device's)
+  krca::DeviceGuard dg(st);
+  if (int rc = dg.status()) return rc;
   if (int rc = stage_sample<KC>(zh, d, 0, d.P, ws, phi, st)) return rc;
-  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, st, /*rescore=*/false)) return rc;
-  if (dbg != 0) return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
-  // the exact-count re-score (memory-bound, writes count only) and the merge chain (sort, float64
+  // the exact-count re-scores (memory-bound, write count only) and the merge chain (sort, float64
   // top-k re-scoring, rectangle and deep passes: candidate buffers and outputs only) are
-  // independent: the re-score runs on a side stream forked from and joined back into st
-  hipStream_t side = krca::side_stream();
-  hipEvent_t fork, join;
-  KRCA_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-  KRCA_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-  KRCA_HIP(hipEventRecord(fork, st));
-  KRCA_HIP(hipStreamWaitEvent(side, fork, 0));
-  int rc = launch_rescore(z32, d, ws, count, side);
-  KRCA_HIP(hipEventRecord(join, side));
-  if (!rc) rc = stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
-  KRCA_HIP(hipStreamWaitEvent(st, join, 0));  // joined on every path: count is final on st
-  KRCA_HIP(hipEventDestroy(fork));
-  KRCA_HIP(hipEventDestroy(join));
-  return rc;
+  // independent: the re-scores run on a side stream forked from st per main-pass batch (the last
+  // one beside the merge chain) and joined back into st when sw goes out of scope
+  SideWork sw(st, dbg ? st : krca::side_stream(st));
+  if (int rc = sw.init()) return rc;
+  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, sw)) return rc;
+  return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
 }
 
 int kc_for(int32_t k) { return k <= 8 ? 8 : k <= 12 ? 12 : 16; }  // the smallest list size >= k
@@ -1636,9 +1709,9 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
   hipStream_t st = krca::as_stream(stream);
   char* c = reinterpret_cast<char*>(cand);
   switch (kc_for(k)) {
-    case 8: return run_single<8>(zh, z32, d, c, nullptr, count, out_idx, out_val, cert, st);
-    case 12: return run_single<12>(zh, z32, d, c, nullptr, count, out_idx, out_val, cert, st);
-    default: return run_single<16>(zh, z32, d, c, nullptr, count, out_idx, out_val, cert, st);
+    case 8: return run_single<8>(zh, z32, d, c, count, out_idx, out_val, cert, st);
+    case 12: return run_single<12>(zh, z32, d, c, count, out_idx, out_val, cert, st);
+    default: return run_single<16>(zh, z32, d, c, count, out_idx, out_val, cert, st);
   }
 }
 
@@ -1680,10 +1753,13 @@ int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32
                  "krca_corr_shard_tiles: bad args");
   const Dims d = dims_of(P, T, k, tau);
   int rc;
-  switch (kc_for(k)) {
-    case 8: rc = stage_tiles<8>(zh, z32, d, G, g, phi, w, count, 0, st); break;
-    case 12: rc = stage_tiles<12>(zh, z32, d, G, g, phi, w, count, 0, st); break;
-    default: rc = stage_tiles<16>(zh, z32, d, G, g, phi, w, count, 0, st);
+  {
+    SideWork sw(st, st);  // the counts are all-reduced next: re-scores in order on st
+    switch (kc_for(k)) {
+      case 8: rc = stage_tiles<8>(zh, z32, d, G, g, phi, w, count, 0, sw); break;
+      case 12: rc = stage_tiles<12>(zh, z32, d, G, g, phi, w, count, 0, sw); break;
+      default: rc = stage_tiles<16>(zh, z32, d, G, g, phi, w, count, 0, sw);
+    }
   }
   if (rc) return rc;
   KRCA_HIP(hipMemcpyAsync(raw_cnt, w.cnt, (size_t)P * sizeof(int32_t), hipMemcpyDeviceToDevice, st));

@@ -32,9 +32,47 @@ void set_error(const char* fmt, ...);
 #define KRCA_LAUNCH_CHECK() KRCA_HIP(hipGetLastError())
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
-// a non-blocking stream of the calling thread's current device for work a launcher forks off its
-// caller's stream (and joins back with events before returning); created once per thread and device
-hipStream_t side_stream();
+// a non-blocking stream on the device of `st` (the current device for the null stream) for work a
+// launcher forks off its caller's stream (and joins back with events before returning); created
+// once per thread and device
+hipStream_t side_stream(hipStream_t st);
+
+// makes the device of `st` current for the guard's lifetime (events and side streams are created
+// on the current device), restoring the caller's device afterwards
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(hipStream_t st) {
+    if (hipGetDevice(&prev_) != hipSuccess) {
+      rc_ = KRCA_EDEVICE;
+      return;
+    }
+    int dev = prev_;
+    if (st && hipStreamGetDevice(st, &dev) != hipSuccess) {
+      rc_ = KRCA_EDEVICE;
+      return;
+    }
+    if (dev != prev_) {
+      if (hipSetDevice(dev) != hipSuccess) {
+        rc_ = KRCA_EDEVICE;
+        return;
+      }
+      switched_ = true;
+    }
+  }
+  ~DeviceGuard() {
+    if (switched_) (void)hipSetDevice(prev_);
+  }
+  int status() const {
+    if (rc_) set_error("krca: cannot select the device of the caller's stream");
+    return rc_;
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = 0, rc_ = 0;
+  bool switched_ = false;
+};
 
 constexpr int kWave = 64;
 
@@ -56,6 +94,9 @@ struct Tuning {
   int group_impl;   // KRCA_GROUP_IMPL: 0 peeled atomics, 1 one atomic per lane
   int corr_debug;   // KRCA_CORR_DEBUG: profiling aid (results wrong when != 0)
   int corr_rs_grid; // KRCA_CORR_RS_GRID: workgroups of the ambiguous-pair re-score (a multiple of 8)
+  int corr_batch;   // KRCA_CORR_BATCH: super-tiles per main-pass batch (0 = 2048)
+  int corr_amb_tile;  // KRCA_CORR_AMB_TILE: ambiguous-list budget per tile of a batch (-1 = 512; 0 = every
+                      // tile decides its pairs in place)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

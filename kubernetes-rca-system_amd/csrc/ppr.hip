@@ -57,6 +57,7 @@ struct Ctl {          // device control block (header of the ctl buffer)
   int64_t q_total;    // sum of quantised seeds over all ranks
   int32_t converged;  // iteration count at convergence (0 = running)
   int32_t iter;       // iterations done
+  uint32_t done;      // single device, reduction fused: workgroups of the running step that finished
 };
 // ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n].  The long-row
 // accumulators and tickets are zero when allocated and reset by the last chunk of each row.
@@ -153,6 +154,39 @@ struct StepScalars {
   double tele, qtot, uni, alpha;
   int64_t qt;
 };
+
+// Single device (G = 1): the iteration's reduction runs in the step kernel's last workgroup
+// instead of a ppr_reduce launch (the exchange is a buffer swap, so nothing happens between them).
+struct Fuse {
+  int on;
+  double err_limit;
+  int64_t* w_next;  // the buffer the step gathered from = the next step's write target (slots zeroed)
+};
+
+// the reduction of ppr_reduce over ONE slice (G = 1), by a whole workgroup: residual / dangling
+// sums of `slice` (atomically updated by this step's workgroups), convergence, next teleport scale,
+// the next write target's slots zeroed; called by the step's last workgroup only
+__device__ void reduce_single(const int64_t* slice_slots, int64_t* next_slots, double alpha, double err_limit,
+                              Ctl* ctl, int64_t* red) {
+  const int tid = threadIdx.x;
+  int64_t e = 0, d = 0;
+  if (tid < NSPREAD) {
+    e = __hip_atomic_load(slice_slots + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    d = __hip_atomic_load(slice_slots + NSPREAD + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int64_t err = block_sum_i64(e, red);
+  const int64_t dang = block_sum_i64(d, red);
+  if (tid < NSLOT) next_slots[tid] = 0;
+  if (tid != 0) return;
+  ctl->done = 0;
+  if (ctl->converged) return;
+  ctl->iter += 1;
+  if (err_limit > 0.0 && (double)err < err_limit) {
+    ctl->converged = ctl->iter;
+    return;
+  }
+  ctl->tele = (1.0 - alpha) * krca::kFix + alpha * (double)dang;
+}
 
 // r_i <- pulled mass + teleport share; next w_i; residual and dangling contributions
 // (q_i, r_i, deg_i were loaded by the caller together with the row's edges).  flags: PPR_RESIDUAL
@@ -274,7 +308,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
     const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
-    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl) {
+    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz) {
   __shared__ uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
   __shared__ __attribute__((aligned(16))) uint8_t headrow[EDGE_BUDGET];  // at a row's first edge: its row
   __shared__ unsigned long long rowsum[ROW_BUDGET];
@@ -413,6 +447,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     add_slot(send + wslots(n_max), err);
     add_slot(send + wslots(n_max) + NSPREAD, dang);
   }
+  if (fz.on) {  // block-uniform
+    __shared__ int last;
+    if (tid == 0) {
+      __threadfence();  // this workgroup's slot adds are performed before its ticket
+      last = __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+      __threadfence();
+    }
+    __syncthreads();
+    if (last) reduce_single(send + wslots(n_max), fz.w_next + wslots(n_max), alpha, fz.err_limit, ctl, red);
+  }
 }
 
 // one block: sum the G*NSPREAD gathered slots of each quantity (integer -> order-free), decide
@@ -521,10 +565,36 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
   return KRCA_OK;
 }
 
+namespace {
+int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
+                const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
+                int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
+                void* stream);
+}
+
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
                         const uint16_t* lane, const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send,
                         void* ctl, void* stream) {
+  return launch_step(row_ptr, col, plan, plan_len, lane, w_all, outdeg, q_local, n_local, n_max, N, alpha, flags, r_local,
+                     send, ctl, Fuse{0, 0.0, nullptr}, stream);
+}
+
+int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
+                       const uint16_t* lane, int64_t* w, const int32_t* outdeg, const int64_t* q, int64_t N, double alpha,
+                       int32_t flags, double tol, int64_t* r, int64_t* send, void* ctl, void* stream) {
+  KRCA_CHECK_ARG(plan_len > 0 && N > 0, "krca_ppr_solo_step: bad sizes");
+  const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
+  return launch_step(row_ptr, col, plan, plan_len, lane, w, outdeg, q, N, N, N, alpha, flags, r, send, ctl,
+                     Fuse{1, err_limit, w}, stream);
+}
+}  // extern "C"
+
+namespace {
+int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
+                const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
+                int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
+                void* stream) {
   KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 4 == 0 && n_local >= 0 && n_local <= n_max && N > 0,
                  "krca_ppr_shard_step: bad sizes");
   if (plan_len == 0) return KRCA_OK;
@@ -547,10 +617,14 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
   auto kern = (flags & KRCA_PPR_RESIDUAL) ? ppr_step<PPR_RESIDUAL | PPR_WRITE_R>
                : (flags & KRCA_PPR_WRITE_R) ? ppr_step<PPR_WRITE_R> : ppr_step<0>;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, lane, nblk,
-                     reinterpret_cast<const uint32_t*>(w_all), outdeg, q_local, n_local, N, alpha, r_local, send, n_max, reinterpret_cast<Ctl*>(ctl));
+                     reinterpret_cast<const uint32_t*>(w_all), outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
+                     reinterpret_cast<Ctl*>(ctl), fz);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha, double tol,
                           int32_t first, void* ctl, int64_t* send_next, void* stream) {
@@ -618,11 +692,10 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   int cur = 0;  // w buffer the next step gathers from
   for (int it = 0; it < max_iter; ++it) {
     const int32_t flags = tol > 0.0 ? (KRCA_PPR_RESIDUAL | KRCA_PPR_WRITE_R) : (it + 1 == max_iter ? KRCA_PPR_WRITE_R : 0);
-    if ((rc = krca_ppr_shard_step(row_ptr, col, plan, plan_len, lane, wb[cur], outdeg, q, N, N, N, alpha, flags, r,
-                                  wb[cur ^ 1], ctl, stream)))
+    if ((rc = krca_ppr_solo_step(row_ptr, col, plan, plan_len, lane, wb[cur], outdeg, q, N, alpha, flags, tol, r,
+                                 wb[cur ^ 1], ctl, stream)))  // the iteration's reduction in its last workgroup
       return rc;
     cur ^= 1;
-    if ((rc = krca_ppr_shard_reduce(wb[cur], 1, N, N, alpha, tol, 0, ctl, wb[cur ^ 1], stream))) return rc;
     if (tol > 0.0 && (it + 1) % check_every == 0 && it + 1 < max_iter) {
       if ((rc = krca_ppr_ctl_read(ctl, &iters, &conv, stream))) return rc;
       if (conv) break;

@@ -157,6 +157,11 @@ class DeviceShard:
         self.w_all = torch.zeros((1 if world == 1 else world) * slice_words(n_max), **i64)
         self.ctl = torch.zeros(lib.krca_ppr_ctl_size(self.n), dtype=torch.uint8, device=dev)
         self.score_out = None
+        # one device: the iteration's reduction runs in the step kernel's last workgroup
+        # (krca_ppr_solo_step); reduce(first=0) is then a no-op.  Its tolerance is the one of the
+        # solve's first reduce(first=1).
+        self.fused = world == 1 and n_max == N
+        self._tol = 0.0
 
     def _chk(self, rc, what):
         from .native import _check
@@ -213,7 +218,12 @@ class DeviceShard:
     def step(self, alpha, flags=3):
         """flags: krca_ppr_shard_step's KRCA_PPR_RESIDUAL (1) | KRCA_PPR_WRITE_R (2)."""
         e, p = self.eng, self.eng.ptr
-        if self.plan_len:
+        if self.plan_len and self.fused:
+            self._chk(e.lib.krca_ppr_solo_step(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len, p(self.lane),
+                                               p(self.w_all), p(self.outdeg), p(self.q), self.N, float(alpha), int(flags),
+                                               float(self._tol), p(self.r), p(self.send), p(self.ctl), e._stream()),
+                      "krca_ppr_solo_step")
+        elif self.plan_len:
             self._chk(e.lib.krca_ppr_shard_step(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len,
                                                 p(self.lane), p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
                                                 float(alpha), int(flags), p(self.r), p(self.send), p(self.ctl),
@@ -221,6 +231,10 @@ class DeviceShard:
 
     def reduce(self, alpha, tol, first):
         e, p = self.eng, self.eng.ptr
+        if first:
+            self._tol = float(tol)
+        elif self.fused and self.plan_len:
+            return  # done by the step's last workgroup
         self._chk(e.lib.krca_ppr_shard_reduce(p(self.w_all), self.world, self.n_max, self.N, float(alpha), float(tol),
                                               int(first), p(self.ctl), p(self.send), e._stream()),
                   "krca_ppr_shard_reduce")

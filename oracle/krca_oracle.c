@@ -11,6 +11,10 @@
  *                       float64 sliding sums in a fixed order, |z| > thr <=> A^2 > thr^2*B
  *   krco_ppr            networkx 3.4.2 pagerank semantics (_pagerank_scipy) in 2^-60 fixed point
  *   krco_rca_key        root-cause ordering key (PageRank mass x own anomaly)
+ *   krco_corr_z32       the standardized fp32 rows krca_corr_prepare writes (float64 shifted sums
+ *                       for mean / scale, then (x - mean) * scale in float32): bit-exact twin
+ *   krco_corr_counts    |r| > tau counts over those rows with float64 dot products, and the pairs
+ *                       within a band of tau (where another float64 summation order may differ)
  *
  * The floating-point reference for a5/a10 (float64, independent formulation) is the NumPy
  * oracle in oracle/oracle.py; this file pins the exact bits.  Build: oracle/Makefile
@@ -160,5 +164,56 @@ void krco_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key) {
   for (int64_t i = 0; i < n; ++i) {
     const double v = (double)r[i] * (double)q[i];
     memcpy(&key[i], &v, sizeof(v));
+  }
+}
+
+/* corr_stats + corr_transpose of csrc/corr.hip (a9, new primitive): x time-major [T][P][M] */
+void krco_corr_z32(const float* x, int64_t P, int32_t M, int32_t T, int32_t ch, float* mean, float* scale,
+                   float* z32) {
+  const int64_t S = P * (int64_t)M;
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < P; ++p) {
+    const float* xs = x + p * M + ch;
+    const double x0 = (double)xs[0];
+    double s1 = 0.0, s2 = 0.0;
+    for (int32_t t = 0; t < T; ++t) {
+      const double d = (double)xs[(int64_t)t * S] - x0;
+      s1 += d;
+      s2 += d * d;
+    }
+    const double mu = s1 / T;
+    const double var = s2 / T - mu * mu;
+    const float mf = (float)(x0 + mu);
+    const float sc = var > 1e-20 ? (float)(1.0 / sqrt(var * (double)T)) : 0.f;
+    mean[p] = mf;
+    scale[p] = sc;
+    for (int32_t t = 0; t < T; ++t) {
+      const float v = xs[(int64_t)t * S] - mf;
+      z32[p * T + t] = v * sc;
+    }
+  }
+}
+
+/* for each row p of rows[]: count[i] = #{q != p : |sum_t z32[p,t] z32[q,t]| > tau} in float64
+ * (every product is exact in float64; the sum's rounding is <= T 2^-53 sum |products|), and
+ * band[i] = #{q != p : | |r| - tau | <= band_eps} (pairs a different summation order could flip) */
+void krco_corr_counts(const float* z32, int64_t P, int32_t T, const int64_t* rows, int64_t n_rows, double tau,
+                      double band_eps, int32_t* count, int32_t* band) {
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t i = 0; i < n_rows; ++i) {
+    const int64_t p = rows[i];
+    const float* za = z32 + p * T;
+    int32_t c = 0, b = 0;
+    for (int64_t q = 0; q < P; ++q) {
+      if (q == p) continue;
+      const float* zb = z32 + q * T;
+      double acc = 0.0;
+      for (int32_t t = 0; t < T; ++t) acc += (double)za[t] * (double)zb[t];
+      const double a = fabs(acc);
+      c += a > tau;
+      b += fabs(a - tau) <= band_eps;
+    }
+    count[i] = c;
+    band[i] = b;
   }
 }

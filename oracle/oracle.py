@@ -403,6 +403,8 @@ def c_lib():
     lib.krco_ppr_start.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp, ctypes.c_int]
     lib.krco_ppr_start.restype = i32
     lib.krco_rca_key.argtypes = [vp, vp, i64, vp]
+    lib.krco_corr_z32.argtypes = [vp, i64, i32, i32, i32, vp, vp, vp]
+    lib.krco_corr_counts.argtypes = [vp, i64, i32, vp, i64, f64, f64, vp, vp]
     _c = lib
     return lib
 
@@ -455,6 +457,31 @@ def c_ppr_warm(row_ptr, col, outdeg, seed, r_start, alpha, max_iter, tol, seed_f
     it = c_lib().krco_ppr_start(_p(rp), _p(cl), _p(od), N, _p(sd), seed_floor, alpha, max_iter, tol, _p(r), _p(rf),
                                 _p(q), 1)
     return r, it, q
+
+
+def c_corr_z32(x, channel=0):
+    """Bit-exact twin of krca_corr_prepare (csrc/corr.hip corr_stats + corr_transpose): x [T, P, M]
+    float32 -> (z32 [P, T] float32, mean [P], scale [P]).  The |r| > tau counts are defined on these
+    rows (float64 dot products), so they can be checked exactly (new primitive a9)."""
+    x = np.ascontiguousarray(x, np.float32)
+    T, P, M = x.shape
+    z = np.empty((P, T), np.float32)
+    mean = np.empty(P, np.float32)
+    scale = np.empty(P, np.float32)
+    c_lib().krco_corr_z32(_p(x), P, M, T, int(channel), _p(mean), _p(scale), _p(z))
+    return z, mean, scale
+
+
+def c_corr_counts(z32, rows, tau, band_eps=1e-12):
+    """-> (count [n], band [n]): exact |r| > tau counts of `rows` over the fp32 rows z32 (float64
+    sums), and the number of partners within band_eps of tau (float64 summation-order ties)."""
+    z = np.ascontiguousarray(z32, np.float32)
+    rows = np.ascontiguousarray(rows, np.int64)
+    cnt = np.zeros(len(rows), np.int32)
+    band = np.zeros(len(rows), np.int32)
+    c_lib().krco_corr_counts(_p(z), z.shape[0], z.shape[1], _p(rows), len(rows), float(tau), float(band_eps),
+                             _p(cnt), _p(band))
+    return cnt, band
 
 
 def c_rca_key(r, q):

@@ -114,3 +114,24 @@ def test_corr_oracle_matches_brute_force():
         o = np.lexsort((np.arange(300), -a[p]))
         assert idx[p].tolist() == o[:10].tolist()
         assert cnt[p] == (a[p] > 0.5).sum()
+
+
+def test_corr_z32_twin_and_exact_counts():
+    """krco_corr_z32 (the bit-exact twin of krca_corr_prepare) is the float64 standardisation
+    rounded to fp32; krco_corr_counts (sequential float64 sums) equals the BLAS float64 counts
+    outside the summation-order band."""
+    from krca import synth
+    x = synth.make_metrics(400, 2, 300, seed=6, group_size=10)
+    x[:, 9, 0] = 7.0
+    z32, mean, scale = oracle.c_corr_z32(x.numpy(), 0)
+    z = oracle.corr_standardize(x.numpy(), 0)
+    assert z32.dtype == np.float32 and np.all(z32[9] == 0) and scale[9] == 0
+    assert np.max(np.abs(z32 - z)) < 1e-6
+    rows = np.arange(0, 400, 3)
+    cnt, band = oracle.c_corr_counts(z32, rows, 0.5)
+    zd = z32.astype(np.float64)
+    a = np.abs(zd[rows] @ zd.T)
+    a[np.arange(len(rows)), rows] = 0
+    lo, hi = (a > 0.5 + 1e-12).sum(1), (a > 0.5 - 1e-12).sum(1)
+    assert np.all((cnt >= lo) & (cnt <= hi)) and np.array_equal(hi - lo >= band, np.ones(len(rows), bool))
+    assert np.array_equal(cnt[band == 0], lo[band == 0])

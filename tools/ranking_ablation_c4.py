@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Root-cause ranking definitions on the C4 mesh (1M pods / 20M edges, 8 metrics x 1440 steps) on
+the GPU, through the bench's own pieces (krca.rca.DeviceShard / RcaStep: the device scoring and
+the bit-exact fixed-point PageRank).  Recall@10 of the 10 planted roots for damping alpha, seed
+floor and ranking key (r = propagated mass, rq = mass x own anomaly = krca.rca.Config's key,
+q = own anomaly alone), plus the diagnostics that explain them: each root's score s (max |z| at the
+last step) and its rank among all pods, and how many pods pass each floor.  The "auto" floor is
+the expected maximum |z| of P*M null series, Phi^-1(1 - 1/(2 P M)).
+
+  python tools/ranking_ablation_c4.py [--pods 1000000] [--edges 20000000] [--seeds 2] --out F
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
+
+
+def auto_floor(n_series):
+    from scipy.special import ndtri
+    return float(ndtri(1.0 - 1.0 / (2.0 * n_series)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pods", type=int, default=1_000_000)
+    ap.add_argument("--edges", type=int, default=20_000_000)
+    ap.add_argument("--seeds", type=int, default=2)
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    import torch
+    from krca import native, synth
+    from krca.rca import RANKING, Comm, DeviceShard, RcaStep, shard_graph
+    eng = native.NativeEngine(0)
+    M, T = 8, 1440
+    af = auto_floor(a.pods * M)
+    floors = [0.0, 4.0, 5.0, round(af, 3), 6.0]
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in floors for key in ("r", "rq")] + [(None, None, "q")]
+    hits = {d: [] for d in defs}
+    diag = []
+    for seed in range(a.seeds):
+        t0 = time.time()
+        m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)
+        hops = synth.caller_hops(m, m.roots)
+        x = synth.make_metrics_range(0, a.pods, M, T, seed=seed, roots=m.roots, hop_sets=hops, device="cuda")
+        rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, a.pods)
+        sh = DeviceShard(eng, x, rp, col, od, a.pods, a.pods, 1, RANKING)
+        sh.score()
+        s = sh.score_out["score"].cpu().numpy()
+        roots = set(m.roots.tolist())
+        order = np.argsort(-s, kind="stable")
+        rank_of = np.empty(a.pods, np.int64)
+        rank_of[order] = np.arange(a.pods)
+        noise = np.ones(a.pods, bool)
+        noise[m.roots] = False
+        for h in hops:
+            noise[h] = False
+        diag.append(dict(seed=seed, root_scores=[float(s[r]) for r in m.roots], root_rank_by_s=[int(rank_of[r]) for r in m.roots],
+                         noise_max_s=float(s[noise].max()), pods_above={str(f): int((s > f).sum()) for f in floors},
+                         noise_above={str(f): int((s[noise] > f).sum()) for f in floors}))
+        for al, fl, key in defs:
+            if key == "q":
+                idx = order[:10]
+            else:
+                cfg = RANKING.replace(alpha=al, seed_floor=fl)
+                sh.cfg = cfg
+                st = RcaStep(sh, Comm(), cfg, 0)
+                st.propagate()
+                if key == "rq":
+                    idx, _ = st.merge(*sh.local_topk(10))
+                else:
+                    idx = torch.topk(sh.r[:a.pods], 10).indices.cpu().numpy()
+            hits[(al, fl, key)].append(len(roots & set(int(i) for i in idx)) / len(roots))
+        print(f"seed {seed}: {time.time() - t0:.0f}s; roots s={np.round(diag[-1]['root_scores'], 2).tolist()} "
+              f"rank_by_s={diag[-1]['root_rank_by_s']} noise_max_s={diag[-1]['noise_max_s']:.2f}", flush=True)
+        del x, sh
+        torch.cuda.empty_cache()
+    rows = [dict(alpha=al, seed_floor=fl, key=key, recall_at_10=float(np.mean(v)), per_seed=v)
+            for (al, fl, key), v in hits.items()]
+    out = dict(config=dict(vars(a), metrics=M, tsteps=T, window=RANKING.window, auto_floor=af), rows=rows,
+               diagnostics=diag)
+    txt = json.dumps(out, indent=1)
+    if a.out:
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        open(a.out, "w").write(txt + "\n")
+    for r in rows:
+        print(f"alpha={r['alpha']} floor={r['seed_floor']} key={r['key']:3s} recall@10={r['recall_at_10']:.2f} "
+              f"{r['per_seed']}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
