@@ -91,8 +91,12 @@ int krca_rolling_score_variant(int64_t P, int32_t M, int32_t T, int32_t W);
  *                   krca_log_index_size(nbytes) int64) and *n_lines (device int64).
  *   krca_log_match: (same workspace; it also keeps the first line id of every 256-byte chunk
  *                   there) per line start/end byte offsets and 13-bit mask; per container the line
- *                   count, the 13-bin histogram and the first three matching line ids per bin
- *                   (-1 when fewer) — atomics-free segmented reduction. */
+ *                   count and the 13-bin histogram — atomics-free segmented reduction.  The first
+ *                   three matching lines per bin (the reference's evidence, :159-163) are marked in
+ *                   the line masks: bit 16 + c of line_mask[l] is set iff line l is one of the first
+ *                   three lines of its container in category c (bits 0-12: the categories).
+ *                   examples (nullable) additionally receives them as a dense id table
+ *                   [D][13][3] (-1 when fewer). */
 /* The compiled matcher's identity: the Unicode version of the interpreter that generated the
  * tables (re.IGNORECASE folds, \d, str.splitlines separators; non-ASCII text matches the
  * reference exactly only under that version) and gen_log_dfa.pattern_digest of the 13 patterns
@@ -105,8 +109,19 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
 int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
                    int64_t* workspace, int64_t n_lines,
                    int64_t* line_start /*[L]*/, int64_t* line_end /*[L]*/, uint32_t* line_mask /*[L]*/,
-                   int32_t* doc_lines /*[D]*/, int32_t* hist /*[D][13]*/, int32_t* examples /*[D][13][3]*/,
+                   int32_t* doc_lines /*[D]*/, int32_t* hist /*[D][13]*/, int32_t* examples /*[D][13][3], nullable*/,
                    int64_t* doc_line0 /*[D], nullable: first line id of each container*/, void* stream);
+/* krca_log_scan: krca_log_index + krca_log_match in one call when the caller's line arrays hold
+ * line_cap lines (the same loop, ref:agents/logs_agent.py:140-151): the line index is built in ONE
+ * pass over the text (decoupled look-back for the line ids), the later kernels read the line count
+ * on the device, and the stream is synchronised once, at the end, for *n_lines_host.  When
+ * *n_lines_host > line_cap the outputs past the index are not valid: size the arrays and call
+ * krca_log_match with the same workspace (the index is kept there). */
+int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs,
+                  int64_t* workspace, int64_t line_cap,
+                  int64_t* line_start /*[line_cap]*/, int64_t* line_end /*[line_cap]*/, uint32_t* line_mask /*[line_cap]*/,
+                  int32_t* doc_lines /*[D]*/, int32_t* hist /*[D][13]*/, int32_t* examples /*[D][13][3], nullable*/,
+                  int64_t* doc_line0 /*[D], nullable*/, int64_t* n_lines_host, void* stream);
 
 /* ---- a13: error-template hashing + per-container template histograms (new primitive) ------
  * template(line) = line bytes with every maximal [A-Za-z0-9_] run that contains an ASCII digit or

@@ -508,7 +508,7 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     float* sdnc = sdnr + TB;
     int* wcount = reinterpret_cast<int*>(sdnc + TC);  // list length per wave
     int* sflag = wcount + G::NW;  // [0] a list passed its window, [1] ranked ambiguous pairs
-    long long* sbase = reinterpret_cast<long long*>(sflag + 4);  // their base in the list (-1: decide here)
+    long long* sbase = reinterpret_cast<long long*>(sflag + 4);  // their base in the list (slots past amb_cap: decided here)
     int2* lists = reinterpret_cast<int2*>(smem + EPI_LIST_OFF);
     {
       if (rq < TB) {
@@ -694,28 +694,33 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         if (s2 < CAPC) A.buf[(int64_t)gc * CAPC + s2] = make_int2(ent.y, gr);
       }
       if (!RECT && atot) {  // block-uniform
-        if (tid == 0) *sbase = (abase_t >= 0 && abase_t + atot <= A.amb_cap) ? abase_t : -1;
+        if (tid == 0) *sbase = abase_t;
         __syncthreads();
-        const long long abase = *sbase;
-        if (abase >= 0) {
+        // the list slots [abase, abase + atot) were reserved; those below amb_cap are written (the
+        // re-score kernel reads min(fill, amb_cap) entries, so every one of them must be), the rest
+        // -- a tile straddling the cap, or past it -- are decided here
+        const long long room = A.amb_cap - *sbase;  // entries of this tile that fit (may be <= 0)
+        if (room > 0) {
           for (int q = tid; q < ntot; q += G::NTH) {
             const int2 ent = *entry_at(q);
             const uint32_t rk = (uint32_t)ent.x >> 18;
-            if (rk) {
-              const long long slot = abase + rk - 1;
+            if (rk && (long long)rk <= room) {
+              const long long slot = *sbase + rk - 1;
               A.amb[slot] = make_int2((int)(rowA + (ent.x & 255)), (int)(rowB + ((ent.x >> 8) & 255)) | (diag ? 0 : AMB_BOTH));
               A.ambv[slot] = __int_as_float(ent.y);
             }
           }
-        } else {
-          // the batch's list is full (a tau inside the bulk of |r|): this tile's ambiguous pairs are
-          // decided here, 16 lanes per pair, float64 from the two fp32 rows (corr_amb_rescore's
-          // arithmetic)
+        }
+        if (room < atot) {
+          // the batch's list is full (a tau inside the bulk of |r|): this tile's ambiguous pairs past
+          // it are decided here, 16 lanes per pair, float64 from the two fp32 rows
+          // (corr_amb_rescore's arithmetic)
           const int sub = tid & 15;
           for (int q0 = 0; q0 < ntot; q0 += G::NTH / 16) {
             const int q = q0 + (tid >> 4);
             const int2 ent = q < ntot ? *entry_at(q) : make_int2(0, 0);
-            if (q < ntot && ((uint32_t)ent.x >> 18) != 0) {  // uniform over the 16-lane group
+            const uint32_t rk = (uint32_t)ent.x >> 18;
+            if (q < ntot && rk != 0 && (long long)rk > room) {  // uniform over the 16-lane group
               const int64_t a = rowA + (ent.x & 255), b = rowB + ((ent.x >> 8) & 255);
               const double acc = dot16_f64(A.z32 + a * A.T, A.z32 + b * A.T, A.T, sub);
               if (sub == 0 && fabs(acc) > (double)A.tau) {

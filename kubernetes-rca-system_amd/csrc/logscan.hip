@@ -625,14 +625,197 @@ __global__ __launch_bounds__(TPB) void log_lines(const uint8_t* __restrict__ tex
   }
 }
 
+// the line count a kernel works on: the host's L, or (fused scan, Ld != null) the device count when
+// it fits the caller's arrays (0 otherwise: the caller re-runs with larger arrays)
+__device__ __forceinline__ int64_t lines_of(int64_t L, const int64_t* Ld, int64_t cap) {
+  if (!Ld) return L;
+  const int64_t n = *Ld;
+  return n <= cap ? n : 0;
+}
+
 // the end of the last line: the text's end, minus a trailing separator
 __global__ void log_last_end(const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off,
-                             int64_t D, int64_t L, int64_t* __restrict__ line_end) {
+                             int64_t D, int64_t L, const int64_t* __restrict__ Ld, int64_t cap,
+                             int64_t* __restrict__ line_end) {
+  L = lines_of(L, Ld, cap);
   if (L == 0 || nbytes == 0) return;
   int64_t k = D - 1;
   while (k > 0 && doc_off[k] >= nbytes) --k;  // the last non-empty container
   const uint32_t b1 = text[nbytes - 1], b2 = nbytes >= 2 ? text[nbytes - 2] : 0u, b3 = nbytes >= 3 ? text[nbytes - 3] : 0u;
   line_end[L - 1] = nbytes - sep_len(b3, b2, b1, doc_off[k] == nbytes - 1);
+}
+
+// ---- log_index_lines: log_count + log_scan + log_lines in ONE pass over the text -------------
+// The text is read once: a workgroup keeps its tile's per-piece line-start masks and separator
+// lengths in registers while it finds the tile's first line id by a decoupled look-back over the
+// tiles before it (status word per tile: flag AGG = the tile's own total, INC = inclusive prefix;
+// tiles take their index from a ticket counter in start order, so every tile waited on has started
+// and never waits on a later one), then writes line_start / line_end from the registers.
+// Separator lengths as bit planes over the 16 positions of a piece (sep_len's cases): L0 = odd
+// lengths (1, 3), L1 = lengths 2 and 3.  Also writes chunk_cnt / tile bases / chunk_line0, so
+// krca_log_match can take over when the caller's line arrays are too small.
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t lb_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// high bits of sep_len's length-1 / length-2 / length-3 cases at the 4 positions of word w (given
+// the word before it), as 4-bit masks; cs4 = container first byte at p-1 for each position
+__device__ __forceinline__ void sep_planes(uint32_t wprev, uint32_t w, uint32_t cs4, uint32_t& l0, uint32_t& l1) {
+  const uint32_t B1 = __builtin_amdgcn_alignbit(w, wprev, 24);  // text[p-1] at byte k
+  const uint32_t B2 = __builtin_amdgcn_alignbit(w, wprev, 16);
+  const uint32_t nl = high_bits4(swar_eq(B1, 0x0A));
+  const uint32_t crlf = nl & high_bits4(swar_eq(B2, 0x0D)) & ~cs4;
+  uint32_t one = (nl & ~crlf) | high_bits4(swar_range(B1, 0x0B, 0x0D) | swar_range(B1, 0x1C, 0x1E));
+  uint32_t two = crlf;
+  if ((w | wprev) & 0x80808080u) {  // U+0085 (2 bytes), U+2028 / U+2029 (3 bytes)
+    const uint32_t B3 = __builtin_amdgcn_alignbit(w, wprev, 8);
+    two |= high_bits4(swar_eq(B2, 0xC2) & swar_eq(B1, 0x85));
+    const uint32_t three = high_bits4(swar_eq(B3, 0xE2) & swar_eq(B2, 0x80) & (swar_eq(B1, 0xA8) | swar_eq(B1, 0xA9)));
+    one |= three;
+    two |= three;
+  }
+  l0 = one;
+  l1 = two;
+}
+
+__global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                       const int64_t* __restrict__ doc_off, int64_t D,
+                                                       const int32_t* __restrict__ chunk_doc,
+                                                       int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_base,
+                                                       unsigned long long* __restrict__ status,
+                                                       unsigned int* __restrict__ ticket, int64_t ntiles, int64_t cap,
+                                                       int64_t* __restrict__ line_start, int64_t* __restrict__ line_end,
+                                                       int64_t* __restrict__ chunk_line0, int64_t* __restrict__ n_lines) {
+  constexpr int NIT = TILE / (TPB * PIECE);  // 16 passes of 4 KiB
+  __shared__ int32_t s_cnt[TPB];
+  __shared__ int64_t s_base[TPB];
+  __shared__ int64_t s_wsum[TPB / 64];
+  __shared__ uint32_t s_cs[NBW];
+  __shared__ int64_t s_tile, s_excl;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+  s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t tile0 = tile * TILE;
+  tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
+  uint32_t SL[NIT];  // line starts (low half) | odd separator lengths (high half), per piece
+  uint32_t L1[NIT];  // separator lengths 2 and 3
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (q < nbytes) {  // an aligned 16-byte block holding a text byte never crosses the last page
+      const uint4 v = *reinterpret_cast<const uint4*>(text + q);
+      w[0] = v.x;
+      w[1] = v.y;
+      w[2] = v.z;
+      w[3] = v.w;
+    }
+    uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
+    if (lane == 0) wp = q >= 4 && q <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q - 4) : 0u;
+    uint32_t S = high_bits4(sep_flags(wp, w[0])) | (high_bits4(sep_flags(w[0], w[1])) << 4) |
+                 (high_bits4(sep_flags(w[1], w[2])) << 8) | (high_bits4(sep_flags(w[2], w[3])) << 12);
+    uint32_t C = 0;  // container first bytes at q-1+j, j = 0..16 (non-empty containers only)
+    if (q < nbytes) {
+      C = piece_container_starts(s_cs, tile0, q);
+      S |= C >> 1;
+      if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
+    } else {
+      S = 0;
+    }
+    uint32_t a0, b0, a1, b1, a2, b2, a3, b3;
+    sep_planes(wp, w[0], C & 0xFu, a0, b0);
+    sep_planes(w[0], w[1], (C >> 4) & 0xFu, a1, b1);
+    sep_planes(w[1], w[2], (C >> 8) & 0xFu, a2, b2);
+    sep_planes(w[2], w[3], (C >> 12) & 0xFu, a3, b3);
+    const uint32_t l0 = a0 | (a1 << 4) | (a2 << 8) | (a3 << 12), l1 = b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
+    SL[it] = S | ((l0 & S) << 16);
+    L1[it] = l1 & S;
+    uint32_t c = __popc(S);
+#pragma unroll
+    for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
+    if ((threadIdx.x & (LANES_PER_CHUNK - 1)) == 0)
+      s_cnt[it * (TPB / LANES_PER_CHUNK) + threadIdx.x / LANES_PER_CHUNK] = (int32_t)c;
+  }
+  __syncthreads();
+  // chunk counts, their scan inside the tile, the tile total
+  const int64_t v = s_cnt[threadIdx.x];
+  chunk_cnt[tile * TPB + threadIdx.x] = (int32_t)v;
+  int64_t x = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = (int64_t)__shfl_up((long long)x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wid] = x;
+  __syncthreads();
+  int64_t before = x - v;
+  for (int u = 0; u < wid; ++u) before += s_wsum[u];
+  const int64_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  // decoupled look-back (wave 0): the tile's first line id
+  if (wid == 0) {
+    int64_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], LB_INC | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[tile], LB_AGG | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int64_t top = tile - 1;; top -= 64) {
+        const int64_t t = top - lane;  // lane 0 = the nearest predecessor of the window
+        uint64_t s = t >= 0 ? lb_load(&status[t]) : LB_INC;
+        while (__any((s >> 62) == 0)) {  // some predecessor has not published yet
+          __builtin_amdgcn_s_sleep(1);
+          if ((s >> 62) == 0) s = lb_load(&status[t]);
+        }
+        const uint64_t inc = __ballot((s >> 62) == 2);
+        const int first = inc ? __builtin_ctzll(inc) : 64;  // nearest inclusive prefix (lowest lane)
+        int64_t val = (lane <= first && t >= 0) ? (int64_t)(s & LB_VAL) : 0;
+        for (int off = 32; off > 0; off >>= 1) val += (int64_t)__shfl_xor((long long)val, off, 64);
+        excl += val;
+        if (inc) break;
+      }
+      if (lane == 0) __hip_atomic_store(&status[tile], LB_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  const int64_t excl = s_excl;
+  if (threadIdx.x == 0) {
+    tile_base[tile] = excl;
+    if (tile == ntiles - 1) {
+      tile_base[ntiles] = excl + total;
+      *n_lines = excl + total;
+    }
+  }
+  s_base[threadIdx.x] = excl + before;
+  chunk_line0[tile * TPB + threadIdx.x] = excl + before;
+  __syncthreads();
+  // line starts and the previous line's end, from the registers
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
+    const uint32_t S = SL[it] & 0xFFFFu;
+    const uint32_t n = __popc(S);
+    uint32_t xs = n;
+#pragma unroll
+    for (int off = 1; off < LANES_PER_CHUNK; off <<= 1) {
+      const uint32_t y = __shfl_up(xs, off, 64);
+      if ((lane & (LANES_PER_CHUNK - 1)) >= off) xs += y;
+    }
+    int64_t id = s_base[it * (TPB / LANES_PER_CHUNK) + threadIdx.x / LANES_PER_CHUNK] + (xs - n);
+    uint32_t rem = S;
+    const uint32_t l0 = SL[it] >> 16, l1 = L1[it];
+    while (rem) {
+      const int k = __ffs(rem) - 1;
+      rem &= rem - 1;
+      const int64_t pos = q + k;
+      const int sl = (int)((l0 >> k) & 1u) | (int)(((l1 >> k) & 1u) << 1);
+      if (id < cap) line_start[id] = pos;
+      if (id >= 1 && id - 1 < cap) line_end[id - 1] = pos - sl;
+      ++id;
+    }
+  }
 }
 
 // LDS form of the transition table for log_dfa / log_dfa_long: an entry holds the target state's
@@ -756,11 +939,13 @@ __device__ __forceinline__ uint32_t word_in_line(int j, uint32_t lo4, uint32_t h
 }
 
 __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
+                                                   const int64_t* __restrict__ Ld, int64_t cap,
                                                    const int64_t* __restrict__ line_start,
                                                    const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
                                                    int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
   __shared__ DfaLds4 d;
   dfa4_load(d);
+  L = lines_of(L, Ld, cap);
   for (int64_t l0 = (int64_t)blockIdx.x * DFA_TPB; l0 < L; l0 += (int64_t)gridDim.x * DFA_TPB) {
     // buffer resource at the group's first line: offsets stay 32-bit (the group's short lines
     // span < 1 MiB), reads past the text return 0 and never fault
@@ -964,16 +1149,26 @@ __device__ __forceinline__ int64_t first_line_at(const int64_t* __restrict__ lin
   return lo;
 }
 
+// Example lines as bits: bit 16 + c of line_mask[l] is set when line l is one of the first three
+// lines of its container in category c (the reference's evidence, ref:agents/logs_agent.py:159-163),
+// so the examples cost no more than the masks they sit beside (a dense [D][13][3] id table is 156 B
+// per container: 2/3 of the scan's writes at C5).  DENSE also writes that table (A/B, compat).
+constexpr uint32_t CAT_BITS = (1u << KRCA_NCAT) - 1u;
+constexpr int EX_SHIFT = 16;
+static_assert(EX_SHIFT + KRCA_NCAT <= 32, "example bits must fit the line mask");
+
+template <bool DENSE>
 __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_off, int64_t D,
                                                 const int64_t* __restrict__ chunk_line0, int64_t nchunks,
                                                 const int64_t* __restrict__ line_start,
-                                                const uint32_t* __restrict__ line_mask, int64_t L,
+                                                uint32_t* __restrict__ line_mask, int64_t L,
+                                                const int64_t* __restrict__ Ld, int64_t cap,
                                                 int32_t* __restrict__ doc_lines, int32_t* __restrict__ hist,
                                                 int32_t* __restrict__ examples, int64_t* __restrict__ doc_line0) {
-  // the block's examples, then its histograms, are assembled in one LDS buffer and leave in
-  // coalesced rows (a lane writing its own 52 ints at a 208-byte stride touched ~26 lines per store
-  // instruction); one 39 KB buffer instead of two (52 KB) keeps 4 workgroups per CU, not 3
-  __shared__ int32_t s_ex[TPB * KRCA_NCAT * 3];
+  // the block's histograms (and dense examples) are assembled in LDS and leave in coalesced rows (a
+  // lane writing its own 52 ints at a 208-byte stride touched ~26 lines per store instruction)
+  __shared__ int32_t s_ex[TPB * KRCA_NCAT * (DENSE ? 3 : 1)];
+  L = lines_of(L, Ld, cap);
   int32_t mycnt[KRCA_NCAT];  // this lane's container histogram (small or big path)
 #pragma unroll
   for (int c = 0; c < KRCA_NCAT; ++c) mycnt[c] = 0;
@@ -992,57 +1187,71 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
       cnt[c] = 0;
       ex[c][0] = ex[c][1] = ex[c][2] = -1;
     }
+    uint32_t full = 0;  // bins holding three examples already
     for (int64_t l = lo; l < hi; ++l) {
-      const uint32_t m = line_mask[l];
+      const uint32_t m = line_mask[l] & CAT_BITS;
+      const uint32_t exb = m & ~full;
+      if (exb) line_mask[l] = m | (exb << EX_SHIFT);
 #pragma unroll
       for (int c = 0; c < KRCA_NCAT; ++c) {
         if ((m >> c) & 1u) {
           const int f = cnt[c];
-          if (f == 0) ex[c][0] = (int32_t)l;
-          if (f == 1) ex[c][1] = (int32_t)l;
-          if (f == 2) ex[c][2] = (int32_t)l;
+          if (DENSE) {
+            if (f == 0) ex[c][0] = (int32_t)l;
+            if (f == 1) ex[c][1] = (int32_t)l;
+            if (f == 2) ex[c][2] = (int32_t)l;
+          }
+          if (f == 2) full |= 1u << c;
           cnt[c] = f + 1;
         }
       }
     }
     doc_lines[d] = (int32_t)(hi - lo);
     if (doc_line0) doc_line0[d] = lo;
-    int32_t* ed = s_ex + threadIdx.x * KRCA_NCAT * 3;
 #pragma unroll
-    for (int c = 0; c < KRCA_NCAT; ++c) {
-      mycnt[c] = cnt[c];
-      ed[c * 3] = ex[c][0];
-      ed[c * 3 + 1] = ex[c][1];
-      ed[c * 3 + 2] = ex[c][2];
+    for (int c = 0; c < KRCA_NCAT; ++c) mycnt[c] = cnt[c];
+    if (DENSE) {
+      int32_t* ed = s_ex + threadIdx.x * KRCA_NCAT * 3;
+#pragma unroll
+      for (int c = 0; c < KRCA_NCAT; ++c) {
+        ed[c * 3] = ex[c][0];
+        ed[c * 3 + 1] = ex[c][1];
+        ed[c * 3 + 2] = ex[c][2];
+      }
     }
   }
   uint64_t big = __ballot(valid && !small);
+  const uint64_t below = (1ull << lane) - 1ull;  // lanes before this one
   while (big) {  // wave-uniform: the wave takes the large containers one at a time
     const int j = __ffsll((unsigned long long)big) - 1;
     big &= big - 1;
     const int64_t dj = d - lane + j;
     const int64_t blo = __shfl(lo, j, 64), bhi = __shfl(hi, j, 64);
     int32_t cnt[KRCA_NCAT];
-    int32_t found[KRCA_NCAT];
 #pragma unroll
-    for (int c = 0; c < KRCA_NCAT; ++c) {
-      cnt[c] = 0;
-      found[c] = 0;
-    }
+    for (int c = 0; c < KRCA_NCAT; ++c) cnt[c] = 0;
     int32_t* ex = s_ex + (threadIdx.x - lane + j) * KRCA_NCAT * 3;
     for (int64_t b = blo; b < bhi; b += 64) {
-      const uint32_t m = (b + lane < bhi) ? line_mask[b + lane] : 0u;
+      const bool in = b + lane < bhi;
+      const uint32_t m = in ? (line_mask[b + lane] & CAT_BITS) : 0u;
+      uint32_t exb = 0;
 #pragma unroll
       for (int c = 0; c < KRCA_NCAT; ++c) {
-        uint64_t bal = __ballot((m >> c) & 1u);
-        cnt[c] += __popcll(bal);
-        while (found[c] < 3 && bal) {
-          const int q = __ffsll((unsigned long long)bal) - 1;
-          if (lane == 0) ex[c * 3 + found[c]] = (int32_t)(b + q);
-          ++found[c];
-          bal &= bal - 1;
+        const uint64_t bal = __ballot((m >> c) & 1u);
+        const int f = cnt[c];  // wave-uniform
+        // this line is an example of bin c when fewer than three came before it in the container
+        if (((m >> c) & 1u) && f + __popcll(bal & below) < 3) exb |= 1u << c;
+        if (DENSE && f < 3) {
+          uint64_t bb = bal;
+          for (int k = f; k < 3 && bb; ++k) {
+            const int q = __ffsll((unsigned long long)bb) - 1;
+            if (lane == 0) ex[c * 3 + k] = (int32_t)(b + q);
+            bb &= bb - 1;
+          }
         }
+        cnt[c] = f + __popcll(bal);
       }
+      if (exb) line_mask[b + lane] = m | (exb << EX_SHIFT);
     }
     if (lane == j) {  // counts are wave-uniform (ballots): the container's own lane keeps them
 #pragma unroll
@@ -1051,14 +1260,18 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
     if (lane == 0) {
       doc_lines[dj] = (int32_t)(bhi - blo);
       if (doc_line0) doc_line0[dj] = blo;
+      if (DENSE) {
 #pragma unroll
-      for (int c = 0; c < KRCA_NCAT; ++c)
-        for (int k = found[c]; k < 3; ++k) ex[c * 3 + k] = -1;
+        for (int c = 0; c < KRCA_NCAT; ++c)
+          for (int k = cnt[c] < 3 ? cnt[c] : 3; k < 3; ++k) ex[c * 3 + k] = -1;
+      }
     }
   }
-  __syncthreads();
   const int nv = (int)(D - d0 < TPB ? D - d0 : TPB);
-  for (int i = threadIdx.x; i < nv * KRCA_NCAT * 3; i += TPB) examples[d0 * KRCA_NCAT * 3 + i] = s_ex[i];
+  if (DENSE) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nv * KRCA_NCAT * 3; i += TPB) examples[d0 * KRCA_NCAT * 3 + i] = s_ex[i];
+  }
   __syncthreads();  // the buffer now takes the histograms
 #pragma unroll
   for (int c = 0; c < KRCA_NCAT; ++c) s_ex[threadIdx.x * KRCA_NCAT + c] = mycnt[c];
@@ -1074,13 +1287,15 @@ extern "C" {
 
 // workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts |
 // [ntiles*TPB] int32 chunk -> container | [ntiles*TPB] int64 first line id per chunk |
-// [1] long-line count | int32 long-line queue [nbytes / LONG_LINE + 1]
+// [1] long-line count | int32 long-line queue [nbytes / LONG_LINE + 1] | [ntiles] look-back status |
+// [1] tile ticket (the last two: krca_log_scan)
 const char* krca_log_dfa_unicode(void) { return KRCA_DFA_UNIDATA; }
 uint64_t krca_log_dfa_digest(void) { return KRCA_DFA_DIGEST; }
 
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
-  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2);
+  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2) +
+         nt + 1;  // + krca_log_scan's look-back status words and tile ticket
 }
 
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
@@ -1111,7 +1326,7 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
                    int64_t n_lines, int64_t* line_start, int64_t* line_end, uint32_t* line_mask, int32_t* doc_lines,
                    int32_t* hist, int32_t* examples, int64_t* doc_line0, void* stream) {
   KRCA_CHECK_ARG(nbytes >= 0 && ndocs >= 1 && n_lines >= 0, "krca_log_match: bad sizes");
-  KRCA_CHECK_ARG(doc_off && ws && doc_lines && hist && examples, "krca_log_match: null pointer");
+  KRCA_CHECK_ARG(doc_off && ws && doc_lines && hist, "krca_log_match: null pointer");
   KRCA_CHECK_ARG(((uintptr_t)text & 15) == 0, "krca_log_match: text must be 16-byte aligned");
   KRCA_CHECK_ARG(n_lines == 0 || (line_start && line_end && line_mask), "krca_log_match: null line arrays");
   const int64_t nt = num_tiles(nbytes);
@@ -1134,7 +1349,8 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
     hipLaunchKernelGGL(log_lines, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs, cdoc, chunk, tile,
                        n_lines, line_start, line_end, chunk_line0);
     KRCA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, n_lines, line_end);
+    hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, n_lines,
+                       (const int64_t*)nullptr, (int64_t)0, line_end);
     KRCA_LAUNCH_CHECK();
     if (impl == 2) {  // A/B: the round-1 walk (16-byte window, code point per step)
       const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, DFA_TPB), 256 * 4);
@@ -1143,7 +1359,7 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
     } else {  // persistent: the 50 KB table is filled once per workgroup, 3 workgroups per CU
       const int64_t grid = std::min<int64_t>(krca::ceil_div(n_lines, DFA_TPB), 256 * 3);
       hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, n_lines,
-                         (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+                         (const int64_t*)nullptr, (int64_t)0, (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
     }
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,
@@ -1152,10 +1368,59 @@ int krca_log_match(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   } else {  // no lines: chunk_line0 = 0 for log_hist
     KRCA_HIP(hipMemsetAsync(chunk_line0, 0, nt * TPB * sizeof(int64_t), st));
   }
-  hipLaunchKernelGGL(log_hist, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
-                     (const int64_t*)chunk_line0, nt * TPB, line_start, line_mask, n_lines, doc_lines, hist, examples,
-                     doc_line0);
+  hipLaunchKernelGGL(examples ? log_hist<true> : log_hist<false>, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB),
+                     0, st, doc_off, ndocs, (const int64_t*)chunk_line0, nt * TPB, line_start, line_mask, n_lines,
+                     (const int64_t*)nullptr, (int64_t)0, doc_lines, hist, examples, doc_line0);
   KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
+                  int64_t line_cap, int64_t* line_start, int64_t* line_end, uint32_t* line_mask, int32_t* doc_lines,
+                  int32_t* hist, int32_t* examples, int64_t* doc_line0, int64_t* n_lines_host, void* stream) {
+  KRCA_CHECK_ARG(nbytes >= 0 && ndocs >= 1 && ndocs < INT32_MAX && line_cap >= 0, "krca_log_scan: bad sizes");
+  KRCA_CHECK_ARG(doc_off && ws && doc_lines && hist && n_lines_host, "krca_log_scan: null pointer");
+  KRCA_CHECK_ARG(nbytes == 0 || text, "krca_log_scan: null text");
+  KRCA_CHECK_ARG(((uintptr_t)text & 15) == 0, "krca_log_scan: text must be 16-byte aligned");
+  KRCA_CHECK_ARG(line_cap == 0 || (line_start && line_end && line_mask), "krca_log_scan: null line arrays");
+  const int64_t nt = num_tiles(nbytes);
+  int64_t* tile = ws;  // tile[nt] = the line count, on the device
+  int32_t* chunk = reinterpret_cast<int32_t*>(ws + nt + 1);
+  int32_t* cdoc = chunk + 2 * krca::ceil_div(nt * TPB, 2);
+  int64_t* chunk_line0 = ws + (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2;
+  int32_t* n_long = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB);
+  int32_t* long_q = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB + 1);
+  unsigned long long* status =
+      reinterpret_cast<unsigned long long*>(chunk_line0 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2));
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(status + nt);
+  hipStream_t st = krca::as_stream(stream);
+  KRCA_HIP(hipMemsetAsync(cdoc, 0, nt * TPB * sizeof(int32_t), st));  // defined map even off-contract
+  KRCA_HIP(hipMemsetAsync(status, 0, (nt + 1) * sizeof(unsigned long long), st));
+  KRCA_HIP(hipMemsetAsync(n_long, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
+                     nbytes, cdoc);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(log_index_lines, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
+                     (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
+                     tile + nt);
+  KRCA_LAUNCH_CHECK();
+  const int64_t* Ld = tile + nt;
+  hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, (int64_t)0, Ld, line_cap,
+                     line_end);
+  KRCA_LAUNCH_CHECK();
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, DFA_TPB), 256 * 3));
+  hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0, Ld, line_cap,
+                     (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,
+                     (const int64_t*)line_end, line_mask, (const int32_t*)long_q, (const int32_t*)n_long);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(examples ? log_hist<true> : log_hist<false>, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB),
+                     0, st, doc_off, ndocs, (const int64_t*)chunk_line0, nt * TPB, line_start, line_mask, (int64_t)0, Ld,
+                     line_cap, doc_lines, hist, examples, doc_line0);
+  KRCA_LAUNCH_CHECK();
+  KRCA_HIP(hipMemcpyAsync(n_lines_host, Ld, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  KRCA_HIP(hipStreamSynchronize(st));
   return KRCA_OK;
 }
 

@@ -37,6 +37,8 @@ SIGNATURES = {
     "krca_log_index": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "krca_log_match": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),
+    "krca_log_scan": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                              c_vp, c_vp]),
     "krca_template_hash": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "krca_template_hist_ws_size": (c_i64, [c_i64]),
     "krca_template_hist": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -167,6 +169,27 @@ def check_doc_off(doc_off, nbytes):
         raise KrcaError("log scan: doc_off must be non-decreasing from 0 to len(text)")
 
 
+def example_ids(line_mask, doc_line0, doc_lines):
+    """[D, 13, 3] ids of the first three lines per container and category (-1 when fewer) from the
+    example bits of the line masks (bit 16 + c, include/krca.h krca_log_match); host numpy."""
+    lm = np.asarray(line_mask).view(np.uint32)
+    D = len(doc_lines)
+    out = np.full((D, NCAT, 3), -1, np.int32)
+    lines = np.flatnonzero(lm >> 16)
+    if len(lines) == 0:
+        return out
+    doc = np.searchsorted(np.asarray(doc_line0, np.int64), lines, side="right") - 1
+    for c in range(NCAT):
+        sel = ((lm[lines] >> (16 + c)) & 1).astype(bool)
+        li, d = lines[sel], doc[sel]
+        if len(li) == 0:
+            continue
+        _, first, inv = np.unique(d, return_index=True, return_inverse=True)
+        k = np.arange(len(li)) - first[inv]  # lines ascend inside a container
+        out[d, c, k] = li
+    return out
+
+
 class LogScan:
     """Device results of krca_log_match for D containers (host copies)."""
 
@@ -199,6 +222,7 @@ class NativeEngine:
         self.lib = load_library()
         self.device = torch.device("cuda", device)
         self._ws = {}
+        self._log_cap = 0  # line capacity of krca_log_scan's arrays: the last scan's lines + 25 %
 
     # -- helpers ---------------------------------------------------------------------------
     def _stream(self):
@@ -420,10 +444,12 @@ class NativeEngine:
                             f"{unicodedata.unidata_version}: regenerate csrc/log_dfa_tables.h "
                             f"(csrc/gen_log_dfa.py) for non-ASCII logs")
 
-    def log_scan_device(self, text, doc_off, validate=True):
+    def log_scan_device(self, text, doc_off, validate=True, dense_examples=False):
         """text uint8 device tensor (16-byte aligned), doc_off int64 device tensor [D+1].
         validate: check the doc_off contract on the device first (one stream sync); pass False only
-        when the offsets were checked on the host (check_doc_off) before the upload."""
+        when the offsets were checked on the host (check_doc_off) before the upload.
+        The example lines are marked in line_mask (bits 16-28, include/krca.h; example_ids() turns
+        them into the [D, 13, 3] id table); dense_examples also has the device write that table."""
         torch = self.torch
         nbytes = text.numel()
         D = doc_off.numel() - 1
@@ -433,23 +459,43 @@ class NativeEngine:
             if not ok:
                 raise KrcaError("log scan: doc_off must be non-decreasing from 0 to len(text)")
         ws = self._workspace("logidx", 8 * self.lib.krca_log_index_size(nbytes))
-        nl = torch.zeros(1, dtype=torch.int64, device=self.device)
         st = self._stream()
-        _check(self.lib.krca_log_index(self.ptr(text), nbytes, self.ptr(doc_off), D, self.ptr(ws), self.ptr(nl), st),
-               "krca_log_index")
-        L = int(nl.item())
-        ls = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
-        le = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
-        lm = torch.empty(max(L, 1), dtype=torch.int32, device=self.device)
         dl = torch.empty(D, dtype=torch.int32, device=self.device)
         d0 = torch.empty(D, dtype=torch.int64, device=self.device)
         hist = torch.empty((D, NCAT), dtype=torch.int32, device=self.device)
-        ex = torch.empty((D, NCAT, 3), dtype=torch.int32, device=self.device)
-        _check(self.lib.krca_log_match(self.ptr(text), nbytes, self.ptr(doc_off), D, self.ptr(ws), L,
-                                       self.ptr(ls), self.ptr(le), self.ptr(lm), self.ptr(dl), self.ptr(hist),
-                                       self.ptr(ex), self.ptr(d0), self._stream()), "krca_log_match")
+        ex = torch.empty((D, NCAT, 3), dtype=torch.int32, device=self.device) if dense_examples else None
+        exp = self.ptr(ex) if ex is not None else None
+        if self.lib_tuning_log_impl() != 0:  # A/B walks: the two-call protocol (index, then match)
+            nl = torch.zeros(1, dtype=torch.int64, device=self.device)
+            _check(self.lib.krca_log_index(self.ptr(text), nbytes, self.ptr(doc_off), D, self.ptr(ws), self.ptr(nl),
+                                           st), "krca_log_index")
+            L = int(nl.item())
+            cap = -1
+        else:
+            # one call (krca_log_scan) into line arrays of the capacity the last scan needed (+25 %);
+            # a larger window falls through to krca_log_match with the index the call left in ws
+            cap = max(self._log_cap, 1024)
+            ls, le, lm = (torch.empty(cap, dtype=dt, device=self.device) for dt in (torch.int64, torch.int64, torch.int32))
+            nh = c_i64(0)
+            _check(self.lib.krca_log_scan(self.ptr(text), nbytes, self.ptr(doc_off), D, self.ptr(ws), cap,
+                                          self.ptr(ls), self.ptr(le), self.ptr(lm), self.ptr(dl), self.ptr(hist),
+                                          exp, self.ptr(d0), ctypes.byref(nh), st), "krca_log_scan")
+            L = int(nh.value)
+            self._log_cap = max(self._log_cap, L + L // 4)
+        if L > cap:
+            ls = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
+            le = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
+            lm = torch.empty(max(L, 1), dtype=torch.int32, device=self.device)
+            _check(self.lib.krca_log_match(self.ptr(text), nbytes, self.ptr(doc_off), D, self.ptr(ws), L,
+                                           self.ptr(ls), self.ptr(le), self.ptr(lm), self.ptr(dl), self.ptr(hist),
+                                           exp, self.ptr(d0), st), "krca_log_match")
         return dict(n_lines_total=L, line_start=ls[:L], line_end=le[:L], line_mask=lm[:L], doc_lines=dl,
                     doc_line0=d0, hist=hist, examples=ex, text=text)
+
+    def lib_tuning_log_impl(self):
+        v = c_i32(0)
+        _check(self.lib.krca_tune_get(b"KRCA_LOG_IMPL", ctypes.byref(v)), "krca_tune_get", self.lib)
+        return int(v.value)
 
     # -- a13 ---------------------------------------------------------------------------------
     def template_hist_device(self, scan):
@@ -551,7 +597,7 @@ class NativeEngine:
         text = self.upload_blob(blob)
         off = self._dev(doc_off)
         r = self.log_scan_device(text, off, validate=False)
-        ex = r["examples"].cpu().numpy()
+        ex = example_ids(r["line_mask"].cpu().numpy(), r["doc_line0"].cpu().numpy(), r["doc_lines"].cpu().numpy())
         ids = np.unique(ex[ex >= 0]).astype(np.int64)
         starts, ends = {}, {}
         if len(ids):
@@ -563,12 +609,17 @@ class NativeEngine:
         return LogScan(blob, r["doc_lines"].cpu().numpy(), r["hist"].cpu().numpy(), ex, starts, ends)
 
     # -- a10 ---------------------------------------------------------------------------------
-    def ppr_pack(self, row_ptr_host, col_host, n_max=None):
+    def ppr_pack(self, row_ptr_host, col_host, n_max=None, n_total=None):
         """Host-built plan + packed columns + lane info (krca_ppr_pack), uploaded:
-        (plan, plan_len, pk, lane, n_dict)."""
+        (plan, plan_len, pk, lane, n_dict).  Columns must index the global node range
+        [0, n_total) (default: this CSR's rows); a larger one would make the step kernel gather
+        past the exchange table, so it is refused here."""
         rp = np.ascontiguousarray(row_ptr_host, dtype=np.int64)
         cl = np.ascontiguousarray(col_host, dtype=np.int32)
         N = len(rp) - 1
+        limit = int(n_total if n_total is not None else N)
+        if len(cl) and int(cl.max()) >= limit:
+            raise KrcaError(f"krca_ppr_pack: column {int(cl.max())} >= node count {limit}")
         n = self.lib.krca_ppr_plan_size(rp.ctypes.data_as(c_vp), N)
         plan = np.zeros(max(n, 4), dtype=np.int64)
         pk = np.zeros(len(cl) + 64, dtype=np.int32)  # the step's clamped loads stay inside the padding

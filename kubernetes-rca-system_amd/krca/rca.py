@@ -145,7 +145,7 @@ class DeviceShard:
         self.n = int(outdeg_local.shape[0])
         # plan + packed columns (remapped to the exchange layout, dictionary blocks where they pay)
         self.plan, self.plan_len, self.col, self.lane, self.n_dict = (
-            engine.ppr_pack(row_ptr_local, col_local, n_max) if self.n else (None, 0, None, None, 0))
+            engine.ppr_pack(row_ptr_local, col_local, n_max, n_total=N) if self.n else (None, 0, None, None, 0))
         self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr_local)).to(dev)
         self.outdeg = torch.from_numpy(np.ascontiguousarray(outdeg_local)).to(dev)
         i64 = dict(dtype=torch.int64, device=dev)

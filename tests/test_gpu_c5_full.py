@@ -62,10 +62,10 @@ def test_c5_full_window_1m_pods():
     cs = np.sort(rng.choice(P, 20_000, replace=False))
     hist = scan["hist"].cpu().numpy()
     nl = scan["doc_lines"].cpu().numpy()
-    ex = scan["examples"].cpu().numpy()
     ls, le = scan["line_start"].cpu().numpy(), scan["line_end"].cpu().numpy()
     tm = scan["templates"]
     d0 = scan["doc_line0"].cpu().numpy()
+    ex = native.example_ids(scan["line_mask"].cpu().numpy(), d0, nl)  # the example bits of the masks
     nt = tm["n_templates"].cpu().numpy()
     th = tm["tmpl_hash"].cpu().numpy().view(np.uint64)
     tc = tm["tmpl_count"].cpu().numpy()

@@ -136,7 +136,7 @@ def test_log_scan_reference_corpus(eng):
     # per-line masks against the masks the reference produced
     blob, off = pack_documents(docs)
     r = eng.log_scan_device(eng.upload_blob(blob), torch.from_numpy(off).cuda())
-    masks = r["line_mask"].cpu().numpy().tolist()
+    masks = (r["line_mask"].cpu().numpy() & 0x1FFF).tolist()  # bits 16-28: the example marks
     assert masks == [m for c in g["containers"] for m in c["masks"]]
 
 
@@ -228,6 +228,35 @@ def test_log_scan_block_edges(eng):
 def test_log_scan_synthetic_large(eng):
     docs = synth.make_log_corpus(20000, lines_per_doc=6, seed=3, hazard_rate=0.01)
     _check_docs(eng, docs)
+
+
+def test_log_scan_one_call_and_fallback_identical(eng):
+    """krca_log_scan (line index in one pass with a decoupled look-back over > 64 tiles, every later
+    kernel on the device line count) equals the two-call protocol (krca_log_index, then
+    krca_log_match), both when its line arrays are too small (it leaves the index in the workspace
+    and krca_log_match takes over) and when they hold every line."""
+    docs = synth.make_log_corpus(40000, lines_per_doc=5, seed=8, hazard_rate=0.02)
+    docs += ["a\r", "\nb", "x ", " y", "q\x85", "", "z\r", "\r\n", "é" * 3000 + "Killed"]
+    blob, off = pack_documents(docs)
+    assert len(blob) > 65 * 65536  # look-back windows of 64 tiles
+    tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
+    fresh = native.NativeEngine()
+    out = []
+    for e, impl in ((fresh, 0), (fresh, 0), (eng, 1)):  # fallback (cap 1024), one call, two calls
+        with native.tune(e.lib, KRCA_LOG_IMPL=impl):
+            r = e.log_scan_device(tb, toff)
+            out.append({k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")})
+    assert fresh._log_cap >= out[0]["line_start"].shape[0]
+    for o in out[1:]:
+        for k in out[0]:
+            assert np.array_equal(out[0][k], o[k]), k
+    # the dense example table (A/B form) equals the example bits of the masks, in both protocols
+    for e in (fresh, eng):
+        r = e.log_scan_device(tb, toff, dense_examples=True)
+        bits = native.example_ids(r["line_mask"].cpu().numpy(), r["doc_line0"].cpu().numpy(),
+                                  r["doc_lines"].cpu().numpy())
+        assert np.array_equal(r["examples"].cpu().numpy(), bits)
+        assert np.array_equal(r["line_mask"].cpu().numpy(), out[0]["line_mask"])
 
 
 # ---- a10 personalized PageRank ---------------------------------------------------------------
