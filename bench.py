@@ -46,7 +46,8 @@ def parse(argv=None):
     ap.add_argument("--window", type=int, default=RANKING.window)
     ap.add_argument("--iters", type=int, default=RANKING.iters)
     ap.add_argument("--alpha", type=float, default=RANKING.alpha)
-    ap.add_argument("--seed-floor", type=float, default=RANKING.seed_floor)
+    ap.add_argument("--seed-floor", type=float, default=RANKING.seed_floor,
+                    help="personalization floor in |z| units (default: krca.rca.Config's scale-aware floor)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample-pods", type=int, default=25_000)
     ap.add_argument("--cpu-warmup", type=int, default=3)
@@ -174,6 +175,7 @@ def main():
             dist.init_process_group(backend)
     eng = native.NativeEngine(local)
     cfg = Config(window=args.window, seed_floor=args.seed_floor, alpha=args.alpha, iters=args.iters)
+    cfg = cfg.replace(seed_floor=cfg.floor(args.pods, args.metrics))  # resolved once: every rank, the oracle
 
     # ---- synthetic mesh (host graph, device metrics; not timed) --------------------------
     t0 = time.time()
@@ -296,7 +298,7 @@ def main():
                                    "(rolling z-score -> 30-iteration seeded PPR -> top-10), ranking of krca.rca.Config",
                        "pods": args.pods, "edges": mesh.n_edges, "metrics": args.metrics, "tsteps": args.tsteps,
                        "window": args.window, "ppr_iters": args.iters, "alpha": args.alpha,
-                       "seed_floor": args.seed_floor, "parallelism": f"pod-sharded x{world}"},
+                       "seed_floor": cfg.seed_floor, "parallelism": f"pod-sharded x{world}"},
             "e2e_rca_latency_ms": latency_ms, "e2e_rca_latency_p95_ms": latency_p95_ms,
             "step_ms_median": float(np.median(step_ms)), "step_ms_p95": float(np.percentile(step_ms, 95)),
             "pipelined_streams": n_pipe,

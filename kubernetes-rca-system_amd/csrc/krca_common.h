@@ -97,6 +97,9 @@ struct Tuning {
   int corr_batch;   // KRCA_CORR_BATCH: super-tiles per main-pass batch (0 = 2048)
   int corr_amb_tile;  // KRCA_CORR_AMB_TILE: ambiguous-list budget per tile of a batch (-1 = 512; 0 = every
                       // tile decides its pairs in place)
+  int ppr_fuse;     // KRCA_PPR_FUSE: single device, the iteration's reduction in the step's last workgroup
+                    // (0 = a ppr_reduce launch after each step)
+  int ppr_nt;       // KRCA_PPR_NT: the step streams its plan / column / row arrays with non-temporal loads
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

@@ -694,6 +694,10 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   __shared__ int64_t s_wsum[TPB / 64];
   __shared__ uint32_t s_cs[NBW];
   __shared__ int64_t s_tile, s_excl;
+  // per piece: line starts (low half) | odd separator lengths (high half), and the lengths 2 / 3;
+  // in LDS rather than registers (16 pieces x 2 words per lane took the kernel to 215 VGPRs)
+  __shared__ uint32_t s_sl[NIT * TPB];
+  __shared__ uint16_t s_l1[NIT * TPB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
   s_cnt[threadIdx.x] = 0;
@@ -701,9 +705,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   const int64_t tile = s_tile;
   const int64_t tile0 = tile * TILE;
   tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
-  uint32_t SL[NIT];  // line starts (low half) | odd separator lengths (high half), per piece
-  uint32_t L1[NIT];  // separator lengths 2 and 3
-#pragma unroll
+#pragma unroll 4
   for (int it = 0; it < NIT; ++it) {
     const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
     uint32_t w[4] = {0, 0, 0, 0};
@@ -732,8 +734,8 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
     sep_planes(w[1], w[2], (C >> 8) & 0xFu, a2, b2);
     sep_planes(w[2], w[3], (C >> 12) & 0xFu, a3, b3);
     const uint32_t l0 = a0 | (a1 << 4) | (a2 << 8) | (a3 << 12), l1 = b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
-    SL[it] = S | ((l0 & S) << 16);
-    L1[it] = l1 & S;
+    s_sl[it * TPB + threadIdx.x] = S | ((l0 & S) << 16);
+    s_l1[it * TPB + threadIdx.x] = (uint16_t)(l1 & S);
     uint32_t c = __popc(S);
 #pragma unroll
     for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
@@ -792,10 +794,11 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   chunk_line0[tile * TPB + threadIdx.x] = excl + before;
   __syncthreads();
   // line starts and the previous line's end, from the registers
-#pragma unroll
+#pragma unroll 2
   for (int it = 0; it < NIT; ++it) {
     const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
-    const uint32_t S = SL[it] & 0xFFFFu;
+    const uint32_t sl_ = s_sl[it * TPB + threadIdx.x];
+    const uint32_t S = sl_ & 0xFFFFu;
     const uint32_t n = __popc(S);
     uint32_t xs = n;
 #pragma unroll
@@ -805,7 +808,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
     }
     int64_t id = s_base[it * (TPB / LANES_PER_CHUNK) + threadIdx.x / LANES_PER_CHUNK] + (xs - n);
     uint32_t rem = S;
-    const uint32_t l0 = SL[it] >> 16, l1 = L1[it];
+    const uint32_t l0 = sl_ >> 16, l1 = s_l1[it * TPB + threadIdx.x];
     while (rem) {
       const int k = __ffs(rem) - 1;
       rem &= rem - 1;

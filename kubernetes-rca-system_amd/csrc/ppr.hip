@@ -51,6 +51,15 @@ using namespace pprl;
 
 constexpr int PPR_RESIDUAL = KRCA_PPR_RESIDUAL;
 constexpr int PPR_WRITE_R = KRCA_PPR_WRITE_R;
+constexpr int PPR_NT = 4;  // stream the plan / column / row arrays with non-temporal loads (KRCA_PPR_NT)
+
+// a load of streamed data: non-temporal when NT, so it does not evict the gathered code table
+// from the XCD's L2
+template <bool NT, class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 
 struct Ctl {          // device control block (header of the ctl buffer)
   double tele;        // (1-alpha)*2^60 + alpha*D   for the next step
@@ -237,6 +246,7 @@ __device__ __forceinline__ int64_t dict_words(int64_t e0, int32_t nu) {  // pk o
   return ((e0 + nu + 3) & ~int64_t(3)) - e0;
 }
 
+template <bool NT>
 __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int64_t b, const int32_t* __restrict__ pk,
                                           Head& H) {
   const int64_t* pe = plan + 4 * b;
@@ -254,7 +264,7 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
 #pragma unroll
   for (int j = 0; j < SEG; ++j) {
     const int64_t u = tid + j * TPB;
-    H.c[j] = pk[H.m.e0 + (u < top ? u : top)];
+    H.c[j] = ld_stream<NT>(pk + H.m.e0 + (u < top ? u : top));
   }
 }
 
@@ -266,15 +276,18 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
   const int tid = threadIdx.x;
   const int nrows = m.code > 0 ? m.code - m.rb : 1;
   const int64_t my_row = m.rb + (tid < nrows ? tid : 0);
-  R.my_off = row_ptr[my_row];
-  R.my_end = row_ptr[my_row + 1];
-  R.my_q = q[my_row];
-  R.my_r = (FLAGS & PPR_RESIDUAL) ? r[my_row] : 0;
-  R.my_deg = outdeg[my_row];
-  R.li = lane_info[b * TPB + tid];  // zero for long-row chunks
+  constexpr bool NT = (FLAGS & PPR_NT) != 0;
+  R.my_off = ld_stream<NT>(row_ptr + my_row);
+  R.my_end = ld_stream<NT>(row_ptr + my_row + 1);
+  R.my_q = ld_stream<NT>(q + my_row);
+  R.my_r = (FLAGS & PPR_RESIDUAL) ? ld_stream<NT>(r + my_row) : 0;
+  R.my_deg = ld_stream<NT>(outdeg + my_row);
+  R.li = ld_stream<NT>(lane_info + b * TPB + tid);  // zero for long-row chunks
   // unconditional 16-byte load (used by dictionary blocks only): in-bounds, 16-byte aligned
   const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
-  R.ix = *reinterpret_cast<const uint4*>(pk + wb + (tid * SEG < m.e1 - m.e0 ? tid * (SEG / 2) : 0));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 ix = ld_stream<NT>(reinterpret_cast<const u32x4*>(pk + wb + (tid * SEG < m.e1 - m.e0 ? tid * (SEG / 2) : 0)));
+  R.ix = make_uint4(ix.x, ix.y, ix.z, ix.w);
 }
 
 __device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict__ w, uint32_t (&v)[SEG]) {
@@ -326,13 +339,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   const int tid = threadIdx.x;
   Head H0, H1;
   Rows R0, R1;
-  load_head(plan, b, pk, H0);
+  load_head<(FLAGS & PPR_NT) != 0>(plan, b, pk, H0);
   uint32_t v[SEG];  // codes: decoded where summed (a prefetched register is never computed on early)
   gather(H0, w, v);
   load_rows<FLAGS>(H0.m, b, lane_info, row_ptr, pk, outdeg, q, r, R0);
   Meta cur = H0.m;
   int64_t b1 = b + gridDim.x;
-  if (b1 < nblk) load_head(plan, b1, pk, H1);
+  if (b1 < nblk) load_head<(FLAGS & PPR_NT) != 0>(plan, b1, pk, H1);
   int64_t err = 0, dang = 0;
 #ifdef PPR_TIMING
   uint64_t tacc[5] = {0, 0, 0, 0, 0};
@@ -370,7 +383,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       gather(hn, w, v);
       load_rows<FLAGS>(next, b1, lane_info, row_ptr, pk, outdeg, q, r, rn);
     }
-    if (b2 < nblk) load_head(plan, b2, pk, hl);
+    if (b2 < nblk) load_head<(FLAGS & PPR_NT) != 0>(plan, b2, pk, hl);
     if (shortb) {
       const int nrows = cur.code - cur.rb;
       __syncthreads();
@@ -450,9 +463,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   if (fz.on) {  // block-uniform
     __shared__ int last;
     if (tid == 0) {
-      __threadfence();  // this workgroup's slot adds are performed before its ticket
+      // this workgroup's slot adds are performed (at the memory side, device-scope atomics) before
+      // its ticket; the last workgroup reads the slots with agent-scope atomic loads.  (A
+      // __threadfence() here -- a release fence per workgroup -- doubled the step: 39 -> 77 us.)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       last = __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-      __threadfence();
     }
     __syncthreads();
     if (last) reduce_single(send + wslots(n_max), fz.w_next + wslots(n_max), alpha, fz.err_limit, ctl, red);
@@ -585,8 +600,15 @@ int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t
                        int32_t flags, double tol, int64_t* r, int64_t* send, void* ctl, void* stream) {
   KRCA_CHECK_ARG(plan_len > 0 && N > 0, "krca_ppr_solo_step: bad sizes");
   const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
-  return launch_step(row_ptr, col, plan, plan_len, lane, w, outdeg, q, N, N, N, alpha, flags, r, send, ctl,
-                     Fuse{1, err_limit, w}, stream);
+  if (krca::tuning().ppr_fuse)
+    return launch_step(row_ptr, col, plan, plan_len, lane, w, outdeg, q, N, N, N, alpha, flags, r, send, ctl,
+                       Fuse{1, err_limit, w}, stream);
+  // the step, then the reduction over the slice it wrote (zeroing the slots of the buffer it
+  // gathered from: the next step's write target)
+  if (int rc = launch_step(row_ptr, col, plan, plan_len, lane, w, outdeg, q, N, N, N, alpha, flags, r, send, ctl,
+                           Fuse{0, 0.0, nullptr}, stream))
+    return rc;
+  return krca_ppr_shard_reduce(send, 1, N, N, alpha, tol, 0, ctl, w, stream);
 }
 }  // extern "C"
 
@@ -614,8 +636,10 @@ int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan,
   }();
   const int64_t resident = krca::tuning().ppr_grid > 0 ? (int64_t)krca::tuning().ppr_grid : occupancy;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nblk, resident));
-  auto kern = (flags & KRCA_PPR_RESIDUAL) ? ppr_step<PPR_RESIDUAL | PPR_WRITE_R>
-               : (flags & KRCA_PPR_WRITE_R) ? ppr_step<PPR_WRITE_R> : ppr_step<0>;
+  const bool nt = krca::tuning().ppr_nt != 0;
+  auto kern = (flags & KRCA_PPR_RESIDUAL) ? (nt ? ppr_step<PPR_RESIDUAL | PPR_WRITE_R | PPR_NT> : ppr_step<PPR_RESIDUAL | PPR_WRITE_R>)
+              : (flags & KRCA_PPR_WRITE_R) ? (nt ? ppr_step<PPR_WRITE_R | PPR_NT> : ppr_step<PPR_WRITE_R>)
+                                           : (nt ? ppr_step<PPR_NT> : ppr_step<0>);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, lane, nblk,
                      reinterpret_cast<const uint32_t*>(w_all), outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
                      reinterpret_cast<Ctl*>(ctl), fz);

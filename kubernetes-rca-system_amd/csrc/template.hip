@@ -69,6 +69,78 @@ __device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& wor
   return h;
 }
 
+// The word-state machine of the template as a table, (state, byte) -> next state | flags, so that
+// a byte costs one LDS read and the FNV step instead of ~20 class tests and selects (round 2: ~30
+// vector instructions per byte).  States: 0 outside a word; 1 in a word holding a digit (masked
+// whatever follows); 2..9 in a word of hex letters only, length 1..8 (9: >= 8, masked at its end);
+// 10 in any other word.  An entry holds the next state's row as a byte offset (state * 512) and the
+// flags START (this byte starts a word: keep the hash) and MEND (this non-word byte ends a masked
+// word: the hash becomes "<*>" from the kept state).
+constexpr int TS_STATES = 11;
+constexpr uint32_t TS_ROW = 512;  // bytes per state row (256 u16 entries)
+constexpr uint32_t TS_START = 1u << 13, TS_MEND = 1u << 14, TS_OFF = (1u << 13) - 1u;
+static_assert((TS_STATES - 1) * TS_ROW <= TS_OFF, "row offsets must fit below the flags");
+
+__device__ __forceinline__ uint16_t tstate_entry(int st, uint32_t b) {
+  const bool dg = b >= '0' && b <= '9';
+  const bool hl = (b >= 'a' && b <= 'f') || (b >= 'A' && b <= 'F');
+  const bool wc = dg || hl || (b >= 'g' && b <= 'z') || (b >= 'G' && b <= 'Z') || b == '_';
+  int nx;
+  uint32_t fl = 0;
+  if (!wc) {
+    nx = 0;
+    if (st == 1 || st == 9) fl = TS_MEND;
+  } else if (st == 0) {
+    fl = TS_START;
+    nx = dg ? 1 : (hl ? 2 : 10);
+  } else if (st == 1) {
+    nx = 1;
+  } else if (st <= 9) {
+    nx = dg ? 1 : (hl ? (st < 9 ? st + 1 : 9) : 10);
+  } else {
+    nx = dg ? 1 : 10;
+  }
+  return (uint16_t)((uint32_t)nx * TS_ROW | fl);
+}
+
+// one byte of the walk: st = the current state's row offset in bytes
+__device__ __forceinline__ void tstep(const uint8_t* __restrict__ T, uint32_t b, uint32_t& st, uint64_t& h,
+                                      uint64_t& hb) {
+  const uint32_t t = *reinterpret_cast<const uint16_t*>(T + st + 2 * b);
+  if (t & TS_MEND) h = fnv3_mask(hb);  // a masked word ended at the previous byte (rare)
+  if (t & TS_START) hb = h;
+  h = fnv(h, b);
+  st = t & TS_OFF;
+}
+
+// the template hash of the line at LDS offsets [s, e) of the staged span (the span holds 3 bytes
+// past e): the lane's bytes re-aligned to its line start (alignbyte of two aligned dwords), full
+// dwords with no per-byte range test, then the <= 3 tail bytes
+__device__ __forceinline__ uint64_t line_hash_tab(const uint8_t* __restrict__ sb, int s, int e,
+                                                  const uint8_t* __restrict__ T) {
+  uint64_t h = kFnvOff, hb = 0;
+  uint32_t st = 0;
+  const uint32_t sh = (uint32_t)(s & 3);
+  int q = s & ~3;
+  uint32_t lo = *reinterpret_cast<const uint32_t*>(sb + q);
+  int n = e - s;
+  for (; n >= 4; n -= 4) {
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(sb + q + 4);
+    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    lo = hi;
+    q += 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tstep(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
+  }
+  if (n > 0) {
+    const uint32_t hi = (int)sh + n > 4 ? *reinterpret_cast<const uint32_t*>(sb + q + 4) : 0u;
+    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    for (int k = 0; k < n; ++k) tstep(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
+  }
+  if (st == 1 * TS_ROW || st == 9 * TS_ROW) h = fnv3_mask(hb);  // a trailing masked word
+  return h;
+}
+
 // Workgroup per 256 consecutive lines.  Lines are contiguous in the text, so the workgroup first
 // copies the bytes its lines span into LDS (16 B per lane, coalesced: every text byte crosses HBM
 // once) and every lane then hashes its line from LDS.  A lane whose line reaches past the staged
@@ -81,6 +153,9 @@ __global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restric
                                                         const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
                                                         int64_t L, uint64_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[SPAN];
+  __shared__ __attribute__((aligned(16))) uint8_t tstate[TS_STATES * TS_ROW];
+  for (int i = threadIdx.x; i < TS_STATES * 256; i += TPB)
+    reinterpret_cast<uint16_t*>(tstate)[i] = tstate_entry(i >> 8, (uint32_t)(i & 255));
   const int64_t l0 = (int64_t)blockIdx.x * TPB;
   const int64_t i = l0 + threadIdx.x;
   const int64_t l1 = min(l0 + TPB, L);
@@ -115,7 +190,7 @@ __global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restric
   if (i >= L) return;
   const int64_t s = ls[i], e = le[i];
   if (e <= a1) {
-    out[i] = line_hash(s, e, [&](int64_t q) -> uint32_t { return *reinterpret_cast<const uint32_t*>(sbuf + (q - a0)); });
+    out[i] = line_hash_tab(sbuf, (int)(s - a0), (int)(e - a0), tstate);
   } else {  // past the staged span: aligned dwords from the text (the last one may be partial)
     out[i] = line_hash(s, e, [&](int64_t q) -> uint32_t {
       if (q + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(text + q);

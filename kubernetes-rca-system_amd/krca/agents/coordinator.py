@@ -125,7 +125,9 @@ class Coordinator:
         scores = self.metrics_agent.last_scores
         if scores is not None and hasattr(c, 'get_dependency_csr'):
             names, row_ptr, col, outdeg = c.get_dependency_csr(namespace)
-            idx, val, rank = self.engine.rank_root_causes(scores['score'], row_ptr, col, outdeg, self.rank_config)
+            zl = scores.get('z_last')
+            idx, val, rank = self.engine.rank_root_causes(scores['score'], row_ptr, col, outdeg, self.rank_config,
+                                                          n_metrics=int(zl.shape[1]) if zl is not None else 1)
             sc = np.asarray(scores['score'].cpu() if hasattr(scores['score'], 'cpu') else scores['score'])
             return [{'component': f"Pod/{names[i]}", 'rank': r + 1, 'score': float(v), 'pagerank': float(rank[i]),
                      'anomaly': float(sc[i])} for r, (i, v) in enumerate(zip(idx.tolist(), val.tolist()))]

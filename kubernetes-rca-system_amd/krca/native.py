@@ -661,15 +661,17 @@ class NativeEngine:
         r, rf, q, iters = self._ppr_full(row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor)
         return r, rf, iters
 
-    def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None):
+    def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None, n_metrics=1):
         """The root-cause ranking of krca.rca.Config (the same definition as RcaStep / bench.py):
-        seeded PageRank (cfg.alpha, cfg.seed_floor, cfg.iters / cfg.tol), key r_i * q_i, top-k.
+        seeded PageRank (cfg.alpha, cfg.floor(pods, n_metrics), cfg.iters / cfg.tol), key r_i * q_i,
+        top-k (seed = each pod's max |z| over its n_metrics metrics).
         Returns host (idx int32 [k], score float64 [k] = r_i * p_i, r float64 [N] PageRank mass)."""
         from .rca import RANKING
         cfg = cfg or RANKING
         torch = self.torch
         k = min(int(k or cfg.k), len(outdeg))
-        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol, cfg.seed_floor)
+        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol,
+                                     cfg.floor(len(outdeg), n_metrics))
         key = torch.empty_like(rf)
         _check(self.lib.krca_ppr_rca_key(self.ptr(rf), self.ptr(q), rf.numel(), self.ptr(key), self._stream()),
                "krca_ppr_rca_key")

@@ -57,14 +57,27 @@ def shard_graph(row_ptr, col, outdeg, lo, hi):
     return rp, c, np.asarray(outdeg[lo:hi], np.int32)
 
 
+def null_floor(n_series, minimum=4.0):
+    """The seed floor of a mesh with n_series scored series: the expected maximum |z| of that many
+    null (Gaussian) series, Phi^-1(1 - 1/(2 n)), at least `minimum`, rounded to 1e-3 so that every
+    rank, the bench and the oracle chain get the same float (stdlib NormalDist: no scipy)."""
+    from statistics import NormalDist
+    if n_series <= 1:
+        return float(minimum)
+    return max(float(minimum), round(NormalDist().inv_cdf(1.0 - 1.0 / (2.0 * n_series)), 3))
+
+
 class Config:
     """The one root-cause ranking definition ("Ranking"), shared by bench.py,
     :class:`RcaStep`, the streaming replay and ``Coordinator.ranked_root_causes``:
 
     * rolling z-scores over a trailing window of `window` steps, exceedance at |z| > z_threshold;
     * personalized PageRank (networkx 3.4.2 semantics) with damping `alpha` = 0.5 and
-      personalization p_i ∝ max(s_i - seed_floor, 0), s_i = the pod's max |z| at the last step
-      (seed_floor is in |z| units: only pods past 4 sigma seed the walk);
+      personalization p_i ∝ max(s_i - floor, 0), s_i = the pod's max |z| at the last step.  The
+      floor (|z| units) is `seed_floor` when given, else scale-aware: the expected maximum |z| of
+      the mesh's P·M null series, at least `min_floor` = 4 (:func:`null_floor`; 4.0 up to ~16k
+      series, 5.286 at the C4 mesh's 8M): a fixed floor lets the noise maxima of a large mesh
+      (|z| ≈ 6 over 8M series) seed the walk (measured: DESIGN.md §3.2);
     * `iters` = 30 fixed iterations (tol = 0): at alpha = 0.5 that is within 1e-10 (L1) of the
       converged vector, so the result is networkx's converged PageRank (pinned at 2k / 20k nodes,
       tests/golden/ppr_nx_meshes.npz);
@@ -72,7 +85,8 @@ class Config:
       index.  Ranking by r alone sends the mass to the dependency sinks below the faulty pods
       (measured recall of the planted roots: DESIGN.md §3.2)."""
 
-    def __init__(self, window=60, z_threshold=3.0, seed_floor=4.0, alpha=0.5, iters=30, tol=0.0, k=10):
+    def __init__(self, window=60, z_threshold=3.0, seed_floor=None, alpha=0.5, iters=30, tol=0.0, k=10,
+                 min_floor=4.0):
         self.window = window
         self.z_threshold = z_threshold
         self.seed_floor = seed_floor
@@ -80,10 +94,17 @@ class Config:
         self.iters = iters
         self.tol = tol
         self.k = k
+        self.min_floor = min_floor
+
+    def floor(self, n_pods, n_metrics=1):
+        """The seed floor for a mesh of n_pods pods scored over n_metrics metrics each."""
+        if self.seed_floor is not None:
+            return float(self.seed_floor)
+        return null_floor(int(n_pods) * int(n_metrics), self.min_floor)
 
     def as_dict(self):
         return dict(window=self.window, z_threshold=self.z_threshold, seed_floor=self.seed_floor, alpha=self.alpha,
-                    iters=self.iters, tol=self.tol, k=self.k)
+                    iters=self.iters, tol=self.tol, k=self.k, min_floor=self.min_floor)
 
     def replace(self, **kw):
         d = self.as_dict()
@@ -142,6 +163,7 @@ class DeviceShard:
         dev = engine.device
         self.N, self.n_max, self.world = N, n_max, world
         self.x = x_local
+        self.M = int(x_local.shape[2]) if x_local is not None and x_local.dim() == 3 else 1  # metrics per pod
         self.n = int(outdeg_local.shape[0])
         # plan + packed columns (remapped to the exchange layout, dictionary blocks where they pay)
         self.plan, self.plan_len, self.col, self.lane, self.n_dict = (
@@ -173,6 +195,7 @@ class DeviceShard:
         forward by delta steps (krca_stream_score); outputs as the batch scorer over the series so far."""
         torch, e, p = self.torch, self.eng, self.eng.ptr
         d, P, M = x_new.shape
+        self.M = int(M)
         if P != self.n:
             raise ValueError(f"stream window has {P} pods, the shard owns {self.n}")
         if getattr(self, "_stream_state", None) is None:
@@ -248,16 +271,54 @@ class DeviceShard:
         return idx, val
 
 
-class RcaStep:
-    """One rank's view of the pod-sharded RCA step."""
+def graph_default(comm, cfg, shard=None):
+    """Whether RcaStep captures its PageRank solve in a HIP graph by default: fixed-iteration solves
+    (tol <= 0: no host read-back between iterations) on one device.  Sharded solves (an RCCL
+    all-gather per iteration) stay eager unless KRCA_RCA_GRAPH=1; KRCA_RCA_GRAPH=0 turns it off."""
+    import os
+    env = os.environ.get("KRCA_RCA_GRAPH")
+    if cfg.tol > 0 or env == "0" or not isinstance(shard, DeviceShard):
+        return False
+    if comm.world == 1:
+        return True
+    return env == "1"
 
-    def __init__(self, shard, comm, cfg, offset):
+
+class RcaStep:
+    """One rank's view of the pod-sharded RCA step.
+
+    With `graph` (default: :func:`graph_default`) the whole PageRank solve (init, exchange,
+    first reduce, iters x (step, exchange, reduce)) is captured once into a HIP graph on the
+    shard's fixed buffers and replayed per step: one launch instead of ~2 host calls per iteration
+    (at C4 the host-side gaps were ~0.4 ms of the 1.75 ms solve).  Replays compute exactly the
+    eager sequence: the captured kernels and pointers are the same (G = 1's ping-pong swaps are
+    baked into the capture)."""
+
+    def __init__(self, shard, comm, cfg, offset, graph=None):
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
+        self.graph = graph_default(comm, cfg, shard) if graph is None else bool(graph)
+        self._g = None
 
     def propagate(self):
         """Seeded PageRank on the current scores: init, exchange, then iters x (step, exchange, reduce)."""
+        if not self.graph:
+            return self._propagate()
+        import torch
+        if self._g is None:
+            self._propagate()  # eager warm-up: statics, occupancy queries, workspaces
+            g = torch.cuda.CUDAGraph()
+            cur = torch.cuda.current_stream(self.s.eng.device)
+            side = torch.cuda.Stream(self.s.eng.device)
+            side.wait_stream(cur)
+            with torch.cuda.graph(g, stream=side):
+                self._propagate()
+            cur.wait_stream(side)
+            self._g = g
+        self._g.replay()
+
+    def _propagate(self):
         s, c, cfg = self.s, self.comm, self.cfg
-        s.init(cfg.alpha, cfg.seed_floor)
+        s.init(cfg.alpha, cfg.floor(s.N, s.M))
         c.exchange(s)
         s.reduce(cfg.alpha, cfg.tol, 1)
         for it in range(cfg.iters):

@@ -72,9 +72,9 @@ class StreamingRCA:
     def rerank(self):
         s, cfg = self.shard, self.cfg
         if self.solved:
-            s.init_warm(cfg.alpha, cfg.seed_floor)
+            s.init_warm(cfg.alpha, cfg.floor(s.N, s.M))
         else:
-            s.init(cfg.alpha, cfg.seed_floor)
+            s.init(cfg.alpha, cfg.floor(s.N, s.M))
         self.comm.exchange(s)
         s.reduce(cfg.alpha, self.tol, 1)
         for it in range(self.max_iter):

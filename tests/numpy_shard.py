@@ -42,6 +42,7 @@ class NumpyShard:
     def __init__(self, x_local, row_ptr_local, col_local, outdeg_local, N, n_max, world, cfg):
         self.cfg, self.N, self.n_max, self.world = cfg, N, n_max, world
         self.x = np.asarray(x_local, np.float32)
+        self.M = int(self.x.shape[2]) if self.x.ndim == 3 else 1  # metrics per pod (the seed floor's scale)
         self.rp = np.asarray(row_ptr_local, np.int64)
         c = np.asarray(col_local, np.int64)
         self.col = remap_cols(c, n_max)
@@ -114,6 +115,7 @@ class NumpyShard:
         """krca_stream_score's contract restated: outputs of the batch scorer over the whole series
         so far, n_exceed over the last `horizon` evaluated steps (a difference of prefix counts)."""
         x_new = np.asarray(x_new.cpu() if hasattr(x_new, "cpu") else x_new, np.float32)
+        self.M = int(x_new.shape[2])
         hist = getattr(self, "_hist", None)
         self._hist = x_new if hist is None else np.concatenate([hist, x_new])
         assert len(self._hist) == t0 + len(x_new)

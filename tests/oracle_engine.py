@@ -47,12 +47,12 @@ class OracleEngine:
         docs = [blob[doc_off[i]:doc_off[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(doc_off) - 1)]
         return OracleLogScan(docs)
 
-    def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None):
+    def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None, n_metrics=1):
         from krca.rca import RANKING
         cfg = cfg or RANKING
         seed = np.asarray(seed.cpu() if hasattr(seed, "cpu") else seed, np.float32)
         k = min(int(k or cfg.k), len(outdeg))
-        rf, r, _, q = oracle.c_ppr(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol, cfg.seed_floor,
+        rf, r, _, q = oracle.c_ppr(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol, cfg.floor(len(outdeg), n_metrics),
                                    return_q=True)
         idx, _ = oracle.topk_ref(oracle.c_rca_key(r, q), k)
         rr = r.astype(np.float64) / 2.0 ** 60

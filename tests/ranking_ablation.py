@@ -28,7 +28,10 @@ def main():
     ap.add_argument("--edges", type=int, default=200_000)
     ap.add_argument("--out")
     a = ap.parse_args()
-    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0) for key in ("r", "rq")] + [(None, None, "q")]
+    from scipy.special import ndtri
+    auto = round(float(ndtri(1.0 - 1.0 / (2.0 * a.pods * 8))), 3)  # expected max |z| of P*M null series
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0, auto, 5.0) for key in ("r", "rq")] + \
+        [(None, None, "q")]
     hits = {d: [] for d in defs}
     for seed in range(a.seeds):
         m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)

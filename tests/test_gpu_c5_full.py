@@ -79,13 +79,13 @@ def test_c5_full_window_1m_pods():
         assert list(zip(th[d0[d]:d0[d] + nt[d]].tolist(), tc[d0[d]:d0[d] + nt[d]].tolist())) == want, d
     # ranks: cold then warm, bit-identical to the C oracle chain
     rf, r_ref, it_ref, q = oracle.c_ppr(mesh.row_ptr, mesh.col, mesh.outdeg, sc0, cfg.alpha, 100, 1e-9,
-                                        cfg.seed_floor, return_q=True)
+                                        cfg.floor(P, M), return_q=True)
     assert np.array_equal(r0, r_ref) and it0 == it_ref
     ridx, _ = oracle.topk_ref(oracle.c_rca_key(r_ref, q), cfg.k)
     assert [int(i) for i in top0] == [int(i) for i in ridx]
     score = sc["score"].cpu().numpy()
     r_ref, it, q = oracle.c_ppr_warm(mesh.row_ptr, mesh.col, mesh.outdeg, score, r_ref, cfg.alpha, 100, 1e-9,
-                                     cfg.seed_floor)
+                                     cfg.floor(P, M))
     assert np.array_equal(s.shard.r[:P].cpu().numpy(), r_ref) and s.last_iters == it
     ridx, _ = oracle.topk_ref(oracle.c_rca_key(r_ref, q), cfg.k)
     assert [int(i) for i in top] == [int(i) for i in ridx]

@@ -324,12 +324,39 @@ def test_rca_step_single_gpu_vs_oracle(eng, n, iters):
     step = RcaStep(DeviceShard(eng, x, rp, col, od, n, n_max, 1, cfg), Comm(), cfg, 0)
     idx, key = step.run()
     score = step.s.score_out["score"].cpu().numpy()
-    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
     assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
     assert list(idx) == list(ridx)
     idx2, _ = step.run()  # re-run on the same buffers: identical
     assert list(idx2) == list(idx)
     assert len(set(idx.tolist()) & set(m.roots.tolist())) >= 8
+
+
+def test_rca_step_graph_replay_equals_eager(eng):
+    """RcaStep's HIP-graph solve (captured once, replayed per step) equals the eager launch
+    sequence bit for bit, also after the scores change under the captured buffers."""
+    from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
+    n = 20000
+    m = synth.make_graph(n, avg_degree=20, seed=5)
+    hops = synth.caller_hops(m, m.roots)
+    cfg = Config(iters=30)
+    lo, hi, n_max = shard_range(n, 1, 0)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
+    xs = [synth.make_metrics(n, 8, 300, window=60, seed=s, roots=m.roots, hop_sets=hops).cuda() for s in (1, 2)]
+    res = {}
+    for graph in (False, True):
+        x = xs[0].clone()
+        step = RcaStep(DeviceShard(eng, x, rp, col, od, n, n_max, 1, cfg), Comm(), cfg, 0, graph=graph)
+        assert step.graph == graph
+        out = []
+        for xi in xs + xs[:1]:
+            x.copy_(xi)  # new metrics under the same buffers (the graph's inputs)
+            idx, key = step.run()
+            out.append((list(idx), list(key), step.s.r[:n].cpu().numpy().copy()))
+        res[graph] = out
+    for (ia, ka, ra), (ib, kb, rb) in zip(res[False], res[True]):
+        assert ia == ib and ka == kb and np.array_equal(ra, rb)
+    assert np.array_equal(res[True][0][2], res[True][2][2]) and not np.array_equal(res[True][0][2], res[True][1][2])
 
 
 @pytest.mark.parametrize("G", [2, 3])
@@ -355,7 +382,7 @@ def test_rca_sharded_path_emulated_on_one_gpu(eng, G):
 
     for s in shards:
         s.score()
-        s.init(cfg.alpha, cfg.seed_floor)
+        s.init(cfg.alpha, cfg.floor(n, 8))
     exchange()
     for s in shards:
         s.reduce(cfg.alpha, cfg.tol, 1)
@@ -366,7 +393,7 @@ def test_rca_sharded_path_emulated_on_one_gpu(eng, G):
         for s in shards:
             s.reduce(cfg.alpha, cfg.tol, 0)
     score = torch.cat([s.score_out["score"] for s in shards]).cpu().numpy()
-    _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+    _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
     got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
     assert np.array_equal(got, r)
 

@@ -33,7 +33,10 @@ def _csr(edges, n):
     return rp, src[o].astype(np.int32), np.bincount(src, minlength=n).astype(np.int32)
 
 
-def _rca_from_scores(eng, rp, col, od, score, cfg=RANKING):
+GOLDEN_CFG = RANKING.replace(seed_floor=4.0)  # the goldens were captured at the fixed floor 4
+
+
+def _rca_from_scores(eng, rp, col, od, score, cfg=GOLDEN_CFG):
     """The bench path (DeviceShard + RcaStep on one rank) seeded with given scores."""
     n = len(od)
     sh = DeviceShard(eng, None, rp, col, od, n, n, 1, cfg)
@@ -50,7 +53,7 @@ def test_ranking_pinned_to_networkx(eng, name):
     e, s, ref = g[f"{name}_edges"], g[f"{name}_seed"], g[f"{name}_rank"]
     n = len(s)
     rp, col, od = _csr(e, n)
-    idx, val, r = eng.rank_root_causes(s, rp, col, od)          # the Coordinator's entry point
+    idx, val, r = eng.rank_root_causes(s, rp, col, od, GOLDEN_CFG)  # the Coordinator's entry point
     big = ref >= 1e-12
     assert np.max(np.abs(r[big] - ref[big]) / ref[big]) < 1e-5
     assert np.max(np.abs(r[~big] - ref[~big])) < 1e-12
@@ -88,7 +91,7 @@ def test_c2mini_golden(eng):
     assert np.allclose(got["z_last"].cpu().numpy(), g["z_last_f64"], rtol=1e-5, atol=1e-5)
     # a10 (networkx-pinned ranking definition)
     rp, col, od = _csr(e, C.P)
-    idx, _, r = eng.rank_root_causes(g["score"], rp, col, od)
+    idx, _, r = eng.rank_root_causes(g["score"], rp, col, od, GOLDEN_CFG)
     assert idx.tolist() == g["ppr_top10"].tolist()
     big = g["ppr_rank"] >= 1e-12
     assert np.max(np.abs(r[big] - g["ppr_rank"][big]) / g["ppr_rank"][big]) < 1e-5
@@ -129,7 +132,7 @@ def test_c2_full_rca_step(eng):
     assert np.array_equal(so["score"].cpu().numpy(), ref["score"])
     assert np.allclose(so["z_last"].cpu().numpy(), ref["z_last"], rtol=1e-5, atol=1e-6)
     ridx, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, ref["score"], RANKING.alpha, RANKING.iters,
-                                 RANKING.seed_floor, RANKING.k)
+                                 RANKING.floor(n, 8), RANKING.k)
     assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
     assert [int(i) for i in idx] == ridx.tolist()
     assert len(set(ridx.tolist()) & set(m.roots.tolist())) >= 8
@@ -156,7 +159,7 @@ def test_c4_full_rca_step_1m_pods(eng):
     assert np.array_equal(step.s.score_out["flags"][sel].cpu().numpy(), ref["flags"])
     assert np.array_equal(score[samp], ref["score"])
     ridx, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, RANKING.alpha, RANKING.iters,
-                                 RANKING.seed_floor, RANKING.k)
+                                 RANKING.floor(n, 8), RANKING.k)
     assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
     assert [int(i) for i in idx] == ridx.tolist()
     del x

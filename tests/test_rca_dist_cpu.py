@@ -55,6 +55,7 @@ def _worker(rank, world, port, out_q):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_rca_matches_single_process_oracle(world):
     import oracle
+    from krca.rca import Config
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -68,7 +69,7 @@ def test_sharded_rca_matches_single_process_oracle(world):
     res.sort()
     m, x = _mesh()
     score = oracle.c_rolling_score(x, 60)["score"]
-    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, 0.5, 12, 4.0, 10)
+    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, 0.5, 12, Config().floor(N, M), 10)
     r_sharded = np.concatenate([rr for _, _, rr, _, _ in res])
     assert np.array_equal(r_sharded, r)
     for _, _, _, idx, _ in res:  # every rank holds the same merged top-10

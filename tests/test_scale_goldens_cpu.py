@@ -31,7 +31,10 @@ def test_ranking_definition_is_shared():
     import inspect
     from krca.agents.coordinator import Coordinator
     from krca.stream import StreamingRCA
-    assert (RANKING.alpha, RANKING.seed_floor, RANKING.iters, RANKING.tol, RANKING.k) == (0.5, 4.0, 30, 0.0, 10)
+    assert (RANKING.alpha, RANKING.seed_floor, RANKING.iters, RANKING.tol, RANKING.k) == (0.5, None, 30, 0.0, 10)
+    # the scale-aware floor: 4 up to ~16k series, the null max of P*M series beyond (C2 4.369, C4 5.286)
+    assert RANKING.floor(2000, 8) == 4.003 and RANKING.floor(1000, 8) == 4.0
+    assert RANKING.floor(10_000, 8) == 4.369 and RANKING.floor(1_000_000, 8) == 5.286
     c = Coordinator(None, engine=object())
     assert c.rank_config is RANKING
     assert (c.metrics_agent.window, c.metrics_agent.z_threshold) == (RANKING.window, RANKING.z_threshold)
@@ -49,7 +52,7 @@ def test_oracle_ppr_matches_networkx_meshes(meshes, name):
     e, s = meshes[f"{name}_edges"], meshes[f"{name}_seed"]
     n = len(s)
     rp, col, od = _csr(e, n)
-    rf, r, it, q = oracle.c_ppr(rp, col, od, s, RANKING.alpha, RANKING.iters, 0.0, RANKING.seed_floor,
+    rf, r, it, q = oracle.c_ppr(rp, col, od, s, RANKING.alpha, RANKING.iters, 0.0, 4.0,  # the floor the goldens were captured at
                                 return_q=True)
     x = r.astype(np.float64) / 2.0 ** 60
     ref = meshes[f"{name}_rank"]
@@ -82,7 +85,7 @@ def test_c2mini_oracle_outputs():
     assert np.array_equal(sc["n_exceed"], g["n_exceed_f64"])  # no sample within rounding of |z| = 3
     # a10 under the ranking definition, against networkx
     rp, col, od = _csr(e, C.P)
-    rf, r, it, q = oracle.c_ppr(rp, col, od, g["score"], RANKING.alpha, RANKING.iters, 0.0, RANKING.seed_floor,
+    rf, r, it, q = oracle.c_ppr(rp, col, od, g["score"], RANKING.alpha, RANKING.iters, 0.0, 4.0,
                                 return_q=True)
     xr = r.astype(np.float64) / 2.0 ** 60
     ref = g["ppr_rank"]
@@ -113,6 +116,6 @@ def test_coordinator_ranking_equals_bench_ranking_cpu():
     got = [int(r["component"].split("-")[-1]) for r in res["ranked_root_causes"]]
     score = oracle.c_rolling_score(x, RANKING.window)["score"]
     idx, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, RANKING.alpha, RANKING.iters,
-                                RANKING.seed_floor, RANKING.k)
+                                RANKING.floor(3000, 8), RANKING.k)
     assert got == idx.tolist()
     assert Config().as_dict() == RANKING.as_dict()

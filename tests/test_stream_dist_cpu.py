@@ -78,15 +78,17 @@ def test_sharded_stream_matches_oracle_chain(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     m, x = _mesh()
+    from krca.rca import Config
+    FLOOR = Config().floor(x.shape[1], x.shape[2])  # the scale-aware floor of krca.rca.Config
     r_ref, t = None, 0
     for wi, d in enumerate(WINDOWS):
         t += d
         score = oracle.c_rolling_score(x[:t], W)["score"]
         if r_ref is None:
-            _, r_ref, it = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, 4.0)
-            q_ = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, 4.0, return_q=True)[3]
+            _, r_ref, it = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, FLOOR)
+            q_ = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, FLOOR, return_q=True)[3]
         else:
-            r_ref, it, q_ = oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, score, r_ref, 0.5, 60, 1e-9, 4.0)
+            r_ref, it, q_ = oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, score, r_ref, 0.5, 60, 1e-9, FLOOR)
         top = oracle.topk_ref(oracle.c_rca_key(r_ref, q_), 10)[0].tolist()
         r_sh = np.concatenate([res[g][wi][0] for g in range(world)])
         assert np.array_equal(r_sh, r_ref), (world, wi)

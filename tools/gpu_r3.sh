@@ -29,6 +29,10 @@ prof() {  # prof NAME SECONDS ARGS... (rocprofv3 kernel-trace stats of python3 A
   local name=$1 secs=$2; shift 2
   step $name $secs rocprofv3 --kernel-trace --stats --output-format csv -d $O/$name -o run -- python3 "$@"
 }
+pmc() {  # pmc NAME WHAT COUNTERS... (one counter pass of tools/prof_kernels.py WHAT, its own kill timeout)
+  local name=$1 what=$2; shift 2
+  step $name 120 timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $O/$name -o run -- python3 tools/prof_kernels.py $what --reps 1
+}
 for s in "$@"; do
   case $s in
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread ;;
@@ -37,11 +41,30 @@ for s in "$@"; do
     bench_trace) prof bench_trace 400 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     corr100k) prof corr100k 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5 ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 --tau 0.5 ;;
+    corr_batch)  # C3 with the main pass in smaller batches: re-scores of batch b beside the tiles of b + 1
+      for b in 128 256 512; do
+        export KRCA_CORR_BATCH=$b; step corr_batch$b 300 python3 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5
+      done; unset KRCA_CORR_BATCH ;;
     ranking) step ranking 600 python3 -u tools/ranking_ablation_c4.py --seeds 2 --out $O/ranking_ablation_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
+    ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
+    ppr_nt) export KRCA_PPR_NT=1; prof ppr_nt 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_NT ;;
+    bench_nograph) export KRCA_RCA_GRAPH=0; step bench_nograph 300 python3 bench.py --no-cpu-baseline; unset KRCA_RCA_GRAPH ;;
+    bench2) step bench2 300 python3 bench.py --no-cpu-baseline ;;
+    tests_tmpl) step tests_tmpl 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread -k "template or tmpl or c2mini or c5 or stream" ;;
     logs) prof logs 300 tools/prof_kernels.py logs --reps 5 ;;
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
     c5) step c5 400 python3 -u tools/bench_stream.py ;;
+    pmc_ppr)
+      pmc pmc_ppr_sq ppr SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
+      pmc pmc_ppr_sq2 ppr SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD
+      pmc pmc_ppr_tcc ppr TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum
+      pmc pmc_ppr_tcp ppr TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum
+      pmc pmc_ppr_ea ppr TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum
+      pmc pmc_ppr_grbm ppr GRBM_GUI_ACTIVE GRBM_COUNT ;;
+    pmc_logs)
+      pmc pmc_logs_ea logs TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum
+      pmc pmc_logs_sq logs SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

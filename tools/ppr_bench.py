@@ -70,7 +70,7 @@ def main():
     if a.check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        _, r, _, q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, s, cfg.alpha, cfg.iters, 0.0, cfg.seed_floor,
+        _, r, _, q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, s, cfg.alpha, cfg.iters, 0.0, cfg.floor(len(s), 8),
                                   return_q=True)
         out["bit_identical"] = bool(np.array_equal(sh.r[:N].cpu().numpy(), r))
         idx, _ = step.merge(*sh.local_topk(cfg.k))
