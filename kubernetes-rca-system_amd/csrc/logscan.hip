@@ -680,6 +680,59 @@ __device__ __forceinline__ void sep_planes(uint32_t wprev, uint32_t w, uint32_t 
   l1 = two;
 }
 
+// high bits of the 4 bytes of f -> bits 0..3 (one multiply: the four partial products land on
+// distinct bits, no carries)
+__device__ __forceinline__ uint32_t gather4(uint32_t f) { return ((f & 0x80808080u) * 0x00204081u) >> 28; }
+
+// Line starts S and the separator-length planes L0 (lengths 1, 3) / L1 (lengths 2, 3) at the 16
+// positions q..q+15 of a piece, sep_before / sep_len restated on 16-bit masks: the byte tests run
+// once per byte of the piece (T(k) = test of byte q+k; bit -1 = byte q-1 from wp) and the "byte
+// before p" forms are those masks shifted by one -- instead of re-testing the shifted words
+// (sep_flags + sep_planes: ~390 vector instructions per piece and wave).  cs = container first
+// bytes at q-1+k (bit k): a "\r" there belongs to the previous container, so "\r\n" is not one
+// separator across it.
+__device__ __forceinline__ void piece_flags(uint32_t wp, const uint32_t (&w)[4], uint32_t cs, uint32_t& S,
+                                            uint32_t& L0, uint32_t& L1) {
+  uint32_t nl = 0, cr = 0, sep = 0;  // bit k: byte q+k is "\n" / "\r" / a one-byte separator
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    nl |= gather4(swar_eq(w[j], 0x0A)) << (4 * j);
+    cr |= gather4(swar_eq(w[j], 0x0D)) << (4 * j);
+    sep |= gather4(swar_range(w[j], 0x0A, 0x0D) | swar_range(w[j], 0x1C, 0x1E)) << (4 * j);
+  }
+  // bytes q-1, q-2 (bit 0, 1 of the "before" masks)
+  const uint32_t b1 = wp >> 24, b2 = (wp >> 16) & 0xFFu;
+  const uint32_t sep1 = (sep << 1) | (uint32_t)((b1 >= 0x0A && b1 <= 0x0D) || (b1 >= 0x1C && b1 <= 0x1E));  // byte p-1
+  const uint32_t cr1 = (cr << 1) | (uint32_t)(b1 == 0x0D);
+  const uint32_t nl1 = (nl << 1) | (uint32_t)(b1 == 0x0A);
+  const uint32_t cr2 = (cr << 2) | ((uint32_t)(b1 == 0x0D) << 1) | (uint32_t)(b2 == 0x0D);
+  S = (sep1 & ~(cr1 & nl)) & 0xFFFFu;
+  const uint32_t crlf = nl1 & cr2 & ~cs;  // "\r\n" ends at p-1 (length 2)
+  L0 = sep1 & ~crlf;
+  L1 = crlf;
+  if ((wp | w[0] | w[1] | w[2] | w[3]) & 0x80808080u) {  // U+0085 (C2 85), U+2028 / U+2029 (E2 80 A8/A9)
+    uint32_t c2 = 0, x85 = 0, e2 = 0, x80 = 0, a8 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c2 |= gather4(swar_eq(w[j], 0xC2)) << (4 * j);
+      x85 |= gather4(swar_eq(w[j], 0x85)) << (4 * j);
+      e2 |= gather4(swar_eq(w[j], 0xE2)) << (4 * j);
+      x80 |= gather4(swar_eq(w[j], 0x80)) << (4 * j);
+      a8 |= gather4(swar_eq(w[j], 0xA8) | swar_eq(w[j], 0xA9)) << (4 * j);
+    }
+    const uint32_t b3 = (wp >> 8) & 0xFFu;
+    const uint32_t two = ((x85 << 1) | (uint32_t)(b1 == 0x85)) & ((c2 << 2) | ((uint32_t)(b1 == 0xC2) << 1) | (uint32_t)(b2 == 0xC2));
+    const uint32_t three = ((a8 << 1) | (uint32_t)(b1 == 0xA8 || b1 == 0xA9)) &
+                           ((x80 << 2) | ((uint32_t)(b1 == 0x80) << 1) | (uint32_t)(b2 == 0x80)) &
+                           ((e2 << 3) | ((uint32_t)(b1 == 0xE2) << 2) | ((uint32_t)(b2 == 0xE2) << 1) | (uint32_t)(b3 == 0xE2));
+    S |= (two | three) & 0xFFFFu;
+    L0 |= three;
+    L1 |= two | three;
+  }
+  L0 &= 0xFFFFu;
+  L1 &= 0xFFFFu;
+}
+
 __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict__ text, int64_t nbytes,
                                                        const int64_t* __restrict__ doc_off, int64_t D,
                                                        const int32_t* __restrict__ chunk_doc,
@@ -718,22 +771,16 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
     }
     uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
     if (lane == 0) wp = q >= 4 && q <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q - 4) : 0u;
-    uint32_t S = high_bits4(sep_flags(wp, w[0])) | (high_bits4(sep_flags(w[0], w[1])) << 4) |
-                 (high_bits4(sep_flags(w[1], w[2])) << 8) | (high_bits4(sep_flags(w[2], w[3])) << 12);
     uint32_t C = 0;  // container first bytes at q-1+j, j = 0..16 (non-empty containers only)
+    if (q < nbytes) C = piece_container_starts(s_cs, tile0, q);
+    uint32_t S, l0, l1;
+    piece_flags(wp, w, C & 0xFFFFu, S, l0, l1);
     if (q < nbytes) {
-      C = piece_container_starts(s_cs, tile0, q);
       S |= C >> 1;
       if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
     } else {
       S = 0;
     }
-    uint32_t a0, b0, a1, b1, a2, b2, a3, b3;
-    sep_planes(wp, w[0], C & 0xFu, a0, b0);
-    sep_planes(w[0], w[1], (C >> 4) & 0xFu, a1, b1);
-    sep_planes(w[1], w[2], (C >> 8) & 0xFu, a2, b2);
-    sep_planes(w[2], w[3], (C >> 12) & 0xFu, a3, b3);
-    const uint32_t l0 = a0 | (a1 << 4) | (a2 << 8) | (a3 << 12), l1 = b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
     s_sl[it * TPB + threadIdx.x] = S | ((l0 & S) << 16);
     s_l1[it * TPB + threadIdx.x] = (uint16_t)(l1 & S);
     uint32_t c = __popc(S);

@@ -68,7 +68,7 @@ struct Ctl {          // device control block (header of the ctl buffer)
   int32_t iter;       // iterations done
   uint32_t done;      // single device, reduction fused: workgroups of the running step that finished
 };
-// ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n].  The long-row
+// ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n] (8-byte slots) | double coef[n].  The long-row
 // accumulators and tickets are zero when allocated and reset by the last chunk of each row.
 
 __device__ __forceinline__ int64_t* acc_long_of(Ctl* ctl) {
@@ -76,6 +76,11 @@ __device__ __forceinline__ int64_t* acc_long_of(Ctl* ctl) {
 }
 __device__ __forceinline__ uint32_t* ticket_of(Ctl* ctl, int64_t n) {
   return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctl) + CTL_BYTES + 8 * n);
+}
+// per-row edge coefficient alpha / outdeg (0 for a dangling row), written by the solve's init:
+// the step multiplies instead of dividing per row and iteration
+__device__ __forceinline__ double* coef_of(Ctl* ctl, int64_t n) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(ctl) + CTL_BYTES + 16 * n);
 }
 
 __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
@@ -102,6 +107,11 @@ __device__ __forceinline__ int64_t edge_weight(int64_t rj, int32_t deg, double a
   const double coef = alpha / (double)deg;
   return (int64_t)((double)rj * coef);
 }
+__device__ __forceinline__ double edge_coef(int32_t deg, double alpha) { return deg == 0 ? 0.0 : alpha / (double)deg; }
+// the same weight from the row's coefficient (coef = alpha / deg exactly as above; 0: dangling)
+__device__ __forceinline__ int64_t edge_weight_c(int64_t rj, double coef) {
+  return coef == 0.0 ? 0 : (int64_t)((double)rj * coef);
+}
 
 
 __device__ __forceinline__ int64_t quantise(float s, float floor_) {
@@ -113,7 +123,7 @@ __device__ __forceinline__ int64_t quantise(float s, float floor_) {
 __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, float seed_floor,
                                                 const int32_t* __restrict__ outdeg, int64_t n, int64_t N,
                                                 double alpha, int64_t* __restrict__ q, int64_t* __restrict__ r,
-                                                int64_t* __restrict__ send, int64_t n_max) {
+                                                int64_t* __restrict__ send, int64_t n_max, double* __restrict__ coef) {
   __shared__ int64_t red[TPB / 64];
   const int64_t r0 = (int64_t)(krca::kFix / (double)N);
   int64_t dang = 0, qs = 0;
@@ -123,6 +133,7 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
     q[i] = qi;
     qs += qi;
     r[i] = r0;
+    coef[i] = edge_coef(deg, alpha);
     reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(r0, deg, alpha));
     if (deg == 0) dang += r0;
   }
@@ -139,7 +150,7 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
 __global__ __launch_bounds__(TPB) void ppr_init_warm(const float* __restrict__ seed, float seed_floor,
                                                      const int32_t* __restrict__ outdeg, int64_t n, double alpha,
                                                      int64_t* __restrict__ q, const int64_t* __restrict__ r,
-                                                     int64_t* __restrict__ send, int64_t n_max) {
+                                                     int64_t* __restrict__ send, int64_t n_max, double* __restrict__ coef) {
   __shared__ int64_t red[TPB / 64];
   int64_t dang = 0, qs = 0;
   for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
@@ -148,6 +159,7 @@ __global__ __launch_bounds__(TPB) void ppr_init_warm(const float* __restrict__ s
     q[i] = qi;
     qs += qi;
     const int64_t ri = r[i];
+    coef[i] = edge_coef(deg, alpha);
     reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(ri, deg, alpha));
     if (deg == 0) dang += ri;
   }
@@ -160,8 +172,8 @@ __global__ __launch_bounds__(TPB) void ppr_init_warm(const float* __restrict__ s
 }
 
 struct StepScalars {
-  double tele, qtot, uni, alpha;
-  int64_t qt;
+  double tele, tq, alpha;  // tq = tele / q_total: t_i = q_i * tq (no per-row division)
+  int64_t qt, tu;          // tu: the uniform share when every seed is at the floor
 };
 
 // Single device (G = 1): the iteration's reduction runs in the step kernel's last workgroup
@@ -202,16 +214,15 @@ __device__ void reduce_single(const int64_t* slice_slots, int64_t* next_slots, d
 // = the L1 stop rule needs |r_new - r_old| (ro was loaded), PPR_WRITE_R = store r_new (every
 // iteration under a tolerance; only the last one of a fixed-iteration solve).
 template <int FLAGS>
-__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi, int64_t ro, int32_t deg,
+__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi, int64_t ro, double coef,
                                            const StepScalars& k, int64_t* __restrict__ r,
                                            int64_t* __restrict__ send, int64_t& err, int64_t& dang) {
-  const double pd = k.qt > 0 ? (double)qi / k.qtot : k.uni;
-  const int64_t t = (int64_t)(pd * k.tele);
+  const int64_t t = k.qt > 0 ? (int64_t)((double)qi * k.tq) : k.tu;
   const int64_t rn = pulled + t;
   if (FLAGS & PPR_WRITE_R) r[i] = rn;
   if (FLAGS & PPR_RESIDUAL) err += rn > ro ? rn - ro : ro - rn;
-  if (deg == 0) dang += rn;
-  reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(rn, deg, k.alpha));
+  if (coef == 0.0) dang += rn;
+  reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight_c(rn, coef));
 }
 
 // One plan entry, loaded in two parts so that a prefetched value is never copied or computed on
@@ -237,7 +248,7 @@ struct Head {
 struct Rows {
   int64_t my_off, my_end;  // row_ptr of the lane's row and the next (absolute; short blocks)
   int64_t my_q, my_r;
-  int32_t my_deg;
+  double my_coef;  // alpha / outdeg (coef_of)
   uint32_t li;  // krca_ppr_pack lane info: (row holding edge 8t) << 8 | head bits of edges 8t .. 8t+7
   uint4 ix;     // dictionary blocks: the slots of edges 8t .. 8t+7 (uint16 pairs)
 };
@@ -271,7 +282,7 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
 template <int FLAGS>
 __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16_t* __restrict__ lane_info,
                                           const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk,
-                                          const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q,
+                                          const double* __restrict__ coef, const int64_t* __restrict__ q,
                                           const int64_t* __restrict__ r, Rows& R) {
   const int tid = threadIdx.x;
   const int nrows = m.code > 0 ? m.code - m.rb : 1;
@@ -281,7 +292,7 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
   R.my_end = ld_stream<NT>(row_ptr + my_row + 1);
   R.my_q = ld_stream<NT>(q + my_row);
   R.my_r = (FLAGS & PPR_RESIDUAL) ? ld_stream<NT>(r + my_row) : 0;
-  R.my_deg = ld_stream<NT>(outdeg + my_row);
+  R.my_coef = ld_stream<NT>(coef + my_row);
   R.li = ld_stream<NT>(lane_info + b * TPB + tid);  // zero for long-row chunks
   // unconditional 16-byte load (used by dictionary blocks only): in-bounds, 16-byte aligned
   const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
@@ -290,10 +301,16 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
   R.ix = make_uint4(ix.x, ix.y, ix.z, ix.w);
 }
 
+// every lane gathers all SEG columns (past the block's count, load_head clamped the column to its
+// last one: a valid address, the value is dropped by the select), so the 8 loads issue back to
+// back instead of one exec-masked branch each
 __device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict__ w, uint32_t (&v)[SEG]) {
   const int64_t lim = H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0;
+  uint32_t g[SEG];
 #pragma unroll
-  for (int j = 0; j < SEG; ++j) v[j] = threadIdx.x + j * TPB < lim ? w[H.c[j]] : 0;
+  for (int j = 0; j < SEG; ++j) g[j] = w[H.c[j]];
+#pragma unroll
+  for (int j = 0; j < SEG; ++j) v[j] = threadIdx.x + j * TPB < lim ? g[j] : 0u;
 }
 
 // Persistent, software-pipelined step.  Workgroup g takes plan entries g, g + G, g + 2G, ...;
@@ -333,8 +350,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   StepScalars k;
   k.tele = ctl->tele;
   k.qt = ctl->q_total;
-  k.qtot = (double)k.qt;
-  k.uni = 1.0 / (double)N;
+  k.tq = k.tele / (double)k.qt;
+  k.tu = (int64_t)((1.0 / (double)N) * k.tele);
   k.alpha = alpha;
   const int tid = threadIdx.x;
   Head H0, H1;
@@ -342,10 +359,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   load_head<(FLAGS & PPR_NT) != 0>(plan, b, pk, H0);
   uint32_t v[SEG];  // codes: decoded where summed (a prefetched register is never computed on early)
   gather(H0, w, v);
-  load_rows<FLAGS>(H0.m, b, lane_info, row_ptr, pk, outdeg, q, r, R0);
+  const double* coef = coef_of(ctl, n);
+  load_rows<FLAGS>(H0.m, b, lane_info, row_ptr, pk, coef, q, r, R0);
   Meta cur = H0.m;
   int64_t b1 = b + gridDim.x;
-  if (b1 < nblk) load_head<(FLAGS & PPR_NT) != 0>(plan, b1, pk, H1);
+  // prefetches past the workgroup's last entry load the grid's last entry again (clamped, results
+  // unused): every path issues the same loads, so the compiler's vector-memory waits stay counted
+  // (vmcnt(N)) instead of vmcnt(0) at the join of an `if (b1 < nblk)`, which made the sum phase
+  // wait for the NEXT entry's gathers and rows and undid the software pipeline
+  load_head<(FLAGS & PPR_NT) != 0>(plan, b1 < nblk ? b1 : nblk - 1, pk, H1);
   int64_t err = 0, dang = 0;
 #ifdef PPR_TIMING
   uint64_t tacc[5] = {0, 0, 0, 0, 0};
@@ -363,12 +385,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     const bool dict = cur.nu > 0;
     int64_t sacc_long = 0;
     if (shortb) {
-      const int nst = dict ? cur.nu : ne;  // staged values: slots or edges
+      // every lane stores all SEG values (EDGE_BUDGET slots; the gathers past the block's staged
+      // count returned 0 and the sum reads only slots / edges of the block): no divergent store
+      // per value (each cost an exec-mask save / branch / restore: ~32 scalar + vector
+      // instructions per entry)
 #pragma unroll
-      for (int j = 0; j < SEG; ++j) {
-        const int e = tid + j * TPB;
-        if (e < nst) vals[e] = v[j];
-      }
+      for (int j = 0; j < SEG; ++j) vals[tid + j * TPB] = v[j];
       if (tid < cur.code - cur.rb && rc.my_end > rc.my_off)  // a non-empty row: its index at its first edge
         headrow[(int)(rc.my_off - cur.e0)] = (uint8_t)tid;
       rowsum[tid] = 0ull;
@@ -379,11 +401,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     // v is free: gathers and rows of the next entry, head of the one after
     const int64_t b2 = b1 + gridDim.x;
     const Meta next = hn.m;
-    if (b1 < nblk) {
-      gather(hn, w, v);
-      load_rows<FLAGS>(next, b1, lane_info, row_ptr, pk, outdeg, q, r, rn);
-    }
-    if (b2 < nblk) load_head<(FLAGS & PPR_NT) != 0>(plan, b2, pk, hl);
+    gather(hn, w, v);
+    load_rows<FLAGS>(next, b1 < nblk ? b1 : nblk - 1, lane_info, row_ptr, pk, coef, q, r, rn);
+    load_head<(FLAGS & PPR_NT) != 0>(plan, b2 < nblk ? b2 : nblk - 1, pk, hl);
     if (shortb) {
       const int nrows = cur.code - cur.rb;
       __syncthreads();
@@ -394,29 +414,32 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
         int row = (int)(rc.li >> 8);        // the row holding edge a
         const uint2 hr = *reinterpret_cast<const uint2*>(headrow + a);  // rows at the lane's heads
         const uint4 sx = rc.ix;  // this lane's own slots (prefetched with the rows)
-        int64_t x[SEG];
+        // the 8 LDS reads are unconditional (a slot past the block's edges is clamped into the
+        // table and its value dropped by the select), so they issue back to back: a read under a
+        // per-edge branch was a branch with its own lgkmcnt(0) wait, 8 dependent LDS round trips
+        uint32_t c[SEG];
 #pragma unroll
         for (int kk = 0; kk < SEG; ++kk) {
           const uint32_t wd = kk < 2 ? sx.x : kk < 4 ? sx.y : kk < 6 ? sx.z : sx.w;
           const int sl = dict ? (int)((wd >> (16 * (kk & 1))) & 0xFFFFu) : a + kk;
-          x[kk] = a + kk < ne ? wdec(vals[sl]) : 0;
+          c[kk] = vals[sl & (EDGE_BUDGET - 1)];
         }
         int64_t sacc = 0;
 #pragma unroll
         for (int kk = 0; kk < SEG; ++kk) {
           if (kk > 0 && ((M >> kk) & 1u)) {
-            if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);  // no return: no wait
+            atomicAdd(&rowsum[row], (unsigned long long)sacc);  // no return: no wait
             sacc = 0;
             row = (int)(((kk < 4 ? hr.x : hr.y) >> (8 * (kk & 3))) & 0xFFu);
           }
-          sacc += x[kk];
+          sacc += a + kk < ne ? wdec(c[kk]) : 0;
         }
-        if (sacc) atomicAdd(&rowsum[row], (unsigned long long)sacc);
+        atomicAdd(&rowsum[row], (unsigned long long)sacc);
       }
       __syncthreads();
       PPR_T(1);
       if (tid < nrows)
-        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[tid], rc.my_q, rc.my_r, rc.my_deg, k, r, send, err, dang);
+        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[tid], rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
       __syncthreads();  // rowsum / vals / headrow are rewritten by the next entry
       PPR_T(2);
     } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
@@ -434,7 +457,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
           const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          update_row<FLAGS>(rb, pulled, rc.my_q, rc.my_r, rc.my_deg, k, r, send, err, dang);
+          update_row<FLAGS>(rb, pulled, rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
         }
       }
       PPR_T(3);
@@ -527,6 +550,10 @@ __global__ __launch_bounds__(TPB) void remap_cols(const int32_t* __restrict__ co
   }
 }
 
+double* host_coef(void* ctl, int64_t n) {  // coef_of on the host side of the ctl layout
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(ctl) + CTL_BYTES + 16 * n);
+}
+
 unsigned grid_for(int64_t n, int64_t cap = 2048) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(n, TPB), cap));
 }
@@ -536,7 +563,7 @@ unsigned grid_for(int64_t n, int64_t cap = 2048) {
 extern "C" {
 
 
-int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 16 * std::max<int64_t>(n_local, 1); }
+int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 24 * std::max<int64_t>(n_local, 1); }
 
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream) {
   KRCA_CHECK_ARG(E >= 0 && n_max > 0, "krca_ppr_remap_cols: bad sizes");
@@ -558,7 +585,7 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
   KRCA_HIP(hipMemsetAsync(send + wslots(n_max), 0, NSLOT * sizeof(int64_t), st));
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N,
-                       alpha, q_local, r_local, send, n_max);
+                       alpha, q_local, r_local, send, n_max, host_coef(ctl, n_local));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -575,7 +602,7 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
   KRCA_HIP(hipMemsetAsync(send + wslots(n_max), 0, NSLOT * sizeof(int64_t), st));
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init_warm, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local,
-                       alpha, q_local, r_local, send, n_max);
+                       alpha, q_local, r_local, send, n_max, host_coef(ctl, n_local));
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

@@ -272,27 +272,26 @@ class DeviceShard:
 
 
 def graph_default(comm, cfg, shard=None):
-    """Whether RcaStep captures its PageRank solve in a HIP graph by default: fixed-iteration solves
-    (tol <= 0: no host read-back between iterations) on one device.  Sharded solves (an RCCL
-    all-gather per iteration) stay eager unless KRCA_RCA_GRAPH=1; KRCA_RCA_GRAPH=0 turns it off."""
+    """Whether RcaStep captures its PageRank solve in a HIP graph: only with KRCA_RCA_GRAPH=1, for
+    fixed-iteration solves (tol <= 0: no host read-back between iterations) of a device shard.
+    Measured at C4 on one MI355X (`profiles/r3/bench_graph_ab.txt`): the replayed graph ran the
+    step 0.26 ms and the one-step latency 0.2 ms SLOWER than the eager launches -- the ~13 us per
+    iteration between the step kernels is the GPU's dependent-kernel boundary, not host time -- so
+    eager is the default."""
     import os
-    env = os.environ.get("KRCA_RCA_GRAPH")
-    if cfg.tol > 0 or env == "0" or not isinstance(shard, DeviceShard):
+    if os.environ.get("KRCA_RCA_GRAPH") != "1" or cfg.tol > 0 or not isinstance(shard, DeviceShard):
         return False
-    if comm.world == 1:
-        return True
-    return env == "1"
+    return True
 
 
 class RcaStep:
     """One rank's view of the pod-sharded RCA step.
 
-    With `graph` (default: :func:`graph_default`) the whole PageRank solve (init, exchange,
+    With `graph` (default: :func:`graph_default`, off) the whole PageRank solve (init, exchange,
     first reduce, iters x (step, exchange, reduce)) is captured once into a HIP graph on the
-    shard's fixed buffers and replayed per step: one launch instead of ~2 host calls per iteration
-    (at C4 the host-side gaps were ~0.4 ms of the 1.75 ms solve).  Replays compute exactly the
-    eager sequence: the captured kernels and pointers are the same (G = 1's ping-pong swaps are
-    baked into the capture)."""
+    shard's fixed buffers and replayed per step: one launch instead of ~2 host calls per iteration.
+    Replays compute exactly the eager sequence: the captured kernels and pointers are the same
+    (G = 1's ping-pong swaps are baked into the capture)."""
 
     def __init__(self, shard, comm, cfg, offset, graph=None):
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset

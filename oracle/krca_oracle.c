@@ -129,11 +129,12 @@ int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t
       acc[i] = s;
     }
     int64_t err = 0, dn = 0;
-    const double qd = (double)qtot;
-    const double uni = 1.0 / (double)N;
+    /* teleport share t_i = q_i * (tele / qtot) (csrc/ppr.hip update_row: one scale per iteration,
+       no per-row division); uniform 1/N when every seed is at the floor */
+    const double tq = tele / (double)qtot;
+    const int64_t tu = (int64_t)((1.0 / (double)N) * tele);
     for (int64_t i = 0; i < N; ++i) {
-      const double pd = qtot > 0 ? (double)q[i] / qd : uni;
-      const int64_t t = (int64_t)(pd * tele);
+      const int64_t t = qtot > 0 ? (int64_t)((double)q[i] * tq) : tu;
       const int64_t rn = acc[i] + t;
       const int64_t ro = r[i];
       r[i] = rn;

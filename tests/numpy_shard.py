@@ -79,8 +79,10 @@ class NumpyShard:
         acc = np.zeros(self.n, np.int64)
         np.add.at(acc, self.rows, _wdec(w[self.col]))
         qt = self.ctl["q_total"]
-        pd = self.q.astype(np.float64) / float(qt) if qt > 0 else np.full(self.n, 1.0 / float(self.N))
-        t = (pd * self.ctl["tele"]).astype(np.int64)
+        tele = self.ctl["tele"]
+        # t_i = q_i * (tele / qtot) (csrc/ppr.hip update_row), uniform 1/N when every seed is at the floor
+        t = ((self.q.astype(np.float64) * (tele / float(qt))).astype(np.int64) if qt > 0
+             else np.full(self.n, np.int64((1.0 / float(self.N)) * tele), np.int64))
         rn = acc + t
         err = int(np.abs(rn - self.r).sum())
         self.r = rn
