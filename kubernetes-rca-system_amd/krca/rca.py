@@ -126,6 +126,7 @@ class Comm:
 
     def __init__(self, world=1, rank=0, group=None):
         self.world, self.rank, self.group = world, rank, group
+        self._gloo = None  # the backend, looked up once
 
     def exchange(self, shard):
         """Make every rank's send slice visible in shard.w_all (G = 1: swap the ping-pong pair)."""
@@ -139,15 +140,20 @@ class Comm:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             return
-        all_gather_flat(out, inp, self.world, self.group)
+        if self._gloo is None:
+            import torch.distributed as dist
+            self._gloo = dist.get_backend(self.group) == "gloo"
+        all_gather_flat(out, inp, self.world, self.group, self._gloo)
 
 
-def all_gather_flat(out, inp, world, group=None):
+def all_gather_flat(out, inp, world, group=None, gloo=None):
     """out[world * inp.numel()] <- every rank's inp.  RCCL ("nccl") gathers into the flat tensor
     directly; gloo has no all_gather_into_tensor, so it takes the list form.  Chosen once from the
     backend, so a real RCCL failure (timeout, size mismatch) propagates instead of being retried."""
     import torch.distributed as dist
-    if dist.get_backend(group) == "gloo":
+    if gloo is None:
+        gloo = dist.get_backend(group) == "gloo"
+    if gloo:
         dist.all_gather(list(out.view(world, -1).unbind(0)), inp, group=group)
     else:
         dist.all_gather_into_tensor(out, inp, group=group)
@@ -179,11 +185,21 @@ class DeviceShard:
         self.w_all = torch.zeros((1 if world == 1 else world) * slice_words(n_max), **i64)
         self.ctl = torch.zeros(lib.krca_ppr_ctl_size(self.n), dtype=torch.uint8, device=dev)
         self.score_out = None
-        # one device: the iteration's reduction runs in the step kernel's last workgroup
-        # (krca_ppr_solo_step); reduce(first=0) is then a no-op.  Its tolerance is the one of the
-        # solve's first reduce(first=1).
+        # one device: krca_ppr_solo_step launches the step and its reduction (in the step's last
+        # workgroup under KRCA_PPR_FUSE); reduce(first=0) is then a no-op.  Its tolerance is the one
+        # of the solve's first reduce(first=1).
         self.fused = world == 1 and n_max == N
         self._tol = 0.0
+        # ctypes argument tuples of the per-iteration calls, keyed by the buffers / scalars / stream
+        # they bind (at 8 ranks a step is ~5 us of GPU work: rebuilding ~17 ctypes objects per
+        # call was host time on the critical path)
+        self._argc = {}
+
+    def _cached(self, key, build):
+        a = self._argc.get(key)
+        if a is None:
+            a = self._argc[key] = build()
+        return a
 
     def _chk(self, rc, what):
         from .native import _check
@@ -241,26 +257,32 @@ class DeviceShard:
     def step(self, alpha, flags=3):
         """flags: krca_ppr_shard_step's KRCA_PPR_RESIDUAL (1) | KRCA_PPR_WRITE_R (2)."""
         e, p = self.eng, self.eng.ptr
-        if self.plan_len and self.fused:
-            self._chk(e.lib.krca_ppr_solo_step(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len, p(self.lane),
-                                               p(self.w_all), p(self.outdeg), p(self.q), self.N, float(alpha), int(flags),
-                                               float(self._tol), p(self.r), p(self.send), p(self.ctl), e._stream()),
-                      "krca_ppr_solo_step")
-        elif self.plan_len:
-            self._chk(e.lib.krca_ppr_shard_step(p(self.row_ptr), p(self.col), p(self.plan), self.plan_len,
-                                                p(self.lane), p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
-                                                float(alpha), int(flags), p(self.r), p(self.send), p(self.ctl),
-                                                e._stream()), "krca_ppr_shard_step")
+        if not self.plan_len:
+            return
+        st = e._stream()
+        key = ("step", self.w_all.data_ptr(), self.send.data_ptr(), float(alpha), int(flags), float(self._tol), st.value)
+        if self.fused:
+            args = self._cached(key, lambda: (p(self.row_ptr), p(self.col), p(self.plan), self.plan_len, p(self.lane),
+                                              p(self.w_all), p(self.outdeg), p(self.q), self.N, float(alpha), int(flags),
+                                              float(self._tol), p(self.r), p(self.send), p(self.ctl), st))
+            self._chk(e.lib.krca_ppr_solo_step(*args), "krca_ppr_solo_step")
+        else:
+            args = self._cached(key, lambda: (p(self.row_ptr), p(self.col), p(self.plan), self.plan_len, p(self.lane),
+                                              p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
+                                              float(alpha), int(flags), p(self.r), p(self.send), p(self.ctl), st))
+            self._chk(e.lib.krca_ppr_shard_step(*args), "krca_ppr_shard_step")
 
     def reduce(self, alpha, tol, first):
         e, p = self.eng, self.eng.ptr
         if first:
             self._tol = float(tol)
         elif self.fused and self.plan_len:
-            return  # done by the step's last workgroup
-        self._chk(e.lib.krca_ppr_shard_reduce(p(self.w_all), self.world, self.n_max, self.N, float(alpha), float(tol),
-                                              int(first), p(self.ctl), p(self.send), e._stream()),
-                  "krca_ppr_shard_reduce")
+            return  # launched by krca_ppr_solo_step
+        st = e._stream()
+        key = ("reduce", self.w_all.data_ptr(), self.send.data_ptr(), float(alpha), float(tol), int(first), st.value)
+        args = self._cached(key, lambda: (p(self.w_all), self.world, self.n_max, self.N, float(alpha), float(tol),
+                                          int(first), p(self.ctl), p(self.send), st))
+        self._chk(e.lib.krca_ppr_shard_reduce(*args), "krca_ppr_shard_reduce")
 
     def local_topk(self, k):
         e, p = self.eng, self.eng.ptr
