@@ -236,7 +236,9 @@ int64_t krca_ppr_ctl_size(int64_t n_local);
  * pk must have 64 zero words of padding past E (the step issues clamped 16-byte loads).  lane_host
  * [krca_ppr_lane_size(plan_len)] uint16: per block and lane t, (row holding edge 8t) << 8 | the
  * bits of the edges 8t .. 8t+7 that start a non-empty row (the step's segmented row sums need no
- * search).  Returns the number of dictionary blocks (>= 0) or a negative error.
+ * search).  Returns the number of dictionary blocks (>= 0) or a negative error (KRCA_EINVAL for a
+ * column outside [0, N) or a remapped column id >= 2^30: the step addresses the gathered table at
+ * 32-bit byte offsets).
  * (KRCA_PPR_DICT=0 packs every block direct; krca_ppr_remap_cols remaps a column array alone.) */
 int64_t krca_ppr_lane_size(int64_t plan_len);
 int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,

@@ -243,7 +243,7 @@ struct Meta {
 };
 struct Head {
   Meta m;
-  int32_t c[SEG];
+  uint32_t c[SEG];  // remapped columns (uint32 units of the exchange layout)
 };
 struct Rows {
   int64_t my_off, my_end;  // row_ptr of the lane's row and the next (absolute; short blocks)
@@ -267,15 +267,18 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
   H.m.code = (int32_t)pe[1];
   H.m.e0 = pe[2];
   H.m.e1 = pe[3];
-  const int tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
   // every lane loads (clamped index; gather() masks the lanes past lim): a predicated default
-  // value would have to wait for whatever load last wrote that register
-  const int64_t lim = H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0;
-  const int64_t top = lim > 0 ? lim - 1 : 0;
+  // value would have to wait for whatever load last wrote that register.  Indices are 32-bit
+  // offsets from a wave-uniform base, so each load is one `global_load ... v_off, s[base]`
+  // (a 64-bit per-lane address cost 2-3 vector instructions per load)
+  const uint32_t lim = (uint32_t)(H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0);
+  const uint32_t top = lim > 0 ? lim - 1 : 0;
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(pk) + H.m.e0;
 #pragma unroll
   for (int j = 0; j < SEG; ++j) {
-    const int64_t u = tid + j * TPB;
-    H.c[j] = ld_stream<NT>(pk + H.m.e0 + (u < top ? u : top));
+    const uint32_t u = tid + j * TPB;
+    H.c[j] = ld_stream<NT>(base + (u < top ? u : top));
   }
 }
 
@@ -284,20 +287,22 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
                                           const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk,
                                           const double* __restrict__ coef, const int64_t* __restrict__ q,
                                           const int64_t* __restrict__ r, Rows& R) {
-  const int tid = threadIdx.x;
-  const int nrows = m.code > 0 ? m.code - m.rb : 1;
-  const int64_t my_row = m.rb + (tid < nrows ? tid : 0);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nrows = (uint32_t)(m.code > 0 ? m.code - m.rb : 1);
+  const uint32_t off = tid < nrows ? tid : 0;  // the lane's row, from the block's first (wave-uniform base)
   constexpr bool NT = (FLAGS & PPR_NT) != 0;
-  R.my_off = ld_stream<NT>(row_ptr + my_row);
-  R.my_end = ld_stream<NT>(row_ptr + my_row + 1);
-  R.my_q = ld_stream<NT>(q + my_row);
-  R.my_r = (FLAGS & PPR_RESIDUAL) ? ld_stream<NT>(r + my_row) : 0;
-  R.my_coef = ld_stream<NT>(coef + my_row);
+  const int64_t* rp = row_ptr + m.rb;
+  R.my_off = ld_stream<NT>(rp + off);
+  R.my_end = ld_stream<NT>(rp + off + 1);
+  R.my_q = ld_stream<NT>(q + m.rb + off);
+  R.my_r = (FLAGS & PPR_RESIDUAL) ? ld_stream<NT>(r + m.rb + off) : 0;
+  R.my_coef = ld_stream<NT>(coef + m.rb + off);
   R.li = ld_stream<NT>(lane_info + b * TPB + tid);  // zero for long-row chunks
   // unconditional 16-byte load (used by dictionary blocks only): in-bounds, 16-byte aligned
   const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 ix = ld_stream<NT>(reinterpret_cast<const u32x4*>(pk + wb + (tid * SEG < m.e1 - m.e0 ? tid * (SEG / 2) : 0)));
+  const u32x4* ixb = reinterpret_cast<const u32x4*>(pk + wb);
+  const u32x4 ix = ld_stream<NT>(ixb + (tid * SEG < (uint32_t)(m.e1 - m.e0) ? tid : 0u));
   R.ix = make_uint4(ix.x, ix.y, ix.z, ix.w);
 }
 
@@ -305,10 +310,11 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
 // last one: a valid address, the value is dropped by the select), so the 8 loads issue back to
 // back instead of one exec-masked branch each
 __device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict__ w, uint32_t (&v)[SEG]) {
-  const int64_t lim = H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0;
+  const uint32_t lim = (uint32_t)(H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0);
   uint32_t g[SEG];
 #pragma unroll
-  for (int j = 0; j < SEG; ++j) g[j] = w[H.c[j]];
+  for (int j = 0; j < SEG; ++j)  // 32-bit byte offsets (krca_ppr_pack keeps remapped columns < 2^30)
+    g[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w) + (H.c[j] << 2));
 #pragma unroll
   for (int j = 0; j < SEG; ++j) v[j] = threadIdx.x + j * TPB < lim ? g[j] : 0u;
 }

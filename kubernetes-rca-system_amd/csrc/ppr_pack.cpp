@@ -152,8 +152,12 @@ int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int6
   KRCA_CHECK_ARG(E == 0 || col_host, "krca_ppr_pack: null col");
   int rc = krca_ppr_plan(row_ptr_host, N, plan_host, plan_len);
   if (rc) return rc;
-  for (int64_t e = 0; e < E; ++e)
+  for (int64_t e = 0; e < E; ++e) {
     KRCA_CHECK_ARG(col_host[e] >= 0, "krca_ppr_pack: negative column at edge %lld", (long long)e);
+    // the step gathers at 32-bit byte offsets of the exchange table
+    KRCA_CHECK_ARG(remap_col(col_host[e], n_max) < (int64_t(1) << 30), "krca_ppr_pack: column %lld past the 2^30-word table",
+                   (long long)col_host[e]);
+  }
   return pack_blocks(row_ptr_host, col_host, N, n_max, plan_host, plan_len, pk_host, lane_host);
 }
 

@@ -49,6 +49,7 @@ for s in "$@"; do
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
     ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
     ppr_w5) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_w5.so; prof ppr_w5 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
+    ppr_prev) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_prev.so; prof ppr_prev 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_nt) export KRCA_PPR_NT=1; prof ppr_nt 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_NT ;;
     bench_nograph) export KRCA_RCA_GRAPH=0; step bench_nograph 300 python3 bench.py --no-cpu-baseline; unset KRCA_RCA_GRAPH ;;
     bench2) step bench2 300 python3 bench.py --no-cpu-baseline ;;
