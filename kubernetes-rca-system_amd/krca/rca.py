@@ -214,19 +214,45 @@ class DeviceShard:
         self.M = int(M)
         if P != self.n:
             raise ValueError(f"stream window has {P} pods, the shard owns {self.n}")
-        if getattr(self, "_stream_state", None) is None:
-            nbytes = e.lib.krca_stream_state_size(P, M, self.cfg.window, horizon)
-            dev = e.device
-            self._stream_state = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
-            self.score_out = dict(z_last=torch.empty((max(P, 1), M), dtype=torch.float32, device=dev),
-                                  score=torch.empty(max(P, 1), dtype=torch.float32, device=dev),
-                                  n_exceed=torch.empty(max(P, 1), dtype=torch.int32, device=dev),
-                                  flags=torch.empty(max(P, 1), dtype=torch.uint8, device=dev))
+        self._ensure_stream(int(M), horizon)
         o = self.score_out
         self._chk(e.lib.krca_stream_score(p(x_new), P, M, int(d), int(t0), self.cfg.window, int(horizon),
                                           float(self.cfg.z_threshold), p(self._stream_state), p(o["z_last"]), p(o["score"]),
                                           p(o["n_exceed"]), p(o["flags"]), e._stream()), "krca_stream_score")
         return o
+
+    def _ensure_stream(self, M, horizon):
+        """The rolling state (krca_stream_state_size bytes) and the score outputs, allocated once."""
+        torch, e = self.torch, self.eng
+        if getattr(self, "_stream_state", None) is not None:
+            return
+        P, dev = self.n, e.device
+        nbytes = e.lib.krca_stream_state_size(P, M, self.cfg.window, horizon)
+        self._stream_state = torch.zeros(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        self.score_out = dict(z_last=torch.empty((max(P, 1), M), dtype=torch.float32, device=dev),
+                              score=torch.empty(max(P, 1), dtype=torch.float32, device=dev),
+                              n_exceed=torch.empty(max(P, 1), dtype=torch.int32, device=dev),
+                              flags=torch.empty(max(P, 1), dtype=torch.uint8, device=dev))
+
+    # -- snapshots of the stream (krca.stream.StreamingRCA.snapshot / restore) --------------------
+    def state_dict(self, M, horizon):
+        """The rank's stream state as host arrays: the rolling state bytes (plain data:
+        krca_stream_state_size's float64 sums, sample ring and exceedance bits, no pointers) and the
+        ranks of the last solve (the next window's warm start)."""
+        self.M = int(M)
+        self._ensure_stream(self.M, horizon)
+        return dict(stream_state=self._stream_state.cpu().numpy(), r=self.r[:self.n].cpu().numpy())
+
+    def load_state_dict(self, st, M, horizon):
+        torch = self.torch
+        self.M = int(M)
+        self._ensure_stream(self.M, horizon)
+        ss, r = np.asarray(st["stream_state"], np.uint8), np.asarray(st["r"], np.int64)
+        if ss.shape != tuple(self._stream_state.shape) or r.shape != (self.n,):
+            raise ValueError(f"snapshot state {ss.shape} / ranks {r.shape} do not fit this shard "
+                             f"({tuple(self._stream_state.shape)} / ({self.n},))")
+        self._stream_state.copy_(torch.from_numpy(ss))
+        self.r[:self.n].copy_(torch.from_numpy(r))
 
     def init_warm(self, alpha, seed_floor):
         """Re-seed from the current scores, start from the ranks of the previous solve."""

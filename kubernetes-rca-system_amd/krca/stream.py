@@ -20,10 +20,19 @@ pull-CSR.
    Integer fixed point: each window's ranks are bit-identical to oracle/krca_oracle.c run on the
    same chain, for any G.
 
+4. Between windows a rank can snapshot its stream (rolling state, warm-start ranks, step count)
+   to a file and a new process restore it: the stream then continues bit for bit.
+
 The per-rank numeric work sits behind the shard interface of krca/rca.py (DeviceShard; the CPU
 tests drive the same orchestration with tests/numpy_shard.py over gloo).
 """
+import json
+
+import numpy as np
+
 from .rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
+
+SNAPSHOT_VERSION = 1
 
 
 class StreamingRCA:
@@ -96,6 +105,38 @@ class StreamingRCA:
         out["top"] = self.rerank()
         out["iters"] = self.last_iters
         return out
+
+    # -- 4. snapshots ----------------------------------------------------------------------------
+    def _meta(self):
+        return dict(version=SNAPSHOT_VERSION, shard=type(self.shard).__name__, N=self.N, M=self.M, H=self.H,
+                    lo=self.lo, hi=self.hi, n_max=self.n_max, world=self.comm.world, rank=self.comm.rank,
+                    cfg=self.cfg.as_dict(), tol=self.tol)
+
+    def snapshot(self, path):
+        """Write this rank's stream state to `path` (.npz; each rank its own file, e.g. a path with
+        the rank in it): the rolling state of its pods, the ranks the next window warm-starts from,
+        the step count and the configuration it was built with.  Taken between windows; restoring it
+        into a StreamingRCA of the same mesh, partition and configuration continues the stream bit
+        for bit (tests/test_stream_dist_cpu.py, tests/test_gpu_stream.py).  The reference persists
+        investigations only (ref:utils/db_handler.py:13); this is the stream's own checkpoint."""
+        meta = dict(self._meta(), t=self.t, solved=self.solved, last_iters=self.last_iters)
+        arrays = self.shard.state_dict(self.M, self.H)
+        blob = np.frombuffer(json.dumps(meta, sort_keys=True).encode(), np.uint8)
+        with open(path, "wb") as f:
+            np.savez(f, meta=blob, **arrays)
+
+    def restore(self, path):
+        """Load a snapshot written by :meth:`snapshot` (no pickles: allow_pickle=False).  Raises
+        ValueError when it was taken on another mesh size, partition, horizon or configuration."""
+        with np.load(path, allow_pickle=False) as z:
+            meta = json.loads(bytes(z["meta"]).decode())
+            arrays = {k: z[k] for k in z.files if k != "meta"}
+        want = json.loads(json.dumps(self._meta(), sort_keys=True))
+        diff = sorted(k for k in want if meta.get(k) != want[k])
+        if diff:
+            raise ValueError(f"snapshot {path} does not match this stream: {', '.join(diff)} differ")
+        self.shard.load_state_dict(arrays, self.M, self.H)
+        self.t, self.solved, self.last_iters = int(meta["t"]), bool(meta["solved"]), int(meta["last_iters"])
 
 
 def window_bytes(P, M, delta):

@@ -131,6 +131,18 @@ class NumpyShard:
         self.score_out = out
         return out
 
+    def state_dict(self, M, horizon):
+        """Stream snapshot of this restatement: the series so far (its whole rolling state) + ranks."""
+        hist = getattr(self, "_hist", None)
+        r = getattr(self, "r", None)
+        return dict(hist=np.zeros((0, self.n, M), np.float32) if hist is None else hist,
+                    r=np.zeros(self.n, np.int64) if r is None else r.copy())
+
+    def load_state_dict(self, st, M, horizon):
+        self.M = int(M)
+        self._hist = np.asarray(st["hist"], np.float32)
+        self.r = np.asarray(st["r"], np.int64).copy()
+
     def init_warm(self, alpha, floor):
         """krca_ppr_shard_init_warm: new seeds, w and dangling mass from the kept ranks."""
         s = self.score_out["score"]

@@ -35,7 +35,7 @@ def _mesh():
     return m, x
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, out_q, snap_dir=None, snap_at=2):
     sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"),
                     os.path.join(ROOT, "tests")]
     import torch.distributed as dist
@@ -49,11 +49,20 @@ def _worker(rank, world, port, out_q):
     cfg = Config(window=W)
     lo, hi, n_max = shard_range(N, world, rank)
     rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
-    shard = NumpyShard(np.zeros((0, hi - lo, M), np.float32), rp, col, od, N, n_max, world, cfg)
-    s = StreamingRCA(None, m.row_ptr, m.col, m.outdeg, M, cfg, horizon=H, tol=1e-9, max_iter=60,
-                     comm=Comm(world, rank), shard=shard)
+
+    def fresh():
+        shard = NumpyShard(np.zeros((0, hi - lo, M), np.float32), rp, col, od, N, n_max, world, cfg)
+        return shard, StreamingRCA(None, m.row_ptr, m.col, m.outdeg, M, cfg, horizon=H, tol=1e-9, max_iter=60,
+                                   comm=Comm(world, rank), shard=shard)
+    shard, s = fresh()
     t, rows = 0, []
-    for d in WINDOWS:
+    for wi, d in enumerate(WINDOWS):
+        if snap_dir is not None and wi == snap_at:
+            # checkpoint between windows, continue in a new stream object restored from the file
+            path = os.path.join(snap_dir, f"stream_rank{rank}.npz")
+            s.snapshot(path)
+            shard, s = fresh()
+            s.restore(path)
         out = s.window(x[t:t + d, lo:hi, :])
         t += d
         rows.append((shard.r.copy(), out["iters"], [int(i) for i in out["top"][0]],
@@ -64,13 +73,15 @@ def _worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_sharded_stream_matches_oracle_chain(world):
+@pytest.mark.parametrize("world,snap", [(1, False), (2, False), (3, False), (2, True)])
+def test_sharded_stream_matches_oracle_chain(world, snap, tmp_path):
+    """snap: every rank snapshots its stream after window 2 and continues in a restored object."""
     import oracle
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, str(tmp_path) if snap else None))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -95,3 +106,29 @@ def test_sharded_stream_matches_oracle_chain(world):
         for g in range(world):
             assert res[g][wi][1] == it, (world, wi, res[g][wi][1], it)
             assert res[g][wi][2] == top, (world, wi)
+
+
+def test_snapshot_refuses_another_stream(tmp_path):
+    """A snapshot restores only into a stream of the same mesh, partition, horizon and config."""
+    sys.path[:0] = [os.path.join(ROOT, "tests")]
+    from krca.rca import Comm, Config, shard_graph, shard_range
+    from krca.stream import StreamingRCA
+    from numpy_shard import NumpyShard
+    m, x = _mesh()
+
+    def make(cfg, horizon):
+        lo, hi, n_max = shard_range(N, 1, 0)
+        rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
+        sh = NumpyShard(np.zeros((0, N, M), np.float32), rp, col, od, N, n_max, 1, cfg)
+        return StreamingRCA(None, m.row_ptr, m.col, m.outdeg, M, cfg, horizon=horizon, tol=1e-9, max_iter=60,
+                            comm=Comm(1, 0), shard=sh)
+    s = make(Config(window=W), H)
+    s.window(x[:W + 5])
+    path = str(tmp_path / "s.npz")
+    s.snapshot(path)
+    for other in (make(Config(window=W, alpha=0.6), H), make(Config(window=W), H + 1)):
+        with pytest.raises(ValueError, match="differ"):
+            other.restore(path)
+    ok = make(Config(window=W), H)
+    ok.restore(path)
+    assert ok.t == W + 5 and ok.solved
