@@ -246,10 +246,9 @@ struct Head {
   uint32_t c[SEG];  // remapped columns (uint32 units of the exchange layout)
 };
 struct Rows {
-  int64_t my_off, my_end;  // row_ptr of the lane's row and the next (absolute; short blocks)
   int64_t my_q, my_r;
   double my_coef;  // alpha / outdeg (coef_of)
-  uint32_t li;  // krca_ppr_pack lane info: (row holding edge 8t) << 8 | head bits of edges 8t .. 8t+7
+  uint2 li;     // krca_ppr_pack lane info: byte k = block-relative row holding edge 8t + k
   uint4 ix;     // dictionary blocks: the slots of edges 8t .. 8t+7 (uint16 pairs)
 };
 
@@ -283,24 +282,23 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
 }
 
 template <int FLAGS>
-__device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16_t* __restrict__ lane_info,
-                                          const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk,
+__device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint64_t* __restrict__ lane_info,
+                                          const int32_t* __restrict__ pk,
                                           const double* __restrict__ coef, const int64_t* __restrict__ q,
                                           const int64_t* __restrict__ r, Rows& R) {
   const uint32_t tid = threadIdx.x;
   const uint32_t nrows = (uint32_t)(m.code > 0 ? m.code - m.rb : 1);
   const uint32_t off = tid < nrows ? tid : 0;  // the lane's row, from the block's first (wave-uniform base)
   constexpr bool NT = (FLAGS & PPR_NT) != 0;
-  const int64_t* rp = row_ptr + m.rb;
-  R.my_off = ld_stream<NT>(rp + off);
-  R.my_end = ld_stream<NT>(rp + off + 1);
   R.my_q = ld_stream<NT>(q + m.rb + off);
   R.my_r = (FLAGS & PPR_RESIDUAL) ? ld_stream<NT>(r + m.rb + off) : 0;
   R.my_coef = ld_stream<NT>(coef + m.rb + off);
-  R.li = ld_stream<NT>(lane_info + b * TPB + tid);  // zero for long-row chunks
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x2 l = ld_stream<NT>(reinterpret_cast<const u32x2*>(lane_info + b * TPB) + tid);  // zero for long-row chunks
+  R.li = make_uint2(l.x, l.y);
   // unconditional 16-byte load (used by dictionary blocks only): in-bounds, 16-byte aligned
   const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* ixb = reinterpret_cast<const u32x4*>(pk + wb);
   const u32x4 ix = ld_stream<NT>(ixb + (tid * SEG < (uint32_t)(m.e1 - m.e0) ? tid : 0u));
   R.ix = make_uint4(ix.x, ix.y, ix.z, ix.w);
@@ -324,13 +322,13 @@ __device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict
 // entry i+2 are in flight, so neither the gather latency nor the dependent plan -> column latency
 // is paid per entry.  The loop is unrolled x2 over ping-pong Head / Rows slots (no copies of
 // in-flight loads).  A short block in three barrier-separated phases:
-//  stage   the gathered values (or distinct-column values) go to LDS; every non-empty row records
-//          its index at its first edge (headrow);
-//  sum     lane t sums its 8 contiguous edges [8t, 8t+8) as row segments: the row holding edge 8t
-//          and the head bits of its 8 edges come from the host-built lane info (krca_ppr_pack), its
-//          8 values and the rows at its heads are independent LDS reads, and each finished segment
-//          is one no-return LDS atomic into its row's sum: no dependent LDS chain (round 1 searched
-//          the row offsets and walked the row ends, ~25 dependent LDS round trips per lane);
+//  stage   the gathered values (or distinct-column values) go to LDS;
+//  sum     lane t sums its 8 contiguous edges [8t, 8t+8) as row segments: the row holding each of
+//          its edges comes from the host-built lane info (krca_ppr_pack, one byte per edge), its 8
+//          values are independent LDS reads, and each finished segment is one no-return LDS atomic
+//          into its row's sum: no dependent LDS chain and no row offsets (round 1 searched the row
+//          offsets and walked the row ends, ~25 dependent LDS round trips per lane; round 3 first
+//          staged each row's index at its first edge and loaded two row offsets per row);
 //  update  lane r updates row r (teleport, residual, next w).
 #ifdef PPR_TIMING
 __device__ unsigned long long g_ppr_timing[4096 * 5];  // per workgroup: stage, sum, update, long, blocks
@@ -342,11 +340,10 @@ __device__ unsigned long long g_ppr_timing[4096 * 5];  // per workgroup: stage, 
 template <int FLAGS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 8))) void ppr_step(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
-    const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
+    const uint64_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
     int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz) {
   __shared__ uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
-  __shared__ __attribute__((aligned(16))) uint8_t headrow[EDGE_BUDGET];  // at a row's first edge: its row
   __shared__ unsigned long long rowsum[ROW_BUDGET];
   __shared__ int64_t red[TPB / 64];
   int64_t b = blockIdx.x;
@@ -366,7 +363,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   uint32_t v[SEG];  // codes: decoded where summed (a prefetched register is never computed on early)
   gather(H0, w, v);
   const double* coef = coef_of(ctl, n);
-  load_rows<FLAGS>(H0.m, b, lane_info, row_ptr, pk, coef, q, r, R0);
+  load_rows<FLAGS>(H0.m, b, lane_info, pk, coef, q, r, R0);
   Meta cur = H0.m;
   int64_t b1 = b + gridDim.x;
   // prefetches past the workgroup's last entry load the grid's last entry again (clamped, results
@@ -397,8 +394,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       // instructions per entry)
 #pragma unroll
       for (int j = 0; j < SEG; ++j) vals[tid + j * TPB] = v[j];
-      if (tid < cur.code - cur.rb && rc.my_end > rc.my_off)  // a non-empty row: its index at its first edge
-        headrow[(int)(rc.my_off - cur.e0)] = (uint8_t)tid;
       rowsum[tid] = 0ull;
     } else {
 #pragma unroll
@@ -408,7 +403,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     const int64_t b2 = b1 + gridDim.x;
     const Meta next = hn.m;
     gather(hn, w, v);
-    load_rows<FLAGS>(next, b1 < nblk ? b1 : nblk - 1, lane_info, row_ptr, pk, coef, q, r, rn);
+    load_rows<FLAGS>(next, b1 < nblk ? b1 : nblk - 1, lane_info, pk, coef, q, r, rn);
     load_head<(FLAGS & PPR_NT) != 0>(plan, b2 < nblk ? b2 : nblk - 1, pk, hl);
     if (shortb) {
       const int nrows = cur.code - cur.rb;
@@ -416,9 +411,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       PPR_T(0);
       const int a = tid * SEG;
       if (a < ne) {
-        const uint32_t M = rc.li & 0xFFu;  // head bits of edges a .. a+7
-        int row = (int)(rc.li >> 8);        // the row holding edge a
-        const uint2 hr = *reinterpret_cast<const uint2*>(headrow + a);  // rows at the lane's heads
+        const uint2 hr = rc.li;  // byte k: the row holding edge a + k
         const uint4 sx = rc.ix;  // this lane's own slots (prefetched with the rows)
         // the 8 LDS reads are unconditional (a slot past the block's edges is clamped into the
         // table and its value dropped by the select), so they issue back to back: a read under a
@@ -430,14 +423,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
           const int sl = dict ? (int)((wd >> (16 * (kk & 1))) & 0xFFFFu) : a + kk;
           c[kk] = vals[sl & (EDGE_BUDGET - 1)];
         }
-        int64_t sacc = 0;
+        int64_t sacc = wdec(c[0]);
+        uint32_t row = hr.x & 0xFFu;
 #pragma unroll
-        for (int kk = 0; kk < SEG; ++kk) {
-          if (kk > 0 && ((M >> kk) & 1u)) {
+        for (int kk = 1; kk < SEG; ++kk) {
+          const uint32_t rk = ((kk < 4 ? hr.x : hr.y) >> (8 * (kk & 3))) & 0xFFu;
+          if (rk != row) {  // edge a + kk starts the next row's segment
             atomicAdd(&rowsum[row], (unsigned long long)sacc);  // no return: no wait
             sacc = 0;
-            row = (int)(((kk < 4 ? hr.x : hr.y) >> (8 * (kk & 3))) & 0xFFu);
           }
+          row = rk;
           sacc += a + kk < ne ? wdec(c[kk]) : 0;
         }
         atomicAdd(&rowsum[row], (unsigned long long)sacc);
@@ -446,7 +441,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       PPR_T(1);
       if (tid < nrows)
         update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[tid], rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
-      __syncthreads();  // rowsum / vals / headrow are rewritten by the next entry
+      __syncthreads();  // rowsum / vals are rewritten by the next entry
       PPR_T(2);
     } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
       const int64_t tot = block_sum_i64(sacc_long, red);
@@ -614,14 +609,14 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
 }
 
 namespace {
-int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
+int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint64_t* lane,
                 const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                 int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
                 void* stream);
 }
 
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
-                        const uint16_t* lane, const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
+                        const uint64_t* lane, const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send,
                         void* ctl, void* stream) {
   return launch_step(row_ptr, col, plan, plan_len, lane, w_all, outdeg, q_local, n_local, n_max, N, alpha, flags, r_local,
@@ -629,7 +624,7 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
 }
 
 int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
-                       const uint16_t* lane, int64_t* w, const int32_t* outdeg, const int64_t* q, int64_t N, double alpha,
+                       const uint64_t* lane, int64_t* w, const int32_t* outdeg, const int64_t* q, int64_t N, double alpha,
                        int32_t flags, double tol, int64_t* r, int64_t* send, void* ctl, void* stream) {
   KRCA_CHECK_ARG(plan_len > 0 && N > 0, "krca_ppr_solo_step: bad sizes");
   const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
@@ -646,7 +641,7 @@ int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t
 }  // extern "C"
 
 namespace {
-int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
+int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint64_t* lane,
                 const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                 int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
                 void* stream) {
@@ -727,7 +722,7 @@ int64_t krca_ppr_workspace_size(int64_t N) {
 }
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int64_t* plan,
-             int64_t plan_len, const uint16_t* lane, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
+             int64_t plan_len, const uint64_t* lane, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
              void* workspace, float* r_out, int64_t* r_fixed, int64_t* q_out, int32_t* iters_host, void* stream) {
   KRCA_CHECK_ARG(N > 0 && N < INT32_MAX, "krca_ppr: N=%lld out of range", (long long)N);
   KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && lane && seed && workspace && r_out, "krca_ppr: null pointer");

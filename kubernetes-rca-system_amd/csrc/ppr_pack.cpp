@@ -67,27 +67,23 @@ int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out) {
 // columns fit becomes a dictionary block (sorted distinct columns, then uint16 slots per edge),
 // every other block stays direct.  Returns the number of dictionary blocks.
 int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_max, int64_t* plan, int64_t plan_len,
-                    int32_t* pk, uint16_t* lane) {
+                    int32_t* pk, uint64_t* lane) {
   auto remap = [n_max](int64_t j) { return (int32_t)remap_col(j, n_max); };
   std::vector<int32_t> uniq;
   std::vector<uint16_t> slot;
-  std::vector<int16_t> head;  // block-relative row starting at each edge (-1: none)
   int64_t ndict = 0;
   for (int64_t p = 0; p < plan_len; p += 4) {
     const int64_t rb = plan[p], code = plan[p + 1], e0 = plan[p + 2], e1 = plan[p + 3];
     const int64_t ne = e1 - e0;
-    uint16_t* li = lane + (p / 4) * TPB;
+    uint64_t* li = lane + (p / 4) * TPB;
     for (int t = 0; t < TPB; ++t) li[t] = 0;
-    if (code > 0) {  // lane t: (row holding edge 8t) << 8 | head bits of its edges 8t .. 8t+7
-      head.assign(ne, -1);
-      for (int64_t rr = rb; rr < code; ++rr)
-        if (rp[rr + 1] > rp[rr]) head[rp[rr] - e0] = (int16_t)(rr - rb);
-      int cur_row = 0;
-      for (int64_t e = 0; e < ne; ++e) {
-        if (head[e] >= 0) cur_row = head[e];
-        const int t = (int)(e / SEG), k = (int)(e % SEG);
-        if (k == 0) li[t] = (uint16_t)(cur_row << 8);
-        if (head[e] >= 0) li[t] |= (uint16_t)(1u << k);
+    if (code > 0) {  // lane t: byte k = block-relative row holding edge 8t + k (past the block's
+                     // last edge: that edge's row, so the lane's tail starts no segment)
+      int64_t rr = rb;
+      for (int64_t e = 0; e < ceil_div(ne, SEG) * SEG; ++e) {
+        if (e < ne)
+          while (rp[rr + 1] - e0 <= e) ++rr;  // the row holding edge e (empty rows hold none)
+        li[e / SEG] |= (uint64_t)(rr - rb) << (8 * (e % SEG));
       }
     }
     bool dict = false;
@@ -145,7 +141,7 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host, in
 int64_t krca_ppr_lane_size(int64_t plan_len) { return plan_len / 4 * TPB; }
 
 int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
-                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host) {
+                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint64_t* lane_host) {
   KRCA_CHECK_ARG(row_ptr_host && plan_host && pk_host && lane_host && N > 0 && N < INT32_MAX && n_max > 0,
                  "krca_ppr_pack: bad arguments");
   const int64_t E = row_ptr_host[N];

@@ -122,7 +122,7 @@ def test_ppr_pack_decodes_to_the_remapped_columns():
         n = lib.krca_ppr_plan_size(rp.ctypes.data_as(vp), len(rp) - 1)
         plan = np.zeros(n, np.int64)
         pk = np.zeros(len(col), np.int32)
-        lane = np.zeros(lib.krca_ppr_lane_size(n), np.uint16)
+        lane = np.zeros(lib.krca_ppr_lane_size(n), np.uint64)
         nd = lib.krca_ppr_pack(rp.ctypes.data_as(vp), col.ctypes.data_as(vp), len(rp) - 1, n_max,
                                plan.ctypes.data_as(vp), n, pk.ctypes.data_as(vp), lane.ctypes.data_as(vp))
         assert nd > 0.5 * (n // 4), nd  # most blocks of a service mesh are dictionary blocks
@@ -130,18 +130,17 @@ def test_ppr_pack_decodes_to_the_remapped_columns():
         got = np.full(len(col), -1, np.int64)
         for bi, (h, code, e0, e1) in enumerate(plan.reshape(-1, 4)):
             nu = int(h) >> 32
-            if code > 0:  # lane info: row holding edge 8t, head bits of edges 8t .. 8t+7
+            if code > 0:  # lane info: byte k = block-relative row holding edge 8t + k
                 rb = int(h) & 0xFFFFFFFF
-                rows = np.arange(rb, code)
-                starts = rp[rows] - e0
-                nonempty = rp[rows + 1] > rp[rows]
-                for t in range(0, (e1 - e0 + 7) // 8):
+                ne = int(e1 - e0)
+                # the row holding each edge of the block (empty rows hold none)
+                holder = np.repeat(np.arange(code - rb), np.diff(rp[rb:code + 1]))
+                assert len(holder) == ne
+                for t in range(0, (ne + 7) // 8):
                     li = int(lane[bi * 256 + t])
-                    a = 8 * t
-                    hold = rows[nonempty & (starts <= a)].max() - rb
-                    assert li >> 8 == hold
-                    heads = set((starts[nonempty] - a).tolist()) & set(range(8))
-                    assert li & 0xFF == sum(1 << k for k in heads if a + k < e1 - e0)
+                    for k in range(8):
+                        e = min(8 * t + k, ne - 1)  # past the block: the last edge's row
+                        assert (li >> (8 * k)) & 0xFF == holder[e], (bi, t, k)
             if nu == 0:
                 got[e0:e1] = pk[e0:e1]
                 continue

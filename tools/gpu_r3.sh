@@ -48,13 +48,14 @@ for s in "$@"; do
     ranking) step ranking 600 python3 -u tools/ranking_ablation_c4.py --seeds 2 --out $O/ranking_ablation_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
     ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
-    ppr_w5) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_w5.so; prof ppr_w5 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
+    ppr_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#ppr_}.so; prof $s 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_prev) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_prev.so; prof ppr_prev 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_nt) export KRCA_PPR_NT=1; prof ppr_nt 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_NT ;;
     bench_nograph) export KRCA_RCA_GRAPH=0; step bench_nograph 300 python3 bench.py --no-cpu-baseline; unset KRCA_RCA_GRAPH ;;
     bench2) step bench2 300 python3 bench.py --no-cpu-baseline ;;
     tests_tmpl) step tests_tmpl 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread -k "template or tmpl or c2mini or c5 or stream" ;;
     logs) prof logs 300 tools/prof_kernels.py logs --reps 5 ;;
+    logs_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#logs_}.so; prof $s 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LIB ;;
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
     c5) step c5 400 python3 -u tools/bench_stream.py ;;
     pmc_ppr)
