@@ -26,9 +26,18 @@
 #include <stdint.h>
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "krca_common.h"
 #define KRCA_DFA_QUAL static __device__ __constant__ const
 #include "log_dfa_tables.h"
+
+#ifndef LOG_IDX_BATCH
+#define LOG_IDX_BATCH 4  // pieces per lane whose loads log_index_lines' first phase issues together
+#endif
+#ifndef LOG_IDX_PERSIST
+#define LOG_IDX_PERSIST 1  // log_index_lines: resident workgroups loop over the tiles (0: one tile each)
+#endif
 
 namespace {
 
@@ -752,25 +761,41 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   __shared__ uint32_t s_sl[NIT * TPB];
   __shared__ uint16_t s_l1[NIT * TPB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // tiles in ticket order, each workgroup taking the next until none is left: every tile a
+  // look-back waits on has been taken by a running workgroup, so the wait always ends
+  for (;;) {
   if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
   s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t tile = s_tile;
+  const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
+  if (tile >= ntiles) return;  // uniform
   const int64_t tile0 = tile * TILE;
   tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
-#pragma unroll 4
-  for (int it = 0; it < NIT; ++it) {
-    const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (q < nbytes) {  // an aligned 16-byte block holding a text byte never crosses the last page
-      const uint4 v = *reinterpret_cast<const uint4*>(text + q);
-      w[0] = v.x;
-      w[1] = v.y;
-      w[2] = v.z;
-      w[3] = v.w;
+  // the pieces' loads go out LOG_IDX_BATCH at a time, unconditionally (a piece past the text
+  // reloads the last aligned block, an aligned 16-byte block holding a text byte never crosses the
+  // text's last page; its bytes are zeroed below): a load under `if (q < nbytes)` made each piece
+  // wait for its own load, one piece in flight per lane
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int64_t qlast = (nbytes - 1) & ~(int64_t)(PIECE - 1);
+  const int64_t wave0 = tile0 + (int64_t)__builtin_amdgcn_readfirstlane(wid) * 64 * PIECE;
+  for (int it0 = 0; it0 < NIT; it0 += LOG_IDX_BATCH) {
+    u32x4 raw[LOG_IDX_BATCH];
+    uint32_t pw[LOG_IDX_BATCH];  // bytes q0-4 .. q0-1 of the wave's first piece (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < LOG_IDX_BATCH; ++j) {
+      const int64_t q = tile0 + (int64_t)(it0 + j) * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
+      raw[j] = *reinterpret_cast<const u32x4*>(text + (q < nbytes ? q : qlast));
+      const int64_t q0 = wave0 + (int64_t)(it0 + j) * TPB * PIECE;
+      pw[j] = q0 >= 4 && q0 <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q0 - 4) : 0u;
     }
+#pragma unroll
+  for (int jj = 0; jj < LOG_IDX_BATCH; ++jj) {
+    const int it = it0 + jj;
+    const int64_t q = tile0 + (int64_t)it * TPB * PIECE + (int64_t)threadIdx.x * PIECE;
+    const bool in = q < nbytes;
+    uint32_t w[4] = {in ? raw[jj].x : 0u, in ? raw[jj].y : 0u, in ? raw[jj].z : 0u, in ? raw[jj].w : 0u};
     uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
-    if (lane == 0) wp = q >= 4 && q <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q - 4) : 0u;
+    if (lane == 0) wp = pw[jj];
     uint32_t C = 0;  // container first bytes at q-1+j, j = 0..16 (non-empty containers only)
     if (q < nbytes) C = piece_container_starts(s_cs, tile0, q);
     uint32_t S, l0, l1;
@@ -788,6 +813,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
     for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
     if ((threadIdx.x & (LANES_PER_CHUNK - 1)) == 0)
       s_cnt[it * (TPB / LANES_PER_CHUNK) + threadIdx.x / LANES_PER_CHUNK] = (int32_t)c;
+  }
   }
   __syncthreads();
   // chunk counts, their scan inside the tile, the tile total
@@ -865,6 +891,8 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
       if (id >= 1 && id - 1 < cap) line_end[id - 1] = pos - sl;
       ++id;
     }
+  }
+  __syncthreads();  // the LDS planes and bases are rewritten by the next tile
   }
 }
 
@@ -1450,7 +1478,18 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
                      nbytes, cdoc);
   KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(log_index_lines, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
+  static const int64_t resident = [] {  // workgroups the device keeps resident (occupancy API)
+    int dev = 0, cus = 256, per_cu = 4;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&log_index_lines), TPB, 0) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 4;
+    return (int64_t)cus * per_cu;
+  }();
+  const int64_t grid_ix = LOG_IDX_PERSIST ? std::min<int64_t>(nt, resident) : nt;
+  hipLaunchKernelGGL(log_index_lines, dim3((unsigned)grid_ix), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
                      (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
                      tile + nt);
   KRCA_LAUNCH_CHECK();
