@@ -123,9 +123,15 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8
 // (Line starts at container first bytes are counted by log_count from its tile bitmap: every
 // container is valid UTF-8 on its own, so away from those bytes the raw separator test is exact.)
 // doc_off outside the contract (include/krca.h) is clamped to [0, nbytes] so no write leaves the map.
+// (krca_log_scan: also zeroes the look-back status words + ticket and the long-line count, so the
+// scan needs no memset launches of its own)
 __global__ __launch_bounds__(TPB) void log_chunk_doc(const int64_t* __restrict__ doc_off, int64_t D, int64_t nbytes,
-                                                     int32_t* __restrict__ chunk_doc) {
+                                                     int32_t* __restrict__ chunk_doc,
+                                                     unsigned long long* __restrict__ zero64, int64_t n_zero64,
+                                                     int32_t* __restrict__ zero32) {
   const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  for (int64_t i = d; i < n_zero64; i += (int64_t)gridDim.x * TPB) zero64[i] = 0ull;
+  if (d == 0 && zero32) *zero32 = 0;
   if (d >= D) return;
   const int64_t s = min(max(doc_off[d], (int64_t)0), nbytes);
   const int64_t e = min(max(doc_off[d + 1], s), nbytes);
@@ -642,16 +648,21 @@ __device__ __forceinline__ int64_t lines_of(int64_t L, const int64_t* Ld, int64_
   return n <= cap ? n : 0;
 }
 
-// the end of the last line: the text's end, minus a trailing separator
+// the end of the last line: the text's end, minus a trailing separator (L >= 1, nbytes >= 1)
+__device__ __forceinline__ int64_t last_line_end(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                 const int64_t* __restrict__ doc_off, int64_t D) {
+  int64_t k = D - 1;
+  while (k > 0 && doc_off[k] >= nbytes) --k;  // the last non-empty container
+  const uint32_t b1 = text[nbytes - 1], b2 = nbytes >= 2 ? text[nbytes - 2] : 0u, b3 = nbytes >= 3 ? text[nbytes - 3] : 0u;
+  return nbytes - sep_len(b3, b2, b1, doc_off[k] == nbytes - 1);
+}
+
 __global__ void log_last_end(const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off,
                              int64_t D, int64_t L, const int64_t* __restrict__ Ld, int64_t cap,
                              int64_t* __restrict__ line_end) {
   L = lines_of(L, Ld, cap);
   if (L == 0 || nbytes == 0) return;
-  int64_t k = D - 1;
-  while (k > 0 && doc_off[k] >= nbytes) --k;  // the last non-empty container
-  const uint32_t b1 = text[nbytes - 1], b2 = nbytes >= 2 ? text[nbytes - 2] : 0u, b3 = nbytes >= 3 ? text[nbytes - 3] : 0u;
-  line_end[L - 1] = nbytes - sep_len(b3, b2, b1, doc_off[k] == nbytes - 1);
+  line_end[L - 1] = last_line_end(text, nbytes, doc_off, D);
 }
 
 // ---- log_index_lines: log_count + log_scan + log_lines in ONE pass over the text -------------
@@ -859,8 +870,11 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   if (threadIdx.x == 0) {
     tile_base[tile] = excl;
     if (tile == ntiles - 1) {
-      tile_base[ntiles] = excl + total;
-      *n_lines = excl + total;
+      const int64_t n = excl + total;
+      tile_base[ntiles] = n;
+      *n_lines = n;
+      // the last line's end (no later line start writes it; log_last_end's work)
+      if (n >= 1 && n <= cap && nbytes > 0) line_end[n - 1] = last_line_end(text, nbytes, doc_off, D);
     }
   }
   s_base[threadIdx.x] = excl + before;
@@ -1390,7 +1404,7 @@ int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, 
   hipStream_t st = krca::as_stream(stream);
   KRCA_HIP(hipMemsetAsync(cdoc, 0, nt * TPB * sizeof(int32_t), st));  // defined map even off-contract
   hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
-                     nbytes, cdoc);
+                     nbytes, cdoc, (unsigned long long*)nullptr, (int64_t)0, (int32_t*)nullptr);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(log_count, dim3((unsigned)nt), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
                      (const int32_t*)cdoc, chunk, tile);
@@ -1472,11 +1486,12 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
       reinterpret_cast<unsigned long long*>(chunk_line0 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2));
   unsigned int* ticket = reinterpret_cast<unsigned int*>(status + nt);
   hipStream_t st = krca::as_stream(stream);
-  KRCA_HIP(hipMemsetAsync(cdoc, 0, nt * TPB * sizeof(int32_t), st));  // defined map even off-contract
-  KRCA_HIP(hipMemsetAsync(status, 0, (nt + 1) * sizeof(unsigned long long), st));
-  KRCA_HIP(hipMemsetAsync(n_long, 0, sizeof(int32_t), st));
+  // one launch before the index: the chunk -> container map (every chunk of the text is written
+  // under the doc_off contract; off it, tile_container_starts clamps what it reads), and the zeroed
+  // look-back status words + ticket and long-line count (no memset launches: each dependent
+  // launch costs ~10 us at the front of the scan)
   hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
-                     nbytes, cdoc);
+                     nbytes, cdoc, status, nt + 1, n_long);
   KRCA_LAUNCH_CHECK();
   static const int64_t resident = [] {  // workgroups the device keeps resident (occupancy API)
     int dev = 0, cus = 256, per_cu = 4;
@@ -1493,10 +1508,7 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
                      (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
                      tile + nt);
   KRCA_LAUNCH_CHECK();
-  const int64_t* Ld = tile + nt;
-  hipLaunchKernelGGL(log_last_end, dim3(1), dim3(1), 0, st, text, nbytes, doc_off, ndocs, (int64_t)0, Ld, line_cap,
-                     line_end);
-  KRCA_LAUNCH_CHECK();
+  const int64_t* Ld = tile + nt;  // (the last line's end: written by log_index_lines' last tile)
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, DFA_TPB), 256 * 3));
   hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0, Ld, line_cap,
                      (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
