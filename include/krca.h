@@ -270,6 +270,10 @@ int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const 
                        int64_t N, double alpha, int32_t flags, double tol, int64_t* r, int64_t* send /*!= w*/,
                        void* ctl, void* stream);
 int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);
+/* the same two numbers without a synchronisation: enqueues their copy into host[0] = iteration at
+ * convergence (0 = running), host[1] = iterations done; host should be pinned memory, read after
+ * an event recorded behind it (the host's convergence polls then overlap the next iterations) */
+int krca_ppr_ctl_copy(const void* ctl, int32_t* host /*[2]*/, void* stream);
 int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream);
 /* root-cause key = bits of (double)r_i * (double)q_i: ranks pods by propagated mass times their
  * own anomaly; order-preserving as int64, fed to krca_topk_i64 */

@@ -700,6 +700,14 @@ int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_h
   return KRCA_OK;
 }
 
+int krca_ppr_ctl_copy(const void* ctl, int32_t* host, void* stream) {
+  KRCA_CHECK_ARG(ctl && host, "krca_ppr_ctl_copy: null pointer");
+  static_assert(offsetof(Ctl, iter) == offsetof(Ctl, converged) + 4, "converged, iter adjacent");
+  KRCA_HIP(hipMemcpyAsync(host, &reinterpret_cast<const Ctl*>(ctl)->converged, 2 * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, krca::as_stream(stream)));
+  return KRCA_OK;
+}
+
 int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream) {
   if (n <= 0) return KRCA_OK;
   KRCA_CHECK_ARG(r && out, "krca_ppr_fixed_to_float: null pointer");

@@ -82,6 +82,7 @@ SIGNATURES = {
     "krca_ppr_solo_step": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_f64, c_i32, c_f64, c_vp,
                                    c_vp, c_vp, c_vp]),
     "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),
+    "krca_ppr_ctl_copy": (c_i32, [c_vp, c_vp, c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "krca_betweenness_ws_size": (c_i64, [c_i64, c_i32]),

@@ -261,6 +261,26 @@ class DeviceShard:
                                                  self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
                                                  p(self.send), e._stream()), "krca_ppr_shard_init_warm")
 
+    def ctl_async(self):
+        """Enqueue a copy of (iteration at convergence, iterations done) into pinned host memory and
+        an event behind it; ctl_wait(handle) reads it.  Two slots: one poll in flight while the
+        caller enqueues the next iterations."""
+        torch, e, p = self.torch, self.eng, self.eng.ptr
+        if getattr(self, "_poll", None) is None:
+            self._poll = [torch.zeros(2, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self._poll_ev = [torch.cuda.Event() for _ in range(2)]
+            self._poll_i = 0
+        i = self._poll_i
+        self._poll_i ^= 1
+        self._chk(e.lib.krca_ppr_ctl_copy(p(self.ctl), self._poll[i].data_ptr(), e._stream()), "krca_ppr_ctl_copy")
+        self._poll_ev[i].record(torch.cuda.current_stream(e.device))
+        return i
+
+    def ctl_wait(self, handle):
+        self._poll_ev[handle].synchronize()
+        conv, it = (int(v) for v in self._poll[handle].tolist())
+        return (conv or it), bool(conv)
+
     def ctl_read(self):
         """(iterations done, converged) of the solve in flight (synchronises the stream)."""
         import ctypes

@@ -86,12 +86,20 @@ class StreamingRCA:
             s.init(cfg.alpha, cfg.floor(s.N, s.M))
         self.comm.exchange(s)
         s.reduce(cfg.alpha, self.tol, 1)
-        for it in range(self.max_iter):
-            s.step(cfg.alpha, 3)  # tol > 0: residual + ranks every iteration
-            self.comm.exchange(s)
-            s.reduce(cfg.alpha, self.tol, 0)
-            if (it + 1) % self.check_every == 0 and it + 1 < self.max_iter and s.ctl_read()[1]:
+        # iterations in batches of check_every; the convergence flag of batch b is read while batch
+        # b + 1 runs (a pinned copy + event): the GPU never idles on the poll, and iterations enqueued
+        # past convergence do nothing (the kernels exit on the device-held flag), so the ranks and
+        # the iteration count are the same as with a synchronous check after every batch
+        it, pending = 0, None
+        while it < self.max_iter:
+            for _ in range(min(self.check_every, self.max_iter - it)):
+                s.step(cfg.alpha, 3)  # tol > 0: residual + ranks every iteration
+                self.comm.exchange(s)
+                s.reduce(cfg.alpha, self.tol, 0)
+            it += min(self.check_every, self.max_iter - it)
+            if pending is not None and s.ctl_wait(pending)[1]:
                 break
+            pending = s.ctl_async() if it < self.max_iter else None
         iters, conv = s.ctl_read()
         self.last_iters = iters if conv else -iters
         self.solved = True

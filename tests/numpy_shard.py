@@ -155,6 +155,12 @@ class NumpyShard:
         snd[self.ws + 2 * NSPREAD] = int(self.q.sum())
         self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
 
+    def ctl_async(self):  # the restatement runs eagerly: the poll is the current state
+        return self.ctl_read()
+
+    def ctl_wait(self, handle):
+        return handle
+
     def ctl_read(self):
         c = self.ctl
         return (c["converged"] or c["iter"]), bool(c["converged"])

@@ -40,6 +40,7 @@ for s in "$@"; do
     bench) step bench 300 python3 bench.py ;;
     bench_trace) prof bench_trace 400 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     corr100k) prof corr100k 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5 ;;
+    corr100k_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#corr100k_}.so; prof $s 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5; unset KRCA_LIB ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 --tau 0.5 ;;
     corr_batch)  # C3 with the main pass in smaller batches: re-scores of batch b beside the tiles of b + 1
       for b in 128 256 512; do
@@ -48,6 +49,7 @@ for s in "$@"; do
     ranking) step ranking 600 python3 -u tools/ranking_ablation_c4.py --seeds 2 --out $O/ranking_ablation_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
     ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
+    ppr_timing) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_wtime.so; step ppr_timing 300 python3 tools/ppr_timing.py; unset KRCA_LIB ;;
     ppr_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#ppr_}.so; prof $s 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_prev) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_prev.so; prof ppr_prev 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_nt) export KRCA_PPR_NT=1; prof ppr_nt 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_NT ;;
@@ -58,6 +60,8 @@ for s in "$@"; do
     logs_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#logs_}.so; prof $s 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LIB ;;
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
     c5) step c5 400 python3 -u tools/bench_stream.py ;;
+    c5_trace) step c5_trace 400 rocprofv3 --kernel-trace --output-format csv -d $O/c5_trace -o run -- python3 -u tools/bench_stream.py --windows 4
+      python3 tools/trace_gaps.py $O/c5_trace/run_kernel_trace.csv > $O/c5_gaps.txt; rm -f $O/c5_trace/run_kernel_trace.csv ;;
     pmc_ppr)
       pmc pmc_ppr_sq ppr SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
       pmc pmc_ppr_sq2 ppr SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD
