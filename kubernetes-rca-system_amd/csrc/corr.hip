@@ -765,10 +765,14 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       float* rowp = tile + r * EPI_LD + ch * BM;
       Cand<KC> cd;
       cd.init();
+      // the self product, also from a 128-block the sample does not scan: with an odd sample size
+      // the last sampled 256-block's second half is not scanned and, being a sample block, it is
+      // nobody's own block either, so its pods' self products were never recorded (and a stale
+      // value below 0.25 made a live pod "flat": its top-k the lowest indices)
+      const int self = (g < P && g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
+      if (self >= 0 && (self >= BM / 2) == (part == 1)) A.selfd[g] = rowp[self];  // before part 1's list lands
       if (active) {
         const int cend = (int)std::min<int64_t>(BM, P - c0);
-        const int self = (g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
-        if (self >= 0 && (self >= BM / 2) == (part == 1)) A.selfd[g] = rowp[self];  // before part 1's list lands
         float lim = -1.f;
         const int cb = part * (BM / 2), ce = std::min(cend, cb + BM / 2);
         for (int c4 = cb; c4 < ce; c4 += 4) {
@@ -1449,6 +1453,9 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   if (int rc = set_lds_attr<KC>()) return rc;
   const int64_t I0 = lo / TB, I1 = krca::ceil_div(lo + n, TB);
   const int nsb2_all = (d.nsb + 1) / 2;
+  // self products default to 1 ("not flat"): every pod's is recorded by a sample tile, and a
+  // missed one must never read as a stale value below the flat threshold
+  KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.selfd + lo), 0x3F800000 /* 1.0f */, (size_t)n, st));
   for (int c0 = 0; c0 < nsb2_all; c0 += NSB / 2) {  // chunks of NSB 128-blocks
     const int nsb_c = std::min(NSB, d.nsb - 2 * c0);
     const int nsb2 = (nsb_c + 1) / 2;

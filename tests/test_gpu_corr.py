@@ -149,6 +149,25 @@ def test_corr_c3_every_row(eng):
     assert banded <= 1000
 
 
+def test_corr_odd_sample_self_products(eng):
+    """An odd threshold sample (P = 120k, k = 10: 19 blocks of 128 pods) leaves the second half of
+    its last 256-block unscanned, and that block is nobody's own block either: the self products
+    of its pods (2432 .. 2559) must still be recorded -- a missed one read a stale value and could
+    turn a live pod "flat" (top-k = the lowest indices).  A flat pod inside that half (2500) must
+    still be handled as flat; the whole half and 512 random rows are checked exactly."""
+    P, T, k = 120_000, 256, 10
+    x = synth.make_metrics(P, 1, T, seed=5, group_size=20, device="cuda")
+    x[:, 2500, 0] = 42.0
+    res = eng.corr_topk(x, k=k, tau=TAU)
+    z = torch.from_numpy(twin_z(x)).cuda().double()
+    del x
+    assert (res["cert"] > 0).all(), np.nonzero(res["cert"] <= 0)[0][:10]
+    assert res["idx"][2500].tolist() == list(range(k)) and not res["val"][2500].any()
+    rows = np.concatenate([np.arange(2432, 2560), np.random.default_rng(1).choice(P, 512, replace=False)])
+    _, _, bad = device_check(res, z, [rows], k)
+    assert bad == (0, 0, 0), bad
+
+
 def test_corr_batches_and_full_lists_identical(eng):
     """The main pass in many batches (KRCA_CORR_BATCH) and with ambiguous lists that fill at once
     (KRCA_CORR_AMB_TILE = 0: every tile decides its pairs in place; 8: mixed) gives the same outputs
