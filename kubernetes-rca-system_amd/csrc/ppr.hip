@@ -256,6 +256,18 @@ __device__ __forceinline__ int64_t dict_words(int64_t e0, int32_t nu) {  // pk o
   return ((e0 + nu + 3) & ~int64_t(3)) - e0;
 }
 
+// a bounds-checked buffer over [p, p + bytes): loads past the end return 0, so the lanes past a
+// block's count need no clamped index (each clamp was a compare + select or min per load); the
+// byte offsets tid * size are loop-invariant registers and the per-slot strides are immediates
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_over(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ int64_t buf_i64(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0));
+  return (int64_t)(((uint64_t)v.y << 32) | v.x);
+}
+
 template <bool NT>
 __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int64_t b, const int32_t* __restrict__ pk,
                                           Head& H) {
@@ -267,18 +279,14 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
   H.m.e0 = pe[2];
   H.m.e1 = pe[3];
   const uint32_t tid = threadIdx.x;
-  // every lane loads (clamped index; gather() masks the lanes past lim): a predicated default
-  // value would have to wait for whatever load last wrote that register.  Indices are 32-bit
-  // offsets from a wave-uniform base, so each load is one `global_load ... v_off, s[base]`
-  // (a 64-bit per-lane address cost 2-3 vector instructions per load)
+  // every lane loads (a predicated default value would have to wait for whatever load last wrote
+  // that register): slots past the block's count read 0 from the bounds-checked buffer, i.e.
+  // column 0, a valid gather whose value no sum reads (dictionary slots >= nu and edges >= ne are
+  // never summed; long-row chunks mask their sum)
   const uint32_t lim = (uint32_t)(H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0);
-  const uint32_t top = lim > 0 ? lim - 1 : 0;
-  const uint32_t* base = reinterpret_cast<const uint32_t*>(pk) + H.m.e0;
+  const __amdgpu_buffer_rsrc_t rs = buf_over(pk + H.m.e0, 4 * lim);
 #pragma unroll
-  for (int j = 0; j < SEG; ++j) {
-    const uint32_t u = tid + j * TPB;
-    H.c[j] = ld_stream<NT>(base + (u < top ? u : top));
-  }
+  for (int j = 0; j < SEG; ++j) H.c[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * tid), 4 * j * TPB, 0);
 }
 
 template <int FLAGS>
@@ -288,33 +296,29 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint64
                                           const int64_t* __restrict__ r, Rows& R) {
   const uint32_t tid = threadIdx.x;
   const uint32_t nrows = (uint32_t)(m.code > 0 ? m.code - m.rb : 1);
-  const uint32_t off = tid < nrows ? tid : 0;  // the lane's row, from the block's first (wave-uniform base)
   constexpr bool NT = (FLAGS & PPR_NT) != 0;
-  R.my_q = ld_stream<NT>(q + m.rb + off);
-  R.my_r = (FLAGS & PPR_RESIDUAL) ? ld_stream<NT>(r + m.rb + off) : 0;
-  R.my_coef = ld_stream<NT>(coef + m.rb + off);
+  // the lane's row (lanes past the block's rows read 0 and update nothing)
+  R.my_q = buf_i64(buf_over(q + m.rb, 8 * nrows), 8 * tid);
+  R.my_r = (FLAGS & PPR_RESIDUAL) ? buf_i64(buf_over(r + m.rb, 8 * nrows), 8 * tid) : 0;
+  R.my_coef = __builtin_bit_cast(double, buf_i64(buf_over(coef + m.rb, 8 * nrows), 8 * tid));
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const u32x2 l = ld_stream<NT>(reinterpret_cast<const u32x2*>(lane_info + b * TPB) + tid);  // zero for long-row chunks
   R.li = make_uint2(l.x, l.y);
-  // unconditional 16-byte load (used by dictionary blocks only): in-bounds, 16-byte aligned
+  // the lane's 16 bytes of edge slots (used by dictionary blocks only; lanes past the edges read 0)
   const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
-  const u32x4* ixb = reinterpret_cast<const u32x4*>(pk + wb);
-  const u32x4 ix = ld_stream<NT>(ixb + (tid * SEG < (uint32_t)(m.e1 - m.e0) ? tid : 0u));
+  const uint32_t nlane = (uint32_t)((m.e1 - m.e0 + SEG - 1) / SEG);
+  const u32x4 ix = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(buf_over(pk + wb, 16 * nlane),
+                                                                                    (int)(16 * tid), 0, 0));
   R.ix = make_uint4(ix.x, ix.y, ix.z, ix.w);
 }
 
-// every lane gathers all SEG columns (past the block's count, load_head clamped the column to its
-// last one: a valid address, the value is dropped by the select), so the 8 loads issue back to
-// back instead of one exec-masked branch each
+// every lane gathers all SEG columns (past the block's count load_head read column 0: a valid
+// address whose value no sum reads), so the 8 loads issue back to back with no select
 __device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict__ w, uint32_t (&v)[SEG]) {
-  const uint32_t lim = (uint32_t)(H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0);
-  uint32_t g[SEG];
 #pragma unroll
   for (int j = 0; j < SEG; ++j)  // 32-bit byte offsets (krca_ppr_pack keeps remapped columns < 2^30)
-    g[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w) + (H.c[j] << 2));
-#pragma unroll
-  for (int j = 0; j < SEG; ++j) v[j] = threadIdx.x + j * TPB < lim ? g[j] : 0u;
+    v[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(w) + (H.c[j] << 2));
 }
 
 // Persistent, software-pipelined step.  Workgroup g takes plan entries g, g + G, g + 2G, ...;
@@ -395,9 +399,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
 #pragma unroll
       for (int j = 0; j < SEG; ++j) vals[tid + j * TPB] = v[j];
       rowsum[tid] = 0ull;
-    } else {
+    } else {  // a chunk of a long row: its edges [0, ne) (the gathers past them read column 0)
 #pragma unroll
-      for (int j = 0; j < SEG; ++j) sacc_long += wdec(v[j]);
+      for (int j = 0; j < SEG; ++j) sacc_long += tid + j * TPB < ne ? wdec(v[j]) : 0;
     }
     // v is free: gathers and rows of the next entry, head of the one after
     const int64_t b2 = b1 + gridDim.x;

@@ -412,6 +412,13 @@ class RcaStep:
             idx = torch.from_numpy(np.asarray(idx, np.int64))
             val = torch.from_numpy(np.asarray(val, np.int64))
         kk = int(idx.numel())
+        if self.comm.world == 1:  # nothing to gather: one copy of (idx | val) to the host
+            a = torch.cat((idx.to(torch.int64), val.to(torch.int64))).cpu().numpy()
+            gi, gv = a[:kk] + self.offset, a[kk:]
+            ok = a[:kk] >= 0
+            gi, gv = gi[ok], gv[ok]
+            order = sorted(range(len(gi)), key=lambda j: (-int(gv[j]), int(gi[j])))
+            return gi[order[:k]], gv[order[:k]]
         cand = torch.full((2, k), -1, dtype=torch.int64, device=idx.device)
         cand[0, :kk] = idx.to(torch.int64) + self.offset
         cand[1, :kk] = val.to(torch.int64)

@@ -100,10 +100,14 @@ class StreamingRCA:
             if pending is not None and s.ctl_wait(pending)[1]:
                 break
             pending = s.ctl_async() if it < self.max_iter else None
-        iters, conv = s.ctl_read()
+        # the final counts ride behind the key / top-k launches: one synchronisation (the merge's
+        # copy of the candidates) instead of a read-back before them
+        h = s.ctl_async()
+        top = self.rca.merge(*s.local_topk(cfg.k))
+        iters, conv = s.ctl_wait(h)
         self.last_iters = iters if conv else -iters
         self.solved = True
-        return self.rca.merge(*s.local_topk(cfg.k))
+        return top
 
     def window(self, x_new, log_text=None, doc_off=None):
         """One streaming window: rescoring, log histograms (+ templates), re-ranking."""

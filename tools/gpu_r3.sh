@@ -59,6 +59,7 @@ for s in "$@"; do
     logs) prof logs 300 tools/prof_kernels.py logs --reps 5 ;;
     logs_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#logs_}.so; prof $s 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LIB ;;
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
+    tmpl_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#tmpl_}.so; prof $s 300 tools/prof_kernels.py tmpl --reps 5; unset KRCA_LIB ;;
     c5) step c5 400 python3 -u tools/bench_stream.py ;;
     c5_trace) step c5_trace 400 rocprofv3 --kernel-trace --output-format csv -d $O/c5_trace -o run -- python3 -u tools/bench_stream.py --windows 4
       python3 tools/trace_gaps.py $O/c5_trace/run_kernel_trace.csv > $O/c5_gaps.txt; rm -f $O/c5_trace/run_kernel_trace.csv ;;
