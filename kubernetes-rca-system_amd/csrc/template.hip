@@ -148,17 +148,27 @@ __device__ __forceinline__ uint64_t line_hash_tab(const uint8_t* __restrict__ sb
 // instead.  (Round 1 read every line through that window: each window refill was a dependent
 // global load, and with 64 lanes at random phases nearly every byte step of a wave waited on one:
 // 1.63 ms for the 2.5M-line C5 window.)
+// A wave takes as long as its longest line, so the workgroup first orders its lines by length
+// (a counting sort on length / 4 in LDS) and lane t of wave w hashes the t-th line of the w-th
+// quarter: on the C5 corpus the mean of the waves' longest lines falls from 1.43x to 1.11x the
+// mean line length.
 constexpr int SPAN = 24 * 1024;  // a multiple of 16 * TPB
+constexpr int NLB = 128;          // length buckets of 4 bytes (the last one takes every longer line)
 __global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restrict__ text, int64_t nbytes,
                                                         const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
                                                         int64_t L, uint64_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[SPAN];
   __shared__ __attribute__((aligned(16))) uint8_t tstate[TS_STATES * TS_ROW];
+  __shared__ uint32_t bcnt[NLB];
+  __shared__ uint32_t span_se[TPB];  // a line's staged span offsets (start | end << 16), ~0 past the span
+  __shared__ uint8_t perm[TPB];
   for (int i = threadIdx.x; i < TS_STATES * 256; i += TPB)
     reinterpret_cast<uint16_t*>(tstate)[i] = tstate_entry(i >> 8, (uint32_t)(i & 255));
+  if (threadIdx.x < NLB) bcnt[threadIdx.x] = 0u;
   const int64_t l0 = (int64_t)blockIdx.x * TPB;
   const int64_t i = l0 + threadIdx.x;
   const int64_t l1 = min(l0 + TPB, L);
+  const int64_t my_s = i < L ? ls[i] : 0, my_e = i < L ? le[i] : 0;
   const int64_t a0 = ls[l0] & ~(int64_t)15;
   const int64_t a1 = min(min(le[l1 - 1], nbytes), a0 + SPAN - 4);  // dword reads may touch 3 bytes past
   // every staging load is issued before the first LDS write (one latency per workgroup, not one
@@ -186,13 +196,37 @@ __global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restric
     }
     reinterpret_cast<uint4*>(sbuf)[threadIdx.x + j * TPB] = st[j];
   }
+  // counting sort of the workgroup's lines by length / 4 (lines past L: bucket 0, skipped below)
+  const uint32_t bk = i < L ? (uint32_t)min<int64_t>((my_e - my_s) >> 2, NLB - 1) : 0u;
+  span_se[threadIdx.x] = i < L && my_e <= a1 ? (uint32_t)(my_s - a0) | ((uint32_t)(my_e - a0) << 16) : ~0u;
   __syncthreads();
-  if (i >= L) return;
-  const int64_t s = ls[i], e = le[i];
-  if (e <= a1) {
-    out[i] = line_hash_tab(sbuf, (int)(s - a0), (int)(e - a0), tstate);
+  const uint32_t rank = atomicAdd(&bcnt[bk], 1u);  // (LDS) order inside a bucket: arrival
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the NLB counts, two per lane
+    const int lane = threadIdx.x;
+    const uint32_t c0 = bcnt[2 * lane], c1 = bcnt[2 * lane + 1];
+    uint32_t x = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    const uint32_t ex = x - c0 - c1;
+    bcnt[2 * lane] = ex;
+    bcnt[2 * lane + 1] = ex + c0;
+  }
+  __syncthreads();
+  perm[bcnt[bk] + rank] = (uint8_t)threadIdx.x;
+  __syncthreads();
+  const int j = perm[threadIdx.x];
+  const int64_t li = l0 + j;
+  if (li >= L) return;
+  const uint32_t se = span_se[j];
+  if (se != ~0u) {
+    out[li] = line_hash_tab(sbuf, (int)(se & 0xFFFFu), (int)(se >> 16), tstate);
   } else {  // past the staged span: aligned dwords from the text (the last one may be partial)
-    out[i] = line_hash(s, e, [&](int64_t q) -> uint32_t {
+    const int64_t s = ls[li], e = le[li];
+    out[li] = line_hash(s, e, [&](int64_t q) -> uint32_t {
       if (q + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(text + q);
       uint32_t v = 0;
       for (int k = 0; k < 4; ++k)

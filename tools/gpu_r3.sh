@@ -48,6 +48,7 @@ for s in "$@"; do
       done; unset KRCA_CORR_BATCH ;;
     ranking) step ranking 600 python3 -u tools/ranking_ablation_c4.py --seeds 2 --out $O/ranking_ablation_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
+    ppr_bytes) step ppr_bytes 300 python3 tools/ppr_bench.py --reps 5 ;;
     ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
     ppr_timing) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_wtime.so; step ppr_timing 300 python3 tools/ppr_timing.py; unset KRCA_LIB ;;
     ppr_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#ppr_}.so; prof $s 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
