@@ -71,6 +71,9 @@ for s in "$@"; do
       pmc pmc_ppr_tcp ppr TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum
       pmc pmc_ppr_ea ppr TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum
       pmc pmc_ppr_grbm ppr GRBM_GUI_ACTIVE GRBM_COUNT ;;
+    pmc_logs_ea) pmc pmc_logs_ea logs TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum ;;
+    pmc_logs_ea_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#pmc_logs_ea_}.so
+      pmc $s logs TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum; unset KRCA_LIB ;;
     pmc_logs)
       pmc pmc_logs_ea logs TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum
       pmc pmc_logs_sq logs SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS ;;
