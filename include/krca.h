@@ -221,7 +221,7 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host /*{
                   int64_t plan_len);
 int64_t krca_ppr_workspace_size(int64_t N);
 int krca_ppr(const int64_t* row_ptr, const int32_t* col /*pk*/, const int32_t* outdeg, int64_t N,
-             const int64_t* plan, int64_t plan_len, const uint64_t* lane /*krca_ppr_pack*/, const float* seed,
+             const int64_t* plan, int64_t plan_len, const uint16_t* lane /*krca_ppr_pack*/, const float* seed,
              float seed_floor, double alpha, int32_t max_iter, double tol, void* workspace, float* r_out, int64_t* r_fixed /*nullable*/,
              int64_t* q_out /*nullable: quantised seeds*/, int32_t* iters_host, void* stream);
 int64_t krca_ppr_ctl_size(int64_t n_local);
@@ -234,15 +234,17 @@ int64_t krca_ppr_ctl_size(int64_t n_local);
  * entry's first word carries nu in its high 32 bits (0 = direct block: pk[e] = column of edge e).
  * Each distinct column is gathered once per block instead of once per edge.  The DEVICE copy of
  * pk must have 64 zero words of padding past E (the step issues clamped 16-byte loads).  lane_host
- * [krca_ppr_lane_size(plan_len)] uint64: per short block and lane t, byte k = the block-relative
- * row holding edge 8t + k (past the block's last edge: that edge's row), so the step's segmented
- * row sums need neither a search nor the row offsets.  Returns the number of dictionary blocks (>= 0) or a negative error (KRCA_EINVAL for a
+ * [krca_ppr_lane_size(plan_len)] uint16: per block 2 x 256 words.  The block's non-empty rows get
+ * consecutive sum slots 0, 1, ...; word t (lane t) = (slot of the row holding edge 8t) << 8 | the
+ * bits of the edges 8t + 1 .. 8t + 7 that start a row, and word 256 + r = the slot of row rb + r
+ * (256 for a row without edges), so the step's segmented row sums need neither a search nor the
+ * row offsets.  Returns the number of dictionary blocks (>= 0) or a negative error (KRCA_EINVAL for a
  * column outside [0, N) or a remapped column id >= 2^30: the step addresses the gathered table at
  * 32-bit byte offsets).
  * (KRCA_PPR_DICT=0 packs every block direct; krca_ppr_remap_cols remaps a column array alone.) */
 int64_t krca_ppr_lane_size(int64_t plan_len);
 int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
-                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint64_t* lane_host);
+                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host);
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream);
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
@@ -256,7 +258,7 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
 #define KRCA_PPR_RESIDUAL 1
 #define KRCA_PPR_WRITE_R 2
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const int64_t* plan, int64_t plan_len,
-                        const uint64_t* lane /*krca_ppr_pack*/, const int64_t* w_all /*[G][slice]*/, const int32_t* outdeg,
+                        const uint16_t* lane /*krca_ppr_pack*/, const int64_t* w_all /*[G][slice]*/, const int32_t* outdeg,
                         const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
                         int32_t flags, int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
@@ -266,7 +268,7 @@ int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_
  * the codes of w, writes r and send, zeroes w's partial-sum slots (w is the next step's write
  * target: the caller swaps w and send, exactly as around krca_ppr_shard_reduce). */
 int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const int64_t* plan, int64_t plan_len,
-                       const uint64_t* lane, int64_t* w /*[slice(N)]*/, const int32_t* outdeg, const int64_t* q,
+                       const uint16_t* lane, int64_t* w /*[slice(N)]*/, const int32_t* outdeg, const int64_t* q,
                        int64_t N, double alpha, int32_t flags, double tol, int64_t* r, int64_t* send /*!= w*/,
                        void* ctl, void* stream);
 int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_host, void* stream);

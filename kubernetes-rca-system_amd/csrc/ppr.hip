@@ -248,7 +248,8 @@ struct Head {
 struct Rows {
   int64_t my_q, my_r;
   double my_coef;  // alpha / outdeg (coef_of)
-  uint2 li;     // krca_ppr_pack lane info: byte k = block-relative row holding edge 8t + k
+  uint32_t li;  // krca_ppr_pack lane word: (sum slot of the row holding edge 8t) << 8 | head bits
+  uint32_t rs;  // the sum slot of the lane's row (ROW_BUDGET: a row without edges)
   uint4 ix;     // dictionary blocks: the slots of edges 8t .. 8t+7 (uint16 pairs)
 };
 
@@ -290,7 +291,7 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
 }
 
 template <int FLAGS>
-__device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint64_t* __restrict__ lane_info,
+__device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16_t* __restrict__ lane_info,
                                           const int32_t* __restrict__ pk,
                                           const double* __restrict__ coef, const int64_t* __restrict__ q,
                                           const int64_t* __restrict__ r, Rows& R) {
@@ -301,10 +302,10 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint64
   R.my_q = buf_i64(buf_over(q + m.rb, 8 * nrows), 8 * tid);
   R.my_r = (FLAGS & PPR_RESIDUAL) ? buf_i64(buf_over(r + m.rb, 8 * nrows), 8 * tid) : 0;
   R.my_coef = __builtin_bit_cast(double, buf_i64(buf_over(coef + m.rb, 8 * nrows), 8 * tid));
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x2 l = ld_stream<NT>(reinterpret_cast<const u32x2*>(lane_info + b * TPB) + tid);  // zero for long-row chunks
-  R.li = make_uint2(l.x, l.y);
+  const uint16_t* lb = lane_info + b * 2 * TPB;  // zero / empty for long-row chunks
+  R.li = ld_stream<NT>(lb + tid);
+  R.rs = ld_stream<NT>(lb + TPB + tid);
   // the lane's 16 bytes of edge slots (used by dictionary blocks only; lanes past the edges read 0)
   const int64_t wb = m.nu > 0 ? m.e0 + dict_words(m.e0, m.nu) : (m.e0 & ~int64_t(3));
   const uint32_t nlane = (uint32_t)((m.e1 - m.e0 + SEG - 1) / SEG);
@@ -327,12 +328,14 @@ __device__ __forceinline__ void gather(const Head& H, const uint32_t* __restrict
 // is paid per entry.  The loop is unrolled x2 over ping-pong Head / Rows slots (no copies of
 // in-flight loads).  A short block in three barrier-separated phases:
 //  stage   the gathered values (or distinct-column values) go to LDS;
-//  sum     lane t sums its 8 contiguous edges [8t, 8t+8) as row segments: the row holding each of
-//          its edges comes from the host-built lane info (krca_ppr_pack, one byte per edge), its 8
-//          values are independent LDS reads, and each finished segment is one no-return LDS atomic
-//          into its row's sum: no dependent LDS chain and no row offsets (round 1 searched the row
-//          offsets and walked the row ends, ~25 dependent LDS round trips per lane; round 3 first
-//          staged each row's index at its first edge and loaded two row offsets per row);
+//  sum     lane t sums its 8 contiguous edges [8t, 8t+8) as row segments: the host-built lane word
+//          (krca_ppr_pack, 2 bytes) gives the sum slot of the row holding edge 8t and the edges that
+//          start a row; the block's non-empty rows have consecutive slots, so each segment ends in
+//          one no-return LDS atomic into the current slot and moves to the next; the 8 values are
+//          independent LDS reads: no dependent LDS chain and no row offsets (round 1 searched the
+//          row offsets and walked the row ends, ~25 dependent LDS round trips per lane; round 3
+//          first staged each row's index at its first edge and loaded two row offsets per row,
+//          then carried one row byte per edge: 8 bytes per lane);
 //  update  lane r updates row r (teleport, residual, next w).
 #ifdef PPR_TIMING
 __device__ unsigned long long g_ppr_timing[4096 * 5];  // per workgroup: stage, sum, update, long, blocks
@@ -344,11 +347,11 @@ __device__ unsigned long long g_ppr_timing[4096 * 5];  // per workgroup: stage, 
 template <int FLAGS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 8))) void ppr_step(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
-    const uint64_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
+    const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
     int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz) {
   __shared__ uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
-  __shared__ unsigned long long rowsum[ROW_BUDGET];
+  __shared__ unsigned long long rowsum[ROW_BUDGET + 1];  // + the zero slot of rows without edges
   __shared__ int64_t red[TPB / 64];
   int64_t b = blockIdx.x;
   if (b >= nblk) return;
@@ -361,6 +364,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   k.tu = (int64_t)((1.0 / (double)N) * k.tele);
   k.alpha = alpha;
   const int tid = threadIdx.x;
+  if (tid == 0) rowsum[ROW_BUDGET] = 0ull;  // never added to (the entries' barriers order it)
   Head H0, H1;
   Rows R0, R1;
   load_head<(FLAGS & PPR_NT) != 0>(plan, b, pk, H0);
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       PPR_T(0);
       const int a = tid * SEG;
       if (a < ne) {
-        const uint2 hr = rc.li;  // byte k: the row holding edge a + k
+        const uint32_t M = rc.li & 0xFFu;  // bits of the lane's edges that start a row
         const uint4 sx = rc.ix;  // this lane's own slots (prefetched with the rows)
         // the 8 LDS reads are unconditional (a slot past the block's edges is clamped into the
         // table and its value dropped by the select), so they issue back to back: a read under a
@@ -428,15 +432,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
           c[kk] = vals[sl & (EDGE_BUDGET - 1)];
         }
         int64_t sacc = wdec(c[0]);
-        uint32_t row = hr.x & 0xFFu;
+        uint32_t row = rc.li >> 8;  // the slot of the row holding edge a; each head: the next slot
 #pragma unroll
         for (int kk = 1; kk < SEG; ++kk) {
-          const uint32_t rk = ((kk < 4 ? hr.x : hr.y) >> (8 * (kk & 3))) & 0xFFu;
-          if (rk != row) {  // edge a + kk starts the next row's segment
+          if ((M >> kk) & 1u) {  // edge a + kk starts the next row's segment
             atomicAdd(&rowsum[row], (unsigned long long)sacc);  // no return: no wait
             sacc = 0;
+            ++row;
           }
-          row = rk;
           sacc += a + kk < ne ? wdec(c[kk]) : 0;
         }
         atomicAdd(&rowsum[row], (unsigned long long)sacc);
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       __syncthreads();
       PPR_T(1);
       if (tid < nrows)
-        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[tid], rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
+        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[rc.rs], rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
       __syncthreads();  // rowsum / vals are rewritten by the next entry
       PPR_T(2);
     } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
@@ -613,14 +616,14 @@ int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t*
 }
 
 namespace {
-int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint64_t* lane,
+int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
                 const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                 int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
                 void* stream);
 }
 
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
-                        const uint64_t* lane, const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
+                        const uint16_t* lane, const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send,
                         void* ctl, void* stream) {
   return launch_step(row_ptr, col, plan, plan_len, lane, w_all, outdeg, q_local, n_local, n_max, N, alpha, flags, r_local,
@@ -628,7 +631,7 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
 }
 
 int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
-                       const uint64_t* lane, int64_t* w, const int32_t* outdeg, const int64_t* q, int64_t N, double alpha,
+                       const uint16_t* lane, int64_t* w, const int32_t* outdeg, const int64_t* q, int64_t N, double alpha,
                        int32_t flags, double tol, int64_t* r, int64_t* send, void* ctl, void* stream) {
   KRCA_CHECK_ARG(plan_len > 0 && N > 0, "krca_ppr_solo_step: bad sizes");
   const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
@@ -645,7 +648,7 @@ int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t
 }  // extern "C"
 
 namespace {
-int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint64_t* lane,
+int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
                 const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                 int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
                 void* stream) {
@@ -734,7 +737,7 @@ int64_t krca_ppr_workspace_size(int64_t N) {
 }
 
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int64_t* plan,
-             int64_t plan_len, const uint64_t* lane, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
+             int64_t plan_len, const uint16_t* lane, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
              void* workspace, float* r_out, int64_t* r_fixed, int64_t* q_out, int32_t* iters_host, void* stream) {
   KRCA_CHECK_ARG(N > 0 && N < INT32_MAX, "krca_ppr: N=%lld out of range", (long long)N);
   KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && lane && seed && workspace && r_out, "krca_ppr: null pointer");

@@ -40,6 +40,6 @@ KRCA_HD int64_t remap_col(int64_t j, int64_t n_max) {
 // host: CSR-adaptive row blocks (ppr_pack.cpp)
 int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out);
 int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_max, int64_t* plan, int64_t plan_len,
-                    int32_t* pk, uint64_t* lane);
+                    int32_t* pk, uint16_t* lane);
 
 }  // namespace pprl

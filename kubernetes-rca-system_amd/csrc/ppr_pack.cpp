@@ -67,7 +67,7 @@ int64_t build_plan(const int64_t* rp, int64_t N, int64_t* out) {
 // columns fit becomes a dictionary block (sorted distinct columns, then uint16 slots per edge),
 // every other block stays direct.  Returns the number of dictionary blocks.
 int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_max, int64_t* plan, int64_t plan_len,
-                    int32_t* pk, uint64_t* lane) {
+                    int32_t* pk, uint16_t* lane) {
   auto remap = [n_max](int64_t j) { return (int32_t)remap_col(j, n_max); };
   std::vector<int32_t> uniq;
   std::vector<uint16_t> slot;
@@ -75,15 +75,24 @@ int64_t pack_blocks(const int64_t* rp, const int32_t* col, int64_t N, int64_t n_
   for (int64_t p = 0; p < plan_len; p += 4) {
     const int64_t rb = plan[p], code = plan[p + 1], e0 = plan[p + 2], e1 = plan[p + 3];
     const int64_t ne = e1 - e0;
-    uint64_t* li = lane + (p / 4) * TPB;
-    for (int t = 0; t < TPB; ++t) li[t] = 0;
-    if (code > 0) {  // lane t: byte k = block-relative row holding edge 8t + k (past the block's
-                     // last edge: that edge's row, so the lane's tail starts no segment)
-      int64_t rr = rb;
-      for (int64_t e = 0; e < ceil_div(ne, SEG) * SEG; ++e) {
-        if (e < ne)
-          while (rp[rr + 1] - e0 <= e) ++rr;  // the row holding edge e (empty rows hold none)
-        li[e / SEG] |= (uint64_t)(rr - rb) << (8 * (e % SEG));
+    uint16_t* li = lane + (p / 4) * 2 * TPB;  // [TPB] lane words, then [TPB] row slots
+    uint16_t* rs = li + TPB;
+    for (int t = 0; t < TPB; ++t) {
+      li[t] = 0;
+      rs[t] = (uint16_t)ROW_BUDGET;  // no edges: the block's always-zero sum slot
+    }
+    if (code > 0) {
+      // the block's non-empty rows get consecutive sum slots, so a lane's next segment is the next
+      // slot: lane t = (slot of the row holding edge 8t) << 8 | bits of its edges that start a row
+      int slot = -1;
+      for (int64_t rr = rb; rr < code; ++rr) {
+        if (rp[rr + 1] == rp[rr]) continue;
+        rs[rr - rb] = (uint16_t)++slot;
+        const int64_t f = rp[rr] - e0;  // the row's first edge
+        if (f % SEG) li[f / SEG] |= (uint16_t)(1u << (f % SEG));
+        for (int64_t e = (f + SEG - 1) / SEG * SEG; e < rp[rr + 1] - e0; e += SEG)  // lanes starting inside the row
+          li[e / SEG] = (uint16_t)((li[e / SEG] & 0xFFu) | (slot << 8));
+        if (f % SEG == 0) li[f / SEG] = (uint16_t)((li[f / SEG] & 0xFFu) | (slot << 8));
       }
     }
     bool dict = false;
@@ -138,10 +147,10 @@ int krca_ppr_plan(const int64_t* row_ptr_host, int64_t N, int64_t* plan_host, in
   return KRCA_OK;
 }
 
-int64_t krca_ppr_lane_size(int64_t plan_len) { return plan_len / 4 * TPB; }
+int64_t krca_ppr_lane_size(int64_t plan_len) { return plan_len / 4 * 2 * TPB; }
 
 int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
-                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint64_t* lane_host) {
+                      int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host) {
   KRCA_CHECK_ARG(row_ptr_host && plan_host && pk_host && lane_host && N > 0 && N < INT32_MAX && n_max > 0,
                  "krca_ppr_pack: bad arguments");
   const int64_t E = row_ptr_host[N];

@@ -624,12 +624,12 @@ class NativeEngine:
         n = self.lib.krca_ppr_plan_size(rp.ctypes.data_as(c_vp), N)
         plan = np.zeros(max(n, 4), dtype=np.int64)
         pk = np.zeros(len(cl) + 64, dtype=np.int32)  # the step's clamped loads stay inside the padding
-        lane = np.zeros(max(self.lib.krca_ppr_lane_size(n), 1), dtype=np.uint64)
+        lane = np.zeros(max(self.lib.krca_ppr_lane_size(n), 1), dtype=np.uint16)
         nd = self.lib.krca_ppr_pack(rp.ctypes.data_as(c_vp), cl.ctypes.data_as(c_vp), N, int(n_max or N),
                                     plan.ctypes.data_as(c_vp), n, pk.ctypes.data_as(c_vp), lane.ctypes.data_as(c_vp))
         if nd < 0:
             _check(int(nd), "krca_ppr_pack", self.lib)
-        return self._dev(plan), n, self._dev(pk), self._dev(lane.view(np.int64)), int(nd)
+        return self._dev(plan), n, self._dev(pk), self._dev(lane.view(np.int16)), int(nd)
 
     def ppr_plan(self, row_ptr_host):
         rp = np.ascontiguousarray(row_ptr_host, dtype=np.int64)

@@ -58,7 +58,7 @@ for m in cases:
             pl = lib.krca_ppr_plan_size(rp.ctypes.data, Nn)
             plan = np.zeros(pl, np.int64)
             pk = np.zeros(len(col), np.int32)
-            lane = np.zeros(lib.krca_ppr_lane_size(pl), np.uint64)
+            lane = np.zeros(lib.krca_ppr_lane_size(pl), np.uint16)
             nd = lib.krca_ppr_pack(rp.ctypes.data, col.ctypes.data, Nn, n_max, plan.ctypes.data, pl, pk.ctypes.data,
                                    lane.ctypes.data)
             assert nd >= 0, lib.krca_last_error()

@@ -122,7 +122,7 @@ def test_ppr_pack_decodes_to_the_remapped_columns():
         n = lib.krca_ppr_plan_size(rp.ctypes.data_as(vp), len(rp) - 1)
         plan = np.zeros(n, np.int64)
         pk = np.zeros(len(col), np.int32)
-        lane = np.zeros(lib.krca_ppr_lane_size(n), np.uint64)
+        lane = np.zeros(lib.krca_ppr_lane_size(n), np.uint16)
         nd = lib.krca_ppr_pack(rp.ctypes.data_as(vp), col.ctypes.data_as(vp), len(rp) - 1, n_max,
                                plan.ctypes.data_as(vp), n, pk.ctypes.data_as(vp), lane.ctypes.data_as(vp))
         assert nd > 0.5 * (n // 4), nd  # most blocks of a service mesh are dictionary blocks
@@ -130,17 +130,21 @@ def test_ppr_pack_decodes_to_the_remapped_columns():
         got = np.full(len(col), -1, np.int64)
         for bi, (h, code, e0, e1) in enumerate(plan.reshape(-1, 4)):
             nu = int(h) >> 32
-            if code > 0:  # lane info: byte k = block-relative row holding edge 8t + k
+            if code > 0:  # lane words: (slot of the row holding edge 8t) << 8 | row-start bits
                 rb = int(h) & 0xFFFFFFFF
                 ne = int(e1 - e0)
-                # the row holding each edge of the block (empty rows hold none)
-                holder = np.repeat(np.arange(code - rb), np.diff(rp[rb:code + 1]))
+                deg = np.diff(rp[rb:code + 1])
+                slots = lane[bi * 512 + 256:bi * 512 + 256 + (code - rb)].astype(np.int64)
+                # non-empty rows: consecutive slots in row order; rows without edges: slot 256
+                assert np.array_equal(slots[deg > 0], np.arange(int((deg > 0).sum())))
+                assert np.all(slots[deg == 0] == 256)
+                holder = np.repeat(slots, deg)  # the slot of the row holding each edge
+                starts = set((rp[rb:code][deg > 0] - e0).tolist())
                 assert len(holder) == ne
                 for t in range(0, (ne + 7) // 8):
-                    li = int(lane[bi * 256 + t])
-                    for k in range(8):
-                        e = min(8 * t + k, ne - 1)  # past the block: the last edge's row
-                        assert (li >> (8 * k)) & 0xFF == holder[e], (bi, t, k)
+                    li = int(lane[bi * 512 + t])
+                    assert li >> 8 == holder[8 * t], (bi, t)
+                    assert li & 0xFE == sum(1 << k for k in range(1, 8) if 8 * t + k in starts), (bi, t)
             if nu == 0:
                 got[e0:e1] = pk[e0:e1]
                 continue

@@ -48,6 +48,8 @@ for s in "$@"; do
       done; unset KRCA_CORR_BATCH ;;
     ranking) step ranking 600 python3 -u tools/ranking_ablation_c4.py --seeds 2 --out $O/ranking_ablation_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
+    ppr_head)  # the same profile with the committed tree's code (ab_head/: git archive HEAD, built in place)
+      step ppr_head 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ppr_head -o run -- python3 ab_head/tools/prof_kernels.py ppr --reps 5 ;;
     ppr_bytes) step ppr_bytes 300 python3 tools/ppr_bench.py --reps 5 ;;
     ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
     ppr_timing) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_wtime.so; step ppr_timing 300 python3 tools/ppr_timing.py; unset KRCA_LIB ;;
@@ -71,6 +73,7 @@ for s in "$@"; do
       pmc pmc_ppr_tcp ppr TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum
       pmc pmc_ppr_ea ppr TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum
       pmc pmc_ppr_grbm ppr GRBM_GUI_ACTIVE GRBM_COUNT ;;
+    pmc_ppr_dram) pmc pmc_ppr_dram ppr TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum ;;
     pmc_logs_ea) pmc pmc_logs_ea logs TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum ;;
     pmc_logs_ea_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#pmc_logs_ea_}.so
       pmc $s logs TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum; unset KRCA_LIB ;;

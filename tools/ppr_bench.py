@@ -55,13 +55,13 @@ def main():
     ne = plan[:, 3] - plan[:, 2]
     d = nu > 0
     edge_bytes = int(4 * nu[d].sum() + 2 * ne[d].sum() + 4 * ne[~d].sum())
-    # algorithmic bytes per iteration: plan + lane info (8 B per lane: the row of
-    # each of its 8 edges) + packed columns + q and the alpha/outdeg coefficients read + weight
+    # algorithmic bytes per iteration: plan + lane info (a 2-byte word per lane and
+    # a 2-byte sum slot per row) + packed columns + q and the alpha/outdeg coefficients read + weight
     # codes written + codes gathered once (compulsory); r is written on the last iteration.
     # fabric_bytes_per_iter prices the gathered table once per XCD instead (8 XCDs, each with its
     # own L2: the least an L2-miss counter can show for a table that every XCD's rows gather from
     # at random).
-    base = 32 * len(plan) + 8 * 256 * len(plan) + edge_bytes + 8 * N + 8 * N + 4 * N
+    base = 32 * len(plan) + 4 * 256 * len(plan) + edge_bytes + 8 * N + 8 * N + 4 * N
     per_iter = base + 4 * N
     fabric_per_iter = base + 8 * 4 * N
     out = dict(kernel="ppr propagate (init + 30 x (step + reduce))", dict=a.dict, pods=N, edges=E,
