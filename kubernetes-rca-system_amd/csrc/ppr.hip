@@ -350,7 +350,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
     int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz) {
-  __shared__ uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
+  __shared__ __attribute__((aligned(16))) uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
   __shared__ unsigned long long rowsum[ROW_BUDGET + 1];  // + the zero slot of rows without edges
   __shared__ int64_t red[TPB / 64];
   int64_t b = blockIdx.x;
@@ -420,29 +420,47 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       const int a = tid * SEG;
       if (a < ne) {
         const uint32_t M = rc.li & 0xFFu;  // bits of the lane's edges that start a row
-        const uint4 sx = rc.ix;  // this lane's own slots (prefetched with the rows)
-        // the 8 LDS reads are unconditional (a slot past the block's edges is clamped into the
-        // table and its value dropped by the select), so they issue back to back: a read under a
-        // per-edge branch was a branch with its own lgkmcnt(0) wait, 8 dependent LDS round trips
+        // the 8 LDS reads are unconditional (a slot past the block's edges reads a value the
+        // sum drops), so they issue back to back: a read under a per-edge branch was a branch
+        // with its own lgkmcnt(0) wait, 8 dependent LDS round trips.  Direct blocks read the
+        // lane's 8 staged edges as two 16-byte reads; dictionary blocks read one slot each (the
+        // branch is block-uniform: no per-value select between the two addressings)
         uint32_t c[SEG];
+        if (dict) {
+          const uint4 sx = rc.ix;  // this lane's own slots (prefetched with the rows)
 #pragma unroll
-        for (int kk = 0; kk < SEG; ++kk) {
-          const uint32_t wd = kk < 2 ? sx.x : kk < 4 ? sx.y : kk < 6 ? sx.z : sx.w;
-          const int sl = dict ? (int)((wd >> (16 * (kk & 1))) & 0xFFFFu) : a + kk;
-          c[kk] = vals[sl & (EDGE_BUDGET - 1)];
+          for (int kk = 0; kk < SEG; ++kk) {
+            const uint32_t wd = kk < 2 ? sx.x : kk < 4 ? sx.y : kk < 6 ? sx.z : sx.w;
+            c[kk] = vals[(wd >> (16 * (kk & 1))) & (EDGE_BUDGET - 1)];
+          }
+        } else {
+          const uint4 lo = *reinterpret_cast<const uint4*>(vals + a), hi = *reinterpret_cast<const uint4*>(vals + a + 4);
+          c[0] = lo.x; c[1] = lo.y; c[2] = lo.z; c[3] = lo.w;
+          c[4] = hi.x; c[5] = hi.y; c[6] = hi.z; c[7] = hi.w;
         }
         int64_t sacc = wdec(c[0]);
-        uint32_t row = rc.li >> 8;  // the slot of the row holding edge a; each head: the next slot
+        // byte offset of the current row's sum slot; each head: the next slot
+        uint32_t row8 = (rc.li >> 8) * (uint32_t)sizeof(unsigned long long);
+        char* const rsb = reinterpret_cast<char*>(rowsum);
+        auto flush = [&]() {
+          atomicAdd(reinterpret_cast<unsigned long long*>(rsb + row8), (unsigned long long)sacc);  // no return: no wait
+          sacc = 0;
+          row8 += (uint32_t)sizeof(unsigned long long);
+        };
+        if (a + SEG <= ne) {  // every edge of the lane is the block's (all lanes but one per block)
 #pragma unroll
-        for (int kk = 1; kk < SEG; ++kk) {
-          if ((M >> kk) & 1u) {  // edge a + kk starts the next row's segment
-            atomicAdd(&rowsum[row], (unsigned long long)sacc);  // no return: no wait
-            sacc = 0;
-            ++row;
+          for (int kk = 1; kk < SEG; ++kk) {
+            if ((M >> kk) & 1u) flush();  // edge a + kk starts the next row's segment
+            sacc += wdec(c[kk]);
           }
-          sacc += a + kk < ne ? wdec(c[kk]) : 0;
+        } else {
+#pragma unroll
+          for (int kk = 1; kk < SEG; ++kk) {
+            if ((M >> kk) & 1u) flush();
+            sacc += a + kk < ne ? wdec(c[kk]) : 0;
+          }
         }
-        atomicAdd(&rowsum[row], (unsigned long long)sacc);
+        atomicAdd(reinterpret_cast<unsigned long long*>(rsb + row8), (unsigned long long)sacc);
       }
       __syncthreads();
       PPR_T(1);
