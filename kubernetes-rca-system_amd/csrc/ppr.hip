@@ -68,7 +68,7 @@ struct Ctl {          // device control block (header of the ctl buffer)
   int32_t iter;       // iterations done
   uint32_t done;      // single device, reduction fused: workgroups of the running step that finished
 };
-// ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n] (8-byte slots) | double coef[n].  The long-row
+// ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n] (8-byte slots) | {double coef, double q}[n].  The long-row
 // accumulators and tickets are zero when allocated and reset by the last chunk of each row.
 
 __device__ __forceinline__ int64_t* acc_long_of(Ctl* ctl) {
@@ -77,8 +77,11 @@ __device__ __forceinline__ int64_t* acc_long_of(Ctl* ctl) {
 __device__ __forceinline__ uint32_t* ticket_of(Ctl* ctl, int64_t n) {
   return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctl) + CTL_BYTES + 8 * n);
 }
-// per-row edge coefficient alpha / outdeg (0 for a dangling row), written by the solve's init:
-// the step multiplies instead of dividing per row and iteration
+// per-row pair {edge coefficient alpha / outdeg (0 for a dangling row), seed q_i as a double},
+// written by the solve's init: the step multiplies instead of dividing per row and iteration, and
+// loads both with one 16-byte read and no int64 -> double conversion ((double)q_i is exact: q_i <
+// 2^53)
+static_assert(CTL_BYTES % 16 == 0, "16-byte row pairs");
 __device__ __forceinline__ double* coef_of(Ctl* ctl, int64_t n) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(ctl) + CTL_BYTES + 16 * n);
 }
@@ -133,7 +136,8 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
     q[i] = qi;
     qs += qi;
     r[i] = r0;
-    coef[i] = edge_coef(deg, alpha);
+    coef[2 * i] = edge_coef(deg, alpha);
+    coef[2 * i + 1] = (double)qi;
     reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(r0, deg, alpha));
     if (deg == 0) dang += r0;
   }
@@ -159,7 +163,8 @@ __global__ __launch_bounds__(TPB) void ppr_init_warm(const float* __restrict__ s
     q[i] = qi;
     qs += qi;
     const int64_t ri = r[i];
-    coef[i] = edge_coef(deg, alpha);
+    coef[2 * i] = edge_coef(deg, alpha);
+    coef[2 * i + 1] = (double)qi;
     reinterpret_cast<uint32_t*>(send)[i] = wenc(edge_weight(ri, deg, alpha));
     if (deg == 0) dang += ri;
   }
@@ -214,10 +219,10 @@ __device__ void reduce_single(const int64_t* slice_slots, int64_t* next_slots, d
 // = the L1 stop rule needs |r_new - r_old| (ro was loaded), PPR_WRITE_R = store r_new (every
 // iteration under a tolerance; only the last one of a fixed-iteration solve).
 template <int FLAGS>
-__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, int64_t qi, int64_t ro, double coef,
+__device__ __forceinline__ void update_row(int64_t i, int64_t pulled, double qd, int64_t ro, double coef,
                                            const StepScalars& k, int64_t* __restrict__ r,
                                            int64_t* __restrict__ send, int64_t& err, int64_t& dang) {
-  const int64_t t = k.qt > 0 ? (int64_t)((double)qi * k.tq) : k.tu;
+  const int64_t t = k.qt > 0 ? (int64_t)(qd * k.tq) : k.tu;  // qd = (double)q_i
   const int64_t rn = pulled + t;
   if (FLAGS & PPR_WRITE_R) r[i] = rn;
   if (FLAGS & PPR_RESIDUAL) err += rn > ro ? rn - ro : ro - rn;
@@ -246,8 +251,8 @@ struct Head {
   uint32_t c[SEG];  // remapped columns (uint32 units of the exchange layout)
 };
 struct Rows {
-  int64_t my_q, my_r;
-  double my_coef;  // alpha / outdeg (coef_of)
+  int64_t my_r;
+  double my_coef, my_qd;  // alpha / outdeg and (double)q_i (coef_of)
   uint32_t li;  // krca_ppr_pack lane word: (sum slot of the row holding edge 8t) << 8 | head bits
   uint32_t rs;  // the sum slot of the lane's row (ROW_BUDGET: a row without edges)
   uint4 ix;     // dictionary blocks: the slots of edges 8t .. 8t+7 (uint16 pairs)
@@ -299,10 +304,12 @@ __device__ __forceinline__ void load_rows(const Meta& m, int64_t b, const uint16
   const uint32_t nrows = (uint32_t)(m.code > 0 ? m.code - m.rb : 1);
   constexpr bool NT = (FLAGS & PPR_NT) != 0;
   // the lane's row (lanes past the block's rows read 0 and update nothing)
-  R.my_q = buf_i64(buf_over(q + m.rb, 8 * nrows), 8 * tid);
-  R.my_r = (FLAGS & PPR_RESIDUAL) ? buf_i64(buf_over(r + m.rb, 8 * nrows), 8 * tid) : 0;
-  R.my_coef = __builtin_bit_cast(double, buf_i64(buf_over(coef + m.rb, 8 * nrows), 8 * tid));
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  R.my_r = (FLAGS & PPR_RESIDUAL) ? buf_i64(buf_over(r + m.rb, 8 * nrows), 8 * tid) : 0;
+  const u32x4 cq = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(buf_over(coef + 2 * m.rb, 16 * nrows),
+                                                                                    (int)(16 * tid), 0, 0));
+  R.my_coef = __builtin_bit_cast(double, ((uint64_t)cq.y << 32) | cq.x);
+  R.my_qd = __builtin_bit_cast(double, ((uint64_t)cq.w << 32) | cq.z);
   const uint16_t* lb = lane_info + b * 2 * TPB;  // zero / empty for long-row chunks
   R.li = ld_stream<NT>(lb + tid);
   R.rs = ld_stream<NT>(lb + TPB + tid);
@@ -465,7 +472,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       __syncthreads();
       PPR_T(1);
       if (tid < nrows)
-        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[rc.rs], rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
+        update_row<FLAGS>(cur.rb + tid, (int64_t)rowsum[rc.rs], rc.my_qd, rc.my_r, rc.my_coef, k, r, send, err, dang);
       __syncthreads();  // rowsum / vals are rewritten by the next entry
       PPR_T(2);
     } else {  // chunk of long row rb: block sum -> row accumulator; the last chunk updates the row
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
           const int64_t pulled = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(acc, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          update_row<FLAGS>(rb, pulled, rc.my_q, rc.my_r, rc.my_coef, k, r, send, err, dang);
+          update_row<FLAGS>(rb, pulled, rc.my_qd, rc.my_r, rc.my_coef, k, r, send, err, dang);
         }
       }
       PPR_T(3);
@@ -589,7 +596,7 @@ unsigned grid_for(int64_t n, int64_t cap = 2048) {
 extern "C" {
 
 
-int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 24 * std::max<int64_t>(n_local, 1); }
+int64_t krca_ppr_ctl_size(int64_t n_local) { return CTL_BYTES + 32 * std::max<int64_t>(n_local, 1); }
 
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream) {
   KRCA_CHECK_ARG(E >= 0 && n_max > 0, "krca_ppr_remap_cols: bad sizes");
