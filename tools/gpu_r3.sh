@@ -38,6 +38,7 @@ for s in "$@"; do
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread ;;
     tests_corr) step tests_corr 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread ;;
     bench) step bench 300 python3 bench.py ;;
+    smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_trace) prof bench_trace 400 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     corr100k) prof corr100k 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5 ;;
     corr100k_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#corr100k_}.so; prof $s 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5; unset KRCA_LIB ;;
