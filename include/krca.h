@@ -263,6 +263,23 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col /*pk*/, const
                         int32_t flags, int64_t* r_local, int64_t* send /*!= w_all*/, void* ctl, void* stream);
 int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha,
                           double tol, int32_t first, void* ctl, int64_t* send_next, void* stream);
+/* Folded iterations (the default of krca/rca.py): init (partial sums in slot set 0 of send; the
+ * send slots and, at G = 1, the other buffer's must be zero before it), exchange, then per
+ * iteration it = 1, 2, ...: krca_ppr_shard_step_folded + exchange, and krca_ppr_shard_finish(it =
+ * the last) after the loop.  Step `it` does the reduction of step it - 1 itself (every workgroup
+ * sums slot set (it - 1) % 3 of the G slices of w_all: convergence, teleport scale, iteration
+ * count), adds its own partial sums into set it % 3 of send and zeroes set (it + 1) % 3 of
+ * next_target, the buffer the NEXT step writes: at G = 1 the ping-pong buffer it gathers from
+ * (w_all), at G > 1 the rank's send itself (the next step writes send again).  next_target must
+ * differ from send at G = 1 and equal it at G > 1.  One kernel and one exchange per iteration
+ * instead of two kernels; results bit-identical to the unfolded sequence. */
+int krca_ppr_shard_step_folded(const int64_t* row_ptr, const int32_t* col /*pk*/, const int64_t* plan, int64_t plan_len,
+                               const uint16_t* lane, const int64_t* w_all, int32_t G, const int32_t* outdeg,
+                               const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
+                               double tol, int32_t it, int32_t flags, int64_t* r_local, int64_t* send,
+                               int64_t* next_target, void* ctl, void* stream);
+int krca_ppr_shard_finish(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha, double tol,
+                          int32_t it, void* ctl, void* stream);
 /* Single device (G = 1, n_max = N): krca_ppr_shard_step with the iteration's krca_ppr_shard_reduce
  * (first = 0) done by the step's last workgroup — one launch per iteration instead of two.  Reads
  * the codes of w, writes r and send, zeroes w's partial-sum slots (w is the next step's write

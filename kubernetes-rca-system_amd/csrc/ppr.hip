@@ -26,7 +26,9 @@
 // (j / n_max) * (2 * slice - n_max)), so the step kernel gathers directly.  At G = 1 the
 // "exchange" is a swap of two such buffers (ping-pong), no copy.
 //
-// One iteration = ppr_step (pull SpMV fused with the rank update) + ppr_reduce (one block).
+// One iteration = ppr_step (pull SpMV fused with the rank update) + ppr_reduce (one block), or --
+// the default of krca/rca.py -- one folded ppr_step that first does the previous step's reduction
+// itself (Fold: every workgroup sums the previous slot set; three rotating sets in the payload).
 //   ppr_step, short-row blocks (<= 2048 edges, <= 256 rows, from krca_ppr_plan): coalesced col
 //     loads and 8 independent w[col] gathers per lane (lane-strided), staged in LDS; each lane
 //     then sums 8 CONTIGUOUS staged edges as row segments (binary search of its first row in the
@@ -189,6 +191,18 @@ struct Fuse {
   int64_t* w_next;  // the buffer the step gathered from = the next step's write target (slots zeroed)
 };
 
+// Folded iteration (krca_ppr_shard_step_folded): step `it` (1-based) does the reduction of step
+// it - 1 itself -- every workgroup sums the G ranks' slot set (it - 1) % NSET of w_all (integers:
+// every workgroup gets the same totals) and decides convergence / the teleport scale locally --
+// writes its own partial sums into set it % NSET of send, and workgroup 0 zeroes set (it + 1) % NSET
+// of the next step's write target.  No ppr_reduce launch between steps: one kernel and one
+// exchange per iteration.
+struct Fold {
+  int on, it, G;
+  double err_limit;
+  int64_t* next;  // the next step's write target (G = 1: the buffer gathered from; G > 1: send)
+};
+
 // the reduction of ppr_reduce over ONE slice (G = 1), by a whole workgroup: residual / dangling
 // sums of `slice` (atomically updated by this step's workgroups), convergence, next teleport scale,
 // the next write target's slots zeroed; called by the step's last workgroup only
@@ -202,7 +216,7 @@ __device__ void reduce_single(const int64_t* slice_slots, int64_t* next_slots, d
   }
   const int64_t err = block_sum_i64(e, red);
   const int64_t dang = block_sum_i64(d, red);
-  if (tid < NSLOT) next_slots[tid] = 0;
+  if (tid < SET_WORDS) next_slots[tid] = 0;
   if (tid != 0) return;
   ctl->done = 0;
   if (ctl->converged) return;
@@ -356,7 +370,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
     const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
-    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz) {
+    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz, Fold fo) {
   __shared__ __attribute__((aligned(16))) uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
   __shared__ unsigned long long rowsum[ROW_BUDGET + 1];  // + the zero slot of rows without edges
   __shared__ int64_t red[TPB / 64];
@@ -364,12 +378,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   if (b >= nblk) return;
   const int32_t conv = ctl->converged;
   if (conv) return;  // converged (tol > 0): no writes (uniform)
-  StepScalars k;
-  k.tele = ctl->tele;
-  k.qt = ctl->q_total;
-  k.tq = k.tele / (double)k.qt;
-  k.tu = (int64_t)((1.0 / (double)N) * k.tele);
-  k.alpha = alpha;
   const int tid = threadIdx.x;
   if (tid == 0) rowsum[ROW_BUDGET] = 0ull;  // never added to (the entries' barriers order it)
   Head H0, H1;
@@ -386,6 +394,53 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   // (vmcnt(N)) instead of vmcnt(0) at the join of an `if (b1 < nblk)`, which made the sum phase
   // wait for the NEXT entry's gathers and rows and undid the software pipeline
   load_head<(FLAGS & PPR_NT) != 0>(plan, b1 < nblk ? b1 : nblk - 1, pk, H1);
+  // the teleport scale of this step (after the first entry's loads are issued: a folded step's
+  // reduction of the previous one overlaps them)
+  StepScalars k;
+  int64_t* my_slots = send + wslots(n_max);  // this step's partial-sum slots
+  if (fo.on) {  // block-uniform
+    const int ps = (fo.it - 1) % NSET, zs = (fo.it + 1) % NSET;
+    const int64_t* wall = reinterpret_cast<const int64_t*>(w);
+    int64_t pe = 0, pd = 0, pq = 0;
+    for (int i = tid; i < fo.G * NSPREAD; i += TPB) {
+      const int64_t* sl = wall + (int64_t)(i / NSPREAD) * slice_words(n_max) + wslots(n_max) + ps * SET_WORDS + (i % NSPREAD);
+      pe += sl[0];
+      pd += sl[NSPREAD];
+      pq += sl[2 * NSPREAD];
+    }
+    {  // block_sum_i64's total is valid in thread 0: broadcast the three through LDS
+      const int64_t se = block_sum_i64(pe, red), sd = block_sum_i64(pd, red), sq = block_sum_i64(pq, red);
+      __syncthreads();
+      if (tid == 0) {
+        red[0] = se;
+        red[1] = sd;
+        red[2] = sq;
+      }
+      __syncthreads();
+    }
+    const int64_t errp = red[0], dangp = red[1], qsp = red[2];
+    __syncthreads();  // red is reused by the step's later block sums
+    const bool stop = fo.it > 1 && fo.err_limit > 0.0 && (double)errp < fo.err_limit;  // step it-1 converged
+    k.tele = (1.0 - alpha) * krca::kFix + alpha * (double)dangp;
+    k.qt = fo.it == 1 ? qsp : ctl->q_total;  // written by step 1's workgroup 0 (an earlier kernel)
+    if (blockIdx.x == 0) {
+      for (int i = tid; i < SET_WORDS; i += TPB) fo.next[wslots(n_max) + zs * SET_WORDS + i] = 0;
+      if (tid == 0) {
+        if (fo.it == 1) ctl->q_total = qsp;
+        ctl->iter = fo.it - 1;
+        if (stop) ctl->converged = fo.it - 1;
+        else ctl->tele = k.tele;
+      }
+    }
+    if (stop) return;  // uniform: every workgroup decided the same
+    my_slots += (fo.it % NSET) * SET_WORDS;
+  } else {
+    k.tele = ctl->tele;
+    k.qt = ctl->q_total;
+  }
+  k.tq = k.tele / (double)k.qt;
+  k.tu = (int64_t)((1.0 / (double)N) * k.tele);
+  k.alpha = alpha;
   int64_t err = 0, dang = 0;
 #ifdef PPR_TIMING
   uint64_t tacc[5] = {0, 0, 0, 0, 0};
@@ -513,8 +568,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   err = block_sum_i64(err, red);
   dang = block_sum_i64(dang, red);
   if (tid == 0) {
-    add_slot(send + wslots(n_max), err);
-    add_slot(send + wslots(n_max) + NSPREAD, dang);
+    add_slot(my_slots, err);
+    add_slot(my_slots + NSPREAD, dang);
   }
   if (fz.on) {  // block-uniform
     __shared__ int last;
@@ -547,7 +602,7 @@ __global__ __launch_bounds__(TPB) void ppr_reduce(const int64_t* __restrict__ w_
   const int64_t dang = block_sum_i64(part[1], red);
   const int64_t qs = block_sum_i64(part[2], red);
   __syncthreads();
-  if (threadIdx.x < NSLOT) send_next[wslots(n_max) + threadIdx.x] = 0;
+  if (threadIdx.x < SET_WORDS) send_next[wslots(n_max) + threadIdx.x] = 0;
   if (threadIdx.x != 0 || ctl->converged) return;
   if (first) {
     ctl->q_total = qs;
@@ -557,6 +612,29 @@ __global__ __launch_bounds__(TPB) void ppr_reduce(const int64_t* __restrict__ w_
       ctl->converged = ctl->iter;
       return;
     }
+  }
+  ctl->tele = (1.0 - alpha) * krca::kFix + alpha * (double)dang;
+}
+
+// the reduction of the last folded step (it): sums set it % NSET of the G slices, counts the
+// iteration and decides convergence -- what ppr_reduce does after every unfolded step
+__global__ __launch_bounds__(TPB) void ppr_finish(const int64_t* __restrict__ w_all, int32_t G, int64_t n_max,
+                                                  double alpha, double err_limit, int it, Ctl* ctl) {
+  __shared__ int64_t red[TPB / 64];
+  int64_t pe = 0, pd = 0;
+  for (int i = threadIdx.x; i < G * NSPREAD; i += TPB) {
+    const int64_t* sl = w_all + (int64_t)(i / NSPREAD) * slice_words(n_max) + wslots(n_max) + (it % NSET) * SET_WORDS +
+                        (i % NSPREAD);
+    pe += sl[0];
+    pd += sl[NSPREAD];
+  }
+  const int64_t err = block_sum_i64(pe, red);
+  const int64_t dang = block_sum_i64(pd, red);
+  if (threadIdx.x != 0 || ctl->converged) return;
+  ctl->iter = it;
+  if (err_limit > 0.0 && (double)err < err_limit) {
+    ctl->converged = it;
+    return;
   }
   ctl->tele = (1.0 - alpha) * krca::kFix + alpha * (double)dang;
 }
@@ -644,7 +722,7 @@ namespace {
 int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
                 const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                 int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
-                void* stream);
+                void* stream, Fold fo = Fold{0, 0, 1, 0.0, nullptr});
 }
 
 int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
@@ -653,6 +731,30 @@ int krca_ppr_shard_step(const int64_t* row_ptr, const int32_t* col, const int64_
                         void* ctl, void* stream) {
   return launch_step(row_ptr, col, plan, plan_len, lane, w_all, outdeg, q_local, n_local, n_max, N, alpha, flags, r_local,
                      send, ctl, Fuse{0, 0.0, nullptr}, stream);
+}
+
+int krca_ppr_shard_step_folded(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
+                               const uint16_t* lane, const int64_t* w_all, int32_t G, const int32_t* outdeg,
+                               const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
+                               double tol, int32_t it, int32_t flags, int64_t* r_local, int64_t* send,
+                               int64_t* next_target, void* ctl, void* stream) {
+  KRCA_CHECK_ARG(G >= 1 && it >= 1 && n_max > 0 && N > 0, "krca_ppr_shard_step_folded: bad sizes");
+  KRCA_CHECK_ARG(next_target && (G == 1 ? next_target == w_all : next_target == send),
+                 "krca_ppr_shard_step_folded: next_target is w_all at G = 1, send at G > 1");
+  const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
+  return launch_step(row_ptr, col, plan, plan_len, lane, w_all, outdeg, q_local, n_local, n_max, N, alpha, flags, r_local,
+                     send, ctl, Fuse{0, 0.0, nullptr}, stream, Fold{1, (int)it, (int)G, err_limit, next_target});
+}
+
+int krca_ppr_shard_finish(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha, double tol,
+                          int32_t it, void* ctl, void* stream) {
+  KRCA_CHECK_ARG(G >= 1 && it >= 1 && n_max > 0 && N > 0, "krca_ppr_shard_finish: bad sizes");
+  KRCA_CHECK_ARG(w_all && ctl, "krca_ppr_shard_finish: null pointer");
+  const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
+  hipLaunchKernelGGL(ppr_finish, dim3(1), dim3(TPB), 0, krca::as_stream(stream), w_all, G, n_max, alpha, err_limit,
+                     (int)it, reinterpret_cast<Ctl*>(ctl));
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
 }
 
 int krca_ppr_solo_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len,
@@ -676,7 +778,7 @@ namespace {
 int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan, int64_t plan_len, const uint16_t* lane,
                 const int64_t* w_all, const int32_t* outdeg, const int64_t* q_local, int64_t n_local, int64_t n_max,
                 int64_t N, double alpha, int32_t flags, int64_t* r_local, int64_t* send, void* ctl, Fuse fz,
-                void* stream) {
+                void* stream, Fold fo) {
   KRCA_CHECK_ARG(plan_len >= 0 && plan_len % 4 == 0 && n_local >= 0 && n_local <= n_max && N > 0,
                  "krca_ppr_shard_step: bad sizes");
   if (plan_len == 0) return KRCA_OK;
@@ -702,7 +804,7 @@ int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan,
                                            : (nt ? ppr_step<PPR_NT> : ppr_step<0>);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, lane, nblk,
                      reinterpret_cast<const uint32_t*>(w_all), outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
-                     reinterpret_cast<Ctl*>(ctl), fz);
+                     reinterpret_cast<Ctl*>(ctl), fz, fo);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

@@ -16,7 +16,9 @@ constexpr int EDGE_BUDGET = 2048;       // edges per short block == LDS slots
 constexpr int ROW_BUDGET = TPB;         // rows per short block (one updating lane per row)
 constexpr int SEG = EDGE_BUDGET / TPB;  // edges per lane: gathered lane-strided, summed contiguous
 constexpr int NSPREAD = 32;             // partial-sum slots per quantity (spreads the atomics)
-constexpr int NSLOT = 3 * NSPREAD;      // send tail: residual[32] | dangling[32] | seed total[32]
+constexpr int SET_WORDS = 3 * NSPREAD;  // one slot set: residual[32] | dangling[32] | seed total[32]
+constexpr int NSET = 3;                 // folded iterations rotate over 3 sets (read, write, zero)
+constexpr int NSLOT = NSET * SET_WORDS; // send tail
 constexpr int CTL_BYTES = 256;  // ctl buffer header (the device Ctl block)
 
 // 32-bit weight code: w < 2^26 as is; above, the top 26 bits (bit 25 set) and the shift in the top

@@ -79,6 +79,9 @@ SIGNATURES = {
     "krca_ppr_lane_size": (c_i64, [c_i64]),
     "krca_ppr_pack": (c_i64, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_shard_reduce": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_step_folded": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64,
+                                           c_f64, c_f64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_ppr_shard_finish": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp]),
     "krca_ppr_solo_step": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_f64, c_i32, c_f64, c_vp,
                                    c_vp, c_vp, c_vp]),
     "krca_ppr_ctl_read": (c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_vp]),

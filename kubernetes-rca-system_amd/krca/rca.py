@@ -10,8 +10,10 @@ Multi-GPU: one process per GPU; rank g owns pods [g*n_max, (g+1
 slice of the metric tensor and its rows of the pull-CSR.  Scoring needs no communication.  Each
 PageRank iteration ends with ONE all-gather over RCCL/xGMI of every rank's
 [weight codes | partial-sum slots] slice (slice_words(n_max) int64: the n_max 32-bit weight codes,
-then residual, dangling mass and seed total, NSPREAD slots each); the partial sums ride in the same payload and every rank reduces them
-identically, so no extra collective or broadcast is needed.  With one rank the exchange is a swap
+then NSET sets of residual, dangling mass and seed total, NSPREAD slots each); the partial sums ride in the same payload and every rank reduces them
+identically, so no extra collective or broadcast is needed.  Iterations are folded
+(krca_ppr_shard_step_folded): each step first reduces the previous step's slot set itself, so an
+iteration is one kernel and one exchange.  With one rank the exchange is a swap
 of two buffers (the step kernel reads one and writes the other).  Arithmetic is integer fixed
 point: the result is bit-identical for any G and to oracle/krca_oracle.c.  The final top-k merges G x k candidates.
 
@@ -24,7 +26,9 @@ import math
 import numpy as np
 
 NSPREAD = 32
-NSLOT = 3 * NSPREAD  # == krca_ppr_nslot()
+SET_WORDS = 3 * NSPREAD  # one slot set: residual | dangling | seed total, NSPREAD slots each
+NSET = 3  # folded iterations rotate over 3 sets (read the previous step's, write, zero the next)
+NSLOT = NSET * SET_WORDS  # == krca_ppr_nslot()
 
 
 def wslots(n_max):
@@ -257,6 +261,7 @@ class DeviceShard:
     def init_warm(self, alpha, seed_floor):
         """Re-seed from the current scores, start from the ranks of the previous solve."""
         e, p = self.eng, self.eng.ptr
+        self._zero_slots()
         self._chk(e.lib.krca_ppr_shard_init_warm(p(self.score_out["score"]), float(seed_floor), p(self.outdeg), self.n,
                                                  self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
                                                  p(self.send), e._stream()), "krca_ppr_shard_init_warm")
@@ -294,8 +299,17 @@ class DeviceShard:
         self.score_out = self.eng.rolling_score_device(self.x, self.cfg.window, self.cfg.z_threshold, self.score_out)
         return self.score_out
 
+    def _zero_slots(self):
+        """Partial-sum slots zeroed before an init adds into send's set 0 (and, at G = 1, the other
+        ping-pong buffer's, which the first folded step writes)."""
+        wsl = wslots(self.n_max)
+        self.send[wsl:].zero_()
+        if self.world == 1:
+            self.w_all[wsl:].zero_()
+
     def init(self, alpha, seed_floor):
         e, p = self.eng, self.eng.ptr
+        self._zero_slots()
         self._chk(e.lib.krca_ppr_shard_init(p(self.score_out["score"]), float(seed_floor), p(self.outdeg), self.n,
                                             self.n_max, self.N, float(alpha), p(self.ctl), p(self.q), p(self.r),
                                             p(self.send), e._stream()), "krca_ppr_shard_init")
@@ -317,6 +331,26 @@ class DeviceShard:
                                               p(self.w_all), p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
                                               float(alpha), int(flags), p(self.r), p(self.send), p(self.ctl), st))
             self._chk(e.lib.krca_ppr_shard_step(*args), "krca_ppr_shard_step")
+
+    def step_folded(self, alpha, tol, it, flags):
+        """Folded iteration `it` (1-based): the reduction of step it - 1 and the step, one kernel."""
+        e, p = self.eng, self.eng.ptr
+        if not self.plan_len:
+            return
+        st = e._stream()
+        nxt = self.w_all if self.world == 1 else self.send
+        key = ("fold", self.w_all.data_ptr(), self.send.data_ptr(), float(alpha), float(tol), int(it), int(flags), st.value)
+        args = self._cached(key, lambda: (p(self.row_ptr), p(self.col), p(self.plan), self.plan_len, p(self.lane),
+                                          p(self.w_all), self.world, p(self.outdeg), p(self.q), self.n, self.n_max, self.N,
+                                          float(alpha), float(tol), int(it), int(flags), p(self.r), p(self.send), p(nxt),
+                                          p(self.ctl), st))
+        self._chk(e.lib.krca_ppr_shard_step_folded(*args), "krca_ppr_shard_step_folded")
+
+    def finish(self, alpha, tol, it):
+        """The reduction of the last folded step (iteration count, convergence)."""
+        e, p = self.eng, self.eng.ptr
+        self._chk(e.lib.krca_ppr_shard_finish(p(self.w_all), self.world, self.n_max, self.N, float(alpha), float(tol),
+                                              int(it), p(self.ctl), e._stream()), "krca_ppr_shard_finish")
 
     def reduce(self, alpha, tol, first):
         e, p = self.eng, self.eng.ptr
@@ -384,14 +418,16 @@ class RcaStep:
         self._g.replay()
 
     def _propagate(self):
+        """init, exchange, then iters x (folded step, exchange) and the last step's reduction: the
+        same results as init / reduce(first) / iters x (step, exchange, reduce), one kernel fewer
+        per iteration (krca_ppr_shard_step_folded)."""
         s, c, cfg = self.s, self.comm, self.cfg
         s.init(cfg.alpha, cfg.floor(s.N, s.M))
         c.exchange(s)
-        s.reduce(cfg.alpha, cfg.tol, 1)
-        for it in range(cfg.iters):
-            s.step(cfg.alpha, step_flags(cfg.tol, it + 1 == cfg.iters))
+        for it in range(1, cfg.iters + 1):
+            s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == cfg.iters))
             c.exchange(s)
-            s.reduce(cfg.alpha, cfg.tol, 0)
+        s.finish(cfg.alpha, cfg.tol, cfg.iters)
 
     def run(self, to_host=True, score_events=None):
         """One RCA step; score_events = (start, end) HIP events recorded around the scoring kernel."""

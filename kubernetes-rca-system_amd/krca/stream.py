@@ -85,21 +85,21 @@ class StreamingRCA:
         else:
             s.init(cfg.alpha, cfg.floor(s.N, s.M))
         self.comm.exchange(s)
-        s.reduce(cfg.alpha, self.tol, 1)
-        # iterations in batches of check_every; the convergence flag of batch b is read while batch
-        # b + 1 runs (a pinned copy + event): the GPU never idles on the poll, and iterations enqueued
-        # past convergence do nothing (the kernels exit on the device-held flag), so the ranks and
-        # the iteration count are the same as with a synchronous check after every batch
+        # folded iterations (each step reduces the previous one: one kernel + one exchange) in
+        # batches of check_every; the convergence flag of batch b is read while batch b + 1 runs (a
+        # pinned copy + event): the GPU never idles on the poll, and iterations enqueued past
+        # convergence do nothing (the kernels exit on the device-held flag), so the ranks and the
+        # iteration count are the same as with a synchronous check after every batch
         it, pending = 0, None
         while it < self.max_iter:
             for _ in range(min(self.check_every, self.max_iter - it)):
-                s.step(cfg.alpha, 3)  # tol > 0: residual + ranks every iteration
+                it += 1
+                s.step_folded(cfg.alpha, self.tol, it, 3)  # tol > 0: residual + ranks every iteration
                 self.comm.exchange(s)
-                s.reduce(cfg.alpha, self.tol, 0)
-            it += min(self.check_every, self.max_iter - it)
             if pending is not None and s.ctl_wait(pending)[1]:
                 break
             pending = s.ctl_async() if it < self.max_iter else None
+        s.finish(cfg.alpha, self.tol, it)
         # the final counts ride behind the key / top-k launches: one synchronisation (the merge's
         # copy of the candidates) instead of a read-back before them
         h = s.ctl_async()

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 import oracle
-from krca.rca import NSPREAD, remap_cols, slice_words, wslots
+from krca.rca import NSET, NSPREAD, SET_WORDS, remap_cols, slice_words, wslots
 
 FIX = 1152921504606846976.0
 
@@ -66,12 +66,50 @@ class NumpyShard:
         self.r = np.full(self.n, r0, np.int64)
         snd = self.send.numpy()
         snd[self.ws:] = 0
+        if self.world == 1:
+            self.w_all.numpy()[self.ws:] = 0  # the first folded step writes the other buffer
         snd.view(np.uint32)[:self.n] = _w(self.r, self.deg, alpha)
         snd[self.ws + NSPREAD] = int(self.r[self.deg == 0].sum())
         snd[self.ws + 2 * NSPREAD] = int(self.q.sum())
         self.ctl = dict(tele=0.0, q_total=0, converged=0, iter=0)
 
-    def step(self, alpha, flags=3):
+    def _set_sums(self, sset):
+        w = self.w_all.numpy().reshape(self.world, slice_words(self.n_max))[:, self.ws + sset * SET_WORDS:]
+        return tuple(int(w[:, i * NSPREAD:(i + 1) * NSPREAD].sum()) for i in range(3))
+
+    def step_folded(self, alpha, tol, it, flags=3):
+        """krca_ppr_shard_step_folded: the reduction of set (it-1) % NSET, then the step into set
+        it % NSET; set (it+1) % NSET of the next write target zeroed."""
+        c = self.ctl
+        if c["converged"]:
+            return
+        err, dang, qs = self._set_sums((it - 1) % NSET)
+        nxt = self.w_all if self.world == 1 else self.send
+        zs = self.ws + ((it + 1) % NSET) * SET_WORDS
+        nxt.numpy()[zs:zs + SET_WORDS] = 0
+        if it == 1:
+            c["q_total"] = qs
+        c["iter"] = it - 1
+        lim = float(self.N) * tol * FIX if tol > 0 else 0.0
+        if it > 1 and lim > 0 and float(err) < lim:
+            c["converged"] = it - 1
+            return
+        c["tele"] = (1.0 - alpha) * FIX + alpha * float(dang)
+        self.step(alpha, flags, sset=it % NSET)
+
+    def finish(self, alpha, tol, it):
+        c = self.ctl
+        if c["converged"]:
+            return
+        err, dang, _ = self._set_sums(it % NSET)
+        c["iter"] = it
+        lim = float(self.N) * tol * FIX if tol > 0 else 0.0
+        if lim > 0 and float(err) < lim:
+            c["converged"] = it
+            return
+        c["tele"] = (1.0 - alpha) * FIX + alpha * float(dang)
+
+    def step(self, alpha, flags=3, sset=0):
         """Pull SpMV fused with the update: reads w_all, writes r and send (krca_ppr_shard_step)."""
         if self.ctl["converged"]:
             return
@@ -88,8 +126,9 @@ class NumpyShard:
         self.r = rn
         snd = self.send.numpy()
         snd.view(np.uint32)[:self.n] = _w(rn, self.deg, alpha)
-        snd[self.ws] += err
-        snd[self.ws + NSPREAD] += int(rn[self.deg == 0].sum())
+        o = self.ws + sset * SET_WORDS
+        snd[o] += err
+        snd[o + NSPREAD] += int(rn[self.deg == 0].sum())
 
     def reduce(self, alpha, tol, first):
         w = self.w_all.numpy().reshape(self.world, slice_words(self.n_max))[:, self.ws:]
@@ -150,6 +189,8 @@ class NumpyShard:
         self.q = np.where(v > 0, (np.maximum(v, 0) * 4294967296.0).astype(np.int64), 0)
         snd = self.send.numpy()
         snd[self.ws:] = 0
+        if self.world == 1:
+            self.w_all.numpy()[self.ws:] = 0
         snd.view(np.uint32)[:self.n] = _w(self.r, self.deg, alpha)
         snd[self.ws + NSPREAD] = int(self.r[self.deg == 0].sum())
         snd[self.ws + 2 * NSPREAD] = int(self.q.sum())

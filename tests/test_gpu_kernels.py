@@ -360,9 +360,11 @@ def test_rca_step_graph_replay_equals_eager(eng):
 
 
 @pytest.mark.parametrize("G", [2, 3])
-def test_rca_sharded_path_emulated_on_one_gpu(eng, G):
+@pytest.mark.parametrize("folded", [False, True])
+def test_rca_sharded_path_emulated_on_one_gpu(eng, G, folded):
     """G pod shards on one device with the all-gather done by copies: the remapped-column /
-    slot-payload path of the multi-GPU step, bit-identical to the single-process oracle."""
+    slot-payload path of the multi-GPU step, unfolded and folded, bit-identical to the
+    single-process oracle."""
     from krca.rca import Config, DeviceShard, shard_graph, shard_range
     n = 30000
     m = synth.make_graph(n, avg_degree=20, seed=11)
@@ -384,14 +386,23 @@ def test_rca_sharded_path_emulated_on_one_gpu(eng, G):
         s.score()
         s.init(cfg.alpha, cfg.floor(n, 8))
     exchange()
-    for s in shards:
-        s.reduce(cfg.alpha, cfg.tol, 1)
-    for _ in range(cfg.iters):
+    if folded:  # krca_ppr_shard_step_folded: each step reduces the previous one's slot set
+        for it in range(1, cfg.iters + 1):
+            for s in shards:
+                s.step_folded(cfg.alpha, cfg.tol, it, 3)
+            exchange()
         for s in shards:
-            s.step(cfg.alpha)
-        exchange()
+            s.finish(cfg.alpha, cfg.tol, cfg.iters)
+            assert s.ctl_read() == (cfg.iters, False)
+    else:
         for s in shards:
-            s.reduce(cfg.alpha, cfg.tol, 0)
+            s.reduce(cfg.alpha, cfg.tol, 1)
+        for _ in range(cfg.iters):
+            for s in shards:
+                s.step(cfg.alpha)
+            exchange()
+            for s in shards:
+                s.reduce(cfg.alpha, cfg.tol, 0)
     score = torch.cat([s.score_out["score"] for s in shards]).cpu().numpy()
     _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
     got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
