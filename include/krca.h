@@ -205,7 +205,8 @@ int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32
  * summation order or GPU count and are bit-identical to oracle/krca_oracle.c.  The per-node edge
  * weight floor(r_j * alpha / outdeg_j) travels as a 32-bit code (26 significant bits + shift,
  * truncating; csrc/ppr.hip wenc/wdec, restated in the oracle), so the gathered table is 4 B/node.
- * krca_ppr runs the whole iteration on one device (synchronous: returns *iters_host); the
+ * krca_ppr runs the whole iteration on one device (synchronous: returns *iters_host; since round
+ * 3 with the folded steps below, one kernel per iteration); the
  * krca_ppr_shard_* steps are the same kernels for G pod-sharded ranks.  Per iteration:
  * krca_ppr_shard_step (pull SpMV fused with the rank update: gathers w_all, writes r_local and
  * this rank's send slice of krca_ppr_slice_words(n_max) int64 words: [n_max uint32 weight codes,

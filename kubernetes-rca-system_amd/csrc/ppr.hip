@@ -877,21 +877,26 @@ int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, 
   KRCA_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
   int rc = krca_ppr_shard_init(seed, seed_floor, outdeg, N, N, N, alpha, ctl, q, r, wb[0], stream);
   if (rc) return rc;
-  if ((rc = krca_ppr_shard_reduce(wb[0], 1, N, N, alpha, tol, 1, ctl, wb[1], stream))) return rc;
+  // folded iterations (one kernel each: step it reduces step it - 1 first); the first writes its
+  // partial sums into the other buffer's slots, zeroed here
+  KRCA_HIP(hipMemsetAsync(wb[1] + wslots(N), 0, NSLOT * sizeof(int64_t), st));
   const int check_every = 8;
   int32_t iters = 0, conv = 0;
   int cur = 0;  // w buffer the next step gathers from
-  for (int it = 0; it < max_iter; ++it) {
-    const int32_t flags = tol > 0.0 ? (KRCA_PPR_RESIDUAL | KRCA_PPR_WRITE_R) : (it + 1 == max_iter ? KRCA_PPR_WRITE_R : 0);
-    if ((rc = krca_ppr_solo_step(row_ptr, col, plan, plan_len, lane, wb[cur], outdeg, q, N, alpha, flags, tol, r,
-                                 wb[cur ^ 1], ctl, stream)))  // the iteration's reduction in its last workgroup
+  int it = 0;
+  while (it < max_iter) {
+    ++it;
+    const int32_t flags = tol > 0.0 ? (KRCA_PPR_RESIDUAL | KRCA_PPR_WRITE_R) : (it == max_iter ? KRCA_PPR_WRITE_R : 0);
+    if ((rc = krca_ppr_shard_step_folded(row_ptr, col, plan, plan_len, lane, wb[cur], 1, outdeg, q, N, N, N, alpha, tol,
+                                         it, flags, r, wb[cur ^ 1], wb[cur], ctl, stream)))
       return rc;
     cur ^= 1;
-    if (tol > 0.0 && (it + 1) % check_every == 0 && it + 1 < max_iter) {
+    if (tol > 0.0 && it % check_every == 0 && it < max_iter) {  // step it's own test is in step it + 1
       if ((rc = krca_ppr_ctl_read(ctl, &iters, &conv, stream))) return rc;
       if (conv) break;
     }
   }
+  if ((rc = krca_ppr_shard_finish(wb[cur], 1, N, N, alpha, tol, it, ctl, stream))) return rc;
   if ((rc = krca_ppr_fixed_to_float(r, N, r_out, stream))) return rc;
   if ((rc = krca_ppr_ctl_read(ctl, &iters, &conv, stream))) return rc;
   if (iters_host) *iters_host = iters;
