@@ -502,8 +502,13 @@ class NativeEngine:
         return int(v.value)
 
     # -- a13 ---------------------------------------------------------------------------------
-    def template_hist_device(self, scan):
-        """Template hashes of every line and per-container template histograms (device)."""
+    def template_hist_device(self, scan, defer_huge=False):
+        """Template hashes of every line and per-container template histograms (device).
+        defer_huge: return without reading back the number of containers above
+        krca_template_max_lines() (a synchronisation); the caller completes the result with
+        template_hist_finish() before it reads any histogram (krca.stream does so after the window's
+        re-ranking is enqueued, so the GPU does not idle on the read).  Until then no other
+        template_hist_device call may run on this engine (the pending count sits in its workspace)."""
         torch = self.torch
         L = scan["n_lines_total"]
         D = scan["doc_lines"].numel()
@@ -518,6 +523,24 @@ class NativeEngine:
         _check(self.lib.krca_template_hist(self.ptr(h), self.ptr(scan["doc_lines"]), self.ptr(scan["doc_line0"]), D,
                                            self.ptr(ws), self.ptr(oh), self.ptr(oc), self.ptr(nt), self._stream()),
                "krca_template_hist")
+        out = dict(hash=h[:L], tmpl_hash=oh[:L], tmpl_count=oc[:L], n_templates=nt)
+        if defer_huge:
+            out["_pending"] = (ws, h, oh, oc, nt, scan)
+            return out
+        self._template_huge(ws, h, oh, oc, nt, scan)
+        return out
+
+    def template_hist_finish(self, out):
+        """Complete a template_hist_device(..., defer_huge=True) result in place (the containers
+        above krca_template_max_lines(), if any).  Returns out."""
+        pend = out.pop("_pending", None)
+        if pend is not None:
+            self._template_huge(*pend)
+        return out
+
+    def _template_huge(self, ws, h, oh, oc, nt, scan):
+        torch = self.torch
+        D = scan["doc_lines"].numel()
         n_huge = int(ws[2].item())  # containers above krca_template_max_lines() (a 4-byte read)
         if n_huge:  # a distinct-hash table + bucketed sorts per container
             huge = np.sort(ws[4 + 2 * D:4 + 2 * D + n_huge].cpu().numpy())
@@ -533,7 +556,6 @@ class NativeEngine:
                                                         self._stream()), "krca_template_hist_huge")
             if int(flag.max().item()):
                 raise KrcaError("template histogram: a hash bucket overflowed (not expected for 64-bit hashes)")
-        return dict(hash=h[:L], tmpl_hash=oh[:L], tmpl_count=oc[:L], n_templates=nt)
 
     def template_hist(self, blob, doc_off):
         """-> list (per container) of [(hash uint64, count)] in ascending hash order."""

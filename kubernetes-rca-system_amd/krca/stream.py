@@ -69,28 +69,47 @@ class StreamingRCA:
         return o
 
     # -- 2. logs ---------------------------------------------------------------------------------
-    def push_logs(self, text, doc_off, templates=True, validate=True):
+    def push_logs(self, text, doc_off, templates=True, validate=True, _defer=False):
         """Window log text of this rank's containers (uint8 device tensor, 16-byte aligned) and its
         container offsets (int64 device tensor): 13-bin histograms (+ template histograms)."""
         scan = self.eng.log_scan_device(text, doc_off, validate=validate)
         if templates:
-            scan["templates"] = self.eng.template_hist_device(scan)
+            scan["templates"] = self.eng.template_hist_device(scan, defer_huge=_defer)
         return scan
 
     # -- 3. re-ranking ---------------------------------------------------------------------------
     def rerank(self):
         s, cfg = self.shard, self.cfg
-        if self.solved:
+        warm = self.solved
+        if warm:
             s.init_warm(cfg.alpha, cfg.floor(s.N, s.M))
         else:
             s.init(cfg.alpha, cfg.floor(s.N, s.M))
         self.comm.exchange(s)
+        it = 0
+        if warm and self.last_iters > 0:
+            # speculative first batch: the previous window's iteration count + 1 (the step that
+            # tests it), then the last step's reduction, key, top-k and merge at once.  Windows
+            # change little, so this usually converges: no step is launched past convergence and the
+            # GPU never waits for the host's poll.  Otherwise the candidates are dropped (the finish
+            # and the key only read the state) and the batches below continue from step `it`.
+            for _ in range(min(self.last_iters + 1, self.max_iter)):
+                it += 1
+                s.step_folded(cfg.alpha, self.tol, it, 3)
+                self.comm.exchange(s)
+            s.finish(cfg.alpha, self.tol, it)
+            h = s.ctl_async()
+            top = self.rca.merge(*s.local_topk(cfg.k))
+            iters, conv = s.ctl_wait(h)
+            if conv or it >= self.max_iter:
+                self.last_iters = iters if conv else -iters
+                return top
         # folded iterations (each step reduces the previous one: one kernel + one exchange) in
         # batches of check_every; the convergence flag of batch b is read while batch b + 1 runs (a
         # pinned copy + event): the GPU never idles on the poll, and iterations enqueued past
         # convergence do nothing (the kernels exit on the device-held flag), so the ranks and the
         # iteration count are the same as with a synchronous check after every batch
-        it, pending = 0, None
+        pending = None
         while it < self.max_iter:
             for _ in range(min(self.check_every, self.max_iter - it)):
                 it += 1
@@ -113,9 +132,13 @@ class StreamingRCA:
         """One streaming window: rescoring, log histograms (+ templates), re-ranking."""
         out = {"scores": self.push_metrics(x_new)}
         if log_text is not None:
-            out["logs"] = self.push_logs(log_text, doc_off)
+            # the template pass's read-back of its oversized-container count waits until the
+            # re-ranking is enqueued (it would otherwise stall the GPU between the two)
+            out["logs"] = self.push_logs(log_text, doc_off, _defer=True)
         out["top"] = self.rerank()
         out["iters"] = self.last_iters
+        if log_text is not None:
+            self.eng.template_hist_finish(out["logs"]["templates"])
         return out
 
     # -- 4. snapshots ----------------------------------------------------------------------------

@@ -35,7 +35,7 @@ def _mesh():
     return m, x
 
 
-def _worker(rank, world, port, out_q, snap_dir=None, snap_at=2):
+def _worker(rank, world, port, out_q, snap_dir=None, snap_at=2, short_at=None):
     sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"),
                     os.path.join(ROOT, "tests")]
     import torch.distributed as dist
@@ -63,6 +63,10 @@ def _worker(rank, world, port, out_q, snap_dir=None, snap_at=2):
             s.snapshot(path)
             shard, s = fresh()
             s.restore(path)
+        if short_at is not None and wi == short_at:
+            # the re-rank's speculative first batch is the previous count + 1 steps: make it fall
+            # short, so the window continues in the polled batches after a dropped merge
+            s.last_iters = 2
         out = s.window(x[t:t + d, lo:hi, :])
         t += d
         rows.append((shard.r.copy(), out["iters"], [int(i) for i in out["top"][0]],
@@ -73,14 +77,16 @@ def _worker(rank, world, port, out_q, snap_dir=None, snap_at=2):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,snap", [(1, False), (2, False), (3, False), (2, True)])
-def test_sharded_stream_matches_oracle_chain(world, snap, tmp_path):
-    """snap: every rank snapshots its stream after window 2 and continues in a restored object."""
+@pytest.mark.parametrize("world,snap,short", [(1, False, False), (2, False, False), (3, False, False), (2, True, False),
+                                              (2, False, True)])
+def test_sharded_stream_matches_oracle_chain(world, snap, short, tmp_path):
+    """snap: every rank snapshots its stream after window 2 and continues in a restored object.
+    short: window 3's speculative first batch is too short (the fallback path)."""
     import oracle
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, str(tmp_path) if snap else None))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, str(tmp_path) if snap else None, 2, 3 if short else None))
              for r in range(world)]
     for p in procs:
         p.start()
