@@ -79,6 +79,13 @@ class StreamingRCA:
 
     # -- 3. re-ranking ---------------------------------------------------------------------------
     def rerank(self):
+        return self._rerank_end(self._rerank_begin())
+
+    def _rerank_begin(self):
+        """Enqueue the re-rank's first part without synchronising: init (warm from the previous
+        window's ranks), and for a warm stream the speculative first batch -- the previous window's
+        iteration count + 1 folded steps (the last one tests the count), the last step's reduction,
+        the key and the local top-k."""
         s, cfg = self.shard, self.cfg
         warm = self.solved
         if warm:
@@ -86,20 +93,28 @@ class StreamingRCA:
         else:
             s.init(cfg.alpha, cfg.floor(s.N, s.M))
         self.comm.exchange(s)
-        it = 0
+        st = dict(it=0, spec=None)
         if warm and self.last_iters > 0:
-            # speculative first batch: the previous window's iteration count + 1 (the step that
-            # tests it), then the last step's reduction, key, top-k and merge at once.  Windows
-            # change little, so this usually converges: no step is launched past convergence and the
-            # GPU never waits for the host's poll.  Otherwise the candidates are dropped (the finish
-            # and the key only read the state) and the batches below continue from step `it`.
+            # windows change little, so this usually converges: no step is launched past
+            # convergence and the GPU never waits on a host poll.  Otherwise the candidates are
+            # dropped (the finish and the key only read the state) and _rerank_end continues in
+            # polled batches from step `it`.
+            it = 0
             for _ in range(min(self.last_iters + 1, self.max_iter)):
                 it += 1
                 s.step_folded(cfg.alpha, self.tol, it, 3)
                 self.comm.exchange(s)
             s.finish(cfg.alpha, self.tol, it)
             h = s.ctl_async()
-            top = self.rca.merge(*s.local_topk(cfg.k))
+            st.update(it=it, spec=(h, s.local_topk(cfg.k)))
+        return st
+
+    def _rerank_end(self, st):
+        s, cfg = self.shard, self.cfg
+        it = st["it"]
+        if st["spec"] is not None:
+            h, cand = st["spec"]
+            top = self.rca.merge(*cand)
             iters, conv = s.ctl_wait(h)
             if conv or it >= self.max_iter:
                 self.last_iters = iters if conv else -iters
@@ -128,17 +143,42 @@ class StreamingRCA:
         self.solved = True
         return top
 
-    def window(self, x_new, log_text=None, doc_off=None):
-        """One streaming window: rescoring, log histograms (+ templates), re-ranking."""
+    def window(self, x_new, log_text=None, doc_off=None, validate=True, templates=True):
+        """One streaming window: rescoring, log histograms (+ templates), re-ranking.
+
+        With log text, the log pass runs on a second HIP stream beside the re-ranking: the
+        re-rank's first part is enqueued first (it needs the new scores only), then the log scan
+        and the template pass go out on the side stream while those PageRank steps run (the scan's
+        one synchronisation waits for the side stream only), and the templates' read-back of the
+        oversized-container count comes after the re-rank's merge.  Outputs as without overlap."""
+        if log_text is None:
+            out = {"scores": self.push_metrics(x_new)}
+            out["top"] = self.rerank()
+            out["iters"] = self.last_iters
+            return out
+        torch = self.eng.torch
+        main = torch.cuda.current_stream(self.eng.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.eng.device)
+        side = self._side
+        ready = main.record_event()  # the window's log text and offsets are on main
         out = {"scores": self.push_metrics(x_new)}
-        if log_text is not None:
-            # the template pass's read-back of its oversized-container count waits until the
-            # re-ranking is enqueued (it would otherwise stall the GPU between the two)
-            out["logs"] = self.push_logs(log_text, doc_off, _defer=True)
-        out["top"] = self.rerank()
+        st = self._rerank_begin()
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            logs = self.push_logs(log_text, doc_off, templates=templates, validate=validate, _defer=True)
+        out["top"] = self._rerank_end(st)
         out["iters"] = self.last_iters
-        if log_text is not None:
-            self.eng.template_hist_finish(out["logs"]["templates"])
+        main.wait_stream(side)
+        tm = logs.get("templates", {})
+        for v in list(logs.values()) + list(tm.values()):
+            if isinstance(v, torch.Tensor):
+                v.record_stream(main)  # allocated on side, read on main from here on
+        if templates:
+            self.eng.template_hist_finish(tm)  # synchronises main (after side)
+        else:
+            main.synchronize()
+        out["logs"] = logs
         return out
 
     # -- 4. snapshots ----------------------------------------------------------------------------

@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--delta", type=int, default=1)
     ap.add_argument("--lines-per-window", type=int, default=2_500_000)
     ap.add_argument("--no-templates", action="store_true")
+    ap.add_argument("--phases", action="store_true",
+                    help="run the window's three parts one after another with events between them (per-part "
+                         "times) instead of StreamingRCA.window (log pass beside the re-ranking)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -107,21 +110,26 @@ def main():
         torch.cuda.synchronize()
         w0 = time.perf_counter()
         es[2].record()
-        s.push_metrics(x[t:t + a.delta])
-        es[3].record()
-        s.push_logs(text[:len(blob)], offd, templates=not a.no_templates, validate=False)
-        es4 = ev()
-        es4.record()
-        top, _ = s.rerank()
+        if a.phases:
+            s.push_metrics(x[t:t + a.delta])
+            es[3].record()
+            s.push_logs(text[:len(blob)], offd, templates=not a.no_templates, validate=False)
+            es4 = ev()
+            es4.record()
+            s.rerank()
+        else:
+            s.window(x[t:t + a.delta], text[:len(blob)], offd, validate=False, templates=not a.no_templates)
         es[4].record()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - w0) * 1e3
         t += a.delta
-        rows.append(dict(h2d_ms=max_over_ranks(es[0].elapsed_time(es[1])),
-                         score_ms=max_over_ranks(es[2].elapsed_time(es[3])),
-                         logs_ms=max_over_ranks(es[3].elapsed_time(es4)),
-                         rerank_ms=max_over_ranks(es4.elapsed_time(es[4])), iters=s.last_iters,
-                         window_ms=max_over_ranks(wall)))
+        row = dict(h2d_ms=max_over_ranks(es[0].elapsed_time(es[1])), iters=s.last_iters,
+                   device_ms=max_over_ranks(es[2].elapsed_time(es[4])), window_ms=max_over_ranks(wall))
+        if a.phases:
+            row.update(score_ms=max_over_ranks(es[2].elapsed_time(es[3])),
+                       logs_ms=max_over_ranks(es[3].elapsed_time(es4)),
+                       rerank_ms=max_over_ranks(es4.elapsed_time(es[4])))
+        rows.append(row)
     med = {k: float(np.median([r[k] for r in rows])) for k in rows[0]}
     p95 = {k: float(np.percentile([r[k] for r in rows], 95)) for k in rows[0]}
     wb = window_bytes(hi - lo, M, a.delta)
@@ -136,8 +144,10 @@ def main():
                        "windows": a.windows, "templates": not a.no_templates, "ranks": world},
             "median": med, "p95": p95, "windows": rows, "prefill_ms": prefill_ms,
             "prefill_gbs_rank0": (4 * (hi - lo) * M * T) / (prefill_ms * 1e-3) / 1e9,
-            "stream_score_bytes_rank0": wb, "stream_score_gbs_rank0": wb / (med["score_ms"] * 1e-3) / 1e9,
-            "logs_gbs_rank0": len(blob) / (med["logs_ms"] * 1e-3) / 1e9,
+            "mode": "phases (sequential, per-part events)" if a.phases else "StreamingRCA.window (log pass on a side stream)",
+            "stream_score_bytes_rank0": wb,
+            "stream_score_gbs_rank0": wb / (med["score_ms"] * 1e-3) / 1e9 if a.phases else None,
+            "logs_gbs_rank0": len(blob) / (med["logs_ms"] * 1e-3) / 1e9 if a.phases else None,
             "h2d_gbs_rank0": len(blob) / (med["h2d_ms"] * 1e-3) / 1e9,
             "window_incl_h2d_ms": med["window_ms"] + med["h2d_ms"],
             "data": "synthetic (krca/synth.py; one log window re-sent every window)",

@@ -7,6 +7,7 @@
 #   ranking      tools/ranking_ablation_c4.py (C4 mesh, 2 seeds)
 #   ppr          rocprofv3 stats of the C4 PageRank propagate   logs / tmpl  same for logs / templates
 #   c5           tools/bench_stream.py (C5 window)
+#   c5_phases    the same, the three parts one after another with per-part events
 set -u
 TAG=$1; shift
 O=gpurun_out/$TAG
@@ -65,6 +66,7 @@ for s in "$@"; do
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
     tmpl_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#tmpl_}.so; prof $s 300 tools/prof_kernels.py tmpl --reps 5; unset KRCA_LIB ;;
     c5) step c5 400 python3 -u tools/bench_stream.py ;;
+    c5_phases) step c5_phases 400 python3 -u tools/bench_stream.py --phases ;;
     c5_trace) step c5_trace 400 rocprofv3 --kernel-trace --output-format csv -d $O/c5_trace -o run -- python3 -u tools/bench_stream.py --windows 4
       python3 tools/trace_gaps.py $O/c5_trace/run_kernel_trace.csv > $O/c5_gaps.txt; rm -f $O/c5_trace/run_kernel_trace.csv ;;
     pmc_ppr)
