@@ -164,12 +164,16 @@ class StreamingRCA:
         ready = main.record_event()  # the window's log text and offsets are on main
         out = {"scores": self.push_metrics(x_new)}
         st = self._rerank_begin()
-        with torch.cuda.stream(side):
-            side.wait_event(ready)
-            logs = self.push_logs(log_text, doc_off, templates=templates, validate=validate, _defer=True)
-        out["top"] = self._rerank_end(st)
-        out["iters"] = self.last_iters
-        main.wait_stream(side)
+        try:
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                logs = self.push_logs(log_text, doc_off, templates=templates, validate=validate, _defer=True)
+        finally:
+            # a log pass that raises (e.g. bad offsets) still leaves the re-rank completed, so the
+            # next window warm-starts from this window's solve as the oracle chain does
+            out["top"] = self._rerank_end(st)
+            out["iters"] = self.last_iters
+            main.wait_stream(side)
         tm = logs.get("templates", {})
         for v in list(logs.values()) + list(tm.values()):
             if isinstance(v, torch.Tensor):

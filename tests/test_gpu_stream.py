@@ -117,3 +117,52 @@ def test_stream_snapshot_restore_continues_bit_for_bit(eng, tmp_path):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), i
         assert np.array_equal(a[2], b[2]), i
         assert a[3] == b[3] and a[4] == b[4], i
+
+
+def test_stream_window_log_overlap_and_error_path(eng):
+    """window(x, text, doc_off) runs the log pass on a side stream beside the re-rank: its 13-bin
+    and template histograms equal the log pass run alone (one container above
+    krca_template_max_lines() takes the deferred path), its ranks / counts / top-k equal a
+    metrics-only stream's; a window whose offsets are refused raises and still completes the
+    re-rank, so the next windows stay identical to the metrics-only stream."""
+    from krca.agents.logs import pack_documents
+    P, M, T, W = 2000, 8, 200, 60
+    m = synth.make_graph(P, avg_degree=8, seed=31)
+    x = synth.make_metrics(P, M, T, window=W, seed=32, roots=m.roots,
+                           hop_sets=synth.caller_hops(m, m.roots)).numpy()
+    docs = synth.make_log_corpus(P, lines_per_doc=2, seed=33, hazard_rate=0.02)
+    docs[5] = "\n".join(["E0101 OOMKilled container worker-7 restarting"] * 5000)
+    blob, off = pack_documents(docs)
+    native.check_doc_off(off, len(blob))
+    text, offd = eng.upload_blob(blob), torch.from_numpy(off).cuda()
+    bad = offd.clone()
+    bad[1] = bad[2] + 1  # not non-decreasing: refused
+    assert int(eng.lib.krca_template_max_lines()) < 5000
+    ref = eng.log_scan_device(text, offd)
+    ref_t = eng.template_hist_device(ref)
+    want = [ref[k].cpu().numpy() for k in ("hist", "doc_line0", "doc_lines", "line_mask")]
+    want_t = [ref_t[k].cpu().numpy() for k in ("n_templates", "tmpl_hash", "tmpl_count")]
+    cfg = Config(window=W)
+    a = StreamingRCA(eng, m.row_ptr, m.col, m.outdeg, M, cfg, tol=1e-9, max_iter=60)
+    b = StreamingRCA(eng, m.row_ptr, m.col, m.outdeg, M, cfg, tol=1e-9, max_iter=60)
+    xd = torch.from_numpy(x).cuda()
+    t = 0
+    for i, d in enumerate([W + 40, 1, 5, 1, 20]):
+        xw = xd[t:t + d].contiguous()
+        t += d
+        ob = b.window(xw)
+        if i == 2:
+            with pytest.raises(native.KrcaError):
+                a.window(xw, text, bad)
+            assert np.array_equal(a.shard.r[:P].cpu().numpy(), b.shard.r[:P].cpu().numpy())
+            assert a.last_iters == b.last_iters
+            continue
+        oa = a.window(xw, text, offd)
+        assert np.array_equal(a.shard.r[:P].cpu().numpy(), b.shard.r[:P].cpu().numpy()), i
+        assert oa["iters"] == ob["iters"] and [int(v) for v in oa["top"][0]] == [int(v) for v in ob["top"][0]], i
+        lg, tm = oa["logs"], oa["logs"]["templates"]
+        assert "_pending" not in tm
+        for w_, k in zip(want, ("hist", "doc_line0", "doc_lines", "line_mask")):
+            assert np.array_equal(lg[k].cpu().numpy(), w_), (i, k)
+        for w_, k in zip(want_t, ("n_templates", "tmpl_hash", "tmpl_count")):
+            assert np.array_equal(tm[k].cpu().numpy(), w_), (i, k)
