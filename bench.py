@@ -55,14 +55,22 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--no-corr", action="store_true", help="skip the correlation leg (C4's second half)")
+    ap.add_argument("--corr-pods", type=int, default=None, help="pods of the correlation leg (default: --pods)")
+    ap.add_argument("--corr-tau", type=float, default=0.5)
+    ap.add_argument("--corr-k", type=int, default=10)
+    ap.add_argument("--corr-runs", type=int, default=3, help="timed correlation calls (after one warm-up call)")
+    ap.add_argument("--corr-check-rows", type=int, default=512)
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run steps back to back on one stream (default: two streams, step i+1's scoring "
                          "overlaps step i's PageRank)")
     ap.add_argument("--profile", action="store_true",
                     help="after the timed steps, one unpipelined step per rank with a HIP event around every "
-                         "launch (scoring, PageRank init / step / exchange / reduce, key + top-k) and roctx "
+                         "launch (scoring, PageRank init / folded step / exchange / finish, key + top-k) and roctx "
                          "ranges for rocprofv3 --marker-trace; per-kernel times go to the JSON line's 'profile'")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    a.corr_pods = 0 if a.no_corr else (a.pods if a.corr_pods is None else a.corr_pods)
+    return a
 
 
 def launch_ranks(n, argv):
@@ -126,13 +134,14 @@ def profile_step(step, stream, world):
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
         timed("krca_rolling_score", s.score)
-        timed("krca_ppr_shard_init", lambda: s.init(cfg.alpha, cfg.seed_floor))
+        # the sequence RcaStep._propagate runs: init, exchange, iters x (folded step, exchange), finish
+        timed("krca_ppr_shard_init", lambda: s.init(cfg.alpha, cfg.floor(s.N, s.M)))
         timed("exchange", lambda: c.exchange(s))
-        timed("krca_ppr_shard_reduce", lambda: s.reduce(cfg.alpha, cfg.tol, 1))
-        for it in range(cfg.iters):
-            timed("krca_ppr_shard_step", lambda: s.step(cfg.alpha, step_flags(cfg.tol, it + 1 == cfg.iters)))
+        for it in range(1, cfg.iters + 1):
+            timed("krca_ppr_shard_step_folded",
+                  lambda: s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == cfg.iters)))
             timed("exchange", lambda: c.exchange(s))
-            timed("krca_ppr_shard_reduce", lambda: s.reduce(cfg.alpha, cfg.tol, 0))
+        timed("krca_ppr_shard_finish", lambda: s.finish(cfg.alpha, cfg.tol, cfg.iters))
         timed("key+topk", lambda: s.local_topk(cfg.k))
         t1.record()
     torch.cuda.synchronize()
@@ -144,6 +153,247 @@ def profile_step(step, stream, world):
     summ["note"] = ("HIP events on the launch stream around each call (host launch gaps included in step_ms, "
                     "not in the per-call times); 'exchange' is the all-gather at G > 1, a buffer swap at G = 1")
     return summ
+
+
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA
+
+
+def score_bytes(pods, metrics, tsteps):
+    """Algorithmic HBM bytes of one krca_rolling_score launch: the series once,
+    z_last, and score / n_exceed / flags per pod."""
+    return 4 * pods * metrics * tsteps + 4 * pods * metrics + 9 * pods
+
+
+def max_over_ranks(v, world):
+    if world == 1:
+        return float(v)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(vals, world):
+    if world == 1:
+        return [float(v) for v in vals]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t)
+    return [float(v) for v in t.tolist()]
+
+
+def gather_rows(t, n_max, world):
+    """This rank's rows (<= n_max of them) -> every rank's rows, each rank's slice padded to n_max;
+    rank g's rows start at g * n_max, which is its first pod (krca.rca.shard_range)."""
+    import torch
+    from krca.rca import all_gather_flat
+    pad = torch.zeros(n_max, dtype=t.dtype, device=t.device)
+    pad[:t.numel()] = t
+    if world == 1:
+        return pad
+    out = torch.empty(world * n_max, dtype=t.dtype, device=t.device)
+    all_gather_flat(out, pad, world)
+    return out
+
+
+def pmc_traffic(args, bytes_alg, world):
+    """HBM bytes per scoring launch from the counters of profiles/pmc_latest.json: as measured when
+    the run's per-rank shape is the measured one (N = 1 at 1M pods), else the measured
+    bytes / algorithmic ratio applied to this rank's algorithmic bytes (the kernel streams each
+    series once, so the ratio does not depend on the pod count)."""
+    if not os.path.exists(args.pmc):
+        return None, None
+    try:
+        pm = json.load(open(args.pmc))
+        meas = pm.get("krca_rolling_score_bytes_per_launch")
+        if meas is None:
+            return None, None
+        alg = score_bytes(pm.get("pods"), pm.get("metrics", 8), pm.get("tsteps", 1440))
+        if pm.get("pods") == args.pods and world == 1 and (args.metrics, args.tsteps) == (8, 1440):
+            return meas, "measured: rocprofv3 PMC pass at this shape (" + os.path.relpath(args.pmc, ROOT) + ")"
+        return meas / alg * bytes_alg, "scaled: measured/algorithmic ratio of the 1M-pod PMC pass x this rank's bytes"
+    except Exception:  # noqa: BLE001
+        return None, None
+
+
+def verify_step(args, cfg, mesh, shard, x, lo, hi, n_max, world, rank):
+    """Untimed parity of the last step at any N: every rank's fixed-point ranks and scores are
+    gathered to rank 0 and compared with the C oracle run on the whole mesh (ranks bit for bit,
+    top-10 identical); each rank checks n_exceed / flags / scores of its own sampled pods against
+    the oracle's scoring (bit-exact / 1e-5), summed over ranks."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n_loc = hi - lo
+    r_all = gather_rows(shard.r[:n_loc], n_max, world)[:args.pods].cpu().numpy()
+    sc_all = gather_rows(shard.score_out["score"][:n_loc], n_max, world)[:args.pods].cpu().numpy()
+    ns = min(max(1, 2000 // world), n_loc)
+    samp = np.sort(np.random.default_rng(1 + rank).choice(n_loc, size=ns, replace=False))
+    st = torch.from_numpy(samp).to(x.device)
+    ref = oracle.c_rolling_score(x[:, st, :].cpu().numpy(), args.window)
+    dev = {k: shard.score_out[k][st].cpu().numpy() for k in ("n_exceed", "flags", "score")}
+    bad = int(np.sum(dev["n_exceed"] != ref["n_exceed"]) + np.sum(dev["flags"] != ref["flags"]))
+    rel = float(np.max(np.abs(dev["score"] - ref["score"]) / np.maximum(ref["score"], 1e-6)))
+    bad_all, ns_all = sum_over_ranks([bad, ns], world)
+    rel = max_over_ranks(rel, world)
+    if rank != 0:
+        return {}
+    ridx, _, r = oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, sc_all, cfg.alpha, cfg.iters, cfg.seed_floor,
+                                 cfg.k)
+    return {"ppr_fixed_point_bit_identical": bool(np.array_equal(r_all, r)),
+            "oracle_top10": [int(i) for i in ridx],
+            "ranks_gathered": world, "score_sample_pods": int(ns_all),
+            "n_exceed_flags_bit_exact": bad_all == 0, "score_max_rel_err": rel}
+
+
+def cpu_baseline(args, cfg, mesh, shard, x, n_loc):
+    """The C restatement (oracle/krca_oracle.c, OpenMP) on the host cores: scoring of a bounded
+    pod sample scaled to the whole mesh, plus PageRank + top-10 on the whole graph (rank 0)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    ps = min(args.cpu_sample_pods, n_loc)
+    xs = x[:, :ps, :].cpu().numpy()
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    score = shard.score_out["score"].cpu().numpy()
+    if len(score) < args.pods:  # N > 1: PageRank seeds of the whole mesh from the oracle's own scoring
+        score = np.concatenate([score[:n_loc], np.zeros(args.pods - n_loc, np.float32)])
+    t_sc, t_pr = [], []
+    for i in range(args.cpu_warmup + args.cpu_runs):  # BASELINE.md §3 protocol
+        t1 = time.perf_counter()
+        oracle.c_rolling_score(xs, args.window)
+        t2 = time.perf_counter()
+        oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+        t3 = time.perf_counter()
+        if i >= args.cpu_warmup:
+            t_sc.append(t2 - t1)
+            t_pr.append(t3 - t2)
+    # whole step on the CPU at the same mesh size, scoring time scaled from the sample
+    t_step = np.asarray(t_sc) * (args.pods / ps) + np.asarray(t_pr)
+    med = float(np.median(t_step))
+    out = {
+        "value": args.pods * args.tsteps / med, "unit": "pod·timesteps/s", "cores": cores, "kind": "port",
+        "sample": f"scoring: oracle/krca_oracle.c on {ps} pods x {args.metrics} x {args.tsteps} "
+                  f"(median {np.median(t_sc):.3f} s, scaled x{args.pods / ps:.0f} to {args.pods} pods); PPR+top-10: "
+                  f"full {args.pods}-node graph (median {np.median(t_pr):.3f} s); OpenMP threads = {cores}; "
+                  f"{args.cpu_warmup} warm-up + {args.cpu_runs} timed runs",
+        "ms_per_step": med * 1e3, "ms_per_step_p95": float(np.percentile(t_step, 95)) * 1e3,
+        "cpu_model": cpu_model(),
+    }
+    ref_t = os.path.join(ROOT, "tests", "golden", "ref_cpu_timings.json")
+    if os.path.exists(ref_t):  # the reference's own Python, timed in the build container
+        rt = json.load(open(ref_t))
+        out["reference_python"] = {
+            "where": "build container (reference code never runs on the GPU box): " + rt["host"]["cpu_model"],
+            "cores": 1, "timings": {k: {kk: v[kk] for kk in ("median_s", "p95_s", "units", "unit") if kk in v}
+                                    for k, v in rt["timings"].items()},
+            "note": "the reference has no rolling scoring or PageRank; these are its per-pod threshold "
+                    "loop, 13-regex line histogram, SPOF betweenness and C1 comprehensive analysis"}
+    return out
+
+
+def corr_check(z32, rows, res_idx, res_val, res_cnt, res_cert, k, tau, band=1e-12):
+    """Rows of the device result against float64 products of the device's own standardized rows
+    (krca_corr_prepare's z32, bit-identical to the C twin: tests/test_gpu_corr.py): counts exact
+    outside a 1e-12 band of tau, the top-k set exact wherever the k-th and (k+1)-th |r| are more
+    than the band apart, values the float32 rounding of the exact r, certificates positive.
+    Returns (bad counts, bad sets, bad values, bad certificates) over the rows."""
+    import torch
+    bad = [0, 0, 0, 0]
+    z64 = z32.double()
+    for i in range(0, len(rows), 128):
+        rr = rows[i:i + 128]
+        R = torch.mm(z64[rr], z64.T)
+        R[torch.arange(len(rr), device=R.device), rr] = 0.0
+        a = R.abs()
+        cnt = res_cnt[rr]
+        lo, hi = (a > tau + band).sum(1), (a > tau - band).sum(1)
+        bad[0] += int(((cnt < lo) | (cnt > hi)).sum())
+        gi = res_idx[rr].long()
+        ex = torch.gather(R, 1, gi)
+        bad[2] += int(((res_val[rr].double() - ex).abs() > 1.2e-7 * ex.abs() + 1e-12).sum())
+        a[torch.arange(len(rr), device=R.device), rr] = -1.0
+        top = torch.topk(a, k + 1, dim=1)
+        gap = top.values[:, k - 1] - top.values[:, k]
+        want = torch.sort(top.indices[:, :k], dim=1).values
+        got = torch.sort(gi, dim=1).values
+        bad[1] += int(((want != got).any(1) & (gap > band)).sum())
+        bad[3] += int((res_cert[rr] <= 0).sum())
+        del R, a
+    del z64
+    return bad
+
+
+def corr_leg(args, eng, world, rank, local):
+    """C4's correlation half (BASELINE configs[3] "... PageRank + correlation"): per-pod top-k |r|
+    partners and exact |r| > tau counts over P pods x T steps of one metric channel, MFMA
+    screening (csrc/corr.hip).  One warm-up call, then `corr_runs` timed calls, each from the
+    metric tensor to the device results (krca_corr_prepare + krca_corr_topk; at N > 1 the
+    pod-sharded krca/corr_dist.py run with its RCCL all-gathers and all-to-all), HIP events on the
+    launch stream at N = 1, wall time behind a barrier and the device synchronisation at N > 1
+    (max over ranks).  Roofline: P(P+1) T flops (the upper triangle incl. the diagonal, 2 per MAC)
+    against the dense fp16 MFMA peak.  Then `corr_check_rows` sampled rows checked exactly."""
+    import torch
+    import torch.distributed as dist
+
+    from krca import synth
+    from krca.corr_dist import CorrShard, TorchComm, corr_shard_range
+    P, T, k, tau = args.corr_pods, args.tsteps, args.corr_k, args.corr_tau
+    dev = torch.device("cuda", local)
+    t_gen = time.time()
+    lo, hi, _ = corr_shard_range(P, world, rank) if world > 1 else (0, P, P)
+    x = synth.make_metrics_range(lo, hi, 1, T, seed=2, group_size=20, device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] corr data [{lo},{hi}) x {T} generated in {time.time() - t_gen:.1f}s")
+    times, res = [], None
+    cs = CorrShard(eng, P, T, k, tau, world, rank) if world > 1 else None
+    comm = TorchComm(world, rank) if world > 1 else None
+    for i in range(1 + args.corr_runs):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        a.record()
+        if world == 1:
+            z = eng.corr_prepare_device(x, 0)
+            res = eng.corr_topk_device(z, k, tau, out=res)
+        else:
+            res = cs.run(x, comm)
+        b.record()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t1) * 1e3
+        if i >= 1:
+            times.append(a.elapsed_time(b) if world == 1 else max_over_ranks(wall, world))
+    ms = float(np.median(times))
+    flop = float(P) * (P + 1) * T
+    tflops = flop / (ms * 1e-3) / 1e12
+    # exactness of sampled rows (own rows of every rank), against the device's standardized rows
+    z32 = z["z32"] if world == 1 else cs.z32[:P]
+    n_loc = hi - lo
+    nrow = min(max(1, args.corr_check_rows // world), n_loc)
+    rows_l = np.sort(np.random.default_rng(7 + rank).choice(n_loc, size=nrow, replace=False))
+    rows = torch.from_numpy(rows_l + lo).to(dev)
+    full = dict(idx=torch.zeros((P, k), dtype=torch.int32, device=dev), val=torch.zeros((P, k), device=dev),
+                cnt=torch.zeros(P, dtype=torch.int32, device=dev), cert=torch.zeros(P, device=dev))
+    full["idx"][lo:hi], full["val"][lo:hi] = res["idx"][:n_loc], res["val"][:n_loc]
+    full["cnt"][lo:hi], full["cert"][lo:hi] = res["count"][:n_loc], res["cert"][:n_loc]
+    bad = corr_check(z32, rows, full["idx"], full["val"], full["cnt"], full["cert"], k, tau)
+    bad = sum_over_ranks(bad + [nrow], world)
+    del x, z32, full
+    torch.cuda.empty_cache()
+    return {"workload": f"C4 correlation half: {P} pods x {T} steps (one metric channel, 20-pod service groups), "
+                        f"top-{k} |Pearson r| partners + exact |r| > {tau} counts per pod",
+            "pods": P, "tsteps": T, "k": k, "tau": tau, "ms": ms, "ms_runs": times,
+            "timing": "HIP events on the launch stream" if world == 1 else "wall clock behind barrier + sync, max over ranks",
+            "parallelism": "one device" if world == 1 else f"pod-sharded super-tiles x{world} (krca/corr_dist.py)",
+            "roofline": {"kernel": "krca_corr_topk (prepare + screening + merges + exact-count re-score)",
+                         "bound": "mfma", "achieved": tflops, "peak": MFMA_PEAK_TFLOPS * world, "unit": "TFLOP/s",
+                         "frac": tflops / (MFMA_PEAK_TFLOPS * world), "algorithmic_flop": flop, "traffic": None},
+            "verify": {"rows_checked": int(bad[4]), "counts_exact": bad[0] == 0, "sets_exact": bad[1] == 0,
+                       "values_exact": bad[2] == 0, "all_certified": bad[3] == 0,
+                       "reference": "float64 products of the device's z32 rows (bit-identical to the C twin)"}}
 
 
 def main():
@@ -273,17 +523,14 @@ def main():
     prof = profile_step(step, streams[0], world) if args.profile else None
 
     # ---- roofline of the dominant kernel (krca_rolling_score) ----------------------------
+    # per rank: this rank's algorithmic bytes over its own average launch; the aggregate is every
+    # rank's bytes over the slowest rank's average launch (at N = 1 the two are the same)
     n_loc = hi - lo
-    bytes_score = 4 * n_loc * args.metrics * args.tsteps + 4 * n_loc * args.metrics + 9 * n_loc
+    bytes_score = score_bytes(n_loc, args.metrics, args.tsteps)
     achieved = bytes_score / (score_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.pmc):
-        try:
-            pm = json.load(open(args.pmc))
-            if pm.get("pods") == args.pods and world == 1:
-                traffic = pm.get("krca_rolling_score_bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
+    score_ms_max = max_over_ranks(score_ms, world)
+    agg_achieved = score_bytes(args.pods, args.metrics, args.tsteps) / (score_ms_max * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args, bytes_score, world)
 
     result = None
     if rank == 0:
@@ -306,78 +553,41 @@ def main():
                                                                                       args.tsteps, args.window)],
             "roofline": {"kernel": "krca_rolling_score", "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": bytes_score,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": bytes_score, "per_rank": True,
                          "avg_launch_ms": score_ms,
                          # the timed steps are pipelined: each scoring launch shares the GPU with the
                          # previous step's PageRank; the same kernel alone (latency steps, same run):
                          "solo_avg_launch_ms": solo_ms,
-                         "solo_frac": bytes_score / (solo_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                         "solo_frac": bytes_score / (solo_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "aggregate": {"achieved": agg_achieved, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                                       "frac": agg_achieved / (HBM_PEAK_GBS * world),
+                                       "bytes_per_step": score_bytes(args.pods, args.metrics, args.tsteps),
+                                       "slowest_rank_avg_launch_ms": score_ms_max}},
             "rca_top10": [int(i) for i in top_idx],
             "world_ranks": world, "backend": backend if world > 1 else None,
             "planted_root_recall": len(set(int(i) for i in top_idx) & set(mesh.roots.tolist())) / len(mesh.roots),
         }
 
-    # ---- verification (not timed): bit-exact PageRank / top-10 vs the C oracle -----------
-    if rank == 0 and world == 1 and not args.no_verify:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        score = shard.score_out["score"].cpu().numpy()
-        ridx, rf, r = oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters,
-                                      cfg.seed_floor, cfg.k)
-        dev_r = shard.r[:n_loc].cpu().numpy()
-        samp = np.random.default_rng(1).choice(n_loc, size=min(2000, n_loc), replace=False)
-        xs = x[:, torch.from_numpy(np.sort(samp)).cuda(), :].cpu().numpy()
-        ref = oracle.c_rolling_score(xs, args.window)
-        dev = {k: shard.score_out[k][torch.from_numpy(np.sort(samp)).cuda()].cpu().numpy()
-               for k in ("n_exceed", "flags", "score")}
-        result["verify"] = {
-            "ppr_fixed_point_bit_identical": bool(np.array_equal(dev_r, r)),
-            "top10_identical": [int(i) for i in ridx] == result["rca_top10"],
-            "score_sample_pods": int(len(samp)),
-            "n_exceed_flags_bit_exact": bool(np.array_equal(dev["n_exceed"], ref["n_exceed"])
-                                             and np.array_equal(dev["flags"], ref["flags"])),
-            "score_max_rel_err": float(np.max(np.abs(dev["score"] - ref["score"]) / np.maximum(ref["score"], 1e-6))),
-        }
+    # ---- verification (not timed): bit-exact PageRank / top-10 vs the C oracle, any N -------
+    if not args.no_verify:
+        v = verify_step(args, cfg, mesh, shard, x, lo, hi, n_max, world, rank)
+        if rank == 0:
+            v["top10_identical"] = v.pop("oracle_top10") == result["rca_top10"]
+            result["verify"] = v
 
-    # ---- CPU baseline: the C restatement on the host cores, bounded sample ---------------
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        ps = min(args.cpu_sample_pods, n_loc)
-        xs = x[:, :ps, :].cpu().numpy()
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        score = shard.score_out["score"].cpu().numpy()
-        t_sc, t_pr = [], []
-        for i in range(args.cpu_warmup + args.cpu_runs):  # BASELINE.md §3 protocol
-            t1 = time.perf_counter()
-            oracle.c_rolling_score(xs, args.window)
-            t2 = time.perf_counter()
-            oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
-            t3 = time.perf_counter()
-            if i >= args.cpu_warmup:
-                t_sc.append(t2 - t1)
-                t_pr.append(t3 - t2)
-        # whole step on the CPU at the same mesh size, scoring time scaled from the sample
-        t_step = np.asarray(t_sc) * (n_loc / ps) + np.asarray(t_pr)
-        med = float(np.median(t_step))
-        result["cpu_baseline"] = {
-            "value": args.pods * args.tsteps / med, "unit": "pod·timesteps/s", "cores": cores, "kind": "port",
-            "sample": f"scoring: oracle/krca_oracle.c on {ps} pods x {args.metrics} x {args.tsteps} "
-                      f"(median {np.median(t_sc):.3f} s, scaled x{n_loc / ps:.0f}); PPR+top-10: full {args.pods}-node "
-                      f"graph (median {np.median(t_pr):.3f} s); OpenMP threads = {cores}; "
-                      f"{args.cpu_warmup} warm-up + {args.cpu_runs} timed runs",
-            "ms_per_step": med * 1e3, "ms_per_step_p95": float(np.percentile(t_step, 95)) * 1e3,
-            "cpu_model": cpu_model(),
-        }
-        ref_t = os.path.join(ROOT, "tests", "golden", "ref_cpu_timings.json")
-        if os.path.exists(ref_t):  # the reference's own Python, timed in the build container
-            rt = json.load(open(ref_t))
-            result["cpu_baseline"]["reference_python"] = {
-                "where": "build container (reference code never runs on the GPU box): " + rt["host"]["cpu_model"],
-                "cores": 1, "timings": {k: {kk: v[kk] for kk in ("median_s", "p95_s", "units", "unit") if kk in v}
-                                        for k, v in rt["timings"].items()},
-                "note": "the reference has no rolling scoring or PageRank; these are its per-pod threshold "
-                        "loop, 13-regex line histogram, SPOF betweenness and C1 comprehensive analysis"}
+    # ---- CPU baseline: the C restatement on the host cores, bounded sample (rank 0) -------
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, cfg, mesh, shard, x, n_loc)
+
+    # ---- C4's correlation half: 1M pods x 1440 steps, MFMA (after the main leg) ------------
+    if args.corr_pods > 0:
+        del x, shards, steps, shard, step
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        corr = corr_leg(args, eng, world, rank, local)
+        if rank == 0:
+            result["corr"] = corr
 
     if rank == 0 and prof is not None:
         result["profile"] = prof

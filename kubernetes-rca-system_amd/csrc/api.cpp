@@ -1,4 +1,6 @@
 // libkrca: version, error reporting and device queries (host-only translation unit).
+#include <map>
+#include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -31,13 +33,15 @@ const NamedKnob kKnobs[] = {
     {"KRCA_CORR_AMB_TILE", &Tuning::corr_amb_tile},
     {"KRCA_PPR_FUSE", &Tuning::ppr_fuse},
     {"KRCA_PPR_NT", &Tuning::ppr_nt},
+    {"KRCA_LOG_FUSED", &Tuning::log_fused},
 };
 Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20), env_int("KRCA_SCORE_NT", 1),
                  env_int("KRCA_PPR_GRID", 0),   env_int("KRCA_PPR_DICT", 1),     env_int("KRCA_LOG_IMPL", 0),
                  env_int("KRCA_GROUP_IMPL", 0),
                  env_int("KRCA_CORR_DEBUG", 0), env_int("KRCA_CORR_RS_GRID", 1024),
                  env_int("KRCA_CORR_BATCH", 0),   env_int("KRCA_CORR_AMB_TILE", -1),
-                 env_int("KRCA_PPR_FUSE", 0), env_int("KRCA_PPR_NT", 0)};
+                 env_int("KRCA_PPR_FUSE", 0), env_int("KRCA_PPR_NT", 0),
+                 env_int("KRCA_LOG_FUSED", 1)};
 const NamedKnob* find_knob(const char* name) {
   if (!name) return nullptr;
   for (const NamedKnob& k : kKnobs)
@@ -72,6 +76,26 @@ hipStream_t side_stream(hipStream_t st) {
     if (cur != dev) (void)hipSetDevice(cur);
   }
   return side[dev];
+}
+
+int64_t resident_workgroups(const void* kernel, int tpb, hipStream_t st, int fallback_per_cu) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (st && hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int64_t> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(kernel, dev);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int cus = 256, per_cu = fallback_per_cu, cur = dev;
+  (void)hipGetDevice(&cur);
+  const bool sw = cur != dev && hipSetDevice(dev) == hipSuccess;  // the occupancy API asks the current device
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, tpb, 0) != hipSuccess || per_cu < 1)
+    per_cu = fallback_per_cu;
+  if (sw) (void)hipSetDevice(cur);
+  return cache[key] = (int64_t)cus * per_cu;
 }
 }  // namespace krca
 

@@ -36,6 +36,10 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // launcher forks off its caller's stream (and joins back with events before returning); created
 // once per thread and device
 hipStream_t side_stream(hipStream_t st);
+// workgroups of `kernel` (block size tpb, no dynamic LDS) that the device of `st` keeps resident:
+// CU count x the occupancy API's blocks per CU (fallback_per_cu if the query fails).  Cached per
+// (kernel, device), so a process driving several devices sizes each device's grid from that device
+int64_t resident_workgroups(const void* kernel, int tpb, hipStream_t st, int fallback_per_cu);
 
 // makes the device of `st` current for the guard's lifetime (events and side streams are created
 // on the current device), restoring the caller's device afterwards
@@ -100,6 +104,7 @@ struct Tuning {
   int ppr_fuse;     // KRCA_PPR_FUSE: single device, the iteration's reduction in the step's last workgroup
                     // (0 = a ppr_reduce launch after each step)
   int ppr_nt;       // KRCA_PPR_NT: the step streams its plan / column / row arrays with non-temporal loads
+  int log_fused;    // KRCA_LOG_FUSED: krca_log_scan walks the DFA inside the line-index pass (0 = index, then log_dfa)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

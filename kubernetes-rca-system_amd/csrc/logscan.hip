@@ -179,12 +179,12 @@ constexpr int NBW = (int)(TILE / 32) + 2;  // bytes tile0-32 .. tile0+TILE+31
 __device__ __forceinline__ void tile_container_starts(uint32_t* s_cs, int64_t tile0, int64_t nbytes,
                                                       const int64_t* __restrict__ doc_off, int64_t D,
                                                       const int32_t* __restrict__ chunk_doc) {
-  for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;
+  for (int i = threadIdx.x; i < NBW; i += blockDim.x) s_cs[i] = 0u;
   __syncthreads();
   const int64_t tend = tile0 + TILE;
   int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
   k0 = k0 < 0 ? 0 : (k0 > D ? D : k0);  // memory safety only: the map is exact under the doc_off contract
-  for (int64_t kb = k0;; kb += TPB) {
+  for (int64_t kb = k0;; kb += blockDim.x) {
     const int64_t k = kb + threadIdx.x;
     const int64_t st = k < D ? doc_off[k] : INT64_MAX;
     if (st >= tile0 - 1 && st < tend && doc_off[k + 1] > st) {
@@ -1371,7 +1371,297 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
   for (int i = threadIdx.x; i < nv * KRCA_NCAT; i += TPB) hist[d0 * KRCA_NCAT + i] = s_ex[i];
 }
 
+// ---- log_index_match: line index AND DFA walk in ONE pass over the text (round 4) ------------
+// log_index_lines + log_dfa re-read the text: the DFA pass fetched it a second time (290 MB at the
+// DRAM-side counters for 184 MB of text, 2.3x the scan's algorithmic bytes).  Here a workgroup of
+// 1024 threads (one per CU: 150 KB of LDS) keeps its 64 KiB tile in LDS after the line-start pass
+// and walks the tile's lines there:
+//   A  each lane loads 4 pieces of 16 bytes (the tile's 64 KiB in flight at once), stores them to
+//      LDS and computes their line-start / separator-length bits (piece_flags); per 256-byte chunk
+//      counts, their scan inside the tile, the tile total published for the look-back (aggregate);
+//   B  the tile's lines in windows of LMAX: a list of (start, end) tile offsets in LDS built from
+//      the start bits, then a lane per line walks it with the DFA from LDS (the 16-byte lockstep
+//      blocks of log_dfa, LDS words instead of buffer loads); masks in LDS;
+//   C  the look-back resolves the tile's first line id (its predecessors have long published their
+//      aggregates by then), and the window's line_start / line_end / line_mask go out coalesced by
+//      line id.
+// Deferred to log_dfa_long (a wave per line, as for long lines): the tile's LAST line, whose end
+// lies in a later tile, and lines longer than LONG_LINE; at most one straddler per tile.
+constexpr int FTPB = 1024;                          // threads of log_index_match
+constexpr int FNIT = (int)(TILE / (FTPB * PIECE));  // 4 pieces of 16 bytes per lane
+constexpr int LMAX = 4096;                          // lines of a tile listed and walked per window
+
+// The lines' DFA masks from the tile text in LDS: byte offsets [s, e) of the tile (e <= TILE - 1;
+// the text array is padded past TILE so a block may read up to 16 bytes beyond e).  Same
+// transitions as log_dfa: ASCII blocks by the byte table, others code point by code point.
+__device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx, const DfaLds4& d, int s, int e) {
+  uint32_t row = 0, acc = 0;
+  int off = s & ~3;  // this block's first byte (4-byte aligned)
+  int rs_ = s & 3;   // s - off: 0..3 at the first block, then negative
+  int re_ = e - off;
+  int ncp = rs_;     // next code point start - off
+  while (re_ > 0) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + j];
+    const int lo = max(rs_, 0), hi = min(re_, 16);
+    const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = ((uint32_t)hi * 0x01010101u) | 0x80808080u;
+    uint32_t in[4], hib = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      in[j] = word_in_line(j, lo4, hi4x);
+      hib |= w[j] & in[j];
+    }
+    if (!hib && ncp <= lo) {  // all-ASCII line bytes: byte table, no decode
+      uint32_t so[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t x = w[j] | (in[j] ^ 0x80808080u);  // outside the line: >= 0x80, NOP
+#pragma unroll
+        for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t t = dfa4_step(d, row, so[k]);
+        row = t;
+        acc |= t;
+      }
+      ncp = 16;
+    } else {  // code points, as the reference decodes them
+#pragma unroll 1
+      for (int k = 0; k < 16; ++k) {
+        if (k < ncp || k < lo || k >= hi) continue;
+        auto at = [&](int r) -> uint32_t {
+          const int p = off + r;
+          return (tx[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+        };
+        uint32_t cp;
+        const uint32_t b = at(k);
+        int len;
+        if (b < 0x80) {
+          cp = b;
+          len = 1;
+        } else if (b < 0xE0) {
+          cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
+          len = 2;
+        } else if (b < 0xF0) {
+          cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
+          len = 3;
+        } else {
+          cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
+          len = 4;
+        }
+        uint32_t sy;
+        if (cp < 128) {
+          sy = d.sym[cp];
+        } else {
+          sy = KRCA_DFA_OTHER;
+          int a = 0, z = KRCA_DFA_NRANGE - 1;
+          while (a <= z) {
+            const int mid = (a + z) >> 1;
+            if (cp < krca_dfa_ranges[mid][0]) z = mid - 1;
+            else if (cp > krca_dfa_ranges[mid][1]) a = mid + 1;
+            else {
+              sy = krca_dfa_ranges[mid][2];
+              break;
+            }
+          }
+          sy *= 4;
+        }
+        const uint32_t t = dfa4_step(d, row, sy);
+        row = t;
+        acc |= t;
+        ncp = k + len;
+      }
+    }
+    off += 16;
+    rs_ -= 16;
+    re_ -= 16;
+    ncp -= 16;
+  }
+  return acc >> 16;
+}
+
+__global__ __launch_bounds__(FTPB) void log_index_match(
+    const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off, int64_t D,
+    const int32_t* __restrict__ chunk_doc, int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_base,
+    unsigned long long* __restrict__ status, unsigned int* __restrict__ ticket, int64_t ntiles, int64_t cap,
+    int64_t* __restrict__ line_start, int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
+    int64_t* __restrict__ chunk_line0, int64_t* __restrict__ n_lines, int32_t* __restrict__ long_q,
+    int32_t* __restrict__ n_long) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_text[TILE / 4 + 8];  // the tile + 32 zero bytes
+  __shared__ DfaLds4 d;
+  __shared__ uint32_t s_cs[NBW];
+  __shared__ uint16_t s_ls[LMAX], s_le[LMAX], s_lm[LMAX];
+  __shared__ int32_t s_cnt[TPB], s_cb[TPB];  // per 256-byte chunk: line starts, exclusive base in the tile
+  __shared__ int32_t s_wsum[TPB / 64];
+  __shared__ int32_t s_prev_end;  // tile offset where the previous tile's last line ends (from line 0)
+  __shared__ int64_t s_tile, s_excl;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  dfa4_load(d);  // once per workgroup (persistent)
+  if (tid < 8) s_text[TILE / 4 + tid] = 0u;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  for (;;) {
+    if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
+    if (tile >= ntiles) return;  // uniform
+    const int64_t tile0 = tile * TILE;
+    // ---- A: text -> LDS, line-start bits, chunk counts -----------------------------------------
+    const int64_t qlast = (nbytes - 1) & ~(int64_t)(PIECE - 1);
+    u32x4 raw[FNIT];
+    uint32_t pw[FNIT];
+#pragma unroll
+    for (int it = 0; it < FNIT; ++it) {  // every piece's load out before any is used
+      const int64_t q = tile0 + ((int64_t)it * FTPB + tid) * PIECE;
+      raw[it] = *reinterpret_cast<const u32x4*>(text + (q < nbytes ? q : qlast));
+      const int64_t q0 = tile0 + ((int64_t)it * FTPB + (int64_t)__builtin_amdgcn_readfirstlane(wid) * 64) * PIECE;
+      pw[it] = q0 >= 4 && q0 <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q0 - 4) : 0u;
+    }
+    tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order s_cnt reuse)
+    uint32_t regS[FNIT], regL1[FNIT];  // per piece: starts | odd lengths << 16; lengths 2/3
+#pragma unroll
+    for (int it = 0; it < FNIT; ++it) {
+      const int pc = it * FTPB + tid;  // piece index in the tile
+      const int64_t q = tile0 + (int64_t)pc * PIECE;
+      const bool in = q < nbytes;
+      uint32_t w[4] = {in ? raw[it].x : 0u, in ? raw[it].y : 0u, in ? raw[it].z : 0u, in ? raw[it].w : 0u};
+      *reinterpret_cast<u32x4*>(s_text + pc * 4) = u32x4{w[0], w[1], w[2], w[3]};
+      uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
+      if (lane == 0) wp = pw[it];
+      const uint32_t C = in ? piece_container_starts(s_cs, tile0, q) : 0u;
+      uint32_t S, l0, l1;
+      piece_flags(wp, w, C & 0xFFFFu, S, l0, l1);
+      if (in) {
+        S |= C >> 1;
+        if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
+      } else {
+        S = 0;
+      }
+      regS[it] = S | ((l0 & S) << 16);
+      regL1[it] = l1 & S;
+      uint32_t c = __popc(S);
+#pragma unroll
+      for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
+      if ((tid & (LANES_PER_CHUNK - 1)) == 0) s_cnt[pc / LANES_PER_CHUNK] = (int32_t)c;
+    }
+    __syncthreads();
+    if (tid < TPB) {  // chunk counts -> exclusive bases inside the tile
+      const int32_t v = s_cnt[tid];
+      chunk_cnt[tile * TPB + tid] = v;
+      int32_t x = v;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      if (lane == 63) s_wsum[wid] = x;
+      s_cb[tid] = x - v;
+    }
+    __syncthreads();
+    const int total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    if (tid < TPB) {
+      int32_t before = 0;
+      for (int u = 0; u < wid; ++u) before += s_wsum[u];
+      s_cb[tid] += before;
+    }
+    if (tid == 0)  // publish the aggregate early: later tiles' look-backs need no more from this one
+      __hip_atomic_store(&status[tile], (tile == 0 ? LB_INC : LB_AGG) | (uint64_t)total, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    // ---- B + C, one window of LMAX lines at a time (one window unless lines average < 16 B) ----
+    const int nwin = total > 0 ? (total + LMAX - 1) / LMAX : 1;
+    for (int win = 0; win < nwin; ++win) {
+      const int lo = win * LMAX, hi = min(total, lo + LMAX);
+      // the window's list: starts of lines [lo, hi), ends of lines [lo, hi) (from the next start)
+#pragma unroll
+      for (int it = 0; it < FNIT; ++it) {
+        const int pc = it * FTPB + tid;
+        const uint32_t S = regS[it] & 0xFFFFu;
+        const uint32_t n = __popc(S);
+        uint32_t xs = n;
+#pragma unroll
+        for (int off = 1; off < LANES_PER_CHUNK; off <<= 1) {
+          const uint32_t y = __shfl_up(xs, off, 64);
+          if ((lane & (LANES_PER_CHUNK - 1)) >= off) xs += y;
+        }
+        int id = s_cb[pc / LANES_PER_CHUNK] + (int)(xs - n);
+        if (id > hi || id + (int)n < lo) continue;  // no start of this piece touches the window
+        uint32_t rem = S;
+        const uint32_t l0 = regS[it] >> 16, l1 = regL1[it];
+        while (rem) {
+          const int k = __ffs(rem) - 1;
+          rem &= rem - 1;
+          const int pos = pc * PIECE + k;  // tile offset
+          const int sl = (int)((l0 >> k) & 1u) | (int)(((l1 >> k) & 1u) << 1);
+          if (id >= lo && id < hi) s_ls[id - lo] = (uint16_t)pos;
+          if (id - 1 >= lo && id - 1 < hi) s_le[id - 1 - lo] = (uint16_t)(pos - sl);
+          if (id == 0) s_prev_end = pos - sl;
+          ++id;
+        }
+      }
+      __syncthreads();
+      // the DFA walk: a lane per line, from LDS (the tile's last line and long lines deferred)
+      for (int j = tid; j < hi - lo; j += FTPB) {
+        if (lo + j == total - 1) continue;
+        const int ls = s_ls[j], le = s_le[j];
+        if (le - ls > LONG_LINE) continue;
+        s_lm[j] = (uint16_t)(ls < le ? dfa_walk_lds(s_text, d, ls, le) : 0u);
+      }
+      if (win == 0 && wid == 0) {  // the look-back: this tile's first line id
+        int64_t excl = 0;
+        if (tile > 0) {
+          for (int64_t top = tile - 1;; top -= 64) {
+            const int64_t t = top - lane;  // lane 0 = the nearest predecessor of the window
+            uint64_t sv = t >= 0 ? lb_load(&status[t]) : LB_INC;
+            while (__any((sv >> 62) == 0)) {  // some predecessor has not published yet
+              __builtin_amdgcn_s_sleep(1);
+              if ((sv >> 62) == 0) sv = lb_load(&status[t]);
+            }
+            const uint64_t inc = __ballot((sv >> 62) == 2);
+            const int first = inc ? __builtin_ctzll(inc) : 64;  // nearest inclusive prefix (lowest lane)
+            int64_t val = (lane <= first && t >= 0) ? (int64_t)(sv & LB_VAL) : 0;
+            for (int off = 32; off > 0; off >>= 1) val += (int64_t)__shfl_xor((long long)val, off, 64);
+            excl += val;
+            if (inc) break;
+          }
+          if (lane == 0)
+            __hip_atomic_store(&status[tile], LB_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+          s_excl = excl;
+          tile_base[tile] = excl;
+          if (total > 0 && excl >= 1 && excl - 1 < cap) line_end[excl - 1] = tile0 + s_prev_end;
+          if (tile == ntiles - 1) {
+            const int64_t nl = excl + total;
+            tile_base[ntiles] = nl;
+            *n_lines = nl;
+            if (nl >= 1 && nl <= cap && nbytes > 0) line_end[nl - 1] = last_line_end(text, nbytes, doc_off, D);
+          }
+        }
+      }
+      __syncthreads();
+      const int64_t excl = s_excl;
+      if (win == 0 && tid < TPB) chunk_line0[tile * TPB + tid] = excl + s_cb[tid];
+      for (int j = tid; j < hi - lo; j += FTPB) {  // coalesced by line id
+        const int64_t id = excl + lo + j;
+        if (id >= cap) continue;
+        const int ls = s_ls[j];
+        line_start[id] = tile0 + ls;
+        const bool last = lo + j == total - 1;
+        if (!last) line_end[id] = tile0 + s_le[j];
+        if (last || s_le[j] - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;  // log_dfa_long
+        else line_mask[id] = s_lm[j];
+      }
+      __syncthreads();  // the window's lists (and, after the last, the tile's LDS) are rewritten next
+    }
+  }
+}
+
 int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, TILE)); }
+// int64 words of the int32 long-line queue: lines longer than LONG_LINE, plus one straddling line
+// per tile (log_index_match defers each tile's last line)
+int64_t long_q_words(int64_t nbytes) { return krca::ceil_div(nbytes / LONG_LINE + 1 + num_tiles(nbytes), 2); }
 
 }  // namespace
 
@@ -1386,7 +1676,7 @@ uint64_t krca_log_dfa_digest(void) { return KRCA_DFA_DIGEST; }
 
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
-  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2) +
+  return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + long_q_words(nbytes) +
          nt + 1;  // + krca_log_scan's look-back status words and tile ticket
 }
 
@@ -1483,7 +1773,7 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   int32_t* n_long = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB);
   int32_t* long_q = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB + 1);
   unsigned long long* status =
-      reinterpret_cast<unsigned long long*>(chunk_line0 + nt * TPB + 1 + krca::ceil_div(nbytes / LONG_LINE + 1, 2));
+      reinterpret_cast<unsigned long long*>(chunk_line0 + nt * TPB + 1 + long_q_words(nbytes));
   unsigned int* ticket = reinterpret_cast<unsigned int*>(status + nt);
   hipStream_t st = krca::as_stream(stream);
   // one launch before the index: the chunk -> container map (every chunk of the text is written
@@ -1493,26 +1783,29 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
                      nbytes, cdoc, status, nt + 1, n_long);
   KRCA_LAUNCH_CHECK();
-  static const int64_t resident = [] {  // workgroups the device keeps resident (occupancy API)
-    int dev = 0, cus = 256, per_cu = 4;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&log_index_lines), TPB, 0) !=
-            hipSuccess || per_cu < 1)
-      per_cu = 4;
-    return (int64_t)cus * per_cu;
-  }();
-  const int64_t grid_ix = LOG_IDX_PERSIST ? std::min<int64_t>(nt, resident) : nt;
-  hipLaunchKernelGGL(log_index_lines, dim3((unsigned)grid_ix), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
-                     (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
-                     tile + nt);
-  KRCA_LAUNCH_CHECK();
-  const int64_t* Ld = tile + nt;  // (the last line's end: written by log_index_lines' last tile)
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, DFA_TPB), 256 * 3));
-  hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0, Ld, line_cap,
-                     (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
-  KRCA_LAUNCH_CHECK();
+  const int64_t* Ld = tile + nt;  // the line count, on the device (written by the index's last tile)
+  if (krca::tuning().log_fused) {
+    // the line index and the DFA walk in one pass over the text (one 1024-thread workgroup per CU;
+    // the tiles' last lines and long lines are walked by log_dfa_long below)
+    const int64_t resident =
+        krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_match), FTPB, st, 1);
+    hipLaunchKernelGGL(log_index_match, dim3((unsigned)std::min<int64_t>(nt, resident)), dim3(FTPB), 0, st, text,
+                       nbytes, doc_off, ndocs, (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap,
+                       line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long);
+    KRCA_LAUNCH_CHECK();
+  } else {  // A/B (KRCA_LOG_FUSED=0): the round-3 line index, then a DFA lane per line re-reading the text
+    // workgroups the stream's device keeps resident (occupancy API, cached per device)
+    const int64_t resident = krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_lines), TPB, st, 4);
+    const int64_t grid_ix = LOG_IDX_PERSIST ? std::min<int64_t>(nt, resident) : nt;
+    hipLaunchKernelGGL(log_index_lines, dim3((unsigned)grid_ix), dim3(TPB), 0, st, text, nbytes, doc_off, ndocs,
+                       (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
+                       tile + nt);
+    KRCA_LAUNCH_CHECK();
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, DFA_TPB), 256 * 3));
+    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0, Ld, line_cap,
+                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    KRCA_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,
                      (const int64_t*)line_end, line_mask, (const int32_t*)long_q, (const int32_t*)n_long);
   KRCA_LAUNCH_CHECK();

@@ -228,6 +228,53 @@ __device__ void reduce_single(const int64_t* slice_slots, int64_t* next_slots, d
   ctl->tele = (1.0 - alpha) * krca::kFix + alpha * (double)dang;
 }
 
+// The reduction of folded step it - 1, done at the start of step it (krca_ppr_shard_step_folded):
+// every wave sums the G x NSPREAD slots of set (it - 1) % NSET of each quantity on its own (a
+// butterfly leaves the total in every lane: integers, so all waves and all workgroups get the same
+// totals, with no LDS and no barrier -- three block sums cost 8 barriers, ~2 us per step at C4) and
+// decides convergence / the teleport scale locally.  The `lead` workgroup also zeroes set
+// (it + 1) % NSET of the next write target and records the decision in ctl.  Returns true when
+// step it - 1 converged (the caller does nothing more).  ppr_fold_only runs just this for a rank
+// that owns no plan entries, so every rank's ctl advances identically.
+__device__ __forceinline__ bool fold_reduce(const Fold& fo, const int64_t* wall, int64_t n_max, double alpha, Ctl* ctl,
+                                            bool lead, StepScalars& k) {
+  const int tid = threadIdx.x;
+  const int ps = (fo.it - 1) % NSET, zs = (fo.it + 1) % NSET;
+  int64_t pe = 0, pd = 0, pq = 0;
+  for (int i = tid & 63; i < fo.G * NSPREAD; i += 64) {
+    const int64_t* sl = wall + (int64_t)(i / NSPREAD) * slice_words(n_max) + wslots(n_max) + ps * SET_WORDS + (i % NSPREAD);
+    pe += sl[0];
+    pd += sl[NSPREAD];
+    pq += sl[2 * NSPREAD];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    pe += (int64_t)__shfl_xor((long long)pe, off, 64);
+    pd += (int64_t)__shfl_xor((long long)pd, off, 64);
+    pq += (int64_t)__shfl_xor((long long)pq, off, 64);
+  }
+  const bool stop = fo.it > 1 && fo.err_limit > 0.0 && (double)pe < fo.err_limit;  // step it-1 converged
+  k.tele = (1.0 - alpha) * krca::kFix + alpha * (double)pd;
+  k.qt = fo.it == 1 ? pq : ctl->q_total;  // written by step 1's lead workgroup (an earlier kernel)
+  if (lead) {
+    for (int i = tid; i < SET_WORDS; i += blockDim.x) fo.next[wslots(n_max) + zs * SET_WORDS + i] = 0;
+    if (tid == 0) {
+      if (fo.it == 1) ctl->q_total = pq;
+      ctl->iter = fo.it - 1;
+      if (stop) ctl->converged = fo.it - 1;
+      else ctl->tele = k.tele;
+    }
+  }
+  return stop;
+}
+
+// a folded step of a rank that owns no plan entries (no rows): the reduction only, one workgroup
+__global__ __launch_bounds__(64) void ppr_fold_only(int64_t n_max, double alpha, Ctl* ctl, Fold fo,
+                                                    const int64_t* __restrict__ w_all) {
+  if (ctl->converged) return;
+  StepScalars k;
+  (void)fold_reduce(fo, w_all, n_max, alpha, ctl, true, k);
+}
+
 // r_i <- pulled mass + teleport share; next w_i; residual and dangling contributions
 // (q_i, r_i, deg_i were loaded by the caller together with the row's edges).  flags: PPR_RESIDUAL
 // = the L1 stop rule needs |r_new - r_old| (ro was loaded), PPR_WRITE_R = store r_new (every
@@ -305,8 +352,11 @@ __device__ __forceinline__ void load_head(const int64_t* __restrict__ plan, int6
   // never summed; long-row chunks mask their sum)
   const uint32_t lim = (uint32_t)(H.m.nu > 0 ? (int64_t)H.m.nu : H.m.e1 - H.m.e0);
   const __amdgpu_buffer_rsrc_t rs = buf_over(pk + H.m.e0, 4 * lim);
+  // the slot stride goes into the VGPR offset, never the SGPR one: the raw-buffer range check
+  // covers VGPR + immediate offset only, so an SGPR stride would let a lane below `lim` read past
+  // the block (and, for the last entry, past pk) instead of getting 0
 #pragma unroll
-  for (int j = 0; j < SEG; ++j) H.c[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * tid), 4 * j * TPB, 0);
+  for (int j = 0; j < SEG; ++j) H.c[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (tid + j * TPB)), 0, 0);
 }
 
 template <int FLAGS>
@@ -399,37 +449,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   StepScalars k;
   int64_t* my_slots = send + wslots(n_max);  // this step's partial-sum slots
   if (fo.on) {  // block-uniform
-    const int ps = (fo.it - 1) % NSET, zs = (fo.it + 1) % NSET;
-    const int64_t* wall = reinterpret_cast<const int64_t*>(w);
-    // every wave sums the G x 32 slots of each quantity on its own (a butterfly leaves the total in
-    // every lane): integers, so all waves and all workgroups get the same totals, and the prologue
-    // needs no LDS and no barrier (three block sums cost 8 barriers, ~2 us per step at C4)
-    int64_t pe = 0, pd = 0, pq = 0;
-    for (int i = tid & 63; i < fo.G * NSPREAD; i += 64) {
-      const int64_t* sl = wall + (int64_t)(i / NSPREAD) * slice_words(n_max) + wslots(n_max) + ps * SET_WORDS + (i % NSPREAD);
-      pe += sl[0];
-      pd += sl[NSPREAD];
-      pq += sl[2 * NSPREAD];
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      pe += (int64_t)__shfl_xor((long long)pe, off, 64);
-      pd += (int64_t)__shfl_xor((long long)pd, off, 64);
-      pq += (int64_t)__shfl_xor((long long)pq, off, 64);
-    }
-    const int64_t errp = pe, dangp = pd, qsp = pq;
-    const bool stop = fo.it > 1 && fo.err_limit > 0.0 && (double)errp < fo.err_limit;  // step it-1 converged
-    k.tele = (1.0 - alpha) * krca::kFix + alpha * (double)dangp;
-    k.qt = fo.it == 1 ? qsp : ctl->q_total;  // written by step 1's workgroup 0 (an earlier kernel)
-    if (blockIdx.x == 0) {
-      for (int i = tid; i < SET_WORDS; i += TPB) fo.next[wslots(n_max) + zs * SET_WORDS + i] = 0;
-      if (tid == 0) {
-        if (fo.it == 1) ctl->q_total = qsp;
-        ctl->iter = fo.it - 1;
-        if (stop) ctl->converged = fo.it - 1;
-        else ctl->tele = k.tele;
-      }
-    }
-    if (stop) return;  // uniform: every workgroup decided the same
+    if (fold_reduce(fo, reinterpret_cast<const int64_t*>(w), n_max, alpha, ctl, blockIdx.x == 0, k))
+      return;  // step it - 1 converged: uniform, every workgroup decided the same
     my_slots += (fo.it % NSET) * SET_WORDS;
   } else {
     k.tele = ctl->tele;
@@ -739,8 +760,18 @@ int krca_ppr_shard_step_folded(const int64_t* row_ptr, const int32_t* col, const
   KRCA_CHECK_ARG(next_target && (G == 1 ? next_target == w_all : next_target == send),
                  "krca_ppr_shard_step_folded: next_target is w_all at G = 1, send at G > 1");
   const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
+  const Fold fo{1, (int)it, (int)G, err_limit, next_target};
+  if (plan_len == 0) {  // a rank without rows still does the step's reduction: its ctl (iteration
+                        // count, convergence) and slot rotation advance with every other rank's
+    KRCA_CHECK_ARG(w_all && ctl && n_local == 0, "krca_ppr_shard_step_folded: no plan for %lld rows",
+                   (long long)n_local);
+    hipLaunchKernelGGL(ppr_fold_only, dim3(1), dim3(64), 0, krca::as_stream(stream), n_max, alpha,
+                       reinterpret_cast<Ctl*>(ctl), fo, w_all);
+    KRCA_LAUNCH_CHECK();
+    return KRCA_OK;
+  }
   return launch_step(row_ptr, col, plan, plan_len, lane, w_all, outdeg, q_local, n_local, n_max, N, alpha, flags, r_local,
-                     send, ctl, Fuse{0, 0.0, nullptr}, stream, Fold{1, (int)it, (int)G, err_limit, next_target});
+                     send, ctl, Fuse{0, 0.0, nullptr}, stream, fo);
 }
 
 int krca_ppr_shard_finish(const int64_t* w_all, int32_t G, int64_t n_max, int64_t N, double alpha, double tol,
@@ -783,16 +814,9 @@ int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan,
                  "krca_ppr_shard_step: null pointer");
   KRCA_CHECK_ARG(w_all != send, "krca_ppr_shard_step: w_all and send must be distinct buffers (ping-pong)");
   const int64_t nblk = plan_len / 4;
-  static const int64_t occupancy = [] {  // workgroups the device keeps resident (occupancy API)
-    int dev = 0, cus = 256, per_cu = 4;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&ppr_step<0>), TPB, 0) !=
-            hipSuccess || per_cu < 1)
-      per_cu = 4;
-    return (int64_t)cus * per_cu;
-  }();
+  // workgroups the stream's device keeps resident (occupancy API, cached per device)
+  const int64_t occupancy =
+      krca::resident_workgroups(reinterpret_cast<const void*>(&ppr_step<0>), TPB, krca::as_stream(stream), 4);
   const int64_t resident = krca::tuning().ppr_grid > 0 ? (int64_t)krca::tuning().ppr_grid : occupancy;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nblk, resident));
   const bool nt = krca::tuning().ppr_nt != 0;

@@ -124,6 +124,11 @@ def load_library(path=None):
     p = path or _LIB_PATH
     if not os.path.exists(p):
         raise KrcaError(f"libkrca.so not found at {p} (build with `make -C kubernetes-rca-system_amd/csrc`)")
+    # torch first: its HIP runtime must be the process's one.  libkrca links libamdhip64.so.7, which
+    # resolves to the copy torch already loaded; loaded before torch it pulls in /opt/rocm's copy and
+    # torch then loads its own beside it (two HIP runtimes: a later call failed with "no ROCm-capable
+    # device is detected" on the GPU box)
+    import torch  # noqa: F401
     lib = ctypes.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
@@ -132,6 +137,17 @@ def load_library(path=None):
     if path is None or _lib is None:
         _lib = lib
     return lib
+
+
+def library_info():
+    """Which libkrca this process loaded: its path, krca_version() and the SHA-256 of the file (so a
+    GPU run's record names the exact build it exercised)."""
+    import hashlib
+    lib = load_library()
+    with open(_LIB_PATH, "rb") as f:
+        digest = hashlib.sha256(f.read()).hexdigest()
+    return {"path": os.path.relpath(_LIB_PATH, os.path.dirname(os.path.dirname(os.path.dirname(_LIB_PATH)))),
+            "version": int(lib.krca_version()), "sha256": digest[:16]}
 
 
 def _check(rc, what, lib=None):

@@ -21,6 +21,7 @@ The per-rank numeric work is behind a small backend interface so the same orches
 on the device (:class:`DeviceShard`, libkrca) and, in the CPU test-suite, on a NumPy restatement
 with the gloo backend (tests/test_rca_dist_cpu.py).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -150,13 +151,23 @@ class Comm:
         all_gather_flat(out, inp, self.world, self.group, self._gloo)
 
 
+def _collective_dtypes():
+    import torch
+    return (torch.uint8, torch.int8, torch.int32, torch.int64, torch.float32, torch.float64)
+
+
 def all_gather_flat(out, inp, world, group=None, gloo=None):
     """out[world * inp.numel()] <- every rank's inp.  RCCL ("nccl") gathers into the flat tensor
     directly; gloo has no all_gather_into_tensor, so it takes the list form.  Chosen once from the
     backend, so a real RCCL failure (timeout, size mismatch) propagates instead of being retried."""
+    import torch
     import torch.distributed as dist
     if gloo is None:
         gloo = dist.get_backend(group) == "gloo"
+    if out.dtype not in _collective_dtypes():
+        # a gather only moves bytes: dtypes the backends lack (RCCL / NCCL have no int16, gloo
+        # refuses it: the correlation's fp16 rows travel as int16) go as uint8 views
+        out, inp = out.view(torch.uint8), inp.view(torch.uint8)
     if gloo:
         dist.all_gather(list(out.view(world, -1).unbind(0)), inp, group=group)
     else:
@@ -335,10 +346,19 @@ class DeviceShard:
     def step_folded(self, alpha, tol, it, flags):
         """Folded iteration `it` (1-based): the reduction of step it - 1 and the step, one kernel."""
         e, p = self.eng, self.eng.ptr
-        if not self.plan_len:
-            return
         st = e._stream()
         nxt = self.w_all if self.world == 1 else self.send
+        if not self.plan_len:
+            # a rank that owns no pods still runs the step's reduction (krca_ppr_shard_step_folded
+            # launches it alone for an empty plan): its iteration count and convergence flag must
+            # advance with the other ranks', or its convergence poll never stops and the
+            # collectives mismatch
+            null = ctypes.c_void_p(0)
+            self._chk(e.lib.krca_ppr_shard_step_folded(null, null, null, 0, null, p(self.w_all), self.world, null, null,
+                                                       0, self.n_max, self.N, float(alpha), float(tol), int(it),
+                                                       int(flags), null, p(self.send), p(nxt), p(self.ctl), st),
+                      "krca_ppr_shard_step_folded")
+            return
         key = ("fold", self.w_all.data_ptr(), self.send.data_ptr(), float(alpha), float(tol), int(it), int(flags), st.value)
         args = self._cached(key, lambda: (p(self.row_ptr), p(self.col), p(self.plan), self.plan_len, p(self.lane),
                                           p(self.w_all), self.world, p(self.outdeg), p(self.q), self.n, self.n_max, self.N,

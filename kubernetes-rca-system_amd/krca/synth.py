@@ -251,3 +251,33 @@ def make_log_corpus(n_docs, lines_per_doc=2.5, error_rate=0.3, seed=0, hazard_ra
         docs.append("\n".join(lines[k:k + c]) + ("\n" if c and rng.random() < 0.5 else ""))
         k += c
     return docs
+
+
+def spread_hops(mesh, roots, hops=2, per_root=20, seed=0):
+    """Callers of each root that carry the fault's symptoms, for the 'spread' ranking scenario
+    (DESIGN.md §3.2): per root and hop, up to `per_root` not-yet-chosen callers of that root's
+    previous hop, sampled (seeded).  Unlike caller_hops (every caller up to a global cap), the
+    anomalous callers stay a small set per root, so the root is what they have in common."""
+    rng = np.random.default_rng(int(seed) + 99)
+    seen = set(int(r) for r in roots)
+    frontier = {int(r): [int(r)] for r in roots}
+    out = []
+    for _ in range(hops):
+        nxt, newf = [], {}
+        for r, fr in frontier.items():
+            cand = []
+            for v in fr:
+                cand.extend(mesh.col[mesh.row_ptr[v]:mesh.row_ptr[v + 1]].tolist())
+            cand = [c for c in dict.fromkeys(cand) if c not in seen]
+            if len(cand) > per_root:
+                cand = rng.choice(cand, per_root, replace=False).tolist()
+            seen.update(cand)
+            nxt.extend(cand)
+            newf[r] = cand
+        frontier = newf
+        out.append(np.asarray(nxt, np.int64))
+    return out
+
+
+# the spread scenario's spikes: callers one hop up carry a LARGER spike than the root itself
+SPREAD_SIGMAS = dict(root_sigma=8.0, hop_sigma=9.0, hop_decay=0.9)

@@ -13,3 +13,12 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libkrca.so on the device)")
     config.addinivalue_line("markers", "slow: long-running")
+
+
+def pytest_report_header(config):
+    """The libkrca build the run loads (path, krca_version(), SHA-256 prefix), in the run's header."""
+    try:
+        from krca import native
+        return f"libkrca: {native.library_info()}"
+    except Exception as e:  # noqa: BLE001  (no build yet: the CPU suite reports it)
+        return f"libkrca: not loaded ({e})"

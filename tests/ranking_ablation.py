@@ -3,7 +3,8 @@
 oracle; DESIGN.md §3.2 "Ranking").  For seeded C2-shaped meshes (10k pods / 200k edges, 8 metrics
 x 1440 steps) with 10 planted root pods and their callers perturbed hop by hop (krca/synth.py),
 reports the recall@10 of the planted roots for PageRank damping alpha, seed floor and ranking key
-(r = propagated mass alone, r*q = mass times own anomaly, q = anomaly alone).
+(r = propagated mass alone, r*q = mass times own anomaly, psq = mass received from callers x
+sqrt(own anomaly), q = anomaly alone).  --spread: the callers carry the symptoms (synth.spread_hops).
 
   python tests/ranking_ablation.py [--seeds 3] [--out profiles/r2/ranking_ablation.json]
 """
@@ -21,22 +22,35 @@ import oracle  # noqa: E402
 from krca import synth  # noqa: E402
 
 
+def psq_key(r, q, alpha):
+    """The mass a pod received from its callers (r minus its own teleport share (1 - alpha) p_i)
+    times the square root of its own anomaly: an alternative key evaluated beside r and r*q."""
+    rr, qq = r.astype(np.float64), q.astype(np.float64)
+    p = qq / qq.sum() * 2.0 ** 60 if qq.sum() > 0 else np.zeros_like(qq)
+    return (rr - (1.0 - alpha) * p) * np.sqrt(qq)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, default=3)
     ap.add_argument("--pods", type=int, default=10_000)
     ap.add_argument("--edges", type=int, default=200_000)
     ap.add_argument("--out")
+    ap.add_argument("--spread", action="store_true",
+                    help="the anomaly spreads to the callers (synth.spread_hops: 20 sampled callers per root and "
+                         "hop, 2 hops; root 8 sigma, hop h 9 * 0.9^(h-1) sigma): the callers look as anomalous "
+                         "as the root, the reference's premise that symptoms show up upstream of the cause")
     a = ap.parse_args()
     from scipy.special import ndtri
     auto = round(float(ndtri(1.0 - 1.0 / (2.0 * a.pods * 8))), 3)  # expected max |z| of P*M null series
-    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0, auto, 5.0) for key in ("r", "rq")] + \
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0, auto, 5.0) for key in ("r", "rq", "psq")] + \
         [(None, None, "q")]
     hits = {d: [] for d in defs}
     for seed in range(a.seeds):
         m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)
-        hops = synth.caller_hops(m, m.roots)
-        x = synth.make_metrics(a.pods, 8, 1440, seed=seed, roots=m.roots, hop_sets=hops).numpy()
+        hops = synth.spread_hops(m, m.roots, seed=seed) if a.spread else synth.caller_hops(m, m.roots)
+        kw = synth.SPREAD_SIGMAS if a.spread else {}
+        x = synth.make_metrics(a.pods, 8, 1440, seed=seed, roots=m.roots, hop_sets=hops, **kw).numpy()
         s = oracle.c_rolling_score(x, 60)["score"]
         roots = set(m.roots.tolist())
         for al, fl, key in defs:
@@ -44,7 +58,7 @@ def main():
                 idx, _ = oracle.topk_ref(s.astype(np.float64), 10)
             else:
                 _, r, _, q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, s, al, 30, 0.0, fl, return_q=True)
-                kv = oracle.c_rca_key(r, q) if key == "rq" else r
+                kv = oracle.c_rca_key(r, q) if key == "rq" else psq_key(r, q, al) if key == "psq" else r
                 idx, _ = oracle.topk_ref(kv, 10)
             hits[(al, fl, key)].append(len(roots & set(int(i) for i in idx)) / len(roots))
     rows = [dict(alpha=al, seed_floor=fl, key=key, recall_at_10=float(np.mean(v)), per_seed=v)

@@ -2,7 +2,10 @@
 
 Two ranks rehearsed on one GPU over gloo (KRCA_BENCH_BACKEND=gloo, the ranks share the device):
 the JSON line reports the ranks of the communicator, and the sharded step (pod-sharded scoring,
-one all-gather per PageRank iteration) ranks the same top-10 as one rank.
+one all-gather per PageRank iteration) ranks the same top-10 as one rank.  At N = 2 the line
+verifies itself (ranks gathered to rank 0, bit-identical to the oracle; sampled scores of every
+rank), carries the CPU baseline and the per-rank / aggregate roofline, and its correlation leg runs
+the pod-sharded krca/corr_dist.py path with its own exactness check.
 """
 import json
 import os
@@ -15,7 +18,8 @@ from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
-ARGS = ["--pods", "20000", "--edges", "400000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+ARGS = ["--pods", "20000", "--edges", "400000", "--steps", "2", "--warmup", "1", "--cpu-warmup", "1", "--cpu-runs", "2",
+        "--corr-runs", "1"]
 
 
 def run_bench(n, extra=()):
@@ -35,6 +39,17 @@ def test_bench_gpus_2_runs_two_ranks():
     two = run_bench(2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["world_ranks"] == 2
     assert two["rca_top10"] == one["rca_top10"]
-    assert one["verify"]["ppr_fixed_point_bit_identical"] and one["verify"]["top10_identical"]
+    for line in (one, two):
+        v = line["verify"]
+        assert v["ppr_fixed_point_bit_identical"] and v["top10_identical"] and v["n_exceed_flags_bit_exact"], v
+        assert v["ranks_gathered"] == line["n_gpus"] and v["score_max_rel_err"] < 1e-5
+        assert line["cpu_baseline"]["value"] > 0 and line["roofline"]["traffic"] is not None
+        assert line["roofline"]["aggregate"]["peak"] == 8000.0 * line["n_gpus"]
+        c = line["corr"]
+        assert c["pods"] == 20000 and c["ms"] > 0 and all(c["verify"][key] for key in
+                                                          ("counts_exact", "sets_exact", "values_exact", "all_certified"))
+    assert two["corr"]["parallelism"].startswith("pod-sharded")
     prof = one["profile"]
-    assert prof["krca_ppr_shard_step"]["launches"] == 30 and prof["krca_rolling_score"]["launches"] == 1
+    # the profiled step is the folded sequence RcaStep runs: init, 30 x (folded step, exchange), finish
+    assert prof["krca_ppr_shard_step_folded"]["launches"] == 30 and prof["krca_rolling_score"]["launches"] == 1
+    assert prof["krca_ppr_shard_finish"]["launches"] == 1 and prof["exchange"]["launches"] == 31

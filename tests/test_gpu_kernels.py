@@ -259,6 +259,42 @@ def test_log_scan_one_call_and_fallback_identical(eng):
         assert np.array_equal(r["line_mask"].cpu().numpy(), out[0]["line_mask"])
 
 
+def test_log_scan_fused_walk_identical(eng):
+    """krca_log_scan's fused pass (log_index_match: the DFA walks each 64 KiB tile's lines from LDS
+    in the line-index pass; each tile's last line and lines over 1 KiB go to log_dfa_long) equals
+    the round-3 path (KRCA_LOG_FUSED=0: the index, then log_dfa re-reading the text) on every
+    output, and the oracle: tiles of more than 4,096 lines (several list windows per tile: 2-byte
+    and empty lines), lines straddling one and several tiles (a 300 KiB line leaves whole tiles
+    without a line start), CRLF and U+2028 split across a tile edge, lines of exactly 1,024 and
+    1,025 bytes, a text ending mid-piece."""
+    rng = np.random.default_rng(13)
+    docs = synth.make_log_corpus(5000, lines_per_doc=4, seed=12, hazard_rate=0.02)
+    docs.append("e\n" * 40000)                         # 2-byte lines: ~32k lines per tile
+    docs.append("\n" * 70000 + "Error")                # empty lines
+    docs.append("k" * 300_000 + " OOMKilled " + "m" * 1000)  # tiles with no line start
+    docs.append("x" * 1024 + "\n" + "y" * 1020 + "Error\n" + "z" * 1023)  # 1024 / 1025 bytes
+
+    def to_tile_end(extra):  # filler so that the next byte sits `extra` bytes before a tile edge
+        pos = sum(len(d.encode()) for d in docs) + 1
+        return (-pos - extra) % 65536 + 1
+    docs.append("p" * to_tile_end(1) + "\r\nKilled timeout")  # CRLF split across a tile edge
+    docs.append("w" * to_tile_end(1) + "\u2028 Traceback")    # U+2028 split across a tile edge
+    docs += ["".join(rng.choice(["Error ", "\r\n", "é", "\x85", "panic:", "v" * 200, " "]) for _ in range(30))
+             for _ in range(300)]
+    docs.append("tail Error é")                        # the text ends mid-piece
+    blob, off = pack_documents(docs)
+    tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
+    out = {}
+    for fused in (1, 0):
+        with native.tune(eng.lib, KRCA_LOG_FUSED=fused):
+            r = eng.log_scan_device(tb, toff)
+            out[fused] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
+    assert out[1].keys() == out[0].keys()
+    for k in out[0]:
+        assert np.array_equal(out[1][k], out[0][k]), k
+    _check_docs(eng, docs)
+
+
 # ---- a10 personalized PageRank ---------------------------------------------------------------
 def test_ppr_known_answer(eng):
     import json
@@ -407,6 +443,96 @@ def test_rca_sharded_path_emulated_on_one_gpu(eng, G, folded):
     _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
     got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
     assert np.array_equal(got, r)
+
+
+@pytest.mark.parametrize("n,G", [(9, 4), (49, 8), (30000, 3)])
+def test_rca_folded_tolerance_with_empty_rank_emulated(eng, n, G):
+    """Folded steps under a tolerance (the stream's re-rank loop), G shards on one device with the
+    all-gather done by copies, including ranks that own no pods (shard_range(9, 4) and (49, 8)
+    leave the last rank empty): every rank's control block reports the same iteration count and
+    convergence after every step -- a rank without rows runs the step's reduction alone
+    (krca_ppr_shard_step_folded, empty plan) -- and the ranks are bit-identical to the C oracle.
+    Before that, an empty rank never advanced its count, so its convergence poll never stopped and
+    its all-gathers outlived the other ranks'."""
+    from krca.agents.topology import csr_from_edges
+    from krca.rca import Config, DeviceShard, shard_graph, shard_range
+    rng = np.random.default_rng(n)
+    E = min(n * 12, n * (n - 1))
+    src, dst = rng.integers(0, n, E), rng.integers(0, n, E)
+    keep = src != dst
+    rp_all, col_all, od_all = csr_from_edges(n, src[keep], dst[keep])
+    seed = (rng.random(n) * 2.0).astype(np.float32)
+    cfg = Config(alpha=0.85, seed_floor=1.0)
+    tol, max_iter = 1e-9, 200
+    shards = []
+    for g in range(G):
+        lo, hi, n_max = shard_range(n, G, g)
+        rp, col, od = shard_graph(rp_all, col_all, od_all, lo, hi)
+        s = DeviceShard(eng, None, rp, col, od, n, n_max, G, cfg)
+        s.score_out = {"score": torch.from_numpy(np.concatenate([seed[lo:hi], np.zeros(1, np.float32)])).cuda()}
+        shards.append(s)
+    assert any(s.n == 0 for s in shards) or n == 30000
+
+    def exchange():
+        wall = torch.cat([s.send for s in shards])
+        for s in shards:
+            s.w_all.copy_(wall)
+
+    for s in shards:
+        s.init(cfg.alpha, cfg.floor(n))
+    exchange()
+    it = 0
+    while it < max_iter:
+        it += 1
+        for s in shards:
+            s.step_folded(cfg.alpha, tol, it, 3)
+        exchange()
+        states = {s.ctl_read() for s in shards}
+        assert len(states) == 1, (it, states)  # every rank (empty ones too) at the same count / flag
+        if states.pop()[1]:
+            break
+    for s in shards:
+        s.finish(cfg.alpha, tol, it)
+    _, r_ref, it_ref = oracle.c_ppr(rp_all, col_all, od_all, seed, cfg.alpha, max_iter, tol, cfg.floor(n))
+    assert it_ref > 0 and {s.ctl_read() for s in shards} == {(it_ref, True)}
+    got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
+    assert np.array_equal(got, r_ref)
+
+
+def test_stream_cold_solve_fresh_streams_bit_identical(eng):
+    """Regression for a cold-solve mismatch seen once during round 3's folded-iteration work
+    (call r3ac: a fresh stream's first solve came out with the uniform teleport on part of the
+    pods, i.e. some workgroups had read a zero seed total).  Several fresh StreamingRCA objects,
+    each pushed a history and solved cold under the L1 stop rule, one after another on the same
+    device (stale device memory between them): ranks and iteration counts bit-identical to
+    oracle.c_ppr every time, and the second solve (warm) to oracle.c_ppr_warm."""
+    from krca.rca import Config
+    from krca.stream import StreamingRCA
+    P, M, T = 200_000, 4, 200
+    mesh = synth.make_graph(P, avg_degree=12, seed=21)
+    hops = synth.caller_hops(mesh, mesh.roots)
+    x = synth.make_metrics_range(0, P, M, T + 1, seed=21, roots=mesh.roots, hop_sets=hops, device="cuda")
+    cfg = Config(window=30)
+    fl = cfg.floor(P, M)
+    ref = None
+    for trial in range(3):
+        s = StreamingRCA(eng, mesh.row_ptr, mesh.col, mesh.outdeg, M, cfg, horizon=T, tol=1e-9, max_iter=100)
+        s.push_metrics(x[:T])
+        s.rerank()
+        sc0 = s.shard.score_out["score"].cpu().numpy()
+        r0 = s.shard.r[:P].cpu().numpy()
+        if ref is None:
+            _, r_ref, it_ref = oracle.c_ppr(mesh.row_ptr, mesh.col, mesh.outdeg, sc0, cfg.alpha, 100, 1e-9, fl)
+            ref = (sc0, r_ref, it_ref)
+        assert np.array_equal(sc0, ref[0]), trial
+        assert np.array_equal(r0, ref[1]) and s.last_iters == ref[2], trial
+        s.push_metrics(x[T:T + 1])
+        s.rerank()
+        r_w, it_w, _ = oracle.c_ppr_warm(mesh.row_ptr, mesh.col, mesh.outdeg, s.shard.score_out["score"].cpu().numpy(),
+                                         ref[1], cfg.alpha, 100, 1e-9, fl)
+        assert np.array_equal(s.shard.r[:P].cpu().numpy(), r_w) and s.last_iters == it_w, trial
+        del s
+    torch.cuda.synchronize()
 
 
 # ---- a13 error templates -------------------------------------------------------------------

@@ -86,3 +86,41 @@ def test_bench_metrics_do_not_depend_on_sharding():
     for cuts in ([0, 150, 300], [0, 100, 200, 300], [0, 77, 154, 231, 300]):
         parts = [synth.make_metrics_range(a, b, 8, 100, **kw) for a, b in zip(cuts, cuts[1:])]
         assert torch.equal(full, torch.cat(parts, 1))
+
+
+def _gather_worker(rank, world, port, out_q):
+    sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd")]
+    import torch
+    import torch.distributed as dist
+    from krca.rca import all_gather_flat
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = {}
+    for dt in (torch.int16, torch.float16, torch.int64, torch.float32):
+        inp = (torch.arange(6) + 100 * rank).to(dt)
+        out = torch.empty(6 * world, dtype=dt)
+        all_gather_flat(out, inp, world)
+        got[str(dt)] = out.tolist()
+    out_q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_gather_flat_moves_dtypes_the_backends_lack():
+    """The correlation's fp16 rows travel as int16 (krca/corr_dist.py), a dtype gloo refuses and
+    RCCL / NCCL do not have: all_gather_flat moves such tensors as uint8 views, bit for bit."""
+    import torch
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for dt in (torch.int16, torch.float16, torch.int64, torch.float32):
+        want = torch.cat([(torch.arange(6) + 100 * r).to(dt) for r in range(world)]).tolist()
+        assert res[0][str(dt)] == want and res[1][str(dt)] == want

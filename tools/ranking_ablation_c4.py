@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--seeds", type=int, default=2)
     ap.add_argument("--out")
+    ap.add_argument("--spread", action="store_true",
+                    help="the anomaly spreads to the callers (synth.spread_hops: 20 sampled callers per root and "
+                         "hop, 2 hops; root 8 sigma, hop h 9 * 0.9^(h-1) sigma): the callers look as anomalous "
+                         "as the root, the reference's premise that symptoms show up upstream of the cause")
     a = ap.parse_args()
     import torch
     from krca import native, synth
@@ -40,14 +44,15 @@ def main():
     M, T = 8, 1440
     af = auto_floor(a.pods * M)
     floors = [0.0, 4.0, 5.0, round(af, 3), 6.0]
-    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in floors for key in ("r", "rq")] + [(None, None, "q")]
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in floors for key in ("r", "rq", "psq")] + [(None, None, "q")]
     hits = {d: [] for d in defs}
     diag = []
     for seed in range(a.seeds):
         t0 = time.time()
         m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)
-        hops = synth.caller_hops(m, m.roots)
-        x = synth.make_metrics_range(0, a.pods, M, T, seed=seed, roots=m.roots, hop_sets=hops, device="cuda")
+        hops = synth.spread_hops(m, m.roots, seed=seed) if a.spread else synth.caller_hops(m, m.roots)
+        kw = synth.SPREAD_SIGMAS if a.spread else {}
+        x = synth.make_metrics_range(0, a.pods, M, T, seed=seed, roots=m.roots, hop_sets=hops, device="cuda", **kw)
         rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, a.pods)
         sh = DeviceShard(eng, x, rp, col, od, a.pods, a.pods, 1, RANKING)
         sh.score()
@@ -73,6 +78,10 @@ def main():
                 st.propagate()
                 if key == "rq":
                     idx, _ = st.merge(*sh.local_topk(10))
+                elif key == "psq":  # mass received from callers x sqrt(own anomaly) (tests/ranking_ablation.py)
+                    rr, qq = sh.r[:a.pods].double(), sh.q[:a.pods].double()
+                    p = qq / qq.sum() * 2.0 ** 60 if float(qq.sum()) > 0 else torch.zeros_like(qq)
+                    idx = torch.topk((rr - (1.0 - al) * p) * qq.sqrt(), 10).indices.cpu().numpy()
                 else:
                     idx = torch.topk(sh.r[:a.pods], 10).indices.cpu().numpy()
             hits[(al, fl, key)].append(len(roots & set(int(i) for i in idx)) / len(roots))
