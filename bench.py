@@ -185,8 +185,8 @@ def sum_over_ranks(vals, world):
 
 
 def gather_rows(t, n_max, world):
-    """This rank's rows (<= n_max of them) -> every rank's rows, each rank's slice padded to n_max;
-    rank g's rows start at g * n_max, which is its first pod (krca.rca.shard_range)."""
+    """This rank's rows (<= n_max of them) -> every rank's rows, each rank's slice padded to n_max
+    (krca.rca.Partition.unpad puts them back in pod order)."""
     import torch
     from krca.rca import all_gather_flat
     pad = torch.zeros(n_max, dtype=t.dtype, device=t.device)
@@ -218,7 +218,7 @@ def pmc_traffic(args, bytes_alg, world):
         return None, None
 
 
-def verify_step(args, cfg, mesh, shard, x, lo, hi, n_max, world, rank):
+def verify_step(args, cfg, mesh, shard, x, part, rank):
     """Untimed parity of the last step at any N: every rank's fixed-point ranks and scores are
     gathered to rank 0 and compared with the C oracle run on the whole mesh (ranks bit for bit,
     top-10 identical); each rank checks n_exceed / flags / scores of its own sampled pods against
@@ -226,9 +226,10 @@ def verify_step(args, cfg, mesh, shard, x, lo, hi, n_max, world, rank):
     import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n_loc = hi - lo
-    r_all = gather_rows(shard.r[:n_loc], n_max, world)[:args.pods].cpu().numpy()
-    sc_all = gather_rows(shard.score_out["score"][:n_loc], n_max, world)[:args.pods].cpu().numpy()
+    lo, hi, n_max = part.range(rank)
+    world, n_loc = part.world, hi - lo
+    r_all = part.unpad(gather_rows(shard.r[:n_loc], n_max, world).cpu().numpy())
+    sc_all = part.unpad(gather_rows(shard.score_out["score"][:n_loc], n_max, world).cpu().numpy())
     ns = min(max(1, 2000 // world), n_loc)
     samp = np.sort(np.random.default_rng(1 + rank).choice(n_loc, size=ns, replace=False))
     st = torch.from_numpy(samp).to(x.device)
@@ -407,7 +408,7 @@ def main():
     import torch.distributed as dist
 
     from krca import native, synth
-    from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
+    from krca.rca import Comm, Config, DeviceShard, Partition, RcaStep, shard_graph
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -431,8 +432,13 @@ def main():
     t0 = time.time()
     mesh = synth.make_graph(args.pods, n_edges=args.edges, seed=args.seed)
     hops = synth.caller_hops(mesh, mesh.roots)
-    lo, hi, n_max = shard_range(args.pods, world, rank)
-    rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, lo, hi)
+    # contiguous ranges of ceil(N / G) pods.  (Partition.balanced caps the in-edges per rank -- the
+    # mesh's hub services sit at low ids -- but measured no gain at G = 8: the PageRank iteration's
+    # fixed cost dominates a small shard's step, and the capped ranks score more pods;
+    # tools/g8_step_emulation.py)
+    part = Partition.uniform(args.pods, world)
+    lo, hi, n_max = part.range(rank)
+    rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, lo, hi, part)
     x = synth.make_metrics_range(lo, hi, args.metrics, args.tsteps, window=args.window, seed=args.seed,
                                  roots=mesh.roots, hop_sets=hops, device=torch.device("cuda", local))
     n_pipe = 1 if args.no_pipeline else 2
@@ -545,7 +551,9 @@ def main():
                                    "(rolling z-score -> 30-iteration seeded PPR -> top-10), ranking of krca.rca.Config",
                        "pods": args.pods, "edges": mesh.n_edges, "metrics": args.metrics, "tsteps": args.tsteps,
                        "window": args.window, "ppr_iters": args.iters, "alpha": args.alpha,
-                       "seed_floor": cfg.seed_floor, "parallelism": f"pod-sharded x{world}"},
+                       "seed_floor": cfg.seed_floor, "parallelism": f"pod-sharded x{world}",
+                       "partition": "uniform contiguous pod ranges (krca.rca.Partition.uniform)",
+                       "shard_bounds": [int(b) for b in part.bounds]},
             "e2e_rca_latency_ms": latency_ms, "e2e_rca_latency_p95_ms": latency_p95_ms,
             "step_ms_median": float(np.median(step_ms)), "step_ms_p95": float(np.percentile(step_ms, 95)),
             "pipelined_streams": n_pipe,
@@ -571,7 +579,7 @@ def main():
 
     # ---- verification (not timed): bit-exact PageRank / top-10 vs the C oracle, any N -------
     if not args.no_verify:
-        v = verify_step(args, cfg, mesh, shard, x, lo, hi, n_max, world, rank)
+        v = verify_step(args, cfg, mesh, shard, x, part, rank)
         if rank == 0:
             v["top10_identical"] = v.pop("oracle_top10") == result["rca_top10"]
             result["verify"] = v

@@ -176,12 +176,14 @@ __device__ __forceinline__ uint32_t sep_flags(uint32_t wprev, uint32_t w) {
 // tile0-32+j): one coalesced pass over doc_off from the container holding byte tile0-1 (chunk_doc),
 // instead of a dependent doc_off walk per 16-byte piece.  Used by log_count and log_lines.
 constexpr int NBW = (int)(TILE / 32) + 2;  // bytes tile0-32 .. tile0+TILE+31
-__device__ __forceinline__ void tile_container_starts(uint32_t* s_cs, int64_t tile0, int64_t nbytes,
-                                                      const int64_t* __restrict__ doc_off, int64_t D,
-                                                      const int32_t* __restrict__ chunk_doc) {
-  for (int i = threadIdx.x; i < NBW; i += blockDim.x) s_cs[i] = 0u;
+template <int64_t TL>
+__device__ __forceinline__ void tile_container_starts_t(uint32_t* s_cs, int64_t tile0, int64_t nbytes,
+                                                        const int64_t* __restrict__ doc_off, int64_t D,
+                                                        const int32_t* __restrict__ chunk_doc) {
+  constexpr int NB = (int)(TL / 32) + 2;
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) s_cs[i] = 0u;
   __syncthreads();
-  const int64_t tend = tile0 + TILE;
+  const int64_t tend = tile0 + TL;
   int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
   k0 = k0 < 0 ? 0 : (k0 > D ? D : k0);  // memory safety only: the map is exact under the doc_off contract
   for (int64_t kb = k0;; kb += blockDim.x) {
@@ -193,6 +195,11 @@ __device__ __forceinline__ void tile_container_starts(uint32_t* s_cs, int64_t ti
     }
     if (__syncthreads_or(st >= tend)) break;  // doc_off is sorted: no later container starts inside
   }
+}
+__device__ __forceinline__ void tile_container_starts(uint32_t* s_cs, int64_t tile0, int64_t nbytes,
+                                                      const int64_t* __restrict__ doc_off, int64_t D,
+                                                      const int32_t* __restrict__ chunk_doc) {
+  tile_container_starts_t<TILE>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);
 }
 
 // container first bytes at q-1+j, j = 0..16, from the tile bitmap
@@ -1373,28 +1380,69 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
 
 // ---- log_index_match: line index AND DFA walk in ONE pass over the text (round 4) ------------
 // log_index_lines + log_dfa re-read the text: the DFA pass fetched it a second time (290 MB at the
-// DRAM-side counters for 184 MB of text, 2.3x the scan's algorithmic bytes).  Here a workgroup of
-// 1024 threads (one per CU: 150 KB of LDS) keeps its 64 KiB tile in LDS after the line-start pass
-// and walks the tile's lines there:
-//   A  each lane loads 4 pieces of 16 bytes (the tile's 64 KiB in flight at once), stores them to
-//      LDS and computes their line-start / separator-length bits (piece_flags); per 256-byte chunk
-//      counts, their scan inside the tile, the tile total published for the look-back (aggregate);
+// DRAM-side counters for 184 MB of text, the scan 2.3x its algorithmic bytes).  Here a workgroup
+// keeps its 32 KiB tile in LDS after the line-start pass and walks the tile's lines there.  Two
+// workgroups per CU (75 KB of LDS each: the tile, a 16-bit transition table, the line list), so one
+// can stream its tile in while the other walks (the walk is bound by LDS throughput, the load by
+// memory latency; one 1024-thread workgroup per CU with a 64 KiB tile ran the phases one after the
+// other: 262 us against 113 + 83 us for the two-kernel path, r4e):
+//   A  each lane loads 4 pieces of 16 bytes, stores them to LDS and computes their line-start /
+//      separator-length bits (piece_flags); per 256-byte chunk counts, their scan inside the tile,
+//      the tile total published for the look-back (aggregate);
 //   B  the tile's lines in windows of LMAX: a list of (start, end) tile offsets in LDS built from
-//      the start bits, then a lane per line walks it with the DFA from LDS (the 16-byte lockstep
-//      blocks of log_dfa, LDS words instead of buffer loads); masks in LDS;
+//      the start bits, then a lane per line walks it with the DFA from LDS (16-byte lockstep blocks
+//      as in log_dfa); masks in LDS;
 //   C  the look-back resolves the tile's first line id (its predecessors have long published their
 //      aggregates by then), and the window's line_start / line_end / line_mask go out coalesced by
 //      line id.
-// Deferred to log_dfa_long (a wave per line, as for long lines): the tile's LAST line, whose end
-// lies in a later tile, and lines longer than LONG_LINE; at most one straddler per tile.
-constexpr int FTPB = 1024;                          // threads of log_index_match
-constexpr int FNIT = (int)(TILE / (FTPB * PIECE));  // 4 pieces of 16 bytes per lane
-constexpr int LMAX = 4096;                          // lines of a tile listed and walked per window
+// Deferred: the tile's LAST line, whose end lies in a later tile (straddler queue -> log_dfa_strad,
+// a lane per line), and lines longer than LONG_LINE (long queue -> log_dfa_long, a wave per line).
+constexpr int64_t FTILE = 32768;                     // bytes per tile of log_index_match
+constexpr int FTPB = 512;                            // its threads
+constexpr int FNIT = (int)(FTILE / (FTPB * PIECE));  // 4 pieces of 16 bytes per lane
+constexpr int FCH = (int)(FTILE / CH);               // 128 chunks of 256 bytes per tile
+constexpr int FNBW = (int)(FTILE / 32) + 2;          // container-start bitmap words
+constexpr int LMAX = 2048;                           // lines of a tile listed and walked per window
 
-// The lines' DFA masks from the tile text in LDS: byte offsets [s, e) of the tile (e <= TILE - 1;
-// the text array is padded past TILE so a block may read up to 16 bytes beyond e).  Same
-// transitions as log_dfa: ASCII blocks by the byte table, others code point by code point.
-__device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx, const DfaLds4& d, int s, int e) {
+int64_t num_ftiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, FTILE)); }
+
+// 16-bit transition table (25 KB instead of DfaLds4's 50 KB): entry = the target state's row as a
+// byte offset (target * 64) | 0x8000 when the target reports a category; the category mask is read
+// from out[] only on those (rare) entries.  Row 31 of every state is the NOP column (identity) for
+// bytes outside the line, as in DfaLds4.
+constexpr int D2_RS = 32;
+struct DfaLds2 {
+  uint16_t trans[KRCA_DFA_NSTATE * D2_RS];
+  uint16_t out[KRCA_DFA_NSTATE];
+  uint8_t sym[256];  // byte -> symbol * 2 (bytes >= 0x80 and separators -> NOP)
+};
+static_assert(KRCA_DFA_NSTATE * D2_RS * 2 <= 0x8000, "row byte offsets must fit 15 bits");
+
+__device__ __forceinline__ void dfa2_load(DfaLds2& d) {
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * D2_RS; i += blockDim.x) {
+    const int st = i / D2_RS, c = i % D2_RS;
+    const uint32_t t = c < KRCA_DFA_NSYM ? krca_dfa_trans[st * KRCA_DFA_NSYM + c] : (uint32_t)st;
+    d.trans[i] = (uint16_t)((t * D2_RS * 2) | (krca_dfa_out[t] ? 0x8000u : 0u));
+  }
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE; i += blockDim.x) d.out[i] = (uint16_t)krca_dfa_out[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    const uint32_t sy = i < 128 ? krca_dfa_ascii_sym[i] : NOP_SYM;
+    d.sym[i] = (uint8_t)((sy == KRCA_DFA_SEP ? NOP_SYM : sy) * 2);  // no separator inside a line
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t dfa2_step(const DfaLds2& d, uint32_t row, uint32_t so, uint32_t& acc) {
+  const uint32_t t =
+      *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(d.trans) + ((row & 0x7FFFu) + so));
+  if (t & 0x8000u) acc |= d.out[(t & 0x7FFFu) >> 6];
+  return t;
+}
+
+// The DFA mask of the line at tile offsets [s, e) from the tile text in LDS (e < FTILE; the text
+// array is padded past the tile so a block may read up to 16 bytes beyond e).  Same transitions
+// as log_dfa: ASCII blocks by the byte table, others code point by code point.
+__device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx, const DfaLds2& d, int s, int e) {
   uint32_t row = 0, acc = 0;
   int off = s & ~3;  // this block's first byte (4-byte aligned)
   int rs_ = s & 3;   // s - off: 0..3 at the first block, then negative
@@ -1421,11 +1469,7 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
         for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
       }
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t t = dfa4_step(d, row, so[k]);
-        row = t;
-        acc |= t;
-      }
+      for (int k = 0; k < 16; ++k) row = dfa2_step(d, row, so[k], acc);
       ncp = 16;
     } else {  // code points, as the reference decodes them
 #pragma unroll 1
@@ -1466,11 +1510,9 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
               break;
             }
           }
-          sy *= 4;
+          sy *= 2;
         }
-        const uint32_t t = dfa4_step(d, row, sy);
-        row = t;
-        acc |= t;
+        row = dfa2_step(d, row, sy, acc);
         ncp = k + len;
       }
     }
@@ -1479,34 +1521,37 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
     re_ -= 16;
     ncp -= 16;
   }
-  return acc >> 16;
+  return acc;
 }
 
+// ntiles: FTILE tiles; tile_base / n_lines keep the TILE (64 KiB) tiles' bases that krca_log_match
+// reads (tile_base[T] = the first line of 32 KiB tile 2T), chunk counts / bases are per 256-byte
+// chunk as before
 __global__ __launch_bounds__(FTPB) void log_index_match(
     const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off, int64_t D,
     const int32_t* __restrict__ chunk_doc, int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_base,
-    unsigned long long* __restrict__ status, unsigned int* __restrict__ ticket, int64_t ntiles, int64_t cap,
-    int64_t* __restrict__ line_start, int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
+    int64_t nt64, unsigned long long* __restrict__ status, unsigned int* __restrict__ ticket, int64_t ntiles,
+    int64_t cap, int64_t* __restrict__ line_start, int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
     int64_t* __restrict__ chunk_line0, int64_t* __restrict__ n_lines, int32_t* __restrict__ long_q,
-    int32_t* __restrict__ n_long) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_text[TILE / 4 + 8];  // the tile + 32 zero bytes
-  __shared__ DfaLds4 d;
-  __shared__ uint32_t s_cs[NBW];
+    int32_t* __restrict__ n_long, int32_t* __restrict__ strad_q, int32_t* __restrict__ n_strad) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_text[FTILE / 4 + 8];  // the tile + 32 zero bytes
+  __shared__ DfaLds2 d;
+  __shared__ uint32_t s_cs[FNBW];
   __shared__ uint16_t s_ls[LMAX], s_le[LMAX], s_lm[LMAX];
-  __shared__ int32_t s_cnt[TPB], s_cb[TPB];  // per 256-byte chunk: line starts, exclusive base in the tile
-  __shared__ int32_t s_wsum[TPB / 64];
+  __shared__ int32_t s_cnt[FCH], s_cb[FCH];  // per 256-byte chunk: line starts, exclusive base in the tile
+  __shared__ int32_t s_wsum[FCH / 64];
   __shared__ int32_t s_prev_end;  // tile offset where the previous tile's last line ends (from line 0)
   __shared__ int64_t s_tile, s_excl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  dfa4_load(d);  // once per workgroup (persistent)
-  if (tid < 8) s_text[TILE / 4 + tid] = 0u;
+  dfa2_load(d);  // once per workgroup (persistent)
+  if (tid < 8) s_text[FTILE / 4 + tid] = 0u;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   for (;;) {
     if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
     const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
     if (tile >= ntiles) return;  // uniform
-    const int64_t tile0 = tile * TILE;
+    const int64_t tile0 = tile * FTILE;
     // ---- A: text -> LDS, line-start bits, chunk counts -----------------------------------------
     const int64_t qlast = (nbytes - 1) & ~(int64_t)(PIECE - 1);
     u32x4 raw[FNIT];
@@ -1518,7 +1563,7 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
       const int64_t q0 = tile0 + ((int64_t)it * FTPB + (int64_t)__builtin_amdgcn_readfirstlane(wid) * 64) * PIECE;
       pw[it] = q0 >= 4 && q0 <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q0 - 4) : 0u;
     }
-    tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order s_cnt reuse)
+    tile_container_starts_t<FTILE>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order LDS reuse)
     uint32_t regS[FNIT], regL1[FNIT];  // per piece: starts | odd lengths << 16; lengths 2/3
 #pragma unroll
     for (int it = 0; it < FNIT; ++it) {
@@ -1546,9 +1591,9 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
       if ((tid & (LANES_PER_CHUNK - 1)) == 0) s_cnt[pc / LANES_PER_CHUNK] = (int32_t)c;
     }
     __syncthreads();
-    if (tid < TPB) {  // chunk counts -> exclusive bases inside the tile
+    if (tid < FCH) {  // chunk counts -> exclusive bases inside the tile
       const int32_t v = s_cnt[tid];
-      chunk_cnt[tile * TPB + tid] = v;
+      chunk_cnt[tile * FCH + tid] = v;
       int32_t x = v;
       for (int off = 1; off < 64; off <<= 1) {
         const int32_t y = __shfl_up(x, off, 64);
@@ -1558,8 +1603,10 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
       s_cb[tid] = x - v;
     }
     __syncthreads();
-    const int total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-    if (tid < TPB) {
+    int total = 0;
+#pragma unroll
+    for (int u = 0; u < FCH / 64; ++u) total += s_wsum[u];
+    if (tid < FCH) {
       int32_t before = 0;
       for (int u = 0; u < wid; ++u) before += s_wsum[u];
       s_cb[tid] += before;
@@ -1585,7 +1632,7 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
           if ((lane & (LANES_PER_CHUNK - 1)) >= off) xs += y;
         }
         int id = s_cb[pc / LANES_PER_CHUNK] + (int)(xs - n);
-        if (id > hi || id + (int)n < lo) continue;  // no start of this piece touches the window
+        if (id > hi || id + (int)n <= lo) continue;  // none of this piece's starts touches the window
         uint32_t rem = S;
         const uint32_t l0 = regS[it] >> 16, l1 = regL1[it];
         while (rem) {
@@ -1630,11 +1677,11 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
         }
         if (lane == 0) {
           s_excl = excl;
-          tile_base[tile] = excl;
+          if ((tile & 1) == 0) tile_base[tile >> 1] = excl;  // the 64 KiB tiles' bases (krca_log_match)
           if (total > 0 && excl >= 1 && excl - 1 < cap) line_end[excl - 1] = tile0 + s_prev_end;
           if (tile == ntiles - 1) {
             const int64_t nl = excl + total;
-            tile_base[ntiles] = nl;
+            tile_base[nt64] = nl;
             *n_lines = nl;
             if (nl >= 1 && nl <= cap && nbytes > 0) line_end[nl - 1] = last_line_end(text, nbytes, doc_off, D);
           }
@@ -1642,15 +1689,23 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
       }
       __syncthreads();
       const int64_t excl = s_excl;
-      if (win == 0 && tid < TPB) chunk_line0[tile * TPB + tid] = excl + s_cb[tid];
+      if (win == 0 && tid < FCH) chunk_line0[tile * FCH + tid] = excl + s_cb[tid];
+      if (win == 0 && tile == ntiles - 1)  // an odd tile count: the last 64 KiB tile's missing half has no
+        for (int64_t c = ntiles * FCH + tid; c < nt64 * TPB; c += FTPB) {  // line starts (log_hist and
+          chunk_cnt[c] = 0;                                                 // log_lines read its chunks)
+          chunk_line0[c] = excl + total;
+        }
       for (int j = tid; j < hi - lo; j += FTPB) {  // coalesced by line id
         const int64_t id = excl + lo + j;
         if (id >= cap) continue;
         const int ls = s_ls[j];
         line_start[id] = tile0 + ls;
-        const bool last = lo + j == total - 1;
-        if (!last) line_end[id] = tile0 + s_le[j];
-        if (last || s_le[j] - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;  // log_dfa_long
+        if (lo + j == total - 1) {  // its end is in a later tile: log_dfa_strad, or log_dfa_long
+          strad_q[atomicAdd(n_strad, 1)] = (int32_t)id;
+          continue;
+        }
+        line_end[id] = tile0 + s_le[j];
+        if (s_le[j] - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;
         else line_mask[id] = s_lm[j];
       }
       __syncthreads();  // the window's lists (and, after the last, the tile's LDS) are rewritten next
@@ -1658,10 +1713,51 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
   }
 }
 
+// the tiles' last lines (one per tile of log_index_match): a lane per line, code point by code
+// point from global memory (a few thousand lines per scan); one longer than LONG_LINE goes on to
+// log_dfa_long's queue (launched after this kernel)
+__global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                     const int64_t* __restrict__ line_start,
+                                                     const int64_t* __restrict__ line_end,
+                                                     uint32_t* __restrict__ line_mask, const int32_t* __restrict__ q,
+                                                     const int32_t* __restrict__ nq, int32_t* __restrict__ long_q,
+                                                     int32_t* __restrict__ n_long) {
+  __shared__ DfaLds dfa;
+  const int n = *nq;
+  if ((int64_t)blockIdx.x * TPB >= n) return;  // uniform: no line for this block, skip the table fill
+  dfa_load(dfa);
+  for (int i = blockIdx.x * TPB + threadIdx.x; i < n; i += gridDim.x * TPB) {
+    const int64_t l = q[i];
+    const int64_t s = line_start[l], e = line_end[l];
+    if (e - s > LONG_LINE) {
+      long_q[atomicAdd(n_long, 1)] = (int32_t)l;
+      continue;
+    }
+    Bytes B;
+    B.init(text, nbytes);
+    uint32_t row = 0, mask = 0;
+    for (int64_t p = s; p < e;) {
+      uint32_t cp;
+      const int len = decode(B, p, cp);
+      const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
+      row = t & (kAcc - 1);
+      if (t & kAcc) mask |= dfa.out[row / KRCA_DFA_NSYM];
+      p += len;
+    }
+    line_mask[l] = mask;
+  }
+}
+
 int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, TILE)); }
-// int64 words of the int32 long-line queue: lines longer than LONG_LINE, plus one straddling line
-// per tile (log_index_match defers each tile's last line)
-int64_t long_q_words(int64_t nbytes) { return krca::ceil_div(nbytes / LONG_LINE + 1 + num_tiles(nbytes), 2); }
+// int64 words of the int32 long-line queue (lines longer than LONG_LINE)
+int64_t long_q_words(int64_t nbytes) { return krca::ceil_div(nbytes / LONG_LINE + 1, 2); }
+// krca_log_scan's tail of the workspace (int64 words): look-back status words for the 2 x num_tiles
+// 32 KiB tiles of log_index_match (num_tiles of log_index_lines use the first half), the tile
+// ticket, the straddler count, the int32 straddler queue (one line per 32 KiB tile)
+int64_t scan_tail_words(int64_t nbytes) {
+  const int64_t nt = num_tiles(nbytes);
+  return 2 * nt + 2 + krca::ceil_div(2 * nt + 1, 2);
+}
 
 }  // namespace
 
@@ -1677,7 +1773,7 @@ uint64_t krca_log_dfa_digest(void) { return KRCA_DFA_DIGEST; }
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
   return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + long_q_words(nbytes) +
-         nt + 1;  // + krca_log_scan's look-back status words and tile ticket
+         scan_tail_words(nbytes);  // + krca_log_scan's look-back status words, ticket, straddler queue
 }
 
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
@@ -1774,24 +1870,31 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   int32_t* long_q = reinterpret_cast<int32_t*>(chunk_line0 + nt * TPB + 1);
   unsigned long long* status =
       reinterpret_cast<unsigned long long*>(chunk_line0 + nt * TPB + 1 + long_q_words(nbytes));
-  unsigned int* ticket = reinterpret_cast<unsigned int*>(status + nt);
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(status + 2 * nt);
+  int32_t* n_strad = reinterpret_cast<int32_t*>(status + 2 * nt + 1);
+  int32_t* strad_q = reinterpret_cast<int32_t*>(status + 2 * nt + 2);
   hipStream_t st = krca::as_stream(stream);
   // one launch before the index: the chunk -> container map (every chunk of the text is written
   // under the doc_off contract; off it, tile_container_starts clamps what it reads), and the zeroed
   // look-back status words + ticket and long-line count (no memset launches: each dependent
   // launch costs ~10 us at the front of the scan)
   hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
-                     nbytes, cdoc, status, nt + 1, n_long);
+                     nbytes, cdoc, status, 2 * nt + 2, n_long);  // status words, ticket, straddler count
   KRCA_LAUNCH_CHECK();
   const int64_t* Ld = tile + nt;  // the line count, on the device (written by the index's last tile)
   if (krca::tuning().log_fused) {
-    // the line index and the DFA walk in one pass over the text (one 1024-thread workgroup per CU;
-    // the tiles' last lines and long lines are walked by log_dfa_long below)
+    // the line index and the DFA walk in one pass over the text (two 512-thread workgroups per CU,
+    // 32 KiB tiles); the tiles' last lines go to log_dfa_strad, long lines to log_dfa_long
+    const int64_t ntf = num_ftiles(nbytes);
     const int64_t resident =
-        krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_match), FTPB, st, 1);
-    hipLaunchKernelGGL(log_index_match, dim3((unsigned)std::min<int64_t>(nt, resident)), dim3(FTPB), 0, st, text,
-                       nbytes, doc_off, ndocs, (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap,
-                       line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long);
+        krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_match), FTPB, st, 2);
+    hipLaunchKernelGGL(log_index_match, dim3((unsigned)std::min<int64_t>(ntf, resident)), dim3(FTPB), 0, st, text,
+                       nbytes, doc_off, ndocs, (const int32_t*)cdoc, chunk, tile, nt, status, ticket, ntf, line_cap,
+                       line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long, strad_q, n_strad);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(log_dfa_strad, dim3((unsigned)krca::ceil_div(ntf, TPB)), dim3(TPB), 0, st, text, nbytes,
+                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, (const int32_t*)strad_q,
+                       (const int32_t*)n_strad, long_q, n_long);
     KRCA_LAUNCH_CHECK();
   } else {  // A/B (KRCA_LOG_FUSED=0): the round-3 line index, then a DFA lane per line re-reading the text
     // workgroups the stream's device keeps resident (occupancy API, cached per device)

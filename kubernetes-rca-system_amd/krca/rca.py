@@ -55,10 +55,100 @@ def shard_range(N, world, rank):
     return lo, hi, n_max
 
 
-def shard_graph(row_ptr, col, outdeg, lo, hi):
-    """Rows [lo, hi) of a pull-CSR (column ids stay global)."""
+# Partition.balanced: a rank may hold up to EDGE_SLACK x the mean in-edges per rank before its
+# edges, not its pods, bound it.  A rank's step is its scoring (pods) overlapped with the PageRank
+# solve, whose iterations all wait for the rank with the most edges; the scoring is the larger part
+# (C4: 7.1 ms of scoring against ~1 ms of PageRank on one GPU), so the pods stay balanced and the
+# edges are only capped
+EDGE_SLACK = 2.0
+
+
+class Partition:
+    """Contiguous pod ranges of G ranks: rank g owns pods [bounds[g], bounds[g+1]) -- their metric
+    series, their rows of the pull-CSR -- and its exchange slice holds n_slot = max range weight
+    codes.  A column j owned by rank g is addressed by its VIRTUAL id g * n_slot + (j - bounds[g]),
+    so the device's remap (j + (j / n_max) * (2 * slice - n_max), csrc/ppr_layout.h) with n_max =
+    n_slot lands every code in its owner's slice; for uniform ranges of n_slot pods the virtual id
+    is the pod id itself.
+
+    uniform(N, G): ranges of ceil(N / G) pods (shard_range).  balanced(row_ptr, G): ranges of at most
+    t x N / G pods and t x EDGE_SLACK x E / G in-edges, t as small as covers the mesh.  The
+    synthetic mesh wires services by preferential
+    attachment, so the heavily called services sit at low pod ids: with uniform ranges rank 0 of 8
+    holds 10.6M of the C4 mesh's 20M edges and its PageRank step takes 25 us against ~4 for the
+    others (tools/ppr_g8_emulation.py, profiles/r4/ppr_g8_emulation.json), and every iteration's
+    all-gather waits for it."""
+
+    def __init__(self, bounds):
+        b = np.asarray(bounds, np.int64)
+        if b.ndim != 1 or len(b) < 2 or b[0] != 0 or np.any(np.diff(b) < 0):
+            raise ValueError(f"partition bounds must rise from 0: {b[:8]}")
+        self.bounds, self.world, self.N = b, len(b) - 1, int(b[-1])
+        self.n_slot = max(1, int(np.max(np.diff(b))))
+
+    @classmethod
+    def uniform(cls, N, world):
+        n_max = max(1, math.ceil(N / world))
+        return cls([min(N, g * n_max) for g in range(world)] + [N])
+
+    @classmethod
+    def balanced(cls, row_ptr, world, edge_slack=EDGE_SLACK):
+        """The smallest t for which G contiguous ranges of <= t * N / G pods and <= t * edge_slack *
+        E / G in-edges each cover the mesh (bisection on t, greedy longest ranges), and those ranges."""
+        rp = np.asarray(row_ptr, np.int64)
+        N, E = len(rp) - 1, int(rp[-1])
+        if world == 1 or N == 0:
+            return cls([0] + [N] * world)
+        pods_cap, edges_cap = N / world, edge_slack * max(E, 1) / world
+
+        def cover(t):
+            b, pos = [0], 0
+            for _ in range(world):
+                hi = min(N, pos + max(1, int(t * pods_cap)))
+                # the longest range from pos whose in-edges stay within the cap (at least one pod)
+                hi = max(pos + 1, min(hi, int(np.searchsorted(rp, rp[pos] + t * edges_cap, side="right")) - 1))
+                pos = min(N, hi)
+                b.append(pos)
+            return b
+        lo_t, hi_t = 1.0, float(world)
+        for _ in range(50):
+            mid = 0.5 * (lo_t + hi_t)
+            if cover(mid)[-1] >= N:
+                hi_t = mid
+            else:
+                lo_t = mid
+        b = cover(hi_t)
+        b[-1] = N
+        return cls(b)
+
+    def range(self, rank):
+        """(lo, hi, n_slot) of `rank` (shard_range's triple)."""
+        return int(self.bounds[rank]), int(self.bounds[rank + 1]), self.n_slot
+
+    def owner(self, j):
+        return np.clip(np.searchsorted(self.bounds, np.asarray(j, np.int64), side="right") - 1, 0, self.world - 1)
+
+    def virtual(self, col):
+        """Global pod ids -> the exchange layout's virtual ids (int32 when they fit)."""
+        c = np.asarray(col, np.int64)
+        g = self.owner(c)
+        v = g * self.n_slot + (c - self.bounds[g])
+        return v.astype(np.int32) if self.world * self.n_slot < 2 ** 31 else v
+
+    def unpad(self, flat):
+        """world * n_slot per-rank padded rows (gather order) -> the N rows in pod order."""
+        a = np.asarray(flat)
+        return np.concatenate([a[g * self.n_slot:g * self.n_slot + int(self.bounds[g + 1] - self.bounds[g])]
+                               for g in range(self.world)])
+
+
+def shard_graph(row_ptr, col, outdeg, lo, hi, part=None):
+    """Rows [lo, hi) of a pull-CSR.  Column ids stay global, or become `part`'s virtual ids (the
+    exchange layout of a Partition whose ranges are not all n_slot long)."""
     rp = np.asarray(row_ptr[lo:hi + 1], np.int64) - int(row_ptr[lo])
     c = np.asarray(col[int(row_ptr[lo]):int(row_ptr[hi])], np.int32)
+    if part is not None:
+        c = part.virtual(c)
     return rp, c, np.asarray(outdeg[lo:hi], np.int32)
 
 
@@ -188,7 +278,8 @@ class DeviceShard:
         self.n = int(outdeg_local.shape[0])
         # plan + packed columns (remapped to the exchange layout, dictionary blocks where they pay)
         self.plan, self.plan_len, self.col, self.lane, self.n_dict = (
-            engine.ppr_pack(row_ptr_local, col_local, n_max, n_total=N) if self.n else (None, 0, None, None, 0))
+            engine.ppr_pack(row_ptr_local, col_local, n_max, n_total=max(N, world * n_max)) if self.n
+            else (None, 0, None, None, 0))
         self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr_local)).to(dev)
         self.outdeg = torch.from_numpy(np.ascontiguousarray(outdeg_local)).to(dev)
         i64 = dict(dtype=torch.int64, device=dev)

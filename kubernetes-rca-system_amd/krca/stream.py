@@ -30,17 +30,18 @@ import json
 
 import numpy as np
 
-from .rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
+from .rca import Comm, Config, DeviceShard, Partition, RcaStep, shard_graph
 
 SNAPSHOT_VERSION = 1
 
 
 class StreamingRCA:
     def __init__(self, engine, row_ptr, col, outdeg, n_metrics, cfg=None, horizon=1440, tol=1e-9, max_iter=100,
-                 check_every=4, comm=None, shard=None):
+                 check_every=4, comm=None, shard=None, partition=None):
         """row_ptr / col / outdeg: the whole mesh's pull-CSR (host arrays); this rank keeps its rows.
         comm: krca.rca.Comm (world, rank) — default one rank.  shard: a prepared per-rank backend
-        (tests); default DeviceShard on `engine`."""
+        (tests); default DeviceShard on `engine`.  partition: a krca.rca.Partition, or "balanced"
+        (pods + in-edges balanced ranges); default uniform ranges of ceil(N / G) pods."""
         self.eng = engine
         self.cfg = cfg or Config()
         self.comm = comm or Comm()
@@ -48,9 +49,12 @@ class StreamingRCA:
         self.M = int(n_metrics)
         self.H = int(horizon)
         self.tol, self.max_iter, self.check_every = float(tol), int(max_iter), int(check_every)
-        self.lo, self.hi, self.n_max = shard_range(self.N, self.comm.world, self.comm.rank)
+        if partition == "balanced":
+            partition = Partition.balanced(row_ptr, self.comm.world)
+        self.part = partition or Partition.uniform(self.N, self.comm.world)
+        self.lo, self.hi, self.n_max = self.part.range(self.comm.rank)
         if shard is None:
-            rp, c, od = shard_graph(row_ptr, col, outdeg, self.lo, self.hi)
+            rp, c, od = shard_graph(row_ptr, col, outdeg, self.lo, self.hi, self.part)
             shard = DeviceShard(engine, None, rp, c, od, self.N, self.n_max, self.comm.world, self.cfg)
         self.shard = shard
         self.rca = RcaStep(self.shard, self.comm, self.cfg, self.lo)

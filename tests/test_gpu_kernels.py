@@ -282,16 +282,30 @@ def test_log_scan_fused_walk_identical(eng):
     docs += ["".join(rng.choice(["Error ", "\r\n", "é", "\x85", "panic:", "v" * 200, " "]) for _ in range(30))
              for _ in range(300)]
     docs.append("tail Error é")                        # the text ends mid-piece
+    nb = sum(len(d.encode()) for d in docs)
+    if (nb + 32767) // 32768 % 2 == 0:  # an odd number of 32 KiB tiles: the last 64 KiB tile is half-covered
+        docs.append("f" * 32768 + " ERROR")
     blob, off = pack_documents(docs)
+    assert (len(blob) + 32767) // 32768 % 2 == 1
     tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
+    nws = 8 * int(eng.lib.krca_log_index_size(len(blob)))
     out = {}
-    for fused in (1, 0):
-        with native.tune(eng.lib, KRCA_LOG_FUSED=fused):
-            r = eng.log_scan_device(tb, toff)
-            out[fused] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
-    assert out[1].keys() == out[0].keys()
-    for k in out[0]:
-        assert np.array_equal(out[1][k], out[0][k]), k
+    # the fused pass with line arrays that hold every line, the fallback (krca_log_match after a
+    # krca_log_scan into too small arrays: a fresh engine), and the round-3 path; the workspace is
+    # filled with garbage before each call (what the scan leaves unwritten must not be read)
+    for name, fused, fresh in (("fused", 1, False), ("fallback", 1, True), ("unfused", 0, False)):
+        e = native.NativeEngine() if fresh else eng
+        e._workspace("logidx", nws).fill_(0x5B)
+        with native.tune(e.lib, KRCA_LOG_FUSED=fused):
+            if not fresh:
+                e.log_scan_device(tb, toff)  # sizes the engine's line arrays
+                e._workspace("logidx", nws).fill_(0x5B)
+            r = e.log_scan_device(tb, toff)
+            out[name] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
+    for name in ("fallback", "unfused"):
+        assert out["fused"].keys() == out[name].keys()
+        for k in out["fused"]:
+            assert np.array_equal(out["fused"][k], out[name][k]), (name, k)
     _check_docs(eng, docs)
 
 

@@ -33,18 +33,19 @@ def _mesh():
     return m, x
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, out_q, balanced=False):
     sys.path[:0] = [os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"),
                     os.path.join(ROOT, "tests")]
     import torch.distributed as dist
-    from krca.rca import Comm, Config, RcaStep, shard_graph, shard_range
+    from krca.rca import Comm, Config, Partition, RcaStep, shard_graph
     from numpy_shard import NumpyShard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m, x = _mesh()
     cfg = Config(iters=12)
-    lo, hi, n_max = shard_range(N, world, rank)
-    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
+    part = Partition.balanced(m.row_ptr, world) if balanced else Partition.uniform(N, world)
+    lo, hi, n_max = part.range(rank)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi, part)
     shard = NumpyShard(x[:, lo:hi, :], rp, col, od, N, n_max, world, cfg)
     idx, key = RcaStep(shard, Comm(world, rank), cfg, lo).run()
     out_q.put((rank, lo, shard.r.copy(), [int(i) for i in idx], [int(k) for k in key]))
@@ -52,14 +53,16 @@ def _worker(rank, world, port, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_rca_matches_single_process_oracle(world):
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, False), (2, True), (4, True)])
+def test_sharded_rca_matches_single_process_oracle(world, balanced):
+    """Uniform ranges and pods + in-edges balanced ranges (krca.rca.Partition: ranges of different
+    lengths, columns in the exchange layout's virtual ids): the same bits either way."""
     import oracle
     from krca.rca import Config
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, balanced)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -124,3 +127,35 @@ def test_all_gather_flat_moves_dtypes_the_backends_lack():
     for dt in (torch.int16, torch.float16, torch.int64, torch.float32):
         want = torch.cat([(torch.arange(6) + 100 * r).to(dt) for r in range(world)]).tolist()
         assert res[0][str(dt)] == want and res[1][str(dt)] == want
+
+
+def test_partition_balanced_ranges():
+    """Partition.balanced: contiguous ranges covering [0, N); no range past t x N / G pods or
+    t x EDGE_SLACK x E / G in-edges (t from the bisection, within 10 % of the uniform ranges' pod
+    balance on this mesh); virtual ids land in the owner's slice; unpad inverts the gather."""
+    from krca import synth
+    from krca.rca import EDGE_SLACK, Partition, remap_cols, slice_words
+    m = synth.make_graph(20000, avg_degree=20, seed=2)
+    E = int(m.row_ptr[-1])
+    for world in (1, 2, 3, 8):
+        p = Partition.balanced(m.row_ptr, world)
+        b = p.bounds
+        assert b[0] == 0 and b[-1] == 20000 and np.all(np.diff(b) >= 0) and p.world == world
+        edges = np.diff(m.row_ptr[b])
+        t = max(np.max(np.diff(b)) / (20000 / world), np.max(edges) / (EDGE_SLACK * E / world))
+        assert t < 1.5, (world, t)
+        j = np.arange(20000)
+        g = p.owner(j)
+        assert np.all((b[g] <= j) & (j < b[g + 1]))
+        v = p.virtual(j).astype(np.int64)
+        u = remap_cols(v, p.n_slot)  # uint32 index of the code in w_all[world][slice]
+        assert np.array_equal(u // (2 * slice_words(p.n_slot)), g)
+        assert np.array_equal(u % (2 * slice_words(p.n_slot)), j - b[g])
+        padded = np.full(world * p.n_slot, -1)
+        for r in range(world):
+            padded[r * p.n_slot:r * p.n_slot + b[r + 1] - b[r]] = np.arange(b[r], b[r + 1])
+        assert np.array_equal(p.unpad(padded), j)
+    u = Partition.uniform(20000, 3)
+    assert np.array_equal(u.virtual(np.arange(20000)), np.arange(20000))
+    hub = Partition.balanced(m.row_ptr, 8)  # the hub services at low ids: a short first range
+    assert hub.bounds[1] < 20000 // 8 and np.max(np.diff(m.row_ptr[hub.bounds])) <= 1.5 * EDGE_SLACK * E / 8

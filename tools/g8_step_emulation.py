@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""One rank's pipelined RCA step at G = 8, emulated on one GPU: which pod partition keeps the
+PageRank solve from bounding the step (krca.rca.Partition).
+
+bench.py's step on rank g of G: the scoring of its pods (krca_rolling_score) on one HIP stream
+while the previous step's PageRank (init, 30 folded steps, each followed by the exchange, finish,
+key, top-k) runs on the other; every PageRank iteration waits for the all-gather, i.e. for the rank
+with the most edges.  Here the rank with the most PageRank work under each partition runs exactly
+that two-stream pipeline on its own shard (its metric rows generated as bench.py generates them),
+with a device copy of its send slice standing in for the all-gather (RCCL's own latency is not
+included: it adds the same per-iteration time under either partition).  Reports ms per step for
+the uniform ranges (ceil(N / G) pods) and for Partition.balanced, plus each one's scoring and
+PageRank parts run alone.  Prints one JSON line.
+
+  python tools/g8_step_emulation.py [--pods 1000000] [--edges 20000000] [--world 8] [--steps 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
+
+
+class CopyComm:
+    """Comm stand-in: the exchange lands this rank's send slice in its own slot of w_all."""
+
+    def __init__(self, world, rank, sw):
+        self.world, self.rank, self.sw = world, rank, sw
+
+    def exchange(self, shard):
+        shard.w_all[self.rank * self.sw:(self.rank + 1) * self.sw].copy_(shard.send)
+
+
+def run_rank(a, m, hops, cfg, part, g, M, T):
+    """bench.py's two-stream pipeline on rank g's shard: ms per step, and its two parts alone."""
+    import torch
+    from krca import native, synth
+    from krca.rca import DeviceShard, RcaStep, shard_graph, slice_words
+    G = part.world
+    lo, hi, n_slot = part.range(g)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi, part)
+    x = synth.make_metrics_range(lo, hi, M, T, seed=0, roots=m.roots, hop_sets=hops, device="cuda")
+    engs = [native.NativeEngine(0) for _ in range(2)]
+    shards = [DeviceShard(e, x, rp, col, od, a.pods, n_slot, G, cfg) for e in engs]
+    comm = CopyComm(G, g, slice_words(n_slot))
+    steps = [RcaStep(sh, comm, cfg, lo) for sh in shards]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    done = [None]
+
+    def enqueue(i):
+        j = i % 2
+        with torch.cuda.stream(streams[j]):
+            if done[0] is not None:
+                streams[j].wait_event(done[0])
+            shards[j].score()
+            done[0] = torch.cuda.Event()
+            done[0].record()
+            steps[j].propagate()
+            shards[j].local_topk(cfg.k)
+
+    for i in range(4):
+        enqueue(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        enqueue(i)
+    torch.cuda.synchronize()
+    pipe_ms = (time.perf_counter() - t0) / a.steps * 1e3
+    parts = {}
+    for name, fn in (("scoring", shards[0].score), ("pagerank", steps[0].propagate)):
+        ev = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ev.append(e0.elapsed_time(e1))
+        parts[name] = float(np.median(ev))
+    res = dict(pods=hi - lo, edges=int(m.row_ptr[hi] - m.row_ptr[lo]), pipelined_ms_per_step=pipe_ms,
+               scoring_ms_alone=parts["scoring"], pagerank_ms_alone=parts["pagerank"])
+    del x, shards, steps, engs
+    torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pods", type=int, default=1_000_000)
+    ap.add_argument("--edges", type=int, default=20_000_000)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    from krca import synth
+    from krca.rca import RANKING, Partition
+    M, T = 8, 1440
+    m = synth.make_graph(a.pods, n_edges=a.edges, seed=0)
+    hops = synth.caller_hops(m, m.roots)
+    cfg = RANKING.replace(seed_floor=RANKING.floor(a.pods, M))
+    G = a.world
+    out = dict(what=f"one rank's pipelined step at G={G} on one GPU (device copy for the all-gather)",
+               pods=a.pods, edges=m.n_edges, steps=a.steps)
+    for pname, part in (("uniform", Partition.uniform(a.pods, G)), ("balanced", Partition.balanced(m.row_ptr, G))):
+        edges = np.diff(m.row_ptr[part.bounds])
+        pods = np.diff(part.bounds)
+        res = {}
+        # the rank with the most edges (every PageRank iteration waits for it) and the one with the
+        # most pods (the longest scoring): the job's step is at least the slower of the two
+        for g in sorted({int(np.argmax(edges)), int(np.argmax(pods))}):
+            res[f"rank{g}"] = run_rank(a, m, hops, cfg, part, g, M, T)
+        out[pname] = dict(bounds=[int(b) for b in part.bounds], ranks=res,
+                          step_ms_bound=max(r["pipelined_ms_per_step"] for r in res.values()))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,7 +22,7 @@ for t in cal ppr bench logs; do
   case $t in
     cal) cmd=(tools/bin/pmc_calib) ;;
     ppr) cmd=(python3 tools/ppr_bench.py --reps 2) ;;
-    bench) cmd=(python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-pipeline) ;;
+    bench) cmd=(python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-pipeline --no-corr) ;;
     logs) cmd=(python3 tools/prof_kernels.py logs --docs 1000000 --reps 1) ;;
   esac
   pass ${t}_rd TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum -- "${cmd[@]}"

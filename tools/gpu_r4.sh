@@ -39,11 +39,14 @@ for s in "$@"; do
     probe) step probe 60 tools/bin/buffer_range_probe ;;
     tests_new) step tests_new 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "empty_rank or cold_solve_fresh or bench_gpus" ;;
     bench_n2) step bench_n2 600 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 5 --warmup 2 ;;
+    tests_logs) step tests_logs 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread -k "log_scan or c2mini or c5 or stream or logs" ;;
+    logs_unfused) export KRCA_LOG_FUSED=0; prof logs_unfused 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread ;;
     tests_corr) step tests_corr 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread ;;
     bench) step bench 300 python3 bench.py ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_trace) prof bench_trace 400 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench_trace_full) prof bench_trace_full 700 bench.py ;;
     corr100k) prof corr100k 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5 ;;
     corr100k_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#corr100k_}.so; prof $s 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5; unset KRCA_LIB ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 --tau 0.5 ;;
@@ -52,8 +55,13 @@ for s in "$@"; do
         export KRCA_CORR_BATCH=$b; step corr_batch$b 300 python3 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5
       done; unset KRCA_CORR_BATCH ;;
     ranking) step ranking 600 python3 -u tools/ranking_ablation_c4.py --seeds 2 --out $O/ranking_ablation_c4.json ;;
+    ranking_spread) step ranking_spread 900 python3 -u tools/ranking_ablation_c4.py --seeds 2 --spread --out $O/ranking_ablation_spread_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
     ppr_g8) step ppr_g8 300 python3 tools/ppr_g8_emulation.py ;;
+    repeat_window) step repeat_window 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 ;;
+    repeat_window_unfused) step repeat_window_unfused 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 KRCA_LOG_FUSED=0 ;;
+    diag_window) step diag_window 300 python3 -u tools/diag_window_templates.py ;;
+    g8_step) step g8_step 400 python3 tools/g8_step_emulation.py ;;
     ppr_head)  # the same profile with the committed tree's code (ab_head/: git archive HEAD, built in place)
       step ppr_head 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ppr_head -o run -- python3 ab_head/tools/prof_kernels.py ppr --reps 5 ;;
     ppr_bytes) step ppr_bytes 300 python3 tools/ppr_bench.py --reps 5 ;;
