@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "krca_common.h"
 #define KRCA_DFA_QUAL static __device__ __constant__ const
@@ -1397,14 +1398,23 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
 //      line id.
 // Deferred: the tile's LAST line, whose end lies in a later tile (straddler queue -> log_dfa_strad,
 // a lane per line), and lines longer than LONG_LINE (long queue -> log_dfa_long, a wave per line).
-constexpr int64_t FTILE = 32768;                     // bytes per tile of log_index_match
-constexpr int FTPB = 512;                            // its threads
-constexpr int FNIT = (int)(FTILE / (FTPB * PIECE));  // 4 pieces of 16 bytes per lane
-constexpr int FCH = (int)(FTILE / CH);               // 128 chunks of 256 bytes per tile
-constexpr int FNBW = (int)(FTILE / 32) + 2;          // container-start bitmap words
-constexpr int LMAX = 2048;                           // lines of a tile listed and walked per window
+// Two shapes (KRCA_LOG_FUSED = 1 / 2): 32 KiB tiles, 512 threads, the 16-bit table -- two
+// workgroups per CU; or 64 KiB tiles, 1024 threads, DfaLds4's 32-bit table (the category mask in
+// every entry: no branch per byte) -- one workgroup per CU, 16 waves.
+template <int64_t TILE_B, int NT, bool U32>
+struct FCfg {
+  static constexpr int64_t FTILE = TILE_B;                    // bytes per tile
+  static constexpr int FTPB = NT;                             // threads
+  static constexpr int FNIT = (int)(TILE_B / (NT * PIECE));   // 4 pieces of 16 bytes per lane
+  static constexpr int FCH = (int)(TILE_B / CH);              // 256-byte chunks per tile
+  static constexpr int FNBW = (int)(TILE_B / 32) + 2;         // container-start bitmap words
+  static constexpr int LMAX = (int)(TILE_B / 16);             // lines of a tile listed and walked per window
+  static constexpr bool W32 = U32;
+};
+using FSmall = FCfg<32768, 512, false>;
+using FBig = FCfg<65536, 1024, true>;
 
-int64_t num_ftiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, FTILE)); }
+int64_t num_ftiles(int64_t nbytes, int64_t tile_b) { return std::max<int64_t>(1, krca::ceil_div(nbytes, tile_b)); }
 
 // 16-bit transition table (25 KB instead of DfaLds4's 50 KB): entry = the target state's row as a
 // byte offset (target * 64) | 0x8000 when the target reports a category; the category mask is read
@@ -1442,7 +1452,25 @@ __device__ __forceinline__ uint32_t dfa2_step(const DfaLds2& d, uint32_t row, ui
 // The DFA mask of the line at tile offsets [s, e) from the tile text in LDS (e < FTILE; the text
 // array is padded past the tile so a block may read up to 16 bytes beyond e).  Same transitions
 // as log_dfa: ASCII blocks by the byte table, others code point by code point.
-__device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx, const DfaLds2& d, int s, int e) {
+// one byte step of either table: the 32-bit one ORs its entry (mask in the high half), the 16-bit
+// one reads out[] on a reporting entry
+__device__ __forceinline__ uint32_t dstep(const DfaLds4& d, uint32_t row, uint32_t so, uint32_t& acc) {
+  const uint32_t t = dfa4_step(d, row, so);
+  acc |= t;
+  return t;
+}
+__device__ __forceinline__ uint32_t dstep(const DfaLds2& d, uint32_t row, uint32_t so, uint32_t& acc) {
+  return dfa2_step(d, row, so, acc);
+}
+__device__ __forceinline__ uint32_t dmask(const DfaLds4&, uint32_t acc) { return acc >> 16; }
+__device__ __forceinline__ uint32_t dmask(const DfaLds2&, uint32_t acc) { return acc; }
+__device__ __forceinline__ uint32_t dsym_scale(const DfaLds4&) { return 4; }
+__device__ __forceinline__ uint32_t dsym_scale(const DfaLds2&) { return 2; }
+__device__ __forceinline__ void dload(DfaLds4& d) { dfa4_load(d); }
+__device__ __forceinline__ void dload(DfaLds2& d) { dfa2_load(d); }
+
+template <class TAB>
+__device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx, const TAB& d, int s, int e) {
   uint32_t row = 0, acc = 0;
   int off = s & ~3;  // this block's first byte (4-byte aligned)
   int rs_ = s & 3;   // s - off: 0..3 at the first block, then negative
@@ -1469,7 +1497,7 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
         for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
       }
 #pragma unroll
-      for (int k = 0; k < 16; ++k) row = dfa2_step(d, row, so[k], acc);
+      for (int k = 0; k < 16; ++k) row = dstep(d, row, so[k], acc);
       ncp = 16;
     } else {  // code points, as the reference decodes them
 #pragma unroll 1
@@ -1510,9 +1538,9 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
               break;
             }
           }
-          sy *= 2;
+          sy *= dsym_scale(d);
         }
-        row = dfa2_step(d, row, sy, acc);
+        row = dstep(d, row, sy, acc);
         ncp = k + len;
       }
     }
@@ -1521,21 +1549,35 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
     re_ -= 16;
     ncp -= 16;
   }
-  return acc;
+  return dmask(d, acc);
 }
 
 // ntiles: FTILE tiles; tile_base / n_lines keep the TILE (64 KiB) tiles' bases that krca_log_match
 // reads (tile_base[T] = the first line of 32 KiB tile 2T), chunk counts / bases are per 256-byte
 // chunk as before
-__global__ __launch_bounds__(FTPB) void log_index_match(
+#ifdef LOG_TIMING
+__device__ unsigned long long g_log_timing[1024 * 8];  // per workgroup: ticket, A, scan, look-back, list, walk, write, tiles
+#define LT_INIT() uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t lt_p = clock64()
+#define LT(i) do { const uint64_t tn = clock64(); lt_acc[i] += tn - lt_p; lt_p = tn; } while (0)
+#define LT_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 1024) for (int i_ = 0; i_ < 8; ++i_) g_log_timing[blockIdx.x * 8 + i_] += lt_acc[i_]; } while (0)
+#else
+#define LT_INIT() do {} while (0)
+#define LT(i) do {} while (0)
+#define LT_FLUSH() do {} while (0)
+#endif
+template <class CF>
+__global__ __launch_bounds__(CF::FTPB) void log_index_match(
     const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off, int64_t D,
     const int32_t* __restrict__ chunk_doc, int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_base,
     int64_t nt64, unsigned long long* __restrict__ status, unsigned int* __restrict__ ticket, int64_t ntiles,
     int64_t cap, int64_t* __restrict__ line_start, int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
     int64_t* __restrict__ chunk_line0, int64_t* __restrict__ n_lines, int32_t* __restrict__ long_q,
     int32_t* __restrict__ n_long, int32_t* __restrict__ strad_q, int32_t* __restrict__ n_strad) {
+  constexpr int64_t FTILE = CF::FTILE;
+  constexpr int FTPB = CF::FTPB, FNIT = CF::FNIT, FCH = CF::FCH, FNBW = CF::FNBW, LMAX = CF::LMAX;
+  using TAB = typename std::conditional<CF::W32, DfaLds4, DfaLds2>::type;
   __shared__ __attribute__((aligned(16))) uint32_t s_text[FTILE / 4 + 8];  // the tile + 32 zero bytes
-  __shared__ DfaLds2 d;
+  __shared__ TAB d;
   __shared__ uint32_t s_cs[FNBW];
   __shared__ uint16_t s_ls[LMAX], s_le[LMAX], s_lm[LMAX];
   __shared__ int32_t s_cnt[FCH], s_cb[FCH];  // per 256-byte chunk: line starts, exclusive base in the tile
@@ -1543,14 +1585,19 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
   __shared__ int32_t s_prev_end;  // tile offset where the previous tile's last line ends (from line 0)
   __shared__ int64_t s_tile, s_excl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  dfa2_load(d);  // once per workgroup (persistent)
+  dload(d);  // once per workgroup (persistent)
   if (tid < 8) s_text[FTILE / 4 + tid] = 0u;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  LT_INIT();
   for (;;) {
     if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
     const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
-    if (tile >= ntiles) return;  // uniform
+    if (tile >= ntiles) {  // uniform
+      LT_FLUSH();
+      return;
+    }
+    LT(0);
     const int64_t tile0 = tile * FTILE;
     // ---- A: text -> LDS, line-start bits, chunk counts -----------------------------------------
     const int64_t qlast = (nbytes - 1) & ~(int64_t)(PIECE - 1);
@@ -1591,6 +1638,7 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
       if ((tid & (LANES_PER_CHUNK - 1)) == 0) s_cnt[pc / LANES_PER_CHUNK] = (int32_t)c;
     }
     __syncthreads();
+    LT(1);
     if (tid < FCH) {  // chunk counts -> exclusive bases inside the tile
       const int32_t v = s_cnt[tid];
       chunk_cnt[tile * FCH + tid] = v;
@@ -1615,6 +1663,44 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
       __hip_atomic_store(&status[tile], (tile == 0 ? LB_INC : LB_AGG) | (uint64_t)total, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+    LT(2);
+    // the look-back right away (wave 0): its inclusive prefix goes out before this tile's walk, so
+    // later tiles find it within a round or two instead of summing aggregates back over every tile
+    // still walking (published after the walk, the look-backs scanned ~2 x 512 tiles: 443 us, r4g)
+    if (wid == 0) {
+      int64_t excl = 0;
+      if (tile > 0) {
+        for (int64_t top = tile - 1;; top -= 64) {
+          const int64_t t = top - lane;  // lane 0 = the nearest predecessor of the window
+          uint64_t sv = t >= 0 ? lb_load(&status[t]) : LB_INC;
+          while (__any((sv >> 62) == 0)) {  // some predecessor has not published yet
+            __builtin_amdgcn_s_sleep(1);
+            if ((sv >> 62) == 0) sv = lb_load(&status[t]);
+          }
+          const uint64_t inc = __ballot((sv >> 62) == 2);
+          const int first = inc ? __builtin_ctzll(inc) : 64;  // nearest inclusive prefix (lowest lane)
+          int64_t val = (lane <= first && t >= 0) ? (int64_t)(sv & LB_VAL) : 0;
+          for (int off = 32; off > 0; off >>= 1) val += (int64_t)__shfl_xor((long long)val, off, 64);
+          excl += val;
+          if (inc) break;
+        }
+        if (lane == 0)
+          __hip_atomic_store(&status[tile], LB_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane == 0) {
+        s_excl = excl;
+        if (FTILE == TILE) tile_base[tile] = excl;  // the 64 KiB tiles' bases (krca_log_match)
+        else if ((tile & 1) == 0) tile_base[tile >> 1] = excl;
+        if (tile == ntiles - 1) {
+          const int64_t nl = excl + total;
+          tile_base[nt64] = nl;
+          *n_lines = nl;
+          if (nl >= 1 && nl <= cap && nbytes > 0) line_end[nl - 1] = last_line_end(text, nbytes, doc_off, D);
+        }
+      }
+    }
+    LT(3);  // (thread 0 is in wave 0: the look-back)
     // ---- B + C, one window of LMAX lines at a time (one window unless lines average < 16 B) ----
     const int nwin = total > 0 ? (total + LMAX - 1) / LMAX : 1;
     for (int win = 0; win < nwin; ++win) {
@@ -1647,6 +1733,7 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
         }
       }
       __syncthreads();
+      LT(4);
       // the DFA walk: a lane per line, from LDS (the tile's last line and long lines deferred)
       for (int j = tid; j < hi - lo; j += FTPB) {
         if (lo + j == total - 1) continue;
@@ -1654,42 +1741,12 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
         if (le - ls > LONG_LINE) continue;
         s_lm[j] = (uint16_t)(ls < le ? dfa_walk_lds(s_text, d, ls, le) : 0u);
       }
-      if (win == 0 && wid == 0) {  // the look-back: this tile's first line id
-        int64_t excl = 0;
-        if (tile > 0) {
-          for (int64_t top = tile - 1;; top -= 64) {
-            const int64_t t = top - lane;  // lane 0 = the nearest predecessor of the window
-            uint64_t sv = t >= 0 ? lb_load(&status[t]) : LB_INC;
-            while (__any((sv >> 62) == 0)) {  // some predecessor has not published yet
-              __builtin_amdgcn_s_sleep(1);
-              if ((sv >> 62) == 0) sv = lb_load(&status[t]);
-            }
-            const uint64_t inc = __ballot((sv >> 62) == 2);
-            const int first = inc ? __builtin_ctzll(inc) : 64;  // nearest inclusive prefix (lowest lane)
-            int64_t val = (lane <= first && t >= 0) ? (int64_t)(sv & LB_VAL) : 0;
-            for (int off = 32; off > 0; off >>= 1) val += (int64_t)__shfl_xor((long long)val, off, 64);
-            excl += val;
-            if (inc) break;
-          }
-          if (lane == 0)
-            __hip_atomic_store(&status[tile], LB_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-          s_excl = excl;
-          if ((tile & 1) == 0) tile_base[tile >> 1] = excl;  // the 64 KiB tiles' bases (krca_log_match)
-          if (total > 0 && excl >= 1 && excl - 1 < cap) line_end[excl - 1] = tile0 + s_prev_end;
-          if (tile == ntiles - 1) {
-            const int64_t nl = excl + total;
-            tile_base[nt64] = nl;
-            *n_lines = nl;
-            if (nl >= 1 && nl <= cap && nbytes > 0) line_end[nl - 1] = last_line_end(text, nbytes, doc_off, D);
-          }
-        }
-      }
       __syncthreads();
+      LT(5);
       const int64_t excl = s_excl;
       if (win == 0 && tid < FCH) chunk_line0[tile * FCH + tid] = excl + s_cb[tid];
+      if (win == 0 && tid == 0 && total > 0 && excl >= 1 && excl - 1 < cap)
+        line_end[excl - 1] = tile0 + s_prev_end;  // the previous tile's last line ends before line 0 here
       if (win == 0 && tile == ntiles - 1)  // an odd tile count: the last 64 KiB tile's missing half has no
         for (int64_t c = ntiles * FCH + tid; c < nt64 * TPB; c += FTPB) {  // line starts (log_hist and
           chunk_cnt[c] = 0;                                                 // log_lines read its chunks)
@@ -1709,13 +1766,26 @@ __global__ __launch_bounds__(FTPB) void log_index_match(
         else line_mask[id] = s_lm[j];
       }
       __syncthreads();  // the window's lists (and, after the last, the tile's LDS) are rewritten next
+      LT(6);
     }
+#ifdef LOG_TIMING
+    lt_acc[7] += 1;
+#endif
   }
 }
 
-// the tiles' last lines (one per tile of log_index_match): a lane per line, code point by code
-// point from global memory (a few thousand lines per scan); one longer than LONG_LINE goes on to
-// log_dfa_long's queue (launched after this kernel)
+// the tiles' last lines (one per tile of log_index_match: a few thousand per scan), a lane per line:
+// the lane's line (up to STRAD_B bytes from its 16-byte aligned start) is staged in a lane-private
+// LDS slot with every load issued at once, then walked code point by code point from LDS (a walk
+// through global memory waited on one dependent 16-byte load per block: 58 us for 5.6k lines, r4g).
+// Longer lines walk from global memory; lines longer than LONG_LINE go on to log_dfa_long's queue
+// (launched after this kernel).
+constexpr int STRAD_B = 256;
+struct LdsBytes {  // byte p of the text from a lane-private LDS copy of [a0, a0 + STRAD_B)
+  const uint8_t* b;
+  int64_t a0;
+  __device__ __forceinline__ uint32_t at(int64_t p) const { return b[p - a0]; }
+};
 __global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__ text, int64_t nbytes,
                                                      const int64_t* __restrict__ line_start,
                                                      const int64_t* __restrict__ line_end,
@@ -1723,6 +1793,7 @@ __global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__
                                                      const int32_t* __restrict__ nq, int32_t* __restrict__ long_q,
                                                      int32_t* __restrict__ n_long) {
   __shared__ DfaLds dfa;
+  __shared__ __attribute__((aligned(16))) uint4 sbuf[TPB * (STRAD_B / 16)];
   const int n = *nq;
   if ((int64_t)blockIdx.x * TPB >= n) return;  // uniform: no line for this block, skip the table fill
   dfa_load(dfa);
@@ -1733,16 +1804,34 @@ __global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__
       long_q[atomicAdd(n_long, 1)] = (int32_t)l;
       continue;
     }
-    Bytes B;
-    B.init(text, nbytes);
     uint32_t row = 0, mask = 0;
-    for (int64_t p = s; p < e;) {
-      uint32_t cp;
-      const int len = decode(B, p, cp);
-      const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
-      row = t & (kAcc - 1);
-      if (t & kAcc) mask |= dfa.out[row / KRCA_DFA_NSYM];
-      p += len;
+    auto walk = [&](auto& B) {
+      for (int64_t p = s; p < e;) {
+        uint32_t cp;
+        const int len = decode(B, p, cp);
+        const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
+        row = t & (kAcc - 1);
+        if (t & kAcc) mask |= dfa.out[row / KRCA_DFA_NSYM];
+        p += len;
+      }
+    };
+    const int64_t a0 = s & ~(int64_t)15;
+    if (e + 3 - a0 <= STRAD_B) {  // (decode may look up to 3 bytes past e: still inside the copy)
+      uint4* mine = sbuf + threadIdx.x * (STRAD_B / 16);
+      uint4 v[STRAD_B / 16];
+#pragma unroll
+      for (int k = 0; k < STRAD_B / 16; ++k) {  // an aligned 16-byte block holding a text byte never
+        const int64_t b = a0 + 16 * k;          // crosses the text's last page; blocks past it stay 0
+        v[k] = b < nbytes ? *reinterpret_cast<const uint4*>(text + b) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < STRAD_B / 16; ++k) mine[k] = v[k];
+      LdsBytes B{reinterpret_cast<const uint8_t*>(mine), a0};
+      walk(B);
+    } else {
+      Bytes B;
+      B.init(text, nbytes);
+      walk(B);
     }
     line_mask[l] = mask;
   }
@@ -1883,14 +1972,21 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   KRCA_LAUNCH_CHECK();
   const int64_t* Ld = tile + nt;  // the line count, on the device (written by the index's last tile)
   if (krca::tuning().log_fused) {
-    // the line index and the DFA walk in one pass over the text (two 512-thread workgroups per CU,
-    // 32 KiB tiles); the tiles' last lines go to log_dfa_strad, long lines to log_dfa_long
-    const int64_t ntf = num_ftiles(nbytes);
-    const int64_t resident =
-        krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_match), FTPB, st, 2);
-    hipLaunchKernelGGL(log_index_match, dim3((unsigned)std::min<int64_t>(ntf, resident)), dim3(FTPB), 0, st, text,
-                       nbytes, doc_off, ndocs, (const int32_t*)cdoc, chunk, tile, nt, status, ticket, ntf, line_cap,
-                       line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long, strad_q, n_strad);
+    // the line index and the DFA walk in one pass over the text (KRCA_LOG_FUSED = 1: 32 KiB tiles,
+    // two 512-thread workgroups per CU; 2: 64 KiB tiles, one 1024-thread workgroup per CU); the
+    // tiles' last lines go to log_dfa_strad, long lines to log_dfa_long
+    auto launch = [&](auto cfg) -> int64_t {
+      using CF = decltype(cfg);
+      const int64_t ntf = num_ftiles(nbytes, CF::FTILE);
+      const int64_t resident =
+          krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_match<CF>), CF::FTPB, st, 1);
+      hipLaunchKernelGGL(log_index_match<CF>, dim3((unsigned)std::min<int64_t>(ntf, resident)), dim3(CF::FTPB), 0, st,
+                         text, nbytes, doc_off, ndocs, (const int32_t*)cdoc, chunk, tile, nt, status, ticket, ntf,
+                         line_cap, line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long, strad_q,
+                         n_strad);
+      return ntf;
+    };
+    const int64_t ntf = krca::tuning().log_fused == 2 ? launch(FBig{}) : launch(FSmall{});
     KRCA_LAUNCH_CHECK();
     hipLaunchKernelGGL(log_dfa_strad, dim3((unsigned)krca::ceil_div(ntf, TPB)), dim3(TPB), 0, st, text, nbytes,
                        (const int64_t*)line_start, (const int64_t*)line_end, line_mask, (const int32_t*)strad_q,
@@ -1920,5 +2016,16 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   KRCA_HIP(hipStreamSynchronize(st));
   return KRCA_OK;
 }
+
+#ifdef LOG_TIMING
+int krca_log_debug_timing(unsigned long long* host, int reset) {  // timing variant builds only
+  KRCA_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_log_timing), sizeof(g_log_timing)));
+  if (reset) {
+    static unsigned long long zero[1024 * 8];
+    KRCA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_log_timing), zero, sizeof(zero)));
+  }
+  return KRCA_OK;
+}
+#endif
 
 }  // extern "C"

@@ -222,13 +222,34 @@ class Comm:
     def __init__(self, world=1, rank=0, group=None):
         self.world, self.rank, self.group = world, rank, group
         self._gloo = None  # the backend, looked up once
+        self._direct = None  # RCCL: (process group, options) for the per-iteration all-gather
 
     def exchange(self, shard):
         """Make every rank's send slice visible in shard.w_all (G = 1: swap the ping-pong pair)."""
         if self.world == 1:
             shard.send, shard.w_all = shard.w_all, shard.send
+            return
+        if self._direct is None:
+            self._direct = self._direct_gather()
+        if self._direct:
+            # the PageRank exchange runs 30 times per solve: the process group's all-gather called
+            # directly skips the public wrapper's per-call checks and option building (host time
+            # that, at 8 ranks, is of the order of the ~20 us step itself; DESIGN.md §5)
+            pg, opts = self._direct
+            pg._allgather_base(shard.w_all, shard.send, opts).wait()
         else:
             self.all_gather(shard.w_all, shard.send)
+
+    def _direct_gather(self):
+        """(group, AllgatherOptions) when the backend is RCCL / NCCL and the group has the direct
+        entry point, else False (gloo: the list form of all_gather_flat)."""
+        import torch.distributed as dist
+        if dist.get_backend(self.group) == "gloo":
+            return False
+        pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+        if not hasattr(pg, "_allgather_base") or not hasattr(dist, "AllgatherOptions"):
+            return False
+        return pg, dist.AllgatherOptions()
 
     def all_gather(self, out, inp):
         if self.world == 1:

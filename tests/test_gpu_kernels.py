@@ -260,8 +260,9 @@ def test_log_scan_one_call_and_fallback_identical(eng):
 
 
 def test_log_scan_fused_walk_identical(eng):
-    """krca_log_scan's fused pass (log_index_match: the DFA walks each 64 KiB tile's lines from LDS
-    in the line-index pass; each tile's last line and lines over 1 KiB go to log_dfa_long) equals
+    """krca_log_scan's fused pass (log_index_match: the DFA walks each tile's lines from LDS in the
+    line-index pass; each tile's last line goes to log_dfa_strad, lines over 1 KiB to log_dfa_long),
+    in both shapes (KRCA_LOG_FUSED=1: 32 KiB tiles, 16-bit table; 2: 64 KiB tiles, 32-bit table), equals
     the round-3 path (KRCA_LOG_FUSED=0: the index, then log_dfa re-reading the text) on every
     output, and the oracle: tiles of more than 4,096 lines (several list windows per tile: 2-byte
     and empty lines), lines straddling one and several tiles (a 300 KiB line leaves whole tiles
@@ -293,7 +294,8 @@ def test_log_scan_fused_walk_identical(eng):
     # the fused pass with line arrays that hold every line, the fallback (krca_log_match after a
     # krca_log_scan into too small arrays: a fresh engine), and the round-3 path; the workspace is
     # filled with garbage before each call (what the scan leaves unwritten must not be read)
-    for name, fused, fresh in (("fused", 1, False), ("fallback", 1, True), ("unfused", 0, False)):
+    for name, fused, fresh in (("fused", 1, False), ("fallback", 1, True), ("fused64", 2, False),
+                               ("fallback64", 2, True), ("unfused", 0, False)):
         e = native.NativeEngine() if fresh else eng
         e._workspace("logidx", nws).fill_(0x5B)
         with native.tune(e.lib, KRCA_LOG_FUSED=fused):
@@ -302,7 +304,7 @@ def test_log_scan_fused_walk_identical(eng):
                 e._workspace("logidx", nws).fill_(0x5B)
             r = e.log_scan_device(tb, toff)
             out[name] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
-    for name in ("fallback", "unfused"):
+    for name in ("fallback", "fused64", "fallback64", "unfused"):
         assert out["fused"].keys() == out[name].keys()
         for k in out["fused"]:
             assert np.array_equal(out["fused"][k], out[name][k]), (name, k)
