@@ -104,7 +104,9 @@ struct Tuning {
   int ppr_fuse;     // KRCA_PPR_FUSE: single device, the iteration's reduction in the step's last workgroup
                     // (0 = a ppr_reduce launch after each step)
   int ppr_nt;       // KRCA_PPR_NT: the step streams its plan / column / row arrays with non-temporal loads
+  int ppr_xcd;      // KRCA_PPR_XCD: each XCD's workgroups take one contiguous eighth of the plan entries
   int log_fused;    // KRCA_LOG_FUSED: krca_log_scan walks the DFA inside the line-index pass (0 = index, then log_dfa)
+  int log_dfa2;     // KRCA_LOG_DFA2: the unfused scan's DFA walks two lines per lane (log_dfa2)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

@@ -1169,6 +1169,220 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
   }
 }
 
+// log_dfa with TWO lines per lane (KRCA_LOG_DFA2, round 4): a byte step is a dependent LDS read
+// (the next row comes out of the table), so one line per lane leaves each wave one chain of LDS
+// round trips per block; here each lane walks lines l and l + DFA_TPB of a 2 * DFA_TPB group
+// together and the all-ASCII blocks of both lines interleave their 16 steps (two independent
+// chains).  A line that has ended keeps stepping on NOP bytes (identity) until the other one
+// ends; a block with a non-ASCII byte in either line walks the two lines one after the other.
+// Same transitions and outputs as log_dfa.
+struct DfaLine {
+  int off, rs_, re_, ncp;  // as in log_dfa: block start (from base), s - P, e - P, next code point - P
+  uint32_t row, acc;
+};
+
+__device__ __forceinline__ void dfa_line_words(const DfaLine& L, uint4 cur, const uint8_t* __restrict__ text,
+                                               int64_t base, int end_off, uint32_t (&w)[4], uint32_t (&in)[4],
+                                               int& lo, int& hi, bool& fast) {
+  w[0] = cur.x; w[1] = cur.y; w[2] = cur.z; w[3] = cur.w;
+  if (L.off + 16 > end_off) {  // the text's last bytes (a buffer load straddling the end reads 0)
+#pragma unroll 1
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t b = L.off + k < end_off ? (uint32_t)text[base + L.off + k] : 0u;
+      w[k >> 2] = (w[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (b << (8 * (k & 3)));
+    }
+  }
+  lo = max(L.rs_, 0);
+  hi = max(min(L.re_, 16), 0);
+  const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = ((uint32_t)hi * 0x01010101u) | 0x80808080u;
+  uint32_t hib = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    in[j] = hi > 0 ? word_in_line(j, lo4, hi4x) : 0u;
+    hib |= w[j] & in[j];
+  }
+  fast = !hib && (L.ncp <= lo || hi == 0);
+}
+
+// the code-point path of one line's block (log_dfa's, unchanged)
+__device__ __forceinline__ void dfa_line_slow(const DfaLds4& d, DfaLine& L, const uint32_t (&w)[4],
+                                              const uint8_t* __restrict__ text, int64_t base, int end_off, int lo,
+                                              int hi) {
+#pragma unroll 1
+  for (int k = 0; k < 16; ++k) {
+    if (k < L.ncp || k < lo || k >= hi) continue;
+    auto at = [&](int r) -> uint32_t {
+      if (r < 16) return (w[r >> 2] >> (8 * (r & 3))) & 0xFFu;
+      return L.off + r < end_off ? (uint32_t)text[base + L.off + r] : 0u;
+    };
+    uint32_t cp;
+    const uint32_t b = at(k);
+    int len;
+    if (b < 0x80) {
+      cp = b;
+      len = 1;
+    } else if (b < 0xE0) {
+      cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
+      len = 2;
+    } else if (b < 0xF0) {
+      cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
+      len = 3;
+    } else {
+      cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
+      len = 4;
+    }
+    uint32_t sy;
+    if (cp < 128) {
+      sy = d.sym[cp];
+    } else {
+      sy = KRCA_DFA_OTHER;
+      int a = 0, z = KRCA_DFA_NRANGE - 1;
+      while (a <= z) {
+        const int mid = (a + z) >> 1;
+        if (cp < krca_dfa_ranges[mid][0]) z = mid - 1;
+        else if (cp > krca_dfa_ranges[mid][1]) a = mid + 1;
+        else {
+          sy = krca_dfa_ranges[mid][2];
+          break;
+        }
+      }
+      sy *= 4;
+    }
+    const uint32_t t = dfa4_step(d, L.row, sy);
+    L.row = t;
+    L.acc |= t;
+    L.ncp = k + len;
+  }
+}
+
+__device__ __forceinline__ void dfa_line_syms(const DfaLds4& d, const uint32_t (&w)[4], const uint32_t (&in)[4],
+                                              uint32_t (&so)[16]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t x = w[j] | (in[j] ^ 0x80808080u);  // outside the line: >= 0x80, NOP
+#pragma unroll
+    for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
+  }
+}
+
+// after a block: true when the line has more blocks (then advanced); an ended line stays put
+// (its later blocks re-read the same 16 bytes as NOPs)
+__device__ __forceinline__ bool dfa_line_next(DfaLine& L, bool fast_done) {
+  if (fast_done) L.ncp = 16;
+  if (L.re_ <= 16) {
+    L.re_ = 0;
+    L.rs_ = 0;
+    L.ncp = 0;
+    return false;
+  }
+  L.off += 16;
+  L.rs_ -= 16;
+  L.re_ -= 16;
+  L.ncp -= 16;
+  return true;
+}
+
+__global__ __launch_bounds__(DFA_TPB) void log_dfa2(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
+                                                    const int64_t* __restrict__ Ld, int64_t cap,
+                                                    const int64_t* __restrict__ line_start,
+                                                    const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
+                                                    int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
+  __shared__ DfaLds4 d;
+  dfa4_load(d);
+  L = lines_of(L, Ld, cap);
+  constexpr int64_t GL = 2 * (int64_t)DFA_TPB;  // lines per group
+  for (int64_t l0 = (int64_t)blockIdx.x * GL; l0 < L; l0 += (int64_t)gridDim.x * GL) {
+    // buffer resource at the group's first line (the group's short lines span < 2 MiB: 32-bit
+    // offsets), reads past the text return 0
+    const int64_t base = line_start[l0] & ~(int64_t)15;
+    const int64_t rem = nbytes - base;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(text + base), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
+    const int end_off = (int)min(rem, (int64_t)INT32_MAX);
+    DfaLine A{0, 0, 0, 0, 0u, 0u}, B{0, 0, 0, 0, 0u, 0u};
+    const int64_t la = l0 + threadIdx.x, lb = la + DFA_TPB;
+    bool wa = false, wb = false;  // lines this lane writes
+    auto setup = [&](int64_t l, DfaLine& X, bool& wx) {
+      if (l >= L) return;
+      const int64_t s = line_start[l], e = line_end[l];
+      if (e - s > LONG_LINE) {
+        long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // a wave per long line (log_dfa_long)
+        return;
+      }
+      wx = true;
+      if (s >= e) return;  // empty: mask 0, no block
+      X.off = (int)((s & ~(int64_t)3) - base);
+      X.rs_ = (int)(s & 3);
+      X.re_ = (int)(e - (s & ~(int64_t)3));
+      X.ncp = X.rs_;
+    };
+    setup(la, A, wa);
+    setup(lb, B, wb);
+    auto load = [&](int q) -> uint4 {
+      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, q, 0, 0));
+    };
+    // one block of both lines; the next blocks are loaded into na / nb first (ping-pong, as log_dfa)
+    auto block = [&](uint4& ca, uint4& na, uint4& cb, uint4& nb) -> bool {
+      na = load(A.re_ > 16 ? A.off + 16 : A.off);
+      nb = load(B.re_ > 16 ? B.off + 16 : B.off);
+      uint32_t w0[4], i0[4], w1[4], i1[4];
+      int lo0, hi0, lo1, hi1;
+      bool f0, f1;
+      dfa_line_words(A, ca, text, base, end_off, w0, i0, lo0, hi0, f0);
+      dfa_line_words(B, cb, text, base, end_off, w1, i1, lo1, hi1, f1);
+      if (f0 && f1) {  // both all-ASCII (or ended): two interleaved chains
+        uint32_t s0[16], s1[16];
+        dfa_line_syms(d, w0, i0, s0);
+        dfa_line_syms(d, w1, i1, s1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t t0 = dfa4_step(d, A.row, s0[k]);
+          const uint32_t t1 = dfa4_step(d, B.row, s1[k]);
+          A.row = t0;
+          A.acc |= t0;
+          B.row = t1;
+          B.acc |= t1;
+        }
+      } else {
+        if (f0) {
+          uint32_t s0[16];
+          dfa_line_syms(d, w0, i0, s0);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t t0 = dfa4_step(d, A.row, s0[k]);
+            A.row = t0;
+            A.acc |= t0;
+          }
+        } else {
+          dfa_line_slow(d, A, w0, text, base, end_off, lo0, hi0);
+        }
+        if (f1) {
+          uint32_t s1[16];
+          dfa_line_syms(d, w1, i1, s1);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t t1 = dfa4_step(d, B.row, s1[k]);
+            B.row = t1;
+            B.acc |= t1;
+          }
+        } else {
+          dfa_line_slow(d, B, w1, text, base, end_off, lo1, hi1);
+        }
+      }
+      const bool ma = dfa_line_next(A, f0 && hi0 > 0);
+      const bool mb = dfa_line_next(B, f1 && hi1 > 0);
+      return ma || mb;
+    };
+    if (A.re_ > 0 || B.re_ > 0) {
+      uint4 ca = load(A.off), cb = load(B.off), na, nb;
+      while (block(ca, na, cb, nb) && block(na, ca, nb, cb)) {
+      }
+    }
+    if (wa) line_mask[la] = A.acc >> 16;
+    if (wb) line_mask[lb] = B.acc >> 16;
+  }
+}
+
 __global__ __launch_bounds__(TPB) void log_dfa_long(const uint8_t* __restrict__ text, int64_t nbytes,
                                                     const int64_t* __restrict__ line_start,
                                                     const int64_t* __restrict__ line_end,
@@ -1778,8 +1992,7 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
 // the lane's line (up to STRAD_B bytes from its 16-byte aligned start) is staged in a lane-private
 // LDS slot with every load issued at once, then walked code point by code point from LDS (a walk
 // through global memory waited on one dependent 16-byte load per block: 58 us for 5.6k lines, r4g).
-// Longer lines walk from global memory; lines longer than LONG_LINE go on to log_dfa_long's queue
-// (launched after this kernel).
+// Longer lines go on to log_dfa_long's queue (a wave per line, launched after this kernel).
 constexpr int STRAD_B = 256;
 struct LdsBytes {  // byte p of the text from a lane-private LDS copy of [a0, a0 + STRAD_B)
   const uint8_t* b;
@@ -1800,38 +2013,29 @@ __global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__
   for (int i = blockIdx.x * TPB + threadIdx.x; i < n; i += gridDim.x * TPB) {
     const int64_t l = q[i];
     const int64_t s = line_start[l], e = line_end[l];
-    if (e - s > LONG_LINE) {
-      long_q[atomicAdd(n_long, 1)] = (int32_t)l;
-      continue;
+    const int64_t a0 = s & ~(int64_t)15;
+    if (e + 3 - a0 > STRAD_B) {  // (decode may look up to 3 bytes past e): a wave per line instead
+      long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // (a lane walking it from global memory waited on
+      continue;                                   // one dependent load per block: 44 us per scan, r4i)
     }
     uint32_t row = 0, mask = 0;
-    auto walk = [&](auto& B) {
-      for (int64_t p = s; p < e;) {
-        uint32_t cp;
-        const int len = decode(B, p, cp);
-        const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
-        row = t & (kAcc - 1);
-        if (t & kAcc) mask |= dfa.out[row / KRCA_DFA_NSYM];
-        p += len;
-      }
-    };
-    const int64_t a0 = s & ~(int64_t)15;
-    if (e + 3 - a0 <= STRAD_B) {  // (decode may look up to 3 bytes past e: still inside the copy)
-      uint4* mine = sbuf + threadIdx.x * (STRAD_B / 16);
-      uint4 v[STRAD_B / 16];
+    uint4* mine = sbuf + threadIdx.x * (STRAD_B / 16);
+    uint4 v[STRAD_B / 16];
 #pragma unroll
-      for (int k = 0; k < STRAD_B / 16; ++k) {  // an aligned 16-byte block holding a text byte never
-        const int64_t b = a0 + 16 * k;          // crosses the text's last page; blocks past it stay 0
-        v[k] = b < nbytes ? *reinterpret_cast<const uint4*>(text + b) : make_uint4(0u, 0u, 0u, 0u);
-      }
+    for (int k = 0; k < STRAD_B / 16; ++k) {  // an aligned 16-byte block holding a text byte never
+      const int64_t b = a0 + 16 * k;          // crosses the text's last page; blocks past it stay 0
+      v[k] = b < nbytes ? *reinterpret_cast<const uint4*>(text + b) : make_uint4(0u, 0u, 0u, 0u);
+    }
 #pragma unroll
-      for (int k = 0; k < STRAD_B / 16; ++k) mine[k] = v[k];
-      LdsBytes B{reinterpret_cast<const uint8_t*>(mine), a0};
-      walk(B);
-    } else {
-      Bytes B;
-      B.init(text, nbytes);
-      walk(B);
+    for (int k = 0; k < STRAD_B / 16; ++k) mine[k] = v[k];
+    LdsBytes B{reinterpret_cast<const uint8_t*>(mine), a0};
+    for (int64_t p = s; p < e;) {
+      uint32_t cp;
+      const int len = decode(B, p, cp);
+      const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
+      row = t & (kAcc - 1);
+      if (t & kAcc) mask |= dfa.out[row / KRCA_DFA_NSYM];
+      p += len;
     }
     line_mask[l] = mask;
   }
@@ -1839,7 +2043,9 @@ __global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__
 
 int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, TILE)); }
 // int64 words of the int32 long-line queue (lines longer than LONG_LINE)
-int64_t long_q_words(int64_t nbytes) { return krca::ceil_div(nbytes / LONG_LINE + 1, 2); }
+// (lines longer than LONG_LINE: at most nbytes / LONG_LINE; log_dfa_strad's longer straddlers: at
+// most one per 32 KiB tile)
+int64_t long_q_words(int64_t nbytes) { return krca::ceil_div(nbytes / LONG_LINE + 2 * num_tiles(nbytes) + 2, 2); }
 // krca_log_scan's tail of the workspace (int64 words): look-back status words for the 2 x num_tiles
 // 32 KiB tiles of log_index_match (num_tiles of log_index_lines use the first half), the tile
 // ticket, the straddler count, the int32 straddler queue (one line per 32 KiB tile)
@@ -1854,7 +2060,7 @@ extern "C" {
 
 // workspace (int64 units): [ntiles+1] tile base | [ntiles*TPB] int32 chunk counts |
 // [ntiles*TPB] int32 chunk -> container | [ntiles*TPB] int64 first line id per chunk |
-// [1] long-line count | int32 long-line queue [nbytes / LONG_LINE + 1] | [ntiles] look-back status |
+// [1] long-line count | int32 long-line queue [long_q_words] | [ntiles] look-back status |
 // [1] tile ticket (the last two: krca_log_scan)
 const char* krca_log_dfa_unicode(void) { return KRCA_DFA_UNIDATA; }
 uint64_t krca_log_dfa_digest(void) { return KRCA_DFA_DIGEST; }
@@ -2000,9 +2206,11 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
                        (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
                        tile + nt);
     KRCA_LAUNCH_CHECK();
-    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, DFA_TPB), 256 * 3));
-    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0, Ld, line_cap,
-                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    const bool two = krca::tuning().log_dfa2 != 0;  // two lines per lane (log_dfa2)
+    const int64_t grid =
+        std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, (two ? 2 : 1) * DFA_TPB), 256 * 3));
+    hipLaunchKernelGGL(two ? log_dfa2 : log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0,
+                       Ld, line_cap, (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,

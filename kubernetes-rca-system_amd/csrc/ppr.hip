@@ -420,12 +420,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ pk, const int64_t* __restrict__ plan,
     const uint16_t* __restrict__ lane_info, int64_t nblk, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ outdeg, const int64_t* __restrict__ q, int64_t n, int64_t N, double alpha,
-    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz, Fold fo) {
+    int64_t* __restrict__ r, int64_t* __restrict__ send, int64_t n_max, Ctl* ctl, Fuse fz, Fold fo, int xcd) {
   __shared__ __attribute__((aligned(16))) uint32_t vals[EDGE_BUDGET];  // staged codes: edge (direct) or slot (dictionary) i
   __shared__ unsigned long long rowsum[ROW_BUDGET + 1];  // + the zero slot of rows without edges
   __shared__ int64_t red[TPB / 64];
-  int64_t b = blockIdx.x;
-  if (b >= nblk) return;
+  // entries of this workgroup: b, b + stride, ... below lim.  xcd (the host sets it when the grid is
+  // a multiple of 8 and nblk >= grid): workgroups g, g + 8, ... (one XCD, for speed only) share one
+  // contiguous eighth of the plan, so the callers an XCD's L2 holds are those of neighbouring rows
+  int64_t b = blockIdx.x, lim = nblk, stride = gridDim.x;
+  if (xcd) {
+    const int64_t x = blockIdx.x & 7;
+    stride = gridDim.x >> 3;
+    b = x * nblk / 8 + (blockIdx.x >> 3);
+    lim = (x + 1) * nblk / 8;
+  }
+  if (b >= lim) return;
   const int32_t conv = ctl->converged;
   if (conv) return;  // converged (tol > 0): no writes (uniform)
   const int tid = threadIdx.x;
@@ -438,12 +447,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   const double* coef = coef_of(ctl, n);
   load_rows<FLAGS>(H0.m, b, lane_info, pk, coef, q, r, R0);
   Meta cur = H0.m;
-  int64_t b1 = b + gridDim.x;
+  int64_t b1 = b + stride;
   // prefetches past the workgroup's last entry load the grid's last entry again (clamped, results
   // unused): every path issues the same loads, so the compiler's vector-memory waits stay counted
   // (vmcnt(N)) instead of vmcnt(0) at the join of an `if (b1 < nblk)`, which made the sum phase
   // wait for the NEXT entry's gathers and rows and undid the software pipeline
-  load_head<(FLAGS & PPR_NT) != 0>(plan, b1 < nblk ? b1 : nblk - 1, pk, H1);
+  load_head<(FLAGS & PPR_NT) != 0>(plan, b1 < lim ? b1 : lim - 1, pk, H1);
   // the teleport scale of this step (after the first entry's loads are issued: a folded step's
   // reduction of the previous one overlaps them)
   StepScalars k;
@@ -488,11 +497,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
       for (int j = 0; j < SEG; ++j) sacc_long += tid + j * TPB < ne ? wdec(v[j]) : 0;
     }
     // v is free: gathers and rows of the next entry, head of the one after
-    const int64_t b2 = b1 + gridDim.x;
+    const int64_t b2 = b1 + stride;
     const Meta next = hn.m;
     gather(hn, w, v);
-    load_rows<FLAGS>(next, b1 < nblk ? b1 : nblk - 1, lane_info, pk, coef, q, r, rn);
-    load_head<(FLAGS & PPR_NT) != 0>(plan, b2 < nblk ? b2 : nblk - 1, pk, hl);
+    load_rows<FLAGS>(next, b1 < lim ? b1 : lim - 1, lane_info, pk, coef, q, r, rn);
+    load_head<(FLAGS & PPR_NT) != 0>(plan, b2 < lim ? b2 : lim - 1, pk, hl);
     if (shortb) {
       const int nrows = cur.code - cur.rb;
       __syncthreads();
@@ -571,7 +580,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
 #ifdef PPR_TIMING
     tacc[4] += 1;
 #endif
-    if (b1 >= nblk) return false;
+    if (b1 >= lim) return false;
     cur = next;
     b = b1;
     b1 = b2;
@@ -820,12 +829,13 @@ int launch_step(const int64_t* row_ptr, const int32_t* col, const int64_t* plan,
   const int64_t resident = krca::tuning().ppr_grid > 0 ? (int64_t)krca::tuning().ppr_grid : occupancy;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nblk, resident));
   const bool nt = krca::tuning().ppr_nt != 0;
+  const int xcd = krca::tuning().ppr_xcd != 0 && grid % 8 == 0 && nblk >= grid;
   auto kern = (flags & KRCA_PPR_RESIDUAL) ? (nt ? ppr_step<PPR_RESIDUAL | PPR_WRITE_R | PPR_NT> : ppr_step<PPR_RESIDUAL | PPR_WRITE_R>)
               : (flags & KRCA_PPR_WRITE_R) ? (nt ? ppr_step<PPR_WRITE_R | PPR_NT> : ppr_step<PPR_WRITE_R>)
                                            : (nt ? ppr_step<PPR_NT> : ppr_step<0>);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TPB), 0, krca::as_stream(stream), row_ptr, col, plan, lane, nblk,
                      reinterpret_cast<const uint32_t*>(w_all), outdeg, q_local, n_local, N, alpha, r_local, send, n_max,
-                     reinterpret_cast<Ctl*>(ctl), fz, fo);
+                     reinterpret_cast<Ctl*>(ctl), fz, fo, xcd);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

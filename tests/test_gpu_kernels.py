@@ -126,6 +126,22 @@ def _check_docs(eng, docs):
             assert scan.examples(d, c) == ex[c], (d, c)
 
 
+@pytest.mark.parametrize("knobs", [dict(KRCA_LOG_FUSED=0), dict(KRCA_LOG_FUSED=1), dict(KRCA_LOG_FUSED=2),
+                                   dict(KRCA_LOG_FUSED=0, KRCA_LOG_DFA2=1),
+                                   dict(KRCA_LOG_FUSED=0, KRCA_LOG_IMPL=1), dict(KRCA_LOG_FUSED=0, KRCA_LOG_IMPL=2)])
+def test_log_scan_no_match_across_container_end(eng, knobs):
+    """A container without a trailing separator ends its last line: the next container's first
+    bytes must not complete a pattern ("Erro" | "r", "StatusCode=50" | "0", "OOMKille" | "d"),
+    nor may the bytes after the text's end; at every offset of the 16-byte block, every walk."""
+    docs = []
+    for pad in range(16):
+        docs += ["p" * pad + " state Erro", "r happened", "x StatusCode=50", "0 y", "OOMKille", "d z",
+                 "q" * pad + "Kille", "d", "Tracebac", "k", "panic", ": x", "time", "out"]
+    docs.append("tail StatusCode=50")  # the text's last bytes
+    with native.tune(eng.lib, **knobs):
+        _check_docs(eng, docs)
+
+
 def test_log_scan_reference_corpus(eng):
     import json
     import os
@@ -295,16 +311,16 @@ def test_log_scan_fused_walk_identical(eng):
     # krca_log_scan into too small arrays: a fresh engine), and the round-3 path; the workspace is
     # filled with garbage before each call (what the scan leaves unwritten must not be read)
     for name, fused, fresh in (("fused", 1, False), ("fallback", 1, True), ("fused64", 2, False),
-                               ("fallback64", 2, True), ("unfused", 0, False)):
+                               ("fallback64", 2, True), ("unfused", 0, False), ("unfused2", 10, False)):
         e = native.NativeEngine() if fresh else eng
         e._workspace("logidx", nws).fill_(0x5B)
-        with native.tune(e.lib, KRCA_LOG_FUSED=fused):
+        with native.tune(e.lib, KRCA_LOG_FUSED=fused % 10, KRCA_LOG_DFA2=fused // 10):
             if not fresh:
                 e.log_scan_device(tb, toff)  # sizes the engine's line arrays
                 e._workspace("logidx", nws).fill_(0x5B)
             r = e.log_scan_device(tb, toff)
             out[name] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
-    for name in ("fallback", "fused64", "fallback64", "unfused"):
+    for name in ("fallback", "fused64", "fallback64", "unfused", "unfused2"):
         assert out["fused"].keys() == out[name].keys()
         for k in out["fused"]:
             assert np.array_equal(out["fused"][k], out[name][k]), (name, k)
@@ -348,6 +364,23 @@ def test_ppr_bit_exact_vs_oracle(eng, n, deg, tol, iters):
     assert np.max(np.abs(rr[~big] - x[~big])) < 1e-13
     idx, _ = eng.topk(rf, 10)
     assert np.array_equal(idx, oracle.topk_ref(ro, 10)[0])
+
+
+@pytest.mark.parametrize("grid", [16, 40, 0])
+def test_ppr_xcd_entry_map_bit_identical(eng, grid):
+    """KRCA_PPR_XCD: workgroups g, g + 8, ... take one contiguous eighth of the plan entries (small
+    grids force nblk >= grid at 40k pods; grid 0 = the occupancy grid, where the map stays off below
+    that many blocks); tolerance runs included (the converged early exit)."""
+    m = synth.make_graph(40000, avg_degree=12, seed=5)
+    rng = np.random.default_rng(5)
+    seed = (rng.random(40000) ** 8).astype(np.float32)
+    rfo, ro, ito = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, 40, 1e-9)
+    with native.tune(eng.lib, KRCA_PPR_XCD=1, KRCA_PPR_GRID=grid):
+        r, rf, it = eng.ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, 40, 1e-9)
+        assert it == abs(ito) and np.array_equal(rf.cpu().numpy(), ro)
+        r, rf, it = eng.ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, 25, 0.0)
+    rfo, ro, _ = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, seed, 0.85, 25, 0.0)
+    assert np.array_equal(rf.cpu().numpy(), ro)
 
 
 def test_ppr_long_rows_and_dangling(eng):
