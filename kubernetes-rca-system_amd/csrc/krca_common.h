@@ -106,7 +106,6 @@ struct Tuning {
   int ppr_nt;       // KRCA_PPR_NT: the step streams its plan / column / row arrays with non-temporal loads
   int ppr_xcd;      // KRCA_PPR_XCD: each XCD's workgroups take one contiguous eighth of the plan entries
   int log_fused;    // KRCA_LOG_FUSED: krca_log_scan walks the DFA inside the line-index pass (0 = index, then log_dfa)
-  int log_dfa2;     // KRCA_LOG_DFA2: the unfused scan's DFA walks two lines per lane (log_dfa2)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

@@ -925,15 +925,43 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
 constexpr uint32_t kAcc = 0x8000u;
 static_assert(KRCA_DFA_NSTATE * KRCA_DFA_NSYM <= (int)kAcc, "row offsets must fit below kAcc");
 
+// Table fills.  Every entry needs the target's category mask, a load that depends on the
+// transition load: a plain loop paid two dependent global-memory round trips per iteration (48 of
+// them for a 256-lane workgroup: ~40 us, the whole time of log_dfa_strad, and ~20 us at the front
+// of log_dfa and the fused scan, r4j).  Now the masks go to LDS first (one round), then U
+// independent transition loads per lane are in flight at once.
+template <int U, class LD, class ST>
+__device__ __forceinline__ void fill_table(int n, LD load, ST store) {
+  for (int i0 = threadIdx.x; i0 < n; i0 += U * (int)blockDim.x) {
+    uint32_t t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      t[u] = i < n ? load(i) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      if (i < n) store(i, t[u]);
+    }
+  }
+}
+__device__ __forceinline__ void fill_out(uint16_t* out) {
+  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE; i += blockDim.x) out[i] = krca_dfa_out[i];
+  __syncthreads();
+}
+
 __device__ __forceinline__ uint32_t dfa_row_entry(int i) {
   const uint32_t t = krca_dfa_trans[i];
   return t * KRCA_DFA_NSYM | (krca_dfa_out[t] ? kAcc : 0u);
 }
 
 __device__ __forceinline__ void dfa_load(DfaLds& dfa) {
-  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * KRCA_DFA_NSYM; i += blockDim.x) dfa.trans[i] = (uint16_t)dfa_row_entry(i);
-  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE; i += blockDim.x) dfa.out[i] = krca_dfa_out[i];
   for (int i = threadIdx.x; i < 128; i += blockDim.x) dfa.ascii[i] = krca_dfa_ascii_sym[i];
+  fill_out(dfa.out);
+  fill_table<16>(
+      KRCA_DFA_NSTATE * KRCA_DFA_NSYM, [](int i) -> uint32_t { return krca_dfa_trans[i]; },
+      [&](int i, uint32_t t) { dfa.trans[i] = (uint16_t)(t * KRCA_DFA_NSYM | (dfa.out[t] ? kAcc : 0u)); });
   __syncthreads();
 }
 
@@ -1003,15 +1031,21 @@ static_assert(KRCA_NCAT <= 16, "category masks must fit 16 bits");
 
 struct DfaLds4 {
   uint32_t trans[KRCA_DFA_NSTATE * DFA_RS];  // (out[target] << 16) | target * DFA_RS * 4
+  uint16_t out[KRCA_DFA_NSTATE];             // (staging for the fill)
   uint8_t sym[256];                          // byte -> symbol * 4 (bytes >= 0x80 -> NOP)
 };
 
+// the DFA row entry at table index i (DFA_RS columns per state: the symbols, then NOP = itself)
+__device__ __forceinline__ uint32_t dfa_target(int i, int rs) {
+  const int st = i / rs, c = i % rs;
+  return c < KRCA_DFA_NSYM ? (uint32_t)krca_dfa_trans[st * KRCA_DFA_NSYM + c] : (uint32_t)st;
+}
+
 __device__ __forceinline__ void dfa4_load(DfaLds4& d) {
-  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * DFA_RS; i += blockDim.x) {
-    const int st = i / DFA_RS, c = i % DFA_RS;
-    const uint32_t t = c < KRCA_DFA_NSYM ? krca_dfa_trans[st * KRCA_DFA_NSYM + c] : (uint32_t)st;
-    d.trans[i] = ((uint32_t)krca_dfa_out[t] << 16) | (t * DFA_RS * 4);
-  }
+  fill_out(d.out);
+  fill_table<8>(
+      KRCA_DFA_NSTATE * DFA_RS, [](int i) { return dfa_target(i, DFA_RS); },
+      [&](int i, uint32_t t) { d.trans[i] = ((uint32_t)d.out[t] << 16) | (t * DFA_RS * 4); });
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t sy = i < 128 ? krca_dfa_ascii_sym[i] : NOP_SYM;
     d.sym[i] = (uint8_t)((sy == KRCA_DFA_SEP ? NOP_SYM : sy) * 4);  // no separator inside a line
@@ -1029,9 +1063,17 @@ __device__ __forceinline__ uint32_t dfa4_step(const DfaLds4& d, uint32_t row, ui
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(d.trans) + a);
 }
 
+// hi4x for word_in_line: the bytes 0x80 + hi - 1 (0x7F for hi = 0), so that hi4x - i has bit 7 set
+// iff i < hi.  (Until round 4 the bytes were 0x80 + hi, which admitted i = hi: the byte at the
+// line's end -- the separator, a NOP, or at a container without a trailing separator the NEXT
+// container's first byte, which could complete a pattern: "Erro" | "r".  Found by
+// test_log_scan_no_match_across_container_end.)
+__device__ __forceinline__ uint32_t line_hi4x(int hi) {
+  return (((uint32_t)hi * 0x01010101u) | 0x80808080u) - 0x01010101u;
+}
 // Line bytes of a block, four at a time: byte k of word j (block index i = 4j + k) is in the line
 // iff lo <= i < hi (lo = s - P clamped to [0, 16], hi = e - P clamped to [0, 16], broadcast to
-// the four bytes as lo4 / hi4 | 0x80808080).  SWAR on bytes < 0x80, no borrows: bit 7 of each
+// the four bytes as lo4 / line_hi4x(hi)).  SWAR on bytes < 0x80, no borrows: bit 7 of each
 // byte of the result is set iff the byte is in the line.
 __device__ __forceinline__ uint32_t word_in_line(int j, uint32_t lo4, uint32_t hi4x) {
   const uint32_t idx = 0x03020100u + 0x04040404u * (uint32_t)j;
@@ -1082,7 +1124,7 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
         }
       }
       const int lo = max(rs_, 0), hi = min(re_, 16);
-      const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = ((uint32_t)hi * 0x01010101u) | 0x80808080u;
+      const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = line_hi4x(hi);
       uint32_t in[4], hib = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1166,220 +1208,6 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
       }
     }
     line_mask[l] = acc >> 16;
-  }
-}
-
-// log_dfa with TWO lines per lane (KRCA_LOG_DFA2, round 4): a byte step is a dependent LDS read
-// (the next row comes out of the table), so one line per lane leaves each wave one chain of LDS
-// round trips per block; here each lane walks lines l and l + DFA_TPB of a 2 * DFA_TPB group
-// together and the all-ASCII blocks of both lines interleave their 16 steps (two independent
-// chains).  A line that has ended keeps stepping on NOP bytes (identity) until the other one
-// ends; a block with a non-ASCII byte in either line walks the two lines one after the other.
-// Same transitions and outputs as log_dfa.
-struct DfaLine {
-  int off, rs_, re_, ncp;  // as in log_dfa: block start (from base), s - P, e - P, next code point - P
-  uint32_t row, acc;
-};
-
-__device__ __forceinline__ void dfa_line_words(const DfaLine& L, uint4 cur, const uint8_t* __restrict__ text,
-                                               int64_t base, int end_off, uint32_t (&w)[4], uint32_t (&in)[4],
-                                               int& lo, int& hi, bool& fast) {
-  w[0] = cur.x; w[1] = cur.y; w[2] = cur.z; w[3] = cur.w;
-  if (L.off + 16 > end_off) {  // the text's last bytes (a buffer load straddling the end reads 0)
-#pragma unroll 1
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t b = L.off + k < end_off ? (uint32_t)text[base + L.off + k] : 0u;
-      w[k >> 2] = (w[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (b << (8 * (k & 3)));
-    }
-  }
-  lo = max(L.rs_, 0);
-  hi = max(min(L.re_, 16), 0);
-  const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = ((uint32_t)hi * 0x01010101u) | 0x80808080u;
-  uint32_t hib = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    in[j] = hi > 0 ? word_in_line(j, lo4, hi4x) : 0u;
-    hib |= w[j] & in[j];
-  }
-  fast = !hib && (L.ncp <= lo || hi == 0);
-}
-
-// the code-point path of one line's block (log_dfa's, unchanged)
-__device__ __forceinline__ void dfa_line_slow(const DfaLds4& d, DfaLine& L, const uint32_t (&w)[4],
-                                              const uint8_t* __restrict__ text, int64_t base, int end_off, int lo,
-                                              int hi) {
-#pragma unroll 1
-  for (int k = 0; k < 16; ++k) {
-    if (k < L.ncp || k < lo || k >= hi) continue;
-    auto at = [&](int r) -> uint32_t {
-      if (r < 16) return (w[r >> 2] >> (8 * (r & 3))) & 0xFFu;
-      return L.off + r < end_off ? (uint32_t)text[base + L.off + r] : 0u;
-    };
-    uint32_t cp;
-    const uint32_t b = at(k);
-    int len;
-    if (b < 0x80) {
-      cp = b;
-      len = 1;
-    } else if (b < 0xE0) {
-      cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
-      len = 2;
-    } else if (b < 0xF0) {
-      cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
-      len = 3;
-    } else {
-      cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
-      len = 4;
-    }
-    uint32_t sy;
-    if (cp < 128) {
-      sy = d.sym[cp];
-    } else {
-      sy = KRCA_DFA_OTHER;
-      int a = 0, z = KRCA_DFA_NRANGE - 1;
-      while (a <= z) {
-        const int mid = (a + z) >> 1;
-        if (cp < krca_dfa_ranges[mid][0]) z = mid - 1;
-        else if (cp > krca_dfa_ranges[mid][1]) a = mid + 1;
-        else {
-          sy = krca_dfa_ranges[mid][2];
-          break;
-        }
-      }
-      sy *= 4;
-    }
-    const uint32_t t = dfa4_step(d, L.row, sy);
-    L.row = t;
-    L.acc |= t;
-    L.ncp = k + len;
-  }
-}
-
-__device__ __forceinline__ void dfa_line_syms(const DfaLds4& d, const uint32_t (&w)[4], const uint32_t (&in)[4],
-                                              uint32_t (&so)[16]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = w[j] | (in[j] ^ 0x80808080u);  // outside the line: >= 0x80, NOP
-#pragma unroll
-    for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
-  }
-}
-
-// after a block: true when the line has more blocks (then advanced); an ended line stays put
-// (its later blocks re-read the same 16 bytes as NOPs)
-__device__ __forceinline__ bool dfa_line_next(DfaLine& L, bool fast_done) {
-  if (fast_done) L.ncp = 16;
-  if (L.re_ <= 16) {
-    L.re_ = 0;
-    L.rs_ = 0;
-    L.ncp = 0;
-    return false;
-  }
-  L.off += 16;
-  L.rs_ -= 16;
-  L.re_ -= 16;
-  L.ncp -= 16;
-  return true;
-}
-
-__global__ __launch_bounds__(DFA_TPB) void log_dfa2(const uint8_t* __restrict__ text, int64_t nbytes, int64_t L,
-                                                    const int64_t* __restrict__ Ld, int64_t cap,
-                                                    const int64_t* __restrict__ line_start,
-                                                    const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
-                                                    int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
-  __shared__ DfaLds4 d;
-  dfa4_load(d);
-  L = lines_of(L, Ld, cap);
-  constexpr int64_t GL = 2 * (int64_t)DFA_TPB;  // lines per group
-  for (int64_t l0 = (int64_t)blockIdx.x * GL; l0 < L; l0 += (int64_t)gridDim.x * GL) {
-    // buffer resource at the group's first line (the group's short lines span < 2 MiB: 32-bit
-    // offsets), reads past the text return 0
-    const int64_t base = line_start[l0] & ~(int64_t)15;
-    const int64_t rem = nbytes - base;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(text + base), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
-    const int end_off = (int)min(rem, (int64_t)INT32_MAX);
-    DfaLine A{0, 0, 0, 0, 0u, 0u}, B{0, 0, 0, 0, 0u, 0u};
-    const int64_t la = l0 + threadIdx.x, lb = la + DFA_TPB;
-    bool wa = false, wb = false;  // lines this lane writes
-    auto setup = [&](int64_t l, DfaLine& X, bool& wx) {
-      if (l >= L) return;
-      const int64_t s = line_start[l], e = line_end[l];
-      if (e - s > LONG_LINE) {
-        long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // a wave per long line (log_dfa_long)
-        return;
-      }
-      wx = true;
-      if (s >= e) return;  // empty: mask 0, no block
-      X.off = (int)((s & ~(int64_t)3) - base);
-      X.rs_ = (int)(s & 3);
-      X.re_ = (int)(e - (s & ~(int64_t)3));
-      X.ncp = X.rs_;
-    };
-    setup(la, A, wa);
-    setup(lb, B, wb);
-    auto load = [&](int q) -> uint4 {
-      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, q, 0, 0));
-    };
-    // one block of both lines; the next blocks are loaded into na / nb first (ping-pong, as log_dfa)
-    auto block = [&](uint4& ca, uint4& na, uint4& cb, uint4& nb) -> bool {
-      na = load(A.re_ > 16 ? A.off + 16 : A.off);
-      nb = load(B.re_ > 16 ? B.off + 16 : B.off);
-      uint32_t w0[4], i0[4], w1[4], i1[4];
-      int lo0, hi0, lo1, hi1;
-      bool f0, f1;
-      dfa_line_words(A, ca, text, base, end_off, w0, i0, lo0, hi0, f0);
-      dfa_line_words(B, cb, text, base, end_off, w1, i1, lo1, hi1, f1);
-      if (f0 && f1) {  // both all-ASCII (or ended): two interleaved chains
-        uint32_t s0[16], s1[16];
-        dfa_line_syms(d, w0, i0, s0);
-        dfa_line_syms(d, w1, i1, s1);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const uint32_t t0 = dfa4_step(d, A.row, s0[k]);
-          const uint32_t t1 = dfa4_step(d, B.row, s1[k]);
-          A.row = t0;
-          A.acc |= t0;
-          B.row = t1;
-          B.acc |= t1;
-        }
-      } else {
-        if (f0) {
-          uint32_t s0[16];
-          dfa_line_syms(d, w0, i0, s0);
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const uint32_t t0 = dfa4_step(d, A.row, s0[k]);
-            A.row = t0;
-            A.acc |= t0;
-          }
-        } else {
-          dfa_line_slow(d, A, w0, text, base, end_off, lo0, hi0);
-        }
-        if (f1) {
-          uint32_t s1[16];
-          dfa_line_syms(d, w1, i1, s1);
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const uint32_t t1 = dfa4_step(d, B.row, s1[k]);
-            B.row = t1;
-            B.acc |= t1;
-          }
-        } else {
-          dfa_line_slow(d, B, w1, text, base, end_off, lo1, hi1);
-        }
-      }
-      const bool ma = dfa_line_next(A, f0 && hi0 > 0);
-      const bool mb = dfa_line_next(B, f1 && hi1 > 0);
-      return ma || mb;
-    };
-    if (A.re_ > 0 || B.re_ > 0) {
-      uint4 ca = load(A.off), cb = load(B.off), na, nb;
-      while (block(ca, na, cb, nb) && block(na, ca, nb, cb)) {
-      }
-    }
-    if (wa) line_mask[la] = A.acc >> 16;
-    if (wb) line_mask[lb] = B.acc >> 16;
   }
 }
 
@@ -1643,12 +1471,10 @@ struct DfaLds2 {
 static_assert(KRCA_DFA_NSTATE * D2_RS * 2 <= 0x8000, "row byte offsets must fit 15 bits");
 
 __device__ __forceinline__ void dfa2_load(DfaLds2& d) {
-  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE * D2_RS; i += blockDim.x) {
-    const int st = i / D2_RS, c = i % D2_RS;
-    const uint32_t t = c < KRCA_DFA_NSYM ? krca_dfa_trans[st * KRCA_DFA_NSYM + c] : (uint32_t)st;
-    d.trans[i] = (uint16_t)((t * D2_RS * 2) | (krca_dfa_out[t] ? 0x8000u : 0u));
-  }
-  for (int i = threadIdx.x; i < KRCA_DFA_NSTATE; i += blockDim.x) d.out[i] = (uint16_t)krca_dfa_out[i];
+  fill_out(d.out);
+  fill_table<8>(
+      KRCA_DFA_NSTATE * D2_RS, [](int i) { return dfa_target(i, D2_RS); },
+      [&](int i, uint32_t t) { d.trans[i] = (uint16_t)((t * D2_RS * 2) | (d.out[t] ? 0x8000u : 0u)); });
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t sy = i < 128 ? krca_dfa_ascii_sym[i] : NOP_SYM;
     d.sym[i] = (uint8_t)((sy == KRCA_DFA_SEP ? NOP_SYM : sy) * 2);  // no separator inside a line
@@ -1695,7 +1521,7 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + j];
     const int lo = max(rs_, 0), hi = min(re_, 16);
-    const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = ((uint32_t)hi * 0x01010101u) | 0x80808080u;
+    const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = line_hi4x(hi);
     uint32_t in[4], hib = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -2178,9 +2004,10 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   KRCA_LAUNCH_CHECK();
   const int64_t* Ld = tile + nt;  // the line count, on the device (written by the index's last tile)
   if (krca::tuning().log_fused) {
-    // the line index and the DFA walk in one pass over the text (KRCA_LOG_FUSED = 1: 32 KiB tiles,
-    // two 512-thread workgroups per CU; 2: 64 KiB tiles, one 1024-thread workgroup per CU); the
-    // tiles' last lines go to log_dfa_strad, long lines to log_dfa_long
+    // A/B: the line index and the DFA walk in one pass over the text (KRCA_LOG_FUSED = 1: 32 KiB
+    // tiles, two 512-thread workgroups per CU; 2: 64 KiB tiles, one 1024-thread workgroup per CU);
+    // the tiles' last lines go to log_dfa_strad, long lines to log_dfa_long.  It reads the text
+    // once but runs its phases one after the other per tile: slower than the default
     auto launch = [&](auto cfg) -> int64_t {
       using CF = decltype(cfg);
       const int64_t ntf = num_ftiles(nbytes, CF::FTILE);
@@ -2198,7 +2025,7 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
                        (const int64_t*)line_start, (const int64_t*)line_end, line_mask, (const int32_t*)strad_q,
                        (const int32_t*)n_strad, long_q, n_long);
     KRCA_LAUNCH_CHECK();
-  } else {  // A/B (KRCA_LOG_FUSED=0): the round-3 line index, then a DFA lane per line re-reading the text
+  } else {  // default (KRCA_LOG_FUSED=0): the line index, then a DFA lane per line re-reading the text
     // workgroups the stream's device keeps resident (occupancy API, cached per device)
     const int64_t resident = krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_lines), TPB, st, 4);
     const int64_t grid_ix = LOG_IDX_PERSIST ? std::min<int64_t>(nt, resident) : nt;
@@ -2206,11 +2033,9 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
                        (const int32_t*)cdoc, chunk, tile, status, ticket, nt, line_cap, line_start, line_end, chunk_line0,
                        tile + nt);
     KRCA_LAUNCH_CHECK();
-    const bool two = krca::tuning().log_dfa2 != 0;  // two lines per lane (log_dfa2)
-    const int64_t grid =
-        std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, (two ? 2 : 1) * DFA_TPB), 256 * 3));
-    hipLaunchKernelGGL(two ? log_dfa2 : log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0,
-                       Ld, line_cap, (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(krca::ceil_div(line_cap, DFA_TPB), 256 * 3));
+    hipLaunchKernelGGL(log_dfa, dim3((unsigned)grid), dim3(DFA_TPB), 0, st, text, nbytes, (int64_t)0, Ld, line_cap,
+                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, long_q, n_long);
     KRCA_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(log_dfa_long, dim3(256), dim3(TPB), 0, st, text, nbytes, (const int64_t*)line_start,

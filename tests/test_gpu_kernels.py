@@ -127,7 +127,6 @@ def _check_docs(eng, docs):
 
 
 @pytest.mark.parametrize("knobs", [dict(KRCA_LOG_FUSED=0), dict(KRCA_LOG_FUSED=1), dict(KRCA_LOG_FUSED=2),
-                                   dict(KRCA_LOG_FUSED=0, KRCA_LOG_DFA2=1),
                                    dict(KRCA_LOG_FUSED=0, KRCA_LOG_IMPL=1), dict(KRCA_LOG_FUSED=0, KRCA_LOG_IMPL=2)])
 def test_log_scan_no_match_across_container_end(eng, knobs):
     """A container without a trailing separator ends its last line: the next container's first
@@ -311,16 +310,16 @@ def test_log_scan_fused_walk_identical(eng):
     # krca_log_scan into too small arrays: a fresh engine), and the round-3 path; the workspace is
     # filled with garbage before each call (what the scan leaves unwritten must not be read)
     for name, fused, fresh in (("fused", 1, False), ("fallback", 1, True), ("fused64", 2, False),
-                               ("fallback64", 2, True), ("unfused", 0, False), ("unfused2", 10, False)):
+                               ("fallback64", 2, True), ("unfused", 0, False)):
         e = native.NativeEngine() if fresh else eng
         e._workspace("logidx", nws).fill_(0x5B)
-        with native.tune(e.lib, KRCA_LOG_FUSED=fused % 10, KRCA_LOG_DFA2=fused // 10):
+        with native.tune(e.lib, KRCA_LOG_FUSED=fused):
             if not fresh:
                 e.log_scan_device(tb, toff)  # sizes the engine's line arrays
                 e._workspace("logidx", nws).fill_(0x5B)
             r = e.log_scan_device(tb, toff)
             out[name] = {k: v.cpu().numpy() for k, v in r.items() if hasattr(v, "cpu")}
-    for name in ("fallback", "fused64", "fallback64", "unfused", "unfused2"):
+    for name in ("fallback", "fused64", "fallback64", "unfused"):
         assert out["fused"].keys() == out[name].keys()
         for k in out["fused"]:
             assert np.array_equal(out["fused"][k], out[name][k]), (name, k)

@@ -18,12 +18,14 @@ pass() {  # pass NAME COUNTERS -- CMD...
   local rc=$?; echo "$name EXIT=$rc" >> $O/status
   [ $rc -eq 0 ] || { tail -3 $O/$name.err; exit $rc; }
 }
-for t in cal ppr bench logs; do
+for t in cal ppr bench logs logs_fused; do
+  unset KRCA_LOG_FUSED
   case $t in
     cal) cmd=(tools/bin/pmc_calib) ;;
     ppr) cmd=(python3 tools/ppr_bench.py --reps 2) ;;
     bench) cmd=(python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-pipeline --no-corr) ;;
     logs) cmd=(python3 tools/prof_kernels.py logs --docs 1000000 --reps 1) ;;
+    logs_fused) export KRCA_LOG_FUSED=2; cmd=(python3 tools/prof_kernels.py logs --docs 1000000 --reps 1) ;;
   esac
   pass ${t}_rd TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum -- "${cmd[@]}"
   pass ${t}_dram TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B -- "${cmd[@]}"

@@ -41,7 +41,7 @@ for s in "$@"; do
     bench_n2) step bench_n2 600 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 5 --warmup 2 ;;
     tests_logs) step tests_logs 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread -k "log_scan or c2mini or c5 or stream or logs" ;;
     pprx_*) o=${s#pprx_}; prof $s 300 tools/ppr_bench.py --order ${o%_*} --xcd ${o##*_} --check --reps 10 ;;
-    logs_dfa2) export KRCA_LOG_FUSED=0 KRCA_LOG_DFA2=1; prof logs_dfa2 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED KRCA_LOG_DFA2 ;;
+    logs_fused1) export KRCA_LOG_FUSED=1; prof logs_fused1 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     logs_fused2) export KRCA_LOG_FUSED=2; prof logs_fused2 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     log_timing2) export KRCA_LOG_FUSED=2 KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing2 300 python3 tools/log_timing.py; unset KRCA_LIB KRCA_LOG_FUSED ;;
     logs_unfused) export KRCA_LOG_FUSED=0; prof logs_unfused 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
@@ -62,7 +62,7 @@ for s in "$@"; do
     ranking_spread) step ranking_spread 900 python3 -u tools/ranking_ablation_c4.py --seeds 2 --spread --out $O/ranking_ablation_spread_c4.json ;;
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
     ppr_g8) step ppr_g8 300 python3 tools/ppr_g8_emulation.py ;;
-    log_timing) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing 300 python3 tools/log_timing.py; unset KRCA_LIB ;;
+    log_timing) export KRCA_LOG_FUSED=1 KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing 300 python3 tools/log_timing.py; unset KRCA_LIB KRCA_LOG_FUSED ;;
     repeat_window) step repeat_window 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 ;;
     repeat_window_unfused) step repeat_window_unfused 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 KRCA_LOG_FUSED=0 ;;
     diag_window) step diag_window 300 python3 -u tools/diag_window_templates.py ;;

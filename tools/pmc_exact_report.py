@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--out")
     a = ap.parse_args()
     res = {}
-    for t in ("cal", "ppr", "bench", "logs"):
+    for t in ("cal", "ppr", "bench", "logs", "logs_fused"):
         rd, dr, wr = (load(os.path.join(a.d, f"{t}_{p}")) for p in ("rd", "dram", "wr"))
         kern = {}
         for k in set(rd) | set(dr) | set(wr):

@@ -22,11 +22,14 @@ def main():
     kern, src = {}, {}
     for f in a.reports:
         rep = json.load(open(f))
-        for sec in ("bench", "ppr", "logs"):
-            for k, e in rep.get(sec, {}).items():
+        for sec in ("bench", "ppr", "logs", "logs_fused"):
+            for k0, e in rep.get(sec, {}).items():
+                k = ("fused/" if sec == "logs_fused" else "") + k0  # the KRCA_LOG_FUSED=2 scan's kernels
                 if "dram_read_bytes" not in e or "dram_write_bytes" not in e:
                     continue
-                if k.startswith("at::") or k.startswith("__amd") or k.startswith("elementwise"):
+                if sec.startswith("logs") and e.get("dispatches", 2) < 2:
+                    continue  # the sizing call's first-scan kernels (log_lines ...), not the scan's
+                if k0.startswith("at::") or k0.startswith("__amd") or k0.startswith("elementwise"):
                     continue  # torch / runtime setup kernels
                 kern[k] = {"section": sec, "dram_read_bytes": e["dram_read_bytes"],
                            "dram_write_bytes": e["dram_write_bytes"],
