@@ -12,6 +12,9 @@ included: it adds the same per-iteration time under either partition).  Reports 
 the uniform ranges (ceil(N / G) pods) and for Partition.balanced, plus each one's scoring and
 PageRank parts run alone.  Prints one JSON line.
 
+The replicated alternative: every rank scores its own pods, the scores are all-gathered once per
+step, and each rank runs the whole mesh's solve alone (no collective inside the solve).
+
   python tools/g8_step_emulation.py [--pods 1000000] [--edges 20000000] [--world 8] [--steps 20]
 """
 import argparse
@@ -89,6 +92,68 @@ def run_rank(a, m, hops, cfg, part, g, M, T):
     return res
 
 
+def run_replicated(a, m, hops, cfg, part, g, M, T):
+    """The replicated-PageRank step on rank g: scoring of its pods, the all-gather of the scores
+    (4 B per pod; a device copy into the full vector stands in for it), then the whole mesh's
+    30-iteration solve on this rank alone (no per-iteration collective), pipelined as bench.py's
+    two streams.  ms per step, and the parts alone."""
+    import torch
+    from krca import native, synth
+    from krca.rca import Comm, DeviceShard, RcaStep, shard_graph
+    lo, hi, n_slot = part.range(g)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi, part)
+    x = synth.make_metrics_range(lo, hi, M, T, seed=0, roots=m.roots, hop_sets=hops, device="cuda")
+    engs = [native.NativeEngine(0) for _ in range(2)]
+    scor = [DeviceShard(e, x, rp, col, od, a.pods, n_slot, part.world, cfg) for e in engs]
+    full = [DeviceShard(e, None, m.row_ptr, m.col, m.outdeg, a.pods, a.pods, 1, cfg) for e in engs]
+    sfull = [torch.zeros(a.pods, dtype=torch.float32, device="cuda") for _ in range(2)]
+    for sh, sv in zip(full, sfull):
+        sh.score_out = {"score": sv}
+    steps = [RcaStep(sh, Comm(), cfg, 0) for sh in full]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    done = [None]
+
+    def gather(j):  # the all-gather of the scores: this rank's slice into the full vector
+        sfull[j][lo:hi].copy_(scor[j].score_out["score"][:hi - lo])
+
+    def enqueue(i):
+        j = i % 2
+        with torch.cuda.stream(streams[j]):
+            if done[0] is not None:
+                streams[j].wait_event(done[0])
+            scor[j].score()
+            done[0] = torch.cuda.Event()
+            done[0].record()
+            gather(j)
+            steps[j].propagate()
+            full[j].local_topk(cfg.k)
+
+    for i in range(4):
+        enqueue(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        enqueue(i)
+    torch.cuda.synchronize()
+    pipe_ms = (time.perf_counter() - t0) / a.steps * 1e3
+    parts = {}
+    for name, fn in (("scoring", scor[0].score), ("pagerank_full_mesh", steps[0].propagate)):
+        ev = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ev.append(e0.elapsed_time(e1))
+        parts[name] = float(np.median(ev))
+    res = dict(pods=hi - lo, edges=int(m.row_ptr[-1]), pipelined_ms_per_step=pipe_ms,
+               scoring_ms_alone=parts["scoring"], pagerank_ms_alone=parts["pagerank_full_mesh"])
+    del x, scor, full, steps, engs
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pods", type=int, default=1_000_000)
@@ -115,6 +180,11 @@ def main():
             res[f"rank{g}"] = run_rank(a, m, hops, cfg, part, g, M, T)
         out[pname] = dict(bounds=[int(b) for b in part.bounds], ranks=res,
                           step_ms_bound=max(r["pipelined_ms_per_step"] for r in res.values()))
+    part = Partition.uniform(a.pods, G)
+    pods = np.diff(part.bounds)
+    g = int(np.argmax(pods))
+    out["replicated"] = dict(ranks={f"rank{g}": run_replicated(a, m, hops, cfg, part, g, M, T)})
+    out["replicated"]["step_ms_bound"] = out["replicated"]["ranks"][f"rank{g}"]["pipelined_ms_per_step"]
     print(json.dumps(out), flush=True)
 
 
