@@ -67,6 +67,34 @@ class StreamingRCA:
         if isinstance(self.shard, DeviceShard):
             self._side = engine.torch.cuda.Stream(device=engine.device)
 
+    def prime(self, log_bytes, n_docs, lines_per_doc=2.5, templates=True):
+        """Pay the log pass's one-time costs before the first window instead of in it: a synthetic
+        text of `log_bytes` bytes in `n_docs` containers (`lines_per_doc` lines each) is scanned (and
+        template-hashed) on the side stream.  That loads the log kernels' code and sizes the
+        engine's line arrays and workspaces for windows of that size (a first window paid 7-8x the
+        steady-state time for them).  No stream state changes: ranks, metric history, the
+        iteration count stay as they were."""
+        import numpy as np
+        torch = self.eng.torch
+        n_docs = max(int(n_docs), 1)
+        n_lines = max(int(n_docs * lines_per_doc), n_docs)
+        L = max(int(log_bytes) // n_lines, 2)
+        line = np.full(L, ord("x"), np.uint8)
+        line[-1] = ord("\n")
+        blob = np.tile(line, n_lines)
+        per = n_lines // n_docs
+        off = np.minimum(np.arange(n_docs + 1, dtype=np.int64) * per * L, len(blob))
+        off[-1] = len(blob)
+        text = self.eng.upload_blob(blob.tobytes())
+        offd = torch.from_numpy(off).to(self.eng.device)
+        side = self._side or torch.cuda.current_stream(self.eng.device)
+        side.wait_stream(torch.cuda.current_stream(self.eng.device))
+        with torch.cuda.stream(side):
+            logs = self.push_logs(text, offd, templates=templates, validate=False, _defer=True)
+            if templates:
+                self.eng.template_hist_finish(logs.get("templates", {}))
+        side.synchronize()
+
     # -- 1. metrics ------------------------------------------------------------------------------
     def push_metrics(self, x_new):
         """x_new float32 [delta, n_local, M] (time-major, this rank's pods [lo, hi))."""

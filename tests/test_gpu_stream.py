@@ -124,7 +124,8 @@ def test_stream_window_log_overlap_and_error_path(eng):
     and template histograms equal the log pass run alone (one container above
     krca_template_max_lines() takes the deferred path), its ranks / counts / top-k equal a
     metrics-only stream's; a window whose offsets are refused raises and still completes the
-    re-rank, so the next windows stay identical to the metrics-only stream."""
+    re-rank, so the next windows stay identical to the metrics-only stream.  The log stream is
+    primed first (StreamingRCA.prime), the metrics-only one not."""
     from krca.agents.logs import pack_documents
     P, M, T, W = 2000, 8, 200, 60
     m = synth.make_graph(P, avg_degree=8, seed=31)
@@ -144,6 +145,7 @@ def test_stream_window_log_overlap_and_error_path(eng):
     want_t = [ref_t[k].cpu().numpy() for k in ("n_templates", "tmpl_hash", "tmpl_count")]
     cfg = Config(window=W)
     a = StreamingRCA(eng, m.row_ptr, m.col, m.outdeg, M, cfg, tol=1e-9, max_iter=60)
+    a.prime(len(blob), len(docs), lines_per_doc=2)  # changes no stream state: a stays equal to b
     b = StreamingRCA(eng, m.row_ptr, m.col, m.outdeg, M, cfg, tol=1e-9, max_iter=60)
     xd = torch.from_numpy(x).cuda()
     t = 0
