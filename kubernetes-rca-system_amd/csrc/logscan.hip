@@ -673,6 +673,17 @@ __global__ void log_last_end(const uint8_t* __restrict__ text, int64_t nbytes, c
   line_end[L - 1] = last_line_end(text, nbytes, doc_off, D);
 }
 
+// per-phase cycle counters of the tile kernels (a -DLOG_TIMING build, tools/log_timing.py)
+#ifdef LOG_TIMING
+__device__ unsigned long long g_log_timing[1024 * 8];  // per workgroup: phase cycles (log_index_match: ticket, A, scan, look-back, list, walk, write; log_index_lines: ticket + container starts, loads + flags, scan, look-back, writes), tiles
+#define LT_INIT() uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t lt_p = clock64()
+#define LT(i) do { const uint64_t tn = clock64(); lt_acc[i] += tn - lt_p; lt_p = tn; } while (0)
+#define LT_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 1024) for (int i_ = 0; i_ < 8; ++i_) g_log_timing[blockIdx.x * 8 + i_] += lt_acc[i_]; } while (0)
+#else
+#define LT_INIT() do {} while (0)
+#define LT(i) do {} while (0)
+#define LT_FLUSH() do {} while (0)
+#endif
 // ---- log_index_lines: log_count + log_scan + log_lines in ONE pass over the text -------------
 // The text is read once: a workgroup keeps its tile's per-piece line-start masks and separator
 // lengths in registers while it finds the tile's first line id by a decoupled look-back over the
@@ -780,16 +791,24 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   __shared__ uint32_t s_sl[NIT * TPB];
   __shared__ uint16_t s_l1[NIT * TPB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  LT_INIT();
   // tiles in ticket order, each workgroup taking the next until none is left: every tile a
-  // look-back waits on has been taken by a running workgroup, so the wait always ends
+  // look-back waits on has been taken by a running workgroup, so the wait always ends.  (Taking
+  // the next tile's ticket while still on this one, to build its container bitmap during the
+  // look-back, measured slower: 113.6 -> 135.8 us, r4r -- a claimed tile publishes its aggregate
+  // only after its holder finishes the current one, and later tiles' look-backs wait for it.)
   for (;;) {
   if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
   s_cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
-  if (tile >= ntiles) return;  // uniform
+  if (tile >= ntiles) {  // uniform
+    LT_FLUSH();
+    return;
+  }
   const int64_t tile0 = tile * TILE;
   tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
+  LT(0);
   // the pieces' loads go out LOG_IDX_BATCH at a time, unconditionally (a piece past the text
   // reloads the last aligned block, an aligned 16-byte block holding a text byte never crosses the
   // text's last page; its bytes are zeroed below): a load under `if (q < nbytes)` made each piece
@@ -835,6 +854,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   }
   }
   __syncthreads();
+  LT(1);
   // chunk counts, their scan inside the tile, the tile total
   const int64_t v = s_cnt[threadIdx.x];
   chunk_cnt[tile * TPB + threadIdx.x] = (int32_t)v;
@@ -848,6 +868,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   int64_t before = x - v;
   for (int u = 0; u < wid; ++u) before += s_wsum[u];
   const int64_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  LT(2);
   // decoupled look-back (wave 0): the tile's first line id
   if (wid == 0) {
     int64_t excl = 0;
@@ -888,6 +909,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   s_base[threadIdx.x] = excl + before;
   chunk_line0[tile * TPB + threadIdx.x] = excl + before;
   __syncthreads();
+  LT(3);
   // line starts and the previous line's end, from the registers
 #pragma unroll 2
   for (int it = 0; it < NIT; ++it) {
@@ -915,6 +937,10 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
     }
   }
   __syncthreads();  // the LDS planes and bases are rewritten by the next tile
+  LT(4);
+#ifdef LOG_TIMING
+  lt_acc[7] += 1;
+#endif
   }
 }
 
@@ -1595,16 +1621,6 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
 // ntiles: FTILE tiles; tile_base / n_lines keep the TILE (64 KiB) tiles' bases that krca_log_match
 // reads (tile_base[T] = the first line of 32 KiB tile 2T), chunk counts / bases are per 256-byte
 // chunk as before
-#ifdef LOG_TIMING
-__device__ unsigned long long g_log_timing[1024 * 8];  // per workgroup: ticket, A, scan, look-back, list, walk, write, tiles
-#define LT_INIT() uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t lt_p = clock64()
-#define LT(i) do { const uint64_t tn = clock64(); lt_acc[i] += tn - lt_p; lt_p = tn; } while (0)
-#define LT_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 1024) for (int i_ = 0; i_ < 8; ++i_) g_log_timing[blockIdx.x * 8 + i_] += lt_acc[i_]; } while (0)
-#else
-#define LT_INIT() do {} while (0)
-#define LT(i) do {} while (0)
-#define LT_FLUSH() do {} while (0)
-#endif
 template <class CF>
 __global__ __launch_bounds__(CF::FTPB) void log_index_match(
     const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off, int64_t D,

@@ -43,6 +43,7 @@ for s in "$@"; do
     pprx_*) o=${s#pprx_}; prof $s 300 tools/ppr_bench.py --order ${o%_*} --xcd ${o##*_} --check --reps 10 ;;
     logs_fused1) export KRCA_LOG_FUSED=1; prof logs_fused1 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     logs_fused2) export KRCA_LOG_FUSED=2; prof logs_fused2 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
+    log_timing0) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing0 300 python3 tools/log_timing.py; unset KRCA_LIB ;;
     log_timing2) export KRCA_LOG_FUSED=2 KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing2 300 python3 tools/log_timing.py; unset KRCA_LIB KRCA_LOG_FUSED ;;
     logs_unfused) export KRCA_LOG_FUSED=0; prof logs_unfused 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread ;;

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-phase cycle split of log_index_match (a -DLOG_TIMING build loaded through KRCA_LIB): one
+"""Per-phase cycle split of log_index_match (KRCA_LOG_FUSED=1/2) or log_index_lines (the default)
+from a -DLOG_TIMING build loaded through KRCA_LIB: one
 1M-container scan of the C5 corpus, then the per-workgroup sums of thread 0's clock between the
 kernel's barriers -- ticket, A (loads, container starts, line-start bits, chunk counts), scan +
 aggregate, look-back, list build, DFA walk, writes -- per tile.  Diagnostic only."""
@@ -35,10 +36,12 @@ def main():
     fn(buf.ctypes.data_as(ctypes.c_void_p), 1)
     t = buf.reshape(1024, 8).astype(np.float64)
     t = t[t[:, 7] > 0]
-    names = ["ticket", "A_loads_flags", "scan_agg", "lookback", "list", "walk", "write"]
+    fused = int(os.environ.get("KRCA_LOG_FUSED", "0")) != 0
+    names = (["ticket", "A_loads_flags", "scan_agg", "lookback", "list", "walk", "write"] if fused else
+             ["ticket_container_starts", "loads_flags", "scan", "lookback", "writes", "-", "-"])
     tiles = t[:, 7].sum()
     per_tile = {n: float(t[:, i].sum() / tiles) for i, n in enumerate(names)}
-    out = dict(bytes=len(blob), workgroups=int(len(t)), tiles=int(tiles), cycles_per_tile=per_tile,
+    out = dict(kernel="log_index_match" if fused else "log_index_lines", bytes=len(blob), workgroups=int(len(t)), tiles=int(tiles), cycles_per_tile=per_tile,
                total_cycles_per_wg_mean=float(t[:, :7].sum(1).mean()), total_cycles_per_wg_max=float(t[:, :7].sum(1).max()))
     print(json.dumps(out), flush=True)
 
