@@ -141,6 +141,40 @@ def test_log_scan_no_match_across_container_end(eng, knobs):
         _check_docs(eng, docs)
 
 
+@pytest.mark.parametrize("knobs", [dict(KRCA_LOG_FUSED=0), dict(KRCA_LOG_FUSED=1), dict(KRCA_LOG_FUSED=2),
+                                   dict(KRCA_LOG_FUSED=0, KRCA_LOG_IMPL=1), dict(KRCA_LOG_FUSED=0, KRCA_LOG_IMPL=2)])
+def test_log_scan_fragment_fuzz(eng, knobs):
+    """Every literal alternative of the 13 patterns cut at a random point, its halves scattered
+    over lines and containers with separators, multi-byte characters and fillers of random length
+    (so pattern halves meet at container ends without a trailing separator, at 16-byte block edges,
+    at line ends and across separators): histograms and examples equal the oracle's, every walk."""
+    import re as _re
+    from krca.patterns import ERROR_PATTERNS
+    lits = [a for _, p in ERROR_PATTERNS for a in p.strip("()").split("|")]
+    lits = [_re.sub(r"\\d", "7", a).replace("\\", "") for a in lits]  # StatusCode=5\d\d -> digits
+    rng = np.random.default_rng(21)
+    seps = ["\n", "\r", "\r\n", "\x0b", "\x0c", "\x1c", "\x1d", "\x1e", "\x85", "\u2028", "\u2029", ""]
+    other = ["é", "İ", "\u212a", "ſ", "x", " ", "0", "a" * 13, "q" * 40]
+    docs = []
+    for _ in range(1500):
+        parts = []
+        for _ in range(int(rng.integers(0, 12))):
+            r = rng.random()
+            if r < 0.45:
+                a = lits[int(rng.integers(0, len(lits)))]
+                cut = int(rng.integers(0, len(a) + 1))
+                parts.append(a[:cut] if rng.random() < 0.5 else a[cut:])
+            elif r < 0.6:
+                parts.append(lits[int(rng.integers(0, len(lits)))])
+            elif r < 0.8:
+                parts.append(seps[int(rng.integers(0, len(seps)))])
+            else:
+                parts.append(other[int(rng.integers(0, len(other)))] * int(rng.integers(1, 4)))
+        docs.append("".join(parts))
+    with native.tune(eng.lib, **knobs):
+        _check_docs(eng, docs)
+
+
 def test_log_scan_reference_corpus(eng):
     import json
     import os
