@@ -641,6 +641,22 @@ def test_template_hist_vs_oracle(eng):
         assert got[d] == oracle.template_hist(text), d
 
 
+def test_template_hist_fragment_fuzz(eng):
+    """Words, digit runs and hex runs cut at random points and scattered over lines and containers
+    (no trailing separator, so a word's halves meet at container ends; 8-hex-digit runs split and
+    joined; underscores, UTF-8 and the multi-byte separators beside them): every container's
+    template histogram equals the oracle's."""
+    rng = np.random.default_rng(29)
+    frags = ["dead", "beef", "cafe", "12", "x", "_", " ", "DEADBEEF", "0", "ab12", "deadbee", "f", "9z",
+             "é", "\u2028", "\x85", "\n", "\r\n", "\r", "-", "/", "GET", "worker", "id=", "0x"]
+    docs = []
+    for _ in range(3000):
+        docs.append("".join(frags[int(i)] for i in rng.integers(0, len(frags), int(rng.integers(0, 14)))))
+    got = eng.template_hist(*pack_documents(docs))
+    for d, text in enumerate(docs):
+        assert got[d] == oracle.template_hist(text), (d, repr(text))
+
+
 def test_template_hist_huge_containers(eng):
     """Containers above krca_template_max_lines() lines: distinct-hash table + bucketed sorts,
     exact vs the oracle (few templates repeated many times; all-distinct templates; a mix)."""
