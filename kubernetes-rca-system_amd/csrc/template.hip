@@ -27,6 +27,8 @@ constexpr int BIG = 4096;  // max lines per container handled by the LDS path
 constexpr uint64_t kFnvOff = 0xcbf29ce484222325ull;
 constexpr uint64_t kFnvPrime = 0x100000001b3ull;
 
+// (the 64-bit multiply is ~10 % of tmpl_hash_kernel: a build with a multiply-free stand-in ran
+// 140.9 against 156.2 us, r4w; the per-byte state-table read, a dependent LDS chain, is the rest)
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t b) { return (h ^ b) * kFnvPrime; }
 __device__ __forceinline__ bool is_word(uint32_t b) {
   return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
