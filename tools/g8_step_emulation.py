@@ -160,6 +160,10 @@ def main():
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--ppr-grids", default="", help="comma list of KRCA_PPR_GRID values: the uniform "
+                    "partition's binding rank re-run with the PageRank step's grid capped (leaving CUs to "
+                    "the scoring that overlaps it); e.g. 256,512")
+    ap.add_argument("--only-grids", action="store_true", help="skip the partition / replicated runs")
     a = ap.parse_args()
     from krca import synth
     from krca.rca import RANKING, Partition
@@ -170,6 +174,19 @@ def main():
     G = a.world
     out = dict(what=f"one rank's pipelined step at G={G} on one GPU (device copy for the all-gather)",
                pods=a.pods, edges=m.n_edges, steps=a.steps)
+    if a.ppr_grids:
+        from krca import native
+        part = Partition.uniform(a.pods, G)
+        g = int(np.argmax(np.diff(m.row_ptr[part.bounds])))
+        lib = native.load_library()
+        out["uniform_ppr_grid"] = {}
+        for grid in [int(v) for v in a.ppr_grids.split(",")]:
+            assert lib.krca_tune_set(b"KRCA_PPR_GRID", grid) == 0
+            out["uniform_ppr_grid"][str(grid)] = run_rank(a, m, hops, cfg, part, g, M, T)
+        lib.krca_tune_set(b"KRCA_PPR_GRID", 0)
+        if a.only_grids:
+            print(json.dumps(out), flush=True)
+            return
     for pname, part in (("uniform", Partition.uniform(a.pods, G)), ("balanced", Partition.balanced(m.row_ptr, G))):
         edges = np.diff(m.row_ptr[part.bounds])
         pods = np.diff(part.bounds)

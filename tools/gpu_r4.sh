@@ -68,6 +68,7 @@ for s in "$@"; do
     repeat_window_unfused) step repeat_window_unfused 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 KRCA_LOG_FUSED=0 ;;
     diag_window) step diag_window 300 python3 -u tools/diag_window_templates.py ;;
     g8_step) step g8_step 400 python3 tools/g8_step_emulation.py ;;
+    g8_grid) step g8_grid 400 python3 tools/g8_step_emulation.py --ppr-grids 0,1024,512,256 --only-grids ;;
     ppr_head)  # the same profile with the committed tree's code (ab_head/: git archive HEAD, built in place)
       step ppr_head 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ppr_head -o run -- python3 ab_head/tools/prof_kernels.py ppr --reps 5 ;;
     ppr_bytes) step ppr_bytes 300 python3 tools/ppr_bench.py --reps 5 ;;
