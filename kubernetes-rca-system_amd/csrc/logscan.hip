@@ -5,24 +5,25 @@
 // plus the first three matching lines per bin (the evidence of :159-163) and len(lines).
 //
 // Input: one UTF-8 blob holding D container logs back to back (doc_off[D+1] byte offsets).
-// Pipeline (HBM-bound; the blob is read twice, the 2nd time mostly from L2):
-//   log_count   count line starts per 256-byte chunk (str.splitlines separators: \n \r \r\n
-//               \v \f \x1c \x1d \x1e U+0085 U+2028 U+2029; container starts): streaming, a lane
-//               tests 16 bytes of a coalesced dwordx4; container starts are a per-container
-//               correction added by log_chunk_doc.  Containers must be valid UTF-8 each (they
-//               are encoded from str), so no multi-byte separator straddles two containers.
-//   log_scan    one workgroup: exclusive scan of the per-tile totals -> tile_base, n_lines.
-//   log_match   lane = chunk again, persistent workgroups with the DFA in LDS: line ids from
-//               the tile scan, UTF-8 decode, DFA step per code point (csrc/log_dfa_tables.h,
-//               compiled from the 13 regexes with Python's IGNORECASE folds and \d digit set),
-//               per-line OR of the state outputs.  A chunk starting mid-line warms the DFA up
-//               over the preceding <= 23 code points (the longest pattern is 23 long, so the DFA
-//               state depends on no more).  Line pieces that straddle chunks are combined in LDS
-//               by the owning lane; only lines straddling a 64 KiB tile use an atomic OR
-//               (deterministic: OR is order-free).
-//   log_hist    lane per container: one binary search for its first line (the next lane's is its
-//               end), a private loop over <= 32 line masks, or the whole wave (13 ballots per 64
-//               lines) for a larger container — counts and first three line ids per bin, no atomics.
+// krca_log_scan (one call, one stream synchronisation for the line count):
+//   log_chunk_doc     thread per container: the 256-byte chunk -> container map; zeroes the
+//                     look-back status words, the tile ticket and the queue counts.
+//   log_index_lines   persistent workgroups take 64 KiB tiles in ticket order: line-start bits and
+//                     separator lengths per 16-byte piece (str.splitlines separators: \n \r \r\n \v
+//                     \f \x1c \x1d \x1e U+0085 U+2028 U+2029; container starts from a per-tile LDS
+//                     bitmap), chunk counts, the tile's first line id by a decoupled look-back,
+//                     line_start / line_end written.  Containers are valid UTF-8 each, so no
+//                     multi-byte separator straddles two of them.
+//   log_dfa           lane per line, lockstep 16-byte blocks, the 13-pattern DFA
+//                     (csrc/log_dfa_tables.h: the 13 regexes with Python's IGNORECASE folds and \d)
+//                     from an LDS table; lines over 1 KiB queue for log_dfa_long (a wave per line,
+//                     64 segments each warmed up over the <= 23 code points before it).
+//   log_hist          lane per container (or a wave for a large one): 13 counts, the first three
+//                     example lines per bin marked in the line masks, no atomics.
+// A/B paths (tests require identical outputs): KRCA_LOG_FUSED = 1 / 2, log_index_match walking the
+// DFA inside the index pass from the LDS-resident tile (+ log_dfa_strad for each tile's last line);
+// KRCA_LOG_IMPL = 1, the chunk-lane log_match; = 2, the round-1 walk log_dfa_window.  When the
+// caller's line arrays are too small, krca_log_match finishes from the index in the workspace.
 #include <stdint.h>
 #include <cstdlib>
 
