@@ -40,6 +40,8 @@ for s in "$@"; do
     tests_new) step tests_new 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "empty_rank or cold_solve_fresh or bench_gpus" ;;
     bench_n2) step bench_n2 600 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 5 --warmup 2 ;;
     tests_logs) step tests_logs 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread -k "log_scan or c2mini or c5 or stream or logs" ;;
+    pprw_*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#pprw_}.so; prof $s 300 tools/ppr_bench.py --reps 10; unset KRCA_LIB ;;
+    pprbase) prof pprbase 300 tools/ppr_bench.py --reps 10 ;;
     pprx_*) o=${s#pprx_}; prof $s 300 tools/ppr_bench.py --order ${o%_*} --xcd ${o##*_} --check --reps 10 ;;
     logs_fused1) export KRCA_LOG_FUSED=1; prof logs_fused1 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     logs_fused2) export KRCA_LOG_FUSED=2; prof logs_fused2 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
