@@ -66,7 +66,8 @@ int krca_usage_flags(const float* usage /*[P][2]*/, int64_t P, uint8_t* flags /*
  *   z_last[p][m] = z at t = T-1 (0 if B <= 1e-12*W^2),   score[p] = max_m |z_last|,
  *   n_exceed[p]  = sum over m, t of exceed(t) (bit-exact vs oracle/krca_oracle.c),
  *   flags[p]     = KRCA_F_* of x[T-1][p][0] (CPU %) and x[T-1][p][1] (memory %) if M >= 2.
- * M must be a power of two <= 64. */
+ * M must be a power of two <= 64.  Samples are expected finite (a missing sample is the caller's
+ * to impute); a NaN / Inf never faults and gives what oracle/krca_oracle.c gives (tested). */
 int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t W, float z_thr,
                        float* z_last, float* score, int32_t* n_exceed, uint8_t* flags, void* stream);
 /* which kernel krca_rolling_score launches for these sizes (host query, no device work):

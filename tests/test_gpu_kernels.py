@@ -52,6 +52,24 @@ def test_rolling_score_vs_oracle(eng, P, M, T, W):
     assert np.allclose(z, zl, rtol=1e-5, atol=1e-5)
 
 
+def test_rolling_score_non_finite_samples_as_oracle(eng):
+    """Non-finite samples are outside the reference's inputs (missing metrics are absent, not NaN);
+    the contract is only that a NaN / +-Inf in a series never faults and gives what the C twin
+    gives: counts and flags bit-exact, z / score equal (NaN where the twin has NaN)."""
+    P, M, T, W = 300, 8, 200, 30
+    x = synth.make_metrics(P, M, T, window=W, seed=41, roots=np.arange(0, P, 11)).numpy().copy()
+    rng = np.random.default_rng(41)
+    for val in (np.nan, np.inf, -np.inf):
+        idx = rng.integers(0, x.size, 40)
+        x.reshape(-1)[idx] = val
+    got = eng.rolling_score(torch.from_numpy(x).cuda(), window=W, z_threshold=3.0)
+    ref = oracle.c_rolling_score(x, W, 3.0)
+    assert np.array_equal(got["n_exceed_host"], ref["n_exceed"])
+    assert np.array_equal(got["flags"], ref["flags"])
+    assert np.allclose(got["z_last"].cpu().numpy(), ref["z_last"], rtol=1e-5, atol=1e-6, equal_nan=True)
+    assert np.allclose(got["score"].cpu().numpy(), ref["score"], rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
 SCORE_VARIANTS = [("2", "20"), ("1", "20"), ("4", "20"), ("4", "15")] + [("0", c) for c in ("10", "12", "15", "20", "30")]
 
 
