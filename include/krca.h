@@ -166,7 +166,8 @@ int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspa
  * krca_corr_pad_steps(T)] (fp16 bits); cand [krca_corr_cand_size(P, T, k) 4-byte words]; count [P];
  * out_idx/out_val [P*k]; cert [P].  k <= krca_corr_max_k(), 2 <= P <= 2^22.  krca_corr_topk
  * synchronises the stream once (it reads how many candidate buffers overflowed to decide on the
- * second pass). */
+ * second pass).  The series must be finite: the certificates and the exact counts are proofs over
+ * finite rows (a NaN row's products compare false everywhere; its results are unspecified). */
 int64_t krca_corr_pad_rows(int64_t P);
 int32_t krca_corr_pad_steps(int32_t T);
 int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k);
