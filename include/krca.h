@@ -207,6 +207,11 @@ int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32
  * summation order or GPU count and are bit-identical to oracle/krca_oracle.c.  The per-node edge
  * weight floor(r_j * alpha / outdeg_j) travels as a 32-bit code (26 significant bits + shift,
  * truncating; csrc/ppr.hip wenc/wdec, restated in the oracle), so the gathered table is 4 B/node.
+ * The codes bound the reachable tolerance: each sweep carries ~2^-26 of the mass in truncation, so
+ * a tol below ~2^-26 / N (e.g. 1e-9 on a 2-node cycle) is not met -- krca_ppr then fails with
+ * KRCA_ENOTCONV as the oracle reports no convergence (networkx would raise
+ * PowerIterationFailedConvergence at its own, float64, limit).  networkx's default 1e-6 is met at
+ * every N.
  * krca_ppr runs the whole iteration on one device (synchronous: returns *iters_host; since round
  * 3 with the folded steps below, one kernel per iteration); the
  * krca_ppr_shard_* steps are the same kernels for G pod-sharded ranks.  Per iteration:

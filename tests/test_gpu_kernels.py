@@ -434,6 +434,54 @@ def test_ppr_xcd_entry_map_bit_identical(eng, grid):
     assert np.array_equal(rf.cpu().numpy(), ro)
 
 
+@pytest.mark.parametrize("case", ["self_loops", "no_edges", "single", "two_cycle", "star_in", "star_out",
+                                  "zero_seed", "one_seed"])
+def test_ppr_small_graph_edge_cases(eng, case):
+    """Self-loops (the topology agent's deployment merged into its service), a graph without edges,
+    one node, a 2-cycle, stars into / out of a hub, all-zero and single-pod personalization: the
+    fixed point bit-identical to the C oracle (iteration count included) and within 1e-5 of the
+    float64 restatement."""
+    from krca.agents.topology import csr_from_edges
+    rng = np.random.default_rng(3)
+    n = {"single": 1, "two_cycle": 2}.get(case, 50)
+    src, dst = [], []
+    if case == "self_loops":
+        src, dst = list(range(0, 50, 2)) + list(range(50)), list(range(0, 50, 2)) + list((np.arange(50) + 1) % 50)
+    elif case == "two_cycle":
+        src, dst = [0, 1], [1, 0]
+    elif case == "star_in":
+        src, dst = list(range(1, n)), [0] * (n - 1)
+    elif case == "star_out":
+        src, dst = [0] * (n - 1), list(range(1, n))
+    elif case in ("zero_seed", "one_seed"):
+        src, dst = list(rng.integers(0, n, 200)), list(rng.integers(0, n, 200))
+    pairs = sorted(set(zip(src, dst)))  # a DiGraph: each (caller, callee) once
+    rp, col, od = csr_from_edges(n, [a for a, _ in pairs], [b for _, b in pairs])
+    seed = (rng.random(n) ** 4).astype(np.float32)
+    if case == "zero_seed":
+        seed[:] = 0
+    if case == "one_seed":
+        seed[:] = 0
+        seed[7] = 1
+    if case == "two_cycle":
+        # below the weight codes' resolution (26 significant bits: ~2^-26 of the mass per sweep) a
+        # tolerance of N * 1e-9 is not reachable on two nodes: the oracle reports no convergence
+        # (negative count) and the device call raises, as networkx's PowerIterationFailedConvergence
+        _, _, ito = oracle.c_ppr(rp, col, od, seed, 0.85, 200, 1e-9)
+        assert ito == -200
+        with pytest.raises(native.KrcaError):
+            eng.ppr(rp, col, od, seed, 0.85, 200, 1e-9)
+    for iters, tol in ((60, 0.0), (200, 1e-6 if case == "two_cycle" else 1e-9)):
+        r, rf, it = eng.ppr(rp, col, od, seed, 0.85, iters, tol)
+        rfo, ro, ito = oracle.c_ppr(rp, col, od, seed, 0.85, iters, tol)
+        assert np.array_equal(rf.cpu().numpy(), ro) and it == abs(ito), (case, iters)
+        qs = np.floor(seed.astype(np.float64) * 2.0 ** 32) / 2.0 ** 32
+        x, _ = oracle.ppr_f64(rp, col, od, qs, 0.85, it, 0.0)
+        rr = r.cpu().numpy().astype(np.float64)
+        big = x >= 1e-9
+        assert np.max(np.abs(rr[big] - x[big]) / x[big]) < 1e-5, case
+
+
 def test_ppr_long_rows_and_dangling(eng):
     # a hub with 10k callers (long-row chunks + int64 atomics), isolated and dangling nodes
     n = 12000
