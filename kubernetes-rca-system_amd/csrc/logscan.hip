@@ -815,7 +815,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   // text's last page; its bytes are zeroed below): a load under `if (q < nbytes)` made each piece
   // wait for its own load, one piece in flight per lane
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const int64_t qlast = (nbytes - 1) & ~(int64_t)(PIECE - 1);
+  const int64_t qlast = nbytes > 0 ? (nbytes - 1) & ~(int64_t)(PIECE - 1) : 0;  // (krca_log_scan returns before any kernel when nbytes == 0)
   const int64_t wave0 = tile0 + (int64_t)__builtin_amdgcn_readfirstlane(wid) * 64 * PIECE;
   for (int it0 = 0; it0 < NIT; it0 += LOG_IDX_BATCH) {
     u32x4 raw[LOG_IDX_BATCH];
@@ -1663,7 +1663,7 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
     LT(0);
     const int64_t tile0 = tile * FTILE;
     // ---- A: text -> LDS, line-start bits, chunk counts -----------------------------------------
-    const int64_t qlast = (nbytes - 1) & ~(int64_t)(PIECE - 1);
+    const int64_t qlast = nbytes > 0 ? (nbytes - 1) & ~(int64_t)(PIECE - 1) : 0;  // (krca_log_scan returns before any kernel when nbytes == 0)
     u32x4 raw[FNIT];
     uint32_t pw[FNIT];
 #pragma unroll
@@ -2018,6 +2018,19 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   int32_t* n_strad = reinterpret_cast<int32_t*>(status + 2 * nt + 1);
   int32_t* strad_q = reinterpret_cast<int32_t*>(status + 2 * nt + 2);
   hipStream_t st = krca::as_stream(stream);
+  if (nbytes == 0) {
+    // no text (the pointer may be null): every container is empty and no kernel may read text --
+    // the index pass's unconditional piece loads clamp to the last 16-byte block that holds a
+    // byte, and there is none (an empty window faulted there: test_log_scan_degenerate_texts)
+    KRCA_HIP(hipMemsetAsync(tile, 0, (nt + 1) * sizeof(int64_t), st));  // tile bases, the line count
+    KRCA_HIP(hipMemsetAsync(chunk_line0, 0, nt * TPB * sizeof(int64_t), st));
+    KRCA_HIP(hipMemsetAsync(doc_lines, 0, ndocs * sizeof(int32_t), st));
+    KRCA_HIP(hipMemsetAsync(hist, 0, ndocs * KRCA_NCAT * sizeof(int32_t), st));
+    if (examples) KRCA_HIP(hipMemsetAsync(examples, 0xFF, ndocs * KRCA_NCAT * 3 * sizeof(int32_t), st));  // -1
+    if (doc_line0) KRCA_HIP(hipMemsetAsync(doc_line0, 0, ndocs * sizeof(int64_t), st));
+    *n_lines_host = 0;
+    return KRCA_OK;
+  }
   // one launch before the index: the chunk -> container map (every chunk of the text is written
   // under the doc_off contract; off it, tile_container_starts clamps what it reads), and the zeroed
   // look-back status words + ticket and long-line count (no memset launches: each dependent

@@ -193,6 +193,20 @@ def test_log_scan_fragment_fuzz(eng, knobs):
         _check_docs(eng, docs)
 
 
+@pytest.mark.parametrize("fused", [0, 1, 2])
+def test_log_scan_degenerate_texts(eng, fused):
+    """An all-empty window (one and several empty containers: no text at all), a text of exactly one
+    16-byte piece / one 32 KiB / one 64 KiB tile, a single separator, a text of separators only;
+    histograms, line counts and the template histograms against the oracle."""
+    cases = [[""], ["", "", ""], ["x" * 15 + "\n"], ["\n"], ["\r\n" * 7 + "\x85"],
+             ["a" * 32767 + "\n"], ["Error " * 5461 + "ab"], ["b" * 65535 + "\n", ""], ["", "Killed", ""]]
+    with native.tune(eng.lib, KRCA_LOG_FUSED=fused):
+        for docs in cases:
+            _check_docs(eng, docs)
+            got = eng.template_hist(*pack_documents(docs))
+            assert got == [oracle.template_hist(d) for d in docs], [len(d) for d in docs]
+
+
 def test_log_scan_reference_corpus(eng):
     import json
     import os
