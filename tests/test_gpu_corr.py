@@ -110,7 +110,7 @@ def test_corr_prepare_matches_twin(eng):
 
 
 @pytest.mark.parametrize("P,T,group,k", [(6000, 1440, 20, 10), (130, 200, 7, 16), (257, 64, 0, 5), (2, 30, 0, 1),
-                                         (1000, 100, 50, 10)])
+                                         (1000, 100, 50, 10), (60, 3, 0, 4), (33, 5, 0, 7), (300, 17, 0, 9)])
 def test_corr_full_vs_oracle(eng, P, T, group, k):
     x = synth.make_metrics(P, 2, T, seed=P + T, group_size=group)
     x[:, 3 % P, 0] = 42.0  # a flat series: r = 0 with everything
