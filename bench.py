@@ -593,7 +593,11 @@ def main():
         del x, shards, steps, shard, step
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        corr = corr_leg(args, eng, world, rank, local)
+        try:
+            corr = corr_leg(args, eng, world, rank, local)
+        except Exception as e:  # the headline line is printed whatever befalls its second leg
+            log(f"[rank {rank}] corr leg failed: {e!r}")
+            corr = {"error": repr(e)[:500]}
         if rank == 0:
             result["corr"] = corr
 
