@@ -76,7 +76,7 @@ for s in "$@"; do
       step ppr_head 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ppr_head -o run -- python3 ab_head/tools/prof_kernels.py ppr --reps 5 ;;
     ppr_bytes) step ppr_bytes 300 python3 tools/ppr_bench.py --reps 5 ;;
     ppr_fuse) export KRCA_PPR_FUSE=1; prof ppr_fuse 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_FUSE ;;
-    ppr_timing) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_wtime.so; step ppr_timing 300 python3 tools/ppr_timing.py; unset KRCA_LIB ;;
+    ppr_timing) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ptime.so PPR_TIMING_DUMP=$O/ppr_timing.npz; step ppr_timing 300 python3 tools/ppr_timing.py; unset KRCA_LIB PPR_TIMING_DUMP ;;
     ppr_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#ppr_}.so; prof $s 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_prev) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_prev.so; prof ppr_prev 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_LIB ;;
     ppr_nt) export KRCA_PPR_NT=1; prof ppr_nt 300 tools/prof_kernels.py ppr --reps 5; unset KRCA_PPR_NT ;;

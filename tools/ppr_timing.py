@@ -43,6 +43,8 @@ def main():
                cycles_per_wg_mean=float(tot.mean()) / RANKING.iters, cycles_per_wg_max=float(tot.max()) / RANKING.iters,
                split_mean={k: float(t[:, i].mean()) / RANKING.iters for i, k in enumerate(("stage", "sum", "update", "long"))},
                cycles_per_block={k: float(t[:, i].sum() / t[:, 4].sum()) for i, k in enumerate(("stage", "sum", "update", "long"))})
+    if os.environ.get("PPR_TIMING_DUMP"):  # per-workgroup counters + the plan, for a cost-model fit
+        np.savez(os.environ["PPR_TIMING_DUMP"], t=buf.reshape(4096, 5), plan=sh.plan.cpu().numpy().reshape(-1, 4))
     print(json.dumps(out))
 
 
