@@ -61,6 +61,11 @@ def parse(argv=None):
     ap.add_argument("--corr-k", type=int, default=10)
     ap.add_argument("--corr-runs", type=int, default=3, help="timed correlation calls (after one warm-up call)")
     ap.add_argument("--corr-check-rows", type=int, default=512)
+    ap.add_argument("--ppr-partition", choices=("balanced", "uniform"), default="balanced",
+                    help="G > 1: PageRank rows on Partition.balanced ranges (scores all-gathered once per step, "
+                         "krca.rca.SplitShard) or on the scoring's uniform ranges")
+    ap.add_argument("--ppr-edge-slack", type=float, default=1.5,
+                    help="Partition.balanced's in-edge cap per rank, in multiples of E / G")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run steps back to back on one stream (default: two streams, step i+1's scoring "
                          "overlaps step i's PageRank)")
@@ -218,17 +223,18 @@ def pmc_traffic(args, bytes_alg, world):
         return None, None
 
 
-def verify_step(args, cfg, mesh, shard, x, part, rank):
-    """Untimed parity of the last step at any N: every rank's fixed-point ranks and scores are
-    gathered to rank 0 and compared with the C oracle run on the whole mesh (ranks bit for bit,
-    top-10 identical); each rank checks n_exceed / flags / scores of its own sampled pods against
-    the oracle's scoring (bit-exact / 1e-5), summed over ranks."""
+def verify_step(args, cfg, mesh, shard, x, part, ppart, rank):
+    """Untimed parity of the last step at any N: every rank's fixed-point ranks (its rows of
+    `ppart`) and scores (its pods of `part`) are gathered to rank 0 and compared with the C oracle
+    run on the whole mesh (ranks bit for bit, top-10 identical); each rank checks n_exceed / flags /
+    scores of its own sampled pods against the oracle's scoring (bit-exact / 1e-5), summed over ranks."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     lo, hi, n_max = part.range(rank)
     world, n_loc = part.world, hi - lo
-    r_all = part.unpad(gather_rows(shard.r[:n_loc], n_max, world).cpu().numpy())
+    plo, phi, p_slot = ppart.range(rank)
+    r_all = ppart.unpad(gather_rows(shard.r[:phi - plo], p_slot, world).cpu().numpy())
     sc_all = part.unpad(gather_rows(shard.score_out["score"][:n_loc], n_max, world).cpu().numpy())
     ns = min(max(1, 2000 // world), n_loc)
     samp = np.sort(np.random.default_rng(1 + rank).choice(n_loc, size=ns, replace=False))
@@ -408,7 +414,7 @@ def main():
     import torch.distributed as dist
 
     from krca import native, synth
-    from krca.rca import Comm, Config, DeviceShard, Partition, RcaStep, shard_graph
+    from krca.rca import Comm, Config, DeviceShard, Partition, RcaStep, SplitShard, shard_graph
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -438,18 +444,32 @@ def main():
     # tools/g8_step_emulation.py)
     part = Partition.uniform(args.pods, world)
     lo, hi, n_max = part.range(rank)
-    rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, lo, hi, part)
+    # the PageRank rows: at G > 1 by default Partition.balanced ranges, so that the hub services'
+    # in-edges do not all land on rank 0 (10.6M of 20M at G = 8 with uniform ranges); the scores
+    # then travel in one all-gather per step (krca.rca.SplitShard)
+    split = world > 1 and args.ppr_partition == "balanced"
+    ppart = Partition.balanced(mesh.row_ptr, world, edge_slack=args.ppr_edge_slack) if split else part
+    plo, phi, p_slot = ppart.range(rank)
+    rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, plo, phi, ppart)
     x = synth.make_metrics_range(lo, hi, args.metrics, args.tsteps, window=args.window, seed=args.seed,
                                  roots=mesh.roots, hop_sets=hops, device=torch.device("cuda", local))
     n_pipe = 1 if args.no_pipeline else 2
     # one engine per pipeline slot: workspaces are per engine, and the slots run concurrently
     engs = [eng] + [native.NativeEngine(local) for _ in range(n_pipe - 1)]
-    shards = [DeviceShard(e, x, rp, col, od, args.pods, n_max, world, cfg) for e in engs]
-    steps = [RcaStep(sh, Comm(world, rank), cfg, lo) for sh in shards]
+    comms = [Comm(world, rank) for _ in range(n_pipe)]
+    if split:
+        nograph = (np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32))
+        shards = [SplitShard(DeviceShard(e, x, *nograph, args.pods, n_max, world, cfg),
+                             DeviceShard(e, None, rp, col, od, args.pods, p_slot, world, cfg), part, ppart, rank, c)
+                  for e, c in zip(engs, comms)]
+    else:
+        shards = [DeviceShard(e, x, rp, col, od, args.pods, n_max, world, cfg) for e in engs]
+    steps = [RcaStep(sh, c, cfg, plo) for sh, c in zip(shards, comms)]
     streams = [torch.cuda.Stream() for _ in range(n_pipe)]
     shard, step = shards[0], steps[0]
     torch.cuda.synchronize()
-    log(f"[rank {rank}] mesh N={args.pods} E={mesh.n_edges} shard=[{lo},{hi}) setup {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] mesh N={args.pods} E={mesh.n_edges} scoring=[{lo},{hi}) pagerank=[{plo},{phi}) "
+        f"({int(mesh.row_ptr[phi] - mesh.row_ptr[plo])} in-edges) setup {time.time() - t0:.1f}s")
 
     score_done = [None]  # the scoring kernels run one at a time; only PageRank overlaps them
 
@@ -553,7 +573,10 @@ def main():
                        "window": args.window, "ppr_iters": args.iters, "alpha": args.alpha,
                        "seed_floor": cfg.seed_floor, "parallelism": f"pod-sharded x{world}",
                        "partition": "uniform contiguous pod ranges (krca.rca.Partition.uniform)",
-                       "shard_bounds": [int(b) for b in part.bounds]},
+                       "shard_bounds": [int(b) for b in part.bounds],
+                       "ppr_partition": (f"Partition.balanced(edge_slack={args.ppr_edge_slack}), scores all-gathered "
+                                         "once per step (krca.rca.SplitShard)") if split else "the scoring's ranges",
+                       "ppr_bounds": [int(b) for b in ppart.bounds]},
             "e2e_rca_latency_ms": latency_ms, "e2e_rca_latency_p95_ms": latency_p95_ms,
             "step_ms_median": float(np.median(step_ms)), "step_ms_p95": float(np.percentile(step_ms, 95)),
             "pipelined_streams": n_pipe,
@@ -580,7 +603,7 @@ def main():
     # ---- verification (not timed): bit-exact PageRank / top-10 vs the C oracle, any N -------
     if not args.no_verify:
         try:
-            v = verify_step(args, cfg, mesh, shard, x, part, rank)
+            v = verify_step(args, cfg, mesh, shard, x, part, ppart, rank)
             if rank == 0:
                 v["top10_identical"] = v.pop("oracle_top10") == result["rca_top10"]
         except Exception as e:  # reported, never a lost line (a failed check is not a passed one)

@@ -505,6 +505,61 @@ class DeviceShard:
         return idx, val
 
 
+class SplitShard:
+    """A rank whose PageRank rows are not its scored pods (bench.py at G > 1).
+
+    The scoring runs on `scorer` over the rank's range of `spart` (uniform: every rank streams the
+    same number of series), ONE all-gather per step moves the scores (4 B per pod, every rank's
+    padded slice: pod order, since the ranges are uniform), and the PageRank solve runs on `ppr`
+    over the rank's range of `ppart` (Partition.balanced: the hub services' in-edges spread over
+    the ranks), seeded from its rows' slice of the gathered scores.  The solve is the same
+    pod-sharded one (one all-gather per iteration), so the ranks stay bit-identical to the oracle.
+    Everything :class:`RcaStep` and :class:`Comm` use besides score() -- init, folded steps, send /
+    w_all, top-k, r -- is the PageRank shard's; score_out is the scorer's."""
+
+    def __init__(self, scorer, ppr, spart, ppart, rank, comm):
+        import torch
+        if spart.world < 2 or spart.world != ppart.world or spart.N != ppart.N:
+            raise ValueError("SplitShard: two partitions of the same pods over the same G > 1 ranks")
+        if not np.array_equal(spart.bounds, Partition.uniform(spart.N, spart.world).bounds):
+            raise ValueError("SplitShard: the scoring partition must be uniform (its gathered slices are then in pod order)")
+        self.scorer, self.ppr, self.comm, self.rank = scorer, ppr, comm, rank
+        self.spart, self.ppart = spart, ppart
+        lo, hi, s_slot = spart.range(rank)
+        self.n_score = hi - lo
+        plo, phi, _ = ppart.range(rank)
+        dev = ppr.send.device
+        self._pad = torch.zeros(s_slot, dtype=torch.float32, device=dev)
+        self._all = torch.zeros(spart.world * s_slot + 1, dtype=torch.float32, device=dev)
+        view = self._all[plo:plo + max(phi - plo, 1)]
+        ppr.score_out = {"score": view.numpy() if dev.type == "cpu" else view}
+
+    def __getattr__(self, name):  # only reached for names the wrapper does not define
+        if name in ("scorer", "ppr"):
+            raise AttributeError(name)
+        return getattr(self.ppr, name)
+
+    @property
+    def M(self):
+        return self.scorer.M
+
+    @property
+    def score_out(self):
+        return getattr(self.scorer, "score_out", None)
+
+    def score(self):
+        """The rank's scoring, then the all-gather of every rank's scores."""
+        import torch
+        out = self.scorer.score()
+        s, n = out["score"], self.n_score
+        if isinstance(s, np.ndarray):
+            self._pad[:n] = torch.from_numpy(np.ascontiguousarray(s[:n], np.float32))
+        else:
+            self._pad[:n].copy_(s[:n])
+        self.comm.all_gather(self._all[:-1], self._pad)
+        return out
+
+
 def graph_default(comm, cfg, shard=None):
     """Whether RcaStep captures its PageRank solve in a HIP graph: only with KRCA_RCA_GRAPH=1, for
     fixed-iteration solves (tol <= 0: no host read-back between iterations) of a device shard.

@@ -4,7 +4,8 @@ Two ranks rehearsed on one GPU over gloo (KRCA_BENCH_BACKEND=gloo, the ranks sha
 the JSON line reports the ranks of the communicator, and the sharded step (pod-sharded scoring,
 one all-gather per PageRank iteration) ranks the same top-10 as one rank.  At N = 2 the line
 verifies itself (ranks gathered to rank 0, bit-identical to the oracle; sampled scores of every
-rank), carries the CPU baseline and the per-rank / aggregate roofline, and its correlation leg runs
+rank), whether the PageRank rows are the scoring's uniform ranges or Partition.balanced ones (the
+default at N > 1: scores all-gathered once per step), carries the CPU baseline and the per-rank / aggregate roofline, and its correlation leg runs
 the pod-sharded krca/corr_dist.py path with its own exactness check.
 """
 import json
@@ -36,9 +37,17 @@ def run_bench(n, extra=()):
 
 def test_bench_gpus_2_runs_two_ranks():
     one = run_bench(1, ["--profile"])
-    two = run_bench(2)
+    two = run_bench(2, ["--profile"])
+    # the PageRank rows on the scoring's own uniform ranges (no score all-gather)
+    two_u = run_bench(2, ["--ppr-partition", "uniform", "--no-corr", "--no-cpu-baseline"])
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["world_ranks"] == 2
-    assert two["rca_top10"] == one["rca_top10"]
+    assert two["rca_top10"] == one["rca_top10"] == two_u["rca_top10"]
+    # default at N > 1: PageRank on Partition.balanced ranges, scores all-gathered (krca.rca.SplitShard)
+    assert two["config"]["ppr_bounds"] != two["config"]["shard_bounds"], two["config"]
+    assert two_u["config"]["ppr_bounds"] == two_u["config"]["shard_bounds"]
+    vu = two_u["verify"]
+    assert vu["ppr_fixed_point_bit_identical"] and vu["top10_identical"] and vu["n_exceed_flags_bit_exact"], vu
+    assert two["profile"]["krca_ppr_shard_step_folded"]["launches"] == 30
     for line in (one, two):
         v = line["verify"]
         assert v["ppr_fixed_point_bit_identical"] and v["top10_identical"] and v["n_exceed_flags_bit_exact"], v

@@ -38,6 +38,7 @@ for s in "$@"; do
   case $s in
     probe) step probe 60 tools/bin/buffer_range_probe ;;
     tests_new) step tests_new 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "empty_rank or cold_solve_fresh or bench_gpus" ;;
+    bench_n4) step bench_n4 700 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 4 --steps 3 --warmup 1 --no-corr --cpu-runs 2 --cpu-warmup 1 ;;
     bench_n2) step bench_n2 600 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 5 --warmup 2 ;;
     tests_logs) step tests_logs 600 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread -k "log_scan or c2mini or c5 or stream or logs" ;;
     pprw_*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#pprw_}.so; prof $s 300 tools/ppr_bench.py --reps 10; unset KRCA_LIB ;;
@@ -71,6 +72,8 @@ for s in "$@"; do
     repeat_window_unfused) step repeat_window_unfused 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 KRCA_LOG_FUSED=0 ;;
     diag_window) step diag_window 300 python3 -u tools/diag_window_templates.py ;;
     g8_step) step g8_step 400 python3 tools/g8_step_emulation.py ;;
+    g8_dec) step g8_dec 500 python3 tools/g8_step_emulation.py --decoupled 1.0,1.5,2.0 ;;
+    g8_dec_w*) step $s 500 python3 tools/g8_step_emulation.py --world ${s#g8_dec_w} --steps 50 --decoupled 1.5 ;;
     g8_grid) step g8_grid 400 python3 tools/g8_step_emulation.py --ppr-grids 0,1024,512,256 --only-grids ;;
     ppr_head)  # the same profile with the committed tree's code (ab_head/: git archive HEAD, built in place)
       step ppr_head 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ppr_head -o run -- python3 ab_head/tools/prof_kernels.py ppr --reps 5 ;;
