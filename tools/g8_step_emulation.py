@@ -154,69 +154,106 @@ def run_replicated(a, m, hops, cfg, part, g, M, T):
     return res
 
 
-def run_decoupled(a, m, hops, cfg, spart, ppart, gs, gp, M, T):
-    """Scoring and PageRank on different partitions: rank gs's scoring shard (spart's range), then
-    the score exchange (one all-gather of 4 B per pod; a device copy of this rank's slice into the
-    full vector stands in for it), then the PageRank solve of rank gp's rows under ppart (every
-    iteration's exchange a device copy, as run_rank), pipelined as bench.py's two streams.  The
-    job's step is the slowest rank's: gs and gp are the binding ranks of the two partitions."""
+class Pipe:
+    """bench.py's two-stream pipelined step of one rank, built once and timed repeatedly: the scoring
+    of x (rows [slo, shi) of the uniform ranges), then the PageRank solve of rank gp's rows of
+    `part` -- on the same shard (coupled: part's range is the scoring range) or, with split, on a
+    PageRank-only shard seeded from a full score vector into which a device copy lands this rank's
+    scores (standing in for SplitShard's score all-gather)."""
+
+    def __init__(self, a, m, cfg, x, slo, shi, s_slot, part, gp, split):
+        import torch
+        from krca import native
+        from krca.rca import DeviceShard, RcaStep, shard_graph, slice_words
+        self.torch, self.cfg, self.split, self.slo, self.shi = torch, cfg, split, slo, shi
+        G = part.world
+        plo, phi, p_slot = part.range(gp)
+        rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, plo, phi, part)
+        engs = [native.NativeEngine(0) for _ in range(2)]
+        if split:
+            nograph = (np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32))
+            self.scor = [DeviceShard(e, x, *nograph, a.pods, s_slot, G, cfg) for e in engs]
+            self.ppr = [DeviceShard(e, None, rp, col, od, a.pods, p_slot, G, cfg) for e in engs]
+            self.sfull = [torch.zeros(a.pods + p_slot, dtype=torch.float32, device="cuda") for _ in range(2)]
+            for sh, sv in zip(self.ppr, self.sfull):
+                sh.score_out = {"score": sv[plo:plo + max(phi - plo, 1)]}
+        else:
+            self.scor = self.ppr = [DeviceShard(e, x, rp, col, od, a.pods, p_slot, G, cfg) for e in engs]
+        comm = CopyComm(G, gp, slice_words(p_slot))
+        self.steps = [RcaStep(sh, comm, cfg, plo) for sh in self.ppr]
+        self.streams = [torch.cuda.Stream() for _ in range(2)]
+        self.done = None
+        self.info = dict(pagerank_rank=gp, pagerank_pods=phi - plo, pagerank_edges=int(m.row_ptr[phi] - m.row_ptr[plo]),
+                         scoring_pods=shi - slo)
+
+    def enqueue(self, i):
+        torch, j = self.torch, i % 2
+        with torch.cuda.stream(self.streams[j]):
+            if self.done is not None:
+                self.streams[j].wait_event(self.done)
+            self.scor[j].score()
+            self.done = torch.cuda.Event()
+            self.done.record()
+            if self.split:
+                self.sfull[j][self.slo:self.shi].copy_(self.scor[j].score_out["score"][:self.shi - self.slo])
+            self.steps[j].propagate()
+            self.ppr[j].local_topk(self.cfg.k)
+
+    def timed(self, n):
+        torch = self.torch
+        for i in range(4):
+            self.enqueue(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n):
+            self.enqueue(i)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3
+
+    def alone(self):
+        torch, parts = self.torch, {}
+        for name, fn in (("scoring", self.scor[0].score), ("pagerank", self.steps[0].propagate)):
+            ev = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ev.append(e0.elapsed_time(e1))
+            parts[name + "_ms_alone"] = float(np.median(ev))
+        return parts
+
+
+def ab_decoupled(a, m, hops, cfg, slacks, reps, M, T):
+    """The coupled uniform step of the rank with the most edges against SplitShard's step (scoring
+    on uniform rank 0's pods, PageRank on each binding rank of Partition.balanced(edge_slack)),
+    built once and timed in alternation `reps` times (the box's clock drifts between separate runs
+    by more than the difference measured)."""
     import torch
-    from krca import native, synth
-    from krca.rca import DeviceShard, RcaStep, shard_graph, slice_words
-    G = ppart.world
-    slo, shi, s_slot = spart.range(gs)
-    plo, phi, p_slot = ppart.range(gp)
-    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, plo, phi, ppart)
+    from krca import synth
+    from krca.rca import Partition
+    G = a.world
+    spart = Partition.uniform(a.pods, G)
+    g = int(np.argmax(np.diff(m.row_ptr[spart.bounds])))
+    slo, shi, s_slot = spart.range(g)
     x = synth.make_metrics_range(slo, shi, M, T, seed=0, roots=m.roots, hop_sets=hops, device="cuda")
-    engs = [native.NativeEngine(0) for _ in range(2)]
-    scor = [DeviceShard(e, x, np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32), a.pods, s_slot,
-                        G, cfg) for e in engs]
-    ppr = [DeviceShard(e, None, rp, col, od, a.pods, p_slot, G, cfg) for e in engs]
-    sfull = [torch.zeros(a.pods + p_slot, dtype=torch.float32, device="cuda") for _ in range(2)]
-    for sh, sv in zip(ppr, sfull):
-        sh.score_out = {"score": sv[plo:plo + max(phi - plo, 1)]}
-    comm = CopyComm(G, gp, slice_words(p_slot))
-    steps = [RcaStep(sh, comm, cfg, plo) for sh in ppr]
-    streams = [torch.cuda.Stream() for _ in range(2)]
-    done = [None]
-
-    def enqueue(i):
-        j = i % 2
-        with torch.cuda.stream(streams[j]):
-            if done[0] is not None:
-                streams[j].wait_event(done[0])
-            scor[j].score()
-            done[0] = torch.cuda.Event()
-            done[0].record()
-            sfull[j][slo:shi].copy_(scor[j].score_out["score"][:shi - slo])
-            steps[j].propagate()
-            ppr[j].local_topk(cfg.k)
-
-    for i in range(4):
-        enqueue(i)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        enqueue(i)
-    torch.cuda.synchronize()
-    pipe_ms = (time.perf_counter() - t0) / a.steps * 1e3
-    parts = {}
-    for name, fn in (("scoring", scor[0].score), ("pagerank", steps[0].propagate)):
-        ev = []
-        for _ in range(5):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            fn()
-            e1.record()
-            torch.cuda.synchronize()
-            ev.append(e0.elapsed_time(e1))
-        parts[name] = float(np.median(ev))
-    res = dict(scoring_rank=gs, scoring_pods=shi - slo, pagerank_rank=gp, pagerank_pods=phi - plo,
-               pagerank_edges=int(m.row_ptr[phi] - m.row_ptr[plo]), pipelined_ms_per_step=pipe_ms,
-               scoring_ms_alone=parts["scoring"], pagerank_ms_alone=parts["pagerank"])
-    del x, scor, ppr, steps, engs
+    pipes = {f"coupled_rank{g}": Pipe(a, m, cfg, x, slo, shi, s_slot, spart, g, False)}
+    bounds = {}
+    for slack in slacks:
+        ppart = Partition.balanced(m.row_ptr, G, edge_slack=slack)
+        bounds[str(slack)] = [int(b) for b in ppart.bounds]
+        for gp in sorted({int(np.argmax(np.diff(m.row_ptr[ppart.bounds]))), int(np.argmax(np.diff(ppart.bounds)))}):
+            pipes[f"split{slack}_rank{gp}"] = Pipe(a, m, cfg, x, slo, shi, s_slot, ppart, gp, True)
+    times = {k: [] for k in pipes}
+    for _ in range(reps):
+        for k, p in pipes.items():
+            times[k].append(p.timed(a.steps))
+    out = {k: dict(p.info, pipelined_ms_per_step=float(np.median(times[k])), runs=times[k], **p.alone())
+           for k, p in pipes.items()}
+    del pipes, x
     torch.cuda.empty_cache()
-    return res
+    return dict(scoring_rank=g, ppr_bounds=bounds, pipes=out)
 
 
 def main():
@@ -231,7 +268,8 @@ def main():
     ap.add_argument("--only-grids", action="store_true", help="skip the partition / replicated runs")
     ap.add_argument("--decoupled", default="", help="comma list of edge slacks: scoring on the uniform ranges, "
                     "PageRank on Partition.balanced(edge_slack=...) ranges (scores exchanged once per step); "
-                    "runs only these")
+                    "runs only these, timed in alternation with the coupled uniform step")
+    ap.add_argument("--reps", type=int, default=5, help="--decoupled: alternating timed runs per pipeline")
     a = ap.parse_args()
     from krca import synth
     from krca.rca import RANKING, Partition
@@ -256,20 +294,7 @@ def main():
             print(json.dumps(out), flush=True)
             return
     if a.decoupled:
-        spart = Partition.uniform(a.pods, G)
-        gs = int(np.argmax(np.diff(spart.bounds)))
-        out["decoupled"] = {}
-        part = Partition.uniform(a.pods, G)
-        g = int(np.argmax(np.diff(m.row_ptr[part.bounds])))
-        out["uniform_coupled"] = dict(rank=g, **run_rank(a, m, hops, cfg, part, g, M, T))
-        for slack in [float(v) for v in a.decoupled.split(",")]:
-            ppart = Partition.balanced(m.row_ptr, G, edge_slack=slack)
-            edges = np.diff(m.row_ptr[ppart.bounds])
-            pods = np.diff(ppart.bounds)
-            res = {f"ppr_rank{gp}": run_decoupled(a, m, hops, cfg, spart, ppart, gs, gp, M, T)
-                   for gp in sorted({int(np.argmax(edges)), int(np.argmax(pods))})}
-            out["decoupled"][str(slack)] = dict(bounds=[int(b) for b in ppart.bounds], ranks=res,
-                                                step_ms_bound=max(r["pipelined_ms_per_step"] for r in res.values()))
+        out["decoupled_ab"] = ab_decoupled(a, m, hops, cfg, [float(v) for v in a.decoupled.split(",")], a.reps, M, T)
         print(json.dumps(out), flush=True)
         return
     for pname, part in (("uniform", Partition.uniform(a.pods, G)), ("balanced", Partition.balanced(m.row_ptr, G))):
