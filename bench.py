@@ -480,11 +480,16 @@ def main():
                 streams[j].wait_event(score_done[0])
             if events is not None:
                 events[0].record()
-            shards[j].score()
+            if split:  # the next step's scoring waits for this kernel, not for the score all-gather
+                shards[j].score_local()
+            else:
+                shards[j].score()
             if events is not None:
                 events[1].record()
             score_done[0] = torch.cuda.Event()
             score_done[0].record()
+            if split:
+                shards[j].exchange_scores()
             steps[j].propagate()
             return j, *shards[j].local_topk(cfg.k)
 

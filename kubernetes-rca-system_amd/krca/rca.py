@@ -549,15 +549,24 @@ class SplitShard:
 
     def score(self):
         """The rank's scoring, then the all-gather of every rank's scores."""
+        out = self.score_local()
+        self.exchange_scores()
+        return out
+
+    def score_local(self):
+        """The rank's scoring alone (a pipelined caller orders the next step's scoring after this,
+        not after the exchange)."""
+        return self.scorer.score()
+
+    def exchange_scores(self):
+        """Every rank's scores into the PageRank shard's seed vector (one all-gather)."""
         import torch
-        out = self.scorer.score()
-        s, n = out["score"], self.n_score
+        s, n = self.scorer.score_out["score"], self.n_score
         if isinstance(s, np.ndarray):
             self._pad[:n] = torch.from_numpy(np.ascontiguousarray(s[:n], np.float32))
         else:
             self._pad[:n].copy_(s[:n])
         self.comm.all_gather(self._all[:-1], self._pad)
-        return out
 
 
 def graph_default(comm, cfg, shard=None):
