@@ -52,6 +52,7 @@ for s in "$@"; do
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread ;;
     tests_corr) step tests_corr 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread ;;
     bench) step bench 300 python3 bench.py ;;
+    benchnt_*) v=${s#benchnt_}; export KRCA_PPR_NT=${v%%_*}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline --no-verify; unset KRCA_PPR_NT ;;
     benchq_*) export KRCA_PPR_GRID=${s#benchq_}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline; unset KRCA_PPR_GRID ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_trace) prof bench_trace 400 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
