@@ -203,6 +203,38 @@ __device__ __forceinline__ double dot16_f64(const float* za, const float* zb, in
   return acc;
 }
 
+// dot16_f64 with the row pod's row in LDS and the partner's loads issued eight steps at a time
+// (corr_amb_rescore_grouped): per lane the same products added in the same order, so the same bits
+__device__ __forceinline__ double dot16_f64_pf(const float* za_lds, const float* zb, int T, int sub) {
+  double acc = 0.0;
+  if ((T & 3) == 0) {
+    const float4* va = reinterpret_cast<const float4*>(za_lds);
+    const float4* vb = reinterpret_cast<const float4*>(zb);
+    const int n4 = T / 4;
+    for (int t0 = sub; t0 < n4; t0 += 16 * 8) {
+      float4 y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + 16 * j;
+        y[j] = vb[t < n4 ? t : sub];  // in range: the tail reloads step 0 and adds nothing
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + 16 * j;
+        if (t < n4) {
+          const float4 x = va[t];
+          acc += (double)x.x * (double)y[j].x + (double)x.y * (double)y[j].y + (double)x.z * (double)y[j].z +
+                 (double)x.w * (double)y[j].w;
+        }
+      }
+    }
+  } else {
+    for (int t = sub; t < T; t += 16) acc += (double)za_lds[t] * (double)zb[t];
+  }
+  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  return acc;
+}
+
 // Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh (TC = 256 in every pass):
 // 8 waves (2 row halves x 4 column quarters), each a 128 x 64 tile = 8 x 4 MFMA 16x16 blocks, K
 // steps of 64 through a double-buffered LDS stage (130 KB with the sample pass's parking area: one
@@ -1007,6 +1039,154 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__
   }
 }
 
+// ---- the re-score grouped by row pod (KRCA_CORR_RS_GROUP) -----------------------------------------
+// corr_amb_rescore reads BOTH rows of every listed pair (11.5 KB at T = 1440; C3: 59.6 GB at the
+// DRAM side for 6.5M pairs, 14 % L2 hits).  Grouped, a wave holds the row pod's z32 row in LDS and
+// reads only the partner rows: a counting sort of the list by row pod (histogram, scan, scatter),
+// then one wave per pod.  The dot products are dot16_f64's, same lanes and order: same bits.
+constexpr int GSCAN = 4 * TPB;  // pods per scan block
+
+__global__ __launch_bounds__(TPB) void corr_amb_hist(const int2* __restrict__ amb, const unsigned long long* __restrict__ amb_n,
+                                                     int64_t cap, int32_t* __restrict__ gcnt) {
+  const int64_t n = (int64_t)min(*amb_n, (unsigned long long)cap);
+  for (int64_t q = (int64_t)blockIdx.x * TPB + threadIdx.x; q < n; q += (int64_t)gridDim.x * TPB)
+    atomicAdd(&gcnt[amb[q].x], 1);
+}
+
+// exclusive scan of TPB x 4 values in LDS order (thread t holds v[4 t .. 4 t + 3]); returns the total
+__device__ __forceinline__ int32_t block_scan4(int32_t (&v)[4], int32_t* sh) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int32_t s = v[0] + v[1] + v[2] + v[3];
+  int32_t incl = s;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) sh[wv] = incl;
+  __syncthreads();
+  int32_t base = 0, total = 0;
+  for (int w = 0; w < TPB / 64; ++w) {
+    base += w < wv ? sh[w] : 0;
+    total += sh[w];
+  }
+  __syncthreads();
+  int32_t run = base + incl - s;
+  for (int j = 0; j < 4; ++j) {
+    const int32_t x = v[j];
+    v[j] = run;
+    run += x;
+  }
+  return total;
+}
+
+__global__ __launch_bounds__(TPB) void corr_scan_blocks(const int32_t* __restrict__ gcnt, int64_t P, int32_t* __restrict__ gsum) {
+  __shared__ int32_t sh[TPB / 64];
+  int32_t v[4];
+  const int64_t i0 = (int64_t)blockIdx.x * GSCAN + 4 * threadIdx.x;
+  for (int j = 0; j < 4; ++j) v[j] = i0 + j < P ? gcnt[i0 + j] : 0;
+  const int32_t tot = block_scan4(v, sh);
+  if (threadIdx.x == 0) gsum[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive scan of the nb block totals, in place
+__global__ __launch_bounds__(TPB) void corr_scan_top(int32_t* __restrict__ gsum, int64_t nb) {
+  __shared__ int32_t sh[TPB / 64];
+  int32_t carry = 0;
+  for (int64_t c = 0; c < nb; c += GSCAN) {
+    int32_t v[4];
+    const int64_t i0 = c + 4 * threadIdx.x;
+    for (int j = 0; j < 4; ++j) v[j] = i0 + j < nb ? gsum[i0 + j] : 0;
+    const int32_t tot = block_scan4(v, sh);
+    for (int j = 0; j < 4; ++j)
+      if (i0 + j < nb) gsum[i0 + j] = v[j] + carry;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+// goff[p] = exclusive prefix of gcnt (goff[P] = the list length), gcur = goff (scatter cursors)
+__global__ __launch_bounds__(TPB) void corr_scan_apply(const int32_t* __restrict__ gcnt, int64_t P,
+                                                       const int32_t* __restrict__ gsum, int32_t* __restrict__ goff,
+                                                       int32_t* __restrict__ gcur) {
+  __shared__ int32_t sh[TPB / 64];
+  int32_t v[4], c[4];
+  const int64_t i0 = (int64_t)blockIdx.x * GSCAN + 4 * threadIdx.x;
+  for (int j = 0; j < 4; ++j) c[j] = v[j] = i0 + j < P ? gcnt[i0 + j] : 0;
+  const int32_t tot = block_scan4(v, sh);
+  const int32_t base = gsum[blockIdx.x];
+  for (int j = 0; j < 4; ++j)
+    if (i0 + j < P) {
+      goff[i0 + j] = gcur[i0 + j] = base + v[j];
+      if (i0 + j == P - 1) goff[P] = base + v[j] + c[j];
+    }
+  (void)tot;
+}
+
+// entries by row pod: {partner | AMB_BOTH, screening value bits} (order within a pod is free: the
+// counts are integer sums)
+__global__ __launch_bounds__(TPB) void corr_amb_scatter(const int2* __restrict__ amb, const float* __restrict__ ambv,
+                                                        const unsigned long long* __restrict__ amb_n, int64_t cap,
+                                                        int32_t* __restrict__ gcur, int2* __restrict__ gs) {
+  const int64_t n = (int64_t)min(*amb_n, (unsigned long long)cap);
+  for (int64_t q = (int64_t)blockIdx.x * TPB + threadIdx.x; q < n; q += (int64_t)gridDim.x * TPB) {
+    const int2 e = amb[q];
+    const int32_t pos = atomicAdd(&gcur[e.x], 1);
+    gs[pos] = make_int2(e.y, __float_as_int(ambv[q]));
+  }
+}
+
+// one wave per row pod with entries (persistent over the pods): its z32 row into the wave's LDS
+// slot, then 4 groups of 16 lanes take its partners, corr_amb_rescore's decision for each
+constexpr int RS_WAVES = TPB / 64;
+__global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* __restrict__ goff, const int2* __restrict__ gs,
+                                                                int64_t P, const float* __restrict__ z32,
+                                                                const float* __restrict__ dn, int T, float tau,
+                                                                float acc_err, int32_t* __restrict__ count) {
+  extern __shared__ float4 rs_lds[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane & 15, grp = lane >> 4;
+  const int T4 = (T + 3) / 4;
+  float* ra = reinterpret_cast<float*>(rs_lds + (size_t)wv * T4);
+  for (int64_t a = (int64_t)blockIdx.x * RS_WAVES + wv; a < P; a += (int64_t)gridDim.x * RS_WAVES) {
+    const int32_t e0 = goff[a], e1 = goff[a + 1];
+    if (e0 == e1) continue;  // wave-uniform
+    const float* za = z32 + a * T;
+    if ((T & 3) == 0) {
+      for (int t = lane; t < T4; t += 64) rs_lds[(size_t)wv * T4 + t] = reinterpret_cast<const float4*>(za)[t];
+    } else {
+      for (int t = lane; t < T; t += 64) ra[t] = za[t];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double sa = (double)dn[a];
+    int hits = 0;
+    for (int32_t q = e0 + grp; q < e1; q += 4) {
+      const int2 e = gs[q];
+      const int64_t b = e.x & (AMB_BOTH - 1);
+      const double sb = (double)dn[b];
+      const double band = sa + sb + 3.0 * sa * sb + (double)acc_err + 1e-9;
+      const double v = fabs((double)__int_as_float(e.y));
+      int hit;
+      if (v > (double)tau + band) {
+        hit = 1;
+      } else if (v <= (double)tau - band) {
+        hit = 0;
+      } else {
+        hit = fabs(dot16_f64_pf(ra, z32 + b * T, T, sub)) > (double)tau;
+      }
+      if (sub == 0 && hit) {
+        ++hits;
+        if (e.x & AMB_BOTH) atomicAdd(&count[b], 1);
+      }
+    }
+    if (sub == 0 && hits) atomicAdd(&count[a], hits);
+    // every lane is past its partners before the next pod's row lands in the slot
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // ---- merge + exact re-scoring ------------------------------------------------------------------
 __device__ __forceinline__ bool cbetter(float a, int32_t ia, float b, int32_t ib) {
   if (ib < 0) return ia >= 0;
@@ -1357,6 +1537,8 @@ struct CorrWs {  // views into a caller's candidate workspace
   int nlist;            // lists in use (2 when the main pass runs in more than one batch)
   float* dn;            // [P] fp16 rounding-error norm of each row
   unsigned long long* amb_n;  // [2]: the lists' fill
+  int32_t *gcnt, *goff, *gcur, *gsum;  // grouped re-score: entries per row pod, offsets [P + 1], cursors, scan blocks
+  int2* gs;                            // [amb_cap] a list's entries grouped by row pod
   uint16_t* zs;         // [RECT_ROWS][Tp]
   int2* lbuf;           // sharded: [n_loc][CAPC] received candidates of the rank's pods
   int32_t* fill;        // sharded: [n_loc]
@@ -1397,6 +1579,11 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
   }
   w.dn = reinterpret_cast<float*>(take(P));
   w.amb_n = reinterpret_cast<unsigned long long*>(take(4));
+  w.gcnt = reinterpret_cast<int32_t*>(take(P));
+  w.goff = reinterpret_cast<int32_t*>(take(P + 1));
+  w.gcur = reinterpret_cast<int32_t*>(take(P));
+  w.gsum = reinterpret_cast<int32_t*>(take(krca::ceil_div(P, GSCAN) + 1));
+  w.gs = reinterpret_cast<int2*>(take(2 * w.amb_cap));
   w.zs = reinterpret_cast<uint16_t*>(take((int64_t)RECT_ROWS * Tp / 2));
   if (G > 0) {
     w.lbuf = reinterpret_cast<int2*>(take(2 * n_loc * CAPC));
@@ -1492,7 +1679,31 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
 // exact |r| > tau counts of the ambiguous pairs in list l (float64 from z32), added to count
 int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int32_t* count, hipStream_t st) {
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
-  hipLaunchKernelGGL(corr_amb_rescore, dim3((unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7)), dim3(TPB), 0, st,
+  const unsigned grid = (unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7);
+  const size_t lds = (size_t)RS_WAVES * ((d.T + 3) / 4) * sizeof(float4);
+  if (krca::tuning().corr_rs_group && lds <= 64 * 1024 && d.P > 0) {  // grouped by row pod (above)
+    const int64_t nb = krca::ceil_div(d.P, GSCAN);
+    KRCA_HIP(hipMemsetAsync(ws.gcnt, 0, (size_t)d.P * sizeof(int32_t), st));
+    hipLaunchKernelGGL(corr_amb_hist, dim3(grid), dim3(TPB), 0, st, (const int2*)ws.amb[l],
+                       (const unsigned long long*)(ws.amb_n + l), ws.amb_cap, ws.gcnt);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(corr_scan_blocks, dim3((unsigned)nb), dim3(TPB), 0, st, (const int32_t*)ws.gcnt, d.P, ws.gsum);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(corr_scan_top, dim3(1), dim3(TPB), 0, st, ws.gsum, nb);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(corr_scan_apply, dim3((unsigned)nb), dim3(TPB), 0, st, (const int32_t*)ws.gcnt, d.P,
+                       (const int32_t*)ws.gsum, ws.goff, ws.gcur);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(corr_amb_scatter, dim3(grid), dim3(TPB), 0, st, (const int2*)ws.amb[l], (const float*)ws.ambv[l],
+                       (const unsigned long long*)(ws.amb_n + l), ws.amb_cap, ws.gcur, ws.gs);
+    KRCA_LAUNCH_CHECK();
+    const unsigned gg = (unsigned)std::min<int64_t>(krca::ceil_div(d.P, RS_WAVES), 2048);
+    hipLaunchKernelGGL(corr_amb_rescore_grouped, dim3(gg), dim3(TPB), lds, st, (const int32_t*)ws.goff,
+                       (const int2*)ws.gs, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
+    KRCA_LAUNCH_CHECK();
+    return KRCA_OK;
+  }
+  hipLaunchKernelGGL(corr_amb_rescore, dim3(grid), dim3(TPB), 0, st,
                      (const int2*)ws.amb[l], (const float*)ws.ambv[l], (const unsigned long long*)(ws.amb_n + l),
                      ws.amb_cap, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
   KRCA_LAUNCH_CHECK();

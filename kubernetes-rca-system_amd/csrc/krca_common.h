@@ -106,6 +106,7 @@ struct Tuning {
   int ppr_nt;       // KRCA_PPR_NT: the step streams its plan / column / row arrays with non-temporal loads
   int ppr_xcd;      // KRCA_PPR_XCD: each XCD's workgroups take one contiguous eighth of the plan entries
   int log_fused;    // KRCA_LOG_FUSED: krca_log_scan walks the DFA inside the line-index pass (0 = index, then log_dfa)
+  int corr_rs_group;  // KRCA_CORR_RS_GROUP: the ambiguous pairs re-scored grouped by row pod (row in LDS; 0 = per pair)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

@@ -170,22 +170,25 @@ def test_corr_odd_sample_self_products(eng):
 
 def test_corr_batches_and_full_lists_identical(eng):
     """The main pass in many batches (KRCA_CORR_BATCH) and with ambiguous lists that fill at once
-    (KRCA_CORR_AMB_TILE = 0: every tile decides its pairs in place; 8: mixed) gives the same outputs
-    bit for bit as the default run (the same float64 re-score in the tile and in the list kernel)."""
+    (KRCA_CORR_AMB_TILE = 0: every tile decides its pairs in place; 8: mixed), and the list re-scored
+    pair by pair instead of grouped by row pod (KRCA_CORR_RS_GROUP = 0), give the same outputs bit for
+    bit as the default run (the same float64 re-score in the tile and in either list kernel)."""
     P, T, k = 40_000, 1440, 10
     x = synth.make_metrics(P, 1, T, seed=3, group_size=20, device="cuda")
     ref = eng.corr_topk(x, k=k, tau=TAU)
     lib = eng.lib
     try:
-        for batch, per_tile in ((4, -1), (0, 0), (3, 8)):
+        for batch, per_tile, group in ((4, -1, 1), (0, 0, 1), (3, 8, 1), (0, -1, 0), (4, -1, 0)):
             assert lib.krca_tune_set(b"KRCA_CORR_BATCH", batch) == 0
             assert lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", per_tile) == 0
+            assert lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", group) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
             for key in ref:
-                assert np.array_equal(got[key], ref[key]), (batch, per_tile, key)
+                assert np.array_equal(got[key], ref[key]), (batch, per_tile, group, key)
     finally:
         lib.krca_tune_set(b"KRCA_CORR_BATCH", 0)
         lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", -1)
+        lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", 1)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
     _, _, bad = device_check(ref, z, [rows], k)

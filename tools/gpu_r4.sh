@@ -50,6 +50,7 @@ for s in "$@"; do
     log_timing2) export KRCA_LOG_FUSED=2 KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing2 300 python3 tools/log_timing.py; unset KRCA_LIB KRCA_LOG_FUSED ;;
     logs_unfused) export KRCA_LOG_FUSED=0; prof logs_unfused 300 tools/prof_kernels.py logs --reps 5; unset KRCA_LOG_FUSED ;;
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread ;;
+    tests_corrq) step tests_corrq 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread -k "batches or c3_every or full_vs" ;;
     tests_corr) step tests_corr 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread ;;
     bench) step bench 300 python3 bench.py ;;
     benchnt_*) v=${s#benchnt_}; export KRCA_PPR_NT=${v%%_*}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline --no-verify; unset KRCA_PPR_NT ;;
@@ -59,6 +60,8 @@ for s in "$@"; do
     bench_trace_full) prof bench_trace_full 700 bench.py ;;
     corr100k) prof corr100k 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5 ;;
     corr100k_w*) export KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_${s#corr100k_}.so; prof $s 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5; unset KRCA_LIB ;;
+    corrg_*) v=${s#corrg_}; export KRCA_CORR_RS_GROUP=${v%%_*}; prof $s 300 tools/prof_kernels.py corr --pods 100000 --reps 3 --tau 0.5; unset KRCA_CORR_RS_GROUP ;;
+    corr1mg_*) v=${s#corr1mg_}; export KRCA_CORR_RS_GROUP=${v%%_*}; step $s 300 python3 tools/prof_kernels.py corr --pods 1000000 --reps 1 --tau 0.5; unset KRCA_CORR_RS_GROUP ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 --tau 0.5 ;;
     corr_batch)  # C3 with the main pass in smaller batches: re-scores of batch b beside the tiles of b + 1
       for b in 128 256 512; do
