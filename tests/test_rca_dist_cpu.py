@@ -65,10 +65,12 @@ def _worker(rank, world, port, out_q, balanced=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balanced", [(2, False), (3, False), (2, True), (4, True), (3, "split")])
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, False), (2, True), (4, True), (3, "split"), (7, "split")])
 def test_sharded_rca_matches_single_process_oracle(world, balanced):
     """Uniform ranges and pods + in-edges balanced ranges (krca.rca.Partition: ranges of different
-    lengths, columns in the exchange layout's virtual ids): the same bits either way."""
+    lengths, columns in the exchange layout's virtual ids), and the split form (scoring uniform,
+    PageRank balanced, scores all-gathered; world 7: the last uniform range is short, so the
+    gathered scores carry padding): the same bits every way."""
     import oracle
     from krca.rca import Config
     ctx = mp.get_context("spawn")
