@@ -138,7 +138,11 @@ def profile_step(step, stream, world):
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
-        timed("krca_rolling_score", s.score)
+        if hasattr(s, "score_local"):  # SplitShard: the scoring, then the score all-gather
+            timed("krca_rolling_score", s.score_local)
+            timed("score_exchange", s.exchange_scores)
+        else:
+            timed("krca_rolling_score", s.score)
         # the sequence RcaStep._propagate runs: init, exchange, iters x (folded step, exchange), finish
         timed("krca_ppr_shard_init", lambda: s.init(cfg.alpha, cfg.floor(s.N, s.M)))
         timed("exchange", lambda: c.exchange(s))

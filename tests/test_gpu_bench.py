@@ -48,6 +48,7 @@ def test_bench_gpus_2_runs_two_ranks():
     vu = two_u["verify"]
     assert vu["ppr_fixed_point_bit_identical"] and vu["top10_identical"] and vu["n_exceed_flags_bit_exact"], vu
     assert two["profile"]["krca_ppr_shard_step_folded"]["launches"] == 30
+    assert two["profile"]["score_exchange"]["launches"] == 1 and two["profile"]["krca_rolling_score"]["launches"] == 1
     for line in (one, two):
         v = line["verify"]
         assert v["ppr_fixed_point_bit_identical"] and v["top10_identical"] and v["n_exceed_flags_bit_exact"], v
