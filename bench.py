@@ -50,7 +50,7 @@ def parse(argv=None):
                     help="personalization floor in |z| units (default: krca.rca.Config's scale-aware floor)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample-pods", type=int, default=25_000)
-    ap.add_argument("--cpu-warmup", type=int, default=3)
+    ap.add_argument("--cpu-warmup", type=int, default=5)  # 5 warm-up + >= 20 timed runs
     ap.add_argument("--cpu-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
