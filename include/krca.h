@@ -79,6 +79,7 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
 #define KRCA_SCORE_RING_BUF 2
 #define KRCA_SCORE_REREAD 3
 #define KRCA_SCORE_PIPE_ROWS 4
+#define KRCA_SCORE_LDS 5 /* A/B (KRCA_SCORE_IMPL=5, W = 60): rows staged by LDS-DMA, 1 KiB per wave instruction */
 int krca_rolling_score_variant(int64_t P, int32_t M, int32_t T, int32_t W);
 
 /* ---- a11/a12: 13-category log histograms (ref:agents/logs_agent.py:124-181) ----------------

@@ -310,6 +310,92 @@ __global__ __launch_bounds__(256) void rolling_score_pipe(const float* __restric
   pod_epilogue(st, epsB, s, active, M, T, x + (active ? s : 0), S, z_last, score, n_exceed, flags);
 }
 
+// LDS-DMA form of rolling_score_pipe (KRCA_SCORE_IMPL=5, A/B; same steps in the same order, same
+// bits).  The workgroup's 256 series of a time row are 1 KiB contiguous: ONE wave instruction
+// (global_load_lds_dwordx4, 16 B per lane) lands a whole row in LDS, instead of four 256-B register
+// loads; a C-row chunk is C / 4 such instructions per wave, double-buffered (2 x C KiB), the next
+// chunk's in flight while the current one is stepped from LDS.  Needs S % 4 == 0 (16-B aligned rows);
+// the last workgroup's lanes past S re-read its first piece (their values are never used).
+template <int W, int C, int AUX>
+__global__ __launch_bounds__(256) void rolling_score_lds(const float* __restrict__ x, int64_t S, int T, int M,
+                                                         double thr2, float* __restrict__ z_last,
+                                                         float* __restrict__ score, int32_t* __restrict__ n_exceed,
+                                                         uint8_t* __restrict__ flags) {
+  static_assert(W % C == 0 && C % 4 == 0, "chunk must divide the window and split over 4 waves");
+  constexpr int NC = W / C;
+  __shared__ float stage[2][C][256];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t s0 = (int64_t)blockIdx.x * 256;
+  const int64_t s = s0 + tid;
+  const bool active = s < S;
+  const int64_t piece = s0 + 4 * lane < S ? s0 + 4 * lane : s0;
+  // rows [t, t + C) of the workgroup's series into stage[buf]; rows >= T are not loaded (never read)
+  auto dma = [&](int buf, int t) {
+#pragma unroll
+    for (int q = 0; q < C / 4; ++q) {
+      const int j = wv + 4 * q;
+      if (t + j < T)
+        __builtin_amdgcn_global_load_lds(x + (int64_t)(t + j) * S + piece,
+                                         (__attribute__((address_space(3))) void*)&stage[buf][j][0], 16, 0, AUX);
+    }
+  };
+  auto landed = [&]() {  // this wave's DMA done, then every wave's
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  const double Wd = (double)W, epsB = kVarEps * Wd * Wd;
+  StepState st{0.0, 0.0, 0, 0.0, 0.0};
+  float ring[W];
+  // prologue: chunks 0 .. NC-1 fill the window (requires T > W, checked by the launcher)
+  dma(0, 0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    landed();
+    dma((c + 1) & 1, (c + 1) * C);  // the next chunk (chunk NC: the first rows past the window)
+#pragma unroll
+    for (int j = 0; j < C; ++j) ring[c * C + j] = stage[c & 1][j][tid];
+  }
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const double vd = (double)ring[j];
+    st.s1 = st.s1 + vd;
+    st.s2 = fma(vd, vd, st.s2);
+  }
+  int k = NC;  // chunk k = rows [k C, k C + C) is in flight into stage[k & 1]
+  int t0 = W;
+  for (; t0 + W < T; t0 += W) {  // full blocks that do not contain t = T-1
+#pragma unroll
+    for (int c = 0; c < NC; ++c, ++k) {
+      landed();
+      dma((k + 1) & 1, (k + 1) * C);
+      const int b = k & 1;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const float v = stage[b][j][tid];
+        step(st, v, ring[c * C + j], Wd, epsB, thr2, false);
+        ring[c * C + j] = v;
+      }
+    }
+  }
+  // final block: rows [t0, T), 1..W of them
+#pragma unroll
+  for (int c = 0; c < NC; ++c, ++k) {
+    landed();
+    if (c + 1 < NC) dma((k + 1) & 1, (k + 1) * C);
+    const int b = k & 1;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int t = t0 + c * C + j;
+      if (t < T) {
+        const float v = stage[b][j][tid];
+        step(st, v, ring[c * C + j], Wd, epsB, thr2, t == T - 1);
+        ring[c * C + j] = v;
+      }
+    }
+  }
+  pod_epilogue(st, epsB, s, active, M, T, x + (active ? s : 0), S, z_last, score, n_exceed, flags);
+}
+
 // Any W: the outgoing sample x[t-W] is re-read (same values, same arithmetic -> same bits).
 __global__ __launch_bounds__(256) void rolling_score_reread(const float* __restrict__ x, int64_t S, int T, int W,
                                                             int M, double thr2, float* __restrict__ z_last,
@@ -451,6 +537,7 @@ int krca_rolling_score_variant(int64_t P, int32_t M, int32_t T, int32_t W) {
   const int64_t S = P * (int64_t)M;
   if (!pipe_window(W)) return KRCA_SCORE_REREAD;
   if (tu.score_impl == KRCA_SCORE_PIPE_ROWS && T > W) return KRCA_SCORE_PIPE_ROWS;  // A/B: forced
+  if (tu.score_impl == KRCA_SCORE_LDS && T > W && W == 60 && S % 4 == 0) return KRCA_SCORE_LDS;  // A/B
   if (tu.score_impl == 0 && T > W) {
     return S * 4 * rows_per_chunk(W) < (int64_t(1) << 31) ? KRCA_SCORE_PIPE : KRCA_SCORE_PIPE_ROWS;
   }
@@ -491,7 +578,14 @@ int krca_rolling_score(const float* x, int64_t P, int32_t M, int32_t T, int32_t 
     hipLaunchKernelGGL(rolling_score_ring<WV>, grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed,  \
                        flags);
   const bool pipe = variant == KRCA_SCORE_PIPE || variant == KRCA_SCORE_PIPE_ROWS;
-  switch (W) {
+  if (variant == KRCA_SCORE_LDS) {  // W = 60, C = 20 only
+    if (nt)
+      hipLaunchKernelGGL((rolling_score_lds<60, 20, 2>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed,
+                         flags);
+    else
+      hipLaunchKernelGGL((rolling_score_lds<60, 20, 0>), grid, block, 0, st, x, S, T, M, thr2, z_last, score, n_exceed,
+                         flags);
+  } else switch (W) {
     case 60:
       if (pipe && chunk == 10) { KRCA_PIPE(60, 10) }
       else if (pipe && chunk == 12) { KRCA_PIPE(60, 12) }

@@ -106,7 +106,7 @@ SIGNATURES = {
 
 KRCA_ENOTCONV = -70
 PPR_RESIDUAL, PPR_WRITE_R = 1, 2  # krca_ppr_shard_step flags
-SCORE_VARIANTS = {0: "pipe", 1: "ring", 2: "ring_buf", 3: "reread", 4: "pipe_rows"}  # krca_rolling_score_variant
+SCORE_VARIANTS = {0: "pipe", 1: "ring", 2: "ring_buf", 3: "reread", 4: "pipe_rows", 5: "lds"}  # krca_rolling_score_variant
 
 
 class KrcaError(RuntimeError):

@@ -103,6 +103,9 @@ def test_tuning_knobs_and_score_variant():
     assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 500, 7)] == "reread"  # any W
     with native.tune(lib, KRCA_SCORE_IMPL=2):
         assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 1440, 60)] == "ring_buf"
+    with native.tune(lib, KRCA_SCORE_IMPL=5):
+        assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1_000_000, 8, 1440, 60)] == "lds"
+        assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 500, 30)] == "ring"  # W != 60
     with native.tune(lib, KRCA_SCORE_IMPL=4):
         assert native.SCORE_VARIANTS[lib.krca_rolling_score_variant(1000, 8, 1440, 60)] == "pipe_rows"
     assert lib.krca_tune_get(b"KRCA_SCORE_IMPL", ctypes.byref(v)) == 0 and v.value == 0  # restored

@@ -70,12 +70,12 @@ def test_rolling_score_non_finite_samples_as_oracle(eng):
     assert np.allclose(got["score"].cpu().numpy(), ref["score"], rtol=1e-5, atol=1e-6, equal_nan=True)
 
 
-SCORE_VARIANTS = [("2", "20"), ("1", "20"), ("4", "20"), ("4", "15")] + [("0", c) for c in ("10", "12", "15", "20", "30")]
+SCORE_VARIANTS = [("2", "20"), ("1", "20"), ("4", "20"), ("4", "15"), ("5", "20")] + [("0", c) for c in ("10", "12", "15", "20", "30")]
 
 
 @pytest.mark.parametrize("P,M,T,W", [(1000, 8, 1440, 60), (128, 8, 61, 60), (129, 8, 139, 60), (700, 8, 200, 30)])
 def test_rolling_score_kernel_variants_bit_exact(eng, monkeypatch, P, M, T, W):
-    """Every kernel form (W-block buffer loads, plain loads, pipelined chunks) = the C oracle."""
+    """Every kernel form (W-block buffer loads, plain loads, pipelined chunks, LDS-DMA rows) = the C oracle."""
     x = synth.make_metrics(P, M, T, window=W, seed=P + T + 1, roots=np.arange(0, P, 9))
     ref = oracle.c_rolling_score(x.numpy(), W, 3.0)
     xd = x.cuda()

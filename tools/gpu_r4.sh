@@ -53,6 +53,8 @@ for s in "$@"; do
     tests_corrq) step tests_corrq 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread -k "batches or c3_every or full_vs" ;;
     tests_corr) step tests_corr 600 python3 -u -m pytest tests/test_gpu_corr.py -x -v -rP --timeout 240 --timeout-method thread ;;
     bench) step bench 300 python3 bench.py ;;
+    score_lds) step score_lds 300 python3 tools/score_ab.py --only pipe_c20,lds,lds_default_policy --rounds 3 --reps 5 ;;
+    tests_score) step tests_score 300 python3 -u -m pytest tests/test_gpu_kernels.py -x -v -rP --timeout 120 --timeout-method thread -k "rolling_score" ;;
     benchnt_*) v=${s#benchnt_}; export KRCA_PPR_NT=${v%%_*}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline --no-verify; unset KRCA_PPR_NT ;;
     benchq_*) export KRCA_PPR_GRID=${s#benchq_}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline; unset KRCA_PPR_GRID ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
