@@ -1681,7 +1681,8 @@ int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   const unsigned grid = (unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7);
   const size_t lds = (size_t)RS_WAVES * ((d.T + 3) / 4) * sizeof(float4);
-  if (krca::tuning().corr_rs_group && lds <= 64 * 1024 && d.P > 0) {  // grouped by row pod (above)
+  // grouped by row pod (above); its offsets are int32 (a list of up to 2^31 - 1 entries)
+  if (krca::tuning().corr_rs_group && lds <= 64 * 1024 && d.P > 0 && ws.amb_cap < (int64_t(1) << 31)) {
     const int64_t nb = krca::ceil_div(d.P, GSCAN);
     KRCA_HIP(hipMemsetAsync(ws.gcnt, 0, (size_t)d.P * sizeof(int32_t), st));
     hipLaunchKernelGGL(corr_amb_hist, dim3(grid), dim3(TPB), 0, st, (const int2*)ws.amb[l],
