@@ -173,3 +173,26 @@ def test_partition_balanced_ranges():
     assert np.array_equal(u.virtual(np.arange(20000)), np.arange(20000))
     hub = Partition.balanced(m.row_ptr, 8)  # the hub services at low ids: a short first range
     assert hub.bounds[1] < 20000 // 8 and np.max(np.diff(m.row_ptr[hub.bounds])) <= 1.5 * EDGE_SLACK * E / 8
+
+
+def test_split_shard_rejects_partitions_it_cannot_gather():
+    """SplitShard needs uniform scoring ranges (the gathered scores are then in pod order), two
+    partitions of the same pods over the same ranks, and more than one rank."""
+    import torch
+    from krca.rca import Comm, Partition, SplitShard
+
+    class Stub:
+        def __init__(self):
+            self.send = torch.zeros(4, dtype=torch.int64)
+
+    m, _ = _mesh()
+    bal = Partition.balanced(m.row_ptr, 3)
+    uni = Partition.uniform(N, 3)
+    assert not np.array_equal(bal.bounds, uni.bounds)
+    for spart, ppart, world in ((bal, bal, 3), (uni, Partition.uniform(N, 2), 3), (Partition.uniform(N, 1),
+                                                                                   Partition.uniform(N, 1), 1)):
+        with pytest.raises(ValueError):
+            SplitShard(Stub(), Stub(), spart, ppart, 0, Comm(world, 0))
+    s = SplitShard(Stub(), Stub(), uni, bal, 1, Comm(3, 1))
+    lo, hi, _ = bal.range(1)
+    assert s.ppr.score_out["score"].shape == (hi - lo,)
