@@ -17,6 +17,10 @@ iteration is one kernel and one exchange.  With one rank the exchange is a swap
 of two buffers (the step kernel reads one and writes the other).  Arithmetic is integer fixed
 point: the result is bit-identical for any G and to oracle/krca_oracle.c.  The final top-k merges G x k candidates.
 
+A rank's PageRank rows need not be the pods it scores: :class:`SplitShard` (the bench's default at
+G > 1) scores a uniform range, all-gathers the scores once per step, and solves on an edge-balanced
+:class:`Partition` range.
+
 The per-rank numeric work is behind a small backend interface so the same orchestration runs
 on the device (:class:`DeviceShard`, libkrca) and, in the CPU test-suite, on a NumPy restatement
 with the gloo backend (tests/test_rca_dist_cpu.py).
