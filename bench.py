@@ -61,9 +61,10 @@ def parse(argv=None):
     ap.add_argument("--corr-k", type=int, default=10)
     ap.add_argument("--corr-runs", type=int, default=3, help="timed correlation calls (after one warm-up call)")
     ap.add_argument("--corr-check-rows", type=int, default=512)
-    ap.add_argument("--ppr-partition", choices=("balanced", "uniform"), default="balanced",
+    ap.add_argument("--ppr-partition", choices=("balanced", "uniform", "replicated"), default="balanced",
                     help="G > 1: PageRank rows on Partition.balanced ranges (scores all-gathered once per step, "
-                         "krca.rca.SplitShard) or on the scoring's uniform ranges")
+                         "krca.rca.SplitShard), on the scoring's uniform ranges, or the whole mesh's solve on "
+                         "every rank (scores all-gathered, no collective inside the solve)")
     ap.add_argument("--ppr-edge-slack", type=float, default=1.5,
                     help="Partition.balanced's in-edge cap per rank, in multiples of E / G")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -237,8 +238,8 @@ def verify_step(args, cfg, mesh, shard, x, part, ppart, rank):
     import oracle
     lo, hi, n_max = part.range(rank)
     world, n_loc = part.world, hi - lo
-    plo, phi, p_slot = ppart.range(rank)
-    r_all = ppart.unpad(gather_rows(shard.r[:phi - plo], p_slot, world).cpu().numpy())
+    plo, phi, p_slot = ppart.range(rank if ppart.world > 1 else 0)  # one range: the replicated solve
+    r_all = ppart.unpad(gather_rows(shard.r[:phi - plo], p_slot, ppart.world).cpu().numpy())
     sc_all = part.unpad(gather_rows(shard.score_out["score"][:n_loc], n_max, world).cpu().numpy())
     ns = min(max(1, 2000 // world), n_loc)
     samp = np.sort(np.random.default_rng(1 + rank).choice(n_loc, size=ns, replace=False))
@@ -451,9 +452,11 @@ def main():
     # the PageRank rows: at G > 1 by default Partition.balanced ranges, so that the hub services'
     # in-edges do not all land on rank 0 (10.6M of 20M at G = 8 with uniform ranges); the scores
     # then travel in one all-gather per step (krca.rca.SplitShard)
-    split = world > 1 and args.ppr_partition == "balanced"
-    ppart = Partition.balanced(mesh.row_ptr, world, edge_slack=args.ppr_edge_slack) if split else part
-    plo, phi, p_slot = ppart.range(rank)
+    split = world > 1 and args.ppr_partition in ("balanced", "replicated")
+    replicated = split and args.ppr_partition == "replicated"
+    ppart = (Partition([0, args.pods]) if replicated else
+             Partition.balanced(mesh.row_ptr, world, edge_slack=args.ppr_edge_slack) if split else part)
+    plo, phi, p_slot = ppart.range(rank if ppart.world > 1 else 0)
     rp, col, od = shard_graph(mesh.row_ptr, mesh.col, mesh.outdeg, plo, phi, ppart)
     x = synth.make_metrics_range(lo, hi, args.metrics, args.tsteps, window=args.window, seed=args.seed,
                                  roots=mesh.roots, hop_sets=hops, device=torch.device("cuda", local))
@@ -464,11 +467,12 @@ def main():
     if split:
         nograph = (np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32))
         shards = [SplitShard(DeviceShard(e, x, *nograph, args.pods, n_max, world, cfg),
-                             DeviceShard(e, None, rp, col, od, args.pods, p_slot, world, cfg), part, ppart, rank, c)
+                             DeviceShard(e, None, rp, col, od, args.pods, p_slot, ppart.world, cfg), part, ppart, rank, c)
                   for e, c in zip(engs, comms)]
     else:
         shards = [DeviceShard(e, x, rp, col, od, args.pods, n_max, world, cfg) for e in engs]
-    steps = [RcaStep(sh, c, cfg, plo) for sh, c in zip(shards, comms)]
+    # the replicated solve iterates without a collective (its exchange is the one-rank buffer swap)
+    steps = [RcaStep(sh, Comm(1, 0) if replicated else c, cfg, plo) for sh, c in zip(shards, comms)]
     streams = [torch.cuda.Stream() for _ in range(n_pipe)]
     shard, step = shards[0], steps[0]
     torch.cuda.synchronize()
@@ -583,7 +587,9 @@ def main():
                        "seed_floor": cfg.seed_floor, "parallelism": f"pod-sharded x{world}",
                        "partition": "uniform contiguous pod ranges (krca.rca.Partition.uniform)",
                        "shard_bounds": [int(b) for b in part.bounds],
-                       "ppr_partition": (f"Partition.balanced(edge_slack={args.ppr_edge_slack}), scores all-gathered "
+                       "ppr_partition": ("replicated: the whole mesh's solve on every rank, scores all-gathered once "
+                                         "per step (krca.rca.SplitShard)") if replicated else
+                                        (f"Partition.balanced(edge_slack={args.ppr_edge_slack}), scores all-gathered "
                                          "once per step (krca.rca.SplitShard)") if split else "the scoring's ranges",
                        "ppr_bounds": [int(b) for b in ppart.bounds]},
             "e2e_rca_latency_ms": latency_ms, "e2e_rca_latency_p95_ms": latency_p95_ms,

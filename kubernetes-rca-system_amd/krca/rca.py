@@ -518,20 +518,25 @@ class SplitShard:
     over the rank's range of `ppart` (Partition.balanced: the hub services' in-edges spread over
     the ranks), seeded from its rows' slice of the gathered scores.  The solve is the same
     pod-sharded one (one all-gather per iteration), so the ranks stay bit-identical to the oracle.
+    With a one-range `ppart` (``Partition([0, N])``) the solve is REPLICATED: every rank runs the
+    whole mesh's PageRank on the gathered scores with no collective inside the solve (its RcaStep
+    takes ``Comm(1, 0)``) and reaches the same top-k on its own -- the measured alternative when the
+    per-iteration all-gather costs more than the solve it shards.
     Everything :class:`RcaStep` and :class:`Comm` use besides score() -- init, folded steps, send /
     w_all, top-k, r -- is the PageRank shard's; score_out is the scorer's."""
 
     def __init__(self, scorer, ppr, spart, ppart, rank, comm):
         import torch
-        if spart.world < 2 or spart.world != ppart.world or spart.N != ppart.N:
-            raise ValueError("SplitShard: two partitions of the same pods over the same G > 1 ranks")
+        if spart.world < 2 or ppart.world not in (1, spart.world) or spart.N != ppart.N:
+            raise ValueError("SplitShard: two partitions of the same pods over the same G > 1 ranks "
+                             "(or one range: the replicated solve)")
         if not np.array_equal(spart.bounds, Partition.uniform(spart.N, spart.world).bounds):
             raise ValueError("SplitShard: the scoring partition must be uniform (its gathered slices are then in pod order)")
         self.scorer, self.ppr, self.comm, self.rank = scorer, ppr, comm, rank
         self.spart, self.ppart = spart, ppart
         lo, hi, s_slot = spart.range(rank)
         self.n_score = hi - lo
-        plo, phi, _ = ppart.range(rank)
+        plo, phi, _ = ppart.range(rank if ppart.world > 1 else 0)
         dev = ppr.send.device
         self._pad = torch.zeros(s_slot, dtype=torch.float32, device=dev)
         self._all = torch.zeros(spart.world * s_slot + 1, dtype=torch.float32, device=dev)
@@ -542,6 +547,24 @@ class SplitShard:
         if name in ("scorer", "ppr"):
             raise AttributeError(name)
         return getattr(self.ppr, name)
+
+    # the exchange buffers are the PageRank shard's, assignments included (a one-rank solve's
+    # exchange swaps them: Comm.exchange at world 1)
+    @property
+    def send(self):
+        return self.ppr.send
+
+    @send.setter
+    def send(self, v):
+        self.ppr.send = v
+
+    @property
+    def w_all(self):
+        return self.ppr.w_all
+
+    @w_all.setter
+    def w_all(self, v):
+        self.ppr.w_all = v
 
     @property
     def M(self):

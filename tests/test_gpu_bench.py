@@ -40,13 +40,16 @@ def test_bench_gpus_2_runs_two_ranks():
     two = run_bench(2, ["--profile"])
     # the PageRank rows on the scoring's own uniform ranges (no score all-gather)
     two_u = run_bench(2, ["--ppr-partition", "uniform", "--no-corr", "--no-cpu-baseline"])
+    # every rank solves the whole mesh on the all-gathered scores (no collective inside the solve)
+    two_r = run_bench(2, ["--ppr-partition", "replicated", "--no-corr", "--no-cpu-baseline"])
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["world_ranks"] == 2
-    assert two["rca_top10"] == one["rca_top10"] == two_u["rca_top10"]
+    assert two["rca_top10"] == one["rca_top10"] == two_u["rca_top10"] == two_r["rca_top10"]
+    assert two_r["config"]["ppr_bounds"] == [0, 20000]
     # default at N > 1: PageRank on Partition.balanced ranges, scores all-gathered (krca.rca.SplitShard)
     assert two["config"]["ppr_bounds"] != two["config"]["shard_bounds"], two["config"]
     assert two_u["config"]["ppr_bounds"] == two_u["config"]["shard_bounds"]
-    vu = two_u["verify"]
-    assert vu["ppr_fixed_point_bit_identical"] and vu["top10_identical"] and vu["n_exceed_flags_bit_exact"], vu
+    for vu in (two_u["verify"], two_r["verify"]):
+        assert vu["ppr_fixed_point_bit_identical"] and vu["top10_identical"] and vu["n_exceed_flags_bit_exact"], vu
     assert two["profile"]["krca_ppr_shard_step_folded"]["launches"] == 30
     assert two["profile"]["score_exchange"]["launches"] == 1 and two["profile"]["krca_rolling_score"]["launches"] == 1
     for line in (one, two):

@@ -50,27 +50,37 @@ def _worker(rank, world, port, out_q, balanced=False):
     lo, hi, n_max = part.range(rank)
     rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi, part)
     comm = Comm(world, rank)
-    if balanced == "split":
+    step_comm = comm
+    if balanced in ("split", "replicated"):
         spart = Partition.uniform(N, world)
         slo, shi, s_slot = spart.range(rank)
         scorer = NumpyShard(x[:, slo:shi, :], np.zeros(1, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int32), N,
                             s_slot, world, cfg)
-        ppr = NumpyShard(x[:, lo:hi, :], rp, col, od, N, n_max, world, cfg)
+        if balanced == "replicated":  # the whole mesh's solve on every rank, no collective inside it
+            part = Partition([0, N])
+            lo, hi, n_max = 0, N, N
+            rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, N, part)
+            ppr = NumpyShard(x, rp, col, od, N, N, 1, cfg)
+            step_comm = Comm(1, 0)
+        else:
+            ppr = NumpyShard(x[:, lo:hi, :], rp, col, od, N, n_max, world, cfg)
         shard = SplitShard(scorer, ppr, spart, part, rank, comm)
     else:
         shard = NumpyShard(x[:, lo:hi, :], rp, col, od, N, n_max, world, cfg)
-    idx, key = RcaStep(shard, comm, cfg, lo).run()
+    idx, key = RcaStep(shard, step_comm, cfg, lo).run()
     out_q.put((rank, lo, shard.r.copy(), [int(i) for i in idx], [int(k) for k in key]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balanced", [(2, False), (3, False), (2, True), (4, True), (3, "split"), (7, "split")])
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, False), (2, True), (4, True), (3, "split"), (7, "split"),
+                                           (3, "replicated")])
 def test_sharded_rca_matches_single_process_oracle(world, balanced):
     """Uniform ranges and pods + in-edges balanced ranges (krca.rca.Partition: ranges of different
     lengths, columns in the exchange layout's virtual ids), and the split form (scoring uniform,
     PageRank balanced, scores all-gathered; world 7: the last uniform range is short, so the
-    gathered scores carry padding): the same bits every way."""
+    gathered scores carry padding), and the replicated solve (scores all-gathered, every rank
+    solves the whole mesh): the same bits every way."""
     import oracle
     from krca.rca import Config
     ctx = mp.get_context("spawn")
@@ -87,8 +97,12 @@ def test_sharded_rca_matches_single_process_oracle(world, balanced):
     m, x = _mesh()
     score = oracle.c_rolling_score(x, 60)["score"]
     ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, 0.5, 12, Config().floor(N, M), 10)
-    r_sharded = np.concatenate([rr for _, _, rr, _, _ in res])
-    assert np.array_equal(r_sharded, r)
+    if balanced == "replicated":  # every rank holds the whole fixed point
+        for _, _, rr, _, _ in res:
+            assert np.array_equal(rr, r)
+    else:
+        r_sharded = np.concatenate([rr for _, _, rr, _, _ in res])
+        assert np.array_equal(r_sharded, r)
     for _, _, _, idx, _ in res:  # every rank holds the same merged top-10
         assert idx == [int(i) for i in ridx]
 
