@@ -61,10 +61,11 @@ def parse(argv=None):
     ap.add_argument("--corr-k", type=int, default=10)
     ap.add_argument("--corr-runs", type=int, default=3, help="timed correlation calls (after one warm-up call)")
     ap.add_argument("--corr-check-rows", type=int, default=512)
-    ap.add_argument("--ppr-partition", choices=("balanced", "uniform", "replicated"), default="balanced",
+    ap.add_argument("--ppr-partition", choices=("auto", "balanced", "uniform", "replicated"), default="auto",
                     help="G > 1: PageRank rows on Partition.balanced ranges (scores all-gathered once per step, "
                          "krca.rca.SplitShard), on the scoring's uniform ranges, or the whole mesh's solve on "
-                         "every rank (scores all-gathered, no collective inside the solve)")
+                         "every rank (scores all-gathered, no collective inside the solve); auto = balanced at "
+                         "G >= 8, uniform below (measured, DESIGN.md §5)")
     ap.add_argument("--ppr-edge-slack", type=float, default=1.5,
                     help="Partition.balanced's in-edge cap per rank, in multiples of E / G")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -452,8 +453,9 @@ def main():
     # the PageRank rows: at G > 1 by default Partition.balanced ranges, so that the hub services'
     # in-edges do not all land on rank 0 (10.6M of 20M at G = 8 with uniform ranges); the scores
     # then travel in one all-gather per step (krca.rca.SplitShard)
-    split = world > 1 and args.ppr_partition in ("balanced", "replicated")
-    replicated = split and args.ppr_partition == "replicated"
+    mode = args.ppr_partition if args.ppr_partition != "auto" else ("balanced" if world >= 8 else "uniform")
+    split = world > 1 and mode in ("balanced", "replicated")
+    replicated = split and mode == "replicated"
     ppart = (Partition([0, args.pods]) if replicated else
              Partition.balanced(mesh.row_ptr, world, edge_slack=args.ppr_edge_slack) if split else part)
     plo, phi, p_slot = ppart.range(rank if ppart.world > 1 else 0)

@@ -164,7 +164,7 @@ class Pipe:
     def __init__(self, a, m, cfg, x, slo, shi, s_slot, part, gp, split):
         import torch
         from krca import native
-        from krca.rca import DeviceShard, RcaStep, shard_graph, slice_words
+        from krca.rca import Comm, DeviceShard, RcaStep, shard_graph, slice_words
         self.torch, self.cfg, self.split, self.slo, self.shi = torch, cfg, split, slo, shi
         G = part.world
         plo, phi, p_slot = part.range(gp)
@@ -179,7 +179,8 @@ class Pipe:
                 sh.score_out = {"score": sv[plo:plo + max(phi - plo, 1)]}
         else:
             self.scor = self.ppr = [DeviceShard(e, x, rp, col, od, a.pods, p_slot, G, cfg) for e in engs]
-        comm = CopyComm(G, gp, slice_words(p_slot))
+        # a one-range partition is the replicated solve: one rank's exchange is the buffer swap
+        comm = Comm(1, 0) if G == 1 else CopyComm(G, gp, slice_words(p_slot))
         self.steps = [RcaStep(sh, comm, cfg, plo) for sh in self.ppr]
         self.streams = [torch.cuda.Stream() for _ in range(2)]
         self.done = None
@@ -245,6 +246,8 @@ def ab_decoupled(a, m, hops, cfg, slacks, reps, M, T):
         bounds[str(slack)] = [int(b) for b in ppart.bounds]
         for gp in sorted({int(np.argmax(np.diff(m.row_ptr[ppart.bounds]))), int(np.argmax(np.diff(ppart.bounds)))}):
             pipes[f"split{slack}_rank{gp}"] = Pipe(a, m, cfg, x, slo, shi, s_slot, ppart, gp, True)
+    if a.with_replicated:  # every rank solves the whole mesh on the gathered scores
+        pipes["replicated"] = Pipe(a, m, cfg, x, slo, shi, s_slot, Partition([0, a.pods]), 0, True)
     times = {k: [] for k in pipes}
     for _ in range(reps):
         for k, p in pipes.items():
@@ -270,6 +273,7 @@ def main():
                     "PageRank on Partition.balanced(edge_slack=...) ranges (scores exchanged once per step); "
                     "runs only these, timed in alternation with the coupled uniform step")
     ap.add_argument("--reps", type=int, default=5, help="--decoupled: alternating timed runs per pipeline")
+    ap.add_argument("--with-replicated", action="store_true", help="--decoupled: add the replicated solve")
     a = ap.parse_args()
     from krca import synth
     from krca.rca import RANKING, Partition
