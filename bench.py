@@ -450,7 +450,7 @@ def main():
     # tools/g8_step_emulation.py)
     part = Partition.uniform(args.pods, world)
     lo, hi, n_max = part.range(rank)
-    # the PageRank rows: at G > 1 by default Partition.balanced ranges, so that the hub services'
+    # the PageRank rows: at G >= 8 by default Partition.balanced ranges, so that the hub services'
     # in-edges do not all land on rank 0 (10.6M of 20M at G = 8 with uniform ranges); the scores
     # then travel in one all-gather per step (krca.rca.SplitShard)
     mode = args.ppr_partition if args.ppr_partition != "auto" else ("balanced" if world >= 8 else "uniform")
