@@ -57,6 +57,7 @@ for s in "$@"; do
     tests_score) step tests_score 300 python3 -u -m pytest tests/test_gpu_kernels.py -x -v -rP --timeout 120 --timeout-method thread -k "rolling_score" ;;
     benchnt_*) v=${s#benchnt_}; export KRCA_PPR_NT=${v%%_*}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline --no-verify; unset KRCA_PPR_NT ;;
     benchx_*) v=${s#benchx_}; export KRCA_PPR_XCD=${v%%_*}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline --no-verify --steps 20; unset KRCA_PPR_XCD ;;
+    benchhw_*) v=${s#benchhw_}; export GPU_MAX_HW_QUEUES=${v%%_*}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline --no-verify --steps 20; unset GPU_MAX_HW_QUEUES ;;
     benchq_*) export KRCA_PPR_GRID=${s#benchq_}; step $s 300 python3 bench.py --no-corr --no-cpu-baseline; unset KRCA_PPR_GRID ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_trace) prof bench_trace 400 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
