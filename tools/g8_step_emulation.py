@@ -16,6 +16,10 @@ The replicated alternative: every rank scores its own pods, the scores are all-g
 step, and each rank runs the whole mesh's solve alone (no collective inside the solve).
 
   python tools/g8_step_emulation.py [--pods 1000000] [--edges 20000000] [--world 8] [--steps 20]
+
+Every pipe's two streams live in this one process: with the box's default 4 hardware queues per
+process some pipes get both of theirs on one queue and run serialised; pass
+--hw-queues 8 (GPU_MAX_HW_QUEUES, set before HIP starts) when comparing several pipes.
 """
 import argparse
 import json
@@ -274,7 +278,10 @@ def main():
                     "runs only these, timed in alternation with the coupled uniform step")
     ap.add_argument("--reps", type=int, default=5, help="--decoupled: alternating timed runs per pipeline")
     ap.add_argument("--with-replicated", action="store_true", help="--decoupled: add the replicated solve")
+    ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the environment's)")
     a = ap.parse_args()
+    if a.hw_queues:  # before anything starts HIP
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
     from krca import synth
     from krca.rca import RANKING, Partition
     M, T = 8, 1440
