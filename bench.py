@@ -65,7 +65,7 @@ def parse(argv=None):
                     help="G > 1: PageRank rows on Partition.balanced ranges (scores all-gathered once per step, "
                          "krca.rca.SplitShard), on the scoring's uniform ranges, or the whole mesh's solve on "
                          "every rank (scores all-gathered, no collective inside the solve); auto = balanced at "
-                         "G >= 8, uniform below (measured, DESIGN.md §5)")
+                         "G >= 4, uniform below (measured, DESIGN.md §5)")
     ap.add_argument("--ppr-edge-slack", type=float, default=1.5,
                     help="Partition.balanced's in-edge cap per rank, in multiples of E / G")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -450,10 +450,10 @@ def main():
     # tools/g8_step_emulation.py)
     part = Partition.uniform(args.pods, world)
     lo, hi, n_max = part.range(rank)
-    # the PageRank rows: at G >= 8 by default Partition.balanced ranges, so that the hub services'
+    # the PageRank rows: at G >= 4 by default Partition.balanced ranges, so that the hub services'
     # in-edges do not all land on rank 0 (10.6M of 20M at G = 8 with uniform ranges); the scores
     # then travel in one all-gather per step (krca.rca.SplitShard)
-    mode = args.ppr_partition if args.ppr_partition != "auto" else ("balanced" if world >= 8 else "uniform")
+    mode = args.ppr_partition if args.ppr_partition != "auto" else ("balanced" if world >= 4 else "uniform")
     split = world > 1 and mode in ("balanced", "replicated")
     replicated = split and mode == "replicated"
     ppart = (Partition([0, args.pods]) if replicated else

@@ -18,7 +18,7 @@ of two buffers (the step kernel reads one and writes the other).  Arithmetic is 
 point: the result is bit-identical for any G and to oracle/krca_oracle.c.  The final top-k merges G x k candidates.
 
 A rank's PageRank rows need not be the pods it scores: :class:`SplitShard` (the bench's default at
-G >= 8) scores a uniform range, all-gathers the scores once per step, and solves on an edge-balanced
+G >= 4) scores a uniform range, all-gathers the scores once per step, and solves on an edge-balanced
 :class:`Partition` range.
 
 The per-rank numeric work is behind a small backend interface so the same orchestration runs
@@ -510,7 +510,7 @@ class DeviceShard:
 
 
 class SplitShard:
-    """A rank whose PageRank rows are not its scored pods (bench.py at G >= 8).
+    """A rank whose PageRank rows are not its scored pods (bench.py at G >= 4).
 
     The scoring runs on `scorer` over the rank's range of `spart` (uniform: every rank streams the
     same number of series), ONE all-gather per step moves the scores (4 B per pod, every rank's

@@ -38,14 +38,14 @@ def run_bench(n, extra=()):
 def test_bench_gpus_2_runs_two_ranks():
     one = run_bench(1, ["--profile"])
     two = run_bench(2, ["--profile", "--ppr-partition", "balanced"])
-    # the PageRank rows on the scoring's own uniform ranges (no score all-gather; the default below N = 8)
+    # the PageRank rows on the scoring's own uniform ranges (no score all-gather; the default below N = 4)
     two_u = run_bench(2, ["--no-corr", "--no-cpu-baseline"])
     # every rank solves the whole mesh on the all-gathered scores (no collective inside the solve)
     two_r = run_bench(2, ["--ppr-partition", "replicated", "--no-corr", "--no-cpu-baseline"])
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["world_ranks"] == 2
     assert two["rca_top10"] == one["rca_top10"] == two_u["rca_top10"] == two_r["rca_top10"]
     assert two_r["config"]["ppr_bounds"] == [0, 20000]
-    # PageRank on Partition.balanced ranges, scores all-gathered (krca.rca.SplitShard; the default at N >= 8)
+    # PageRank on Partition.balanced ranges, scores all-gathered (krca.rca.SplitShard; the default at N >= 4)
     assert two["config"]["ppr_bounds"] != two["config"]["shard_bounds"], two["config"]
     assert two_u["config"]["ppr_bounds"] == two_u["config"]["shard_bounds"]
     for vu in (two_u["verify"], two_r["verify"]):
