@@ -165,7 +165,7 @@ class Pipe:
     PageRank-only shard seeded from a full score vector into which a device copy lands this rank's
     scores (standing in for SplitShard's score all-gather)."""
 
-    def __init__(self, a, m, cfg, x, slo, shi, s_slot, part, gp, split):
+    def __init__(self, a, m, cfg, x, slo, shi, s_slot, part, gp, split, roles=False):
         import torch
         from krca import native
         from krca.rca import Comm, DeviceShard, RcaStep, shard_graph, slice_words
@@ -188,11 +188,35 @@ class Pipe:
         self.steps = [RcaStep(sh, comm, cfg, plo) for sh in self.ppr]
         self.streams = [torch.cuda.Stream() for _ in range(2)]
         self.done = None
+        # roles: the scoring always on one stream, the solve on a second, high-priority one (events
+        # order them: solve i after scoring i, scoring i + 2 after solve i, whose state it reuses)
+        self.roles = roles
+        if roles:
+            self.s_stream = torch.cuda.Stream()
+            self.p_stream = torch.cuda.Stream(priority=-1)
+            self.ev_s = [None, None]
+            self.ev_p = [None, None]
         self.info = dict(pagerank_rank=gp, pagerank_pods=phi - plo, pagerank_edges=int(m.row_ptr[phi] - m.row_ptr[plo]),
                          scoring_pods=shi - slo)
 
     def enqueue(self, i):
         torch, j = self.torch, i % 2
+        if self.roles:
+            with torch.cuda.stream(self.s_stream):
+                if self.ev_p[j] is not None:
+                    self.s_stream.wait_event(self.ev_p[j])
+                self.scor[j].score()
+                self.ev_s[j] = torch.cuda.Event()
+                self.ev_s[j].record()
+            with torch.cuda.stream(self.p_stream):
+                self.p_stream.wait_event(self.ev_s[j])
+                if self.split:
+                    self.sfull[j][self.slo:self.shi].copy_(self.scor[j].score_out["score"][:self.shi - self.slo])
+                self.steps[j].propagate()
+                self.ppr[j].local_topk(self.cfg.k)
+                self.ev_p[j] = torch.cuda.Event()
+                self.ev_p[j].record()
+            return
         with torch.cuda.stream(self.streams[j]):
             if self.done is not None:
                 self.streams[j].wait_event(self.done)
@@ -244,12 +268,16 @@ def ab_decoupled(a, m, hops, cfg, slacks, reps, M, T):
     slo, shi, s_slot = spart.range(g)
     x = synth.make_metrics_range(slo, shi, M, T, seed=0, roots=m.roots, hop_sets=hops, device="cuda")
     pipes = {f"coupled_rank{g}": Pipe(a, m, cfg, x, slo, shi, s_slot, spart, g, False)}
+    if a.roles:
+        pipes[f"coupled_rank{g}_roles"] = Pipe(a, m, cfg, x, slo, shi, s_slot, spart, g, False, roles=True)
     bounds = {}
     for slack in slacks:
         ppart = Partition.balanced(m.row_ptr, G, edge_slack=slack)
         bounds[str(slack)] = [int(b) for b in ppart.bounds]
         for gp in sorted({int(np.argmax(np.diff(m.row_ptr[ppart.bounds]))), int(np.argmax(np.diff(ppart.bounds)))}):
             pipes[f"split{slack}_rank{gp}"] = Pipe(a, m, cfg, x, slo, shi, s_slot, ppart, gp, True)
+            if a.roles:
+                pipes[f"split{slack}_rank{gp}_roles"] = Pipe(a, m, cfg, x, slo, shi, s_slot, ppart, gp, True, roles=True)
     if a.with_replicated:  # every rank solves the whole mesh on the gathered scores
         pipes["replicated"] = Pipe(a, m, cfg, x, slo, shi, s_slot, Partition([0, a.pods]), 0, True)
     times = {k: [] for k in pipes}
@@ -278,6 +306,8 @@ def main():
                     "runs only these, timed in alternation with the coupled uniform step")
     ap.add_argument("--reps", type=int, default=5, help="--decoupled: alternating timed runs per pipeline")
     ap.add_argument("--with-replicated", action="store_true", help="--decoupled: add the replicated solve")
+    ap.add_argument("--roles", action="store_true", help="--decoupled: add role-stream pipes (scoring stream + "
+                    "high-priority solve stream)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the environment's)")
     a = ap.parse_args()
     if a.hw_queues:  # before anything starts HIP
