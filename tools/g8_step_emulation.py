@@ -308,6 +308,7 @@ def main():
     ap.add_argument("--with-replicated", action="store_true", help="--decoupled: add the replicated solve")
     ap.add_argument("--roles", action="store_true", help="--decoupled: add role-stream pipes (scoring stream + "
                     "high-priority solve stream)")
+    ap.add_argument("--grid", type=int, default=0, help="KRCA_PPR_GRID for every pipe (0: the occupancy grid)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the environment's)")
     a = ap.parse_args()
     if a.hw_queues:  # before anything starts HIP
@@ -334,6 +335,10 @@ def main():
         if a.only_grids:
             print(json.dumps(out), flush=True)
             return
+    if a.grid:
+        from krca import native
+        assert native.load_library().krca_tune_set(b"KRCA_PPR_GRID", a.grid) == 0
+        out["ppr_grid"] = a.grid
     if a.decoupled:
         out["decoupled_ab"] = ab_decoupled(a, m, hops, cfg, [float(v) for v in a.decoupled.split(",")], a.reps, M, T)
         print(json.dumps(out), flush=True)

@@ -85,6 +85,7 @@ for s in "$@"; do
     g8_slack_w*) step $s 500 python3 tools/g8_step_emulation.py --world ${s#g8_slack_w} --steps 30 --reps 5 --decoupled 1.25,1.5,2.0,3.0 ;;
     g8_rep_w*) step $s 500 python3 tools/g8_step_emulation.py --world ${s#g8_rep_w} --steps 30 --reps 5 --decoupled 1.5 --with-replicated ;;
     g8_roles_w*) step $s 500 python3 tools/g8_step_emulation.py --world ${s#g8_roles_w} --steps 30 --reps 5 --decoupled 1.5 --roles --hw-queues 16 ;;
+    g8_grid_*) v=${s#g8_grid_}; step $s 500 python3 tools/g8_step_emulation.py --world 8 --steps 30 --reps 5 --decoupled 1.5 --hw-queues 16 --grid ${v%%_*} ;;
     g8_hq_w*) step $s 500 python3 tools/g8_step_emulation.py --world ${s#g8_hq_w} --steps 30 --reps 5 --decoupled 1.5 --with-replicated --hw-queues 16 ;;
     g8_grid) step g8_grid 400 python3 tools/g8_step_emulation.py --ppr-grids 0,1024,512,256 --only-grids ;;
     ppr_head)  # the same profile with the committed tree's code (ab_head/: git archive HEAD, built in place)
