@@ -64,8 +64,9 @@ def parse(argv=None):
     ap.add_argument("--ppr-partition", choices=("auto", "balanced", "uniform", "replicated"), default="auto",
                     help="G > 1: PageRank rows on Partition.balanced ranges (scores all-gathered once per step, "
                          "krca.rca.SplitShard), on the scoring's uniform ranges, or the whole mesh's solve on "
-                         "every rank (scores all-gathered, no collective inside the solve); auto = balanced at "
-                         "G >= 4, uniform below (measured, DESIGN.md §5)")
+                         "every rank (scores all-gathered, no collective inside the solve); auto = the sharded "
+                         "solve (balanced at G >= 4, uniform below: measured, DESIGN.md §5) unless the all-gather "
+                         "measured at startup costs more per solve than the replicated step's measured margin")
     ap.add_argument("--ppr-edge-slack", type=float, default=1.5,
                     help="Partition.balanced's in-edge cap per rank, in multiples of E / G")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -106,6 +107,61 @@ def cpu_model():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+# the replicated step's measured cost over the sharded one per G (ms; DESIGN.md §5, single-GPU
+# emulations with a device copy standing in for the all-gather): the budget the sharded solve's
+# iters x (all-gather - device copy) may spend before replicating the solve is cheaper
+REPLICATED_MARGIN_MS = {2: 0.155, 4: 0.39, 8: 0.50}
+
+
+def exchange_probe(world, n_slot, dev, reps=50):
+    """The PageRank exchange at its real size, measured after init: `reps` all-gathers of one rank's
+    slice (krca_ppr_slice_words(n_slot) int64) through the same call Comm makes, and a device copy of
+    the gathered bytes (what the single-GPU emulations stood in for it).  Per call: the wall time of
+    the back-to-back sequence (host dispatch included: the solve's iterations are issued the same
+    way) and the HIP-event time; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from krca.rca import all_gather_flat, slice_words
+    words = slice_words(n_slot)
+    send = torch.zeros(words, dtype=torch.int64, device=dev)
+    out = torch.zeros(world * words, dtype=torch.int64, device=dev)
+    for _ in range(5):
+        all_gather_flat(out, send, world)
+    res = {}
+    for name, fn in (("allgather", lambda: all_gather_flat(out, send, world)),
+                     ("copy", lambda: out.view(world, -1).copy_(send.expand(world, -1)))):
+        torch.cuda.synchronize()
+        dist.barrier()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        res[name + "_us"] = max_over_ranks((time.perf_counter() - t1) / reps * 1e6, world)
+        res[name + "_event_us"] = max_over_ranks(a.elapsed_time(b) / reps * 1e3, world)
+    res["bytes_per_rank"] = words * 8
+    res["reps"] = reps
+    return res
+
+
+def choose_ppr_mode(args, world, probe):
+    """--ppr-partition auto: the sharded solve (balanced PageRank ranges at G >= 4, the scoring's
+    uniform ranges below) unless iters x (all-gather - device copy) exceeds the replicated step's
+    measured margin at this G, then the replicated solve."""
+    if args.ppr_partition != "auto":
+        return args.ppr_partition, None
+    sharded = "balanced" if world >= 4 else "uniform"
+    if probe is None:
+        return sharded, None
+    margin = REPLICATED_MARGIN_MS.get(world, 0.4)
+    extra_ms = args.iters * max(probe["allgather_us"] - probe["copy_us"], 0.0) / 1e3
+    mode = "replicated" if extra_ms > margin else sharded
+    return mode, {"iters_x_extra_ms": extra_ms, "margin_ms": margin,
+                  "rule": f"replicated when iters x (all-gather - device copy) > {margin} ms (DESIGN.md §5)"}
 
 
 def profile_step(step, stream, world):
@@ -153,7 +209,7 @@ def profile_step(step, stream, world):
                   lambda: s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == cfg.iters)))
             timed("exchange", lambda: c.exchange(s))
         timed("krca_ppr_shard_finish", lambda: s.finish(cfg.alpha, cfg.tol, cfg.iters))
-        timed("key+topk", lambda: s.local_topk(cfg.k))
+        timed("key+topk", lambda: step.local_candidates())
         t1.record()
     torch.cuda.synchronize()
     out = {}
@@ -254,7 +310,7 @@ def verify_step(args, cfg, mesh, shard, x, part, ppart, rank):
     if rank != 0:
         return {}
     ridx, _, r = oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, sc_all, cfg.alpha, cfg.iters, cfg.seed_floor,
-                                 cfg.k)
+                                 cfg.k, key=cfg.key)
     return {"ppr_fixed_point_bit_identical": bool(np.array_equal(r_all, r)),
             "oracle_top10": [int(i) for i in ridx],
             "ranks_gathered": world, "score_sample_pods": int(ns_all),
@@ -277,7 +333,8 @@ def cpu_baseline(args, cfg, mesh, shard, x, n_loc):
         t1 = time.perf_counter()
         oracle.c_rolling_score(xs, args.window)
         t2 = time.perf_counter()
-        oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k)
+        oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k,
+                        key=cfg.key)
         t3 = time.perf_counter()
         if i >= args.cpu_warmup:
             t_sc.append(t2 - t1)
@@ -304,6 +361,30 @@ def cpu_baseline(args, cfg, mesh, shard, x, n_loc):
             "note": "the reference has no rolling scoring or PageRank; these are its per-pod threshold "
                     "loop, 13-regex line histogram, SPOF betweenness and C1 comprehensive analysis"}
     return out
+
+
+def spread_recall(eng, cfg, seed, pods=10_000, edges=200_000):
+    """Untimed: the ranking on a C2-size mesh of the 'spread' failure model (synth.spread_hops: the
+    callers of each planted root carry larger symptoms than the root), one device through RcaStep:
+    recall@k of the planted roots and the top-k against the oracle."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from krca import synth
+    from krca.rca import Comm, DeviceShard, RcaStep, shard_graph
+    m = synth.make_graph(pods, n_edges=edges, seed=seed)
+    hops = synth.spread_hops(m, m.roots, seed=seed)
+    x = synth.make_metrics(pods, 8, 1440, seed=seed, roots=m.roots, hop_sets=hops, **synth.SPREAD_SIGMAS).to(eng.device)
+    c = cfg.replace(seed_floor=None)
+    step = RcaStep(DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, 0, pods), pods, pods, 1, c), Comm(), c, 0)
+    idx, _ = step.run()
+    top = [int(i) for i in idx]
+    ref, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, step.s.score_out["score"].cpu().numpy(), c.alpha, c.iters,
+                                c.floor(pods, 8), c.k, key=c.key)
+    del x, step
+    torch.cuda.empty_cache()
+    return {"recall": len(set(top) & set(m.roots.tolist())) / len(m.roots), "top10_identical": top == ref.tolist(),
+            "mesh": f"C2 spread: {pods} pods / {edges} edges, mesh seed {seed} (synth.spread_hops, synth.SPREAD_SIGMAS)"}
 
 
 def corr_check(z32, rows, res_idx, res_val, res_cnt, res_cert, k, tau, band=1e-12):
@@ -420,7 +501,7 @@ def main():
     import torch.distributed as dist
 
     from krca import native, synth
-    from krca.rca import Comm, Config, DeviceShard, Partition, RcaStep, SplitShard, shard_graph
+    from krca.rca import Comm, Config, DeviceShard, Explain, Partition, RcaStep, SplitShard, shard_graph
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -453,7 +534,11 @@ def main():
     # the PageRank rows: at G >= 4 by default Partition.balanced ranges, so that the hub services'
     # in-edges do not all land on rank 0 (10.6M of 20M at G = 8 with uniform ranges); the scores
     # then travel in one all-gather per step (krca.rca.SplitShard)
-    mode = args.ppr_partition if args.ppr_partition != "auto" else ("balanced" if world >= 4 else "uniform")
+    probe = None
+    if world > 1:  # the all-gather at the balanced ranges' slice size (the largest of the modes)
+        probe = exchange_probe(world, Partition.balanced(mesh.row_ptr, world, edge_slack=args.ppr_edge_slack).n_slot,
+                               torch.device("cuda", local))
+    mode, why = choose_ppr_mode(args, world, probe)
     split = world > 1 and mode in ("balanced", "replicated")
     replicated = split and mode == "replicated"
     ppart = (Partition([0, args.pods]) if replicated else
@@ -473,8 +558,11 @@ def main():
                   for e, c in zip(engs, comms)]
     else:
         shards = [DeviceShard(e, x, rp, col, od, args.pods, n_max, world, cfg) for e in engs]
-    # the replicated solve iterates without a collective (its exchange is the one-rank buffer swap)
-    steps = [RcaStep(sh, Comm(1, 0) if replicated else c, cfg, plo) for sh, c in zip(shards, comms)]
+    # the replicated solve iterates without a collective (its exchange is the one-rank buffer swap);
+    # the default ranking key walks the whole graph (one device copy shared by the pipeline slots)
+    explain = Explain(mesh.row_ptr, mesh.col) if cfg.key == "explained" else None
+    steps = [RcaStep(sh, Comm(1, 0) if replicated else c, cfg, plo, explain=explain, part=part)
+             for sh, c in zip(shards, comms)]
     streams = [torch.cuda.Stream() for _ in range(n_pipe)]
     shard, step = shards[0], steps[0]
     torch.cuda.synchronize()
@@ -501,7 +589,7 @@ def main():
             if split:
                 shards[j].exchange_scores()
             steps[j].propagate()
-            return j, *shards[j].local_topk(cfg.k)
+            return j, *steps[j].local_candidates()
 
     def finish(j, idx, val):
         with torch.cuda.stream(streams[j]):
@@ -593,7 +681,10 @@ def main():
                                          "per step (krca.rca.SplitShard)") if replicated else
                                         (f"Partition.balanced(edge_slack={args.ppr_edge_slack}), scores all-gathered "
                                          "once per step (krca.rca.SplitShard)") if split else "the scoring's ranges",
-                       "ppr_bounds": [int(b) for b in ppart.bounds]},
+                       "ppr_bounds": [int(b) for b in ppart.bounds], "ranking_key": cfg.key},
+            "ppr_exchange_us": probe["allgather_us"] if probe else None,
+            "ppr_mode": mode if world > 1 else "single device (buffer swap)",
+            "ppr_exchange": dict(probe or {"allgather_us": None}, **(why or {})),
             "e2e_rca_latency_ms": latency_ms, "e2e_rca_latency_p95_ms": latency_p95_ms,
             "step_ms_median": float(np.median(step_ms)), "step_ms_p95": float(np.percentile(step_ms, 95)),
             "pipelined_streams": n_pipe,
@@ -628,6 +719,17 @@ def main():
             v = {"error": repr(e)[:500], "ppr_fixed_point_bit_identical": False, "top10_identical": False}
         if rank == 0:
             result["verify"] = v
+
+    # ---- the ranking on the spread failure model (untimed, C2 size, rank 0) ------------------
+    if rank == 0 and not args.no_verify:
+        try:
+            sp = spread_recall(eng, cfg, args.seed + 1)
+            result["planted_root_recall_spread"] = sp.pop("recall")
+            result["spread_check"] = sp
+        except Exception as e:  # noqa: BLE001
+            log(f"[rank 0] spread recall failed: {e!r}")
+            result["planted_root_recall_spread"] = None
+            result["spread_check"] = {"error": repr(e)[:500]}
 
     # ---- CPU baseline: the C restatement on the host cores, bounded sample (rank 0) -------
     if rank == 0 and not args.no_cpu_baseline:

@@ -279,9 +279,11 @@ int krca_ppr_shard_reduce(const int64_t* w_all, int32_t G, int64_t n_max, int64_
  * sums slot set (it - 1) % 3 of the G slices of w_all: convergence, teleport scale, iteration
  * count), adds its own partial sums into set it % 3 of send and zeroes set (it + 1) % 3 of
  * next_target, the buffer the NEXT step writes: at G = 1 the ping-pong buffer it gathers from
- * (w_all), at G > 1 the rank's send itself (the next step writes send again).  next_target must
- * differ from send at G = 1 and equal it at G > 1.  One kernel and one exchange per iteration
- * instead of two kernels; results bit-identical to the unfolded sequence. */
+ * (w_all), at G > 1 the rank's send itself (the next step writes send again).  next_target is
+ * send at G > 1; at G = 1 it is w_all when the exchange swaps the two buffers, or send when the
+ * exchange copies send into w_all (a one-rank collective: krca.rca.Comm(collective=True)).  One
+ * kernel and one exchange per iteration instead of two kernels; results bit-identical to the
+ * unfolded sequence. */
 int krca_ppr_shard_step_folded(const int64_t* row_ptr, const int32_t* col /*pk*/, const int64_t* plan, int64_t plan_len,
                                const uint16_t* lane, const int64_t* w_all, int32_t G, const int32_t* outdeg,
                                const int64_t* q_local, int64_t n_local, int64_t n_max, int64_t N, double alpha,
@@ -304,8 +306,26 @@ int krca_ppr_ctl_read(const void* ctl, int32_t* iters_host, int32_t* converged_h
 int krca_ppr_ctl_copy(const void* ctl, int32_t* host /*[2]*/, void* stream);
 int krca_ppr_fixed_to_float(const int64_t* r, int64_t n, float* out, void* stream);
 /* root-cause key = bits of (double)r_i * (double)q_i: ranks pods by propagated mass times their
- * own anomaly; order-preserving as int64, fed to krca_topk_i64 */
+ * own anomaly; order-preserving as int64, fed to krca_topk_i64 (krca.rca.Config key "rq") */
 int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key, void* stream);
+/* The default root-cause key (krca.rca.Config key "explained"; the sink of
+ * ref:agents/coordinator.py:157-184, edge direction of ref:agents/topology_agent.py:94-159: caller
+ * -> dependency).  krca_rca_explain: over the WHOLE pull-CSR and the scores of every pod (score_all
+ * [N]; q_j = the quantised seed of krca_ppr_shard_init), A_k = edges from anomalous callers of each
+ * anomalous pod k; an anomalous dependency k of an anomalous pod j (edge j -> k, j != k) explains j
+ * when A_k - 1 >= A_j or q_k >= 2 q_j; d_local[j - lo] = the largest q_k over the dependencies that
+ * explain j, for the pods [lo, hi) (0: none).  Only anomalous pods' rows are walked; integer counts
+ * and maxima, so bit-identical to oracle/krca_oracle.c krco_rca_explain.  ws:
+ * krca_rca_explain_ws_size(N) bytes, no initialisation needed.
+ * krca_rca_key_explained: key_i = bits((double)recv_i * (double)u_i) with u_i = q_i - d_i (0 when
+ * <= 0) and recv_i = r_i - t_i, the mass row i received from its callers in the solve's last step (t_i
+ * = that step's teleport share, from the scale the step recorded in ctl): the rows and ctl of a
+ * finished krca_ppr_shard_* / krca_ppr solve, N = the mesh's node count. */
+int64_t krca_rca_explain_ws_size(int64_t N);
+int krca_rca_explain(const float* score_all, int64_t N, float seed_floor, const int64_t* row_ptr, const int32_t* col,
+                     int64_t lo, int64_t hi, int64_t* d_local /*[hi - lo]*/, void* ws, void* stream);
+int krca_rca_key_explained(const int64_t* r_local, const int64_t* q_local, const int64_t* d_local, int64_t n_local,
+                           int64_t N, const void* ctl, int64_t* key, void* stream);
 
 /* ---- top-k (descending value, ties -> lower index), float32 or int64 keys; NaN keys are never
  * selected: with fewer than k non-NaN keys the remaining slots are idx -1, val -inf / INT64_MIN -- */

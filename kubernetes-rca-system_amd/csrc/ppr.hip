@@ -69,6 +69,9 @@ struct Ctl {          // device control block (header of the ctl buffer)
   int32_t converged;  // iteration count at convergence (0 = running)
   int32_t iter;       // iterations done
   uint32_t done;      // single device, reduction fused: workgroups of the running step that finished
+  double tele_used;   // the teleport scale of the last step that updated the rows (written by its
+                      // workgroup 0): krca_rca_key_explained recovers each row's received mass as
+                      // r_i - t_i with the same t_i
 };
 // ctl buffer: Ctl header (CTL_BYTES) | int64 acc_long[n] | uint32 ticket[n] (8-byte slots) | {double coef, double q}[n].  The long-row
 // accumulators and tickets are zero when allocated and reset by the last chunk of each row.
@@ -468,6 +471,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   k.tq = k.tele / (double)k.qt;
   k.tu = (int64_t)((1.0 / (double)N) * k.tele);
   k.alpha = alpha;
+  if (blockIdx.x == 0 && tid == 0) ctl->tele_used = k.tele;  // this step updates the rows with k.tele
   int64_t err = 0, dang = 0;
 #ifdef PPR_TIMING
   uint64_t tacc[5] = {0, 0, 0, 0, 0};
@@ -680,6 +684,28 @@ __global__ __launch_bounds__(TPB) void ppr_rca_key(const int64_t* __restrict__ r
   }
 }
 
+// the default root-cause key (krca_rca_key_explained): u_i = q_i - d_i (the anomaly that no
+// explaining dependency accounts for, d from krca_rca_explain), recv_i = r_i - t_i (the mass the row
+// received from its callers in the last step: t_i is that step's teleport share, update_row's
+// expression with the recorded scale), key = bits((double)recv_i * (double)u_i), 0 when u_i <= 0
+__global__ __launch_bounds__(TPB) void rca_key_explained(const int64_t* __restrict__ r, const int64_t* __restrict__ q,
+                                                         const int64_t* __restrict__ d, int64_t n, int64_t N,
+                                                         const Ctl* __restrict__ ctl, int64_t* __restrict__ key) {
+  const double tele = ctl->tele_used;
+  const int64_t qt = ctl->q_total;
+  const double tq = tele / (double)qt;
+  const int64_t tu = (int64_t)((1.0 / (double)N) * tele);
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const int64_t qi = q[i], u = qi - d[i];
+    double v = 0.0;
+    if (u > 0) {
+      const int64_t t = qt > 0 ? (int64_t)((double)qi * tq) : tu;
+      v = (double)(r[i] - t) * (double)u;
+    }
+    key[i] = __double_as_longlong(v);
+  }
+}
+
 __global__ __launch_bounds__(TPB) void remap_cols(const int32_t* __restrict__ col, int64_t E, int64_t n_max,
                                                   int32_t* __restrict__ out) {
   for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < E; e += (int64_t)gridDim.x * TPB) {
@@ -766,8 +792,8 @@ int krca_ppr_shard_step_folded(const int64_t* row_ptr, const int32_t* col, const
                                double tol, int32_t it, int32_t flags, int64_t* r_local, int64_t* send,
                                int64_t* next_target, void* ctl, void* stream) {
   KRCA_CHECK_ARG(G >= 1 && it >= 1 && n_max > 0 && N > 0, "krca_ppr_shard_step_folded: bad sizes");
-  KRCA_CHECK_ARG(next_target && (G == 1 ? next_target == w_all : next_target == send),
-                 "krca_ppr_shard_step_folded: next_target is w_all at G = 1, send at G > 1");
+  KRCA_CHECK_ARG(next_target && (next_target == send || (G == 1 && next_target == w_all)),
+                 "krca_ppr_shard_step_folded: next_target is send, or w_all at G = 1 (swap exchange)");
   const double err_limit = tol > 0.0 ? (double)N * tol * krca::kFix : 0.0;
   const Fold fo{1, (int)it, (int)G, err_limit, next_target};
   if (plan_len == 0) {  // a rank without rows still does the step's reduction: its ctl (iteration
@@ -885,6 +911,17 @@ int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key
   if (n <= 0) return KRCA_OK;
   KRCA_CHECK_ARG(r && q && key, "krca_ppr_rca_key: null pointer");
   hipLaunchKernelGGL(ppr_rca_key, dim3(grid_for(n)), dim3(TPB), 0, krca::as_stream(stream), r, q, n, key);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+int krca_rca_key_explained(const int64_t* r, const int64_t* q, const int64_t* d, int64_t n, int64_t N, const void* ctl,
+                           int64_t* key, void* stream) {
+  if (n <= 0) return KRCA_OK;
+  KRCA_CHECK_ARG(n <= N && N < INT32_MAX, "krca_rca_key_explained: bad sizes");
+  KRCA_CHECK_ARG(r && q && d && ctl && key, "krca_rca_key_explained: null pointer");
+  hipLaunchKernelGGL(rca_key_explained, dim3(grid_for(n)), dim3(TPB), 0, krca::as_stream(stream), r, q, d, n, N,
+                     reinterpret_cast<const Ctl*>(ctl), key);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

@@ -6,7 +6,8 @@ schema / ``_correlate_findings`` (group by component, first-seen order, max seve
 exactly.  New, additive: ``ranked_root_causes`` — the root-cause ranking
 of krca.rca.Config (the same definition bench.py and RcaStep use: alpha 0.5, p ∝ max(s - floor, 0)
 with the scale-aware floor of Config.floor -- the expected maximum |z| of that many null series,
-at least 4 -- 30 iterations, key r·p) over the dependency graph, seeded by the metrics agent's anomaly scores
+at least 4 -- 30 iterations, key "explained": the mass a pod received from its callers times the
+part of its anomaly no anomalous dependency explains) over the dependency graph, seeded by the metrics agent's anomaly scores
 (bulk path) or by the trace backend's per-service error rates (C1 mock; error rates are not in
 |z| units, so that path seeds with floor 0), computed by ``krca_ppr`` on the device.
 """

@@ -88,6 +88,9 @@ SIGNATURES = {
     "krca_ppr_ctl_copy": (c_i32, [c_vp, c_vp, c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "krca_rca_explain_ws_size": (c_i64, [c_i64]),
+    "krca_rca_explain": (c_i32, [c_vp, c_i64, c_f32, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "krca_rca_key_explained": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "krca_betweenness_ws_size": (c_i64, [c_i64, c_i32]),
     "krca_betweenness": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "krca_selector_match": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
@@ -703,27 +706,53 @@ class NativeEngine:
         r, rf, q, iters = self._ppr_full(row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor)
         return r, rf, iters
 
+    def rca_explain_device(self, score_all, seed_floor, row_ptr, col, lo, hi, out=None):
+        """krca_rca_explain: d int64 [hi - lo] = the largest quantised anomaly of a dependency that
+        explains each pod of [lo, hi), over the whole pull-CSR (row_ptr / col device tensors) and the
+        scores of every pod (float32 device [N])."""
+        torch = self.torch
+        N = int(score_all.numel())
+        n = int(hi) - int(lo)
+        d = out if out is not None else torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        ws = self._workspace("rca_explain", self.lib.krca_rca_explain_ws_size(N))
+        _check(self.lib.krca_rca_explain(self.ptr(score_all), N, float(seed_floor), self.ptr(row_ptr), self.ptr(col),
+                                         int(lo), int(hi), self.ptr(d), self.ptr(ws), self._stream()),
+               "krca_rca_explain")
+        return d
+
     def rank_root_causes(self, seed, row_ptr, col, outdeg, cfg=None, k=None, n_metrics=1):
         """The root-cause ranking of krca.rca.Config (the same definition as RcaStep / bench.py):
-        seeded PageRank (cfg.alpha, cfg.floor(pods, n_metrics), cfg.iters / cfg.tol), key r_i * q_i,
-        top-k (seed = each pod's max |z| over its n_metrics metrics).
-        Returns host (idx int32 [k], score float64 [k] = r_i * p_i, r float64 [N] PageRank mass)."""
+        seeded PageRank (cfg.alpha, cfg.floor(pods, n_metrics), cfg.iters / cfg.tol), then cfg.key --
+        "explained" (default): received mass x the anomaly no explaining dependency accounts for
+        (krca_rca_explain + krca_rca_key_explained); "rq": r_i * q_i -- top-k (seed = each pod's max
+        |z| over its n_metrics metrics).
+        Returns host (idx int32 [k], score float64 [k] = the key's value (received mass or r, times
+        the anomaly, as fractions of the totals), r float64 [N] PageRank mass)."""
         from .rca import RANKING
         cfg = cfg or RANKING
         torch = self.torch
-        k = min(int(k or cfg.k), len(outdeg))
-        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol,
-                                     cfg.floor(len(outdeg), n_metrics))
+        N = len(outdeg)
+        k = min(int(k or cfg.k), N)
+        floor = cfg.floor(N, n_metrics)
+        sd = self._dev(np.asarray(seed, np.float32)) if not isinstance(seed, torch.Tensor) else self._dev(seed, torch.float32)
+        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, sd, cfg.alpha, cfg.iters, cfg.tol, floor)
         key = torch.empty_like(rf)
-        _check(self.lib.krca_ppr_rca_key(self.ptr(rf), self.ptr(q), rf.numel(), self.ptr(key), self._stream()),
-               "krca_ppr_rca_key")
+        if cfg.key == "rq":
+            _check(self.lib.krca_ppr_rca_key(self.ptr(rf), self.ptr(q), rf.numel(), self.ptr(key), self._stream()),
+                   "krca_ppr_rca_key")
+        else:
+            d = self.rca_explain_device(sd, floor, self._dev(np.asarray(row_ptr, np.int64)),
+                                        self._dev(np.asarray(col, np.int32)), 0, N)
+            ctl = self._workspace("ppr", self.lib.krca_ppr_workspace_size(N))  # krca_ppr's ctl: its first bytes
+            _check(self.lib.krca_rca_key_explained(self.ptr(rf), self.ptr(q), self.ptr(d), N, N, self.ptr(ctl),
+                                                   self.ptr(key), self._stream()), "krca_rca_key_explained")
         idx, _ = self.topk_device(key, k)
         idx = idx.cpu().numpy()
-        qt = int(q.sum().item())
+        kv = key.cpu().numpy()[idx].view(np.float64)
+        qt = float(q.sum().item())
         rr = rf.cpu().numpy().astype(np.float64) / 2.0 ** 60
-        qs = q.cpu().numpy()[idx].astype(np.float64)
-        p = qs / qt if qt > 0 else np.full(len(idx), 1.0 / len(outdeg))
-        return idx, rr[idx] * p, rr
+        val = kv / (2.0 ** 60 * qt) if qt > 0 else np.zeros(len(idx))
+        return idx, val, rr
 
     def _ppr_full(self, row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor):
         torch = self.torch

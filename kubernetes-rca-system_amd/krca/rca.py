@@ -4,7 +4,9 @@ This is the north-star path (BASELINE.json): for a pod mesh of N pods with M met
 and a caller -> dependency graph, one step scores every pod (krca_rolling_score), seeds a
 personalized PageRank with the anomalous pods (p_i ∝ max(score_i - seed_floor, 0)), propagates
 for a fixed number of iterations (krca_ppr_shard_step: pull SpMV fused with the rank update),
-and ranks pods by propagated mass x own anomaly (krca_ppr_rca_key + krca_topk_i64).
+and ranks pods by the mass they received from their callers times the part of their own anomaly
+that no anomalous dependency explains (krca_rca_explain + krca_rca_key_explained +
+krca_topk_i64; Config.key).
 
 Multi-GPU: one process per GPU; rank g owns pods [g*n_max, (g+1)*n_max): its
 slice of the metric tensor and its rows of the pull-CSR.  Scoring needs no communication.  Each
@@ -180,12 +182,24 @@ class Config:
     * `iters` = 30 fixed iterations (tol = 0): at alpha = 0.5 that is within 1e-10 (L1) of the
       converged vector, so the result is networkx's converged PageRank (pinned at 2k / 20k nodes,
       tests/golden/ppr_nx_meshes.npz);
-    * pods ranked by the key r_i * p_i (propagated mass times own anomaly), top `k`, ties -> lower
-      index.  Ranking by r alone sends the mass to the dependency sinks below the faulty pods
-      (measured recall of the planted roots: DESIGN.md §3.2)."""
+    * pods ranked by `key`, top `k`, ties -> lower index:
+      "explained" (default): recv_i * u_i -- recv_i the mass pod i received from its callers in the
+      last iteration (r_i minus its teleport share), u_i = max(q_i - d_i, 0) the part of its own
+      anomaly q_i that no explaining dependency accounts for (d_i: the largest anomaly among its
+      anomalous dependencies that collect at least as many anomalous callers besides i, or are at
+      least twice as anomalous; krca_rca_explain).  Symptoms show up upstream of a fault (callers
+      -> dependency): a root is anomalous, its callers' mass converges on it, and nothing below it
+      explains it.  Recall of the planted roots 0.93 / 0.93 at C2 (default / spread failure model,
+      3 seeds) and 1.0 / 1.0 at C4 (DESIGN.md §3.2);
+      "rq": r_i * q_i (propagated mass times own anomaly; rounds 2-4): 1.0 on the default model,
+      0.17 / 0.00 at C2 / C4 when the callers carry the larger symptoms."""
+
+    KEYS = ("explained", "rq")
 
     def __init__(self, window=60, z_threshold=3.0, seed_floor=None, alpha=0.5, iters=30, tol=0.0, k=10,
-                 min_floor=4.0):
+                 min_floor=4.0, key="explained"):
+        if key not in self.KEYS:
+            raise ValueError(f"ranking key {key!r}: one of {self.KEYS}")
         self.window = window
         self.z_threshold = z_threshold
         self.seed_floor = seed_floor
@@ -194,6 +208,7 @@ class Config:
         self.tol = tol
         self.k = k
         self.min_floor = min_floor
+        self.key = key
 
     def floor(self, n_pods, n_metrics=1):
         """The seed floor for a mesh of n_pods pods scored over n_metrics metrics each."""
@@ -203,7 +218,7 @@ class Config:
 
     def as_dict(self):
         return dict(window=self.window, z_threshold=self.z_threshold, seed_floor=self.seed_floor, alpha=self.alpha,
-                    iters=self.iters, tol=self.tol, k=self.k, min_floor=self.min_floor)
+                    iters=self.iters, tol=self.tol, k=self.k, min_floor=self.min_floor, key=self.key)
 
     def replace(self, **kw):
         d = self.as_dict()
@@ -221,16 +236,22 @@ def step_flags(tol, last):
 
 
 class Comm:
-    """All-gather over torch.distributed (nccl == RCCL on ROCm; gloo in CPU tests)."""
+    """All-gather over torch.distributed (nccl == RCCL on ROCm; gloo in CPU tests).
 
-    def __init__(self, world=1, rank=0, group=None):
+    collective=True runs the collectives even with one rank (a world-size-1 process group: on a
+    one-GPU box this is how the RCCL call sites -- the per-iteration all-gather, the candidate
+    merge -- execute on the hardware; tests/test_gpu_rccl.py).  Its shards then use the G > 1 slot
+    protocol (DeviceShard(pingpong=False)): the exchange copies send into w_all instead of swapping."""
+
+    def __init__(self, world=1, rank=0, group=None, collective=False):
         self.world, self.rank, self.group = world, rank, group
+        self.collective = bool(collective) or world > 1
         self._gloo = None  # the backend, looked up once
         self._direct = None  # RCCL: (process group, options) for the per-iteration all-gather
 
     def exchange(self, shard):
         """Make every rank's send slice visible in shard.w_all (G = 1: swap the ping-pong pair)."""
-        if self.world == 1:
+        if not self.collective:
             shard.send, shard.w_all = shard.w_all, shard.send
             return
         if self._direct is None:
@@ -238,25 +259,38 @@ class Comm:
         if self._direct:
             # the PageRank exchange runs 30 times per solve: the process group's all-gather called
             # directly skips the public wrapper's per-call checks and option building (host time
-            # that, at 8 ranks, is of the order of the ~20 us step itself)
+            # that, at 8 ranks, is of the order of the ~20 us step itself).  A first
+            # call that raises (an API this torch does not have) falls back to the public wrapper
+            # for good; later failures propagate.
             pg, opts = self._direct
-            pg._allgather_base(shard.w_all, shard.send, opts).wait()
-        else:
-            self.all_gather(shard.w_all, shard.send)
+            try:
+                pg._allgather_base(shard.w_all, shard.send, opts).wait()
+                self.direct_calls += 1
+                return
+            except (AttributeError, TypeError, RuntimeError):
+                if self.direct_calls:
+                    raise
+                self._direct = False
+        self.all_gather(shard.w_all, shard.send)
+
+    direct_calls = 0  # exchanges that took the direct entry point (tests)
 
     def _direct_gather(self):
         """(group, AllgatherOptions) when the backend is RCCL / NCCL and the group has the direct
-        entry point, else False (gloo: the list form of all_gather_flat)."""
+        entry point, else False (gloo: the list form of all_gather_flat).  AllgatherOptions lives
+        in torch.distributed.distributed_c10d (torch 2.10 does not re-export it from
+        torch.distributed: ADVICE r4)."""
         import torch.distributed as dist
         if dist.get_backend(self.group) == "gloo":
             return False
         pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
-        if not hasattr(pg, "_allgather_base") or not hasattr(dist, "AllgatherOptions"):
+        opts_t = getattr(dist.distributed_c10d, "AllgatherOptions", None)
+        if opts_t is None or not hasattr(pg, "_allgather_base"):
             return False
-        return pg, dist.AllgatherOptions()
+        return pg, opts_t()
 
     def all_gather(self, out, inp):
-        if self.world == 1:
+        if not self.collective:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             return
@@ -292,12 +326,18 @@ def all_gather_flat(out, inp, world, group=None, gloo=None):
 class DeviceShard:
     """Per-rank device state (libkrca kernels on torch's current stream)."""
 
-    def __init__(self, engine, x_local, row_ptr_local, col_local, outdeg_local, N, n_max, world, cfg):
+    def __init__(self, engine, x_local, row_ptr_local, col_local, outdeg_local, N, n_max, world, cfg, pingpong=None):
+        """pingpong (default: world == 1): the G = 1 exchange is a swap of two buffers; False with a
+        one-rank collective Comm (the exchange copies send into w_all, the G > 1 slot protocol)."""
         import torch
         self.torch, self.eng, self.cfg = torch, engine, cfg
         lib = engine.lib
         dev = engine.device
         self.N, self.n_max, self.world = N, n_max, world
+        self.pingpong = (world == 1) if pingpong is None else bool(pingpong)
+        if self.pingpong and world != 1:
+            raise ValueError("DeviceShard: the ping-pong exchange needs one rank")
+        self.host_csr = (row_ptr_local, col_local)  # the whole graph when n == N (Explain's default)
         self.x = x_local
         self.M = int(x_local.shape[2]) if x_local is not None and x_local.dim() == 3 else 1  # metrics per pod
         self.n = int(outdeg_local.shape[0])
@@ -311,6 +351,7 @@ class DeviceShard:
         self.q = torch.zeros(max(self.n, 1), **i64)
         self.r = torch.zeros(max(self.n, 1), **i64)
         self.key = torch.zeros(max(self.n, 1), **i64)
+        self.d = torch.zeros(max(self.n, 1), **i64)  # krca_rca_explain's output for these rows
         self.send = torch.zeros(slice_words(n_max), **i64)
         # G = 1: ping-pong pair (the step reads w_all, writes send; the exchange swaps them)
         self.w_all = torch.zeros((1 if world == 1 else world) * slice_words(n_max), **i64)
@@ -319,7 +360,7 @@ class DeviceShard:
         # one device: krca_ppr_solo_step launches the step and its reduction (in the step's last
         # workgroup under KRCA_PPR_FUSE); reduce(first=0) is then a no-op.  Its tolerance is the one
         # of the solve's first reduce(first=1).
-        self.fused = world == 1 and n_max == N
+        self.fused = self.pingpong and n_max == N
         self._tol = 0.0
         # ctypes argument tuples of the per-iteration calls, keyed by the buffers / scalars / stream
         # they bind (at 8 ranks a step is ~5 us of GPU work: rebuilding ~17 ctypes objects per
@@ -427,11 +468,11 @@ class DeviceShard:
         return self.score_out
 
     def _zero_slots(self):
-        """Partial-sum slots zeroed before an init adds into send's set 0 (and, at G = 1, the other
-        ping-pong buffer's, which the first folded step writes)."""
+        """Partial-sum slots zeroed before an init adds into send's set 0 (and, with the ping-pong
+        exchange, the other buffer's, which the first folded step writes)."""
         wsl = wslots(self.n_max)
         self.send[wsl:].zero_()
-        if self.world == 1:
+        if self.pingpong:
             self.w_all[wsl:].zero_()
 
     def init(self, alpha, seed_floor):
@@ -463,7 +504,7 @@ class DeviceShard:
         """Folded iteration `it` (1-based): the reduction of step it - 1 and the step, one kernel."""
         e, p = self.eng, self.eng.ptr
         st = e._stream()
-        nxt = self.w_all if self.world == 1 else self.send
+        nxt = self.w_all if self.pingpong else self.send
         if not self.plan_len:
             # a rank that owns no pods still runs the step's reduction (krca_ppr_shard_step_folded
             # launches it alone for an empty plan): its iteration count and convergence flag must
@@ -501,10 +542,25 @@ class DeviceShard:
         self._chk(e.lib.krca_ppr_shard_reduce(*args), "krca_ppr_shard_reduce")
 
     def local_topk(self, k):
+        """Top-k of the key r_i * q_i (Config key "rq")."""
         e, p = self.eng, self.eng.ptr
         if self.n == 0:
             return np.zeros(0, np.int64), np.zeros(0, np.int64)
         self._chk(e.lib.krca_ppr_rca_key(p(self.r), p(self.q), self.n, p(self.key), e._stream()), "krca_ppr_rca_key")
+        idx, val = e.topk_device(self.key[:self.n], min(k, self.n))
+        return idx, val
+
+    def local_topk_explained(self, k, score_all, floor, graph, lo):
+        """Top-k of the default key (Config key "explained") over this shard's rows, global pods
+        [lo, lo + n): krca_rca_explain over the whole graph (an :class:`Explain`) and every pod's
+        scores, then krca_rca_key_explained from the finished solve's ranks and ctl."""
+        e, p = self.eng, self.eng.ptr
+        if self.n == 0:
+            return np.zeros(0, np.int64), np.zeros(0, np.int64)
+        rp, col = graph.device(e)
+        e.rca_explain_device(score_all, floor, rp, col, lo, lo + self.n, out=self.d)
+        self._chk(e.lib.krca_rca_key_explained(p(self.r), p(self.q), p(self.d), self.n, self.N, p(self.ctl), p(self.key),
+                                               e._stream()), "krca_rca_key_explained")
         idx, val = e.topk_device(self.key[:self.n], min(k, self.n))
         return idx, val
 
@@ -527,9 +583,9 @@ class SplitShard:
 
     def __init__(self, scorer, ppr, spart, ppart, rank, comm):
         import torch
-        if spart.world < 2 or ppart.world not in (1, spart.world) or spart.N != ppart.N:
+        if (spart.world < 2 and not comm.collective) or ppart.world not in (1, spart.world) or spart.N != ppart.N:
             raise ValueError("SplitShard: two partitions of the same pods over the same G > 1 ranks "
-                             "(or one range: the replicated solve)")
+                             "(or one range: the replicated solve; one rank only with a collective Comm)")
         if not np.array_equal(spart.bounds, Partition.uniform(spart.N, spart.world).bounds):
             raise ValueError("SplitShard: the scoring partition must be uniform (its gathered slices are then in pod order)")
         self.scorer, self.ppr, self.comm, self.rank = scorer, ppr, comm, rank
@@ -585,6 +641,11 @@ class SplitShard:
         not after the exchange)."""
         return self.scorer.score()
 
+    def scores_all(self):
+        """The scores of every pod in pod order (the gathered vector; the uniform ranges put the
+        padding at the end)."""
+        return self._all[:self.spart.N]
+
     def exchange_scores(self):
         """Every rank's scores into the PageRank shard's seed vector (one all-gather)."""
         import torch
@@ -594,6 +655,27 @@ class SplitShard:
         else:
             self._pad[:n].copy_(s[:n])
         self.comm.all_gather(self._all[:-1], self._pad)
+
+
+class Explain:
+    """The whole pull-CSR (global pod ids) that krca_rca_explain walks for the default ranking key:
+    host arrays, uploaded once per device on first use and shared by every RcaStep of a process (the
+    bench's two pipeline slots)."""
+
+    def __init__(self, row_ptr, col):
+        self.row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+        self.col = np.ascontiguousarray(col, np.int32)
+        self.N = len(self.row_ptr) - 1
+        if len(self.col) != int(self.row_ptr[-1]) or (len(self.col) and (int(self.col.min()) < 0 or
+                                                                          int(self.col.max()) >= self.N)):
+            raise ValueError("Explain: a pull-CSR with columns in [0, N) and row_ptr[N] == len(col)")
+        self._dev = {}
+
+    def device(self, engine):
+        key = str(engine.device)
+        if key not in self._dev:
+            self._dev[key] = (engine._dev(self.row_ptr), engine._dev(self.col))
+        return self._dev[key]
 
 
 def graph_default(comm, cfg, shard=None):
@@ -618,10 +700,18 @@ class RcaStep:
     Replays compute exactly the eager sequence: the captured kernels and pointers are the same
     (G = 1's ping-pong swaps are baked into the capture)."""
 
-    def __init__(self, shard, comm, cfg, offset, graph=None):
+    def __init__(self, shard, comm, cfg, offset, graph=None, explain=None, part=None):
+        """explain: the whole pull-CSR (an :class:`Explain` or (row_ptr, col)) for the default key;
+        optional when one rank holds the whole graph (its own rows are it).  part: the Partition
+        whose padded slices a coupled G > 1 shard's scores are gathered in (default uniform)."""
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
         self.graph = graph_default(comm, cfg, shard) if graph is None else bool(graph)
         self._g = None
+        if explain is not None and not isinstance(explain, Explain):
+            explain = Explain(*explain)
+        self.explain = explain
+        self.part = part
+        self._sall = None
 
     def propagate(self):
         """Seeded PageRank on the current scores: init, exchange, then iters x (step, exchange, reduce)."""
@@ -660,8 +750,48 @@ class RcaStep:
         if score_events is not None:
             score_events[1].record()
         self.propagate()
-        idx, val = self.s.local_topk(self.cfg.k)
+        idx, val = self.local_candidates()
         return self.merge(idx, val) if to_host else (idx, val)
+
+    def local_candidates(self):
+        """This rank's top-k (local index, key) under cfg.key, after propagate(): "rq" from the
+        ranks alone; "explained" also needs every pod's scores (gathered at G > 1 unless the shard
+        already holds them) and the whole graph."""
+        s, cfg = self.s, self.cfg
+        if cfg.key == "rq":
+            return s.local_topk(cfg.k)
+        ex = self.explain
+        if ex is None:
+            if self.comm.world != 1 or s.n != s.N:
+                raise ValueError("RcaStep: the 'explained' key needs the whole graph (explain=...) at G > 1")
+            ex = self.explain = Explain(*s.host_csr)
+        return s.local_topk_explained(cfg.k, self.scores_all(), cfg.floor(s.N, s.M), ex, self.offset)
+
+    def scores_all(self):
+        """Every pod's score in pod order: the shard's own at G = 1, the gathered vector of a
+        SplitShard, else one all-gather of the ranks' padded slices."""
+        s = self.s
+        if hasattr(s, "scores_all"):
+            return s.scores_all()
+        sc = s.score_out["score"]
+        if self.comm.world == 1:
+            return sc[:s.N]
+        import torch
+        part = self.part or Partition.uniform(s.N, self.comm.world)
+        lo, hi, n_slot = part.range(self.comm.rank)
+        host = isinstance(sc, np.ndarray)
+        t = torch.from_numpy(np.ascontiguousarray(sc, np.float32)) if host else sc
+        if self._sall is None:
+            self._sall = (torch.zeros(n_slot, dtype=torch.float32, device=t.device),
+                          torch.zeros(self.comm.world * n_slot, dtype=torch.float32, device=t.device))
+        pad, out = self._sall
+        pad[:hi - lo].copy_(t[:hi - lo])
+        self.comm.all_gather(out, pad)
+        if np.array_equal(part.bounds, Partition.uniform(s.N, self.comm.world).bounds):
+            res = out[:s.N]
+        else:
+            res = torch.from_numpy(part.unpad(out.cpu().numpy())).to(t.device)
+        return res.numpy() if host else res
 
     def merge(self, idx, val):
         """Gather G x k (global index, key) candidates; identical top-k on every rank."""
@@ -671,7 +801,7 @@ class RcaStep:
             idx = torch.from_numpy(np.asarray(idx, np.int64))
             val = torch.from_numpy(np.asarray(val, np.int64))
         kk = int(idx.numel())
-        if self.comm.world == 1:  # nothing to gather: one copy of (idx | val) to the host
+        if not self.comm.collective:  # nothing to gather: one copy of (idx | val) to the host
             a = torch.cat((idx.to(torch.int64), val.to(torch.int64))).cpu().numpy()
             gi, gv = a[:kk] + self.offset, a[kk:]
             ok = a[:kk] >= 0

@@ -30,7 +30,7 @@ import json
 
 import numpy as np
 
-from .rca import Comm, Config, DeviceShard, Partition, RcaStep, shard_graph
+from .rca import Comm, Config, DeviceShard, Explain, Partition, RcaStep, shard_graph
 
 SNAPSHOT_VERSION = 1
 
@@ -55,9 +55,11 @@ class StreamingRCA:
         self.lo, self.hi, self.n_max = self.part.range(self.comm.rank)
         if shard is None:
             rp, c, od = shard_graph(row_ptr, col, outdeg, self.lo, self.hi, self.part)
-            shard = DeviceShard(engine, None, rp, c, od, self.N, self.n_max, self.comm.world, self.cfg)
+            shard = DeviceShard(engine, None, rp, c, od, self.N, self.n_max, self.comm.world, self.cfg,
+                                pingpong=not self.comm.collective)
         self.shard = shard
-        self.rca = RcaStep(self.shard, self.comm, self.cfg, self.lo)
+        self.rca = RcaStep(self.shard, self.comm, self.cfg, self.lo, part=self.part,
+                           explain=Explain(row_ptr, col) if self.cfg.key == "explained" else None)
         self.t = 0          # metric steps consumed so far
         self.solved = False  # a previous solve exists (warm start)
         self.last_iters = 0
@@ -143,7 +145,7 @@ class StreamingRCA:
                 self.comm.exchange(s)
             s.finish(cfg.alpha, self.tol, it)
             h = s.ctl_async()
-            st.update(it=it, spec=(h, s.local_topk(cfg.k)))
+            st.update(it=it, spec=(h, self.rca.local_candidates()))
         return st
 
     def _rerank_end(self, st):
@@ -174,7 +176,7 @@ class StreamingRCA:
         # the final counts ride behind the key / top-k launches: one synchronisation (the merge's
         # copy of the candidates) instead of a read-back before them
         h = s.ctl_async()
-        top = self.rca.merge(*s.local_topk(cfg.k))
+        top = self.rca.merge(*self.rca.local_candidates())
         iters, conv = s.ctl_wait(h)
         self.last_iters = iters if conv else -iters
         self.solved = True

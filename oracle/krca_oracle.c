@@ -10,7 +10,10 @@
  *   krco_rolling_score  rolling z-score (new primitive, no reference code):
  *                       float64 sliding sums in a fixed order, |z| > thr <=> A^2 > thr^2*B
  *   krco_ppr            networkx 3.4.2 pagerank semantics (_pagerank_scipy) in 2^-60 fixed point
- *   krco_rca_key        root-cause ordering key (PageRank mass x own anomaly)
+ *   krco_rca_key        root-cause ordering key r x q (PageRank mass x own anomaly; Config key "rq")
+ *   krco_rca_explain    the explanation pass of krca_rca_explain: anomalous callers per pod and, per
+ *                       pod, the largest anomaly of a dependency that explains it
+ *   krco_rca_key_explained  the default root-cause key: received mass x unexplained anomaly
  *   krco_corr_z32       the standardized fp32 rows krca_corr_prepare writes (float64 shifted sums
  *                       for mean / scale, then (x - mean) * scale in float32): bit-exact twin
  *   krco_corr_counts    |r| > tau counts over those rows with float64 dot products, and the pairs
@@ -102,10 +105,12 @@ static uint32_t wenc(int64_t w) {
 static int64_t wdec(uint32_t c) { return (int64_t)(c & 0x3FFFFFFu) << (c >> 26); }
 
 /* Pull-CSR personalized PageRank; returns iterations (negative if no convergence).
- * warm != 0: r holds the start vector on entry (krca_ppr_shard_init_warm), else r0 = 2^60/N. */
-int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
-                       const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r,
-                       float* r_out, int64_t* q, int warm) {
+ * warm != 0: r holds the start vector on entry (krca_ppr_shard_init_warm), else r0 = 2^60/N.
+ * recv (optional): the mass each node received from its callers in the last iteration that updated
+ * the ranks (r = recv + teleport share; what krca_rca_key_explained recovers as r - t). */
+int32_t krco_ppr_ex(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const float* seed,
+                    float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r, float* r_out, int64_t* q,
+                    int warm, int64_t* recv) {
   uint32_t* w = (uint32_t*)malloc(sizeof(uint32_t) * N);
   int64_t qtot = 0, dang = 0;
   const int64_t r0 = (int64_t)(kFix / (double)N);
@@ -150,9 +155,19 @@ int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t
     tele = (1.0 - alpha) * kFix + alpha * (double)dn;
   }
   for (int64_t i = 0; i < N; ++i) r_out[i] = (float)((double)r[i] * (1.0 / kFix));
+  if (recv) {
+    /* no iteration: no teleport share was added either (the device's recorded share is 0) */
+    memcpy(recv, it > 0 ? acc : r, sizeof(int64_t) * N);
+  }
   free(w);
   free(acc);
   return (err_limit > 0.0 && !conv) ? -it : it;
+}
+
+int32_t krco_ppr_start(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N,
+                       const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol, int64_t* r,
+                       float* r_out, int64_t* q, int warm) {
+  return krco_ppr_ex(row_ptr, col, outdeg, N, seed, seed_floor, alpha, max_iter, tol, r, r_out, q, warm, NULL);
 }
 
 int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const float* seed,
@@ -164,6 +179,55 @@ int32_t krco_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outd
 void krco_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key) {
   for (int64_t i = 0; i < n; ++i) {
     const double v = (double)r[i] * (double)q[i];
+    memcpy(&key[i], &v, sizeof(v));
+  }
+}
+
+static int64_t quantise(float s, float seed_floor) {
+  const double v = (double)s - (double)seed_floor;
+  return v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
+}
+
+/* The explanation pass of krca_rca_explain (csrc/explain.hip), over the whole pull-CSR (row k = the
+ * callers j of k, edges j -> k).  q_j = the quantised seed of krca_ppr_shard_init.  For every
+ * anomalous pod k (q_k > 0): A_k = its edges from anomalous callers.  An anomalous dependency k of an
+ * anomalous pod j (edge j -> k, j != k) EXPLAINS j when it collects at least as many anomalous
+ * callers besides j (A_k - 1 >= A_j) or is at least twice as anomalous (q_k >= 2 q_j).  d[j - lo] =
+ * the largest q_k over the dependencies that explain j (0: none), for the pods [lo, hi). */
+void krco_rca_explain(const float* score, int64_t N, float seed_floor, const int64_t* row_ptr, const int32_t* col,
+                      int64_t lo, int64_t hi, int64_t* d) {
+  int64_t* q = (int64_t*)malloc(sizeof(int64_t) * (N > 0 ? N : 1));
+  int32_t* A = (int32_t*)calloc(N > 0 ? N : 1, sizeof(int32_t));
+  for (int64_t i = 0; i < N; ++i) q[i] = quantise(score[i], seed_floor);
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (int64_t k = 0; k < N; ++k) {
+    if (q[k] <= 0) continue;
+    int32_t a = 0;
+    for (int64_t e = row_ptr[k]; e < row_ptr[k + 1]; ++e) a += q[col[e]] > 0;
+    A[k] = a;
+  }
+  memset(d, 0, sizeof(int64_t) * (hi > lo ? hi - lo : 0));
+  for (int64_t k = 0; k < N; ++k) {
+    const int64_t qk = q[k];
+    if (qk <= 0) continue;
+    for (int64_t e = row_ptr[k]; e < row_ptr[k + 1]; ++e) {
+      const int64_t j = col[e];
+      if (j < lo || j >= hi || j == k) continue;
+      const int64_t qj = q[j];
+      if (qj <= 0) continue;
+      if ((A[k] - 1 >= A[j] || qk >= 2 * qj) && qk > d[j - lo]) d[j - lo] = qk;
+    }
+  }
+  free(q);
+  free(A);
+}
+
+/* root-cause key of krca_rca_key_explained: u_i = max(q_i - d_i, 0) (the anomaly no explaining
+ * dependency accounts for), key = bits((double)recv_i * (double)u_i), 0 when u_i = 0 */
+void krco_rca_key_explained(const int64_t* recv, const int64_t* q, const int64_t* d, int64_t n, int64_t* key) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t u = q[i] - d[i];
+    const double v = u > 0 ? (double)recv[i] * (double)u : 0.0;
     memcpy(&key[i], &v, sizeof(v));
   }
 }

@@ -403,6 +403,10 @@ def c_lib():
     lib.krco_ppr_start.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp, ctypes.c_int]
     lib.krco_ppr_start.restype = i32
     lib.krco_rca_key.argtypes = [vp, vp, i64, vp]
+    lib.krco_ppr_ex.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp, ctypes.c_int, vp]
+    lib.krco_ppr_ex.restype = i32
+    lib.krco_rca_explain.argtypes = [vp, i64, f32, vp, vp, i64, i64, vp]
+    lib.krco_rca_key_explained.argtypes = [vp, vp, vp, i64, vp]
     lib.krco_corr_z32.argtypes = [vp, i64, i32, i32, i32, vp, vp, vp]
     lib.krco_corr_counts.argtypes = [vp, i64, i32, vp, i64, f64, f64, vp, vp]
     _c = lib
@@ -484,6 +488,45 @@ def c_corr_counts(z32, rows, tau, band_eps=1e-12):
     return cnt, band
 
 
+def c_ppr_ex(row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor, r_start=None):
+    """krco_ppr_ex -> dict(r, rf, it, q, recv): recv = the mass each node received from its callers in
+    the last iteration (r = recv + teleport share); r_start: warm start (krca_ppr_shard_init_warm)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    od = np.ascontiguousarray(outdeg, np.int32)
+    sd = np.ascontiguousarray(seed, np.float32)
+    N = len(od)
+    r = np.zeros(N, np.int64) if r_start is None else np.array(r_start, np.int64, copy=True)
+    q = np.zeros(N, np.int64)
+    recv = np.zeros(N, np.int64)
+    rf = np.zeros(N, np.float32)
+    it = c_lib().krco_ppr_ex(_p(rp), _p(cl), _p(od), N, _p(sd), seed_floor, alpha, max_iter, tol, _p(r), _p(rf), _p(q),
+                             0 if r_start is None else 1, _p(recv))
+    return dict(r=r, rf=rf, it=it, q=q, recv=recv)
+
+
+def c_rca_explain(score, seed_floor, row_ptr, col, lo=0, hi=None):
+    """krco_rca_explain: d[hi - lo] = the largest quantised anomaly of a dependency that explains
+    each pod of [lo, hi), over the whole pull-CSR and the scores of every pod."""
+    sc = np.ascontiguousarray(score, np.float32)
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    N = len(sc)
+    hi = N if hi is None else int(hi)
+    d = np.zeros(max(hi - lo, 0), np.int64)
+    c_lib().krco_rca_explain(_p(sc), N, seed_floor, _p(rp), _p(cl), int(lo), hi, _p(d))
+    return d
+
+
+def c_rca_key_explained(recv, q, d):
+    recv = np.ascontiguousarray(recv, np.int64)
+    q = np.ascontiguousarray(q, np.int64)
+    d = np.ascontiguousarray(d, np.int64)
+    key = np.zeros(len(q), np.int64)
+    c_lib().krco_rca_key_explained(_p(recv), _p(q), _p(d), len(q), _p(key))
+    return key
+
+
 def c_rca_key(r, q):
     r = np.ascontiguousarray(r, np.int64)
     q = np.ascontiguousarray(q, np.int64)
@@ -492,8 +535,26 @@ def c_rca_key(r, q):
     return key
 
 
-def rca_rank(row_ptr, col, outdeg, score, alpha, iters, seed_floor, k=10):
-    """Reference root-cause ranking of the pipeline: top-k of bits(r*q) (ties -> lower index)."""
-    rf, r, it, q = c_ppr(row_ptr, col, outdeg, score, alpha, iters, 0.0, seed_floor, return_q=True)
-    idx, _ = topk_ref(c_rca_key(r, q), k)
-    return idx, rf, r
+def rca_keys(row_ptr, col, outdeg, score, alpha, iters, seed_floor, key="explained", tol=0.0, r_start=None):
+    """The pipeline's root-cause keys (krca.rca.Config.key) of every pod -> (key, ppr dict).
+    "explained": bits(recv_i * u_i), u = the anomaly no explaining dependency accounts for
+    (krco_rca_explain); "rq": bits(r_i * q_i)."""
+    o = c_ppr_ex(row_ptr, col, outdeg, score, alpha, iters, tol, seed_floor, r_start)
+    return rca_keys_from(o, score, seed_floor, row_ptr, col, key), o
+
+
+def rca_keys_from(o, score, seed_floor, row_ptr, col, key="explained"):
+    """The keys of a finished c_ppr_ex solve `o` (dict r, q, recv)."""
+    if key == "rq":
+        return c_rca_key(o["r"], o["q"])
+    if key != "explained":
+        raise ValueError(f"unknown ranking key {key!r}")
+    o["d"] = c_rca_explain(score, seed_floor, row_ptr, col)
+    return c_rca_key_explained(o["recv"], o["q"], o["d"])
+
+
+def rca_rank(row_ptr, col, outdeg, score, alpha, iters, seed_floor, k=10, key="explained"):
+    """Reference root-cause ranking of the pipeline: top-k of the Config key (ties -> lower index)."""
+    kv, o = rca_keys(row_ptr, col, outdeg, score, alpha, iters, seed_floor, key)
+    idx, _ = topk_ref(kv, k)
+    return idx, o["rf"], o["r"]

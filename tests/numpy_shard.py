@@ -50,6 +50,8 @@ class NumpyShard:
         self.n = len(self.deg)
         self.rows = np.repeat(np.arange(self.n), np.diff(self.rp))
         self.ws = wslots(n_max)
+        self.host_csr = (row_ptr_local, col_local)
+        self.recv = np.zeros(self.n, np.int64)  # acc of the last step that updated the rows
         self.send = torch.zeros(slice_words(n_max), dtype=torch.int64)
         self.w_all = torch.zeros((1 if world == 1 else world) * slice_words(n_max), dtype=torch.int64)
         self.ctl = {}
@@ -64,6 +66,7 @@ class NumpyShard:
         self.q = np.where(v > 0, (np.maximum(v, 0) * 4294967296.0).astype(np.int64), 0)
         r0 = np.int64(FIX / float(self.N))
         self.r = np.full(self.n, r0, np.int64)
+        self.recv = self.r.copy()  # no step yet: no teleport share recorded (the device's is 0)
         snd = self.send.numpy()
         snd[self.ws:] = 0
         if self.world == 1:
@@ -124,6 +127,7 @@ class NumpyShard:
         rn = acc + t
         err = int(np.abs(rn - self.r).sum())
         self.r = rn
+        self.recv = acc
         snd = self.send.numpy()
         snd.view(np.uint32)[:self.n] = _w(rn, self.deg, alpha)
         o = self.ws + sset * SET_WORDS
@@ -149,6 +153,12 @@ class NumpyShard:
 
     def local_topk(self, k):
         key = (self.r.astype(np.float64) * self.q.astype(np.float64)).view(np.int64)
+        return oracle.topk_ref(key, min(k, self.n))
+
+    def local_topk_explained(self, k, score_all, floor, graph, lo):
+        """krca_rca_explain (the C restatement over the whole graph) + krca_rca_key_explained."""
+        d = oracle.c_rca_explain(np.asarray(score_all, np.float32), floor, graph.row_ptr, graph.col, lo, lo + self.n)
+        key = oracle.c_rca_key_explained(self.recv, self.q, d)
         return oracle.topk_ref(key, min(k, self.n))
 
     # -- streaming (krca/stream.py): the batch oracle over the series so far ---------------------
@@ -191,6 +201,7 @@ class NumpyShard:
         snd[self.ws:] = 0
         if self.world == 1:
             self.w_all.numpy()[self.ws:] = 0
+        self.recv = self.r.copy()
         snd.view(np.uint32)[:self.n] = _w(self.r, self.deg, alpha)
         snd[self.ws + NSPREAD] = int(self.r[self.deg == 0].sum())
         snd[self.ws + 2 * NSPREAD] = int(self.q.sum())

@@ -52,13 +52,13 @@ class OracleEngine:
         cfg = cfg or RANKING
         seed = np.asarray(seed.cpu() if hasattr(seed, "cpu") else seed, np.float32)
         k = min(int(k or cfg.k), len(outdeg))
-        rf, r, _, q = oracle.c_ppr(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.tol, cfg.floor(len(outdeg), n_metrics),
-                                   return_q=True)
-        idx, _ = oracle.topk_ref(oracle.c_rca_key(r, q), k)
-        rr = r.astype(np.float64) / 2.0 ** 60
-        qt = int(q.sum())
-        p = q[idx].astype(np.float64) / qt if qt > 0 else np.full(len(idx), 1.0 / len(outdeg))
-        return idx, rr[idx] * p, rr
+        key, o = oracle.rca_keys(row_ptr, col, outdeg, seed, cfg.alpha, cfg.iters, cfg.floor(len(outdeg), n_metrics),
+                                 key=cfg.key, tol=cfg.tol)
+        idx, _ = oracle.topk_ref(key, k)
+        rr = o["r"].astype(np.float64) / 2.0 ** 60
+        qt = float(o["q"].sum())
+        val = key[idx].view(np.float64) / (2.0 ** 60 * qt) if qt > 0 else np.zeros(len(idx))
+        return idx, val, rr
 
     def pod_classify(self, pod_code, cont_off, cont_code):
         return oracle.pod_classify_ref(pod_code, cont_off, cont_code)

@@ -4,7 +4,9 @@ oracle; DESIGN.md §3.2 "Ranking").  For seeded C2-shaped meshes (10k pods / 200
 x 1440 steps) with 10 planted root pods and their callers perturbed hop by hop (krca/synth.py),
 reports the recall@10 of the planted roots for PageRank damping alpha, seed floor and ranking key
 (r = propagated mass alone, r*q = mass times own anomaly, psq = mass received from callers x
-sqrt(own anomaly), q = anomaly alone).  --spread: the callers carry the symptoms (synth.spread_hops).
+sqrt(own anomaly), explained = mass received from callers x the anomaly no explaining dependency
+accounts for (krca.rca.Config's default key), q = anomaly alone).  --spread: the callers carry the
+symptoms (synth.spread_hops).
 
   python tests/ranking_ablation.py [--seeds 3] [--out profiles/r2/ranking_ablation.json]
 """
@@ -43,8 +45,8 @@ def main():
     a = ap.parse_args()
     from scipy.special import ndtri
     auto = round(float(ndtri(1.0 - 1.0 / (2.0 * a.pods * 8))), 3)  # expected max |z| of P*M null series
-    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0, auto, 5.0) for key in ("r", "rq", "psq")] + \
-        [(None, None, "q")]
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in (0.0, 4.0, auto, 5.0)
+            for key in ("r", "rq", "psq", "explained")] + [(None, None, "q")]
     hits = {d: [] for d in defs}
     for seed in range(a.seeds):
         m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)
@@ -56,6 +58,9 @@ def main():
         for al, fl, key in defs:
             if key == "q":
                 idx, _ = oracle.topk_ref(s.astype(np.float64), 10)
+            elif key == "explained":
+                kv, _ = oracle.rca_keys(m.row_ptr, m.col, m.outdeg, s, al, 30, fl, key="explained")
+                idx, _ = oracle.topk_ref(kv, 10)
             else:
                 _, r, _, q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, s, al, 30, 0.0, fl, return_q=True)
                 kv = oracle.c_rca_key(r, q) if key == "rq" else psq_key(r, q, al) if key == "psq" else r

@@ -72,8 +72,17 @@ def test_pod_classify_columnar_scale(eng, P):
 
 
 def test_ranked_root_causes_c1(eng):
+    """The device ranking of the C1 mock equals the oracle engine's (tests/test_agents_cpu.py pins the
+    order and explains it), scores included; with key "rq" the rounds-2-4 order is kept too."""
+    from oracle_engine import OracleEngine
+    from krca.rca import RANKING
     res = A.Coordinator(A.Shim(), engine=eng).run_analysis("comprehensive", A.NS)
+    ref = A.Coordinator(A.Shim(), engine=OracleEngine()).run_analysis("comprehensive", A.NS)
     assert [r["component"] for r in res["ranked_root_causes"]] == [
+        "Service/database", "Service/api-gateway", "Service/frontend", "Service/backend", "Service/resource-service"]
+    assert [r["score"] for r in res["ranked_root_causes"]] == [r["score"] for r in ref["ranked_root_causes"]]
+    rq = A.Coordinator(A.Shim(), engine=eng, rank_config=RANKING.replace(key="rq")).run_analysis("comprehensive", A.NS)
+    assert [r["component"] for r in rq["ranked_root_causes"]] == [
         "Service/api-gateway", "Service/database", "Service/backend", "Service/resource-service", "Service/frontend"]
 
 

@@ -38,17 +38,28 @@ def run_bench(n, extra=()):
 def test_bench_gpus_2_runs_two_ranks():
     one = run_bench(1, ["--profile"])
     two = run_bench(2, ["--profile", "--ppr-partition", "balanced"])
-    # the PageRank rows on the scoring's own uniform ranges (no score all-gather; the default below N = 4)
-    two_u = run_bench(2, ["--no-corr", "--no-cpu-baseline"])
+    # the PageRank rows on the scoring's own uniform ranges (no score all-gather)
+    two_u = run_bench(2, ["--ppr-partition", "uniform", "--no-corr", "--no-cpu-baseline"])
+    # auto: the sharded solve unless the all-gather measured at startup costs more than the margin
+    two_a = run_bench(2, ["--no-corr", "--no-cpu-baseline"])
     # every rank solves the whole mesh on the all-gathered scores (no collective inside the solve)
     two_r = run_bench(2, ["--ppr-partition", "replicated", "--no-corr", "--no-cpu-baseline"])
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["world_ranks"] == 2
-    assert two["rca_top10"] == one["rca_top10"] == two_u["rca_top10"] == two_r["rca_top10"]
+    assert two["rca_top10"] == one["rca_top10"] == two_u["rca_top10"] == two_r["rca_top10"] == two_a["rca_top10"]
+    # the exchange probe and the mode auto took from it
+    ex = two_a["ppr_exchange"]
+    assert two_a["ppr_exchange_us"] == ex["allgather_us"] > 0 and ex["copy_us"] > 0 and ex["bytes_per_rank"] > 0
+    want = "replicated" if ex["iters_x_extra_ms"] > ex["margin_ms"] else "uniform"
+    assert two_a["ppr_mode"] == want, ex
+    assert two["ppr_mode"] == "balanced" and two_r["ppr_mode"] == "replicated" and one["ppr_exchange_us"] is None
+    # the ranking on the spread failure model (untimed C2-size mesh on rank 0), checked against the oracle
+    assert one["spread_check"]["top10_identical"] and one["planted_root_recall_spread"] >= 0.8, one["spread_check"]
+    assert one["config"]["ranking_key"] == "explained"
     assert two_r["config"]["ppr_bounds"] == [0, 20000]
     # PageRank on Partition.balanced ranges, scores all-gathered (krca.rca.SplitShard; the default at N >= 4)
     assert two["config"]["ppr_bounds"] != two["config"]["shard_bounds"], two["config"]
     assert two_u["config"]["ppr_bounds"] == two_u["config"]["shard_bounds"]
-    for vu in (two_u["verify"], two_r["verify"]):
+    for vu in (two_u["verify"], two_r["verify"], two_a["verify"]):
         assert vu["ppr_fixed_point_bit_identical"] and vu["top10_identical"] and vu["n_exceed_flags_bit_exact"], vu
     assert two["profile"]["krca_ppr_shard_step_folded"]["launches"] == 30
     assert two["profile"]["score_exchange"]["launches"] == 1 and two["profile"]["krca_rolling_score"]["launches"] == 1

@@ -10,7 +10,7 @@ Checked:
 - 13-bin histograms, line counts and first-3 examples, and template histograms of 20,000 sampled
   containers == the oracle (Python re / str.splitlines, FNV-1a of the template);
 - the cold and the warm-started fixed-point ranks bit-identical to the C oracle chain
-  (oracle.c_ppr, oracle.c_ppr_warm), with the same iteration counts and top-10.
+  (oracle.c_ppr_ex cold, then warm), with the same iteration counts and top-10 (krca.rca.Config's key).
 """
 import numpy as np
 import pytest
@@ -78,15 +78,16 @@ def test_c5_full_window_1m_pods():
         want = oracle.template_hist(docs[d])
         assert list(zip(th[d0[d]:d0[d] + nt[d]].tolist(), tc[d0[d]:d0[d] + nt[d]].tolist())) == want, d
     # ranks: cold then warm, bit-identical to the C oracle chain
-    rf, r_ref, it_ref, q = oracle.c_ppr(mesh.row_ptr, mesh.col, mesh.outdeg, sc0, cfg.alpha, 100, 1e-9,
-                                        cfg.floor(P, M), return_q=True)
+    fl = cfg.floor(P, M)
+    o = oracle.c_ppr_ex(mesh.row_ptr, mesh.col, mesh.outdeg, sc0, cfg.alpha, 100, 1e-9, fl)
+    r_ref, it_ref = o["r"], o["it"]
     assert np.array_equal(r0, r_ref) and it0 == it_ref
-    ridx, _ = oracle.topk_ref(oracle.c_rca_key(r_ref, q), cfg.k)
+    ridx, _ = oracle.topk_ref(oracle.rca_keys_from(o, sc0, fl, mesh.row_ptr, mesh.col), cfg.k)
     assert [int(i) for i in top0] == [int(i) for i in ridx]
     score = sc["score"].cpu().numpy()
-    r_ref, it, q = oracle.c_ppr_warm(mesh.row_ptr, mesh.col, mesh.outdeg, score, r_ref, cfg.alpha, 100, 1e-9,
-                                     cfg.floor(P, M))
+    o = oracle.c_ppr_ex(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, 100, 1e-9, fl, r_start=r_ref)
+    r_ref, it = o["r"], o["it"]
     assert np.array_equal(s.shard.r[:P].cpu().numpy(), r_ref) and s.last_iters == it
-    ridx, _ = oracle.topk_ref(oracle.c_rca_key(r_ref, q), cfg.k)
+    ridx, _ = oracle.topk_ref(oracle.rca_keys_from(o, score, fl, mesh.row_ptr, mesh.col), cfg.k)
     assert [int(i) for i in top] == [int(i) for i in ridx]
     print(f"C5 window: {scan['n_lines_total']} lines, cold solve {it0} iterations, warm {it}")

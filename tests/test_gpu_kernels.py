@@ -605,6 +605,69 @@ def test_rca_sharded_path_emulated_on_one_gpu(eng, G, folded):
     _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
     got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
     assert np.array_equal(got, r)
+    # the default key per shard (every pod's scores, the whole graph) = the oracle's, bit for bit
+    from krca.rca import Explain
+    ex, sall = Explain(m.row_ptr, m.col), torch.from_numpy(score).cuda()
+    key_ref, _ = oracle.rca_keys(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8))
+    for g, s in enumerate(shards):
+        lo = shard_range(n, G, g)[0]
+        s.local_topk_explained(cfg.k, sall, cfg.floor(n, 8), ex, lo)
+        assert np.array_equal(s.key[:s.n].cpu().numpy(), key_ref[lo:lo + s.n]), g
+
+
+def _explain_graph(n, rng, hubs=True):
+    """A random pull-CSR with hub rows, duplicate edges, self-loops and empty rows."""
+    from krca.agents.topology import csr_from_edges
+    E = n * 8
+    src = rng.integers(0, n, E)
+    dst = np.where(rng.random(E) < (0.3 if hubs else 0.0), rng.integers(0, max(n // 50, 1), E), rng.integers(0, n, E))
+    src = np.concatenate([src, src[:n // 10]])  # duplicates
+    dst = np.concatenate([dst, dst[:n // 10]])
+    loops = rng.integers(0, n, n // 20)
+    return csr_from_edges(n, np.concatenate([src, loops]), np.concatenate([dst, loops]))
+
+
+@pytest.mark.parametrize("n", [1, 7, 3000, 200_000])
+def test_rca_explain_kernel_vs_oracle(eng, n):
+    """krca_rca_explain (csrc/explain.hip) against the C restatement krco_rca_explain: every pod's
+    explaining anomaly d, bit for bit, for the whole range and for sub-ranges (a rank's rows), with
+    few / many / no anomalous pods (floor above every score) and ties of A and of 2q."""
+    rng = np.random.default_rng(n)
+    rp, col, od = _explain_graph(n, rng)
+    rpd, cold = torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda()
+    for frac, floor in ((0.02, 4.0), (0.5, 1.0), (0.0, 100.0)):
+        score = np.where(rng.random(n) < frac, 4.0 + rng.integers(0, 6, n) * 0.5, rng.random(n) * 3.0).astype(np.float32)
+        sd = torch.from_numpy(score).cuda()
+        for lo, hi in ((0, n), (n // 3, n - n // 4), (0, 0), (n - 1, n)):
+            if hi < lo:
+                continue
+            got = eng.rca_explain_device(sd, floor, rpd, cold, lo, hi)[:hi - lo].cpu().numpy()
+            ref = oracle.c_rca_explain(score, floor, rp, col, lo, hi)
+            assert np.array_equal(got, ref), (frac, floor, lo, hi)
+        if frac == 0.02:
+            assert 0 < int((ref > 0).sum()) < n
+
+
+def test_rca_key_explained_single_device_vs_oracle(eng):
+    """The whole default ranking on one device (DeviceShard + RcaStep; and krca_ppr +
+    rank_root_causes): every key bit-identical to oracle.rca_keys, fixed iterations and L1 tolerance."""
+    from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph
+    n = 20000
+    m = synth.make_graph(n, avg_degree=20, seed=31)
+    x = synth.make_metrics(n, 8, 200, window=60, seed=31, roots=m.roots,
+                           hop_sets=synth.spread_hops(m, m.roots, seed=31), **synth.SPREAD_SIGMAS).cuda()
+    for cfg in (Config(), Config(tol=1e-9, iters=100, alpha=0.85)):
+        sh = DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, 0, n), n, n, 1, cfg)
+        step = RcaStep(sh, Comm(), cfg, 0)
+        idx, _ = step.run()
+        score = sh.score_out["score"].cpu().numpy()
+        key, o = oracle.rca_keys(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), tol=cfg.tol)
+        assert np.array_equal(sh.r[:n].cpu().numpy(), o["r"])
+        assert np.array_equal(sh.key[:n].cpu().numpy(), key)
+        ridx = oracle.topk_ref(key, cfg.k)[0]
+        assert [int(i) for i in idx] == ridx.tolist()
+        got = eng.rank_root_causes(score, m.row_ptr, m.col, m.outdeg, cfg, n_metrics=8)[0]
+        assert got.tolist() == ridx.tolist()
 
 
 @pytest.mark.parametrize("n,G", [(9, 4), (49, 8), (30000, 3)])

@@ -33,7 +33,9 @@ def _csr(edges, n):
     return rp, src[o].astype(np.int32), np.bincount(src, minlength=n).astype(np.int32)
 
 
-GOLDEN_CFG = RANKING.replace(seed_floor=4.0)  # the goldens were captured at the fixed floor 4
+# the goldens were captured at the fixed floor 4 with the rounds-2-4 key r * q (they pin the
+# PageRank vector and that key's top-10; the default key is checked against the oracle below)
+GOLDEN_CFG = RANKING.replace(seed_floor=4.0, key="rq")
 
 
 def _rca_from_scores(eng, rp, col, od, score, cfg=GOLDEN_CFG):
@@ -43,7 +45,7 @@ def _rca_from_scores(eng, rp, col, od, score, cfg=GOLDEN_CFG):
     sh.score_out = {"score": torch.from_numpy(np.ascontiguousarray(score, np.float32)).cuda()}
     st = RcaStep(sh, Comm(), cfg, 0)
     st.propagate()
-    idx, _ = st.merge(*sh.local_topk(cfg.k))
+    idx, _ = st.merge(*st.local_candidates())
     return [int(i) for i in idx], sh.r[:n].cpu().numpy()
 
 
@@ -61,6 +63,11 @@ def test_ranking_pinned_to_networkx(eng, name):
     top, rfix = _rca_from_scores(eng, rp, col, od, s)           # the bench / RcaStep path
     assert top == g[f"{name}_top10"].tolist()
     assert np.array_equal(rfix.astype(np.float64) / 2.0 ** 60, r)  # same fixed point
+    # the default key on the same solve: both device paths equal the oracle
+    cfg = GOLDEN_CFG.replace(key="explained")
+    ref, _, _ = oracle.rca_rank(rp, col, od, s, cfg.alpha, cfg.iters, cfg.floor(n), cfg.k)
+    assert eng.rank_root_causes(s, rp, col, od, cfg)[0].tolist() == ref.tolist()
+    assert _rca_from_scores(eng, rp, col, od, s, cfg)[0] == ref.tolist()
 
 
 def test_coordinator_ranking_equals_bench_path(eng):

@@ -63,16 +63,11 @@ def test_stream_windows_rerank_warm_started(eng):
         out = s.window(xd[t:t + d].contiguous())
         t += d
         score = out["scores"]["score"].cpu().numpy()
-        if r_ref is None:
-            rf, r_ref, it = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, 60, 1e-9, cfg.floor(P, M))
-            q = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, 60, 1e-9, cfg.floor(P, M),
-                             return_q=True)[3]
-        else:
-            r_ref, it, q = oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, score, r_ref, cfg.alpha, 60, 1e-9,
-                                             cfg.floor(P, M))
+        o = oracle.c_ppr_ex(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, 60, 1e-9, cfg.floor(P, M), r_start=r_ref)
+        r_ref, it = o["r"], o["it"]
         assert np.array_equal(s.shard.r[:P].cpu().numpy(), r_ref), t
         assert out["iters"] == it, (t, out["iters"], it)
-        ridx, _ = oracle.topk_ref(oracle.c_rca_key(r_ref, q), cfg.k)
+        ridx, _ = oracle.topk_ref(oracle.rca_keys_from(o, score, cfg.floor(P, M), m.row_ptr, m.col), cfg.k)
         assert [int(i) for i in out["top"][0]] == [int(i) for i in ridx], t
 
 

@@ -67,7 +67,9 @@ def _worker(rank, world, port, out_q, balanced=False):
         shard = SplitShard(scorer, ppr, spart, part, rank, comm)
     else:
         shard = NumpyShard(x[:, lo:hi, :], rp, col, od, N, n_max, world, cfg)
-    idx, key = RcaStep(shard, step_comm, cfg, lo).run()
+    # the default key needs every pod's scores (gathered, or the SplitShard's) and the whole graph
+    idx, key = RcaStep(shard, step_comm, cfg, lo, explain=(m.row_ptr, m.col), part=None if balanced in (
+        "split", "replicated") else part).run()
     out_q.put((rank, lo, shard.r.copy(), [int(i) for i in idx], [int(k) for k in key]))
     dist.barrier()
     dist.destroy_process_group()

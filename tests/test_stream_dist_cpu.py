@@ -101,12 +101,10 @@ def test_sharded_stream_matches_oracle_chain(world, snap, short, tmp_path):
     for wi, d in enumerate(WINDOWS):
         t += d
         score = oracle.c_rolling_score(x[:t], W)["score"]
-        if r_ref is None:
-            _, r_ref, it = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, FLOOR)
-            q_ = oracle.c_ppr(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, FLOOR, return_q=True)[3]
-        else:
-            r_ref, it, q_ = oracle.c_ppr_warm(m.row_ptr, m.col, m.outdeg, score, r_ref, 0.5, 60, 1e-9, FLOOR)
-        top = oracle.topk_ref(oracle.c_rca_key(r_ref, q_), 10)[0].tolist()
+        # cold, then warm from the previous window's ranks; the default key of krca.rca.Config
+        o = oracle.c_ppr_ex(m.row_ptr, m.col, m.outdeg, score, 0.5, 60, 1e-9, FLOOR, r_start=r_ref)
+        r_ref, it = o["r"], o["it"]
+        top = oracle.topk_ref(oracle.rca_keys_from(o, score, FLOOR, m.row_ptr, m.col), 10)[0].tolist()
         r_sh = np.concatenate([res[g][wi][0] for g in range(world)])
         assert np.array_equal(r_sh, r_ref), (world, wi)
         for g in range(world):

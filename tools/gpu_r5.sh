@@ -1,0 +1,51 @@
+#!/bin/bash
+# Round-5 GPU call: named steps, each under its own time limit, stopping at the first failure.
+# usage: tools/gpu_r5.sh TAG step [step ...]
+#   tests        all -m gpu tests                    tests_K      -m gpu tests matching -k K
+#   bench        bench.py default line               bench_trace  rocprofv3 stats of bench.py
+#   rank_def     tools/ranking_ablation_c4.py (C4, 2 seeds, default failure model)
+#   rank_spread  the same on the spread failure model
+#   ppr          rocprofv3 stats of the C4 PageRank propagate   logs / tmpl  same for logs / templates
+#   corr100k / corr1m   rocprofv3 stats of the correlation at C3 / 1M pods (tau 0.5)
+#   c5           tools/bench_stream.py (C5 window)   g8           tools/g8_step_emulation.py --decoupled
+#   pmc_*        PMC passes (tools/gpu_pmc_exact.sh targets)
+set -u
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+finish() {
+  find $O -name '*.db' -delete
+  find $O -name '*kernel_trace.csv' -size +4M -delete
+}
+trap finish EXIT
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 $secs "$@" > $O/$name.log 2>&1
+  local rc=$?; echo "$name EXIT=$rc" >> $O/status
+  [ $rc -eq 0 ] || { echo "stop after $name"; tail -30 $O/$name.log; exit $rc; }
+  tail -3 $O/$name.log
+}
+prof() {  # prof NAME SECONDS ARGS... (rocprofv3 kernel-trace stats of python3 ARGS)
+  local name=$1 secs=$2; shift 2
+  step $name $secs rocprofv3 --kernel-trace --stats --output-format csv -d $O/$name -o run -- python3 "$@"
+}
+for s in "$@"; do
+  case $s in
+    tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread ;;
+    tests_*) step $s 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "${s#tests_}" ;;
+    bench) step bench 400 python3 bench.py ;;
+    bench_trace) prof bench_trace 500 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify ;;
+    rank_def) step rank_def 900 python3 -u tools/ranking_ablation_c4.py --out $O/ranking_ablation_c4.json ;;
+    rank_spread) step rank_spread 900 python3 -u tools/ranking_ablation_c4.py --spread --out $O/ranking_ablation_spread_c4.json ;;
+    ppr) prof ppr 300 tools/ppr_bench.py --reps 10 ;;
+    logs) prof logs 300 tools/prof_kernels.py logs --reps 5 ;;
+    tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
+    corr100k) prof corr100k 400 tools/prof_kernels.py corr --pods 100000 --reps 3 ;;
+    corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 ;;
+    c5) step c5 400 python3 tools/bench_stream.py ;;
+    g8) step g8 600 python3 -u tools/g8_step_emulation.py --decoupled ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

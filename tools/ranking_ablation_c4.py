@@ -2,8 +2,10 @@
 """Root-cause ranking definitions on the C4 mesh (1M pods / 20M edges, 8 metrics x 1440 steps) on
 the GPU, through the bench's own pieces (krca.rca.DeviceShard / RcaStep: the device scoring and
 the bit-exact fixed-point PageRank).  Recall@10 of the 10 planted roots for damping alpha, seed
-floor and ranking key (r = propagated mass, rq = mass x own anomaly = krca.rca.Config's key,
-q = own anomaly alone), plus the diagnostics that explain them: each root's score s (max |z| at the
+floor and ranking key (r = propagated mass, rq = mass x own anomaly (rounds 2-4), psq = mass received
+x sqrt(own anomaly), explained = mass received x the anomaly no explaining dependency accounts for
+(krca.rca.Config's key; its top-10 at the Config's alpha and floor also checked against the C
+oracle), q = own anomaly alone), plus the diagnostics that explain them: each root's score s (max |z| at the
 last step) and its rank among all pods, and how many pods pass each floor.  The "auto" floor is
 the expected maximum |z| of P*M null series, Phi^-1(1 - 1/(2 P M)).
 
@@ -39,12 +41,16 @@ def main():
     a = ap.parse_args()
     import torch
     from krca import native, synth
-    from krca.rca import RANKING, Comm, DeviceShard, RcaStep, shard_graph
+    from krca.rca import RANKING, Comm, DeviceShard, Explain, RcaStep, shard_graph
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
     eng = native.NativeEngine(0)
     M, T = 8, 1440
     af = auto_floor(a.pods * M)
     floors = [0.0, 4.0, 5.0, round(af, 3), 6.0]
-    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in floors for key in ("r", "rq", "psq")] + [(None, None, "q")]
+    defs = [(al, fl, key) for al in (0.85, 0.5) for fl in floors for key in ("r", "rq", "psq", "explained")] + \
+        [(None, None, "q")]
+    checks = []
     hits = {d: [] for d in defs}
     diag = []
     for seed in range(a.seeds):
@@ -55,6 +61,7 @@ def main():
         x = synth.make_metrics_range(0, a.pods, M, T, seed=seed, roots=m.roots, hop_sets=hops, device="cuda", **kw)
         rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, a.pods)
         sh = DeviceShard(eng, x, rp, col, od, a.pods, a.pods, 1, RANKING)
+        ex = Explain(m.row_ptr, m.col)
         sh.score()
         s = sh.score_out["score"].cpu().numpy()
         roots = set(m.roots.tolist())
@@ -72,12 +79,15 @@ def main():
             if key == "q":
                 idx = order[:10]
             else:
-                cfg = RANKING.replace(alpha=al, seed_floor=fl)
+                cfg = RANKING.replace(alpha=al, seed_floor=fl, key="rq" if key != "explained" else key)
                 sh.cfg = cfg
-                st = RcaStep(sh, Comm(), cfg, 0)
+                st = RcaStep(sh, Comm(), cfg, 0, explain=ex)
                 st.propagate()
-                if key == "rq":
-                    idx, _ = st.merge(*sh.local_topk(10))
+                if key in ("rq", "explained"):
+                    idx, _ = st.merge(*st.local_candidates())
+                    if key == "explained" and al == RANKING.alpha and fl == round(af, 3):
+                        ref, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, s, al, cfg.iters, fl, 10)
+                        checks.append(dict(seed=seed, top10_identical=[int(i) for i in idx] == ref.tolist()))
                 elif key == "psq":  # mass received from callers x sqrt(own anomaly) (tests/ranking_ablation.py)
                     rr, qq = sh.r[:a.pods].double(), sh.q[:a.pods].double()
                     p = qq / qq.sum() * 2.0 ** 60 if float(qq.sum()) > 0 else torch.zeros_like(qq)
@@ -92,7 +102,7 @@ def main():
     rows = [dict(alpha=al, seed_floor=fl, key=key, recall_at_10=float(np.mean(v)), per_seed=v)
             for (al, fl, key), v in hits.items()]
     out = dict(config=dict(vars(a), metrics=M, tsteps=T, window=RANKING.window, auto_floor=af), rows=rows,
-               diagnostics=diag)
+               diagnostics=diag, oracle_checks=checks)
     txt = json.dumps(out, indent=1)
     if a.out:
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
@@ -100,6 +110,7 @@ def main():
     for r in rows:
         print(f"alpha={r['alpha']} floor={r['seed_floor']} key={r['key']:3s} recall@10={r['recall_at_10']:.2f} "
               f"{r['per_seed']}", flush=True)
+    print("oracle checks:", checks, flush=True)
 
 
 if __name__ == "__main__":
