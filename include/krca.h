@@ -132,7 +132,8 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
  * krca_template_hash: hash[l] for every line of krca_log_match.
  * krca_template_hist: per container d, the distinct hashes of its lines in ascending order and
  *   their counts, written to out_hash/out_count at the container's own line range
- *   [doc_line0[d], doc_line0[d] + n_templates[d]); sort-based.  Containers of <= 8 lines are sorted
+ *   [doc_line0[d], doc_line0[d] + n_templates[d]); the slots past n_templates[d] are NOT written
+ *   (krca.native zero-fills out_hash / out_count first, so its outputs hold 0 there).  Sort-based.  Containers of <= 8 lines are sorted
  *   in one lane's registers, <= 64 by a wave, <= krca_template_max_lines() by a workgroup, all on
  *   device lists (no host round trip).  workspace: krca_template_hist_ws_size(ndocs) bytes, int32
  *   {mid, big, huge counts, 0 | mid list [D] | big list [D] | huge list [D]}: containers above
@@ -311,16 +312,17 @@ int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key
 /* The default root-cause key (krca.rca.Config key "explained"; the sink of
  * ref:agents/coordinator.py:157-184, edge direction of ref:agents/topology_agent.py:94-159: caller
  * -> dependency).  krca_rca_explain: over the WHOLE pull-CSR and the scores of every pod (score_all
- * [N]; q_j = the quantised seed of krca_ppr_shard_init), A_k = edges from anomalous callers of each
- * anomalous pod k; an anomalous dependency k of an anomalous pod j (edge j -> k, j != k) explains j
- * when A_k - 1 >= A_j or q_k >= 2 q_j; d_local[j - lo] = the largest q_k over the dependencies that
- * explain j, for the pods [lo, hi) (0: none).  Only anomalous pods' rows are walked; integer counts
- * and maxima, so bit-identical to oracle/krca_oracle.c krco_rca_explain.  ws:
- * krca_rca_explain_ws_size(N) bytes, no initialisation needed.
- * krca_rca_key_explained: key_i = bits((double)recv_i * (double)u_i) with u_i = q_i - d_i (0 when
- * <= 0) and recv_i = r_i - t_i, the mass row i received from its callers in the solve's last step (t_i
- * = that step's teleport share, from the scale the step recorded in ctl): the rows and ctl of a
- * finished krca_ppr_shard_* / krca_ppr solve, N = the mesh's node count. */
+ * [N]; q_j = the quantised seed of krca_ppr_shard_init), for each anomalous pod k A_k = its edges
+ * from anomalous callers and S_k = the sum of their q; an anomalous dependency k of an anomalous pod
+ * j (edge j -> k, j != k) explains j when (A_k - 1 >= A_j or q_k >= 2 q_j) and A_k q_j <= 3 S_k;
+ * d_local[j - lo] = the largest q_k over the dependencies that explain j, for the pods [lo, hi) (0:
+ * none).  Only anomalous pods' rows are walked; integer counts, sums and maxima, so bit-identical
+ * to oracle/krca_oracle.c krco_rca_explain.  ws: krca_rca_explain_ws_size(N) bytes, no
+ * initialisation needed.
+ * krca_rca_key_explained: key_i = bits(((double)recv_i + (double)t_i / 32) * (double)u_i) with u_i =
+ * q_i - d_i (0 when <= 0), t_i the row's teleport share in the solve's last step (from the scale the
+ * step recorded in ctl) and recv_i = r_i - t_i, the mass the row received from its callers: the rows
+ * and ctl of a finished krca_ppr_shard_* / krca_ppr solve, N = the mesh's node count. */
 int64_t krca_rca_explain_ws_size(int64_t N);
 int krca_rca_explain(const float* score_all, int64_t N, float seed_floor, const int64_t* row_ptr, const int32_t* col,
                      int64_t lo, int64_t hi, int64_t* d_local /*[hi - lo]*/, void* ws, void* stream);

@@ -6,10 +6,12 @@
 // explain it:
 //   q_j   the quantised seed of krca_ppr_shard_init (2^32 per |z| unit above the floor; q > 0 =
 //         anomalous);
-//   A_k   per anomalous pod k: its edges from anomalous callers (row k of the pull-CSR);
+//   A_k   per anomalous pod k: its edges from anomalous callers (row k of the pull-CSR), S_k the sum
+//         of their q;
 //   an anomalous dependency k of an anomalous pod j (edge j -> k, j != k) explains j when it collects
 //   at least as many anomalous callers besides j (A_k - 1 >= A_j: the symptoms converge on k) or is
-//   at least twice as anomalous (q_k >= 2 q_j);
+//   at least twice as anomalous (q_k >= 2 q_j), AND j looks like k's other symptoms (A_k q_j <=
+//   3 S_k: at most 3x their mean -- a pod far above them is a fault of its own that calls k);
 //   d_j   the largest q_k over the dependencies that explain j (0: none).
 // Integer counts and an integer max: the result is independent of the schedule and bit-identical to
 // oracle/krca_oracle.c krco_rca_explain.
@@ -20,7 +22,7 @@
 // collective beyond the scores (all-gathered once per step at G > 1).  Three launches, no host sync:
 //   rca_anomalous        one pass over the N scores (4 B per pod): the anomalous pods' ids, compacted
 //                        with a wave ballot and one atomic per wave (the order does not matter);
-//   rca_caller_counts    a wave per anomalous pod: A_k over its row (lanes stride the callers);
+//   rca_caller_counts    a wave per anomalous pod: A_k and S_k over its row (lanes stride the callers);
 //   rca_explain_scatter  a wave per anomalous pod k: for each anomalous caller j of the rank's range
 //                        that k explains, a 64-bit atomicMax of q_k into d[j - lo].
 #include <algorithm>
@@ -38,6 +40,10 @@ __device__ __forceinline__ int64_t quantise(float s, float floor_) {  // == ppr.
 
 __device__ __forceinline__ int wave_sum(int v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += (int64_t)__shfl_xor((long long)v, off, 64);
   return v;
 }
 
@@ -65,16 +71,26 @@ __global__ __launch_bounds__(TPB) void rca_caller_counts(const int32_t* __restri
                                                          const uint32_t* __restrict__ n_list,
                                                          const float* __restrict__ s, float fl,
                                                          const int64_t* __restrict__ row_ptr,
-                                                         const int32_t* __restrict__ col, int32_t* __restrict__ A) {
+                                                         const int32_t* __restrict__ col, int32_t* __restrict__ A,
+                                                         int64_t* __restrict__ S) {
   const int lane = threadIdx.x & 63;
   const int64_t n = *n_list;
   for (int64_t w = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6; w < n; w += ((int64_t)gridDim.x * TPB) >> 6) {
     const int32_t k = list[w];
     const int64_t e1 = row_ptr[k + 1];
     int c = 0;
-    for (int64_t e = row_ptr[k] + lane; e < e1; e += 64) c += quantise(s[col[e]], fl) > 0;
+    int64_t sum = 0;
+    for (int64_t e = row_ptr[k] + lane; e < e1; e += 64) {
+      const int64_t qc = quantise(s[col[e]], fl);
+      c += qc > 0;
+      sum += qc;  // 0 for a caller at or below the floor
+    }
     c = wave_sum(c);
-    if (lane == 0) A[k] = c;
+    sum = wave_sum64(sum);
+    if (lane == 0) {
+      A[k] = c;
+      S[k] = sum;
+    }
   }
 }
 
@@ -83,7 +99,8 @@ __global__ __launch_bounds__(TPB) void rca_explain_scatter(const int32_t* __rest
                                                            const float* __restrict__ s, float fl,
                                                            const int64_t* __restrict__ row_ptr,
                                                            const int32_t* __restrict__ col,
-                                                           const int32_t* __restrict__ A, int64_t lo, int64_t hi,
+                                                           const int32_t* __restrict__ A,
+                                                           const int64_t* __restrict__ S, int64_t lo, int64_t hi,
                                                            unsigned long long* __restrict__ d) {
   const int lane = threadIdx.x & 63;
   const int64_t n = *n_list;
@@ -91,13 +108,14 @@ __global__ __launch_bounds__(TPB) void rca_explain_scatter(const int32_t* __rest
     const int32_t k = list[w];
     const int64_t qk = quantise(s[k], fl);
     const int32_t ak = A[k];
+    const int64_t sk3 = 3 * S[k];
     const int64_t e1 = row_ptr[k + 1];
     for (int64_t e = row_ptr[k] + lane; e < e1; e += 64) {
       const int64_t j = col[e];
       if (j < lo || j >= hi || j == k) continue;
       const int64_t qj = quantise(s[j], fl);
       if (qj <= 0) continue;
-      if (ak - 1 >= A[j] || qk >= 2 * qj) atomicMax(d + (j - lo), (unsigned long long)qk);
+      if ((ak - 1 >= A[j] || qk >= 2 * qj) && (int64_t)ak * qj <= sk3) atomicMax(d + (j - lo), (unsigned long long)qk);
     }
   }
 }
@@ -108,8 +126,8 @@ constexpr int64_t kListGrid = 1024;  // waves x 4 per workgroup walking the anom
 
 extern "C" {
 
-// workspace: A int32[N] | list int32[N] | counter (256 B)
-int64_t krca_rca_explain_ws_size(int64_t N) { return 8 * std::max<int64_t>(N, 1) + 256; }
+// workspace: S int64[N] | A int32[N] | list int32[N] | counter (256 B)
+int64_t krca_rca_explain_ws_size(int64_t N) { return 16 * std::max<int64_t>(N, 1) + 256; }
 
 int krca_rca_explain(const float* score_all, int64_t N, float seed_floor, const int64_t* row_ptr, const int32_t* col,
                      int64_t lo, int64_t hi, int64_t* d_local, void* ws, void* stream) {
@@ -117,20 +135,21 @@ int krca_rca_explain(const float* score_all, int64_t N, float seed_floor, const 
   KRCA_CHECK_ARG(score_all && row_ptr && col && ws && (hi == lo || d_local), "krca_rca_explain: null pointer");
   hipStream_t st = krca::as_stream(stream);
   char* p = reinterpret_cast<char*>(ws);
-  int32_t* A = reinterpret_cast<int32_t*>(p);
+  int64_t* S = reinterpret_cast<int64_t*>(p);
+  int32_t* A = reinterpret_cast<int32_t*>(p + 8 * N);
   int32_t* list = A + N;
-  uint32_t* n_list = reinterpret_cast<uint32_t*>(p + 8 * N);
+  uint32_t* n_list = reinterpret_cast<uint32_t*>(p + 16 * N);
   KRCA_HIP(hipMemsetAsync(n_list, 0, sizeof(uint32_t), st));
   if (hi > lo) KRCA_HIP(hipMemsetAsync(d_local, 0, (hi - lo) * sizeof(int64_t), st));
   const unsigned g0 = (unsigned)std::min<int64_t>(krca::ceil_div(N, TPB), 2048);
   hipLaunchKernelGGL(rca_anomalous, dim3(g0), dim3(TPB), 0, st, score_all, N, seed_floor, list, n_list);
   KRCA_LAUNCH_CHECK();
   hipLaunchKernelGGL(rca_caller_counts, dim3((unsigned)kListGrid), dim3(TPB), 0, st, list, n_list, score_all,
-                     seed_floor, row_ptr, col, A);
+                     seed_floor, row_ptr, col, A, S);
   KRCA_LAUNCH_CHECK();
   if (hi > lo) {
     hipLaunchKernelGGL(rca_explain_scatter, dim3((unsigned)kListGrid), dim3(TPB), 0, st, list, n_list, score_all,
-                       seed_floor, row_ptr, col, A, lo, hi, reinterpret_cast<unsigned long long*>(d_local));
+                       seed_floor, row_ptr, col, A, S, lo, hi, reinterpret_cast<unsigned long long*>(d_local));
     KRCA_LAUNCH_CHECK();
   }
   return KRCA_OK;

@@ -687,7 +687,8 @@ __global__ __launch_bounds__(TPB) void ppr_rca_key(const int64_t* __restrict__ r
 // the default root-cause key (krca_rca_key_explained): u_i = q_i - d_i (the anomaly that no
 // explaining dependency accounts for, d from krca_rca_explain), recv_i = r_i - t_i (the mass the row
 // received from its callers in the last step: t_i is that step's teleport share, update_row's
-// expression with the recorded scale), key = bits((double)recv_i * (double)u_i), 0 when u_i <= 0
+// expression with the recorded scale), key = bits(((double)recv_i + (double)t_i / 32) * (double)u_i),
+// 0 when u_i <= 0 (the own share at 1/32: a fault whose callers carry no anomaly still ranks by it)
 __global__ __launch_bounds__(TPB) void rca_key_explained(const int64_t* __restrict__ r, const int64_t* __restrict__ q,
                                                          const int64_t* __restrict__ d, int64_t n, int64_t N,
                                                          const Ctl* __restrict__ ctl, int64_t* __restrict__ key) {
@@ -700,7 +701,7 @@ __global__ __launch_bounds__(TPB) void rca_key_explained(const int64_t* __restri
     double v = 0.0;
     if (u > 0) {
       const int64_t t = qt > 0 ? (int64_t)((double)qi * tq) : tu;
-      v = (double)(r[i] - t) * (double)u;
+      v = ((double)(r[i] - t) + (double)t * 0.03125) * (double)u;
     }
     key[i] = __double_as_longlong(v);
   }

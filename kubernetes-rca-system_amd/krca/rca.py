@@ -183,15 +183,17 @@ class Config:
       converged vector, so the result is networkx's converged PageRank (pinned at 2k / 20k nodes,
       tests/golden/ppr_nx_meshes.npz);
     * pods ranked by `key`, top `k`, ties -> lower index:
-      "explained" (default): recv_i * u_i -- recv_i the mass pod i received from its callers in the
-      last iteration (r_i minus its teleport share), u_i = max(q_i - d_i, 0) the part of its own
-      anomaly q_i that no explaining dependency accounts for (d_i: the largest anomaly among its
-      anomalous dependencies that collect at least as many anomalous callers besides i, or are at
-      least twice as anomalous; krca_rca_explain).  Symptoms show up upstream of a fault (callers
-      -> dependency): a root is anomalous, its callers' mass converges on it, and nothing below it
-      explains it.  Recall of the planted roots 0.93 / 0.93 at C2 (default / spread failure model,
-      3 seeds) and 1.0 / 1.0 at C4 (DESIGN.md §3.2);
-      "rq": r_i * q_i (propagated mass times own anomaly; rounds 2-4): 1.0 on the default model,
+      "explained" (default): (recv_i + t_i / 32) * u_i -- recv_i the mass pod i received from its
+      callers in the last iteration, t_i its own teleport share (r_i = recv_i + t_i), u_i =
+      max(q_i - d_i, 0) the part of its own anomaly q_i that no explaining dependency accounts for
+      (d_i: the largest anomaly among its anomalous dependencies k that collect at least as many
+      anomalous callers besides i, or are at least twice as anomalous, and whose other anomalous
+      callers look like i -- i at most 3x their mean; krca_rca_explain).  Symptoms show up upstream
+      of a fault (callers -> dependency): a root is anomalous, its callers' mass converges on it, and
+      nothing below it explains it.  Recall of the planted roots: C2 1.00 / 0.90
+      (default / spread failure model, CPU oracle, 3 seeds), 10k-40k default meshes 1.00, C4 on the
+      GPU in profiles/r5;
+      "rq": r_i * q_i (propagated mass times own anomaly; rounds 2-4): 1.00 on the default model,
       0.17 / 0.00 at C2 / C4 when the callers carry the larger symptoms."""
 
     KEYS = ("explained", "rq")

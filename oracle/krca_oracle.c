@@ -190,21 +190,35 @@ static int64_t quantise(float s, float seed_floor) {
 
 /* The explanation pass of krca_rca_explain (csrc/explain.hip), over the whole pull-CSR (row k = the
  * callers j of k, edges j -> k).  q_j = the quantised seed of krca_ppr_shard_init.  For every
- * anomalous pod k (q_k > 0): A_k = its edges from anomalous callers.  An anomalous dependency k of an
- * anomalous pod j (edge j -> k, j != k) EXPLAINS j when it collects at least as many anomalous
- * callers besides j (A_k - 1 >= A_j) or is at least twice as anomalous (q_k >= 2 q_j).  d[j - lo] =
- * the largest q_k over the dependencies that explain j (0: none), for the pods [lo, hi). */
+ * anomalous pod k (q_k > 0): A_k = its edges from anomalous callers and S_k = the sum of their q.  An
+ * anomalous dependency k of an anomalous pod j (edge j -> k, j != k) EXPLAINS j when
+ *   (A_k - 1 >= A_j  or  q_k >= 2 q_j)   -- the symptoms converge on k (at least as many anomalous
+ *                                           callers besides j), or k is at least twice as anomalous --
+ *   and A_k q_j <= 3 S_k                 -- j looks like k's other symptoms (its anomaly at most 3x
+ *                                           the mean over k's anomalous callers; a pod far above
+ *                                           them is a fault of its own that happens to call k).
+ * d[j - lo] = the largest q_k over the dependencies that explain j (0: none), for pods [lo, hi).
+ * Integer arithmetic throughout (A_k q_j, 3 S_k < 2^63 for q < 2^40 and A < 2^23). */
 void krco_rca_explain(const float* score, int64_t N, float seed_floor, const int64_t* row_ptr, const int32_t* col,
                       int64_t lo, int64_t hi, int64_t* d) {
   int64_t* q = (int64_t*)malloc(sizeof(int64_t) * (N > 0 ? N : 1));
+  int64_t* S = (int64_t*)calloc(N > 0 ? N : 1, sizeof(int64_t));
   int32_t* A = (int32_t*)calloc(N > 0 ? N : 1, sizeof(int32_t));
   for (int64_t i = 0; i < N; ++i) q[i] = quantise(score[i], seed_floor);
 #pragma omp parallel for schedule(dynamic, 1024)
   for (int64_t k = 0; k < N; ++k) {
     if (q[k] <= 0) continue;
     int32_t a = 0;
-    for (int64_t e = row_ptr[k]; e < row_ptr[k + 1]; ++e) a += q[col[e]] > 0;
+    int64_t sum = 0;
+    for (int64_t e = row_ptr[k]; e < row_ptr[k + 1]; ++e) {
+      const int64_t qc = q[col[e]];
+      if (qc > 0) {
+        a += 1;
+        sum += qc;
+      }
+    }
     A[k] = a;
+    S[k] = sum;
   }
   memset(d, 0, sizeof(int64_t) * (hi > lo ? hi - lo : 0));
   for (int64_t k = 0; k < N; ++k) {
@@ -215,19 +229,22 @@ void krco_rca_explain(const float* score, int64_t N, float seed_floor, const int
       if (j < lo || j >= hi || j == k) continue;
       const int64_t qj = q[j];
       if (qj <= 0) continue;
-      if ((A[k] - 1 >= A[j] || qk >= 2 * qj) && qk > d[j - lo]) d[j - lo] = qk;
+      if ((A[k] - 1 >= A[j] || qk >= 2 * qj) && (int64_t)A[k] * qj <= 3 * S[k] && qk > d[j - lo]) d[j - lo] = qk;
     }
   }
   free(q);
+  free(S);
   free(A);
 }
 
 /* root-cause key of krca_rca_key_explained: u_i = max(q_i - d_i, 0) (the anomaly no explaining
- * dependency accounts for), key = bits((double)recv_i * (double)u_i), 0 when u_i = 0 */
-void krco_rca_key_explained(const int64_t* recv, const int64_t* q, const int64_t* d, int64_t n, int64_t* key) {
+ * dependency accounts for), t_i = r_i - recv_i (the row's own teleport share in the last step),
+ * key = bits(((double)recv_i + (double)t_i / 32) * (double)u_i), 0 when u_i = 0 */
+void krco_rca_key_explained(const int64_t* r, const int64_t* recv, const int64_t* q, const int64_t* d, int64_t n,
+                            int64_t* key) {
   for (int64_t i = 0; i < n; ++i) {
     const int64_t u = q[i] - d[i];
-    const double v = u > 0 ? (double)recv[i] * (double)u : 0.0;
+    const double v = u > 0 ? ((double)recv[i] + (double)(r[i] - recv[i]) * 0.03125) * (double)u : 0.0;
     memcpy(&key[i], &v, sizeof(v));
   }
 }

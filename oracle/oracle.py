@@ -406,7 +406,7 @@ def c_lib():
     lib.krco_ppr_ex.argtypes = [vp, vp, vp, i64, vp, f32, f64, i32, f64, vp, vp, vp, ctypes.c_int, vp]
     lib.krco_ppr_ex.restype = i32
     lib.krco_rca_explain.argtypes = [vp, i64, f32, vp, vp, i64, i64, vp]
-    lib.krco_rca_key_explained.argtypes = [vp, vp, vp, i64, vp]
+    lib.krco_rca_key_explained.argtypes = [vp, vp, vp, vp, i64, vp]
     lib.krco_corr_z32.argtypes = [vp, i64, i32, i32, i32, vp, vp, vp]
     lib.krco_corr_counts.argtypes = [vp, i64, i32, vp, i64, f64, f64, vp, vp]
     _c = lib
@@ -518,12 +518,13 @@ def c_rca_explain(score, seed_floor, row_ptr, col, lo=0, hi=None):
     return d
 
 
-def c_rca_key_explained(recv, q, d):
+def c_rca_key_explained(r, recv, q, d):
+    r = np.ascontiguousarray(r, np.int64)
     recv = np.ascontiguousarray(recv, np.int64)
     q = np.ascontiguousarray(q, np.int64)
     d = np.ascontiguousarray(d, np.int64)
     key = np.zeros(len(q), np.int64)
-    c_lib().krco_rca_key_explained(_p(recv), _p(q), _p(d), len(q), _p(key))
+    c_lib().krco_rca_key_explained(_p(r), _p(recv), _p(q), _p(d), len(q), _p(key))
     return key
 
 
@@ -550,7 +551,7 @@ def rca_keys_from(o, score, seed_floor, row_ptr, col, key="explained"):
     if key != "explained":
         raise ValueError(f"unknown ranking key {key!r}")
     o["d"] = c_rca_explain(score, seed_floor, row_ptr, col)
-    return c_rca_key_explained(o["recv"], o["q"], o["d"])
+    return c_rca_key_explained(o["r"], o["recv"], o["q"], o["d"])
 
 
 def rca_rank(row_ptr, col, outdeg, score, alpha, iters, seed_floor, k=10, key="explained"):

@@ -158,7 +158,7 @@ class NumpyShard:
     def local_topk_explained(self, k, score_all, floor, graph, lo):
         """krca_rca_explain (the C restatement over the whole graph) + krca_rca_key_explained."""
         d = oracle.c_rca_explain(np.asarray(score_all, np.float32), floor, graph.row_ptr, graph.col, lo, lo + self.n)
-        key = oracle.c_rca_key_explained(self.recv, self.q, d)
+        key = oracle.c_rca_key_explained(self.r, self.recv, self.q, d)
         return oracle.topk_ref(key, min(k, self.n))
 
     # -- streaming (krca/stream.py): the batch oracle over the series so far ---------------------

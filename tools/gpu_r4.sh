@@ -76,8 +76,6 @@ for s in "$@"; do
     ppr) prof ppr 300 tools/prof_kernels.py ppr --reps 5 ;;
     ppr_g8) step ppr_g8 300 python3 tools/ppr_g8_emulation.py ;;
     log_timing) export KRCA_LOG_FUSED=1 KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/libkrca_ltime.so; step log_timing 300 python3 tools/log_timing.py; unset KRCA_LIB KRCA_LOG_FUSED ;;
-    repeat_window) step repeat_window 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 ;;
-    repeat_window_unfused) step repeat_window_unfused 500 python3 -u tools/repeat_test.py tests/test_gpu_stream.py test_stream_window_log_overlap_and_error_path 12 KRCA_LOG_FUSED=0 ;;
     diag_window) step diag_window 300 python3 -u tools/diag_window_templates.py ;;
     g8_step) step g8_step 400 python3 tools/g8_step_emulation.py ;;
     g8_dec) step g8_dec 500 python3 tools/g8_step_emulation.py --decoupled 1.0,1.5,2.0 ;;
