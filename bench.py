@@ -4,8 +4,9 @@
 BASELINE.json metric, configs[3] shape: synthetic 1M-pod / ~20M-edge mesh, 8 metrics x 1440
 steps (46 GB of float32 metrics — it fits one MI355X, so N=1 runs the whole mesh).  One step =
 the full RCA hot path (krca/rca.py): rolling z-scores of every pod -> seeded personalized
-PageRank (30 fixed-point iterations) -> root-cause top-10 on the host.  Inputs are resident in
-HBM before timing; nothing is cached across steps.
+PageRank (integer fixed point to networkx's L1 stop rule, tol 1e-10, at most 30 iterations: 11
+at C4) -> root-cause top-10 on the host.  Inputs are resident in HBM before timing; nothing is
+cached across steps.
 
 Multi-GPU: `python bench.py --gpus N` starts N ranks itself (a `torch.distributed.run` child
 process, before anything touches the GPU); under an external launcher (WORLD_SIZE set) it must
@@ -44,7 +45,9 @@ def parse(argv=None):
     ap.add_argument("--metrics", type=int, default=8)
     ap.add_argument("--tsteps", type=int, default=1440)
     ap.add_argument("--window", type=int, default=RANKING.window)
-    ap.add_argument("--iters", type=int, default=RANKING.iters)
+    ap.add_argument("--iters", type=int, default=RANKING.iters, help="PageRank iteration cap")
+    ap.add_argument("--tol", type=float, default=RANKING.tol,
+                    help="networkx L1 stop rule (sum |r - r_prev| < N * tol); 0 = exactly --iters iterations")
     ap.add_argument("--alpha", type=float, default=RANKING.alpha)
     ap.add_argument("--seed-floor", type=float, default=RANKING.seed_floor,
                     help="personalization floor in |z| units (default: krca.rca.Config's scale-aware floor)")
@@ -201,14 +204,16 @@ def profile_step(step, stream, world):
             timed("score_exchange", s.exchange_scores)
         else:
             timed("krca_rolling_score", s.score)
-        # the sequence RcaStep._propagate runs: init, exchange, iters x (folded step, exchange), finish
+        # the sequence RcaStep.propagate runs: init, exchange, n x (folded step, exchange), finish, with
+        # n = the planned steps (under the stop rule: the previous solve's count + 1)
+        n = step.plan_iters()
         timed("krca_ppr_shard_init", lambda: s.init(cfg.alpha, cfg.floor(s.N, s.M)))
         timed("exchange", lambda: c.exchange(s))
-        for it in range(1, cfg.iters + 1):
+        for it in range(1, n + 1):
             timed("krca_ppr_shard_step_folded",
-                  lambda: s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == cfg.iters)))
+                  lambda: s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == n)))
             timed("exchange", lambda: c.exchange(s))
-        timed("krca_ppr_shard_finish", lambda: s.finish(cfg.alpha, cfg.tol, cfg.iters))
+        timed("krca_ppr_shard_finish", lambda: s.finish(cfg.alpha, cfg.tol, n))
         timed("key+topk", lambda: step.local_candidates())
         t1.record()
     torch.cuda.synchronize()
@@ -310,7 +315,7 @@ def verify_step(args, cfg, mesh, shard, x, part, ppart, rank):
     if rank != 0:
         return {}
     ridx, _, r = oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, sc_all, cfg.alpha, cfg.iters, cfg.seed_floor,
-                                 cfg.k, key=cfg.key)
+                                 cfg.k, key=cfg.key, tol=cfg.tol)
     return {"ppr_fixed_point_bit_identical": bool(np.array_equal(r_all, r)),
             "oracle_top10": [int(i) for i in ridx],
             "ranks_gathered": world, "score_sample_pods": int(ns_all),
@@ -334,7 +339,7 @@ def cpu_baseline(args, cfg, mesh, shard, x, n_loc):
         oracle.c_rolling_score(xs, args.window)
         t2 = time.perf_counter()
         oracle.rca_rank(mesh.row_ptr, mesh.col, mesh.outdeg, score, cfg.alpha, cfg.iters, cfg.seed_floor, cfg.k,
-                        key=cfg.key)
+                        key=cfg.key, tol=cfg.tol)
         t3 = time.perf_counter()
         if i >= args.cpu_warmup:
             t_sc.append(t2 - t1)
@@ -380,7 +385,7 @@ def spread_recall(eng, cfg, seed, pods=10_000, edges=200_000):
     idx, _ = step.run()
     top = [int(i) for i in idx]
     ref, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, step.s.score_out["score"].cpu().numpy(), c.alpha, c.iters,
-                                c.floor(pods, 8), c.k, key=c.key)
+                                c.floor(pods, 8), c.k, key=c.key, tol=c.tol)
     del x, step
     torch.cuda.empty_cache()
     return {"recall": len(set(top) & set(m.roots.tolist())) / len(m.roots), "top10_identical": top == ref.tolist(),
@@ -518,7 +523,7 @@ def main():
         else:
             dist.init_process_group(backend)
     eng = native.NativeEngine(local)
-    cfg = Config(window=args.window, seed_floor=args.seed_floor, alpha=args.alpha, iters=args.iters)
+    cfg = Config(window=args.window, seed_floor=args.seed_floor, alpha=args.alpha, iters=args.iters, tol=args.tol)
     cfg = cfg.replace(seed_floor=cfg.floor(args.pods, args.metrics))  # resolved once: every rank, the oracle
 
     # ---- synthetic mesh (host graph, device metrics; not timed) --------------------------
@@ -593,7 +598,7 @@ def main():
 
     def finish(j, idx, val):
         with torch.cuda.stream(streams[j]):
-            return steps[j].merge(idx, val)
+            return steps[j].merge(*steps[j].settle(idx, val))
 
     def run_steps(n, events=None, marks=None):
         """marks: host time after each step's top-10 is on the host (per-step spacing)."""
@@ -671,9 +676,11 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f32 (f64 window sums, int64 fixed-point ranks)",
             "data": "synthetic (seeded mesh generator krca/synth.py; no network)",
             "config": {"workload": "C4: synthetic 1M-pod / 20M-edge mesh, 8 metrics x 1440 steps, full RCA step "
-                                   "(rolling z-score -> 30-iteration seeded PPR -> top-10), ranking of krca.rca.Config",
+                                   "(rolling z-score -> seeded PPR to networkx's L1 stop rule -> top-10), ranking of "
+                                   "krca.rca.Config",
                        "pods": args.pods, "edges": mesh.n_edges, "metrics": args.metrics, "tsteps": args.tsteps,
-                       "window": args.window, "ppr_iters": args.iters, "alpha": args.alpha,
+                       "window": args.window, "ppr_iter_cap": args.iters, "ppr_tol": args.tol,
+                       "alpha": args.alpha,
                        "seed_floor": cfg.seed_floor, "parallelism": f"pod-sharded x{world}",
                        "partition": "uniform contiguous pod ranges (krca.rca.Partition.uniform)",
                        "shard_bounds": [int(b) for b in part.bounds],
@@ -704,6 +711,7 @@ def main():
                                        "bytes_per_step": score_bytes(args.pods, args.metrics, args.tsteps),
                                        "slowest_rank_avg_launch_ms": score_ms_max}},
             "rca_top10": [int(i) for i in top_idx],
+            "ppr_iters_run": step.last_iters,
             "world_ranks": world, "backend": backend if world > 1 else None,
             "planted_root_recall": len(set(int(i) for i in top_idx) & set(mesh.roots.tolist())) / len(mesh.roots),
         }

@@ -738,7 +738,9 @@ class NativeEngine:
         k = min(int(k or cfg.k), N)
         floor = cfg.floor(N, n_metrics)
         sd = self._dev(np.asarray(seed, np.float32)) if not isinstance(seed, torch.Tensor) else self._dev(seed, torch.float32)
-        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, sd, cfg.alpha, cfg.iters, cfg.tol, floor)
+        # the ranking's stop rule caps the iterations: a graph too small for the weight codes to reach
+        # the tolerance runs all cfg.iters (krca.rca.Config), as RcaStep and the oracle do
+        r, rf, q, _ = self._ppr_full(row_ptr, col, outdeg, sd, cfg.alpha, cfg.iters, cfg.tol, floor, allow_nonconv=True)
         key = torch.empty_like(rf)
         if cfg.key == "rq":
             _check(self.lib.krca_ppr_rca_key(self.ptr(rf), self.ptr(q), rf.numel(), self.ptr(key), self._stream()),
@@ -757,13 +759,13 @@ class NativeEngine:
         val = kv / (2.0 ** 60 * qt) if qt > 0 else np.zeros(len(idx))
         return idx, val, rr
 
-    def _ppr_full(self, row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor):
+    def _ppr_full(self, row_ptr, col, outdeg, seed, alpha, max_iter, tol, seed_floor, allow_nonconv=False):
         torch = self.torch
         rp_host = np.asarray(row_ptr, dtype=np.int64)
         plan, n, pk, lane, _ = self.ppr_pack(rp_host, col)
         sd = self._dev(seed, torch.float32) if isinstance(seed, torch.Tensor) else self._dev(np.asarray(seed, np.float32))
         return self.ppr_device(self._dev(rp_host), pk, self._dev(np.asarray(outdeg, np.int32)), plan, n, lane, sd, alpha,
-                               max_iter, tol, seed_floor)
+                               max_iter, tol, seed_floor, allow_nonconv=allow_nonconv)
 
 
 _default = None

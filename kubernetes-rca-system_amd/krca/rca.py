@@ -179,9 +179,14 @@ class Config:
       the mesh's P·M null series, at least `min_floor` = 4 (:func:`null_floor`; 4.0 up to ~16k
       series, 5.286 at the C4 mesh's 8M): a fixed floor lets the noise maxima of a large mesh
       (|z| ≈ 6 over 8M series) seed the walk (measured: DESIGN.md §3.2);
-    * `iters` = 30 fixed iterations (tol = 0): at alpha = 0.5 that is within 1e-10 (L1) of the
-      converged vector, so the result is networkx's converged PageRank (pinned at 2k / 20k nodes,
-      tests/golden/ppr_nx_meshes.npz);
+    * networkx's L1 stop rule: iterate until sum |r - r_prev| < N * `tol` (tol = 1e-10), at most
+      `iters` = 30 iterations (a mesh too small for the weight codes to reach the tolerance -- N
+      below ~100 -- runs all 30, which at alpha = 0.5 is within 1e-9 of the converged vector).  At
+      C4 the rule stops after 11 iterations, 1.6e-5 of the mass from the 30-iteration vector, top-10
+      identical on both failure models; tol = 0 runs exactly `iters` (the rounds
+      2-4 definition, pinned to networkx 3.4.2 at 2k / 20k nodes: tests/golden/ppr_nx_meshes.npz).
+      :class:`RcaStep` issues the previous solve's count + 1 steps without a host poll and checks
+      the count when the step's candidates are settled;
     * pods ranked by `key`, top `k`, ties -> lower index:
       "explained" (default): (recv_i + t_i / 32) * u_i -- recv_i the mass pod i received from its
       callers in the last iteration, t_i its own teleport share (r_i = recv_i + t_i), u_i =
@@ -198,7 +203,7 @@ class Config:
 
     KEYS = ("explained", "rq")
 
-    def __init__(self, window=60, z_threshold=3.0, seed_floor=None, alpha=0.5, iters=30, tol=0.0, k=10,
+    def __init__(self, window=60, z_threshold=3.0, seed_floor=None, alpha=0.5, iters=30, tol=1e-10, k=10,
                  min_floor=4.0, key="explained"):
         if key not in self.KEYS:
             raise ValueError(f"ranking key {key!r}: one of {self.KEYS}")
@@ -708,15 +713,30 @@ class RcaStep:
         whose padded slices a coupled G > 1 shard's scores are gathered in (default uniform)."""
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
         self.graph = graph_default(comm, cfg, shard) if graph is None else bool(graph)
+        if self.graph and cfg.tol > 0:
+            raise ValueError("RcaStep: the HIP-graph solve needs a fixed-iteration Config (tol = 0)")
         self._g = None
         if explain is not None and not isinstance(explain, Explain):
             explain = Explain(*explain)
         self.explain = explain
         self.part = part
         self._sall = None
+        self.last_iters = 0  # iterations of the last solve (negative: the cap without convergence)
+        self._spec = None    # under a tolerance: (steps issued, ctl poll handle) of the solve in flight
+
+    def plan_iters(self):
+        """Folded steps the next solve issues: cfg.iters for a fixed-iteration solve; under a
+        tolerance the previous solve's count + 1 (the last step finds the count's convergence and
+        does nothing), cfg.iters before any history or after a solve that hit the cap."""
+        cfg = self.cfg
+        if cfg.tol > 0 and self.last_iters > 0:
+            return min(self.last_iters + 1, cfg.iters)
+        return cfg.iters
 
     def propagate(self):
         """Seeded PageRank on the current scores: init, exchange, then iters x (step, exchange, reduce)."""
+        if self.cfg.tol > 0:
+            return self._propagate_tol()
         if not self.graph:
             return self._propagate()
         import torch
@@ -744,6 +764,48 @@ class RcaStep:
             c.exchange(s)
         s.finish(cfg.alpha, cfg.tol, cfg.iters)
 
+    def _propagate_tol(self):
+        """Under the L1 stop rule: plan_iters() folded steps with no host poll (steps past
+        convergence exit on the device-held flag), the last step's reduction, and a poll of the
+        count enqueued behind them (read by settle())."""
+        s, c, cfg = self.s, self.comm, self.cfg
+        n = self.plan_iters()
+        s.init(cfg.alpha, cfg.floor(s.N, s.M))
+        c.exchange(s)
+        for it in range(1, n + 1):
+            s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == n))
+            c.exchange(s)
+        s.finish(cfg.alpha, cfg.tol, n)
+        self._spec = (n, s.ctl_async())
+
+    def settle(self, idx, val):
+        """After propagate() + local_candidates() under a tolerance: read the solve's count; if the
+        planned steps fell short of convergence (the scores moved), continue in polled batches of 4
+        to convergence or the cap and recompute the candidates.  Every rank takes the same branch
+        (the counts come from the same gathered slots).  Returns the (possibly new) candidates."""
+        if self._spec is None:
+            return idx, val
+        s, c, cfg = self.s, self.comm, self.cfg
+        n, h = self._spec
+        self._spec = None
+        iters, conv = s.ctl_wait(h)
+        if not conv and n < cfg.iters:
+            it, pending = n, None
+            while it < cfg.iters:
+                for _ in range(min(4, cfg.iters - it)):
+                    it += 1
+                    s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, False))
+                    c.exchange(s)
+                if pending is not None and s.ctl_wait(pending)[1]:
+                    break
+                pending = s.ctl_async() if it < cfg.iters else None
+            s.finish(cfg.alpha, cfg.tol, it)
+            h = s.ctl_async()
+            idx, val = self.local_candidates()
+            iters, conv = s.ctl_wait(h)
+        self.last_iters = iters if conv else -iters
+        return idx, val
+
     def run(self, to_host=True, score_events=None):
         """One RCA step; score_events = (start, end) HIP events recorded around the scoring kernel."""
         if score_events is not None:
@@ -752,7 +814,7 @@ class RcaStep:
         if score_events is not None:
             score_events[1].record()
         self.propagate()
-        idx, val = self.local_candidates()
+        idx, val = self.settle(*self.local_candidates())
         return self.merge(idx, val) if to_host else (idx, val)
 
     def local_candidates(self):

@@ -554,8 +554,9 @@ def rca_keys_from(o, score, seed_floor, row_ptr, col, key="explained"):
     return c_rca_key_explained(o["r"], o["recv"], o["q"], o["d"])
 
 
-def rca_rank(row_ptr, col, outdeg, score, alpha, iters, seed_floor, k=10, key="explained"):
-    """Reference root-cause ranking of the pipeline: top-k of the Config key (ties -> lower index)."""
-    kv, o = rca_keys(row_ptr, col, outdeg, score, alpha, iters, seed_floor, key)
+def rca_rank(row_ptr, col, outdeg, score, alpha, iters, seed_floor, k=10, key="explained", tol=0.0):
+    """Reference root-cause ranking of the pipeline: top-k of the Config key (ties -> lower index);
+    iters = the cap, tol = the L1 stop rule (krca.rca.Config)."""
+    kv, o = rca_keys(row_ptr, col, outdeg, score, alpha, iters, seed_floor, key, tol=tol)
     idx, _ = topk_ref(kv, k)
     return idx, o["rf"], o["r"]

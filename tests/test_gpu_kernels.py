@@ -522,7 +522,8 @@ def test_rca_step_single_gpu_vs_oracle(eng, n, iters):
     step = RcaStep(DeviceShard(eng, x, rp, col, od, n, n_max, 1, cfg), Comm(), cfg, 0)
     idx, key = step.run()
     score = step.s.score_out["score"].cpu().numpy()
-    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
+    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k,
+                                  tol=cfg.tol)
     assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
     assert list(idx) == list(ridx)
     idx2, _ = step.run()  # re-run on the same buffers: identical
@@ -537,7 +538,7 @@ def test_rca_step_graph_replay_equals_eager(eng):
     n = 20000
     m = synth.make_graph(n, avg_degree=20, seed=5)
     hops = synth.caller_hops(m, m.roots)
-    cfg = Config(iters=30)
+    cfg = Config(iters=30, tol=0.0)  # the graph replays a fixed-iteration solve
     lo, hi, n_max = shard_range(n, 1, 0)
     rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
     xs = [synth.make_metrics(n, 8, 300, window=60, seed=s, roots=m.roots, hop_sets=hops).cuda() for s in (1, 2)]
@@ -602,13 +603,14 @@ def test_rca_sharded_path_emulated_on_one_gpu(eng, G, folded):
             for s in shards:
                 s.reduce(cfg.alpha, cfg.tol, 0)
     score = torch.cat([s.score_out["score"] for s in shards]).cpu().numpy()
-    _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k)
+    _, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), cfg.k,
+                              tol=cfg.tol)
     got = np.concatenate([s.r[:s.n].cpu().numpy() for s in shards])
     assert np.array_equal(got, r)
     # the default key per shard (every pod's scores, the whole graph) = the oracle's, bit for bit
     from krca.rca import Explain
     ex, sall = Explain(m.row_ptr, m.col), torch.from_numpy(score).cuda()
-    key_ref, _ = oracle.rca_keys(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8))
+    key_ref, _ = oracle.rca_keys(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(n, 8), tol=cfg.tol)
     for g, s in enumerate(shards):
         lo = shard_range(n, G, g)[0]
         s.local_topk_explained(cfg.k, sall, cfg.floor(n, 8), ex, lo)
@@ -644,7 +646,7 @@ def test_rca_explain_kernel_vs_oracle(eng, n):
             got = eng.rca_explain_device(sd, floor, rpd, cold, lo, hi)[:hi - lo].cpu().numpy()
             ref = oracle.c_rca_explain(score, floor, rp, col, lo, hi)
             assert np.array_equal(got, ref), (frac, floor, lo, hi)
-        if frac == 0.02:
+        if frac == 0.02 and n >= 3000:  # the rule fires on some pods, not on all
             assert 0 < int((ref > 0).sum()) < n
 
 
@@ -656,7 +658,7 @@ def test_rca_key_explained_single_device_vs_oracle(eng):
     m = synth.make_graph(n, avg_degree=20, seed=31)
     x = synth.make_metrics(n, 8, 200, window=60, seed=31, roots=m.roots,
                            hop_sets=synth.spread_hops(m, m.roots, seed=31), **synth.SPREAD_SIGMAS).cuda()
-    for cfg in (Config(), Config(tol=1e-9, iters=100, alpha=0.85)):
+    for cfg in (Config(), Config(tol=0.0), Config(tol=1e-9, iters=100, alpha=0.85)):
         sh = DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, 0, n), n, n, 1, cfg)
         step = RcaStep(sh, Comm(), cfg, 0)
         idx, _ = step.run()

@@ -53,7 +53,7 @@ def mesh():
 
 
 def _oracle_top(m, score, cfg):
-    return oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(N, 8), cfg.k)
+    return oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, cfg.alpha, cfg.iters, cfg.floor(N, 8), cfg.k, tol=cfg.tol)
 
 
 def test_rccl_dtype_views(pg):
@@ -73,8 +73,13 @@ def test_rccl_rca_step_uniform(eng, pg, mesh):
     comm = Comm(1, 0, collective=True)
     sh = DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, 0, N), N, N, 1, cfg, pingpong=False)
     assert not sh.fused
-    idx, _ = RcaStep(sh, comm, cfg, 0).run()
-    assert comm.direct_calls == cfg.iters + 1  # init's exchange + one per iteration, the direct path
+    step = RcaStep(sh, comm, cfg, 0)
+    idx, _ = step.run()
+    # init's exchange + one per issued step (the stop rule's count is unknown to the first solve: the
+    # cap), all through the direct entry point
+    assert comm.direct_calls == cfg.iters + 1 and step.last_iters > 0
+    idx2, _ = step.run()  # the second solve issues the count + 1 steps
+    assert comm.direct_calls == cfg.iters + 1 + step.last_iters + 2 and list(idx2) == list(idx)
     score = sh.score_out["score"].cpu().numpy()
     ridx, _, r = _oracle_top(m, score, cfg)
     assert np.array_equal(sh.r[:N].cpu().numpy(), r)
@@ -141,7 +146,7 @@ def test_rccl_graph_capture_with_allgather(eng, pg, mesh):
     """The solve captured into a HIP graph with the RCCL all-gather inside (RcaStep graph=True),
     replayed: the same bits as the eager collective sequence, also after the scores change."""
     m, x0 = mesh
-    cfg = Config()
+    cfg = Config(tol=0.0)  # the graph replays a fixed-iteration solve
     res = {}
     for graph in (False, True):
         x = x0.clone()

@@ -35,7 +35,7 @@ def _csr(edges, n):
 
 # the goldens were captured at the fixed floor 4 with the rounds-2-4 key r * q (they pin the
 # PageRank vector and that key's top-10; the default key is checked against the oracle below)
-GOLDEN_CFG = RANKING.replace(seed_floor=4.0, key="rq")
+GOLDEN_CFG = RANKING.replace(seed_floor=4.0, key="rq", tol=0.0)
 
 
 def _rca_from_scores(eng, rp, col, od, score, cfg=GOLDEN_CFG):
@@ -65,7 +65,7 @@ def test_ranking_pinned_to_networkx(eng, name):
     assert np.array_equal(rfix.astype(np.float64) / 2.0 ** 60, r)  # same fixed point
     # the default key on the same solve: both device paths equal the oracle
     cfg = GOLDEN_CFG.replace(key="explained")
-    ref, _, _ = oracle.rca_rank(rp, col, od, s, cfg.alpha, cfg.iters, cfg.floor(n), cfg.k)
+    ref, _, _ = oracle.rca_rank(rp, col, od, s, cfg.alpha, cfg.iters, cfg.floor(n), cfg.k, tol=cfg.tol)
     assert eng.rank_root_causes(s, rp, col, od, cfg)[0].tolist() == ref.tolist()
     assert _rca_from_scores(eng, rp, col, od, s, cfg)[0] == ref.tolist()
 
@@ -139,7 +139,7 @@ def test_c2_full_rca_step(eng):
     assert np.array_equal(so["score"].cpu().numpy(), ref["score"])
     assert np.allclose(so["z_last"].cpu().numpy(), ref["z_last"], rtol=1e-5, atol=1e-6)
     ridx, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, ref["score"], RANKING.alpha, RANKING.iters,
-                                 RANKING.floor(n, 8), RANKING.k)
+                                 RANKING.floor(n, 8), RANKING.k, tol=RANKING.tol)
     assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
     assert [int(i) for i in idx] == ridx.tolist()
     assert len(set(ridx.tolist()) & set(m.roots.tolist())) >= 8
@@ -166,7 +166,7 @@ def test_c4_full_rca_step_1m_pods(eng):
     assert np.array_equal(step.s.score_out["flags"][sel].cpu().numpy(), ref["flags"])
     assert np.array_equal(score[samp], ref["score"])
     ridx, _, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, RANKING.alpha, RANKING.iters,
-                                 RANKING.floor(n, 8), RANKING.k)
+                                 RANKING.floor(n, 8), RANKING.k, tol=RANKING.tol)
     assert np.array_equal(step.s.r[:n].cpu().numpy(), r)
     assert [int(i) for i in idx] == ridx.tolist()
     del x

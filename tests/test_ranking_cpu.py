@@ -21,7 +21,7 @@ def _recall(seed, spread, key):
     x = synth.make_metrics(10_000, 8, 1440, seed=seed, roots=m.roots, hop_sets=hops, **kw).numpy()
     s = oracle.c_rolling_score(x, RANKING.window)["score"]
     idx, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, s, RANKING.alpha, RANKING.iters,
-                                RANKING.floor(10_000, 8), RANKING.k, key=key)
+                                RANKING.floor(10_000, 8), RANKING.k, key=key, tol=RANKING.tol)
     return len(set(idx.tolist()) & set(m.roots.tolist())) / len(m.roots)
 
 

@@ -98,7 +98,8 @@ def test_sharded_rca_matches_single_process_oracle(world, balanced):
     res.sort()
     m, x = _mesh()
     score = oracle.c_rolling_score(x, 60)["score"]
-    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, 0.5, 12, Config().floor(N, M), 10)
+    ridx, rf, r = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, 0.5, 12, Config().floor(N, M), 10,
+                                  tol=Config().tol)
     if balanced == "replicated":  # every rank holds the whole fixed point
         for _, _, rr, _, _ in res:
             assert np.array_equal(rr, r)

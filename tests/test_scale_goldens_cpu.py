@@ -31,7 +31,8 @@ def test_ranking_definition_is_shared():
     import inspect
     from krca.agents.coordinator import Coordinator
     from krca.stream import StreamingRCA
-    assert (RANKING.alpha, RANKING.seed_floor, RANKING.iters, RANKING.tol, RANKING.k) == (0.5, None, 30, 0.0, 10)
+    assert (RANKING.alpha, RANKING.seed_floor, RANKING.iters, RANKING.tol, RANKING.k, RANKING.key) == (
+        0.5, None, 30, 1e-10, 10, "explained")  # iters: the cap of networkx's L1 stop rule
     # the scale-aware floor: 4 up to ~16k series, the null max of P*M series beyond (C2 4.369, C4 5.286)
     assert RANKING.floor(2000, 8) == 4.003 and RANKING.floor(1000, 8) == 4.0
     assert RANKING.floor(10_000, 8) == 4.369 and RANKING.floor(1_000_000, 8) == 5.286
@@ -116,6 +117,6 @@ def test_coordinator_ranking_equals_bench_ranking_cpu():
     got = [int(r["component"].split("-")[-1]) for r in res["ranked_root_causes"]]
     score = oracle.c_rolling_score(x, RANKING.window)["score"]
     idx, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, score, RANKING.alpha, RANKING.iters,
-                                RANKING.floor(3000, 8), RANKING.k)
+                                RANKING.floor(3000, 8), RANKING.k, tol=RANKING.tol)
     assert got == idx.tolist()
     assert Config().as_dict() == RANKING.as_dict()

@@ -84,9 +84,9 @@ def main():
                 st = RcaStep(sh, Comm(), cfg, 0, explain=ex)
                 st.propagate()
                 if key in ("rq", "explained"):
-                    idx, _ = st.merge(*st.local_candidates())
+                    idx, _ = st.merge(*st.settle(*st.local_candidates()))
                     if key == "explained" and al == RANKING.alpha and fl == round(af, 3):
-                        ref, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, s, al, cfg.iters, fl, 10)
+                        ref, _, _ = oracle.rca_rank(m.row_ptr, m.col, m.outdeg, s, al, cfg.iters, fl, 10, tol=cfg.tol)
                         checks.append(dict(seed=seed, top10_identical=[int(i) for i in idx] == ref.tolist()))
                 elif key == "psq":  # mass received from callers x sqrt(own anomaly) (tests/ranking_ablation.py)
                     rr, qq = sh.r[:a.pods].double(), sh.q[:a.pods].double()
