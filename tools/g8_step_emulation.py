@@ -3,7 +3,7 @@
 PageRank solve from bounding the step (krca.rca.Partition).
 
 bench.py's step on rank g of G: the scoring of its pods (krca_rolling_score) on one HIP stream
-while the previous step's PageRank (init, 30 folded steps, each followed by the exchange, finish,
+while the previous step's PageRank (init, --iters folded steps, each followed by the exchange, finish,
 key, top-k) runs on the other; every PageRank iteration waits for the all-gather, i.e. for the rank
 with the most edges.  Here the rank with the most PageRank work under each partition runs exactly
 that two-stream pipeline on its own shard (its metric rows generated as bench.py generates them),
@@ -99,7 +99,7 @@ def run_rank(a, m, hops, cfg, part, g, M, T):
 def run_replicated(a, m, hops, cfg, part, g, M, T):
     """The replicated-PageRank step on rank g: scoring of its pods, the all-gather of the scores
     (4 B per pod; a device copy into the full vector stands in for it), then the whole mesh's
-    30-iteration solve on this rank alone (no per-iteration collective), pipelined as bench.py's
+    solve on this rank alone (no per-iteration collective), pipelined as bench.py's
     two streams.  ms per step, and the parts alone."""
     import torch
     from krca import native, synth
@@ -183,6 +183,12 @@ class Pipe:
                 sh.score_out = {"score": sv[plo:plo + max(phi - plo, 1)]}
         else:
             self.scor = self.ppr = [DeviceShard(e, x, rp, col, od, a.pods, p_slot, G, cfg) for e in engs]
+            # the default key needs every pod's scores: a device copy of this rank's into a full
+            # vector stands in for the score all-gather RcaStep makes at G > 1
+            self.sfull = [torch.zeros(a.pods + p_slot, dtype=torch.float32, device="cuda") for _ in range(2)]
+        from krca.rca import Explain
+        self.ex = Explain(m.row_ptr, m.col) if cfg.key == "explained" else None
+        self.N, self.plo, self.floor = a.pods, plo, cfg.floor(a.pods, 8)
         # a one-range partition is the replicated solve: one rank's exchange is the buffer swap
         comm = Comm(1, 0) if G == 1 else CopyComm(G, gp, slice_words(p_slot))
         self.steps = [RcaStep(sh, comm, cfg, plo) for sh in self.ppr]
@@ -199,6 +205,14 @@ class Pipe:
         self.info = dict(pagerank_rank=gp, pagerank_pods=phi - plo, pagerank_edges=int(m.row_ptr[phi] - m.row_ptr[plo]),
                          scoring_pods=shi - slo)
 
+    def cand(self, j):
+        """The step's candidates (bench.py: RcaStep.local_candidates)."""
+        if self.ex is None:
+            return self.ppr[j].local_topk(self.cfg.k)
+        if not self.split:
+            self.sfull[j][self.slo:self.shi].copy_(self.scor[j].score_out["score"][:self.shi - self.slo])
+        return self.ppr[j].local_topk_explained(self.cfg.k, self.sfull[j][:self.N], self.floor, self.ex, self.plo)
+
     def enqueue(self, i):
         torch, j = self.torch, i % 2
         if self.roles:
@@ -213,7 +227,7 @@ class Pipe:
                 if self.split:
                     self.sfull[j][self.slo:self.shi].copy_(self.scor[j].score_out["score"][:self.shi - self.slo])
                 self.steps[j].propagate()
-                self.ppr[j].local_topk(self.cfg.k)
+                self.cand(j)
                 self.ev_p[j] = torch.cuda.Event()
                 self.ev_p[j].record()
             return
@@ -226,7 +240,7 @@ class Pipe:
             if self.split:
                 self.sfull[j][self.slo:self.shi].copy_(self.scor[j].score_out["score"][:self.shi - self.slo])
             self.steps[j].propagate()
-            self.ppr[j].local_topk(self.cfg.k)
+            self.cand(j)
 
     def timed(self, n):
         torch = self.torch
@@ -310,6 +324,11 @@ def main():
                     "high-priority solve stream)")
     ap.add_argument("--grid", type=int, default=0, help="KRCA_PPR_GRID for every pipe (0: the occupancy grid)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the environment's)")
+    ap.add_argument("--iters", type=int, default=12,
+                    help="PageRank steps per solve, run as a fixed-iteration solve: the emulated exchange leaves the "
+                         "other ranks' slots empty, so the stop rule cannot decide here.  Default 12 = the rule's "
+                         "11 iterations at C4 (bench.py ppr_iters_run) + the step that finds the convergence "
+                         "(a full step here, an early exit in the real solve: conservative); 30 = rounds 2-4")
     a = ap.parse_args()
     if a.hw_queues:  # before anything starts HIP
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
@@ -318,10 +337,10 @@ def main():
     M, T = 8, 1440
     m = synth.make_graph(a.pods, n_edges=a.edges, seed=0)
     hops = synth.caller_hops(m, m.roots)
-    cfg = RANKING.replace(seed_floor=RANKING.floor(a.pods, M))
+    cfg = RANKING.replace(seed_floor=RANKING.floor(a.pods, M), tol=0.0, iters=a.iters)
     G = a.world
     out = dict(what=f"one rank's pipelined step at G={G} on one GPU (device copy for the all-gather)",
-               pods=a.pods, edges=m.n_edges, steps=a.steps)
+               pods=a.pods, edges=m.n_edges, steps=a.steps, ppr_steps_per_solve=a.iters)
     if a.ppr_grids:
         from krca import native
         part = Partition.uniform(a.pods, G)

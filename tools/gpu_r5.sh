@@ -44,6 +44,7 @@ for s in "$@"; do
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
     corr100k) prof corr100k 400 tools/prof_kernels.py corr --pods 100000 --reps 3 ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 ;;
+    corrdbg_*) v=${s#corrdbg_}; export KRCA_CORR_DEBUG=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${P:-1000000} --reps 1 --tau ${v##*_}; unset KRCA_CORR_DEBUG ;;
     c5) step c5 400 python3 tools/bench_stream.py ;;
     g8) step g8 600 python3 -u tools/g8_step_emulation.py --decoupled ;;
     *) echo "unknown step $s"; exit 2 ;;
