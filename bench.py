@@ -35,7 +35,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def parse(argv=None):
-    from krca.rca import RANKING
+    from krca.rca import EDGE_SLACK, RANKING
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -70,7 +70,7 @@ def parse(argv=None):
                          "every rank (scores all-gathered, no collective inside the solve); auto = the sharded "
                          "solve (balanced at G >= 4, uniform below: measured, DESIGN.md §5) unless the all-gather "
                          "measured at startup costs more per solve than the replicated step's measured margin")
-    ap.add_argument("--ppr-edge-slack", type=float, default=1.5,
+    ap.add_argument("--ppr-edge-slack", type=float, default=EDGE_SLACK,
                     help="Partition.balanced's in-edge cap per rank, in multiples of E / G")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run steps back to back on one stream (default: two streams, step i+1's scoring "
@@ -530,10 +530,7 @@ def main():
     t0 = time.time()
     mesh = synth.make_graph(args.pods, n_edges=args.edges, seed=args.seed)
     hops = synth.caller_hops(mesh, mesh.roots)
-    # contiguous ranges of ceil(N / G) pods.  (Partition.balanced caps the in-edges per rank -- the
-    # mesh's hub services sit at low ids -- but measured no gain at G = 8: the PageRank iteration's
-    # fixed cost dominates a small shard's step, and the capped ranks score more pods;
-    # tools/g8_step_emulation.py)
+    # the scoring: contiguous ranges of ceil(N / G) pods (equal HBM streams per rank)
     part = Partition.uniform(args.pods, world)
     lo, hi, n_max = part.range(rank)
     # the PageRank rows: at G >= 4 by default Partition.balanced ranges, so that the hub services'

@@ -1778,12 +1778,17 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.dn = ws.dn;
   ta.z32 = z32;
   ta.T = d.T;
-  const bool fork = sw.side != st;
+  const bool side_ok = sw.side != st;
   const int64_t SB = sb_batch();
+  const int side_mode = krca::tuning().corr_side;
   for (int64_t b = 0, s0 = 0; s0 < n_mine; ++b, s0 += SB) {
+    // KRCA_CORR_SIDE: 0 every batch's re-score on the side stream (beside the next batch's tiles), 1
+    // each on st after its batch, 2 on st except the last batch's (beside the merge chain)
+    const bool last = s0 + SB >= n_mine;
+    const bool fork = side_ok && (side_mode == 0 || (side_mode == 2 && last));
     const int l = (int)(b & 1) % ws.nlist;
     if (b >= 2 || (b >= 1 && ws.nlist == 1)) {  // list l was drained by the re-score of batch b - nlist
-      if (fork) KRCA_HIP(hipStreamWaitEvent(st, sw.ev[2 + l], 0));
+      if (side_ok) KRCA_HIP(hipStreamWaitEvent(st, sw.ev[2 + l], 0));
       KRCA_HIP(hipMemsetAsync(ws.amb_n + l, 0, sizeof(unsigned long long), st));
     }
     ta.amb = ws.amb[l];
@@ -1802,8 +1807,8 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
       KRCA_HIP(hipStreamWaitEvent(sw.side, sw.ev[l], 0));
       sw.forked = true;
     }
-    if (int rc = launch_rescore(z32, d, ws, l, count, sw.side)) return rc;
-    if (fork) KRCA_HIP(hipEventRecord(sw.ev[2 + l], sw.side));
+    if (int rc = launch_rescore(z32, d, ws, l, count, fork ? sw.side : st)) return rc;
+    if (side_ok) KRCA_HIP(hipEventRecord(sw.ev[2 + l], fork ? sw.side : st));
   }
   return KRCA_OK;
 }

@@ -107,6 +107,9 @@ struct Tuning {
   int ppr_xcd;      // KRCA_PPR_XCD: each XCD's workgroups take one contiguous eighth of the plan entries
   int log_fused;    // KRCA_LOG_FUSED: krca_log_scan walks the DFA inside the line-index pass (0 = index, then log_dfa)
   int corr_rs_group;  // KRCA_CORR_RS_GROUP: the ambiguous pairs re-scored grouped by row pod (row in LDS; 0 = per pair)
+  int corr_side;      // KRCA_CORR_SIDE: where the exact-count re-scores run: 0 every batch's on a side stream beside
+                      // the next batch's tiles, 1 each after its batch on the caller's stream, 2 those after their
+                      // batch except the last (beside the merge chain)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

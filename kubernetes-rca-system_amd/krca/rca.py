@@ -62,11 +62,10 @@ def shard_range(N, world, rank):
 
 
 # Partition.balanced: a rank may hold up to EDGE_SLACK x the mean in-edges per rank before its
-# edges, not its pods, bound it.  A rank's step is its scoring (pods) overlapped with the PageRank
-# solve, whose iterations all wait for the rank with the most edges; the scoring is the larger part
-# (C4: 7.1 ms of scoring against ~1 ms of PageRank on one GPU), so the pods stay balanced and the
-# edges are only capped
-EDGE_SLACK = 2.0
+# edges, not its pods, bound it.  1.5 is the measured best of a sweep of the G = 8 split step
+# (1.25 / 1.5 / 2.0 / 3.0: DESIGN.md §5); bench.py's --ppr-edge-slack and StreamingRCA's
+# partition="balanced" use this one value
+EDGE_SLACK = 1.5
 
 
 class Partition:

@@ -178,17 +178,21 @@ def test_corr_batches_and_full_lists_identical(eng):
     ref = eng.corr_topk(x, k=k, tau=TAU)
     lib = eng.lib
     try:
-        for batch, per_tile, group in ((4, -1, 1), (0, 0, 1), (3, 8, 1), (0, -1, 0), (4, -1, 0)):
+        # (KRCA_CORR_SIDE: the re-scores beside the next batch, after each batch, or after each but the last)
+        for batch, per_tile, group, side in ((4, -1, 1, 0), (0, 0, 1, 0), (3, 8, 1, 0), (0, -1, 0, 0), (4, -1, 0, 0),
+                                             (4, -1, 1, 1), (4, -1, 1, 2), (3, 8, 1, 2)):
             assert lib.krca_tune_set(b"KRCA_CORR_BATCH", batch) == 0
             assert lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", per_tile) == 0
             assert lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", group) == 0
+            assert lib.krca_tune_set(b"KRCA_CORR_SIDE", side) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
             for key in ref:
-                assert np.array_equal(got[key], ref[key]), (batch, per_tile, group, key)
+                assert np.array_equal(got[key], ref[key]), (batch, per_tile, group, side, key)
     finally:
         lib.krca_tune_set(b"KRCA_CORR_BATCH", 0)
         lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", -1)
         lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", 1)
+        lib.krca_tune_set(b"KRCA_CORR_SIDE", 0)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
     _, _, bad = device_check(ref, z, [rows], k)

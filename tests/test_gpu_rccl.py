@@ -142,6 +142,36 @@ def test_rccl_stream_window(eng, pg, mesh):
         assert [int(i) for i in out["top"][0]] == top.tolist(), t
 
 
+@pytest.mark.parametrize("direct", [False, True])
+def test_rccl_graph_capture_plain_allgather(pg, direct):
+    """One all-gather captured into a HIP graph and replayed after its input changed (the public
+    all_gather_into_tensor, or the process group's _allgather_base as Comm.exchange calls it)."""
+    import torch.distributed as dist
+    inp = torch.arange(1000, dtype=torch.int64, device="cuda")
+    out = torch.zeros(1000, dtype=torch.int64, device="cuda")
+    pgd = dist.distributed_c10d._get_default_group()
+    opts = dist.distributed_c10d.AllgatherOptions()
+
+    def gather():
+        if direct:
+            pgd._allgather_base(out, inp, opts).wait()
+        else:
+            dist.all_gather_into_tensor(out, inp)
+    gather()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=side):
+        gather()
+    torch.cuda.current_stream().wait_stream(side)
+    inp.add_(7)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, inp), (out[:5].tolist(), inp[:5].tolist())
+
+
 def test_rccl_graph_capture_with_allgather(eng, pg, mesh):
     """The solve captured into a HIP graph with the RCCL all-gather inside (RcaStep graph=True),
     replayed: the same bits as the eager collective sequence, also after the scores change."""

@@ -34,6 +34,7 @@ prof() {  # prof NAME SECONDS ARGS... (rocprofv3 kernel-trace stats of python3 A
 for s in "$@"; do
   case $s in
     tests) step tests 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread ;;
+    testsall_*) step $s 900 python3 -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread -k "${s#testsall_}" ;;
     tests_*) step $s 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "${s#tests_}" ;;
     bench) step bench 400 python3 bench.py ;;
     bench_trace) prof bench_trace 500 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify ;;
@@ -45,6 +46,7 @@ for s in "$@"; do
     corr100k) prof corr100k 400 tools/prof_kernels.py corr --pods 100000 --reps 3 ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 ;;
     corrdbg_*) v=${s#corrdbg_}; export KRCA_CORR_DEBUG=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${P:-1000000} --reps 1 --tau ${v##*_}; unset KRCA_CORR_DEBUG ;;
+    corrside_*) v=${s#corrside_}; export KRCA_CORR_SIDE=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 3 --tau 0.5; unset KRCA_CORR_SIDE ;;
     c5) step c5 400 python3 tools/bench_stream.py ;;
     g8) step g8 600 python3 -u tools/g8_step_emulation.py --decoupled ;;
     *) echo "unknown step $s"; exit 2 ;;
