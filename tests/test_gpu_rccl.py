@@ -142,10 +142,12 @@ def test_rccl_stream_window(eng, pg, mesh):
         assert [int(i) for i in out["top"][0]] == top.tolist(), t
 
 
+@pytest.mark.parametrize("producer", [False, True])
 @pytest.mark.parametrize("direct", [False, True])
-def test_rccl_graph_capture_plain_allgather(pg, direct):
+def test_rccl_graph_capture_plain_allgather(pg, direct, producer):
     """One all-gather captured into a HIP graph and replayed after its input changed (the public
-    all_gather_into_tensor, or the process group's _allgather_base as Comm.exchange calls it)."""
+    all_gather_into_tensor, or the process group's _allgather_base as Comm.exchange calls it);
+    producer: a kernel that writes the input is captured before it (the graph must order the two)."""
     import torch.distributed as dist
     inp = torch.arange(1000, dtype=torch.int64, device="cuda")
     out = torch.zeros(1000, dtype=torch.int64, device="cuda")
@@ -153,10 +155,14 @@ def test_rccl_graph_capture_plain_allgather(pg, direct):
     opts = dist.distributed_c10d.AllgatherOptions()
 
     def gather():
+        if producer:
+            inp.mul_(3).add_(1)
         if direct:
             pgd._allgather_base(out, inp, opts).wait()
         else:
             dist.all_gather_into_tensor(out, inp)
+        if producer:
+            out.add_(5)  # a consumer after it
     gather()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -167,9 +173,11 @@ def test_rccl_graph_capture_plain_allgather(pg, direct):
     torch.cuda.current_stream().wait_stream(side)
     inp.add_(7)
     out.zero_()
+    want = inp * 3 + 1 if producer else inp.clone()
     g.replay()
     torch.cuda.synchronize()
-    assert torch.equal(out, inp), (out[:5].tolist(), inp[:5].tolist())
+    got = out - 5 if producer else out
+    assert torch.equal(got, want), (got[:5].tolist(), want[:5].tolist())
 
 
 def test_rccl_graph_capture_with_allgather(eng, pg, mesh):

@@ -24,6 +24,8 @@ step() {  # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
   timeout -k 10 $secs "$@" > $O/$name.log 2>&1
   local rc=$?; echo "$name EXIT=$rc" >> $O/status
+  # testsall_*: failing tests (pytest rc 1) do not stop the call; a timeout, crash or fault does
+  if [ $rc -eq 1 ] && [ "${name#testsall_}" != "$name" ]; then tail -5 $O/$name.log; return 0; fi
   [ $rc -eq 0 ] || { echo "stop after $name"; tail -30 $O/$name.log; exit $rc; }
   tail -3 $O/$name.log
 }
