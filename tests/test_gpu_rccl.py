@@ -201,3 +201,35 @@ def test_rccl_graph_capture_with_allgather(eng, pg, mesh):
     for (ia, ra), (ib, rb) in zip(res[False], res[True]):
         assert ia == ib and np.array_equal(ra, rb)
     assert not np.array_equal(res[True][0][1], res[True][1][1])
+
+
+class _CopyExchange:
+    """The exchange as a device copy (what a one-rank all-gather does), for the capture diagnostic."""
+    world, rank, collective = 1, 0, True
+
+    def exchange(self, shard):
+        shard.w_all.copy_(shard.send)
+
+    def all_gather(self, out, inp):
+        out.copy_(inp)
+
+
+@pytest.mark.parametrize("how", ["copy", "public", "direct"])
+def test_rccl_graph_capture_exchange_diagnostic(eng, pg, mesh, how):
+    """The copy-exchange solve captured and replayed, with the exchange a device copy, the public
+    all-gather or the direct one: ranks equal to the eager solve after the replay."""
+    m, x = mesh
+    cfg = Config(tol=0.0)
+    sh_e = DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, 0, N), N, N, 1, cfg, pingpong=False)
+    RcaStep(sh_e, Comm(1, 0, collective=True), cfg, 0).run()
+    ref = sh_e.r[:N].cpu().numpy()
+    comm = _CopyExchange() if how == "copy" else Comm(1, 0, collective=True)
+    if how == "public":
+        comm._direct = False
+    sh = DeviceShard(eng, x, *shard_graph(m.row_ptr, m.col, m.outdeg, 0, N), N, N, 1, cfg, pingpong=False)
+    step = RcaStep(sh, comm, cfg, 0, graph=True)
+    step.run()
+    torch.cuda.synchronize()
+    got = sh.r[:N].cpu().numpy()
+    assert torch.equal(sh.w_all, sh.send), how
+    assert np.array_equal(got, ref), (how, int((got != ref).sum()))
