@@ -56,6 +56,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-warmup", type=int, default=5)  # 5 warm-up + >= 20 timed runs
     ap.add_argument("--cpu-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full-mesh", action="store_true",
+                    help="also time the C restatement's scoring once over EVERY pod of this rank (chunks copied "
+                         "to the host outside the timing; ~5 s of CPU work at C4), beside the scaled sample")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-corr", action="store_true", help="skip the correlation leg (C4's second half)")
@@ -356,6 +359,17 @@ def cpu_baseline(args, cfg, mesh, shard, x, n_loc):
         "ms_per_step": med * 1e3, "ms_per_step_p95": float(np.percentile(t_step, 95)) * 1e3,
         "cpu_model": cpu_model(),
     }
+    if args.cpu_full_mesh:  # one pass of the scoring over the whole mesh, to check the sample's scaling
+        chunk, t_full = 50_000, 0.0
+        for a in range(0, n_loc, chunk):
+            xc = x[:, a:min(a + chunk, n_loc), :].cpu().numpy()
+            t1 = time.perf_counter()
+            oracle.c_rolling_score(xc, args.window)
+            t_full += time.perf_counter() - t1
+            del xc
+        out["full_mesh_scoring"] = {
+            "pods": int(n_loc), "seconds": t_full, "scaled_sample_seconds": float(np.median(t_sc)) * (n_loc / ps),
+            "note": f"oracle.c_rolling_score over all {n_loc} pods in chunks of {chunk} (host copies untimed), once"}
     ref_t = os.path.join(ROOT, "tests", "golden", "ref_cpu_timings.json")
     if os.path.exists(ref_t):  # the reference's own Python, timed in the build container
         rt = json.load(open(ref_t))

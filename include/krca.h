@@ -46,7 +46,7 @@ int krca_device_count(int* n_host);
 
 /* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID, KRCA_PPR_DICT,
  * KRCA_LOG_IMPL, KRCA_GROUP_IMPL, KRCA_CORR_DEBUG, KRCA_CORR_RS_GRID, KRCA_CORR_BATCH, KRCA_CORR_AMB_TILE,
- * KRCA_PPR_FUSE, KRCA_PPR_NT, KRCA_PPR_XCD, KRCA_LOG_FUSED, KRCA_CORR_RS_GROUP, KRCA_CORR_SIDE.  Initialised once from the environment variables
+ * KRCA_PPR_FUSE, KRCA_PPR_NT, KRCA_PPR_XCD, KRCA_LOG_FUSED, KRCA_CORR_RS_GROUP, KRCA_CORR_SIDE, KRCA_CORR_RS_Q16.  Initialised once from the environment variables
  * of the same names when the library loads; launchers never call getenv.  Process-global, not
  * thread-safe (set them before launching work).  Unknown names: KRCA_EINVAL. */
 int krca_tune_set(const char* name, int32_t value);
@@ -169,7 +169,11 @@ int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspa
  * out_idx/out_val [P*k]; cert [P].  k <= krca_corr_max_k(), 2 <= P <= 2^22.  krca_corr_topk
  * synchronises the stream once (it reads how many candidate buffers overflowed to decide on the
  * second pass).  The series must be finite: the certificates and the exact counts are proofs over
- * finite rows (a NaN row's products compare false everywhere; its results are unspecified). */
+ * finite rows (a NaN row's products compare false everywhere; its results are unspecified).
+ * Workspace size: cand holds the per-pod candidate buffers (8 KiB per pod), the threshold
+ * sample's lists, the two ambiguous-pair lists of a main-pass batch (capped per batch), their
+ * by-pod copy and the re-score's int16 partner rows (2 bytes per step per pod): at T = 1440,
+ * k = 10 about 0.15 GB at 10k pods, 2.1 GB at 100k, 15.1 GB at 1M. */
 int64_t krca_corr_pad_rows(int64_t P);
 int32_t krca_corr_pad_steps(int32_t T);
 int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k);

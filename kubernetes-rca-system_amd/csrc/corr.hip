@@ -235,6 +235,39 @@ __device__ __forceinline__ double dot16_f64_pf(const float* za_lds, const float*
   return acc;
 }
 
+// za . zq_b in float64 over 16 lanes (za in LDS, Tq floats, zero past T; zq_b an int16 row of Tq,
+// Tq % 8 == 0): 16-byte loads of 8 steps each, every product exact in float64
+__device__ __forceinline__ double dot16_q16(const float* za_lds, const int16_t* qb, int Tq, int sub) {
+  const float4* va = reinterpret_cast<const float4*>(za_lds);
+  const uint4* vb = reinterpret_cast<const uint4*>(qb);
+  const int n8 = Tq / 8;
+  double acc = 0.0;
+  for (int c0 = sub; c0 < n8; c0 += 16 * 4) {
+    uint4 y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 16 * j;
+      y[j] = vb[c < n8 ? c : sub];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 16 * j;
+      if (c < n8) {
+        const float4 x0 = va[2 * c], x1 = va[2 * c + 1];
+        const uint32_t w[4] = {y[j].x, y[j].y, y[j].z, y[j].w};
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          acc += (double)xs[2 * h] * (double)(int16_t)(w[h] & 0xffffu) +
+                 (double)xs[2 * h + 1] * (double)(int16_t)(w[h] >> 16);
+        }
+      }
+    }
+  }
+  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  return acc;
+}
+
 // Tile kernels.  Rows: 256-pod blocks of zA; columns: TC-pod blocks of zh (TC = 256 in every pass):
 // 8 waves (2 row halves x 4 column quarters), each a 128 x 64 tile = 8 x 4 MFMA 16x16 blocks, K
 // steps of 64 through a double-buffered LDS stage (130 KB with the sample pass's parking area: one
@@ -988,19 +1021,53 @@ __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, 
 //   |h_a.d_b| + |d_a.h_b| + |d_a.d_b| + acc <= dn_a + dn_b + 3 dn_a dn_b + acc
 // (||h|| <= 1 + dn, unit-norm rows, acc = the fp32 accumulation terms of eps), typically ~60 % of the
 // worst-case eps: most listed pairs are decided from their screening value without reading a row.
+//
+// With zq (KRCA_CORR_RS_Q16) the same pass writes the re-score's int16 partner rows: step
+// qs[p] = max|z32[p]| / 32767, zq[p][t] = rint(z32[p][t] / qs[p]) (zero past T up to Tq, a multiple
+// of 8), qn[p] = || z32[p] - qs[p] zq[p] || and nrm[p] = || z32[p] || (float64, rounded up).  A
+// pair's za . (qs_b zq_b) then differs from za . zb by at most nrm_a qn_b (~4e-5 at T = 1440).
 __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32, const uint16_t* __restrict__ zh,
-                                                  int64_t P, int T, int Tp, float* __restrict__ dn) {
+                                                  int64_t P, int T, int Tp, float* __restrict__ dn,
+                                                  int16_t* __restrict__ zq, int Tq, float* __restrict__ qs,
+                                                  float* __restrict__ qn, float* __restrict__ nrm) {
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   if (p >= P) return;
-  double s2 = 0.0;
+  double s2 = 0.0, n2 = 0.0;
+  float mx = 0.f;
   for (int t = lane; t < T; t += 64) {
     const float z = z32[p * T + t];
     const double d = (double)z - (double)(float)__builtin_bit_cast(_Float16, zh[p * Tp + t]);
     s2 += d * d;
+    n2 += (double)z * (double)z;
+    mx = fmaxf(mx, fabsf(z));
   }
-  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off, 64);
+  for (int off = 32; off > 0; off >>= 1) {
+    s2 += __shfl_xor(s2, off, 64);
+    n2 += __shfl_xor(n2, off, 64);
+    mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+  }
   if (lane == 0) dn[p] = (float)(sqrt(s2) * (1.0 + 1e-6)) + 1e-12f;
+  if (!zq) return;
+  const float s = mx / 32767.f;  // 0 for a flat row: every q is 0 and so is the error
+  double e2 = 0.0;
+  for (int t = lane; t < Tq; t += 64) {
+    int q = 0;
+    if (t < T && s > 0.f) {
+      const float z = z32[p * T + t];
+      q = (int)rint((double)z / (double)s);
+      q = q > 32767 ? 32767 : q < -32767 ? -32767 : q;
+      const double e = (double)z - (double)q * (double)s;
+      e2 += e * e;
+    }
+    zq[p * Tq + t] = (int16_t)q;
+  }
+  for (int off = 32; off > 0; off >>= 1) e2 += __shfl_xor(e2, off, 64);
+  if (lane == 0) {
+    qs[p] = s;
+    qn[p] = (float)(sqrt(e2) * (1.0 + 1e-6)) + 1e-12f;
+    nrm[p] = (float)(sqrt(n2) * (1.0 + 1e-6)) + 1e-12f;
+  }
 }
 
 // the ambiguous pairs in list order, 16 lanes each: decided from the screening value and the two
@@ -1141,24 +1208,30 @@ constexpr int RS_WAVES = TPB / 64;
 __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* __restrict__ goff, const int2* __restrict__ gs,
                                                                 int64_t P, const float* __restrict__ z32,
                                                                 const float* __restrict__ dn, int T, float tau,
-                                                                float acc_err, int32_t* __restrict__ count) {
+                                                                float acc_err, int32_t* __restrict__ count,
+                                                                const int16_t* __restrict__ zq, int Tq,
+                                                                const float* __restrict__ qs, const float* __restrict__ qn,
+                                                                const float* __restrict__ nrm) {
   extern __shared__ float4 rs_lds[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane & 15, grp = lane >> 4;
   const int T4 = (T + 3) / 4;
-  float* ra = reinterpret_cast<float*>(rs_lds + (size_t)wv * T4);
+  const int L4 = zq ? Tq / 4 : T4;  // floats per wave slot / 4 (the int16 dot reads zeros past T)
+  float* ra = reinterpret_cast<float*>(rs_lds + (size_t)wv * L4);
   for (int64_t a = (int64_t)blockIdx.x * RS_WAVES + wv; a < P; a += (int64_t)gridDim.x * RS_WAVES) {
     const int32_t e0 = goff[a], e1 = goff[a + 1];
     if (e0 == e1) continue;  // wave-uniform
     const float* za = z32 + a * T;
     if ((T & 3) == 0) {
-      for (int t = lane; t < T4; t += 64) rs_lds[(size_t)wv * T4 + t] = reinterpret_cast<const float4*>(za)[t];
+      for (int t = lane; t < T4; t += 64) rs_lds[(size_t)wv * L4 + t] = reinterpret_cast<const float4*>(za)[t];
     } else {
       for (int t = lane; t < T; t += 64) ra[t] = za[t];
     }
+    for (int t = T + lane; t < 4 * L4; t += 64) ra[t] = 0.f;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const double sa = (double)dn[a];
+    const double na = zq ? (double)nrm[a] : 0.0;
     int hits = 0;
     for (int32_t q = e0 + grp; q < e1; q += 4) {
       const int2 e = gs[q];
@@ -1172,7 +1245,16 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* _
       } else if (v <= (double)tau - band) {
         hit = 0;
       } else {
-        hit = fabs(dot16_f64_pf(ra, z32 + b * T, T, sub)) > (double)tau;
+        // int16 partner row first: |za . qs_b zq_b - za . zb| <= nrm_a qn_b, so outside that band
+        // (+ 1e-9 for the float64 sums) the exact float64 product is on the same side of tau; the
+        // fp32 partner row only inside it (uniform over the 16-lane group)
+        int dec = -1;
+        if (zq) {
+          const double vq = fabs(dot16_q16(ra, zq + b * Tq, Tq, sub) * (double)qs[b]);
+          const double bq = na * (double)qn[b] + 1e-9;
+          dec = vq > (double)tau + bq ? 1 : vq <= (double)tau - bq ? 0 : -1;
+        }
+        hit = dec >= 0 ? dec : fabs(dot16_f64_pf(ra, z32 + b * T, T, sub)) > (double)tau;
       }
       if (sub == 0 && hit) {
         ++hits;
@@ -1536,6 +1618,9 @@ struct CorrWs {  // views into a caller's candidate workspace
   int64_t amb_cap;
   int nlist;            // lists in use (2 when the main pass runs in more than one batch)
   float* dn;            // [P] fp16 rounding-error norm of each row
+  int16_t* zq;          // [P][Tq] int16 partner rows of the grouped re-score (KRCA_CORR_RS_Q16), else null
+  float *qs, *qn, *nrm; // [P] their step, error norm, the fp32 row's norm
+  int Tq;               // T rounded up to 8
   unsigned long long* amb_n;  // [2]: the lists' fill
   int32_t *gcnt, *goff, *gcur, *gsum;  // grouped re-score: entries per row pod, offsets [P + 1], cursors, scan blocks
   int2* gs;                            // [amb_cap] a list's entries grouped by row pod
@@ -1552,7 +1637,7 @@ inline int64_t n_supertiles(int64_t nb2) {
 }
 
 // layout in 4-byte words; sharded adds the local buffers and the exchange counters
-int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, CorrWs* ws) {
+int64_t ws_layout(int64_t P, int T, int Tp, int KC, int64_t n_loc, int G, char* base, CorrWs* ws) {
   int64_t o = 0;
   auto take = [&](int64_t words) {
     char* ptr = base ? base + 4 * o : nullptr;
@@ -1578,6 +1663,13 @@ int64_t ws_layout(int64_t P, int Tp, int KC, int64_t n_loc, int G, char* base, C
     w.ambv[l] = l < w.nlist ? reinterpret_cast<float*>(take(w.amb_cap)) : nullptr;
   }
   w.dn = reinterpret_cast<float*>(take(P));
+  w.Tq = (int)krca::ceil_div(T, 8) * 8;
+  {  // reserved whatever the knobs say (a size query and the call must agree); used when both are on
+    w.zq = reinterpret_cast<int16_t*>(take(P * w.Tq / 2));
+    w.qs = reinterpret_cast<float*>(take(P));
+    w.qn = reinterpret_cast<float*>(take(P));
+    w.nrm = reinterpret_cast<float*>(take(P));
+  }
   w.amb_n = reinterpret_cast<unsigned long long*>(take(4));
   w.gcnt = reinterpret_cast<int32_t*>(take(P));
   w.goff = reinterpret_cast<int32_t*>(take(P + 1));
@@ -1676,11 +1768,15 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   return KRCA_OK;
 }
 
+// the grouped re-score reads int16 partner rows (written by corr_dnorm)
+inline bool q16_rows() { return krca::tuning().corr_rs_q16 && krca::tuning().corr_rs_group; }
+
 // exact |r| > tau counts of the ambiguous pairs in list l (float64 from z32), added to count
 int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int32_t* count, hipStream_t st) {
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   const unsigned grid = (unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7);
-  const size_t lds = (size_t)RS_WAVES * ((d.T + 3) / 4) * sizeof(float4);
+  const int16_t* zq = q16_rows() ? ws.zq : nullptr;
+  const size_t lds = (size_t)RS_WAVES * (zq ? ws.Tq / 4 : (d.T + 3) / 4) * sizeof(float4);
   // grouped by row pod (above); its offsets are int32 (a list of up to 2^31 - 1 entries)
   if (krca::tuning().corr_rs_group && lds <= 64 * 1024 && d.P > 0 && ws.amb_cap < (int64_t(1) << 31)) {
     const int64_t nb = krca::ceil_div(d.P, GSCAN);
@@ -1700,7 +1796,8 @@ int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int
     KRCA_LAUNCH_CHECK();
     const unsigned gg = (unsigned)std::min<int64_t>(krca::ceil_div(d.P, RS_WAVES), 2048);
     hipLaunchKernelGGL(corr_amb_rescore_grouped, dim3(gg), dim3(TPB), lds, st, (const int32_t*)ws.goff,
-                       (const int2*)ws.gs, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count);
+                       (const int2*)ws.gs, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count,
+                       zq, ws.Tq, (const float*)ws.qs, (const float*)ws.qn, (const float*)ws.nrm);
     KRCA_LAUNCH_CHECK();
     return KRCA_OK;
   }
@@ -1752,7 +1849,7 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   if (n_mine == 0) return KRCA_OK;
   const Shard sh{0, G, g, 0};
   hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
-                     d.Tp, ws.dn);
+                     d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
   KRCA_LAUNCH_CHECK();
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   // screening counts: certain above tau + eps, decided in the tile by the pair's own bound or
@@ -1878,7 +1975,7 @@ template <int KC>
 int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, int32_t* count, int32_t* out_idx,
                float* out_val, float* cert, hipStream_t st) {
   CorrWs ws;
-  const int64_t head = ws_layout(d.P, d.Tp, KC, d.P, 0, cand, &ws);
+  const int64_t head = ws_layout(d.P, d.T, d.Tp, KC, d.P, 0, cand, &ws);
   float* phi = reinterpret_cast<float*>(cand + 4 * head);  // one more [P] after the layout
   const int dbg = debug_mode();
   // every launch below goes to st's device (the side stream is that device's)
@@ -1905,7 +2002,7 @@ int64_t krca_corr_pad_rows(int64_t P) { return krca::ceil_div(P, TB) * TB; }
 int32_t krca_corr_pad_steps(int32_t T) { return (int32_t)krca::ceil_div(T, BK) * BK; }
 // single-device candidate workspace (4-byte words): see ws_layout, then phi [P]
 int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k) {
-  return ws_layout(P, krca_corr_pad_steps(T), kc_for(k), P, 0, nullptr, nullptr) + krca::ceil_div(P, 4) * 4;
+  return ws_layout(P, T, krca_corr_pad_steps(T), kc_for(k), P, 0, nullptr, nullptr) + krca::ceil_div(P, 4) * 4;
 }
 int32_t krca_corr_max_k(void) { return KMAX; }
 float krca_corr_eps(int32_t T) {
@@ -1950,7 +2047,7 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
 // (every G-th super-tile; candidates of ANY pod) -> all-reduce count and raw_cnt -> pack_sizes /
 // pack -> all-to-all by owner -> unpack -> shard_merge (own pods; may run the rectangle pass).
 int64_t krca_corr_shard_ws_size(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G) {
-  return ws_layout(P, krca_corr_pad_steps(T), kc_for(k), n_loc, G, nullptr, nullptr);
+  return ws_layout(P, T, krca_corr_pad_steps(T), kc_for(k), n_loc, G, nullptr, nullptr);
 }
 
 #define KRCA_CORR_SHARD_ARGS(name)                                                                        \
@@ -1958,7 +2055,7 @@ int64_t krca_corr_shard_ws_size(int64_t P, int32_t T, int32_t k, int64_t n_loc, 
                  name ": bad sizes");                                                                      \
   KRCA_CHECK_ARG(n_loc >= 0 && G >= 1 && ws, name ": bad shard arguments");                                \
   CorrWs w;                                                                                                \
-  ws_layout(P, krca_corr_pad_steps(T), kc_for(k), n_loc, G, reinterpret_cast<char*>(ws), &w);             \
+  ws_layout(P, T, krca_corr_pad_steps(T), kc_for(k), n_loc, G, reinterpret_cast<char*>(ws), &w);             \
   hipStream_t st = krca::as_stream(stream);
 
 int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, int64_t lo, int64_t n_loc, int32_t G,

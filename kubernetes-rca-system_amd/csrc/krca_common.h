@@ -110,6 +110,8 @@ struct Tuning {
   int corr_side;      // KRCA_CORR_SIDE: where the exact-count re-scores run: 0 every batch's on a side stream beside
                       // the next batch's tiles, 1 each after its batch on the caller's stream, 2 those after their
                       // batch except the last (beside the merge chain)
+  int corr_rs_q16;    // KRCA_CORR_RS_Q16: the grouped re-score reads int16 partner rows (row max / 32767 steps)
+                      // and re-reads the fp32 row only within their error bound of tau (0 = fp32 rows)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

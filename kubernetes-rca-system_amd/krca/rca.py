@@ -285,7 +285,13 @@ class Comm:
         """(group, AllgatherOptions) when the backend is RCCL / NCCL and the group has the direct
         entry point, else False (gloo: the list form of all_gather_flat).  AllgatherOptions lives
         in torch.distributed.distributed_c10d (torch 2.10 does not re-export it from
-        torch.distributed: ADVICE r4)."""
+        torch.distributed: ADVICE r4).
+
+        asyncOp = False, as the public all_gather_into_tensor(async_op=False) sets it: the collective
+        is enqueued on the caller's stream.  The options' default (True) runs it on the process
+        group's internal stream behind an event fork and join; captured into a HIP graph that way,
+        the solve replayed correctly once and then diverged (R5j: the second replay's keys differed
+        from the eager solve's; tests/test_gpu_rccl.py)."""
         import torch.distributed as dist
         if dist.get_backend(self.group) == "gloo":
             return False
@@ -293,7 +299,10 @@ class Comm:
         opts_t = getattr(dist.distributed_c10d, "AllgatherOptions", None)
         if opts_t is None or not hasattr(pg, "_allgather_base"):
             return False
-        return pg, opts_t()
+        opts = opts_t()
+        if hasattr(opts, "asyncOp"):
+            opts.asyncOp = False
+        return pg, opts
 
     def all_gather(self, out, inp):
         if not self.collective:

@@ -2,7 +2,8 @@
 RCCL path calls the group's _allgather_base(w_all, send, AllgatherOptions) directly -- the options
 class comes from torch.distributed.distributed_c10d, where torch 2.10 keeps it -- and falls back
 to the public all-gather for good when the first direct call raises; later failures propagate.
-A one-rank Comm(collective=True) runs the collective too (the world-size-1 RCCL tests)."""
+A one-rank Comm(collective=True) runs the collective too (the world-size-1 RCCL tests).  The
+options carry asyncOp = False (the collective on the caller's stream, as the public wrapper's)."""
 import types
 
 import pytest
@@ -22,7 +23,7 @@ class FakePG:
         self.calls, self.fail = [], fail
 
     def _allgather_base(self, out, inp, opts):
-        self.calls.append((out, inp, type(opts).__name__))
+        self.calls.append((out, inp, type(opts).__name__, getattr(opts, "asyncOp", None)))
         if self.fail:
             self.fail -= 1
             raise RuntimeError("no such collective")
@@ -57,8 +58,9 @@ def test_exchange_calls_allgather_base(monkeypatch):
     for _ in range(3):
         c.exchange(sh)
     assert len(pg.calls) == 3 and c.direct_calls == 3 and not gathered
-    out, inp, opts = pg.calls[0]
+    out, inp, opts, async_op = pg.calls[0]
     assert out is sh.w_all and inp is sh.send and opts == "AllgatherOptions"
+    assert async_op is False  # enqueued on the caller's stream (HIP-graph capture safe)
     assert sh.w_all.tolist() == list(range(6)) * 2
 
 

@@ -171,7 +171,8 @@ def test_corr_odd_sample_self_products(eng):
 def test_corr_batches_and_full_lists_identical(eng):
     """The main pass in many batches (KRCA_CORR_BATCH) and with ambiguous lists that fill at once
     (KRCA_CORR_AMB_TILE = 0: every tile decides its pairs in place; 8: mixed), and the list re-scored
-    pair by pair instead of grouped by row pod (KRCA_CORR_RS_GROUP = 0), give the same outputs bit for
+    pair by pair instead of grouped by row pod (KRCA_CORR_RS_GROUP = 0), or grouped from the fp32
+    partner rows instead of the int16 ones (KRCA_CORR_RS_Q16 = 0), give the same outputs bit for
     bit as the default run (the same float64 re-score in the tile and in either list kernel)."""
     P, T, k = 40_000, 1440, 10
     x = synth.make_metrics(P, 1, T, seed=3, group_size=20, device="cuda")
@@ -179,16 +180,20 @@ def test_corr_batches_and_full_lists_identical(eng):
     lib = eng.lib
     try:
         # (KRCA_CORR_SIDE: the re-scores beside the next batch, after each batch, or after each but the last)
-        for batch, per_tile, group, side in ((4, -1, 1, 0), (0, 0, 1, 0), (3, 8, 1, 0), (0, -1, 0, 0), (4, -1, 0, 0),
-                                             (4, -1, 1, 1), (4, -1, 1, 2), (3, 8, 1, 2)):
+        # (KRCA_CORR_RS_Q16 = 0: the grouped re-score reads the fp32 partner rows, not the int16 ones)
+        for batch, per_tile, group, side, q16 in ((4, -1, 1, 0, 1), (0, 0, 1, 0, 1), (3, 8, 1, 0, 1), (0, -1, 0, 0, 1),
+                                                  (4, -1, 0, 0, 1), (4, -1, 1, 1, 1), (4, -1, 1, 2, 1), (3, 8, 1, 2, 1),
+                                                  (0, -1, 1, 0, 0), (4, -1, 1, 0, 0)):
             assert lib.krca_tune_set(b"KRCA_CORR_BATCH", batch) == 0
             assert lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", per_tile) == 0
             assert lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", group) == 0
             assert lib.krca_tune_set(b"KRCA_CORR_SIDE", side) == 0
+            assert lib.krca_tune_set(b"KRCA_CORR_RS_Q16", q16) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
             for key in ref:
-                assert np.array_equal(got[key], ref[key]), (batch, per_tile, group, side, key)
+                assert np.array_equal(got[key], ref[key]), (batch, per_tile, group, side, q16, key)
     finally:
+        lib.krca_tune_set(b"KRCA_CORR_RS_Q16", 1)
         lib.krca_tune_set(b"KRCA_CORR_BATCH", 0)
         lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", -1)
         lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", 1)
