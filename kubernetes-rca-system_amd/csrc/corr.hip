@@ -19,8 +19,9 @@
 //                      that pod's candidate buffer (one atomic slot reservation per hit; hits are
 //                      sparse by construction of phi); |r| > tau counts via LDS, one global add per
 //                      row / column and tile.
-//   merge              one workgroup per pod: bitonic sort of its (<= CAPC) candidates, the best
-//                      k+6 re-scored in float64 from z32 (fixed-order wave reduction), final top-k;
+//   merge              one workgroup per pod: selection of its best k+7 of (<= CAPC) candidates
+//                      (per-wave register bitonic sorts of 64 and merges into a running best 32),
+//                      the best k+6 re-scored in float64 from z32 (fixed-order wave reduction), final top-k;
 //                      cert[p] = (k-th re-scored |r|) - max(phi, first unre-scored |r|) - eps:
 //                      cert > 0 proves the reported set equals the exact top-k.  A pod whose buffer
 //                      overflowed gets phi2 = (k-th best stored |r|) - 2 eps (any subset bounds the
@@ -32,8 +33,9 @@
 // moves a dot product by <= 2^-10 (+ 2^-24 sqrt(T) from subnormals), fp32 accumulation of T
 // terms of a unit-norm product by <= T 2^-24.  It bounds the candidate pool.  |r| > tau counts
 // are exact: a screening value above tau + eps counts at once, one within eps of tau is appended
-// to the AMBIGUOUS list and re-scored in float64 (corr_amb_rescore), one below tau - eps cannot
-// count.  Reported r values are exact.  The sample and main passes run the same K loop, so a
+// to the AMBIGUOUS list and re-scored in float64 (corr_amb_rescore; grouped by row pod, from the
+// partner's int16 row first and its fp32 row only within the int16 row's error bound of tau), one
+// below tau - eps cannot count.  Reported r values are exact.  The sample and main passes run the same K loop, so a
 // pair's screening value is the same bits in both.
 //
 //   deep merge         a pod whose certificate is <= 0 after the merge (near-ties around its k-th
@@ -1287,8 +1289,32 @@ __global__ __launch_bounds__(TPB) void corr_gather_rows(const uint16_t* __restri
   for (int c = threadIdx.x; c < Tp / 8; c += TPB) dst[c] = r < n ? src[c] : make_uint4(0, 0, 0, 0);
 }
 
-// one workgroup per pod (or per listed pod in the second pass): sort the pod's candidates, re-score
-// the best km = k + 6 in float64, rank, certify.  Pass 0 turns an overflowed buffer into phi2 and
+// compare-exchange of lane pairs (lane, lane ^ j) in (|r| desc, index asc, empties last) order:
+// keep_better picks the better of the two, else the other one
+__device__ __forceinline__ void cand_cx(float& v, int32_t& i, int j, bool keep_better) {
+  const float pv = __shfl_xor(v, j, 64);
+  const int32_t pi = __shfl_xor(i, j, 64);
+  if (cbetter(pv, pi, v, i) == keep_better) {
+    v = pv;
+    i = pi;
+  }
+}
+
+// lanes 0-31 hold a sorted list (best first); (cv, ci) a sorted 64-lane chunk: afterwards lanes
+// 0-31 hold the best 32 of both (bitonic: the chunk's best 32 reversed into lanes 32-63, one merge)
+__device__ __forceinline__ void cand_merge32(float& v, int32_t& i, float cv, int32_t ci, int lane) {
+  const float rv = __shfl(cv, 63 - lane, 64);
+  const int32_t ri = __shfl(ci, 63 - lane, 64);
+  if (lane >= 32) {
+    v = rv;
+    i = ri;
+  }
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1) cand_cx(v, i, j, (lane & j) == 0);
+}
+
+// one workgroup per pod (or per listed pod in the second pass): select the pod's best km + 1
+// candidates, re-score the best km = k + 6 in float64, rank, certify.  Pass 0 turns an overflowed buffer into phi2 and
 // queues the pod for the second main pass (over[0] = count, over[1..] = pods).
 __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, int32_t* __restrict__ cnt,
                                                   const float* __restrict__ phi_used, const float* __restrict__ z32,
@@ -1297,8 +1323,8 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
                                                   int32_t* __restrict__ over, int32_t* __restrict__ out_i,
                                                   float* __restrict__ out_v, float* __restrict__ cert, int64_t lo,
                                                   int32_t* __restrict__ deep) {
-  __shared__ float cv[CAPC];
-  __shared__ int32_t ci[CAPC];
+  __shared__ float wl_v[TPB / 64][32];
+  __shared__ int32_t wl_i[TPB / 64][32];
   __shared__ float top_v[KM + 1];
   __shared__ int32_t top_i[KM + 1];
   __shared__ double exact[KM];
@@ -1318,50 +1344,54 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
       top_v[tid] = 0.f;
     }
   } else {
+    // selection instead of a sort: every wave keeps the best 32 of its 64-candidate chunks (a
+    // bitonic sort of the chunk in registers, then one merge into the running list), wave 0 merges
+    // the waves' lists; the order is total, so the best km + 1 are those of a full sort
+    static_assert(KM + 1 <= 32, "the selection keeps 32 per wave");
     const int nn = overflow ? CAPC : n;
-    int np = 32;
-    while (np < nn) np <<= 1;
-    for (int i = tid; i < np; i += TPB) {
-      if (i < nn) {
-        const int2 c = buf[gl * CAPC + i];
-        cv[i] = __int_as_float(c.x);
-        ci[i] = c.y;
+    float v = 0.f;
+    int32_t iv = -1;
+    for (int c0 = 64 * w; c0 < nn; c0 += TPB) {  // wave-uniform
+      float cvv = 0.f;
+      int32_t cii = -1;
+      if (c0 + lane < nn) {
+        const int2 c = buf[gl * CAPC + c0 + lane];
+        cvv = __int_as_float(c.x);
+        cii = c.y;
+      }
+#pragma unroll
+      for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) cand_cx(cvv, cii, j, ((lane & j) == 0) == ((lane & kk) == 0));
+      if (c0 == 64 * w) {
+        v = cvv;
+        iv = cii;
       } else {
-        cv[i] = 0.f;
-        ci[i] = -1;
+        cand_merge32(v, iv, cvv, cii, lane);
+      }
+    }
+    if (lane < 32) {
+      wl_v[w][lane] = v;
+      wl_i[w][lane] = iv;
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int u = 1; u < TPB / 64; ++u)
+        cand_merge32(v, iv, lane < 32 ? wl_v[u][lane] : 0.f, lane < 32 ? wl_i[u][lane] : -1, lane);
+      if (lane <= KM) {
+        top_v[lane] = v;
+        top_i[lane] = iv;
       }
     }
     __syncthreads();
-    for (int kk = 2; kk <= np; kk <<= 1) {  // bitonic: |r| desc, index asc, empties last
-      for (int j = kk >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < np; i += TPB) {
-          const int l = i ^ j;
-          if (l > i) {
-            const bool desc = (i & kk) == 0;
-            if (cbetter(cv[l], ci[l], cv[i], ci[i]) == desc) {
-              const float tv = cv[i];
-              const int32_t ti = ci[i];
-              cv[i] = cv[l];
-              ci[i] = ci[l];
-              cv[l] = tv;
-              ci[l] = ti;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
     if (overflow && pass == 0) {  // any stored subset bounds the exact k-th from below
       if (tid == 0) {
-        phi2[g] = fabsf(cv[k - 1]) - 2.f * eps - 1e-6f;
+        phi2[g] = fabsf(top_v[k - 1]) - 2.f * eps - 1e-6f;
         cnt[gl] = 0;
         over[1 + atomicAdd(&over[0], 1)] = (int32_t)g;
       }
       return;
-    }
-    if (tid <= KM) {
-      top_v[tid] = tid < np ? cv[tid] : 0.f;
-      top_i[tid] = tid < np ? ci[tid] : -1;
     }
   }
   __syncthreads();
