@@ -46,7 +46,8 @@ int krca_device_count(int* n_host);
 
 /* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID, KRCA_PPR_DICT,
  * KRCA_LOG_IMPL, KRCA_GROUP_IMPL, KRCA_CORR_DEBUG, KRCA_CORR_RS_GRID, KRCA_CORR_BATCH, KRCA_CORR_AMB_TILE,
- * KRCA_PPR_FUSE, KRCA_PPR_NT, KRCA_PPR_XCD, KRCA_LOG_FUSED, KRCA_CORR_RS_GROUP, KRCA_CORR_SIDE, KRCA_CORR_RS_Q16.  Initialised once from the environment variables
+ * KRCA_PPR_FUSE, KRCA_PPR_NT, KRCA_PPR_XCD, KRCA_LOG_FUSED, KRCA_CORR_RS_GROUP, KRCA_CORR_SIDE, KRCA_CORR_RS_Q16,
+ * KRCA_CORR_CAPC.  Initialised once from the environment variables
  * of the same names when the library loads; launchers never call getenv.  Process-global, not
  * thread-safe (set them before launching work).  Unknown names: KRCA_EINVAL. */
 int krca_tune_set(const char* name, int32_t value);
@@ -178,6 +179,8 @@ int64_t krca_corr_pad_rows(int64_t P);
 int32_t krca_corr_pad_steps(int32_t T);
 int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k);
 int32_t krca_corr_max_k(void);
+/* candidates buffered per pod by the main pass (cand's first [P][cap] int2 entries, then the [P] fill counts) */
+int32_t krca_corr_cand_cap(void);
 float krca_corr_eps(int32_t T);
 int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t channel, float* mean, float* scale,
                       float* z32, uint16_t* zh, void* stream);

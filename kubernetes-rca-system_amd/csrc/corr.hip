@@ -60,7 +60,8 @@ constexpr int KM = 24;    // candidates re-scored per pod in the merge (>= k + 6
 constexpr int KMAX = 16;  // largest k served
 constexpr int NSB = 16;   // 128-pod column blocks in the threshold sample (2048 pods)
 constexpr int NSL = NSB + 2;  // sample lists per pod: NSB sample blocks + the pod's own 256-block
-constexpr int CAPC = 1024;    // candidate buffer per pod (main pass appends)
+constexpr int CAPC = 2048;    // candidate buffer per pod (main pass appends; 1024 overflowed ~1 % of
+                              // the pods at C3 / 1M, whose rectangle pass cost 1.8 ms / 123 ms, R5k)
 // Ambiguous |r| ~ tau pairs (screening value within eps of tau, not settled by the pair's own
 // bound) are re-scored in float64 for exact counts.  C3's random-walk series put ~130 partners per
 // pod within eps of tau = 0.5 (~170 in EVERY 256 x 256 tile, about half settled in the tile), so the
@@ -343,6 +344,7 @@ struct TileArgs {
   float* selfd;
   int2* buf;
   int32_t* cnt;
+  int capc;  // candidate slots used per pod (<= CAPC, the buffers' row stride; cand_cap())
   int32_t* count;
   const int32_t* rect_pods;
   int64_t n_rect;
@@ -757,8 +759,8 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         const int64_t lr = RECT ? gr - sh.lo : gr;  // rect: local buffers
         const int s1 = (tag & 1) ? atomicAdd(&A.cnt[lr], 1) : CAPC;
         const int s2 = (!RECT && (tag & 2)) ? atomicAdd(&A.cnt[gc], 1) : CAPC;
-        if (s1 < CAPC) A.buf[lr * CAPC + s1] = make_int2(ent.y, gc);
-        if (s2 < CAPC) A.buf[(int64_t)gc * CAPC + s2] = make_int2(ent.y, gr);
+        if (s1 < A.capc) A.buf[lr * CAPC + s1] = make_int2(ent.y, gc);
+        if (s2 < A.capc) A.buf[(int64_t)gc * CAPC + s2] = make_int2(ent.y, gr);
       }
       if (!RECT && atot) {  // block-uniform
         if (tid == 0) *sbase = abase_t;
@@ -1322,7 +1324,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
                                                   const int32_t* __restrict__ pods, float* __restrict__ phi2,
                                                   int32_t* __restrict__ over, int32_t* __restrict__ out_i,
                                                   float* __restrict__ out_v, float* __restrict__ cert, int64_t lo,
-                                                  int32_t* __restrict__ deep) {
+                                                  int32_t* __restrict__ deep, int capc) {
   __shared__ float wl_v[TPB / 64][32];
   __shared__ int32_t wl_i[TPB / 64][32];
   __shared__ float top_v[KM + 1];
@@ -1335,7 +1337,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
   const float ph = phi_used[g];
   const bool flat = ph > 2.f;
   const int n = cnt[gl];
-  const bool overflow = n > CAPC;
+  const bool overflow = n > capc;
   const int km = k + 6 < KM ? k + 6 : KM;
   if (flat) {  // r = 0 with every partner: the lowest other indices, in order
     if (tid <= KM) {
@@ -1348,7 +1350,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
     // bitonic sort of the chunk in registers, then one merge into the running list), wave 0 merges
     // the waves' lists; the order is total, so the best km + 1 are those of a full sort
     static_assert(KM + 1 <= 32, "the selection keeps 32 per wave");
-    const int nn = overflow ? CAPC : n;
+    const int nn = overflow ? capc : n;
     float v = 0.f;
     int32_t iv = -1;
     for (int c0 = 64 * w; c0 < nn; c0 += TPB) {  // wave-uniform
@@ -1476,7 +1478,7 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
                                                        const float* __restrict__ z32,
                                                        int T, int k, float eps, const int32_t* __restrict__ pods,
                                                        int32_t* __restrict__ out_i, float* __restrict__ out_v,
-                                                       float* __restrict__ cert, int64_t lo) {
+                                                       float* __restrict__ cert, int64_t lo, int capc) {
   __shared__ double ex[CAPC];
   __shared__ int32_t ci[CAPC];
   __shared__ int srest;  // pass 0: the largest screening |r| left out (float bits, >= 0), INT_MIN = none
@@ -1485,7 +1487,7 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
   for (int b = blockIdx.x; b < nd; b += gridDim.x) {
   const int64_t g = pods[1 + b];
   const int64_t gl = g - lo;
-  const int n = min(cnt[gl], CAPC);
+  const int n = min(cnt[gl], capc);
   int np = 32;
   while (np < n) np <<= 1;
   // the merge's k-th exact |r| (its output row, written before it listed the pod)
@@ -1595,23 +1597,25 @@ int debug_mode() { return krca::tuning().corr_debug; }
 constexpr int RECT_ROWS = 4096;  // rows of the second (rectangle) pass per launch
 
 // ---- exchange of the sharded run: candidates of pod p travel to its owner p / n_max ----------
-// totals per destination (clipped at CAPC: a pod past CAPC overflows at its owner anyway)
+// totals per destination (clipped at the cap: the owner's merge reads the all-reduced raw counts,
+// so a pod past the cap on any rank overflows at its owner too)
 __global__ __launch_bounds__(TPB) void corr_pack_count(const int32_t* __restrict__ cnt, int64_t P, int64_t n_max,
-                                                       unsigned long long* __restrict__ tot) {
+                                                       unsigned long long* __restrict__ tot, int capc) {
   const int64_t p = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (p >= P) return;
-  const int c = min(cnt[p], CAPC);
+  const int c = min(cnt[p], capc);
   if (c) atomicAdd(&tot[p / n_max], (unsigned long long)c);
 }
 
 // one wave per pod: reserve its range in the destination's region, copy {pod, partner, r bits}
 __global__ __launch_bounds__(TPB) void corr_pack(const int32_t* __restrict__ cnt, const int2* __restrict__ buf, int64_t P,
                                                  int64_t n_max, const unsigned long long* __restrict__ off,
-                                                 unsigned long long* __restrict__ cursor, int4* __restrict__ send) {
+                                                 unsigned long long* __restrict__ cursor, int4* __restrict__ send,
+                                                 int capc) {
   const int64_t p = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (p >= P) return;
-  const int c = min(cnt[p], CAPC);
+  const int c = min(cnt[p], capc);
   if (c == 0) return;
   const int64_t h = p / n_max;
   unsigned long long base = 0;
@@ -1625,13 +1629,13 @@ __global__ __launch_bounds__(TPB) void corr_pack(const int32_t* __restrict__ cnt
 
 // received entries -> this rank's per-pod buffers (any order: the merge sorts)
 __global__ __launch_bounds__(TPB) void corr_unpack(const int4* __restrict__ recv, int64_t n, int64_t lo,
-                                                   int32_t* __restrict__ fill, int2* __restrict__ lbuf) {
+                                                   int32_t* __restrict__ fill, int2* __restrict__ lbuf, int capc) {
   const int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (e >= n) return;
   const int4 v = recv[e];
   const int64_t q = v.x - lo;
   const int s = atomicAdd(&fill[q], 1);
-  if (s < CAPC) lbuf[q * CAPC + s] = make_int2(v.z, v.y);
+  if (s < capc) lbuf[q * CAPC + s] = make_int2(v.z, v.y);
 }
 
 struct CorrWs {  // views into a caller's candidate workspace
@@ -1798,6 +1802,12 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   return KRCA_OK;
 }
 
+// candidate slots used per pod: CAPC, or fewer under KRCA_CORR_CAPC (tests: overflows on purpose)
+inline int cand_cap() {
+  const int c = krca::tuning().corr_capc;
+  return c >= 64 && c < CAPC ? c : CAPC;
+}
+
 // the grouped re-score reads int16 partner rows (written by corr_dnorm)
 inline bool q16_rows() { return krca::tuning().corr_rs_q16 && krca::tuning().corr_rs_group; }
 
@@ -1897,6 +1907,7 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.acc_err = acc_err;
   ta.phi = phi;
   ta.buf = ws.buf;
+  ta.capc = cand_cap();
   ta.cnt = ws.cnt;
   ta.count = count;
   ta.sh = sh;
@@ -1953,7 +1964,8 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
   KRCA_HIP(hipMemsetAsync(ws.deep, 0, sizeof(int32_t), st));
   KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.phi2), 0x40400000 /* 3.0f */, (size_t)d.P, st));
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n), dim3(TPB), 0, st, (const int2*)lbuf, lcnt, phi, z32, d.P, d.T,
-                     d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo, ws.deep);
+                     d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo, ws.deep,
+                     cand_cap());
   KRCA_LAUNCH_CHECK();
   int32_t n_over = 0;
   KRCA_HIP(hipMemcpyAsync(&n_over, ws.over, sizeof(int32_t), hipMemcpyDeviceToHost, st));
@@ -1962,7 +1974,7 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
     hipLaunchKernelGGL(corr_merge_deep, dim3((unsigned)std::min<int64_t>(n, 2048)), dim3(TPB), 0, st,
                        (const int2*)lbuf, (const int32_t*)lcnt, phi, (const float*)ws.phi2, z32, d.T, d.k, d.eps,
                        (const int32_t*)ws.deep,
-                       out_idx, out_val, cert, lo);
+                       out_idx, out_val, cert, lo, cand_cap());
     KRCA_LAUNCH_CHECK();
     return KRCA_OK;
   };
@@ -1984,6 +1996,7 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
     ta.nsb = d.nsb;
     ta.phi = ws.phi2;
     ta.buf = lbuf;
+    ta.capc = cand_cap();
     ta.cnt = lcnt;
     ta.rect_pods = ws.over + 1 + r0;
     ta.n_rect = nr;
@@ -1996,7 +2009,7 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
   }
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,
                      (const float*)ws.phi2, z32, d.P, d.T, d.k, d.eps, 1, (const int32_t*)(ws.over + 1), ws.phi2,
-                     ws.over, out_idx, out_val, cert, lo, ws.deep);
+                     ws.over, out_idx, out_val, cert, lo, ws.deep, cand_cap());
   KRCA_LAUNCH_CHECK();
   return deep_pass();
 }
@@ -2035,6 +2048,7 @@ int64_t krca_corr_cand_size(int64_t P, int32_t T, int32_t k) {
   return ws_layout(P, T, krca_corr_pad_steps(T), kc_for(k), P, 0, nullptr, nullptr) + krca::ceil_div(P, 4) * 4;
 }
 int32_t krca_corr_max_k(void) { return KMAX; }
+int32_t krca_corr_cand_cap(void) { return CAPC; }
 float krca_corr_eps(int32_t T) {
   return (float)(std::ldexp(1.0, -10) * 1.001 + std::ldexp((double)T, -24) + std::ldexp(std::sqrt((double)T), -23));
 }
@@ -2129,7 +2143,7 @@ int krca_corr_shard_pack_sizes(int64_t P, int32_t T, int32_t k, int64_t n_loc, i
   KRCA_CHECK_ARG(tot_host && n_max > 0 && n_max * G >= P, "krca_corr_shard_pack_sizes: bad args");
   KRCA_HIP(hipMemsetAsync(w.xc, 0, 3 * (size_t)G * sizeof(unsigned long long), st));
   hipLaunchKernelGGL(corr_pack_count, dim3((unsigned)krca::ceil_div(P, TPB)), dim3(TPB), 0, st, (const int32_t*)w.cnt,
-                     P, n_max, w.xc);
+                     P, n_max, w.xc, cand_cap());
   KRCA_LAUNCH_CHECK();
   std::vector<unsigned long long> tot(G), off(G);
   KRCA_HIP(hipMemcpyAsync(tot.data(), w.xc, G * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -2151,7 +2165,7 @@ int krca_corr_shard_pack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t
   KRCA_CHECK_ARG(send && n_max > 0, "krca_corr_shard_pack: bad args");
   hipLaunchKernelGGL(corr_pack, dim3((unsigned)krca::ceil_div(P, TPB / 64)), dim3(TPB), 0, st, (const int32_t*)w.cnt,
                      (const int2*)w.buf, P, n_max, (const unsigned long long*)(w.xc + G), w.xc + 2 * G,
-                     reinterpret_cast<int4*>(send));
+                     reinterpret_cast<int4*>(send), cand_cap());
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
@@ -2163,7 +2177,7 @@ int krca_corr_shard_unpack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32
   KRCA_HIP(hipMemsetAsync(w.fill, 0, (size_t)std::max<int64_t>(n_loc, 1) * sizeof(int32_t), st));
   if (n_recv == 0) return KRCA_OK;
   hipLaunchKernelGGL(corr_unpack, dim3((unsigned)krca::ceil_div(n_recv, TPB)), dim3(TPB), 0, st,
-                     reinterpret_cast<const int4*>(recv), n_recv, lo, w.fill, w.lbuf);
+                     reinterpret_cast<const int4*>(recv), n_recv, lo, w.fill, w.lbuf, cand_cap());
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

@@ -112,6 +112,8 @@ struct Tuning {
                       // batch except the last (beside the merge chain)
   int corr_rs_q16;    // KRCA_CORR_RS_Q16: the grouped re-score reads int16 partner rows (row max / 32767 steps)
                       // and re-reads the fp32 row only within their error bound of tau (0 = fp32 rows)
+  int corr_capc;      // KRCA_CORR_CAPC: candidate slots used per pod, 64 .. krca_corr_cand_cap() (0 = all; tests
+                      // make buffers overflow with fewer)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

@@ -49,6 +49,7 @@ SIGNATURES = {
     "krca_corr_pad_steps": (c_i32, [c_i32]),
     "krca_corr_cand_size": (c_i64, [c_i64, c_i32, c_i32]),
     "krca_corr_max_k": (c_i32, []),
+    "krca_corr_cand_cap": (c_i32, []),
     "krca_corr_eps": (c_f32, [c_i32]),
     "krca_corr_prepare": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_corr_topk": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -262,6 +262,32 @@ def test_corr_list_overflow_refill(eng):
     assert np.all(res["count"][:1200] >= 599)
 
 
+def test_corr_candidate_buffer_overflow(eng):
+    """Candidate buffers that overflow (KRCA_CORR_CAPC = 192 of the krca_corr_cand_cap() slots: most
+    pods of this mesh pass it) take phi2 from the entries that landed, the rectangle pass over their
+    rows and the second merge -- on one device and through the sharded path's pack / all-to-all /
+    unpack (emulated, G = 2).  Partners, values and counts equal the run whose buffers hold every
+    candidate; every row certified."""
+    from krca.corr_dist import run_emulated
+    P, T, k = 20_000, 720, 10
+    x = synth.make_metrics(P, 1, T, seed=8, group_size=20, device="cuda")
+    ref = eng.corr_topk(x, k=k, tau=TAU)
+    cap = eng.lib.krca_corr_cand_cap()
+    raw = eng._ws["corr_cand"].view(torch.int32)[2 * P * cap: 2 * P * cap + P].cpu().numpy()
+    assert (raw > cap).sum() == 0 and (raw > 192).sum() > P // 10, ((raw > cap).sum(), (raw > 192).sum())
+    lib = eng.lib
+    try:
+        assert lib.krca_tune_set(b"KRCA_CORR_CAPC", 192) == 0
+        got = eng.corr_topk(x, k=k, tau=TAU)
+        emu = run_emulated(eng, x, P, T, k, TAU, 2)
+    finally:
+        lib.krca_tune_set(b"KRCA_CORR_CAPC", 0)
+    for res in (got, emu):
+        for key in ("idx", "val", "count"):
+            assert np.array_equal(res[key], ref[key]), key
+        assert (res["cert"] > 0).all(), np.nonzero(res["cert"] <= 0)[0][:10]
+
+
 def test_corr_every_pair_at_tau(eng):
     """600 series x_i = u + v_i from orthogonal Hadamard rows: every in-group pair has r = 0.5 = tau
     (up to the fp32 rounding of the rows), so each in-group tile has 65,536 pairs within eps of tau:
@@ -295,7 +321,7 @@ def test_corr_sharded_path_emulated_on_one_gpu(eng, P, T, G):
     """The pod-sharded correlation (krca/corr_dist.py: G super-tile shares of the triangle, one
     all-to-all of candidates by owner) with the collectives done by copies: every output equals
     the single-device run (same screening products, same candidate sets, same merge).  The one
-    exception is the certificate MARGIN of a pod whose 1,024-entry candidate buffer overflowed: its
+    exception is the certificate MARGIN of a pod whose 2,048-entry candidate buffer overflowed: its
     second threshold phi2 is the k-th best of the candidates that landed first, and arrival order
     differs between one device and the all-to-all.  Its partners, values and count are still
     identical and both certificates positive."""

@@ -238,8 +238,14 @@ def test_rccl_graph_capture_exchange_diagnostic(eng, pg, mesh, how):
         diff = {name: int((getattr(sh_e, name)[:N] != getattr(sh, name)[:N]).sum().item())
                 for name in ("r", "q", "d", "key")}
         diff["score"] = int((sh_e.score_out["score"] != sh.score_out["score"]).sum().item())
-        diff["ctl"] = bytes(sh_e.ctl.cpu().numpy().tobytes()) == bytes(sh.ctl.cpu().numpy().tobytes())
+        ce, cg = sh_e.ctl.cpu().numpy(), sh.ctl.cpu().numpy()
+        he, hg = ce[:48].view(np.uint8), cg[:48].view(np.uint8)
+        diff["ctl_head"] = [(f, float(np.frombuffer(he[o:o + 8].tobytes(), t)[0]), float(np.frombuffer(hg[o:o + 8].tobytes(), t)[0]))
+                            for f, o, t in (("tele", 0, np.float64), ("q_total", 8, np.int64), ("tele_used", 32, np.float64))
+                            if he[o:o + 8].tobytes() != hg[o:o + 8].tobytes()]
+        diff["ctl_head"] += [("conv_iter", ce[16:24].tolist(), cg[16:24].tolist())] if ce[16:24].tobytes() != cg[16:24].tobytes() else []
+        diff["ctl_rest"] = int((ce[48:] != cg[48:]).sum())
         diff["top"] = [int(i) for i in ie] == [int(i) for i in ig]
         report.append((shift, diff))
     assert torch.equal(sh.w_all, sh.send), how
-    assert all(d["top"] and d["r"] == 0 and d["key"] == 0 for _, d in report), (how, report)
+    assert all(d["top"] and d["r"] == 0 and d["key"] == 0 for _, d in report), f"{how}: {report!r}"

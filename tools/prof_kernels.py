@@ -74,9 +74,11 @@ def main():
         P, T = a.pods, a.tsteps
         flops = P * (P + 1) * T  # upper triangle incl. diagonal, 2 flops per MAC
         ws = eng._ws["corr_cand"].view(torch.int32)
-        cnt = ws[2 * P * 1024: 2 * P * 1024 + P].float()  # candidates per pod (CAPC = 1024)
+        cap = eng.lib.krca_corr_cand_cap()
+        cnt = ws[2 * P * cap: 2 * P * cap + P].float()  # candidates per pod (appends, not clipped at cap)
         out = dict(kernel="corr top-k", ms=ms, ms_prepare=ms_prep, flops=flops,
                    tflops=flops / (min(ms) * 1e-3) / 1e12, certified=float((r["cert"] > 0).float().mean()),
+                   cand_over=int((cnt > cap).sum()),
                    cand_mean=float(cnt.mean()), cand_max=float(cnt.max()), cand_p99=float(cnt.quantile(0.99)))
     elif a.what == "bc":
         # f3: betweenness over a strongly connected service graph (each node links to 2 random
