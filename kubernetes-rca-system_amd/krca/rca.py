@@ -747,6 +747,8 @@ class RcaStep:
             return self._propagate_tol()
         if not self.graph:
             return self._propagate()
+        import gc
+
         import torch
         if self._g is None:
             self._propagate()  # eager warm-up: statics, occupancy queries, workspaces
@@ -754,8 +756,17 @@ class RcaStep:
             cur = torch.cuda.current_stream(self.s.eng.device)
             side = torch.cuda.Stream(self.s.eng.device)
             side.wait_stream(cur)
-            with torch.cuda.graph(g, stream=side):
-                self._propagate()
+            # no garbage collection inside the capture: a collected cycle that holds device objects
+            # (another graph, events, a communicator's work) would release them mid-capture, which
+            # the runtime aborts on (torch.cuda.graph collects once before it begins)
+            was = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g, stream=side):
+                    self._propagate()
+            finally:
+                if was:
+                    gc.enable()
             cur.wait_stream(side)
             self._g = g
         self._g.replay()

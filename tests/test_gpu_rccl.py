@@ -247,5 +247,6 @@ def test_rccl_graph_capture_exchange_diagnostic(eng, pg, mesh, how):
         diff["ctl_rest"] = int((ce[48:] != cg[48:]).sum())
         diff["top"] = [int(i) for i in ie] == [int(i) for i in ig]
         report.append((shift, diff))
+        print(how, shift, diff, flush=True)
     assert torch.equal(sh.w_all, sh.send), how
     assert all(d["top"] and d["r"] == 0 and d["key"] == 0 for _, d in report), f"{how}: {report!r}"
