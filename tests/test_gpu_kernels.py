@@ -558,6 +558,36 @@ def test_rca_step_graph_replay_equals_eager(eng):
     assert np.array_equal(res[True][0][2], res[True][2][2]) and not np.array_equal(res[True][0][2], res[True][1][2])
 
 
+@pytest.mark.parametrize("launches", [0, 300, 5000])
+def test_rca_graph_replay_after_eager_launches(eng, launches):
+    """Diagnostic: the captured solve replayed after `launches` unrelated eager kernel launches
+    (tiny torch adds) between its first and second replay still equals the eager solve."""
+    from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph
+    n = 20000
+    m = synth.make_graph(n, avg_degree=20, seed=5)
+    cfg = Config(iters=30, tol=0.0)
+    rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, n)
+    x0 = synth.make_metrics(n, 8, 300, window=60, seed=1, roots=m.roots, hop_sets=synth.caller_hops(m, m.roots)).cuda()
+    refs = []
+    xe = x0.clone()
+    st_e = RcaStep(DeviceShard(eng, xe, rp, col, od, n, n, 1, cfg), Comm(), cfg, 0)
+    for shift in (0.0, 3.0):
+        xe[-1, :50] += shift * 10.0
+        refs.append(([int(i) for i in st_e.run()[0]], st_e.s.r[:n].cpu().numpy().copy()))
+    xg = x0.clone()
+    st_g = RcaStep(DeviceShard(eng, xg, rp, col, od, n, n, 1, cfg), Comm(), cfg, 0, graph=True)
+    junk = torch.zeros(64, device="cuda")
+    got = []
+    for shift in (0.0, 3.0):
+        xg[-1, :50] += shift * 10.0
+        if shift:
+            for _ in range(launches):
+                junk.add_(1.0)
+        got.append(([int(i) for i in st_g.run()[0]], st_g.s.r[:n].cpu().numpy().copy()))
+    for (ie, re), (ig, rg) in zip(refs, got):
+        assert ie == ig and np.array_equal(re, rg), (launches, int((re != rg).sum()))
+
+
 @pytest.mark.parametrize("G", [2, 3])
 @pytest.mark.parametrize("folded", [False, True])
 def test_rca_sharded_path_emulated_on_one_gpu(eng, G, folded):
