@@ -39,6 +39,8 @@ for s in "$@"; do
     testsall_*) step $s 900 python3 -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread -k "${s#testsall_}" ;;
     tests_*) step $s 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "${s#tests_}" ;;
     bench) step bench 400 python3 bench.py ;;
+    graphdbg) step testsall_graphdbg 300 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" &&
+              step testsall_graphdbg_nopkt 300 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" ;;
     bench_cpufull) step bench_cpufull 500 python3 bench.py --steps 3 --warmup 1 --cpu-full-mesh --no-corr ;;
     bench_trace) prof bench_trace 500 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify ;;
     rank_def) step rank_def 900 python3 -u tools/ranking_ablation_c4.py --out $O/ranking_ablation_c4.json ;;
