@@ -693,6 +693,19 @@ class Explain:
         return self._dev[key]
 
 
+def _check_graph_runtime():
+    """The HIP runtime's graph packet capture must be off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0, set
+    before the first HIP call): with it on, a captured solve replayed after some hundreds of other
+    kernel launches computed wrong ranks (R5n / R5o, tests/test_gpu_kernels.py::
+    test_rca_graph_replay_after_eager_launches: 300 unrelated launches between two replays were
+    enough; graphs of torch kernels alone replayed correctly)."""
+    import os
+    if os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
+        raise RuntimeError("RcaStep: the HIP-graph solve needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment "
+                           "before the first HIP call (replays of captured libkrca kernels are otherwise "
+                           "overwritten by later launches on this runtime; DESIGN.md §5)")
+
+
 def graph_default(comm, cfg, shard=None):
     """Whether RcaStep captures its PageRank solve in a HIP graph: only with KRCA_RCA_GRAPH=1, for
     fixed-iteration solves (tol <= 0: no host read-back between iterations) of a device shard.
@@ -703,7 +716,7 @@ def graph_default(comm, cfg, shard=None):
     import os
     if os.environ.get("KRCA_RCA_GRAPH") != "1" or cfg.tol > 0 or not isinstance(shard, DeviceShard):
         return False
-    return True
+    return True  # (RcaStep then checks the runtime setting: _check_graph_runtime)
 
 
 class RcaStep:
@@ -723,6 +736,8 @@ class RcaStep:
         self.graph = graph_default(comm, cfg, shard) if graph is None else bool(graph)
         if self.graph and cfg.tol > 0:
             raise ValueError("RcaStep: the HIP-graph solve needs a fixed-iteration Config (tol = 0)")
+        if self.graph:
+            _check_graph_runtime()
         self._g = None
         if explain is not None and not isinstance(explain, Explain):
             explain = Explain(*explain)

@@ -560,8 +560,9 @@ def test_rca_step_graph_replay_equals_eager(eng):
 
 @pytest.mark.parametrize("launches", [0, 300, 5000])
 def test_rca_graph_replay_after_eager_launches(eng, launches):
-    """Diagnostic: the captured solve replayed after `launches` unrelated eager kernel launches
-    (tiny torch adds) between its first and second replay still equals the eager solve."""
+    """The captured solve replayed after `launches` unrelated eager kernel launches (tiny torch adds)
+    between its first and second replay still equals the eager solve.  Failed at 300 and 5000 with
+    the runtime's graph packet capture on (R5n); tests/conftest.py turns it off, as RcaStep requires."""
     from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph
     n = 20000
     m = synth.make_graph(n, avg_degree=20, seed=5)
@@ -586,37 +587,6 @@ def test_rca_graph_replay_after_eager_launches(eng, launches):
         got.append(([int(i) for i in st_g.run()[0]], st_g.s.r[:n].cpu().numpy().copy()))
     for (ie, re), (ig, rg) in zip(refs, got):
         assert ie == ig and np.array_equal(re, rg), (launches, int((re != rg).sum()))
-
-
-@pytest.mark.parametrize("launches", [0, 300])
-def test_torch_graph_replay_after_eager_launches(launches):
-    """Diagnostic: a HIP graph of torch kernels only (40 dependent elementwise ops), replayed after
-    `launches` unrelated eager launches, on new inputs: the same values as the eager sequence."""
-    x = torch.arange(4096, dtype=torch.float32, device="cuda")
-    y = torch.empty_like(x)
-
-    def seq():
-        y.copy_(x)
-        for i in range(40):
-            y.mul_(1.0001).add_(float(i))
-    seq()
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.graph(g, stream=side):
-        seq()
-    torch.cuda.current_stream().wait_stream(side)
-    g.replay()
-    torch.cuda.synchronize()
-    junk = torch.zeros(64, device="cuda")
-    for _ in range(launches):
-        junk.add_(1.0)
-    x.mul_(-3.0)
-    g.replay()
-    got = y.clone()
-    seq()
-    assert torch.equal(got, y), (launches, int((got != y).sum()))
 
 
 @pytest.mark.parametrize("G", [2, 3])

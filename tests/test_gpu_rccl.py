@@ -215,9 +215,11 @@ class _CopyExchange:
 
 
 @pytest.mark.parametrize("how", ["copy", "public", "direct"])
-def test_rccl_graph_capture_exchange_diagnostic(eng, pg, mesh, how):
-    """The copy-exchange solve captured and replayed, with the exchange a device copy, the public
-    all-gather or the direct one: ranks equal to the eager solve after the replay."""
+def test_rccl_graph_capture_interleaved(eng, pg, mesh, how):
+    """An eager collective solve and a captured one (the exchange a device copy, the public all-gather
+    or the direct one) run alternately, the scores changing between rounds: ranks, keys and top-10
+    equal after every replay.  (With the runtime's graph packet capture on, the second replay ran
+    with clobbered arguments -- a garbage ctl header -- R5k-R5m; tests/conftest.py turns it off.)"""
     m, x0 = mesh
     cfg = Config(tol=0.0)
     xe, xg = x0.clone(), x0.clone()
@@ -247,6 +249,5 @@ def test_rccl_graph_capture_exchange_diagnostic(eng, pg, mesh, how):
         diff["ctl_rest"] = int((ce[48:] != cg[48:]).sum())
         diff["top"] = [int(i) for i in ie] == [int(i) for i in ig]
         report.append((shift, diff))
-        print(how, shift, diff, flush=True)
     assert torch.equal(sh.w_all, sh.send), how
     assert all(d["top"] and d["r"] == 0 and d["key"] == 0 for _, d in report), f"{how}: {report!r}"
