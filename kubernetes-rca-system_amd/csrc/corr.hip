@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
                                                   const int32_t* __restrict__ pods, float* __restrict__ phi2,
                                                   int32_t* __restrict__ over, int32_t* __restrict__ out_i,
                                                   float* __restrict__ out_v, float* __restrict__ cert, int64_t lo,
-                                                  int32_t* __restrict__ deep, int capc) {
+                                                  int32_t* __restrict__ deep, int capc, int km_extra) {
   __shared__ float wl_v[TPB / 64][32];
   __shared__ int32_t wl_i[TPB / 64][32];
   __shared__ float top_v[KM + 1];
@@ -1338,7 +1338,7 @@ __global__ __launch_bounds__(TPB) void corr_merge(const int2* __restrict__ buf, 
   const bool flat = ph > 2.f;
   const int n = cnt[gl];
   const bool overflow = n > capc;
-  const int km = k + 6 < KM ? k + 6 : KM;
+  const int km = k + km_extra < KM ? k + km_extra : KM;
   if (flat) {  // r = 0 with every partner: the lowest other indices, in order
     if (tid <= KM) {
       const int64_t q = tid < g ? tid : tid + 1;
@@ -1802,6 +1802,12 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
   return KRCA_OK;
 }
 
+// candidates the merge re-scores past the k-th: KRCA_CORR_KM_EXTRA (1 .. KM - KMAX), default 6
+inline int km_extra() {
+  const int e = krca::tuning().corr_km_extra;
+  return e >= 1 && e <= KM - KMAX ? e : 6;
+}
+
 // candidate slots used per pod: CAPC, or fewer under KRCA_CORR_CAPC (tests: overflows on purpose)
 inline int cand_cap() {
   const int c = krca::tuning().corr_capc;
@@ -1965,7 +1971,7 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
   KRCA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.phi2), 0x40400000 /* 3.0f */, (size_t)d.P, st));
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n), dim3(TPB), 0, st, (const int2*)lbuf, lcnt, phi, z32, d.P, d.T,
                      d.k, d.eps, 0, (const int32_t*)nullptr, ws.phi2, ws.over, out_idx, out_val, cert, lo, ws.deep,
-                     cand_cap());
+                     cand_cap(), km_extra());
   KRCA_LAUNCH_CHECK();
   int32_t n_over = 0;
   KRCA_HIP(hipMemcpyAsync(&n_over, ws.over, sizeof(int32_t), hipMemcpyDeviceToHost, st));
@@ -2009,7 +2015,7 @@ int stage_merge(const uint16_t* zh, const float* z32, const Dims& d, int64_t lo,
   }
   hipLaunchKernelGGL(corr_merge, dim3((unsigned)n_over), dim3(TPB), 0, st, (const int2*)lbuf, lcnt,
                      (const float*)ws.phi2, z32, d.P, d.T, d.k, d.eps, 1, (const int32_t*)(ws.over + 1), ws.phi2,
-                     ws.over, out_idx, out_val, cert, lo, ws.deep, cand_cap());
+                     ws.over, out_idx, out_val, cert, lo, ws.deep, cand_cap(), km_extra());
   KRCA_LAUNCH_CHECK();
   return deep_pass();
 }

@@ -114,6 +114,7 @@ struct Tuning {
                       // and re-reads the fp32 row only within their error bound of tau (0 = fp32 rows)
   int corr_capc;      // KRCA_CORR_CAPC: candidate slots used per pod, 64 .. krca_corr_cand_cap() (0 = all; tests
                       // make buffers overflow with fewer)
+  int corr_km_extra;  // KRCA_CORR_KM_EXTRA: candidates the merge re-scores in float64 past the k-th (1..8, default 6)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

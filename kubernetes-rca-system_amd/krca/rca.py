@@ -270,7 +270,9 @@ class Comm:
             # for good; later failures propagate.
             pg, opts = self._direct
             try:
-                pg._allgather_base(shard.w_all, shard.send, opts).wait()
+                work = pg._allgather_base(shard.w_all, shard.send, opts)
+                if work is not None:  # asyncOp = False: the group may return no work (already on our stream)
+                    work.wait()
                 self.direct_calls += 1
                 return
             except (AttributeError, TypeError, RuntimeError):

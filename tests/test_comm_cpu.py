@@ -64,6 +64,21 @@ def test_exchange_calls_allgather_base(monkeypatch):
     assert sh.w_all.tolist() == list(range(6)) * 2
 
 
+def test_exchange_accepts_no_work_object(monkeypatch):
+    """asyncOp = False: the process group may return None instead of a work object (torch 2.10's
+    all_gather_into_tensor checks for it too); that is a completed direct call, not a failure."""
+    class NoWorkPG(FakePG):
+        def _allgather_base(self, out, inp, opts):
+            super()._allgather_base(out, inp, opts)
+            return None
+    pg = NoWorkPG()
+    gathered = _patch(monkeypatch, pg)
+    c, sh = rca.Comm(2, 0), _shard()
+    c.exchange(sh)
+    c.exchange(sh)
+    assert c.direct_calls == 2 and len(pg.calls) == 2 and not gathered
+
+
 def test_exchange_falls_back_once_then_for_good(monkeypatch):
     pg = FakePG(fail=1)
     gathered = _patch(monkeypatch, pg)
