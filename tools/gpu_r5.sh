@@ -3,6 +3,7 @@
 # usage: tools/gpu_r5.sh TAG step [step ...]
 #   tests        all -m gpu tests                    tests_K      -m gpu tests matching -k K
 #   bench        bench.py default line               bench_trace  rocprofv3 stats of bench.py
+#   smoke        __graft_entry__.smoke()             bench_cpufull  the CPU baseline also over every pod
 #   rank_def     tools/ranking_ablation_c4.py (C4, 2 seeds, default failure model)
 #   rank_spread  the same on the spread failure model
 #   ppr          rocprofv3 stats of the C4 PageRank propagate   logs / tmpl  same for logs / templates
@@ -39,6 +40,7 @@ for s in "$@"; do
     testsall_*) step $s 900 python3 -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread -k "${s#testsall_}" ;;
     tests_*) step $s 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "${s#tests_}" ;;
     bench) step bench 400 python3 bench.py ;;
+    smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     graphdbg) step testsall_graphdbg 300 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" &&
               step testsall_graphdbg_nopkt 300 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" ;;
     bench_cpufull) step bench_cpufull 500 python3 bench.py --steps 3 --warmup 1 --cpu-full-mesh --no-corr ;;
