@@ -1840,7 +1840,10 @@ int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int
     hipLaunchKernelGGL(corr_amb_scatter, dim3(grid), dim3(TPB), 0, st, (const int2*)ws.amb[l], (const float*)ws.ambv[l],
                        (const unsigned long long*)(ws.amb_n + l), ws.amb_cap, ws.gcur, ws.gs);
     KRCA_LAUNCH_CHECK();
-    const unsigned gg = (unsigned)std::min<int64_t>(krca::ceil_div(d.P, RS_WAVES), 2048);
+    // KRCA_CORR_RSG_GRID caps the grouped kernel's workgroups (default 2048): a CU holding one of them
+    // (23 KB of LDS at T = 1440) still fits a main-pass tile workgroup, more do not
+    const int cap = krca::tuning().corr_rsg_grid > 0 ? krca::tuning().corr_rsg_grid : 2048;
+    const unsigned gg = (unsigned)std::min<int64_t>(krca::ceil_div(d.P, RS_WAVES), cap);
     hipLaunchKernelGGL(corr_amb_rescore_grouped, dim3(gg), dim3(TPB), lds, st, (const int32_t*)ws.goff,
                        (const int2*)ws.gs, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count,
                        zq, ws.Tq, (const float*)ws.qs, (const float*)ws.qn, (const float*)ws.nrm);

@@ -115,6 +115,7 @@ struct Tuning {
   int corr_capc;      // KRCA_CORR_CAPC: candidate slots used per pod, 64 .. krca_corr_cand_cap() (0 = all; tests
                       // make buffers overflow with fewer)
   int corr_km_extra;  // KRCA_CORR_KM_EXTRA: candidates the merge re-scores in float64 past the k-th (1..8, default 6)
+  int corr_rsg_grid;  // KRCA_CORR_RSG_GRID: workgroups of the grouped re-score (0 = 2048)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

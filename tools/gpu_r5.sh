@@ -56,6 +56,7 @@ for s in "$@"; do
     corrside_*) v=${s#corrside_}; export KRCA_CORR_SIDE=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 3 --tau 0.5; unset KRCA_CORR_SIDE ;;
     corrkm_*) v=${s#corrkm_}; export KRCA_CORR_KM_EXTRA=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 3 --tau 0.5; unset KRCA_CORR_KM_EXTRA ;;
     corrbatch_*) v=${s#corrbatch_}; export KRCA_CORR_BATCH=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 3 --tau 0.5; unset KRCA_CORR_BATCH ;;
+    corrrsg_*) v=${s#corrrsg_}; export KRCA_CORR_RSG_GRID=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 1 --tau 0.5; unset KRCA_CORR_RSG_GRID ;;
     c5) step c5 400 python3 tools/bench_stream.py ;;
     cumask) step cumask 600 python3 -u tools/cu_mask_probe.py ;;
     g8_*) step $s 700 python3 -u tools/g8_step_emulation.py --world ${s#g8_} --decoupled 1.5 --reps 5 --with-replicated --hw-queues 16 --steps 30 ;;
