@@ -57,6 +57,7 @@ for s in "$@"; do
     corrkm_*) v=${s#corrkm_}; export KRCA_CORR_KM_EXTRA=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 3 --tau 0.5; unset KRCA_CORR_KM_EXTRA ;;
     corrbatch_*) v=${s#corrbatch_}; export KRCA_CORR_BATCH=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 3 --tau 0.5; unset KRCA_CORR_BATCH ;;
     corrrsg_*) v=${s#corrrsg_}; export KRCA_CORR_RSG_GRID=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 1 --tau 0.5; unset KRCA_CORR_RSG_GRID ;;
+    pmcsq_*) t=${s#pmcsq_}; step $s 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $O/$s -o run -- python3 tools/prof_kernels.py $t --reps 1 ;;
     c5) step c5 400 python3 tools/bench_stream.py ;;
     cumask) step cumask 600 python3 -u tools/cu_mask_probe.py ;;
     g8_*) step $s 700 python3 -u tools/g8_step_emulation.py --world ${s#g8_} --decoupled 1.5 --reps 5 --with-replicated --hw-queues 16 --steps 30 ;;
