@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--prio-only", action="store_true", help="only the stream-priority pipelines")
     a = ap.parse_args()
     import torch
     from krca import native, synth
@@ -91,7 +92,7 @@ def main():
     res["scoring_alone_ms"]["all"] = timed(full, shards[0].score, a.reps)
     res["pagerank_alone_ms"]["all"] = timed(full, lambda: ppr_solve(steps[0]), a.reps)
     streams = {}
-    for name, (ca, cb) in layouts.items():
+    for name, (ca, cb) in ([] if a.prio_only else layouts.items()):
         sa, sb = masked(ca), masked(cb)
         streams[name] = (sa, sb)
         res["scoring_alone_ms"][name + "_A"] = timed(sa, shards[0].score, a.reps)
@@ -130,8 +131,17 @@ def main():
         return (time.perf_counter() - t0) / a.steps * 1e3
 
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    for rep in range(2):
+    lo_p, hi_p = torch.cuda.Stream.priority_range()  # (lowest, highest): a lower number is a higher priority
+    ph, pl = torch.cuda.Stream(priority=hi_p), torch.cuda.Stream(priority=lo_p)
+    res["priority_range"] = [lo_p, hi_p]
+    for rep in range(3):
         res["pipeline_ms_per_step"].setdefault("all_all", []).append(pipeline(s1, s2, 0))
+        res["pipeline_ms_per_step"].setdefault("prio_scoring_high", []).append(pipeline(ph, pl, 0))
+        res["pipeline_ms_per_step"].setdefault("prio_pagerank_high", []).append(pipeline(pl, ph, 0))
+        print("prio", res["pipeline_ms_per_step"]["all_all"][-1], res["pipeline_ms_per_step"]["prio_scoring_high"][-1],
+              res["pipeline_ms_per_step"]["prio_pagerank_high"][-1], flush=True)
+        if a.prio_only:
+            continue
         for name, (sa, sb) in streams.items():
             nb = len(layouts[name][1])
             res["pipeline_ms_per_step"].setdefault(name, []).append(pipeline(sa, sb, 5 * nb))

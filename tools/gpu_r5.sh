@@ -60,6 +60,7 @@ for s in "$@"; do
     pmcsq_*) t=${s#pmcsq_}; step $s 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $O/$s -o run -- python3 tools/prof_kernels.py $t --reps 1 ;;
     c5) step c5 400 python3 tools/bench_stream.py ;;
     cumask) step cumask 600 python3 -u tools/cu_mask_probe.py ;;
+    prio) step prio 600 python3 -u tools/cu_mask_probe.py --prio-only --steps 20 ;;
     g8_*) step $s 700 python3 -u tools/g8_step_emulation.py --world ${s#g8_} --decoupled 1.5 --reps 5 --with-replicated --hw-queues 16 --steps 30 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
