@@ -198,6 +198,20 @@ def test_corr_batches_and_full_lists_identical(eng):
         lib.krca_tune_set(b"KRCA_CORR_AMB_TILE", -1)
         lib.krca_tune_set(b"KRCA_CORR_RS_GROUP", 1)
         lib.krca_tune_set(b"KRCA_CORR_SIDE", 0)
+    # performance knobs that must not change a result: the grouped re-score's grid, and how many
+    # candidates past the k-th the merge re-scores (fewer: more pods take the deep merge; the
+    # certificate margins may differ, the sets, values and counts not)
+    try:
+        for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2)):
+            assert lib.krca_tune_set(knob, val) == 0
+            got = eng.corr_topk(x, k=k, tau=TAU)
+            lib.krca_tune_set(knob, 0 if knob == b"KRCA_CORR_RSG_GRID" else 6)
+            for key in ("idx", "val", "count"):
+                assert np.array_equal(got[key], ref[key]), (knob, key)
+            assert (got["cert"] > 0).all(), knob
+    finally:
+        lib.krca_tune_set(b"KRCA_CORR_RSG_GRID", 0)
+        lib.krca_tune_set(b"KRCA_CORR_KM_EXTRA", 6)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
     _, _, bad = device_check(ref, z, [rows], k)
