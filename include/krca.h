@@ -129,7 +129,8 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
 
 /* ---- a13: error-template hashing + per-container template histograms (new primitive) ------
  * template(line) = line bytes with every maximal [A-Za-z0-9_] run that contains an ASCII digit or
- * is >= 8 hex digits long replaced by "<*>"; hash = FNV-1a-64(template) (csrc/template.hip).
+ * is >= 8 hex digits long replaced by the one byte 0xFF (shown as "<*>"; never in UTF-8 text);
+ * hash = FNV-1a-64(template) (csrc/template.hip).
  * krca_template_hash: hash[l] for every line of krca_log_match.
  * krca_template_hist: per container d, the distinct hashes of its lines in ascending order and
  *   their counts, written to out_hash/out_count at the container's own line range

@@ -2,7 +2,9 @@
 //
 // New primitive (no reference code; semantics defined here and restated in oracle/oracle.py):
 //   template(line) = the line's bytes with every maximal run of [A-Za-z0-9_] that contains an
-//                    ASCII digit, or that is >= 8 characters of [0-9a-fA-F], replaced by "<*>"
+//                    ASCII digit, or that is >= 8 characters of [0-9a-fA-F], replaced by the one
+//                    byte 0xFF (shown as "<*>"; 0xFF never occurs in UTF-8 text, so a masked word
+//                    can not collide with literal text as the 3-byte "<*>" of rounds 1-4 could)
 //                    (masks counters, ids, addresses, timestamps, hashes and UUID groups;
 //                    bytes >= 0x80 are never word characters and pass through unchanged);
 //   h(line)        = FNV-1a-64 over the template bytes (offset 0xcbf29ce484222325,
@@ -40,9 +42,12 @@ __device__ __forceinline__ bool is_hex(uint32_t b) {
 // The template hash of one line in ONE pass, 4 bytes per read (`word_at(q)`: the aligned
 // little-endian dword at byte q).  FNV-1a runs through word bytes as if they stayed; the hash at the
 // word's start is kept, and a word that turns out masked (a digit, or >= 8 hex digits) is replaced
-// by "<*>" from that saved state when it ends — so a word is never re-read, and every lane runs
-// the same select-only instruction stream (no divergence inside the line).
-__device__ __forceinline__ uint64_t fnv3_mask(uint64_t h) { return fnv(fnv(fnv(h, '<'), '*'), '>'); }
+// by the mask byte from that saved state when it ends — so a word is never re-read.  The
+// replacement is one FNV step: with 64 lanes on 64 lines some lane ends a masked word at nearly
+// every byte step, so the branch runs at nearly every step for the whole wave (R5v: three steps
+// there, for "<*>", were the largest part of the kernel's vector instructions).
+constexpr uint32_t kMaskByte = 0xFFu;
+__device__ __forceinline__ uint64_t fnv_mask(uint64_t h) { return fnv(h, kMaskByte); }
 
 template <class WordAt>
 __device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& word_at) {
@@ -57,7 +62,7 @@ __device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& wor
       const bool in = (p >= s) & (p < e);
       const uint32_t b = (wv >> (8 * k)) & 0xFFu;
       const bool wc = in & is_word(b);
-      if (in & !wc & inword & (digit | (hex & (wl >= 8)))) h = fnv3_mask(hb);  // a masked word ends
+      if (in & !wc & inword & (digit | (hex & (wl >= 8)))) h = fnv_mask(hb);  // a masked word ends
       const bool start = wc & !inword;
       hb = start ? h : hb;
       h = in ? fnv(h, b) : h;
@@ -67,7 +72,7 @@ __device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& wor
       inword = in ? wc : inword;
     }
   }
-  if (inword & (digit | (hex & (wl >= 8)))) h = fnv3_mask(hb);  // a trailing masked word
+  if (inword & (digit | (hex & (wl >= 8)))) h = fnv_mask(hb);  // a trailing masked word
   return h;
 }
 
@@ -77,7 +82,7 @@ __device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& wor
 // whatever follows); 2..9 in a word of hex letters only, length 1..8 (9: >= 8, masked at its end);
 // 10 in any other word.  An entry holds the next state's row as a byte offset (state * 512) and the
 // flags START (this byte starts a word: keep the hash) and MEND (this non-word byte ends a masked
-// word: the hash becomes "<*>" from the kept state).
+// word: the hash becomes the mask byte's from the kept state).
 constexpr int TS_STATES = 11;
 constexpr uint32_t TS_ROW = 512;  // bytes per state row (256 u16 entries)
 constexpr uint32_t TS_START = 1u << 13, TS_MEND = 1u << 14, TS_OFF = (1u << 13) - 1u;
@@ -109,7 +114,7 @@ __device__ __forceinline__ uint16_t tstate_entry(int st, uint32_t b) {
 __device__ __forceinline__ void tstep(const uint8_t* __restrict__ T, uint32_t b, uint32_t& st, uint64_t& h,
                                       uint64_t& hb) {
   const uint32_t t = *reinterpret_cast<const uint16_t*>(T + st + 2 * b);
-  if (t & TS_MEND) h = fnv3_mask(hb);  // a masked word ended at the previous byte (rare)
+  if (t & TS_MEND) h = fnv_mask(hb);  // a masked word ended at the previous byte (rare)
   if (t & TS_START) hb = h;
   h = fnv(h, b);
   st = t & TS_OFF;
@@ -139,7 +144,7 @@ __device__ __forceinline__ uint64_t line_hash_tab(const uint8_t* __restrict__ sb
     const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
     for (int k = 0; k < n; ++k) tstep(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
   }
-  if (st == 1 * TS_ROW || st == 9 * TS_ROW) h = fnv3_mask(hb);  // a trailing masked word
+  if (st == 1 * TS_ROW || st == 9 * TS_ROW) h = fnv_mask(hb);  // a trailing masked word
   return h;
 }
 

@@ -84,11 +84,16 @@ _WORD = re.compile(rb"[A-Za-z0-9_]+")
 _HEX = re.compile(rb"[0-9a-fA-F]{8,}")
 
 
+TEMPLATE_MASK = b"\xff"  # the one byte a masked word becomes (never in UTF-8 text; shown as "<*>")
+
+
 def template_of(line_bytes):
+    """csrc/template.hip's template: every maximal [A-Za-z0-9_] run holding a digit, or of >= 8 hex
+    digits, replaced by TEMPLATE_MASK."""
     def sub(m):
         w = m.group(0)
         if any(48 <= c <= 57 for c in w) or _HEX.fullmatch(w):
-            return b"<*>"
+            return TEMPLATE_MASK
         return w
     return _WORD.sub(sub, line_bytes)
 

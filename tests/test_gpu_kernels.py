@@ -852,7 +852,7 @@ def test_template_hist_huge_containers(eng):
 
 
 def test_template_hash_examples(eng):
-    assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/<*>/items <*> <*>"
+    assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/\xff/items \xff \xff"
     assert oracle.template_of(b"uuid 550e8400-e29b-41d4-a716-446655440000 deadbeef") == \
-        b"uuid <*>-<*>-<*>-<*>-<*> <*>"
-    assert oracle.template_of(b"user_42 caf\xc3\xa9 OK") == b"<*> caf\xc3\xa9 OK"
+        b"uuid \xff-\xff-\xff-\xff-\xff \xff"
+    assert oracle.template_of(b"user_42 caf\xc3\xa9 OK") == b"\xff caf\xc3\xa9 OK"
