@@ -140,6 +140,29 @@ def c2mini():
     print("c2mini top10", topk_key(r, p / p.sum()).tolist(), "roots", C.ROOTS, "log lines", int(nl.sum()))
 
 
+def c2mini_templates():
+    """Rewrite only the a13 fields of c2mini.npz from oracle.template_hist (round 5: a masked word
+    became the one byte 0xFF instead of "<*>"); every other field is kept as captured."""
+    import c2mini as C
+    import oracle
+    path = os.path.join(HERE, "c2mini.npz")
+    g = dict(np.load(path))
+    e, x, blob, off = C.inputs()
+    assert C.sha(e, x, off) == str(g["sha"])
+    th, tc, td = [], [], []
+    for d in range(C.P):
+        for h, c in oracle.template_hist(blob[off[d]:off[d + 1]].decode("utf-8", "surrogatepass")):
+            th.append(h)
+            tc.append(c)
+            td.append(d)
+    g.update(tmpl_doc=np.array(td, np.int32), tmpl_hash=np.array(th, np.uint64), tmpl_count=np.array(tc, np.int32))
+    np.savez_compressed(path, **g)
+    print("c2mini templates", len(th))
+
+
 if __name__ == "__main__":
-    meshes()
-    c2mini()
+    if sys.argv[1:] == ["--templates"]:
+        c2mini_templates()
+    else:
+        meshes()
+        c2mini()
