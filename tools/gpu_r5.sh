@@ -63,6 +63,7 @@ for s in "$@"; do
     prio) step prio 600 python3 -u tools/cu_mask_probe.py --prio-only --steps 20 ;;
     scoreab_*) step $s 400 python3 -u tools/score_ab.py --pods ${s#scoreab_} --only pipe_c10,pipe_c12,pipe_c15,pipe_c20,pipe_c30,ring_buf --rounds 3 --reps 5 ;;
     g8slack_*) step $s 700 python3 -u tools/g8_step_emulation.py --world ${s#g8slack_} --decoupled 1.25,1.5,2.0 --reps 5 --hw-queues 16 --steps 30 ;;
+    g8grid_*) step $s 700 python3 -u tools/g8_step_emulation.py --world 8 --decoupled 1.5 --reps 5 --hw-queues 16 --steps 30 --grid ${s#g8grid_} ;;
     g8_*) step $s 700 python3 -u tools/g8_step_emulation.py --world ${s#g8_} --decoupled 1.5 --reps 5 --with-replicated --hw-queues 16 --steps 30 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
