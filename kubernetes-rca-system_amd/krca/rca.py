@@ -709,14 +709,13 @@ def _check_graph_runtime():
 
 
 def graph_default(comm, cfg, shard=None):
-    """Whether RcaStep captures its PageRank solve in a HIP graph: only with KRCA_RCA_GRAPH=1, for
-    fixed-iteration solves (tol <= 0: no host read-back between iterations) of a device shard.
-    Measured at C4 on one MI355X (`profiles/r3/bench_graph_ab.txt`): the replayed graph ran the
-    step 0.26 ms and the one-step latency 0.2 ms SLOWER than the eager launches -- the ~13 us per
-    iteration between the step kernels is the GPU's dependent-kernel boundary, not host time -- so
-    eager is the default."""
+    """Whether RcaStep captures its PageRank solve in a HIP graph: only with KRCA_RCA_GRAPH=1, for a
+    device shard.  Measured at C4 on one MI355X (`profiles/r3/bench_graph_ab.txt`): the replayed
+    graph ran the step 0.26 ms and the one-step latency 0.2 ms SLOWER than the eager launches -- the
+    ~13 us per iteration between the step kernels is the GPU's dependent-kernel boundary, not host
+    time -- so eager is the default."""
     import os
-    if os.environ.get("KRCA_RCA_GRAPH") != "1" or cfg.tol > 0 or not isinstance(shard, DeviceShard):
+    if os.environ.get("KRCA_RCA_GRAPH") != "1" or not isinstance(shard, DeviceShard):
         return False
     return True  # (RcaStep then checks the runtime setting: _check_graph_runtime)
 
@@ -724,11 +723,14 @@ def graph_default(comm, cfg, shard=None):
 class RcaStep:
     """One rank's view of the pod-sharded RCA step.
 
-    With `graph` (default: :func:`graph_default`, off) the whole PageRank solve (init, exchange,
-    first reduce, iters x (step, exchange, reduce)) is captured once into a HIP graph on the
-    shard's fixed buffers and replayed per step: one launch instead of ~2 host calls per iteration.
-    Replays compute exactly the eager sequence: the captured kernels and pointers are the same
-    (G = 1's ping-pong swaps are baked into the capture)."""
+    With `graph` (default: :func:`graph_default`, off) the PageRank solve of n folded steps (init,
+    exchange, n x (step, exchange), the last reduction) is captured into a HIP graph on the shard's
+    fixed buffers, once per n, and replayed: one launch instead of ~2 host calls per iteration.
+    Under the stop rule n is plan_iters() (the previous count + 1: two graphs in practice, the cap's
+    for the first solve and the converged count's); the poll of the count and settle()'s rare
+    continuation stay eager.  Replays compute exactly the eager sequence: the captured kernels and
+    pointers are the same, and G = 1's ping-pong roles after a replay are set to those the captured
+    sequence ends with."""
 
     def __init__(self, shard, comm, cfg, offset, graph=None, explain=None, part=None):
         """explain: the whole pull-CSR (an :class:`Explain` or (row_ptr, col)) for the default key;
@@ -736,11 +738,9 @@ class RcaStep:
         whose padded slices a coupled G > 1 shard's scores are gathered in (default uniform)."""
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
         self.graph = graph_default(comm, cfg, shard) if graph is None else bool(graph)
-        if self.graph and cfg.tol > 0:
-            raise ValueError("RcaStep: the HIP-graph solve needs a fixed-iteration Config (tol = 0)")
         if self.graph:
             _check_graph_runtime()
-        self._g = None
+        self._graphs = {}  # n -> (captured graph, the exchange buffers' roles after it)
         if explain is not None and not isinstance(explain, Explain):
             explain = Explain(*explain)
         self.explain = explain
@@ -759,19 +759,28 @@ class RcaStep:
         return cfg.iters
 
     def propagate(self):
-        """Seeded PageRank on the current scores: init, exchange, then iters x (step, exchange, reduce)."""
-        if self.cfg.tol > 0:
-            return self._propagate_tol()
+        """Seeded PageRank on the current scores: init, exchange, then n x (folded step, exchange)
+        and the last step's reduction; under the stop rule n = plan_iters() and a poll of the
+        iteration count is enqueued behind them (read by settle())."""
+        s, cfg = self.s, self.cfg
+        n = self.plan_iters()
         if not self.graph:
-            return self._propagate()
+            self._solve(n)
+        else:
+            self._replay(n)
+        if cfg.tol > 0:
+            self._spec = (n, s.ctl_async())
+
+    def _replay(self, n):
         import gc
 
         import torch
-        if self._g is None:
-            self._propagate()  # eager warm-up: statics, occupancy queries, workspaces
+        s = self.s
+        if n not in self._graphs:
+            self._solve(n)  # eager warm-up: statics, occupancy queries, workspaces
             g = torch.cuda.CUDAGraph()
-            cur = torch.cuda.current_stream(self.s.eng.device)
-            side = torch.cuda.Stream(self.s.eng.device)
+            cur = torch.cuda.current_stream(s.eng.device)
+            side = torch.cuda.Stream(s.eng.device)
             side.wait_stream(cur)
             # no garbage collection inside the capture: a collected cycle that holds device objects
             # (another graph, events, a communicator's work) would release them mid-capture, which
@@ -780,39 +789,28 @@ class RcaStep:
             gc.disable()
             try:
                 with torch.cuda.graph(g, stream=side):
-                    self._propagate()
+                    self._solve(n)
             finally:
                 if was:
                     gc.enable()
             cur.wait_stream(side)
-            self._g = g
-        self._g.replay()
+            self._graphs[n] = (g, (s.send, s.w_all))
+        g, roles = self._graphs[n]
+        g.replay()
+        s.send, s.w_all = roles
 
-    def _propagate(self):
-        """init, exchange, then iters x (folded step, exchange) and the last step's reduction: the
-        same results as init / reduce(first) / iters x (step, exchange, reduce), one kernel fewer
-        per iteration (krca_ppr_shard_step_folded)."""
+    def _solve(self, n):
+        """init, exchange, then n x (folded step, exchange) and the last step's reduction: the same
+        results as init / reduce(first) / n x (step, exchange, reduce), one kernel fewer per
+        iteration (krca_ppr_shard_step_folded).  Under the stop rule steps past convergence exit on
+        the device-held flag, so n may overshoot with no host poll."""
         s, c, cfg = self.s, self.comm, self.cfg
-        s.init(cfg.alpha, cfg.floor(s.N, s.M))
-        c.exchange(s)
-        for it in range(1, cfg.iters + 1):
-            s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == cfg.iters))
-            c.exchange(s)
-        s.finish(cfg.alpha, cfg.tol, cfg.iters)
-
-    def _propagate_tol(self):
-        """Under the L1 stop rule: plan_iters() folded steps with no host poll (steps past
-        convergence exit on the device-held flag), the last step's reduction, and a poll of the
-        count enqueued behind them (read by settle())."""
-        s, c, cfg = self.s, self.comm, self.cfg
-        n = self.plan_iters()
         s.init(cfg.alpha, cfg.floor(s.N, s.M))
         c.exchange(s)
         for it in range(1, n + 1):
             s.step_folded(cfg.alpha, cfg.tol, it, step_flags(cfg.tol, it == n))
             c.exchange(s)
         s.finish(cfg.alpha, cfg.tol, n)
-        self._spec = (n, s.ctl_async())
 
     def settle(self, idx, val):
         """After propagate() + local_candidates() under a tolerance: read the solve's count; if the

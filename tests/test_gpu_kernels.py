@@ -531,14 +531,17 @@ def test_rca_step_single_gpu_vs_oracle(eng, n, iters):
     assert len(set(idx.tolist()) & set(m.roots.tolist())) >= 8
 
 
-def test_rca_step_graph_replay_equals_eager(eng):
-    """RcaStep's HIP-graph solve (captured once, replayed per step) equals the eager launch
-    sequence bit for bit, also after the scores change under the captured buffers."""
+@pytest.mark.parametrize("tol", [0.0, 1e-10])
+def test_rca_step_graph_replay_equals_eager(eng, tol):
+    """RcaStep's HIP-graph solve (captured once per step count, replayed per step) equals the eager
+    launch sequence bit for bit, also after the scores change under the captured buffers; under
+    the stop rule (tol > 0) the first solve's graph has the cap's 30 steps and the later ones the
+    converged count + 1, and the iteration counts match too."""
     from krca.rca import Comm, Config, DeviceShard, RcaStep, shard_graph, shard_range
     n = 20000
     m = synth.make_graph(n, avg_degree=20, seed=5)
     hops = synth.caller_hops(m, m.roots)
-    cfg = Config(iters=30, tol=0.0)  # the graph replays a fixed-iteration solve
+    cfg = Config(iters=30, tol=tol)
     lo, hi, n_max = shard_range(n, 1, 0)
     rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, lo, hi)
     xs = [synth.make_metrics(n, 8, 300, window=60, seed=s, roots=m.roots, hop_sets=hops).cuda() for s in (1, 2)]
@@ -551,10 +554,12 @@ def test_rca_step_graph_replay_equals_eager(eng):
         for xi in xs + xs[:1]:
             x.copy_(xi)  # new metrics under the same buffers (the graph's inputs)
             idx, key = step.run()
-            out.append((list(idx), list(key), step.s.r[:n].cpu().numpy().copy()))
+            out.append((list(idx), list(key), step.s.r[:n].cpu().numpy().copy(), step.last_iters))
         res[graph] = out
-    for (ia, ka, ra), (ib, kb, rb) in zip(res[False], res[True]):
-        assert ia == ib and ka == kb and np.array_equal(ra, rb)
+        if graph and tol > 0:
+            assert len(step._graphs) >= 2, sorted(step._graphs)  # the cap's, then count + 1
+    for (ia, ka, ra, na), (ib, kb, rb, nb) in zip(res[False], res[True]):
+        assert ia == ib and ka == kb and np.array_equal(ra, rb) and na == nb
     assert np.array_equal(res[True][0][2], res[True][2][2]) and not np.array_equal(res[True][0][2], res[True][1][2])
 
 

@@ -180,11 +180,13 @@ def test_rccl_graph_capture_plain_allgather(pg, direct, producer):
     assert torch.equal(got, want), (got[:5].tolist(), want[:5].tolist())
 
 
-def test_rccl_graph_capture_with_allgather(eng, pg, mesh):
+@pytest.mark.parametrize("tol", [0.0, 1e-10])
+def test_rccl_graph_capture_with_allgather(eng, pg, mesh, tol):
     """The solve captured into a HIP graph with the RCCL all-gather inside (RcaStep graph=True),
-    replayed: the same bits as the eager collective sequence, also after the scores change."""
+    replayed: the same bits as the eager collective sequence, also after the scores change, with a
+    fixed iteration count and under the stop rule (graphs per step count)."""
     m, x0 = mesh
-    cfg = Config(tol=0.0)  # the graph replays a fixed-iteration solve
+    cfg = Config(tol=tol)
     res = {}
     for graph in (False, True):
         x = x0.clone()
