@@ -116,8 +116,12 @@ def log(*a):
 
 
 # the replicated step's measured cost over the sharded one per G (ms; DESIGN.md §5, single-GPU
-# emulations with a device copy standing in for the all-gather): the budget the sharded solve's
-# iters x (all-gather - device copy) may spend before replicating the solve is cheaper
+# emulations with a device copy standing in for the all-gather, 30-step solves): the budget the
+# sharded solve's iters x (all-gather - device copy) may spend before replicating the solve is
+# cheaper.  Both sides scale with the steps a solve runs: the 12-step emulation at G = 8 (the stop
+# rule's count + 1, profiles/r5/g8_step_emulation_R5i.json) gave 0.22 ms, the same ~18 us per
+# iteration break-even as 0.50 ms over 30 (17 us), so the rule keeps the cap (--iters) and these
+# margins.
 REPLICATED_MARGIN_MS = {2: 0.155, 4: 0.39, 8: 0.50}
 
 
@@ -127,16 +131,20 @@ def exchange_probe(world, n_slot, dev, reps=50):
     the gathered bytes (what the single-GPU emulations stood in for it).  Per call: the wall time of
     the back-to-back sequence (host dispatch included: the solve's iterations are issued the same
     way) and the HIP-event time; max over ranks."""
+    import types
+
     import torch
     import torch.distributed as dist
-    from krca.rca import all_gather_flat, slice_words
+    from krca.rca import Comm, slice_words
     words = slice_words(n_slot)
     send = torch.zeros(words, dtype=torch.int64, device=dev)
     out = torch.zeros(world * words, dtype=torch.int64, device=dev)
+    comm = Comm(world, dist.get_rank())  # the solve's own exchange (RCCL: the direct _allgather_base)
+    slot = types.SimpleNamespace(send=send, w_all=out)
     for _ in range(5):
-        all_gather_flat(out, send, world)
+        comm.exchange(slot)
     res = {}
-    for name, fn in (("allgather", lambda: all_gather_flat(out, send, world)),
+    for name, fn in (("allgather", lambda: comm.exchange(slot)),
                      ("copy", lambda: out.view(world, -1).copy_(send.expand(world, -1)))):
         torch.cuda.synchronize()
         dist.barrier()
@@ -151,6 +159,7 @@ def exchange_probe(world, n_slot, dev, reps=50):
         res[name + "_event_us"] = max_over_ranks(a.elapsed_time(b) / reps * 1e3, world)
     res["bytes_per_rank"] = words * 8
     res["reps"] = reps
+    res["direct_calls"] = comm.direct_calls
     return res
 
 
