@@ -43,6 +43,7 @@ for s in "$@"; do
     benchgraph_*) step $s 400 env KRCA_RCA_GRAPH=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python3 bench.py --no-corr --no-cpu-baseline ;;
     bencheager_*) step $s 400 python3 bench.py --no-corr --no-cpu-baseline ;;
     bench8gloo) step bench8gloo 900 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --steps 3 --warmup 1 --no-corr --no-cpu-baseline ;;
+    bench8gloobal) step bench8gloobal 900 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --steps 3 --warmup 1 --no-corr --no-cpu-baseline --ppr-partition balanced ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     graphdbg) step testsall_graphdbg 300 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" &&
               step testsall_graphdbg_nopkt 300 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" ;;
