@@ -25,6 +25,7 @@ for t in ${TARGETS:-cal ppr bench logs logs_fused}; do
     ppr) cmd=(python3 tools/ppr_bench.py --reps 2) ;;
     bench) cmd=(python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-pipeline --no-corr) ;;
     logs) cmd=(python3 tools/prof_kernels.py logs --docs 1000000 --reps 1) ;;
+    logs250k) cmd=(python3 tools/prof_kernels.py logs --docs 250000 --reps 1) ;;
     logs_fused) export KRCA_LOG_FUSED=2; cmd=(python3 tools/prof_kernels.py logs --docs 1000000 --reps 1) ;;
     corr) cmd=(python3 tools/prof_kernels.py corr --pods 100000 --reps 1) ;;
   esac
