@@ -31,7 +31,8 @@ constexpr uint64_t kFnvPrime = 0x100000001b3ull;
 
 // (the 64-bit multiply is ~10 % of tmpl_hash_kernel: a build with a multiply-free stand-in ran
 // 140.9 against 156.2 us, r4w; the per-byte state-table read, a dependent LDS chain, is the rest)
-__device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t b) { return (h ^ b) * kFnvPrime; }
+__device__ __forceinline__ uint64_t fnv_mul(uint64_t x) { return x * kFnvPrime; }
+__device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t b) { return fnv_mul(h ^ b); }
 __device__ __forceinline__ bool is_word(uint32_t b) {
   return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
 }
@@ -76,55 +77,124 @@ __device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& wor
   return h;
 }
 
-// The word-state machine of the template as a table, (state, byte) -> next state | flags, so that
+// The word-state machine of the template as a table, (state, byte) -> next state and flags, so that
 // a byte costs one LDS read and the FNV step instead of ~20 class tests and selects (round 2: ~30
 // vector instructions per byte).  States: 0 outside a word; 1 in a word holding a digit (masked
 // whatever follows); 2..9 in a word of hex letters only, length 1..8 (9: >= 8, masked at its end);
-// 10 in any other word.  An entry holds the next state's row as a byte offset (state * 512) and the
-// flags START (this byte starts a word: keep the hash) and MEND (this non-word byte ends a masked
-// word: the hash becomes the mask byte's from the kept state).
+// 10 in any other word.  Flags: START (this byte starts a word: keep the hash) and MEND (this
+// non-word byte ends a masked word: the hash becomes the mask byte's from the kept state).
 constexpr int TS_STATES = 11;
-constexpr uint32_t TS_ROW = 512;  // bytes per state row (256 u16 entries)
-constexpr uint32_t TS_START = 1u << 13, TS_MEND = 1u << 14, TS_OFF = (1u << 13) - 1u;
-static_assert((TS_STATES - 1) * TS_ROW <= TS_OFF, "row offsets must fit below the flags");
-
-__device__ __forceinline__ uint16_t tstate_entry(int st, uint32_t b) {
+struct TsNext {
+  int nx;
+  bool start, mend;
+};
+__host__ __device__ constexpr TsNext ts_next(int st, uint32_t b) {
   const bool dg = b >= '0' && b <= '9';
   const bool hl = (b >= 'a' && b <= 'f') || (b >= 'A' && b <= 'F');
   const bool wc = dg || hl || (b >= 'g' && b <= 'z') || (b >= 'G' && b <= 'Z') || b == '_';
-  int nx;
-  uint32_t fl = 0;
-  if (!wc) {
-    nx = 0;
-    if (st == 1 || st == 9) fl = TS_MEND;
-  } else if (st == 0) {
-    fl = TS_START;
-    nx = dg ? 1 : (hl ? 2 : 10);
-  } else if (st == 1) {
-    nx = 1;
-  } else if (st <= 9) {
-    nx = dg ? 1 : (hl ? (st < 9 ? st + 1 : 9) : 10);
-  } else {
-    nx = dg ? 1 : 10;
-  }
-  return (uint16_t)((uint32_t)nx * TS_ROW | fl);
+  if (!wc) return {0, false, st == 1 || st == 9};
+  if (st == 0) return {dg ? 1 : (hl ? 2 : 10), true, false};
+  if (st == 1) return {1, false, false};
+  if (st <= 9) return {dg ? 1 : (hl ? (st < 9 ? st + 1 : 9) : 10), false, false};
+  return {dg ? 1 : 10, false, false};
 }
 
-// one byte of the walk: st = the current state's row offset in bytes
-__device__ __forceinline__ void tstep(const uint8_t* __restrict__ T, uint32_t b, uint32_t& st, uint64_t& h,
-                                      uint64_t& hb) {
-  const uint32_t t = *reinterpret_cast<const uint16_t*>(T + st + 2 * b);
-  if (t & TS_MEND) h = fnv_mask(hb);  // a masked word ended at the previous byte (rare)
-  if (t & TS_START) hb = h;
+// Two table layouts, both built at compile time (a workgroup copies the image into LDS with one
+// 16-byte load per lane: filling it entry by entry from the class tests cost each wave ~550
+// instructions, a third of a 74-byte line's walk, R5zt).
+// Rows8 (the kernel's): a byte entry is the next ROW's index, rows 0..10 the states, rows 11..13
+// states 1, 2 and 10 entered by a START byte, row 14 state 0 entered by a MEND byte (each a copy
+// of its state's row): the next address (row << 8) | byte is one byte permute, START-or-MEND is
+// row >= 11 and MEND row >= 14, one compare each (3.75 KB).  Saving the hash at a MEND byte as well
+// is harmless: the saved hash is read only at the end of a masked word, and every word starts with
+// a START byte that saves it again.
+struct Rows8 {
+  static constexpr int NROWS = TS_STATES + 4;
+  static constexpr uint32_t ES = 1, ROWB = 256, BYTES = NROWS * ROWB;
+  static constexpr uint32_t entry(int row, uint32_t b) {
+    constexpr int kBase[4] = {1, 2, 10, 0};  // the state of rows 11..14
+    const TsNext n = ts_next(row < TS_STATES ? row : kBase[row - TS_STATES], b);
+    if (n.mend) return TS_STATES + 3;
+    if (n.start) return n.nx == 1 ? TS_STATES : n.nx == 2 ? TS_STATES + 1 : TS_STATES + 2;
+    return (uint32_t)n.nx;
+  }
+};
+// Packed16 (the round-4 kernel, KRCA_TMPL_IMPL=1): a 16-bit entry is the next state's row byte
+// offset | START << 14 | MEND << 15 (5.6 KB).  PROBE (profiling aids, wrong hashes): 1 the FNV
+// multiply replaced by a 64-bit rotate, 2 the table read replaced by three vector instructions,
+// 3 no walk at all (staging, sort and stores only).
+constexpr uint32_t TS_START = 1u << 14, TS_MEND = 1u << 15, TS_OFF = (1u << 14) - 1u;
+template <int PROBE_ = 0>
+struct Packed16 {
+  static constexpr int NROWS = TS_STATES, PROBE = PROBE_;
+  static constexpr uint32_t ES = 2, ROWB = 512, BYTES = NROWS * ROWB;
+  static constexpr uint32_t entry(int row, uint32_t b) {
+    const TsNext n = ts_next(row, b);
+    return (uint32_t)n.nx * ROWB | (n.start ? TS_START : 0u) | (n.mend ? TS_MEND : 0u);
+  }
+};
+
+template <class LY>
+struct TTable {
+  alignas(16) uint8_t v[LY::BYTES];
+};
+template <class LY>
+constexpr TTable<LY> make_table() {
+  TTable<LY> t{};
+  for (int r = 0; r < LY::NROWS; ++r)
+    for (uint32_t b = 0; b < 256; ++b) {
+      const uint32_t e = LY::entry(r, b), at = r * LY::ROWB + LY::ES * b;
+      t.v[at] = (uint8_t)e;
+      if (LY::ES > 1) t.v[at + 1] = (uint8_t)(e >> 8);
+    }
+  return t;
+}
+template <class LY>
+__device__ constexpr TTable<LY> kTable = make_table<LY>();
+template <class LY, int NT>
+__device__ __forceinline__ void load_table(uint8_t* __restrict__ tstate) {  // (the caller syncs)
+  static_assert(LY::BYTES % 16 == 0, "16-byte copy");
+  for (int i = threadIdx.x; i < (int)LY::BYTES / 16; i += NT)
+    reinterpret_cast<uint4*>(tstate)[i] = reinterpret_cast<const uint4*>(kTable<LY>.v)[i];
+}
+
+// Rows8: byte k of dword w; st = the current row index
+__device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32_t w, int k, uint32_t& st,
+                                           uint64_t& h, uint64_t& hb) {
+  const uint32_t b = (w >> (8 * k)) & 0xFFu;  // (only the hash's XOR reads it)
+  const uint32_t t = T[__builtin_amdgcn_perm(st, w, 0x0c0c0400u | (uint32_t)k)];  // (st << 8) | byte k
+  if (t >= TS_STATES + 3) h = fnv_mask(hb);  // a masked word ended at the previous byte
+  if (t >= TS_STATES) hb = h;                // this byte starts a word (or ended a masked one)
   h = fnv(h, b);
+  st = t;
+}
+__device__ __forceinline__ bool rows_in_masked_word(uint32_t st) { return st == 1 || st == 9 || st == TS_STATES; }
+
+// Packed16: st = the current state's row byte offset
+template <class LY>
+__device__ __forceinline__ void tstep_packed(const uint8_t* __restrict__ T, uint32_t b, uint32_t& st, uint64_t& h,
+                                             uint64_t& hb) {
+  uint32_t t;
+  if constexpr (LY::PROBE == 2) t = ((b * 0x2F3u) ^ st) & (TS_MEND | TS_START | (3u * LY::ROWB));
+  else t = *reinterpret_cast<const uint16_t*>(T + st + 2 * b);
+  if constexpr (LY::PROBE == 1) {
+    if (t & TS_MEND) h = (hb << 1) | (hb >> 63);
+    if (t & TS_START) hb = h;
+    h = ((h ^ b) << 1) | ((h ^ b) >> 63);
+  } else {
+    if (t & TS_MEND) h = fnv_mask(hb);  // a masked word ended at the previous byte (rare)
+    if (t & TS_START) hb = h;
+    h = fnv(h, b);
+  }
   st = t & TS_OFF;
 }
 
-// the template hash of the line at LDS offsets [s, e) of the staged span (the span holds 3 bytes
-// past e): the lane's bytes re-aligned to its line start (alignbyte of two aligned dwords), full
-// dwords with no per-byte range test, then the <= 3 tail bytes
-__device__ __forceinline__ uint64_t line_hash_tab(const uint8_t* __restrict__ sb, int s, int e,
-                                                  const uint8_t* __restrict__ T) {
+// Packed16: the template hash of the line at LDS offsets [s, e) of a staged span (the span holds 3
+// bytes past e): the lane's bytes re-aligned to its line start (alignbyte of two aligned dwords),
+// full dwords with no per-byte range test, then the <= 3 tail bytes
+template <class LY>
+__device__ __forceinline__ uint64_t line_hash_staged(const uint8_t* __restrict__ sb, int s, int e,
+                                                     const uint8_t* __restrict__ T) {
   uint64_t h = kFnvOff, hb = 0;
   uint32_t st = 0;
   const uint32_t sh = (uint32_t)(s & 3);
@@ -137,75 +207,39 @@ __device__ __forceinline__ uint64_t line_hash_tab(const uint8_t* __restrict__ sb
     lo = hi;
     q += 4;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) tstep(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
+    for (int k = 0; k < 4; ++k) tstep_packed<LY>(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
   }
   if (n > 0) {
     const uint32_t hi = (int)sh + n > 4 ? *reinterpret_cast<const uint32_t*>(sb + q + 4) : 0u;
     const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    for (int k = 0; k < n; ++k) tstep(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
+    for (int k = 0; k < n; ++k) tstep_packed<LY>(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
   }
-  if (st == 1 * TS_ROW || st == 9 * TS_ROW) h = fnv_mask(hb);  // a trailing masked word
+  if (st == 1 * LY::ROWB || st == 9 * LY::ROWB) h = fnv_mask(hb);  // a trailing masked word
   return h;
 }
 
-// Workgroup per 256 consecutive lines.  Lines are contiguous in the text, so the workgroup first
-// copies the bytes its lines span into LDS (16 B per lane, coalesced: every text byte crosses HBM
-// once) and every lane then hashes its line from LDS.  A lane whose line reaches past the staged
-// span (a line or a run of lines longer than SPAN bytes) reads through the global 16-byte window
-// instead.  (Round 1 read every line through that window: each window refill was a dependent
-// global load, and with 64 lanes at random phases nearly every byte step of a wave waited on one:
-// 1.63 ms for the 2.5M-line C5 window.)
-// A wave takes as long as its longest line, so the workgroup first orders its lines by length
-// (a counting sort on length / 4 in LDS) and lane t of wave w hashes the t-th line of the w-th
-// quarter: on the C5 corpus the mean of the waves' longest lines falls from 1.43x to 1.11x the
-// mean line length.
-constexpr int SPAN = 24 * 1024;  // a multiple of 16 * TPB
-constexpr int NLB = 128;          // length buckets of 4 bytes (the last one takes every longer line)
-__global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                        const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
-                                                        int64_t L, uint64_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t sbuf[SPAN];
-  __shared__ __attribute__((aligned(16))) uint8_t tstate[TS_STATES * TS_ROW];
-  __shared__ uint32_t bcnt[NLB];
-  __shared__ uint32_t span_se[TPB];  // a line's staged span offsets (start | end << 16), ~0 past the span
-  __shared__ uint8_t perm[TPB];
-  for (int i = threadIdx.x; i < TS_STATES * 256; i += TPB)
-    reinterpret_cast<uint16_t*>(tstate)[i] = tstate_entry(i >> 8, (uint32_t)(i & 255));
-  if (threadIdx.x < NLB) bcnt[threadIdx.x] = 0u;
-  const int64_t l0 = (int64_t)blockIdx.x * TPB;
-  const int64_t i = l0 + threadIdx.x;
-  const int64_t l1 = min(l0 + TPB, L);
-  const int64_t my_s = i < L ? ls[i] : 0, my_e = i < L ? le[i] : 0;
-  const int64_t a0 = ls[l0] & ~(int64_t)15;
-  const int64_t a1 = min(min(le[l1 - 1], nbytes), a0 + SPAN - 4);  // dword reads may touch 3 bytes past
-  // every staging load is issued before the first LDS write (one latency per workgroup, not one
-  // per 4 KiB); a bounds-checked buffer descriptor over [a0, nbytes) returns zeros past the text
-  constexpr int NST = SPAN / (16 * TPB);
-  const int64_t rem = nbytes - a0;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(text + a0), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
-  uint4 st[NST];
-#pragma unroll
-  for (int j = 0; j < NST; ++j) {
-    const int off = 16 * (threadIdx.x + j * TPB);
-    st[j] = off < a1 + 4 - a0 ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0))
-                              : make_uint4(0u, 0u, 0u, 0u);
-  }
-#pragma unroll
-  for (int j = 0; j < NST; ++j) {
-    const int off = 16 * (threadIdx.x + j * TPB);
-    if (off < rem && off + 16 > rem) {  // the text's last partial piece (a straddling buffer load reads as 0)
-      uint32_t ww[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (off + k < rem) ww[k >> 2] |= (uint32_t)text[a0 + off + k] << (8 * (k & 3));
-      st[j] = make_uint4(ww[0], ww[1], ww[2], ww[3]);
-    }
-    reinterpret_cast<uint4*>(sbuf)[threadIdx.x + j * TPB] = st[j];
-  }
-  // counting sort of the workgroup's lines by length / 4 (lines past L: bucket 0, skipped below)
-  const uint32_t bk = i < L ? (uint32_t)min<int64_t>((my_e - my_s) >> 2, NLB - 1) : 0u;
-  span_se[threadIdx.x] = i < L && my_e <= a1 ? (uint32_t)(my_s - a0) | ((uint32_t)(my_e - a0) << 16) : ~0u;
+// the template hash of line [s, e) read from the text itself (a line past a 2 GiB window or span)
+__device__ __forceinline__ uint64_t line_hash_global(const uint8_t* __restrict__ text, int64_t nbytes, int64_t s,
+                                                     int64_t e) {
+  return line_hash(s, e, [&](int64_t q) -> uint32_t {
+    if (q + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(text + q);
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k)
+      if (q + k < nbytes) v |= (uint32_t)text[q + k] << (8 * k);
+    return v;
+  });
+}
+
+// A workgroup's lines ordered by length: a wave takes as long as its longest line, so the lanes of
+// wave w take the w-th run of the lines sorted by length / 4 (a counting sort in LDS; lines past L
+// land in bucket 0 and are skipped by the caller).  On the C5 corpus the mean of the waves'
+// longest lines falls from 1.43x to 1.11x the mean line length at 256 lines per workgroup.
+constexpr int NLB = 128;  // length buckets of 4 bytes (the last one takes every longer line)
+template <int NT>
+__device__ __forceinline__ int sort_by_length(int64_t len, bool valid, uint32_t* __restrict__ bcnt,
+                                              uint16_t* __restrict__ perm) {
+  const uint32_t bk = valid ? (uint32_t)min<int64_t>(len >> 2, NLB - 1) : 0u;
+  for (int i = threadIdx.x; i < NLB; i += NT) bcnt[i] = 0u;
   __syncthreads();
   const uint32_t rank = atomicAdd(&bcnt[bk], 1u);  // (LDS) order inside a bucket: arrival
   __syncthreads();
@@ -223,24 +257,145 @@ __global__ __launch_bounds__(TPB) void tmpl_hash_kernel(const uint8_t* __restric
     bcnt[2 * lane + 1] = ex + c0;
   }
   __syncthreads();
-  perm[bcnt[bk] + rank] = (uint8_t)threadIdx.x;
+  perm[bcnt[bk] + rank] = (uint16_t)threadIdx.x;
   __syncthreads();
-  const int j = perm[threadIdx.x];
+  return perm[threadIdx.x];
+}
+
+// The hash kernel: a workgroup per NT consecutive lines, lane per line in length order, each lane
+// reading its line straight from the text in 16-byte buffer loads at the line's dword-aligned start,
+// one load ahead.  The workgroup holds only the table and the sort in LDS (5 KB), so a CU keeps 8
+// waves per SIMD: the walk is bound by each wave's dependent per-byte chain (table read, flag
+// tests, the hash's multiply), and the waves hide one another's.  (Round 4 staged each
+// workgroup's text span in 24 KB of LDS, which held the CU to 5 waves per SIMD: 159 against 106 us
+// for the same 2.5M lines with this kernel, R5zu; two lines per lane in lockstep, bank-spread and
+// flag-row tables at that occupancy were slower or equal, R5zj-R5zm.)
+template <int NT>
+__global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                       const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
+                                                       int64_t L, uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tstate[Rows8::BYTES];
+  __shared__ uint32_t bcnt[NLB];
+  __shared__ uint16_t perm[NT];
+  load_table<Rows8, NT>(tstate);
+  const int64_t l0 = (int64_t)blockIdx.x * NT;
+  const int64_t i = l0 + threadIdx.x;
+  const int j = sort_by_length<NT>(i < L ? le[i] - ls[i] : 0, i < L, bcnt, perm);  // (syncs: table ready)
+  const int64_t li = l0 + j;
+  if (li >= L) return;
+  const int64_t s = ls[li], e = le[li];
+  const int64_t base = ls[l0] & ~(int64_t)15;  // the workgroup's buffer window starts at its first line
+  if (e - base > (int64_t)INT32_MAX - 64) {    // (a line beyond a 2 GiB window)
+    out[li] = line_hash_global(text, nbytes, s, e);
+    return;
+  }
+  const int64_t rem = nbytes - base;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(text + base), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
+  auto load = [&](int q) -> uint4 {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, q, 0, 0));
+  };
+  // (reads past the text return 0 and are never hashed; a load straddling the text's end reads 0
+  // for all 16 bytes, so that piece is rebuilt byte by byte)
+  auto fix = [&](uint4& v, int q) {
+    if (q + 16 > rem && q < rem) {
+      uint32_t ww[4] = {0, 0, 0, 0};
+      for (int k = 0; k < 16; ++k)
+        if (q + k < rem) ww[k >> 2] |= (uint32_t)text[base + q + k] << (8 * (k & 3));
+      v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+    }
+  };
+  // the line's next 16 bytes as dwords, realigned to its start
+  auto words = [](const uint4& c, const uint4& nx, uint32_t sh, uint32_t* w) {
+    w[0] = __builtin_amdgcn_alignbyte(c.y, c.x, sh);
+    w[1] = __builtin_amdgcn_alignbyte(c.z, c.y, sh);
+    w[2] = __builtin_amdgcn_alignbyte(c.w, c.z, sh);
+    w[3] = __builtin_amdgcn_alignbyte(nx.x, c.w, sh);
+  };
+  const uint32_t sh = (uint32_t)(s & 3);
+  int q = (int)((s & ~(int64_t)3) - base);
+  int n = (int)(e - s);
+  uint64_t h = kFnvOff, hb = 0;
+  uint32_t st = 0;
+  uint4 cur = load(q), nxt = load(q + 16);
+  fix(cur, q);
+  for (; n >= 16; n -= 16) {
+    const uint4 nn = load(q + 32);
+    fix(nxt, q + 16);
+    uint32_t w[4];
+    words(cur, nxt, sh, w);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tstep_rows(tstate, w[k >> 2], k & 3, st, h, hb);
+    cur = nxt;
+    nxt = nn;
+    q += 16;
+  }
+  if (n > 0) {
+    fix(nxt, q + 16);
+    uint32_t w[4];
+    words(cur, nxt, sh, w);
+    for (int k = 0; k < n; ++k) tstep_rows(tstate, w[k >> 2], k & 3, st, h, hb);
+  }
+  if (rows_in_masked_word(st)) h = fnv_mask(hb);  // a trailing masked word
+  out[li] = h;
+}
+
+// The round-4 kernel (KRCA_TMPL_IMPL=1, and the profiling probes): a workgroup per 256 lines copies
+// the bytes its lines span into LDS (16 B per lane and load, coalesced) and every lane hashes its
+// line from there; a line reaching past the staged span is read through the text instead.
+constexpr int SPAN = 24 * 1024;  // a multiple of 16 * TPB
+template <class LY>
+__global__ __launch_bounds__(TPB) void tmpl_hash_staged(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                        const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
+                                                        int64_t L, uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[SPAN];
+  __shared__ __attribute__((aligned(16))) uint8_t tstate[LY::BYTES];
+  __shared__ uint32_t bcnt[NLB];
+  __shared__ uint32_t span_se[TPB];  // a line's staged span offsets (start | end << 16), ~0 past the span
+  __shared__ uint16_t perm[TPB];
+  load_table<LY, TPB>(tstate);
+  const int64_t l0 = (int64_t)blockIdx.x * TPB;
+  const int64_t i = l0 + threadIdx.x;
+  const int64_t l1 = min(l0 + TPB, L);
+  const int64_t my_s = i < L ? ls[i] : 0, my_e = i < L ? le[i] : 0;
+  const int64_t a0 = ls[l0] & ~(int64_t)15;
+  const int64_t a1 = min(min(le[l1 - 1], nbytes), a0 + SPAN - 4);  // dword reads may touch 3 bytes past
+  // every staging load is issued before the first LDS write (one latency per workgroup, not one
+  // per 4 KiB); a bounds-checked buffer descriptor over [a0, nbytes) returns zeros past the text
+  constexpr int NST = SPAN / (16 * TPB);
+  const int64_t rem = nbytes - a0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(text + a0), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
+  uint4 stg[NST];
+#pragma unroll
+  for (int jj = 0; jj < NST; ++jj) {
+    const int off = 16 * (threadIdx.x + jj * TPB);
+    stg[jj] = off < a1 + 4 - a0 ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0))
+                                : make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (int jj = 0; jj < NST; ++jj) {
+    const int off = 16 * (threadIdx.x + jj * TPB);
+    if (off < rem && off + 16 > rem) {  // the text's last partial piece (a straddling buffer load reads as 0)
+      uint32_t ww[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (off + k < rem) ww[k >> 2] |= (uint32_t)text[a0 + off + k] << (8 * (k & 3));
+      stg[jj] = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+    }
+    reinterpret_cast<uint4*>(sbuf)[threadIdx.x + jj * TPB] = stg[jj];
+  }
+  span_se[threadIdx.x] = i < L && my_e <= a1 ? (uint32_t)(my_s - a0) | ((uint32_t)(my_e - a0) << 16) : ~0u;
+  const int j = sort_by_length<TPB>(my_e - my_s, i < L, bcnt, perm);  // (syncs: span, table ready)
   const int64_t li = l0 + j;
   if (li >= L) return;
   const uint32_t se = span_se[j];
-  if (se != ~0u) {
-    out[li] = line_hash_tab(sbuf, (int)(se & 0xFFFFu), (int)(se >> 16), tstate);
-  } else {  // past the staged span: aligned dwords from the text (the last one may be partial)
-    const int64_t s = ls[li], e = le[li];
-    out[li] = line_hash(s, e, [&](int64_t q) -> uint32_t {
-      if (q + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(text + q);
-      uint32_t v = 0;
-      for (int k = 0; k < 4; ++k)
-        if (q + k < nbytes) v |= (uint32_t)text[q + k] << (8 * k);
-      return v;
-    });
+  if constexpr (LY::PROBE == 3) {
+    out[li] = se;
+    return;
   }
+  out[li] = se != ~0u ? line_hash_staged<LY>(sbuf, (int)(se & 0xFFFFu), (int)(se >> 16), tstate)
+                      : line_hash_global(text, nbytes, ls[li], le[li]);
 }
 
 // ---- per-container histograms ----------------------------------------------------------------
@@ -609,8 +764,19 @@ int krca_template_hash(const uint8_t* text, int64_t nbytes, const int64_t* line_
   if (n_lines == 0) return KRCA_OK;
   KRCA_CHECK_ARG(text && line_start && line_end && hash, "krca_template_hash: null pointer");
   KRCA_CHECK_ARG(((uintptr_t)text & 15) == 0, "krca_template_hash: text must be 16-byte aligned");
-  hipLaunchKernelGGL(tmpl_hash_kernel, dim3((unsigned)krca::ceil_div(n_lines, TPB)), dim3(TPB), 0,
-                     krca::as_stream(stream), text, nbytes, line_start, line_end, n_lines, hash);
+  const hipStream_t st = krca::as_stream(stream);
+  const int impl = krca::tuning().tmpl_impl;
+  if (impl == 0) {
+    hipLaunchKernelGGL(tmpl_hash_kernel<512>, dim3((unsigned)krca::ceil_div(n_lines, 512)), dim3(512), 0, st, text,
+                       nbytes, line_start, line_end, n_lines, hash);
+  } else {
+    const auto k = impl == 101   ? tmpl_hash_staged<Packed16<1>>
+                   : impl == 102 ? tmpl_hash_staged<Packed16<2>>
+                   : impl == 103 ? tmpl_hash_staged<Packed16<3>>
+                                 : tmpl_hash_staged<Packed16<0>>;
+    hipLaunchKernelGGL(k, dim3((unsigned)krca::ceil_div(n_lines, TPB)), dim3(TPB), 0, st, text, nbytes, line_start,
+                       line_end, n_lines, hash);
+  }
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

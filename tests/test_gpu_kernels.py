@@ -800,7 +800,16 @@ def test_stream_cold_solve_fresh_streams_bit_identical(eng):
 
 
 # ---- a13 error templates -------------------------------------------------------------------
-def test_template_hist_vs_oracle(eng):
+@pytest.fixture(params=[0, 1], ids=["direct", "staged"])
+def tmpl_impl(eng, request):
+    """The template-hash kernels (KRCA_TMPL_IMPL): lines read straight from the text (default), and
+    the round-4 kernel that stages each workgroup's text in LDS; both must give the oracle's hashes."""
+    assert eng.lib.krca_tune_set(b"KRCA_TMPL_IMPL", request.param) == 0
+    yield request.param
+    eng.lib.krca_tune_set(b"KRCA_TMPL_IMPL", 0)
+
+
+def test_template_hist_vs_oracle(eng, tmpl_impl):
     import json
     import os
     from conftest import GOLDEN
@@ -823,7 +832,7 @@ def test_template_hist_vs_oracle(eng):
         assert got[d] == oracle.template_hist(text), d
 
 
-def test_template_hist_fragment_fuzz(eng):
+def test_template_hist_fragment_fuzz(eng, tmpl_impl):
     """Words, digit runs and hex runs cut at random points and scattered over lines and containers
     (no trailing separator, so a word's halves meet at container ends; 8-hex-digit runs split and
     joined; underscores, UTF-8 and the multi-byte separators beside them): every container's

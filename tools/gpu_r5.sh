@@ -54,6 +54,7 @@ for s in "$@"; do
     ppr) prof ppr 300 tools/ppr_bench.py --reps 10 ;;
     logs) prof logs 300 tools/prof_kernels.py logs --reps 5 ;;
     tmpl) prof tmpl 300 tools/prof_kernels.py tmpl --reps 5 ;;
+    tmplimpl_*) export KRCA_TMPL_IMPL=${s#tmplimpl_}; prof $s 300 tools/prof_kernels.py tmpl --reps 5; unset KRCA_TMPL_IMPL ;;
     corr100k) prof corr100k 400 tools/prof_kernels.py corr --pods 100000 --reps 3 ;;
     corr1m) prof corr1m 600 tools/prof_kernels.py corr --pods 1000000 --reps 1 ;;
     corrdbg_*) v=${s#corrdbg_}; export KRCA_CORR_DEBUG=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${P:-1000000} --reps 1 --tau ${v##*_}; unset KRCA_CORR_DEBUG ;;
