@@ -330,11 +330,18 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
     nxt = nn;
     q += 16;
   }
-  if (n > 0) {
+  if (n > 0) {  // the last 1..15 bytes: whole dwords with static byte positions, then 1..3 bytes
     fix(nxt, q + 16);
     uint32_t w[4];
     words(cur, nxt, sh, w);
-    for (int k = 0; k < n; ++k) tstep_rows(tstate, w[k >> 2], k & 3, st, h, hb);
+    for (; n >= 4; n -= 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tstep_rows(tstate, w[0], k, st, h, hb);
+      w[0] = w[1];
+      w[1] = w[2];
+      w[2] = w[3];
+    }
+    for (int k = 0; k < n; ++k) tstep_rows(tstate, w[0], k, st, h, hb);
   }
   if (rows_in_masked_word(st)) h = fnv_mask(hb);  // a trailing masked word
   out[li] = h;
