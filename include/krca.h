@@ -134,8 +134,9 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
  * krca_template_hash: hash[l] for every line of krca_log_match.
  * krca_template_hist: per container d, the distinct hashes of its lines in ascending order and
  *   their counts, written to out_hash/out_count at the container's own line range
- *   [doc_line0[d], doc_line0[d] + n_templates[d]); the slots past n_templates[d] are NOT written
- *   (krca.native zero-fills out_hash / out_count first, so its outputs hold 0 there).  Sort-based.  Containers of <= 8 lines are sorted
+ *   [doc_line0[d], doc_line0[d] + n_templates[d]), then 0 in the slots up to doc_line0[d] + doc_lines[d]
+ *   (every slot of the line range is written; those of containers above krca_template_max_lines()
+ *   by krca_template_hist_huge).  Sort-based.  Containers of <= 8 lines are sorted
  *   in one lane's registers, <= 64 by a wave, <= krca_template_max_lines() by a workgroup, all on
  *   device lists (no host round trip).  workspace: krca_template_hist_ws_size(ndocs) bytes, int32
  *   {mid, big, huge counts, 0 | mid list [D] | big list [D] | huge list [D]}: containers above

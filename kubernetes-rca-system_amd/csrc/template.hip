@@ -466,6 +466,12 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_lane(const uint64_t* __restrict
       }
     }
   }
+#pragma unroll
+  for (int j = 1; j < LANE_MAX; ++j)  // the slots past the templates (every slot is written: no fill)
+    if (j >= k && j < n) {
+      out_hash[lo + j] = 0ull;
+      out_cnt[lo + j] = 0;
+    }
   n_tmpl[d] = k;
 }
 
@@ -505,6 +511,10 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_small(const uint64_t* __restric
     const int idx = __popcll(heads & ((1ull << lane) - 1ull));
     out_hash[lo + idx] = v;
     out_cnt[lo + idx] = next - lane;
+  }
+  if (lane >= __popcll(heads) && lane < n) {  // the slots past the templates
+    out_hash[lo + lane] = 0ull;
+    out_cnt[lo + lane] = 0;
   }
   if (lane == 0) n_tmpl[d] = __popcll(heads);
   }
@@ -570,6 +580,10 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_big(const uint64_t* __restrict_
     const int next = r + 1 < carry ? pos[r + 1] : n;
     out_hash[lo + r] = key[i];
     out_cnt[lo + r] = next - i;
+  }
+  for (int r = carry + threadIdx.x; r < n; r += TPB) {  // the slots past the templates
+    out_hash[lo + r] = 0ull;
+    out_cnt[lo + r] = 0;
   }
   if (threadIdx.x == 0) n_tmpl[d] = carry;
   }
@@ -824,6 +838,10 @@ int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspa
   const HugeLayout L(n_lines);
   char* ws = static_cast<char*>(workspace);
   hipStream_t st = krca::as_stream(stream);
+  // the container's slots zeroed first; the distinct templates then fill the front (every slot of
+  // the line range is written, as by krca_template_hist)
+  KRCA_HIP(hipMemsetAsync(out_hash, 0, (size_t)n_lines * sizeof(uint64_t), st));
+  KRCA_HIP(hipMemsetAsync(out_count, 0, (size_t)n_lines * sizeof(int32_t), st));
   const unsigned g_cap = (unsigned)std::min<int64_t>(krca::ceil_div(L.cap, TPB), 8192);
   hipLaunchKernelGGL(huge_init, dim3(g_cap), dim3(TPB), 0, st, ws, n_lines);
   KRCA_LAUNCH_CHECK();

@@ -533,11 +533,12 @@ class NativeEngine:
         L = scan["n_lines_total"]
         D = scan["doc_lines"].numel()
         h = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
-        # container d's histogram fills tmpl_*[doc_line0[d] : doc_line0[d] + n_templates[d]]; the
-        # slots past it (a container with repeated templates has fewer templates than lines) are
-        # zero-filled here (one 12 B-per-line memset), so no output slot is left undefined
-        oh = torch.zeros(max(L, 1), dtype=torch.int64, device=self.device)
-        oc = torch.zeros(max(L, 1), dtype=torch.int32, device=self.device)
+        # container d's histogram fills tmpl_*[doc_line0[d] : doc_line0[d] + n_templates[d]] and the
+        # kernels write 0 in the slots past it up to its last line (a container with repeated
+        # templates has fewer templates than lines), so no output slot is left undefined
+        # without a 12 B-per-line memset first
+        oh = torch.empty(max(L, 1), dtype=torch.int64, device=self.device)
+        oc = torch.empty(max(L, 1), dtype=torch.int32, device=self.device)
         nt = torch.zeros(D, dtype=torch.int32, device=self.device)
         _check(self.lib.krca_template_hash(self.ptr(scan["text"]), scan["text"].numel(), self.ptr(scan["line_start"]),
                                            self.ptr(scan["line_end"]), L, self.ptr(h), self._stream()),

@@ -865,6 +865,35 @@ def test_template_hist_huge_containers(eng):
         assert got[d] == oracle.template_hist(text), d
 
 
+def test_template_hist_writes_every_slot(eng):
+    """krca_template_hist (+ _huge) write every slot of each container's line range: its templates,
+    then 0 (include/krca.h) -- checked on outputs pre-filled with a poison pattern, for containers
+    on the lane (<= 8 lines), wave (<= 64), workgroup (<= 4096) and huge paths, repeated templates."""
+    docs = ["a 1\na 2\nb", "x\n" * 5 + "y", "\n".join("t %d" % (i % 3) for i in range(50)),
+            "\n".join("u %s" % ("k" * (i % 7)) for i in range(3000)), "\n".join("v" for _ in range(5000)), "", "z"]
+    blob, off = pack_documents(docs)
+    scan = eng.log_scan_device(eng.upload_blob(blob), torch.from_numpy(off).cuda())
+    ref = eng.template_hist_device(scan)  # (zero-initialised n_templates; huge containers completed)
+    L = scan["n_lines_total"]
+    oh = torch.full((L,), -0x5A5A5A5A5A5A5A5B, dtype=torch.int64, device="cuda")
+    oc = torch.full((L,), -0x5A5A5A5B, dtype=torch.int32, device="cuda")
+    nt = torch.zeros(len(docs), dtype=torch.int32, device="cuda")
+    out = dict(ref)
+    out.update(tmpl_hash=oh, tmpl_count=oc, n_templates=nt)
+    ws = eng._workspace("tmpl_hist_t", eng.lib.krca_template_hist_ws_size(len(docs))).view(torch.int32)
+    assert eng.lib.krca_template_hist(eng.ptr(ref["hash"]), eng.ptr(scan["doc_lines"]), eng.ptr(scan["doc_line0"]),
+                                      len(docs), eng.ptr(ws), eng.ptr(oh), eng.ptr(oc), eng.ptr(nt), eng._stream()) == 0
+    eng._template_huge(ws, ref["hash"], oh, oc, nt, scan)
+    torch.cuda.synchronize()
+    assert int(ws[2].item()) == 1  # one container on the huge path
+    assert torch.equal(oh, ref["tmpl_hash"]) and torch.equal(oc, ref["tmpl_count"]) and torch.equal(nt, ref["n_templates"])
+    d0, dl, n = scan["doc_line0"].cpu().numpy(), scan["doc_lines"].cpu().numpy(), nt.cpu().numpy()
+    ohn, ocn = oh.cpu().numpy(), oc.cpu().numpy()
+    for d in range(len(docs)):
+        assert (ohn[d0[d] + n[d]:d0[d] + dl[d]] == 0).all() and (ocn[d0[d] + n[d]:d0[d] + dl[d]] == 0).all(), d
+        assert (ocn[d0[d]:d0[d] + n[d]] > 0).all(), d
+
+
 def test_template_hash_examples(eng):
     assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/\xff/items \xff \xff"
     assert oracle.template_of(b"uuid 550e8400-e29b-41d4-a716-446655440000 deadbeef") == \

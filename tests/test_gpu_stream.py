@@ -165,7 +165,7 @@ def test_stream_window_log_overlap_and_error_path(eng):
             assert len(bad_) == 0, (i, k, g_.shape, w_.shape, bad_[:5].tolist(), g_[bad_[:5]].tolist(),
                                     w_[bad_[:5]].tolist())
         # template slots: container d's histogram is tmpl_*[doc_line0[d] : doc_line0[d] + n_templates[d]]
-        # and every slot past it is zero (template_hist_device zero-fills the arrays), so the two
+        # and every slot past it is zero (the histogram kernels write them), so the two
         # streams agree on EVERY slot.  (Round 4 briefly compared only the valid slots: the arrays
         # were allocated uninitialised and the primed stream's tails held the prime text's hashes --
         # calls r4d / r4f / r4g.)
