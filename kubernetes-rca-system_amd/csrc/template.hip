@@ -158,14 +158,26 @@ __device__ __forceinline__ void load_table(uint8_t* __restrict__ tstate) {  // (
     reinterpret_cast<uint4*>(tstate)[i] = reinterpret_cast<const uint4*>(kTable<LY>.v)[i];
 }
 
+// h ^ byte k of w in one instruction (the byte read in place as a sub-dword operand; the compiler
+// otherwise shifts bytes 1 and 2 down first)
+__device__ __forceinline__ uint64_t xor_byte(uint64_t h, uint32_t w, int k) {
+  uint32_t lo = (uint32_t)h;
+  switch (k) {
+    case 0: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(lo) : "v"(lo), "v"(w)); break;
+    case 1: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(lo) : "v"(lo), "v"(w)); break;
+    case 2: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(lo) : "v"(lo), "v"(w)); break;
+    default: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(lo) : "v"(lo), "v"(w)); break;
+  }
+  return (h & 0xFFFFFFFF00000000ull) | lo;
+}
+
 // Rows8: byte k of dword w; st = the current row index
 __device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32_t w, int k, uint32_t& st,
                                            uint64_t& h, uint64_t& hb) {
-  const uint32_t b = (w >> (8 * k)) & 0xFFu;  // (only the hash's XOR reads it)
   const uint32_t t = T[__builtin_amdgcn_perm(st, w, 0x0c0c0400u | (uint32_t)k)];  // (st << 8) | byte k
   if (t >= TS_STATES + 3) h = fnv_mask(hb);  // a masked word ended at the previous byte
   if (t >= TS_STATES) hb = h;                // this byte starts a word (or ended a masked one)
-  h = fnv(h, b);
+  h = fnv_mul(xor_byte(h, w, k));
   st = t;
 }
 __device__ __forceinline__ bool rows_in_masked_word(uint32_t st) { return st == 1 || st == 9 || st == TS_STATES; }
