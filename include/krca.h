@@ -131,7 +131,9 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
  * template(line) = line bytes with every maximal [A-Za-z0-9_] run that contains an ASCII digit or
  * is >= 8 hex digits long replaced by the one byte 0xFF (shown as "<*>"; never in UTF-8 text);
  * hash = FNV-1a-64(template) (csrc/template.hip).
- * krca_template_hash: hash[l] for every line of krca_log_match.
+ * krca_template_hash: hash[l] for every line [line_start[l], line_end[l]) (krca_log_match's lines;
+ *   fastest when the starts ascend, as there: a workgroup reads its lines through one window from
+ *   its first line's start; lines outside that window are read directly, same hash).
  * krca_template_hist: per container d, the distinct hashes of its lines in ascending order and
  *   their counts, written to out_hash/out_count at the container's own line range
  *   [doc_line0[d], doc_line0[d] + n_templates[d]), then 0 in the slots up to doc_line0[d] + doc_lines[d]

@@ -250,7 +250,7 @@ constexpr int NLB = 128;  // length buckets of 4 bytes (the last one takes every
 template <int NT>
 __device__ __forceinline__ int sort_by_length(int64_t len, bool valid, uint32_t* __restrict__ bcnt,
                                               uint16_t* __restrict__ perm) {
-  const uint32_t bk = valid ? (uint32_t)min<int64_t>(len >> 2, NLB - 1) : 0u;
+  const uint32_t bk = valid && len > 0 ? (uint32_t)min<int64_t>(len >> 2, NLB - 1) : 0u;
   for (int i = threadIdx.x; i < NLB; i += NT) bcnt[i] = 0u;
   __syncthreads();
   const uint32_t rank = atomicAdd(&bcnt[bk], 1u);  // (LDS) order inside a bucket: arrival
@@ -297,7 +297,8 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
   if (li >= L) return;
   const int64_t s = ls[li], e = le[li];
   const int64_t base = ls[l0] & ~(int64_t)15;  // the workgroup's buffer window starts at its first line
-  if (e - base > (int64_t)INT32_MAX - 64) {    // (a line beyond a 2 GiB window)
+  // (a line beyond a 2 GiB window, or before the window: lines not in text order)
+  if (s < base || e - base > (int64_t)INT32_MAX - 64) {
     out[li] = line_hash_global(text, nbytes, s, e);
     return;
   }
@@ -404,7 +405,8 @@ __global__ __launch_bounds__(TPB) void tmpl_hash_staged(const uint8_t* __restric
     }
     reinterpret_cast<uint4*>(sbuf)[threadIdx.x + jj * TPB] = stg[jj];
   }
-  span_se[threadIdx.x] = i < L && my_e <= a1 ? (uint32_t)(my_s - a0) | ((uint32_t)(my_e - a0) << 16) : ~0u;
+  span_se[threadIdx.x] = i < L && my_s >= a0 && my_e <= a1 && my_s <= my_e
+                            ? (uint32_t)(my_s - a0) | ((uint32_t)(my_e - a0) << 16) : ~0u;
   const int j = sort_by_length<TPB>(my_e - my_s, i < L, bcnt, perm);  // (syncs: span, table ready)
   const int64_t li = l0 + j;
   if (li >= L) return;

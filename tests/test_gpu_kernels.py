@@ -894,6 +894,41 @@ def test_template_hist_writes_every_slot(eng):
         assert (ocn[d0[d]:d0[d] + n[d]] > 0).all(), d
 
 
+@pytest.mark.parametrize("impl", [0, 1])
+def test_template_hash_any_line_order(eng, impl):
+    """krca_template_hash on the scan's lines in a shuffled order, with some lines repeated and a few
+    empty or reversed ranges: every hash equals the in-order hash of the same range (a workgroup's
+    window starts at its first line; lines outside it are read directly)."""
+    docs = synth.make_log_corpus(3000, lines_per_doc=3, seed=5, hazard_rate=0.05)
+    docs.append("z" * 40000 + " 12 " + "q" * 30000)  # a line longer than any staged span
+    blob, off = pack_documents(docs)
+    scan = eng.log_scan_device(eng.upload_blob(blob), torch.from_numpy(off).cuda())
+    L = scan["n_lines_total"]
+    ls, le = scan["line_start"][:L].clone(), scan["line_end"][:L].clone()
+    text = scan["text"]
+
+    def run(s_, e_):
+        out = torch.empty(s_.numel(), dtype=torch.int64, device="cuda")
+        assert eng.lib.krca_template_hash(eng.ptr(text), text.numel(), eng.ptr(s_), eng.ptr(e_), s_.numel(),
+                                          eng.ptr(out), eng._stream()) == 0
+        return out
+
+    with native.tune(eng.lib, KRCA_TMPL_IMPL=impl):
+        ref = run(ls, le).cpu().numpy()
+        rng = np.random.default_rng(3)
+        perm = rng.permutation(L)
+        perm = np.concatenate([perm, perm[:500]])  # repeated lines
+        s2, e2 = ls[torch.from_numpy(perm).cuda()].contiguous(), le[torch.from_numpy(perm).cuda()].contiguous()
+        got = run(s2, e2).cpu().numpy()
+        assert np.array_equal(got, ref[perm])
+        # empty and reversed ranges hash as the empty template
+        e3 = e2.clone()
+        e3[::7] = s2[::7] - 5
+        got = run(s2, e3).cpu().numpy()
+        empty = np.array([0xcbf29ce484222325], dtype=np.uint64).view(np.int64)[0]  # FNV-1a offset basis
+        assert (got[::7] == empty).all() and np.array_equal(got[1::7], ref[perm][1::7])
+
+
 def test_template_hash_examples(eng):
     assert oracle.template_of(b"GET /api/v1/items 200 15ms") == b"GET /api/\xff/items \xff \xff"
     assert oracle.template_of(b"uuid 550e8400-e29b-41d4-a716-446655440000 deadbeef") == \
