@@ -288,20 +288,17 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
                                                        int64_t L, uint64_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t tstate[Rows8::BYTES];
   __shared__ uint32_t bcnt[NLB];
-  __shared__ uint16_t perm[NT];
+  __shared__ __attribute__((aligned(8))) uint16_t perm[4 * NT];  // (then the hashes, NT x 8 B)
   load_table<Rows8, NT>(tstate);
   const int64_t l0 = (int64_t)blockIdx.x * NT;
   const int64_t i = l0 + threadIdx.x;
   const int j = sort_by_length<NT>(i < L ? le[i] - ls[i] : 0, i < L, bcnt, perm);  // (syncs: table ready)
   const int64_t li = l0 + j;
-  if (li >= L) return;
-  const int64_t s = ls[li], e = le[li];
+  const int64_t s = li < L ? ls[li] : 0, e = li < L ? le[li] : 0;
   const int64_t base = ls[l0] & ~(int64_t)15;  // the workgroup's buffer window starts at its first line
-  // (a line beyond a 2 GiB window, or before the window: lines not in text order)
-  if (s < base || e - base > (int64_t)INT32_MAX - 64) {
-    out[li] = line_hash_global(text, nbytes, s, e);
-    return;
-  }
+  // lines in the window are walked here; a line beyond a 2 GiB window, or before the window (lines
+  // not in text order), is read directly after the walk (every lane reaches the barriers below)
+  const bool direct = s >= base && e - base <= (int64_t)INT32_MAX - 64;
   const int64_t rem = nbytes - base;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(text + base), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
@@ -326,8 +323,8 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
     w[3] = __builtin_amdgcn_alignbyte(nx.x, c.w, sh);
   };
   const uint32_t sh = (uint32_t)(s & 3);
-  int q = (int)((s & ~(int64_t)3) - base);
-  int n = (int)(e - s);
+  int q = direct ? (int)((s & ~(int64_t)3) - base) : 0;
+  int n = direct ? (int)(e - s) : 0;
   uint64_t h = kFnvOff, hb = 0;
   uint32_t st = 0;
   uint4 cur = load(q), nxt = load(q + 16);
@@ -357,7 +354,14 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
     for (int k = 0; k < n; ++k) tstep_rows(tstate, w[0], k, st, h, hb);
   }
   if (rows_in_masked_word(st)) h = fnv_mask(hb);  // a trailing masked word
-  out[li] = h;
+  if (!direct) h = line_hash_global(text, nbytes, s, e);
+  // the hashes leave through LDS in line order (full-line stores; one 8-byte store per lane at its
+  // sorted line's slot wrote 41 MB at the DRAM side for 20 MB, R5zzi: 103.0 -> 100.9 us, R5zzj)
+  uint64_t* sh_out = reinterpret_cast<uint64_t*>(perm);  // (perm is dead once every lane has read j)
+  __syncthreads();
+  if (li < L) sh_out[j] = h;
+  __syncthreads();
+  if (l0 + threadIdx.x < L) out[l0 + threadIdx.x] = sh_out[threadIdx.x];
 }
 
 // The round-4 kernel (KRCA_TMPL_IMPL=1, and the profiling probes): a workgroup per 256 lines copies

@@ -28,6 +28,7 @@ for t in ${TARGETS:-cal ppr bench logs logs_fused}; do
     logs250k) cmd=(python3 tools/prof_kernels.py logs --docs 250000 --reps 1) ;;
     logs_fused) export KRCA_LOG_FUSED=2; cmd=(python3 tools/prof_kernels.py logs --docs 1000000 --reps 1) ;;
     corr) cmd=(python3 tools/prof_kernels.py corr --pods 100000 --reps 1) ;;
+    tmpl) cmd=(python3 tools/prof_kernels.py tmpl --docs 1000000 --reps 1) ;;
   esac
   [ $t = corr ] && pass ${t}_l2 TCC_HIT_sum TCC_MISS_sum -- "${cmd[@]}"
   pass ${t}_rd TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum -- "${cmd[@]}"
