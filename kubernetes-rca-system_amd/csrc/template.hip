@@ -446,23 +446,52 @@ __device__ __forceinline__ void wave_append(bool take, int32_t d, int32_t* cnt, 
   if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = d;
 }
 
+// A workgroup's 256 containers hold consecutive line ranges (the log scan's layout): their hashes
+// are staged in LDS with coalesced loads and the results leave the same way (per-lane 8-byte loads
+// and stores at each container's own slots otherwise: a wave's 16 store instructions each touched
+// ~10 cache lines).  Slots of the larger containers in the span are written here too (their raw
+// hashes) and rewritten by the kernels that take them.  A workgroup whose ranges are not
+// consecutive, or whose span exceeds HCAP lines, takes the per-lane path.
+constexpr int HCAP = 1024;
 __global__ __launch_bounds__(TPB) void tmpl_hist_lane(const uint64_t* __restrict__ hash,
                                                       const int32_t* __restrict__ doc_lines,
                                                       const int64_t* __restrict__ doc_line0, int64_t D,
                                                       uint64_t* __restrict__ out_hash, int32_t* __restrict__ out_cnt,
                                                       int32_t* __restrict__ n_tmpl, int32_t* __restrict__ ws) {
-  const int64_t d = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  __shared__ uint64_t s_key[HCAP];
+  __shared__ int32_t s_cn[HCAP];
+  __shared__ int64_t s_lo[TPB + 1];
+  const int64_t d0 = (int64_t)blockIdx.x * TPB;
+  const int64_t d = d0 + threadIdx.x;
+  const int nv = (int)(D - d0 < TPB ? D - d0 : TPB);
   const int n = d < D ? doc_lines[d] : 0;
   int32_t* cnt = ws;
   int32_t* lists = ws + 4;
   wave_append(d < D && n > LANE_MAX && n <= MID_MAX, (int32_t)d, cnt + 0, lists);
   wave_append(d < D && n > MID_MAX && n <= BIG, (int32_t)d, cnt + 1, lists + D);
   wave_append(d < D && n > BIG, (int32_t)d, cnt + 2, lists + 2 * D);
-  if (d >= D || n > LANE_MAX) return;
-  const int64_t lo = doc_line0[d];
+  const int64_t lo = d < D ? doc_line0[d] : 0;
+  s_lo[threadIdx.x] = lo;
+  if ((int)threadIdx.x == nv - 1) s_lo[TPB] = lo + n;  // the span's end
+  __syncthreads();
+  const int64_t s0 = s_lo[0], s1 = s_lo[TPB];
+  const bool next_ok = d >= D || n < 0 || lo + n == ((int)threadIdx.x + 1 < nv ? s_lo[threadIdx.x + 1] : s1);
+  const bool staged = __syncthreads_and(next_ok && (d >= D || n >= 0)) && s1 >= s0 && s1 - s0 <= HCAP;
+  const int span = staged ? (int)(s1 - s0) : 0;
   uint64_t v[LANE_MAX];
+  const bool mine = d < D && n <= LANE_MAX;
+  if (staged) {
+    for (int i = threadIdx.x; i < span; i += TPB) {
+      s_key[i] = hash[s0 + i];
+      s_cn[i] = 0;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < LANE_MAX; ++j) v[j] = j < n ? hash[lo + j] : ~0ull;
+    for (int j = 0; j < LANE_MAX; ++j) v[j] = mine && j < n ? s_key[lo - s0 + j] : ~0ull;
+  } else {
+#pragma unroll
+    for (int j = 0; j < LANE_MAX; ++j) v[j] = mine && j < n ? hash[lo + j] : ~0ull;
+  }
 #pragma unroll
   for (int r = 0; r < LANE_MAX; ++r)
 #pragma unroll
@@ -471,26 +500,37 @@ __global__ __launch_bounds__(TPB) void tmpl_hist_lane(const uint64_t* __restrict
       v[j] = a < b ? a : b;
       v[j + 1] = a < b ? b : a;
     }
-  int k = 0, run = 0;
+  uint64_t* oh = staged ? s_key + (lo - s0) : out_hash + lo;  // (this lane's own slots)
+  int32_t* oc = staged ? s_cn + (lo - s0) : out_cnt + lo;
+  if (mine) {
+    int k = 0, run = 0;
 #pragma unroll
-  for (int j = 0; j < LANE_MAX; ++j) {  // runs of equal keys among the first n
-    if (j < n) {
-      ++run;
-      if (j + 1 == n || v[j + 1] != v[j]) {
-        out_hash[lo + k] = v[j];
-        out_cnt[lo + k] = run;
-        ++k;
-        run = 0;
+    for (int j = 0; j < LANE_MAX; ++j) {  // runs of equal keys among the first n
+      if (j < n) {
+        ++run;
+        if (j + 1 == n || v[j + 1] != v[j]) {
+          oh[k] = v[j];
+          oc[k] = run;
+          ++k;
+          run = 0;
+        }
       }
     }
-  }
 #pragma unroll
-  for (int j = 1; j < LANE_MAX; ++j)  // the slots past the templates (every slot is written: no fill)
-    if (j >= k && j < n) {
-      out_hash[lo + j] = 0ull;
-      out_cnt[lo + j] = 0;
+    for (int j = 1; j < LANE_MAX; ++j)  // the slots past the templates (every slot is written: no fill)
+      if (j >= k && j < n) {
+        oh[j] = 0ull;
+        oc[j] = 0;
+      }
+    n_tmpl[d] = k;
+  }
+  if (staged) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < span; i += TPB) {
+      out_hash[s0 + i] = s_key[i];
+      out_cnt[s0 + i] = s_cn[i];
     }
-  n_tmpl[d] = k;
+  }
 }
 
 // persistent waves over the mid list (LANE_MAX < lines <= 64): a wave per container, bitonic sort
