@@ -12,9 +12,10 @@
 //   sample pass        every pod against the first NSB*128 pods and against its own 256-pod
 //                      block (its likely group): phi[p] = (k-th best sampled |r|) - 2 eps, a lower
 //                      bound every member of p's exact top-k clears on the screening product.
-//   main pass          MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation) over the UPPER triangle
-//                      of 256x256 tiles only (P(P+1)/2 pairs, the algorithmic flop count), in an
-//                      XCD-aware super-tile order, LDS double-buffered.  Epilogue straight from the
+//   main pass          MFMA (v_mfma_f32_16x16x32_f16, fp32 accumulation) over the UPPER triangle
+//                      of 256x256 tiles only (P(P+1)/2 pairs, the algorithmic flop count), one
+//                      512-thread workgroup per tile (8 waves x 128x64), in an XCD-aware
+//                      super-tile order, LDS double-buffered.  Epilogue straight from the
 //                      accumulators: a value above phi of its row pod (column pod) is appended to
 //                      that pod's candidate buffer (one atomic slot reservation per hit; hits are
 //                      sparse by construction of phi); |r| > tau counts via LDS, one global add per
@@ -52,9 +53,9 @@
 
 namespace {
 
-constexpr int TPB = 256;
-constexpr int BM = 128;   // tile rows == cols
-constexpr int BK = 64;    // K step (time samples)
+constexpr int TPB = 256;  // threads of the auxiliary kernels (the tile kernels: Geo<TC>::NTH = 512)
+constexpr int BM = 128;   // half of a 256-pod tile: the sample pass's list granularity
+constexpr int BK = 64;    // K step (time samples); zh rows are padded to a multiple of it
 constexpr int SUPER = 8;  // super-tile edge (tiles) of the XCD-aware order
 constexpr int KM = 24;    // candidates re-scored per pod in the merge (>= k + 6)
 constexpr int KMAX = 16;  // largest k served

@@ -116,8 +116,6 @@ struct Tuning {
                       // make buffers overflow with fewer)
   int corr_km_extra;  // KRCA_CORR_KM_EXTRA: candidates the merge re-scores in float64 past the k-th (1..8, default 6)
   int corr_rsg_grid;  // KRCA_CORR_RSG_GRID: workgroups of the grouped re-score (0 = 2048)
-  int tmpl_impl;      // KRCA_TMPL_IMPL: template hash, 0 lines read from the text at 8 waves per SIMD, 1 the round-4
-                      // kernel (each workgroup's text staged in LDS; 101..103 its profiling probes, wrong hashes)
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

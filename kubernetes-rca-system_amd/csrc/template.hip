@@ -1,23 +1,27 @@
 // Error-template hashing and per-container template histograms.
 //
 // New primitive (no reference code; semantics defined here and restated in oracle/oracle.py):
-//   template(line) = the line's bytes with every maximal run of [A-Za-z0-9_] that contains an
-//                    ASCII digit, or that is >= 8 characters of [0-9a-fA-F], replaced by the one
-//                    byte 0xFF (shown as "<*>"; 0xFF never occurs in UTF-8 text, so a masked word
-//                    can not collide with literal text as the 3-byte "<*>" of rounds 1-4 could)
-//                    (masks counters, ids, addresses, timestamps, hashes and UUID groups;
+//   template(line) = the line's bytes with every UUID (five words of 8, 4, 4, 4 and 12 hex
+//                    characters joined by single '-') and every other maximal run of [A-Za-z0-9_]
+//                    that contains an ASCII digit, or that is >= 8 characters of [0-9a-fA-F],
+//                    replaced by the one byte 0xFF (shown as "<*>"; 0xFF never occurs in UTF-8
+//                    text, so a masked word can not collide with literal text as the 3-byte "<*>" of
+//                    rounds 1-4 could) (masks counters, ids, addresses, timestamps, hashes and UUIDs;
 //                    bytes >= 0x80 are never word characters and pass through unchanged);
 //   h(line)        = FNV-1a-64 over the template bytes (offset 0xcbf29ce484222325,
 //                    prime 0x100000001b3);
 //   per container  = the distinct h of its lines in ascending order with their line counts.
+//   The word machine is csrc/tmpl_dfa.h (a byte-indexed table built at compile time; round 6 added
+//   the UUID rule: rounds 1-5 masked only the groups holding a digit or 8+ hex characters).
 //
-// krca_template_hash: one lane per line (lines from krca_log_match), the workgroup's span of text
-//   staged in LDS (coalesced, once); word bytes are hashed once the word's fate is known (the word
-//   is re-read from LDS).
+// krca_template_hash: one lane per line (lines from krca_log_match), each lane reading its line
+//   straight from the text; FNV-1a runs through word bytes as if they stayed, and a word (or UUID)
+//   that turns out masked is replaced by the mask byte from the hash saved at its start.
 // krca_template_hist: sort-based, atomics-free.  Containers with <= 64 lines: one wave, bitonic
 //   sort of 64-bit keys across lanes (shuffles), run heads by ballot, counts by ballot distance.
 //   <= 4096 lines: one workgroup, bitonic sort in LDS, run compaction by a block scan.
 #include "krca_common.h"
+#include "tmpl_dfa.h"
 
 #include <algorithm>
 #include <climits>
@@ -33,129 +37,24 @@ constexpr uint64_t kFnvPrime = 0x100000001b3ull;
 // 140.9 against 156.2 us, r4w; the per-byte state-table read, a dependent LDS chain, is the rest)
 __device__ __forceinline__ uint64_t fnv_mul(uint64_t x) { return x * kFnvPrime; }
 __device__ __forceinline__ uint64_t fnv(uint64_t h, uint32_t b) { return fnv_mul(h ^ b); }
-__device__ __forceinline__ bool is_word(uint32_t b) {
-  return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
-}
-__device__ __forceinline__ bool is_hex(uint32_t b) {
-  return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'F') || (b >= 'a' && b <= 'f');
-}
 
-// The template hash of one line in ONE pass, 4 bytes per read (`word_at(q)`: the aligned
-// little-endian dword at byte q).  FNV-1a runs through word bytes as if they stayed; the hash at the
-// word's start is kept, and a word that turns out masked (a digit, or >= 8 hex digits) is replaced
-// by the mask byte from that saved state when it ends — so a word is never re-read.  The
-// replacement is one FNV step: with 64 lanes on 64 lines some lane ends a masked word at nearly
-// every byte step, so the branch runs at nearly every step for the whole wave (R5v: three steps
-// there, for "<*>", were the largest part of the kernel's vector instructions).
+// A masked word (or UUID) becomes ONE mask byte: one FNV step from the hash saved at its start
+// (with 64 lanes on 64 lines some lane ends a masked word at nearly every byte step, so this branch
+// runs at nearly every step for the whole wave; R5v: three steps there, for "<*>", were the largest
+// part of the kernel's vector instructions).
 constexpr uint32_t kMaskByte = 0xFFu;
 __device__ __forceinline__ uint64_t fnv_mask(uint64_t h) { return fnv(h, kMaskByte); }
 
-template <class WordAt>
-__device__ __forceinline__ uint64_t line_hash(int64_t s, int64_t e, WordAt&& word_at) {
-  uint64_t h = kFnvOff, hb = 0;
-  bool inword = false, digit = false, hex = true;
-  int wl = 0;
-  for (int64_t q = s & ~(int64_t)3; q < e; q += 4) {
-    const uint32_t wv = word_at(q);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // straight-line selects; only the rare masked-word end branches
-      const int64_t p = q + k;
-      const bool in = (p >= s) & (p < e);
-      const uint32_t b = (wv >> (8 * k)) & 0xFFu;
-      const bool wc = in & is_word(b);
-      if (in & !wc & inword & (digit | (hex & (wl >= 8)))) h = fnv_mask(hb);  // a masked word ends
-      const bool start = wc & !inword;
-      hb = start ? h : hb;
-      h = in ? fnv(h, b) : h;
-      digit = (digit & !start) | (wc & (b >= '0') & (b <= '9'));
-      hex = wc ? ((hex | start) & is_hex(b)) : hex;
-      wl = start ? 1 : (wc ? wl + 1 : wl);
-      inword = in ? wc : inword;
-    }
-  }
-  if (inword & (digit | (hex & (wl >= 8)))) h = fnv_mask(hb);  // a trailing masked word
-  return h;
-}
-
-// The word-state machine of the template as a table, (state, byte) -> next state and flags, so that
-// a byte costs one LDS read and the FNV step instead of ~20 class tests and selects (round 2: ~30
-// vector instructions per byte).  States: 0 outside a word; 1 in a word holding a digit (masked
-// whatever follows); 2..9 in a word of hex letters only, length 1..8 (9: >= 8, masked at its end);
-// 10 in any other word.  Flags: START (this byte starts a word: keep the hash) and MEND (this
-// non-word byte ends a masked word: the hash becomes the mask byte's from the kept state).
-constexpr int TS_STATES = 11;
-struct TsNext {
-  int nx;
-  bool start, mend;
-};
-__host__ __device__ constexpr TsNext ts_next(int st, uint32_t b) {
-  const bool dg = b >= '0' && b <= '9';
-  const bool hl = (b >= 'a' && b <= 'f') || (b >= 'A' && b <= 'F');
-  const bool wc = dg || hl || (b >= 'g' && b <= 'z') || (b >= 'G' && b <= 'Z') || b == '_';
-  if (!wc) return {0, false, st == 1 || st == 9};
-  if (st == 0) return {dg ? 1 : (hl ? 2 : 10), true, false};
-  if (st == 1) return {1, false, false};
-  if (st <= 9) return {dg ? 1 : (hl ? (st < 9 ? st + 1 : 9) : 10), false, false};
-  return {dg ? 1 : 10, false, false};
-}
-
-// Two table layouts, both built at compile time (a workgroup copies the image into LDS with one
-// 16-byte load per lane: filling it entry by entry from the class tests cost each wave ~550
-// instructions, a third of a 74-byte line's walk, R5zt).
-// Rows8 (the kernel's): a byte entry is the next ROW's index, rows 0..10 the states, rows 11..13
-// states 1, 2 and 10 entered by a START byte, row 14 state 0 entered by a MEND byte (each a copy
-// of its state's row): the next address (row << 8) | byte is one byte permute, START-or-MEND is
-// row >= 11 and MEND row >= 14, one compare each (3.75 KB).  Saving the hash at a MEND byte as well
-// is harmless: the saved hash is read only at the end of a masked word, and every word starts with
-// a START byte that saves it again.
-struct Rows8 {
-  static constexpr int NROWS = TS_STATES + 4;
-  static constexpr uint32_t ES = 1, ROWB = 256, BYTES = NROWS * ROWB;
-  static constexpr uint32_t entry(int row, uint32_t b) {
-    constexpr int kBase[4] = {1, 2, 10, 0};  // the state of rows 11..14
-    const TsNext n = ts_next(row < TS_STATES ? row : kBase[row - TS_STATES], b);
-    if (n.mend) return TS_STATES + 3;
-    if (n.start) return n.nx == 1 ? TS_STATES : n.nx == 2 ? TS_STATES + 1 : TS_STATES + 2;
-    return (uint32_t)n.nx;
-  }
-};
-// Packed16 (the round-4 kernel, KRCA_TMPL_IMPL=1): a 16-bit entry is the next state's row byte
-// offset | START << 14 | MEND << 15 (5.6 KB).  PROBE (profiling aids, wrong hashes): 1 the FNV
-// multiply replaced by a 64-bit rotate, 2 the table read replaced by three vector instructions,
-// 3 no walk at all (staging, sort and stores only).
-constexpr uint32_t TS_START = 1u << 14, TS_MEND = 1u << 15, TS_OFF = (1u << 14) - 1u;
-template <int PROBE_ = 0>
-struct Packed16 {
-  static constexpr int NROWS = TS_STATES, PROBE = PROBE_;
-  static constexpr uint32_t ES = 2, ROWB = 512, BYTES = NROWS * ROWB;
-  static constexpr uint32_t entry(int row, uint32_t b) {
-    const TsNext n = ts_next(row, b);
-    return (uint32_t)n.nx * ROWB | (n.start ? TS_START : 0u) | (n.mend ? TS_MEND : 0u);
-  }
-};
-
-template <class LY>
-struct TTable {
-  alignas(16) uint8_t v[LY::BYTES];
-};
-template <class LY>
-constexpr TTable<LY> make_table() {
-  TTable<LY> t{};
-  for (int r = 0; r < LY::NROWS; ++r)
-    for (uint32_t b = 0; b < 256; ++b) {
-      const uint32_t e = LY::entry(r, b), at = r * LY::ROWB + LY::ES * b;
-      t.v[at] = (uint8_t)e;
-      if (LY::ES > 1) t.v[at + 1] = (uint8_t)(e >> 8);
-    }
-  return t;
-}
-template <class LY>
-__device__ constexpr TTable<LY> kTable = make_table<LY>();
-template <class LY, int NT>
+// The table image (tmpl_dfa.h: kRows x 256 one-byte entries = the next row's index, flags encoded
+// in the row ranges), built at compile time; a workgroup copies it into LDS with 16-byte loads
+// (filling it entry by entry from class tests cost each wave ~550 instructions, R5zt).
+__device__ constexpr tdfa::Table kTable = tdfa::make_table();
+constexpr int kTableBytes = tdfa::kRows * 256;
+static_assert(kTableBytes % 16 == 0, "16-byte copy");
+template <int NT>
 __device__ __forceinline__ void load_table(uint8_t* __restrict__ tstate) {  // (the caller syncs)
-  static_assert(LY::BYTES % 16 == 0, "16-byte copy");
-  for (int i = threadIdx.x; i < (int)LY::BYTES / 16; i += NT)
-    reinterpret_cast<uint4*>(tstate)[i] = reinterpret_cast<const uint4*>(kTable<LY>.v)[i];
+  for (int i = threadIdx.x; i < kTableBytes / 16; i += NT)
+    reinterpret_cast<uint4*>(tstate)[i] = reinterpret_cast<const uint4*>(kTable.v)[i];
 }
 
 // h ^ byte k of w in one instruction (the byte read in place as a sub-dword operand; the compiler
@@ -171,75 +70,52 @@ __device__ __forceinline__ uint64_t xor_byte(uint64_t h, uint32_t w, int k) {
   return (h & 0xFFFFFFFF00000000ull) | lo;
 }
 
-// Rows8: byte k of dword w; st = the current row index
+// the flags of entering row t (tmpl_dfa.h): MEND rows end a masked word (the common case); the U
+// rows (a UUID's first group ended / a whole UUID ended) sit past them behind a second, rarely taken
+// test; then START (and every flagged row: harmless, a word's start saves it again) keeps the hash
+__device__ __forceinline__ void tflags(uint32_t t, uint64_t& h, uint64_t& hb, uint64_t& hu) {
+  if (t >= (uint32_t)tdfa::kM0) {
+    if (t >= (uint32_t)tdfa::kU0) {
+      const uint64_t src = t == (uint32_t)tdfa::kU0 ? hb : hu;
+      if (t == (uint32_t)tdfa::kU0) hu = hb;
+      h = fnv_mask(src);
+    } else {
+      h = fnv_mask(hb);
+    }
+  }
+  if (t >= (uint32_t)tdfa::kS0) hb = h;
+}
+
+// byte k of dword w; st = the current row index
 __device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32_t w, int k, uint32_t& st,
-                                           uint64_t& h, uint64_t& hb) {
+                                           uint64_t& h, uint64_t& hb, uint64_t& hu) {
   const uint32_t t = T[__builtin_amdgcn_perm(st, w, 0x0c0c0400u | (uint32_t)k)];  // (st << 8) | byte k
-  if (t >= TS_STATES + 3) h = fnv_mask(hb);  // a masked word ended at the previous byte
-  if (t >= TS_STATES) hb = h;                // this byte starts a word (or ended a masked one)
+  tflags(t, h, hb, hu);
   h = fnv_mul(xor_byte(h, w, k));
   st = t;
 }
-__device__ __forceinline__ bool rows_in_masked_word(uint32_t st) { return st == 1 || st == 9 || st == TS_STATES; }
-
-// Packed16: st = the current state's row byte offset
-template <class LY>
-__device__ __forceinline__ void tstep_packed(const uint8_t* __restrict__ T, uint32_t b, uint32_t& st, uint64_t& h,
-                                             uint64_t& hb) {
-  uint32_t t;
-  if constexpr (LY::PROBE == 2) t = ((b * 0x2F3u) ^ st) & (TS_MEND | TS_START | (3u * LY::ROWB));
-  else t = *reinterpret_cast<const uint16_t*>(T + st + 2 * b);
-  if constexpr (LY::PROBE == 1) {
-    if (t & TS_MEND) h = (hb << 1) | (hb >> 63);
-    if (t & TS_START) hb = h;
-    h = ((h ^ b) << 1) | ((h ^ b) >> 63);
-  } else {
-    if (t & TS_MEND) h = fnv_mask(hb);  // a masked word ended at the previous byte (rare)
-    if (t & TS_START) hb = h;
-    h = fnv(h, b);
-  }
-  st = t & TS_OFF;
+// the end of a line: the flags of the transition on a non-word byte, without hashing it
+__device__ __forceinline__ void tstep_end(const uint8_t* __restrict__ T, uint32_t st, uint64_t& h, uint64_t& hb,
+                                          uint64_t& hu) {
+  tflags(T[(st << 8) | tdfa::kEndByte], h, hb, hu);
 }
 
-// Packed16: the template hash of the line at LDS offsets [s, e) of a staged span (the span holds 3
-// bytes past e): the lane's bytes re-aligned to its line start (alignbyte of two aligned dwords),
-// full dwords with no per-byte range test, then the <= 3 tail bytes
-template <class LY>
-__device__ __forceinline__ uint64_t line_hash_staged(const uint8_t* __restrict__ sb, int s, int e,
-                                                     const uint8_t* __restrict__ T) {
-  uint64_t h = kFnvOff, hb = 0;
-  uint32_t st = 0;
-  const uint32_t sh = (uint32_t)(s & 3);
-  int q = s & ~3;
-  uint32_t lo = *reinterpret_cast<const uint32_t*>(sb + q);
-  int n = e - s;
-  for (; n >= 4; n -= 4) {
-    const uint32_t hi = *reinterpret_cast<const uint32_t*>(sb + q + 4);
-    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    lo = hi;
-    q += 4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tstep_packed<LY>(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
-  }
-  if (n > 0) {
-    const uint32_t hi = (int)sh + n > 4 ? *reinterpret_cast<const uint32_t*>(sb + q + 4) : 0u;
-    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    for (int k = 0; k < n; ++k) tstep_packed<LY>(T, (w >> (8 * k)) & 0xFFu, st, h, hb);
-  }
-  if (st == 1 * LY::ROWB || st == 9 * LY::ROWB) h = fnv_mask(hb);  // a trailing masked word
-  return h;
-}
-
-// the template hash of line [s, e) read from the text itself (a line past a 2 GiB window or span)
+// the template hash of line [s, e) read byte by byte from the text, the table from global memory
+// (a line outside its workgroup's 2 GiB buffer window, or before it: lines not in text order)
 __device__ __forceinline__ uint64_t line_hash_global(const uint8_t* __restrict__ text, int64_t nbytes, int64_t s,
                                                      int64_t e) {
-  return line_hash(s, e, [&](int64_t q) -> uint32_t {
-    if (q + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(text + q);
-    uint32_t v = 0;
-    for (int k = 0; k < 4; ++k)
-      if (q + k < nbytes) v |= (uint32_t)text[q + k] << (8 * k);
-    return v;
-  });
+  uint64_t h = kFnvOff, hb = 0, hu = 0;
+  uint32_t st = 0;
+  e = e < nbytes ? e : nbytes;
+  for (int64_t q = s; q < e; ++q) {
+    const uint32_t b = text[q];
+    const uint32_t t = kTable.v[(st << 8) | b];
+    tflags(t, h, hb, hu);
+    h = fnv(h, b);
+    st = t;
+  }
+  tstep_end(kTable.v, st, h, hb, hu);
+  return h;
 }
 
 // A workgroup's lines ordered by length: a wave takes as long as its longest line, so the lanes of
@@ -276,20 +152,21 @@ __device__ __forceinline__ int sort_by_length(int64_t len, bool valid, uint32_t*
 
 // The hash kernel: a workgroup per NT consecutive lines, lane per line in length order, each lane
 // reading its line straight from the text in 16-byte buffer loads at the line's dword-aligned start,
-// one load ahead.  The workgroup holds only the table and the sort in LDS (5 KB), so a CU keeps 8
-// waves per SIMD: the walk is bound by each wave's dependent per-byte chain (table read, flag
+// one load ahead.  The workgroup holds the table (25.5 KB) and the sort in LDS; at 512 lanes per
+// workgroup the wave cap (4 workgroups, 8 waves per SIMD) binds before the LDS does, so the CU keeps
+// 8 waves per SIMD: the walk is bound by each wave's dependent per-byte chain (table read, flag
 // tests, the hash's multiply), and the waves hide one another's.  (Round 4 staged each
-// workgroup's text span in 24 KB of LDS, which held the CU to 5 waves per SIMD: 159 against 106 us
-// for the same 2.5M lines with this kernel, R5zu; two lines per lane in lockstep, bank-spread and
+// workgroup's text span in 24 KB of LDS at 256 lanes, which held the CU to 5 waves per SIMD: 159
+// against 106 us for the same 2.5M lines, R5zu; two lines per lane in lockstep, bank-spread and
 // flag-row tables at that occupancy were slower or equal, R5zj-R5zm.)
 template <int NT>
 __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict__ text, int64_t nbytes,
                                                        const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
                                                        int64_t L, uint64_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t tstate[Rows8::BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t tstate[kTableBytes];
   __shared__ uint32_t bcnt[NLB];
   __shared__ __attribute__((aligned(8))) uint16_t perm[4 * NT];  // (then the hashes, NT x 8 B)
-  load_table<Rows8, NT>(tstate);
+  load_table<NT>(tstate);
   const int64_t l0 = (int64_t)blockIdx.x * NT;
   const int64_t i = l0 + threadIdx.x;
   const int j = sort_by_length<NT>(i < L ? le[i] - ls[i] : 0, i < L, bcnt, perm);  // (syncs: table ready)
@@ -298,7 +175,7 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
   const int64_t base = ls[l0] & ~(int64_t)15;  // the workgroup's buffer window starts at its first line
   // lines in the window are walked here; a line beyond a 2 GiB window, or before the window (lines
   // not in text order), is read directly after the walk (every lane reaches the barriers below)
-  const bool direct = s >= base && e - base <= (int64_t)INT32_MAX - 64;
+  const bool in_window = s >= base && e - base <= (int64_t)INT32_MAX - 64;
   const int64_t rem = nbytes - base;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(text + base), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
@@ -323,9 +200,9 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
     w[3] = __builtin_amdgcn_alignbyte(nx.x, c.w, sh);
   };
   const uint32_t sh = (uint32_t)(s & 3);
-  int q = direct ? (int)((s & ~(int64_t)3) - base) : 0;
-  int n = direct ? (int)(e - s) : 0;
-  uint64_t h = kFnvOff, hb = 0;
+  int q = in_window ? (int)((s & ~(int64_t)3) - base) : 0;
+  int n = in_window ? (int)(e - s) : 0;
+  uint64_t h = kFnvOff, hb = 0, hu = 0;
   uint32_t st = 0;
   uint4 cur = load(q), nxt = load(q + 16);
   fix(cur, q);
@@ -335,7 +212,7 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
     uint32_t w[4];
     words(cur, nxt, sh, w);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) tstep_rows(tstate, w[k >> 2], k & 3, st, h, hb);
+    for (int k = 0; k < 16; ++k) tstep_rows(tstate, w[k >> 2], k & 3, st, h, hb, hu);
     cur = nxt;
     nxt = nn;
     q += 16;
@@ -346,15 +223,15 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
     words(cur, nxt, sh, w);
     for (; n >= 4; n -= 4) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) tstep_rows(tstate, w[0], k, st, h, hb);
+      for (int k = 0; k < 4; ++k) tstep_rows(tstate, w[0], k, st, h, hb, hu);
       w[0] = w[1];
       w[1] = w[2];
       w[2] = w[3];
     }
-    for (int k = 0; k < n; ++k) tstep_rows(tstate, w[0], k, st, h, hb);
+    for (int k = 0; k < n; ++k) tstep_rows(tstate, w[0], k, st, h, hb, hu);
   }
-  if (rows_in_masked_word(st)) h = fnv_mask(hb);  // a trailing masked word
-  if (!direct) h = line_hash_global(text, nbytes, s, e);
+  tstep_end(tstate, st, h, hb, hu);  // a trailing masked word or UUID
+  if (!in_window) h = line_hash_global(text, nbytes, s, e);
   // the hashes leave through LDS in line order (full-line stores; one 8-byte store per lane at its
   // sorted line's slot wrote 41 MB at the DRAM side for 20 MB, R5zzi: 103.0 -> 100.9 us, R5zzj)
   uint64_t* sh_out = reinterpret_cast<uint64_t*>(perm);  // (perm is dead once every lane has read j)
@@ -362,65 +239,6 @@ __global__ __launch_bounds__(NT) void tmpl_hash_kernel(const uint8_t* __restrict
   if (li < L) sh_out[j] = h;
   __syncthreads();
   if (l0 + threadIdx.x < L) out[l0 + threadIdx.x] = sh_out[threadIdx.x];
-}
-
-// The round-4 kernel (KRCA_TMPL_IMPL=1, and the profiling probes): a workgroup per 256 lines copies
-// the bytes its lines span into LDS (16 B per lane and load, coalesced) and every lane hashes its
-// line from there; a line reaching past the staged span is read through the text instead.
-constexpr int SPAN = 24 * 1024;  // a multiple of 16 * TPB
-template <class LY>
-__global__ __launch_bounds__(TPB) void tmpl_hash_staged(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                        const int64_t* __restrict__ ls, const int64_t* __restrict__ le,
-                                                        int64_t L, uint64_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t sbuf[SPAN];
-  __shared__ __attribute__((aligned(16))) uint8_t tstate[LY::BYTES];
-  __shared__ uint32_t bcnt[NLB];
-  __shared__ uint32_t span_se[TPB];  // a line's staged span offsets (start | end << 16), ~0 past the span
-  __shared__ uint16_t perm[TPB];
-  load_table<LY, TPB>(tstate);
-  const int64_t l0 = (int64_t)blockIdx.x * TPB;
-  const int64_t i = l0 + threadIdx.x;
-  const int64_t l1 = min(l0 + TPB, L);
-  const int64_t my_s = i < L ? ls[i] : 0, my_e = i < L ? le[i] : 0;
-  const int64_t a0 = ls[l0] & ~(int64_t)15;
-  const int64_t a1 = min(min(le[l1 - 1], nbytes), a0 + SPAN - 4);  // dword reads may touch 3 bytes past
-  // every staging load is issued before the first LDS write (one latency per workgroup, not one
-  // per 4 KiB); a bounds-checked buffer descriptor over [a0, nbytes) returns zeros past the text
-  constexpr int NST = SPAN / (16 * TPB);
-  const int64_t rem = nbytes - a0;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(text + a0), 0, (int)(rem < (int64_t)INT32_MAX ? rem : (int64_t)INT32_MAX), 0x00020000);
-  uint4 stg[NST];
-#pragma unroll
-  for (int jj = 0; jj < NST; ++jj) {
-    const int off = 16 * (threadIdx.x + jj * TPB);
-    stg[jj] = off < a1 + 4 - a0 ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0))
-                                : make_uint4(0u, 0u, 0u, 0u);
-  }
-#pragma unroll
-  for (int jj = 0; jj < NST; ++jj) {
-    const int off = 16 * (threadIdx.x + jj * TPB);
-    if (off < rem && off + 16 > rem) {  // the text's last partial piece (a straddling buffer load reads as 0)
-      uint32_t ww[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (off + k < rem) ww[k >> 2] |= (uint32_t)text[a0 + off + k] << (8 * (k & 3));
-      stg[jj] = make_uint4(ww[0], ww[1], ww[2], ww[3]);
-    }
-    reinterpret_cast<uint4*>(sbuf)[threadIdx.x + jj * TPB] = stg[jj];
-  }
-  span_se[threadIdx.x] = i < L && my_s >= a0 && my_e <= a1 && my_s <= my_e
-                            ? (uint32_t)(my_s - a0) | ((uint32_t)(my_e - a0) << 16) : ~0u;
-  const int j = sort_by_length<TPB>(my_e - my_s, i < L, bcnt, perm);  // (syncs: span, table ready)
-  const int64_t li = l0 + j;
-  if (li >= L) return;
-  const uint32_t se = span_se[j];
-  if constexpr (LY::PROBE == 3) {
-    out[li] = se;
-    return;
-  }
-  out[li] = se != ~0u ? line_hash_staged<LY>(sbuf, (int)(se & 0xFFFFu), (int)(se >> 16), tstate)
-                      : line_hash_global(text, nbytes, ls[li], le[li]);
 }
 
 // ---- per-container histograms ----------------------------------------------------------------
@@ -844,18 +662,8 @@ int krca_template_hash(const uint8_t* text, int64_t nbytes, const int64_t* line_
   KRCA_CHECK_ARG(text && line_start && line_end && hash, "krca_template_hash: null pointer");
   KRCA_CHECK_ARG(((uintptr_t)text & 15) == 0, "krca_template_hash: text must be 16-byte aligned");
   const hipStream_t st = krca::as_stream(stream);
-  const int impl = krca::tuning().tmpl_impl;
-  if (impl == 0) {
-    hipLaunchKernelGGL(tmpl_hash_kernel<512>, dim3((unsigned)krca::ceil_div(n_lines, 512)), dim3(512), 0, st, text,
-                       nbytes, line_start, line_end, n_lines, hash);
-  } else {
-    const auto k = impl == 101   ? tmpl_hash_staged<Packed16<1>>
-                   : impl == 102 ? tmpl_hash_staged<Packed16<2>>
-                   : impl == 103 ? tmpl_hash_staged<Packed16<3>>
-                                 : tmpl_hash_staged<Packed16<0>>;
-    hipLaunchKernelGGL(k, dim3((unsigned)krca::ceil_div(n_lines, TPB)), dim3(TPB), 0, st, text, nbytes, line_start,
-                       line_end, n_lines, hash);
-  }
+  hipLaunchKernelGGL(tmpl_hash_kernel<512>, dim3((unsigned)krca::ceil_div(n_lines, 512)), dim3(512), 0, st, text,
+                     nbytes, line_start, line_end, n_lines, hash);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }

@@ -119,6 +119,32 @@ def make_graph(n_pods, avg_degree=20, service_size=20, seed=0, n_roots=10, m_ser
     return Mesh(n_pods, row_ptr, col, outdeg, roots)
 
 
+def chain_roots(mesh, n_chains=5, seed=0):
+    """The held-out failure model (nothing in the ranking was tuned on it): two
+    faults in one call chain.  For each of `n_chains` downstream roots B (well-called pods of
+    distinct services, as make_graph picks its roots), one of B's callers A that has callers of its
+    own is a root too: A calls B, both carry a root's spike, and their callers carry the default
+    model's symptoms (caller_hops over all 2 * n_chains roots).  -> int64 roots, sorted."""
+    rng = np.random.default_rng(int(seed) + 4242)
+    indeg = np.diff(mesh.row_ptr)
+    cand = np.argsort(-indeg, kind="stable")[: max(n_chains * 50, n_chains)]
+    roots, used_srv = [], set()
+    for b in rng.permutation(cand):
+        b = int(b)
+        if b // 20 in used_srv:
+            continue
+        callers = mesh.col[mesh.row_ptr[b]:mesh.row_ptr[b + 1]].astype(np.int64)
+        callers = [int(c) for c in callers if indeg[c] > 0 and c // 20 not in used_srv and c // 20 != b // 20]
+        if not callers:
+            continue
+        a = callers[int(rng.integers(len(callers)))]
+        roots += [a, b]
+        used_srv.update((a // 20, b // 20))
+        if len(roots) == 2 * n_chains:
+            break
+    return np.sort(np.asarray(roots, np.int64))
+
+
 def caller_hops(mesh, roots, hops=3, cap=2000):
     """Pods that (transitively) call the roots: list of int64 arrays per hop (capped)."""
     seen = set(int(r) for r in roots)
@@ -238,11 +264,20 @@ def make_log_corpus(n_docs, lines_per_doc=2.5, error_rate=0.3, seed=0, hazard_ra
     ws = rng.integers(0, len(_WORDS), total)
     pad = rng.integers(20, 120, total)
     hz = rng.random(total) < hazard_rate
+    # 5 % of the lines carry a trace UUID whose hex groups are mostly letters (a13 masks a UUID as one
+    # token, also when a group holds no digit); a generator of its own keeps every other draw as before
+    rng_u = np.random.default_rng(int(seed) + 7777)
+    has_u = rng_u.random(total) < 0.05
+    hexch = np.frombuffer(b"abcdefabcdefabcdef0123456789", np.uint8)
+    uu = hexch[rng_u.integers(0, len(hexch), (total, 32))]
     lines = []
     for i in range(total):
         t = ERROR_LINES[e_idx[i]] if is_err[i] else BENIGN_LINES[b_idx[i]]
         s = t.format(n=int(ns[i]), m=int(ms[i]), w=_WORDS[ws[i]], d=int(ns[i]) % 10, h="%08x" % int(ns[i]))
         s = "2024-05-01T00:00:%02d.%03dZ " % (int(ms[i]) % 60, int(ns[i]) % 1000) + s + " " + "k" * int(pad[i] // 4)
+        if has_u[i]:
+            u = uu[i].tobytes().decode()
+            s += " trace=%s-%s-%s-%s-%s" % (u[:8], u[8:12], u[12:16], u[16:20], u[20:])
         if hz[i]:
             s += " café Kelvin ſ"
         lines.append(s)

@@ -82,20 +82,26 @@ def log_hist(text):
 # ------------------------------------------------------------------------------------------
 _WORD = re.compile(rb"[A-Za-z0-9_]+")
 _HEX = re.compile(rb"[0-9a-fA-F]{8,}")
+# a UUID: five words of 8, 4, 4, 4 and 12 hex characters joined by single '-' (SURVEY.md §8a a13:
+# "UUIDs masked"); tried first at every word start, so the leftmost UUID wins
+_UUID = rb"(?<![A-Za-z0-9_])[0-9a-fA-F]{8}(?:-[0-9a-fA-F]{4}){3}-[0-9a-fA-F]{12}(?![A-Za-z0-9_])"
+_TOKEN = re.compile(rb"(" + _UUID + rb")|[A-Za-z0-9_]+")
 
 
-TEMPLATE_MASK = b"\xff"  # the one byte a masked word becomes (never in UTF-8 text; shown as "<*>")
+TEMPLATE_MASK = b"\xff"  # the one byte a masked word or UUID becomes (never in UTF-8 text; shown as "<*>")
 
 
 def template_of(line_bytes):
-    """csrc/template.hip's template: every maximal [A-Za-z0-9_] run holding a digit, or of >= 8 hex
-    digits, replaced by TEMPLATE_MASK."""
+    """csrc/template.hip's template (csrc/tmpl_dfa.h): every UUID, and every other maximal
+    [A-Za-z0-9_] run holding a digit or of >= 8 hex digits, replaced by TEMPLATE_MASK."""
     def sub(m):
+        if m.group(1) is not None:
+            return TEMPLATE_MASK
         w = m.group(0)
         if any(48 <= c <= 57 for c in w) or _HEX.fullmatch(w):
             return TEMPLATE_MASK
         return w
-    return _WORD.sub(sub, line_bytes)
+    return _TOKEN.sub(sub, line_bytes)
 
 
 def fnv1a64(b):

@@ -38,7 +38,9 @@ def main():
     ap.add_argument("--out")
     a = ap.parse_args()
     res = {}
-    for t in ("cal", "ppr", "bench", "logs", "logs_fused"):
+    for t in ("cal", "ppr", "bench", "logs", "logs_fused", "logs250k", "tmpl", "corr"):
+        if not any(os.path.isdir(os.path.join(a.d, f"{t}_{p}")) for p in ("rd", "dram", "wr")):
+            continue
         rd, dr, wr = (load(os.path.join(a.d, f"{t}_{p}")) for p in ("rd", "dram", "wr"))
         kern = {}
         for k in set(rd) | set(dr) | set(wr):

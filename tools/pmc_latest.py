@@ -22,12 +22,12 @@ def main():
     kern, src = {}, {}
     for f in a.reports:
         rep = json.load(open(f))
-        for sec in ("bench", "ppr", "logs", "logs_fused"):
+        for sec in ("bench", "ppr", "logs", "logs_fused", "tmpl"):
             for k0, e in rep.get(sec, {}).items():
                 k = ("fused/" if sec == "logs_fused" else "") + k0  # the KRCA_LOG_FUSED=2 scan's kernels
                 if "dram_read_bytes" not in e or "dram_write_bytes" not in e:
                     continue
-                if sec.startswith("logs") and e.get("dispatches", 2) < 2:
+                if sec.startswith("logs") and e.get("dispatches", 2) < 2:  # (tmpl: one scan per call too)
                     continue  # the sizing call's first-scan kernels (log_lines ...), not the scan's
                 if k0.startswith("at::") or k0.startswith("__amd") or k0.startswith("elementwise"):
                     continue  # torch / runtime setup kernels

@@ -131,14 +131,6 @@ def main():
         docs = synth.make_log_corpus(a.docs, lines_per_doc=2.5, seed=0, hazard_rate=0.001)
         blob, off = pack_documents(docs)
         scan = eng.log_scan_device(eng.upload_blob(blob), torch.from_numpy(off).cuda())
-        if os.environ.get("KRCA_TMPL_IMPL", "0") in ("101", "102", "103"):  # profiling probes: hashes only
-            L = scan["n_lines_total"]
-            hs = torch.empty(L, dtype=torch.int64, device="cuda")
-            ms = timed(torch, lambda: eng.lib.krca_template_hash(
-                eng.ptr(scan["text"]), scan["text"].numel(), eng.ptr(scan["line_start"]), eng.ptr(scan["line_end"]),
-                L, eng.ptr(hs), eng._stream()), a.reps)
-            print(json.dumps(dict(kernel="template hash probe", ms=ms, lines=L)))
-            return
         eng.template_hist_device(scan)
         ms = timed(torch, lambda: eng.template_hist_device(scan), a.reps)
         L = scan["n_lines_total"]

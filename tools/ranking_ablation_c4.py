@@ -5,11 +5,16 @@ the bit-exact fixed-point PageRank).  Recall@10 of the 10 planted roots for damp
 floor and ranking key (r = propagated mass, rq = mass x own anomaly (rounds 2-4), psq = mass received
 x sqrt(own anomaly), explained = mass received x the anomaly no explaining dependency accounts for
 (krca.rca.Config's key; its top-10 at the Config's alpha and floor also checked against the C
-oracle), q = own anomaly alone), plus the diagnostics that explain them: each root's score s (max |z| at the
-last step) and its rank among all pods, and how many pods pass each floor.  The "auto" floor is
-the expected maximum |z| of P*M null series, Phi^-1(1 - 1/(2 P M)).
+oracle), u = the unexplained anomaly alone (the explanation pass without PageRank), recv = the mass
+received from callers alone (PageRank without the pod's own anomaly), q = own anomaly alone), plus
+the diagnostics that explain them: each root's score s (max |z| at the last step) and its rank
+among all pods, and how many pods pass each floor.  The "auto" floor is the expected maximum |z|
+of P*M null series, Phi^-1(1 - 1/(2 P M)).  u and recv come from the device solve's own arrays
+(q, d = krca_rca_explain's output, r, and the teleport scale the last step recorded: the
+expressions of krca_rca_key_explained).  --model: default, spread or chain (the held-out model of
+synth.chain_roots).
 
-  python tools/ranking_ablation_c4.py [--pods 1000000] [--edges 20000000] [--seeds 2] --out F
+  python tools/ranking_ablation_c4.py [--pods 1000000] [--edges 20000000] [--seeds 2] [--model M] --out F
 """
 import argparse
 import json
@@ -34,11 +39,14 @@ def main():
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--seeds", type=int, default=2)
     ap.add_argument("--out")
+    ap.add_argument("--model", choices=("default", "spread", "chain"), default="default")
     ap.add_argument("--spread", action="store_true",
                     help="the anomaly spreads to the callers (synth.spread_hops: 20 sampled callers per root and "
                          "hop, 2 hops; root 8 sigma, hop h 9 * 0.9^(h-1) sigma): the callers look as anomalous "
                          "as the root, the reference's premise that symptoms show up upstream of the cause")
     a = ap.parse_args()
+    if a.spread:
+        a.model = "spread"
     import torch
     from krca import native, synth
     from krca.rca import RANKING, Comm, DeviceShard, Explain, RcaStep, shard_graph
@@ -49,15 +57,17 @@ def main():
     af = auto_floor(a.pods * M)
     floors = [0.0, 4.0, 5.0, round(af, 3), 6.0]
     defs = [(al, fl, key) for al in (0.85, 0.5) for fl in floors for key in ("r", "rq", "psq", "explained")] + \
-        [(None, None, "q")]
+        [(RANKING.alpha, round(af, 3), "u"), (RANKING.alpha, round(af, 3), "recv"), (None, None, "q")]
     checks = []
     hits = {d: [] for d in defs}
     diag = []
     for seed in range(a.seeds):
         t0 = time.time()
         m = synth.make_graph(a.pods, n_edges=a.edges, seed=seed)
-        hops = synth.spread_hops(m, m.roots, seed=seed) if a.spread else synth.caller_hops(m, m.roots)
-        kw = synth.SPREAD_SIGMAS if a.spread else {}
+        if a.model == "chain":
+            m.roots = synth.chain_roots(m, seed=seed)
+        hops = synth.spread_hops(m, m.roots, seed=seed) if a.model == "spread" else synth.caller_hops(m, m.roots)
+        kw = synth.SPREAD_SIGMAS if a.model == "spread" else {}
         x = synth.make_metrics_range(0, a.pods, M, T, seed=seed, roots=m.roots, hop_sets=hops, device="cuda", **kw)
         rp, col, od = shard_graph(m.row_ptr, m.col, m.outdeg, 0, a.pods)
         sh = DeviceShard(eng, x, rp, col, od, a.pods, a.pods, 1, RANKING)
@@ -78,6 +88,22 @@ def main():
         for al, fl, key in defs:
             if key == "q":
                 idx = order[:10]
+            elif key in ("u", "recv"):  # from the device arrays of the explained solve at this alpha and floor
+                cfg = RANKING.replace(alpha=al, seed_floor=fl, key="explained")
+                sh.cfg = cfg
+                st = RcaStep(sh, Comm(), cfg, 0, explain=ex)
+                st.propagate()
+                st.merge(*st.settle(*st.local_candidates()))
+                q, d, r = sh.q[:a.pods], sh.d[:a.pods], sh.r[:a.pods]
+                hdr = sh.ctl[:40].cpu().numpy()
+                q_total, tele_used = int(hdr[8:16].view(np.int64)[0]), float(hdr[32:40].view(np.float64)[0])
+                if key == "u":
+                    kv = torch.clamp(q - d, min=0).double()
+                else:
+                    t = torch.floor(q.double() * (tele_used / q_total)) if q_total > 0 else \
+                        torch.full_like(q, int(tele_used / a.pods), dtype=torch.float64)
+                    kv = r.double() - t
+                idx = torch.topk(kv, 10).indices.cpu().numpy()  # (float keys: exact ties are rare; order not checked)
             else:
                 cfg = RANKING.replace(alpha=al, seed_floor=fl, key="rq" if key != "explained" else key)
                 sh.cfg = cfg
