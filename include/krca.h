@@ -47,7 +47,7 @@ int krca_device_count(int* n_host);
 /* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID, KRCA_PPR_DICT,
  * KRCA_LOG_IMPL, KRCA_GROUP_IMPL, KRCA_CORR_DEBUG, KRCA_CORR_RS_GRID, KRCA_CORR_BATCH, KRCA_CORR_AMB_TILE,
  * KRCA_PPR_FUSE, KRCA_PPR_NT, KRCA_PPR_XCD, KRCA_LOG_FUSED, KRCA_CORR_RS_GROUP, KRCA_CORR_SIDE, KRCA_CORR_RS_Q16,
- * KRCA_CORR_CAPC, KRCA_CORR_KM_EXTRA, KRCA_CORR_RSG_GRID.  Initialised once from the environment variables
+ * KRCA_CORR_CAPC, KRCA_CORR_KM_EXTRA, KRCA_CORR_RSG_GRID, KRCA_CORR_PROJ.  Initialised once from the environment variables
  * of the same names when the library loads; launchers never call getenv.  Process-global, not
  * thread-safe (set them before launching work).  Unknown names: KRCA_EINVAL. */
 int krca_tune_set(const char* name, int32_t value);
@@ -267,6 +267,12 @@ int64_t krca_ppr_lane_size(int64_t plan_len);
 int64_t krca_ppr_pack(const int64_t* row_ptr_host, const int32_t* col_host, int64_t N, int64_t n_max,
                       int64_t* plan_host, int64_t plan_len, int32_t* pk_host, uint16_t* lane_host);
 int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* out, void* stream);
+/* p[0 .. n) = value by a kernel (not hipMemsetAsync): safe inside a HIP-graph capture whatever
+ * the runtime's graph packet capture setting (the solve's zeroing uses kernels only) */
+int krca_fill_i64(int64_t* p, int64_t n, int64_t value, void* stream);
+/* Seeds are quantised to q = 2^32 per unit above seed_floor, clamped at 256 units (q <= 2^40; NaN
+ * and values at or below the floor are 0), so the int64 seed total needs N <= 2^23 (KRCA_EINVAL
+ * above). */
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                         int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
                         int64_t* r_local, int64_t* send /*[krca_ppr_slice_words(n_max)]*/, void* stream);
@@ -328,8 +334,8 @@ int krca_ppr_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key
  * j (edge j -> k, j != k) explains j when (A_k - 1 >= A_j or q_k >= 2 q_j) and A_k q_j <= 3 S_k;
  * d_local[j - lo] = the largest q_k over the dependencies that explain j, for the pods [lo, hi) (0:
  * none).  Only anomalous pods' rows are walked; integer counts, sums and maxima, so bit-identical
- * to oracle/krca_oracle.c krco_rca_explain.  ws: krca_rca_explain_ws_size(N) bytes, no
- * initialisation needed.
+ * to oracle/krca_oracle.c krco_rca_explain (S_k and A_k q_j in 128 bits: exact for any row).
+ * ws: krca_rca_explain_ws_size(N) bytes, 16-byte aligned, no initialisation needed.
  * krca_rca_key_explained: key_i = bits(((double)recv_i + (double)t_i / 32) * (double)u_i) with u_i =
  * q_i - d_i (0 when <= 0), t_i the row's teleport share in the solve's last step (from the scale the
  * step recorded in ctl) and recv_i = r_i - t_i, the mass the row received from its callers: the rows

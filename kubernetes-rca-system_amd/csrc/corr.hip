@@ -1075,6 +1075,106 @@ __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32,
   }
 }
 
+// ---- projection bound of the exact-count re-score (round 6) ----------------------------------
+// A listed pair (a, b) has screening value S (the fp16 product) and exact r = z_a . z_b.  With the fp16
+// residuals e = z - fp16(z) (f64, exact), r = S_exact + z_a . e_b + e_a . z_b - e_a . e_b, and for an
+// orthonormal basis B of KP rows (the first KP DCT-II vectors; the series are smooth -- random walks
+// and daily sinusoids -- so most of each row lies in their span):
+//   z_a . e_b = (B z_a) . (B e_b) + (Q z_a) . (Q e_b),   |(Q z_a) . (Q e_b)| <= |Q z_a| |Q e_b|,
+// with |Q x|^2 = |x|^2 - |B x|^2.  So r lies within
+//   |Q z_a| |Q e_b| + |Q e_a| |Q z_b| + |e_a| |e_b| + acc_err
+// of S + c, c = (B z_a) . (B e_b) + (B e_a) . (B z_b): a KP-term dot product from the rows'
+// projections (256 B per partner) instead of the 2.9 KB int16 partner row.  On the bench's series
+// |Q z| is ~0.26 of |z| (tools: the band experiment in DESIGN.md §3.5), so 2.5x fewer pairs read a
+// partner row.  Every quantity is float64 (rounded up where it bounds; +1e-9 covers the float64
+// sums, as everywhere in the re-score), so the decision is the exact one.
+constexpr int KP = 32;  // basis vectors: proj[p] = B z_p (KP floats) | B e_p (KP floats)
+__global__ __launch_bounds__(TPB) void corr_dct_basis(double* __restrict__ B, int T) {
+  const int64_t n = (int64_t)KP * T;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const int j = (int)(i / T), t = (int)(i % T);
+    // (rows j >= T are zero: the DCT-II vectors are orthonormal for j < T only, aliases past it)
+    B[i] = j >= T ? 0.0 : j == 0 ? sqrt(1.0 / T) : sqrt(2.0 / T) * cospi((2.0 * t + 1.0) * j / (2.0 * T));
+  }
+}
+
+// 64 rows per workgroup, 4 lanes per row (each a quarter of every 64-step chunk), the chunk's basis
+// columns in LDS; float64 sums, combined over the 4 lanes by shuffles
+constexpr int PJ_ROWS = 64, PJ_TC = 64;
+__global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, const uint16_t* __restrict__ zh,
+                                                 int64_t P, int T, int Tp, const double* __restrict__ B,
+                                                 float* __restrict__ proj, float* __restrict__ pqz,
+                                                 float* __restrict__ pqe) {
+  __shared__ double sB[KP][PJ_TC + 1];
+  __shared__ float sz[PJ_ROWS][PJ_TC + 1];
+  __shared__ float se[PJ_ROWS][PJ_TC + 1];
+  const int tid = threadIdx.x, r = tid >> 2, part = tid & 3;
+  const int64_t p0 = (int64_t)blockIdx.x * PJ_ROWS;
+  double bz[KP], be[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) bz[j] = be[j] = 0.0;
+  double nz = 0.0, ne = 0.0;
+  for (int t0 = 0; t0 < T; t0 += PJ_TC) {
+    __syncthreads();
+    for (int i = tid; i < KP * PJ_TC; i += TPB) {
+      const int j = i / PJ_TC, t = i % PJ_TC;
+      sB[j][t] = t0 + t < T ? B[(int64_t)j * T + t0 + t] : 0.0;
+    }
+    for (int i = tid; i < PJ_ROWS * PJ_TC; i += TPB) {  // coalesced along t
+      const int rr = i / PJ_TC, t = i % PJ_TC;
+      const int64_t p = p0 + rr;
+      float z = 0.f, e = 0.f;
+      if (p < P && t0 + t < T) {
+        z = z32[p * T + t0 + t];
+        e = (float)((double)z - (double)(float)__builtin_bit_cast(_Float16, zh[p * Tp + t0 + t]));  // exact
+      }
+      sz[rr][t] = z;
+      se[rr][t] = e;
+    }
+    __syncthreads();
+    for (int t = part; t < PJ_TC; t += 4) {
+      const double z = (double)sz[r][t], e = (double)se[r][t];
+      nz += z * z;
+      ne += e * e;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        const double b = sB[j][t];
+        bz[j] += z * b;
+        be[j] += e * b;
+      }
+    }
+  }
+  auto sum4 = [](double v) {
+    v += __shfl_xor(v, 1, 4);
+    v += __shfl_xor(v, 2, 4);
+    return v;
+  };
+  nz = sum4(nz);
+  ne = sum4(ne);
+  double nbz = 0.0, nbe = 0.0;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    bz[j] = sum4(bz[j]);
+    be[j] = sum4(be[j]);
+    nbz += bz[j] * bz[j];
+    nbe += be[j] * be[j];
+  }
+  const int64_t p = p0 + r;
+  if (p >= P) return;
+  float* out = proj + p * (2 * KP);
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {  // each of the row's 4 lanes writes a quarter
+    if ((j & 3) == part) {
+      out[j] = (float)bz[j];
+      out[KP + j] = (float)be[j];
+    }
+  }
+  if (part == 0) {  // |Q x| = sqrt(|x|^2 - |B x|^2), rounded up (+1e-12 inside: float64 sums, B's rounding)
+    pqz[p] = (float)(sqrt(fmax(nz - nbz, 0.0) + 1e-12) * (1.0 + 1e-6));
+    pqe[p] = (float)(sqrt(fmax(ne - nbe, 0.0) + 1e-24) * (1.0 + 1e-6));
+  }
+}
+
 // the ambiguous pairs in list order, 16 lanes each: decided from the screening value and the two
 // rows' rounding-error norms when that suffices, else re-scored (float4 loads of the pair's rows of
 // z32, float64 accumulation); persistent over the device-held list length
@@ -1216,7 +1316,8 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* _
                                                                 float acc_err, int32_t* __restrict__ count,
                                                                 const int16_t* __restrict__ zq, int Tq,
                                                                 const float* __restrict__ qs, const float* __restrict__ qn,
-                                                                const float* __restrict__ nrm) {
+                                                                const float* __restrict__ nrm, const float* __restrict__ proj,
+                                                                const float* __restrict__ pqz, const float* __restrict__ pqe) {
   extern __shared__ float4 rs_lds[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane & 15, grp = lane >> 4;
   const int T4 = (T + 3) / 4;
@@ -1237,6 +1338,15 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* _
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const double sa = (double)dn[a];
     const double na = zq ? (double)nrm[a] : 0.0;
+    // the row pod's projections for the projection bound: lane sub < 8 holds B e_a (pairs with the
+    // partner's B z), sub >= 8 holds B z_a (pairs with the partner's B e): one float4 each
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f);
+    double qza = 0.0, qea = 0.0;
+    if (proj) {
+      pa = reinterpret_cast<const float4*>(proj + a * (2 * KP))[sub ^ 8];
+      qza = (double)pqz[a];
+      qea = (double)pqe[a];
+    }
     int hits = 0;
     for (int32_t q = e0 + grp; q < e1; q += 4) {
       const int2 e = gs[q];
@@ -1254,7 +1364,16 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* _
         // (+ 1e-9 for the float64 sums) the exact float64 product is on the same side of tau; the
         // fp32 partner row only inside it (uniform over the 16-lane group)
         int dec = -1;
-        if (zq) {
+        if (proj) {  // the projection bound first (256 B of the partner instead of its row)
+          const float4 pb = reinterpret_cast<const float4*>(proj + b * (2 * KP))[sub];
+          double c = (double)pa.x * (double)pb.x + (double)pa.y * (double)pb.y + (double)pa.z * (double)pb.z +
+                     (double)pa.w * (double)pb.w;
+          for (int off = 8; off > 0; off >>= 1) c += __shfl_xor(c, off, 16);
+          const double est = fabs((double)__int_as_float(e.y) + c);
+          const double bp = qza * (double)pqe[b] + qea * (double)pqz[b] + sa * sb + (double)acc_err + 1e-9;
+          dec = est > (double)tau + bp ? 1 : est <= (double)tau - bp ? 0 : -1;
+        }
+        if (zq && dec < 0) {
           const double vq = fabs(dot16_q16(ra, zq + b * Tq, Tq, sub) * (double)qs[b]);
           const double bq = na * (double)qn[b] + 1e-9;
           dec = vq > (double)tau + bq ? 1 : vq <= (double)tau - bq ? 0 : -1;
@@ -1655,6 +1774,9 @@ struct CorrWs {  // views into a caller's candidate workspace
   float* dn;            // [P] fp16 rounding-error norm of each row
   int16_t* zq;          // [P][Tq] int16 partner rows of the grouped re-score (KRCA_CORR_RS_Q16), else null
   float *qs, *qn, *nrm; // [P] their step, error norm, the fp32 row's norm
+  float* proj;          // [P][2 KP] B z | B e of each row (the projection bound), else unused
+  float *pqz, *pqe;     // [P] |Q z|, |Q e|
+  double* dct;          // [KP][T] the basis
   int Tq;               // T rounded up to 8
   unsigned long long* amb_n;  // [2]: the lists' fill
   int32_t *gcnt, *goff, *gcur, *gsum;  // grouped re-score: entries per row pod, offsets [P + 1], cursors, scan blocks
@@ -1704,6 +1826,10 @@ int64_t ws_layout(int64_t P, int T, int Tp, int KC, int64_t n_loc, int G, char* 
     w.qs = reinterpret_cast<float*>(take(P));
     w.qn = reinterpret_cast<float*>(take(P));
     w.nrm = reinterpret_cast<float*>(take(P));
+    w.proj = reinterpret_cast<float*>(take(P * 2 * KP));  // the projection bound's rows (corr_proj)
+    w.pqz = reinterpret_cast<float*>(take(P));
+    w.pqe = reinterpret_cast<float*>(take(P));
+    w.dct = reinterpret_cast<double*>(take(2 * (int64_t)KP * T));
   }
   w.amb_n = reinterpret_cast<unsigned long long*>(take(4));
   w.gcnt = reinterpret_cast<int32_t*>(take(P));
@@ -1817,6 +1943,8 @@ inline int cand_cap() {
 
 // the grouped re-score reads int16 partner rows (written by corr_dnorm)
 inline bool q16_rows() { return krca::tuning().corr_rs_q16 && krca::tuning().corr_rs_group; }
+// ... and tries the projection bound before them (KRCA_CORR_PROJ, default on)
+inline bool proj_bound() { return krca::tuning().corr_proj && krca::tuning().corr_rs_group; }
 
 // exact |r| > tau counts of the ambiguous pairs in list l (float64 from z32), added to count
 int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int32_t* count, hipStream_t st) {
@@ -1847,7 +1975,8 @@ int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int
     const unsigned gg = (unsigned)std::min<int64_t>(krca::ceil_div(d.P, RS_WAVES), cap);
     hipLaunchKernelGGL(corr_amb_rescore_grouped, dim3(gg), dim3(TPB), lds, st, (const int32_t*)ws.goff,
                        (const int2*)ws.gs, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count,
-                       zq, ws.Tq, (const float*)ws.qs, (const float*)ws.qn, (const float*)ws.nrm);
+                       zq, ws.Tq, (const float*)ws.qs, (const float*)ws.qn, (const float*)ws.nrm,
+                       proj_bound() ? (const float*)ws.proj : nullptr, (const float*)ws.pqz, (const float*)ws.pqe);
     KRCA_LAUNCH_CHECK();
     return KRCA_OK;
   }
@@ -1901,6 +2030,14 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
                      d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
   KRCA_LAUNCH_CHECK();
+  if (proj_bound()) {
+    hipLaunchKernelGGL(corr_dct_basis, dim3((unsigned)krca::ceil_div((int64_t)KP * d.T, TPB)), dim3(TPB), 0, st, ws.dct,
+                       d.T);
+    KRCA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(corr_proj, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
+                       d.Tp, (const double*)ws.dct, ws.proj, ws.pqz, ws.pqe);
+    KRCA_LAUNCH_CHECK();
+  }
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   // screening counts: certain above tau + eps, decided in the tile by the pair's own bound or
   // re-scored within it (exact counts)

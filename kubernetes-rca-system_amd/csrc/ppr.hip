@@ -122,9 +122,12 @@ __device__ __forceinline__ int64_t edge_weight_c(int64_t rj, double coef) {
 }
 
 
+constexpr int64_t kMaxSeedN = (int64_t)1 << 23;  // N x 2^40 (the largest q) fits the int64 seed total
+// a seed's anomaly above the floor in 2^-32 units, clamped at 256 units (q <= 2^40: every product
+// and sum of the explanation pass and the int64 seed total of N <= 2^23 pods stay exact; a NaN is 0)
 __device__ __forceinline__ int64_t quantise(float s, float floor_) {
   const double v = (double)s - (double)floor_;
-  return v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
+  return v > 0.0 ? (int64_t)(fmin(v, 256.0) * 4294967296.0) : 0;
 }
 
 // r0 = floor(2^60/N), w0, seeds; dangling mass and seed total into the send slots
@@ -134,6 +137,11 @@ __global__ __launch_bounds__(TPB) void ppr_init(const float* __restrict__ seed, 
                                                 int64_t* __restrict__ send, int64_t n_max, double* __restrict__ coef) {
   __shared__ int64_t red[TPB / 64];
   const int64_t r0 = (int64_t)(krca::kFix / (double)N);
+#ifdef KRCA_GRAPH_DEBUG
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    printf("KGD init seed=%p q=%p r=%p send=%p coef=%p n=%ld N=%ld alpha=%.4f floor=%.4f\n", (const void*)seed, (void*)q,
+           (void*)r, (void*)send, (void*)coef, (long)n, (long)N, alpha, seed_floor);
+#endif
   int64_t dang = 0, qs = 0;
   for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
     const int32_t deg = outdeg[i];
@@ -430,6 +438,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PPR_WAVES, 
   // entries of this workgroup: b, b + stride, ... below lim.  xcd (the host sets it when the grid is
   // a multiple of 8 and nblk >= grid): workgroups g, g + 8, ... (one XCD, for speed only) share one
   // contiguous eighth of the plan, so the callers an XCD's L2 holds are those of neighbouring rows
+#ifdef KRCA_GRAPH_DEBUG  // tools/graph_replay_probe.py (make gdbg): the kernel arguments and ctl header as seen
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    printf("KGD step fold=%d it=%d G=%d next=%p ctl=%p r=%p send=%p w=%p q=%p plan=%p n=%ld nblk=%ld alpha=%.4f"
+           " | ctl iter=%d conv=%d qt=%ld tele=%.9e\n", fo.on, fo.it, fo.G, (void*)fo.next, (void*)ctl, (void*)r,
+           (void*)send, (const void*)w, (const void*)q, (const void*)plan, (long)n, (long)nblk, alpha, ctl->iter,
+           ctl->converged, (long)ctl->q_total, ctl->tele);
+#endif
   int64_t b = blockIdx.x, lim = nblk, stride = gridDim.x;
   if (xcd) {
     const int64_t x = blockIdx.x & 7;
@@ -661,6 +676,12 @@ __global__ __launch_bounds__(TPB) void ppr_finish(const int64_t* __restrict__ w_
   }
   const int64_t err = block_sum_i64(pe, red);
   const int64_t dang = block_sum_i64(pd, red);
+#ifdef KRCA_GRAPH_DEBUG
+  if (threadIdx.x == 0)
+    printf("KGD finish it=%d G=%d w_all=%p ctl=%p err=%ld dang=%ld | ctl iter=%d conv=%d qt=%ld tele=%.9e\n", it, G,
+           (const void*)w_all, (void*)ctl, (long)err, (long)dang, ctl->iter, ctl->converged, (long)ctl->q_total,
+           ctl->tele);
+#endif
   if (threadIdx.x != 0 || ctl->converged) return;
   ctl->iter = it;
   if (err_limit > 0.0 && (double)err < err_limit) {
@@ -725,6 +746,32 @@ unsigned grid_for(int64_t n, int64_t cap = 2048) {
 
 }  // namespace
 
+namespace {
+// Zeroing on the solve path is done by kernels, never by hipMemsetAsync: a solve captured into a
+// HIP graph with the runtime's graph packet capture on replayed its memset nodes with stale bytes
+// once ~300 later eager launches had reused the runtime's staging memory (R6a,
+// tools/graph_replay_probe.py: every captured kernel's arguments were intact at the bad replay, but
+// the ctl header read back torch kernels' argument words), while kernel nodes replay exactly.
+__global__ __launch_bounds__(TPB) void zero_words2(int64_t* __restrict__ a, int64_t na, int64_t* __restrict__ b,
+                                                   int64_t nb) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < na + nb; i += (int64_t)gridDim.x * TPB) {
+    if (i < na) a[i] = 0;
+    else b[i - na] = 0;
+  }
+}
+__global__ __launch_bounds__(TPB) void fill_words(int64_t* __restrict__ a, int64_t n, int64_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) a[i] = v;
+}
+static_assert(sizeof(Ctl) % 8 == 0, "the ctl header is zeroed in int64 words");
+// the ctl header and the send buffer's partial-sum slots, zeroed before an init adds into them
+int zero_ctl_and_slots(void* ctl, int64_t* send_slots, hipStream_t st) {
+  hipLaunchKernelGGL(zero_words2, dim3(1), dim3(TPB), 0, st, reinterpret_cast<int64_t*>(ctl), (int64_t)(sizeof(Ctl) / 8),
+                     send_slots, (int64_t)NSLOT);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+}  // namespace
+
 extern "C" {
 
 
@@ -739,15 +786,24 @@ int krca_ppr_remap_cols(const int32_t* col, int64_t E, int64_t n_max, int32_t* o
   return KRCA_OK;
 }
 
+int krca_fill_i64(int64_t* p, int64_t n, int64_t value, void* stream) {
+  KRCA_CHECK_ARG(n >= 0, "krca_fill_i64: bad size");
+  if (n == 0) return KRCA_OK;
+  KRCA_CHECK_ARG(p, "krca_fill_i64: null pointer");
+  hipLaunchKernelGGL(fill_words, dim3((unsigned)std::min<int64_t>(krca::ceil_div(n, TPB), 1024)), dim3(TPB), 0,
+                     krca::as_stream(stream), p, n, value);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
 int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local, int64_t n_max,
                         int64_t N, double alpha, void* ctl, int64_t* q_local, int64_t* r_local, int64_t* send,
                         void* stream) {
-  KRCA_CHECK_ARG(N > 0 && N < INT32_MAX && n_local >= 0 && n_local <= n_max, "krca_ppr_shard_init: bad sizes");
+  KRCA_CHECK_ARG(N > 0 && N <= kMaxSeedN && n_local >= 0 && n_local <= n_max, "krca_ppr_shard_init: bad sizes");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0, "krca_ppr_shard_init: alpha must be in (0, 1)");
   KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)), "krca_ppr_shard_init: null pointer");
   hipStream_t st = krca::as_stream(stream);
-  KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
-  KRCA_HIP(hipMemsetAsync(send + wslots(n_max), 0, NSLOT * sizeof(int64_t), st));
+  if (int rc = zero_ctl_and_slots(ctl, send + wslots(n_max), st)) return rc;
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local, N,
                        alpha, q_local, r_local, send, n_max, host_coef(ctl, n_local));
@@ -758,13 +814,12 @@ int krca_ppr_shard_init(const float* seed, float seed_floor, const int32_t* outd
 int krca_ppr_shard_init_warm(const float* seed, float seed_floor, const int32_t* outdeg, int64_t n_local,
                              int64_t n_max, int64_t N, double alpha, void* ctl, int64_t* q_local,
                              const int64_t* r_local, int64_t* send, void* stream) {
-  KRCA_CHECK_ARG(N > 0 && N < INT32_MAX && n_local >= 0 && n_local <= n_max, "krca_ppr_shard_init_warm: bad sizes");
+  KRCA_CHECK_ARG(N > 0 && N <= kMaxSeedN && n_local >= 0 && n_local <= n_max, "krca_ppr_shard_init_warm: bad sizes");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0, "krca_ppr_shard_init_warm: alpha must be in (0, 1)");
   KRCA_CHECK_ARG(ctl && send && (n_local == 0 || (seed && outdeg && q_local && r_local)),
                  "krca_ppr_shard_init_warm: null pointer");
   hipStream_t st = krca::as_stream(stream);
-  KRCA_HIP(hipMemsetAsync(ctl, 0, sizeof(Ctl), st));
-  KRCA_HIP(hipMemsetAsync(send + wslots(n_max), 0, NSLOT * sizeof(int64_t), st));
+  if (int rc = zero_ctl_and_slots(ctl, send + wslots(n_max), st)) return rc;
   if (n_local > 0)
     hipLaunchKernelGGL(ppr_init_warm, dim3(grid_for(n_local)), dim3(TPB), 0, st, seed, seed_floor, outdeg, n_local,
                        alpha, q_local, r_local, send, n_max, host_coef(ctl, n_local));
@@ -935,7 +990,7 @@ int64_t krca_ppr_workspace_size(int64_t N) {
 int krca_ppr(const int64_t* row_ptr, const int32_t* col, const int32_t* outdeg, int64_t N, const int64_t* plan,
              int64_t plan_len, const uint16_t* lane, const float* seed, float seed_floor, double alpha, int32_t max_iter, double tol,
              void* workspace, float* r_out, int64_t* r_fixed, int64_t* q_out, int32_t* iters_host, void* stream) {
-  KRCA_CHECK_ARG(N > 0 && N < INT32_MAX, "krca_ppr: N=%lld out of range", (long long)N);
+  KRCA_CHECK_ARG(N > 0 && N <= kMaxSeedN, "krca_ppr: N=%lld out of range", (long long)N);
   KRCA_CHECK_ARG(row_ptr && col && outdeg && plan && lane && seed && workspace && r_out, "krca_ppr: null pointer");
   KRCA_CHECK_ARG(plan_len > 0 && plan_len % 4 == 0, "krca_ppr: bad plan");
   KRCA_CHECK_ARG(alpha > 0.0 && alpha < 1.0 && max_iter > 0, "krca_ppr: alpha in (0,1), max_iter > 0");

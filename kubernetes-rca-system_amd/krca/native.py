@@ -89,6 +89,7 @@ SIGNATURES = {
     "krca_ppr_ctl_copy": (c_i32, [c_vp, c_vp, c_vp]),
     "krca_ppr_fixed_to_float": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "krca_ppr_rca_key": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "krca_fill_i64": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
     "krca_rca_explain_ws_size": (c_i64, [c_i64]),
     "krca_rca_explain": (c_i32, [c_vp, c_i64, c_f32, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "krca_rca_key_explained": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),

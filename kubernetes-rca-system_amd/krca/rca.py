@@ -487,10 +487,12 @@ class DeviceShard:
     def _zero_slots(self):
         """Partial-sum slots zeroed before an init adds into send's set 0 (and, with the ping-pong
         exchange, the other buffer's, which the first folded step writes)."""
+        e, p = self.eng, self.eng.ptr
         wsl = wslots(self.n_max)
-        self.send[wsl:].zero_()
-        if self.pingpong:
-            self.w_all[wsl:].zero_()
+        # by a libkrca kernel, not torch's zero_ (a memset node in a captured solve; DESIGN.md §5)
+        for buf in (self.send, self.w_all) if self.pingpong else (self.send,):
+            tail = buf[wsl:]
+            self._chk(e.lib.krca_fill_i64(p(tail), tail.numel(), 0, e._stream()), "krca_fill_i64")
 
     def init(self, alpha, seed_floor):
         e, p = self.eng, self.eng.ptr
@@ -695,19 +697,6 @@ class Explain:
         return self._dev[key]
 
 
-def _check_graph_runtime():
-    """The HIP runtime's graph packet capture must be off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0, set
-    before the first HIP call): with it on, a captured solve replayed after some hundreds of other
-    kernel launches computed wrong ranks (R5n / R5o, tests/test_gpu_kernels.py::
-    test_rca_graph_replay_after_eager_launches: 300 unrelated launches between two replays were
-    enough; graphs of torch kernels alone replayed correctly)."""
-    import os
-    if os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
-        raise RuntimeError("RcaStep: the HIP-graph solve needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment "
-                           "before the first HIP call (replays of captured libkrca kernels are otherwise "
-                           "overwritten by later launches on this runtime; DESIGN.md §5)")
-
-
 def graph_default(comm, cfg, shard=None):
     """Whether RcaStep captures its PageRank solve in a HIP graph: only with KRCA_RCA_GRAPH=1, for a
     device shard.  Measured at C4 on one MI355X (`profiles/r3/bench_graph_ab.txt`): the replayed
@@ -717,7 +706,7 @@ def graph_default(comm, cfg, shard=None):
     import os
     if os.environ.get("KRCA_RCA_GRAPH") != "1" or not isinstance(shard, DeviceShard):
         return False
-    return True  # (RcaStep then checks the runtime setting: _check_graph_runtime)
+    return True
 
 
 class RcaStep:
@@ -738,8 +727,6 @@ class RcaStep:
         whose padded slices a coupled G > 1 shard's scores are gathered in (default uniform)."""
         self.s, self.comm, self.cfg, self.offset = shard, comm, cfg, offset
         self.graph = graph_default(comm, cfg, shard) if graph is None else bool(graph)
-        if self.graph:
-            _check_graph_runtime()
         self._graphs = {}  # n -> (captured graph, the exchange buffers' roles after it)
         if explain is not None and not isinstance(explain, Explain):
             explain = Explain(*explain)

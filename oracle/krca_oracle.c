@@ -104,6 +104,12 @@ static uint32_t wenc(int64_t w) {
 }
 static int64_t wdec(uint32_t c) { return (int64_t)(c & 0x3FFFFFFu) << (c >> 26); }
 
+/* csrc/ppr.hip / explain.hip quantise: 2^32 per |z| unit above the floor, clamped at 256 units */
+static int64_t quantise(float s, float seed_floor) {
+  const double v = (double)s - (double)seed_floor;
+  return v > 0.0 ? (int64_t)(fmin(v, 256.0) * 4294967296.0) : 0;
+}
+
 /* Pull-CSR personalized PageRank; returns iterations (negative if no convergence).
  * warm != 0: r holds the start vector on entry (krca_ppr_shard_init_warm), else r0 = 2^60/N.
  * recv (optional): the mass each node received from its callers in the last iteration that updated
@@ -115,8 +121,7 @@ int32_t krco_ppr_ex(const int64_t* row_ptr, const int32_t* col, const int32_t* o
   int64_t qtot = 0, dang = 0;
   const int64_t r0 = (int64_t)(kFix / (double)N);
   for (int64_t i = 0; i < N; ++i) {
-    const double v = (double)seed[i] - (double)seed_floor;
-    q[i] = v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
+    q[i] = quantise(seed[i], seed_floor);
     qtot += q[i];
     if (!warm) r[i] = r0;
     w[i] = wenc(edge_weight(r[i], outdeg[i], alpha));
@@ -183,10 +188,6 @@ void krco_rca_key(const int64_t* r, const int64_t* q, int64_t n, int64_t* key) {
   }
 }
 
-static int64_t quantise(float s, float seed_floor) {
-  const double v = (double)s - (double)seed_floor;
-  return v > 0.0 ? (int64_t)(v * 4294967296.0) : 0;
-}
 
 /* The explanation pass of krca_rca_explain (csrc/explain.hip), over the whole pull-CSR (row k = the
  * callers j of k, edges j -> k).  q_j = the quantised seed of krca_ppr_shard_init.  For every
@@ -198,18 +199,19 @@ static int64_t quantise(float s, float seed_floor) {
  *                                           the mean over k's anomalous callers; a pod far above
  *                                           them is a fault of its own that happens to call k).
  * d[j - lo] = the largest q_k over the dependencies that explain j (0: none), for pods [lo, hi).
- * Integer arithmetic throughout (A_k q_j, 3 S_k < 2^63 for q < 2^40 and A < 2^23). */
+ * Integer arithmetic throughout: q <= 2^40 (quantise), S_k summed and A_k q_j <= 3 S_k compared in
+ * 128 bits (exact for any row length; ADVICE r5: the int64 form wrapped for large seeds). */
 void krco_rca_explain(const float* score, int64_t N, float seed_floor, const int64_t* row_ptr, const int32_t* col,
                       int64_t lo, int64_t hi, int64_t* d) {
   int64_t* q = (int64_t*)malloc(sizeof(int64_t) * (N > 0 ? N : 1));
-  int64_t* S = (int64_t*)calloc(N > 0 ? N : 1, sizeof(int64_t));
+  __int128* S = (__int128*)calloc(N > 0 ? N : 1, sizeof(__int128));
   int32_t* A = (int32_t*)calloc(N > 0 ? N : 1, sizeof(int32_t));
   for (int64_t i = 0; i < N; ++i) q[i] = quantise(score[i], seed_floor);
 #pragma omp parallel for schedule(dynamic, 1024)
   for (int64_t k = 0; k < N; ++k) {
     if (q[k] <= 0) continue;
     int32_t a = 0;
-    int64_t sum = 0;
+    __int128 sum = 0;
     for (int64_t e = row_ptr[k]; e < row_ptr[k + 1]; ++e) {
       const int64_t qc = q[col[e]];
       if (qc > 0) {
@@ -229,7 +231,7 @@ void krco_rca_explain(const float* score, int64_t N, float seed_floor, const int
       if (j < lo || j >= hi || j == k) continue;
       const int64_t qj = q[j];
       if (qj <= 0) continue;
-      if ((A[k] - 1 >= A[j] || qk >= 2 * qj) && (int64_t)A[k] * qj <= 3 * S[k] && qk > d[j - lo]) d[j - lo] = qk;
+      if ((A[k] - 1 >= A[j] || qk >= 2 * qj) && (__int128)A[k] * qj <= 3 * S[k] && qk > d[j - lo]) d[j - lo] = qk;
     }
   }
   free(q);

@@ -9,12 +9,10 @@ for p in (os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "o
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
-# The HIP-graph solve (RcaStep graph=True) needs the runtime's graph packet capture off: with it on,
-# replays of libkrca kernels captured into a graph went wrong once ~300 unrelated eager launches had
-# run since the capture (R5n / R5o: tests/test_gpu_kernels.py::test_rca_graph_replay_after_eager_launches;
-# torch-only graphs were unaffected).  Read by the HIP runtime when it initialises, which no test
-# module does at import.  krca.rca.RcaStep refuses graph mode without it.
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# (Rounds 5 ran the GPU tests with DEBUG_CLR_GRAPH_PACKET_CAPTURE=0: with the runtime's graph packet
+# capture on, a captured solve replayed wrong after ~300 later eager launches.  The cause was the
+# solve's hipMemsetAsync nodes, whose replays read stale staging bytes (tools/graph_replay_probe.py,
+# R6a); the solve zeroes with kernels now, and the tests run with the runtime's default setting.)
 
 
 def pytest_configure(config):

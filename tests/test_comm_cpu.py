@@ -118,3 +118,4 @@ def test_one_rank_swap_or_collective(monkeypatch):
     c = rca.Comm(1, 0, collective=True)
     c.exchange(sh)
     assert len(pg.calls) == 1 and sh.w_all.tolist() == [0, 1, 2, 3]
+

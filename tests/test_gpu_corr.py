@@ -201,17 +201,19 @@ def test_corr_batches_and_full_lists_identical(eng):
     # performance knobs that must not change a result: the grouped re-score's grid, and how many
     # candidates past the k-th the merge re-scores (fewer: more pods take the deep merge; the
     # certificate margins may differ, the sets, values and counts not)
+    # (KRCA_CORR_PROJ = 0: the grouped re-score without the projection bound; counts must not move)
     try:
-        for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2)):
+        for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2), (b"KRCA_CORR_PROJ", 0)):
             assert lib.krca_tune_set(knob, val) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
-            lib.krca_tune_set(knob, 0 if knob == b"KRCA_CORR_RSG_GRID" else 6)
+            lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 1}[knob])
             for key in ("idx", "val", "count"):
                 assert np.array_equal(got[key], ref[key]), (knob, key)
             assert (got["cert"] > 0).all(), knob
     finally:
         lib.krca_tune_set(b"KRCA_CORR_RSG_GRID", 0)
         lib.krca_tune_set(b"KRCA_CORR_KM_EXTRA", 6)
+        lib.krca_tune_set(b"KRCA_CORR_PROJ", 1)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
     _, _, bad = device_check(ref, z, [rows], k)

@@ -685,6 +685,12 @@ def test_rca_explain_kernel_vs_oracle(eng, n):
         full = oracle.c_rca_explain(score, floor, rp, col)
         if frac == 0.02 and n >= 3000:  # the rule fires on some pods, not on all
             assert 0 < int((full > 0).sum()) < n
+    # seeds far past the quantisation's clamp (256 units: q <= 2^40), infinities and NaNs: the
+    # 128-bit sums and typicality test keep device and oracle exact (int64 wrapped)
+    score = np.where(rng.random(n) < 0.3, rng.choice([1e6, 3e38, np.inf, 300.0, 40.0], n), rng.random(n) * 3.0)
+    score = np.where(rng.random(n) < 0.01, np.nan, score).astype(np.float32)
+    got = eng.rca_explain_device(torch.from_numpy(score).cuda(), 4.0, rpd, cold, 0, n)[:n].cpu().numpy()
+    assert np.array_equal(got, oracle.c_rca_explain(score, 4.0, rp, col))
 
 
 def test_rca_key_explained_single_device_vs_oracle(eng):

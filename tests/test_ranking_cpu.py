@@ -107,3 +107,36 @@ def test_explain_rule_magnitude_and_typicality():
     rp, col, _ = _csr(2, [(0, 0), (1, 0)])
     d = oracle.c_rca_explain(np.array([9.0, 4.0], np.float32), fl, rp, col)
     assert d.tolist() == [0, 0]
+
+
+def test_explain_large_seeds_exact():
+    """Seeds past the quantisation clamp (q <= 2^40 = 256 units above the floor; inf too, NaN = 0):
+    krco_rca_explain against the rule in exact Python integers (the int64 typicality
+    product wrapped for large seeds)."""
+    rng = np.random.default_rng(3)
+    n = 400
+    edges = [(int(a), int(b)) for a, b in rng.integers(0, n, (3000, 2)) if a != b]
+    rp, col, _ = _csr(n, edges)
+    s = np.where(rng.random(n) < 0.5, rng.choice([1e6, 3e38, np.inf, 300.0, 40.0, 9.0], n), rng.random(n) * 3.0)
+    s = np.where(rng.random(n) < 0.02, np.nan, s).astype(np.float32)
+    fl = 4.0
+
+    def qz(v):
+        v = float(v) - fl
+        return int(min(v, 256.0) * 2.0 ** 32) if v > 0 else 0  # (NaN > 0 is False)
+    q = [qz(v) for v in s]
+    assert max(q) == 2 ** 40
+    A = [0] * n
+    S = [0] * n
+    for k in range(n):
+        cs = [q[col[e]] for e in range(rp[k], rp[k + 1]) if q[col[e]] > 0]
+        A[k], S[k] = len(cs), sum(cs)
+    want = [0] * n
+    for k in range(n):
+        if q[k] <= 0:
+            continue
+        for e in range(rp[k], rp[k + 1]):
+            j = int(col[e])
+            if j != k and q[j] > 0 and (A[k] - 1 >= A[j] or q[k] >= 2 * q[j]) and A[k] * q[j] <= 3 * S[k]:
+                want[j] = max(want[j], q[k])
+    assert oracle.c_rca_explain(s, fl, rp, col).tolist() == want

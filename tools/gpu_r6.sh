@@ -8,6 +8,7 @@
 #   ppr          rocprofv3 stats of the C4 PageRank propagate   logs / tmpl  same for logs / templates
 #   corr100k / corr1m   rocprofv3 stats of the correlation at C3 / 1M pods (tau 0.5)
 #   c5           tools/bench_stream.py (C5 window)   g8           tools/g8_step_emulation.py --decoupled
+#   graphprobe_J_N / graphprobeoff_J_N  tools/graph_replay_probe.py (--junk J --launches N) with packet capture on / off
 #   pmcmfma      tools/gpu_pmc_mfma.sh (correlation MFMA busy, clock, DRAM bytes at C3 / 1M)
 #   pmcx_T       tools/gpu_pmc_exact.sh with TARGETS=T (one target: cal ppr bench logs tmpl ...)
 set -u
@@ -40,13 +41,12 @@ for s in "$@"; do
     testsall_*) step $s 900 python3 -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread -k "${s#testsall_}" ;;
     tests_*) step $s 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "${s#tests_}" ;;
     bench) step bench 400 python3 bench.py ;;
-    benchgraph_*) step $s 400 env KRCA_RCA_GRAPH=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python3 bench.py --no-corr --no-cpu-baseline ;;
+    benchgraph_*) step $s 400 env KRCA_RCA_GRAPH=1 python3 bench.py --no-corr --no-cpu-baseline ;;
     bencheager_*) step $s 400 python3 bench.py --no-corr --no-cpu-baseline ;;
     bench8gloo) step bench8gloo 900 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --steps 3 --warmup 1 --no-corr --no-cpu-baseline ;;
     bench8gloobal) step bench8gloobal 900 env KRCA_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --steps 3 --warmup 1 --no-corr --no-cpu-baseline --ppr-partition balanced ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    graphdbg) step testsall_graphdbg 300 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" &&
-              step testsall_graphdbg_nopkt 300 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after" ;;
+    graphdbg) step testsall_graphdbg 300 python3 -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread -k "replay_after or graph" ;;
     bench_cpufull) step bench_cpufull 500 python3 bench.py --steps 3 --warmup 1 --cpu-full-mesh --no-corr ;;
     bench_trace) prof bench_trace 500 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify ;;
     rank_*) m=${s#rank_}; step $s 900 python3 -u tools/ranking_ablation_c4.py --model $m --out $O/ranking_ablation_${m}_c4.json ;;
@@ -62,6 +62,8 @@ for s in "$@"; do
     corrrsg_*) v=${s#corrrsg_}; export KRCA_CORR_RSG_GRID=${v%%_*}; prof $s 400 tools/prof_kernels.py corr --pods ${v##*_} --reps 1 --tau 0.5; unset KRCA_CORR_RSG_GRID ;;
     pmcsq_*) t=${s#pmcsq_}; step $s 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $O/$s -o run -- python3 tools/prof_kernels.py $t --reps 1 ;;
     c5) step c5 400 python3 tools/bench_stream.py ;;
+    graphprobe_*) v=${s#graphprobe_}; step $s 300 env KRCA_LIB=kubernetes-rca-system_amd/lib/dbg/libkrca_gdbg.so python3 -u tools/graph_replay_probe.py --junk ${v%%_*} --launches ${v##*_} ;;
+    graphprobeoff_*) v=${s#graphprobeoff_}; step $s 300 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 KRCA_LIB=kubernetes-rca-system_amd/lib/dbg/libkrca_gdbg.so python3 -u tools/graph_replay_probe.py --junk ${v%%_*} --launches ${v##*_} ;;
     pmcmfma) step pmcmfma 1000 env PODS="${PODS:-100000 1000000}" tools/gpu_pmc_mfma.sh $TAG/pmcmfma ;;
     pmcx_*) step $s 1000 env TARGETS="${s#pmcx_}" tools/gpu_pmc_exact.sh $TAG/$s ;;
     cumask) step cumask 600 python3 -u tools/cu_mask_probe.py ;;
