@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32,
 // |Q z| is ~0.26 of |z| (tools: the band experiment in DESIGN.md §3.5), so 2.5x fewer pairs read a
 // partner row.  Every quantity is float64 (rounded up where it bounds; +1e-9 covers the float64
 // sums, as everywhere in the re-score), so the decision is the exact one.
-constexpr int KP = 32;  // basis vectors: proj[p] = B z_p (KP floats) | B e_p (KP floats)
+constexpr int KP = 16;  // basis vectors: proj[p] = B z_p (KP floats) | B e_p (KP floats)
 __global__ __launch_bounds__(TPB) void corr_dct_basis(double* __restrict__ B, int T) {
   const int64_t n = (int64_t)KP * T;
   for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
@@ -1098,21 +1098,27 @@ __global__ __launch_bounds__(TPB) void corr_dct_basis(double* __restrict__ B, in
   }
 }
 
-// 64 rows per workgroup, 4 lanes per row (each a quarter of every 64-step chunk), the chunk's basis
-// columns in LDS; float64 sums, combined over the 4 lanes by shuffles
-constexpr int PJ_ROWS = 64, PJ_TC = 64;
+// 64 rows per workgroup: wave jg owns basis vectors [jg KP/4, (jg + 1) KP/4) and lane r row r, over
+// every step, so a basis value is one broadcast LDS read per wave and a row value one conflict-free
+// read per lane (a handful of float64 sums per lane).  (R6c/R6d: a lane per row quarter of the steps
+// with all KP sums held 256 registers, 3.5 ms at C3; lanes of four basis groups per wave read four
+// basis rows 512 B apart, a 4-way bank conflict per read, 1.08 ms.)
+constexpr int PJ_ROWS = 64, PJ_TC = 64, PJ_J = KP / 4;
+static_assert(TPB == 4 * PJ_ROWS, "four waves: one per basis group");
 __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, const uint16_t* __restrict__ zh,
                                                  int64_t P, int T, int Tp, const double* __restrict__ B,
                                                  float* __restrict__ proj, float* __restrict__ pqz,
                                                  float* __restrict__ pqe) {
-  __shared__ double sB[KP][PJ_TC + 1];
+  __shared__ double sB[KP][PJ_TC];
   __shared__ float sz[PJ_ROWS][PJ_TC + 1];
   __shared__ float se[PJ_ROWS][PJ_TC + 1];
-  const int tid = threadIdx.x, r = tid >> 2, part = tid & 3;
+  __shared__ double sn[4][PJ_ROWS][2];  // per basis group: |B z|^2, |B e|^2 of its vectors
+  const int tid = threadIdx.x, r = tid & 63;
+  const int jg = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t p0 = (int64_t)blockIdx.x * PJ_ROWS;
-  double bz[KP], be[KP];
+  double bz[PJ_J], be[PJ_J];
 #pragma unroll
-  for (int j = 0; j < KP; ++j) bz[j] = be[j] = 0.0;
+  for (int j = 0; j < PJ_J; ++j) bz[j] = be[j] = 0.0;
   double nz = 0.0, ne = 0.0;
   for (int t0 = 0; t0 < T; t0 += PJ_TC) {
     __syncthreads();
@@ -1132,46 +1138,42 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
       se[rr][t] = e;
     }
     __syncthreads();
-    for (int t = part; t < PJ_TC; t += 4) {
+#pragma unroll 4
+    for (int t = 0; t < PJ_TC; ++t) {
       const double z = (double)sz[r][t], e = (double)se[r][t];
       nz += z * z;
       ne += e * e;
 #pragma unroll
-      for (int j = 0; j < KP; ++j) {
-        const double b = sB[j][t];
+      for (int j = 0; j < PJ_J; ++j) {
+        const double b = sB[jg * PJ_J + j][t];  // wave-uniform: a broadcast
         bz[j] += z * b;
         be[j] += e * b;
       }
     }
   }
-  auto sum4 = [](double v) {
-    v += __shfl_xor(v, 1, 4);
-    v += __shfl_xor(v, 2, 4);
-    return v;
-  };
-  nz = sum4(nz);
-  ne = sum4(ne);
   double nbz = 0.0, nbe = 0.0;
 #pragma unroll
-  for (int j = 0; j < KP; ++j) {
-    bz[j] = sum4(bz[j]);
-    be[j] = sum4(be[j]);
+  for (int j = 0; j < PJ_J; ++j) {
     nbz += bz[j] * bz[j];
     nbe += be[j] * be[j];
   }
+  sn[jg][r][0] = nbz;
+  sn[jg][r][1] = nbe;
   const int64_t p = p0 + r;
-  if (p >= P) return;
-  float* out = proj + p * (2 * KP);
+  if (p < P) {
+    float* out = proj + p * (2 * KP);
 #pragma unroll
-  for (int j = 0; j < KP; ++j) {  // each of the row's 4 lanes writes a quarter
-    if ((j & 3) == part) {
-      out[j] = (float)bz[j];
-      out[KP + j] = (float)be[j];
+    for (int j = 0; j < PJ_J; ++j) {
+      out[jg * PJ_J + j] = (float)bz[j];
+      out[KP + jg * PJ_J + j] = (float)be[j];
     }
   }
-  if (part == 0) {  // |Q x| = sqrt(|x|^2 - |B x|^2), rounded up (+1e-12 inside: float64 sums, B's rounding)
-    pqz[p] = (float)(sqrt(fmax(nz - nbz, 0.0) + 1e-12) * (1.0 + 1e-6));
-    pqe[p] = (float)(sqrt(fmax(ne - nbe, 0.0) + 1e-24) * (1.0 + 1e-6));
+  __syncthreads();
+  if (jg == 0 && p < P) {  // |Q x| = sqrt(|x|^2 - |B x|^2), rounded up (+ the float64 sums' and B's rounding)
+    const double bz2 = sn[0][r][0] + sn[1][r][0] + sn[2][r][0] + sn[3][r][0];
+    const double be2 = sn[0][r][1] + sn[1][r][1] + sn[2][r][1] + sn[3][r][1];
+    pqz[p] = (float)(sqrt(fmax(nz - bz2, 0.0) + 1e-12) * (1.0 + 1e-6));
+    pqe[p] = (float)(sqrt(fmax(ne - be2, 0.0) + 1e-24) * (1.0 + 1e-6));
   }
 }
 
@@ -1310,6 +1312,7 @@ __global__ __launch_bounds__(TPB) void corr_amb_scatter(const int2* __restrict__
 // one wave per row pod with entries (persistent over the pods): its z32 row into the wave's LDS
 // slot, then 4 groups of 16 lanes take its partners, corr_amb_rescore's decision for each
 constexpr int RS_WAVES = TPB / 64;
+constexpr int RS_QCAP = 64;  // pairs queued per wave for the row path
 __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* __restrict__ goff, const int2* __restrict__ gs,
                                                                 int64_t P, const float* __restrict__ z32,
                                                                 const float* __restrict__ dn, int T, float tau,
@@ -1319,6 +1322,7 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* _
                                                                 const float* __restrict__ nrm, const float* __restrict__ proj,
                                                                 const float* __restrict__ pqz, const float* __restrict__ pqe) {
   extern __shared__ float4 rs_lds[];
+  __shared__ int32_t rs_queue[RS_WAVES][RS_QCAP];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane & 15, grp = lane >> 4;
   const int T4 = (T + 3) / 4;
   const int L4 = zq ? Tq / 4 : T4;  // floats per wave slot / 4 (the int16 dot reads zeros past T)
@@ -1338,53 +1342,85 @@ __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* _
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const double sa = (double)dn[a];
     const double na = zq ? (double)nrm[a] : 0.0;
-    // the row pod's projections for the projection bound: lane sub < 8 holds B e_a (pairs with the
-    // partner's B z), sub >= 8 holds B z_a (pairs with the partner's B e): one float4 each
-    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the row pod's projections for the projection bound: lane sub < 8 holds 2 floats of B e_a (they
+    // pair with the partner's B z), sub >= 8 2 floats of B z_a (with the partner's B e)
+    float2 pa = make_float2(0.f, 0.f);
     double qza = 0.0, qea = 0.0;
     if (proj) {
-      pa = reinterpret_cast<const float4*>(proj + a * (2 * KP))[sub ^ 8];
+      static_assert(2 * KP == 32, "16 lanes x 2 floats hold a row's projections");
+      pa = reinterpret_cast<const float2*>(proj + a * (2 * KP))[sub ^ 8];
       qza = (double)pqz[a];
       qea = (double)pqe[a];
     }
     int hits = 0;
-    for (int32_t q = e0 + grp; q < e1; q += 4) {
-      const int2 e = gs[q];
-      const int64_t b = e.x & (AMB_BOTH - 1);
-      const double sb = (double)dn[b];
-      const double band = sa + sb + 3.0 * sa * sb + (double)acc_err + 1e-9;
-      const double v = fabs((double)__int_as_float(e.y));
-      int hit;
-      if (v > (double)tau + band) {
-        hit = 1;
-      } else if (v <= (double)tau - band) {
-        hit = 0;
-      } else {
-        // int16 partner row first: |za . qs_b zq_b - za . zb| <= nrm_a qn_b, so outside that band
-        // (+ 1e-9 for the float64 sums) the exact float64 product is on the same side of tau; the
-        // fp32 partner row only inside it (uniform over the 16-lane group)
-        int dec = -1;
-        if (proj) {  // the projection bound first (256 B of the partner instead of its row)
-          const float4 pb = reinterpret_cast<const float4*>(proj + b * (2 * KP))[sub];
-          double c = (double)pa.x * (double)pb.x + (double)pa.y * (double)pb.y + (double)pa.z * (double)pb.z +
-                     (double)pa.w * (double)pb.w;
+    // the decision of one listed pair from the rows (int16 partner row, then the fp32 one within its
+    // bound): uniform over the 16-lane group
+    auto from_rows = [&](int64_t b) -> int {
+      int dec = -1;
+      if (zq) {  // |za . qs_b zq_b - za . zb| <= nrm_a qn_b (+ 1e-9 for the float64 sums)
+        const double vq = fabs(dot16_q16(ra, zq + b * Tq, Tq, sub) * (double)qs[b]);
+        const double bq = na * (double)qn[b] + 1e-9;
+        dec = vq > (double)tau + bq ? 1 : vq <= (double)tau - bq ? 0 : -1;
+      }
+      return dec >= 0 ? dec : (fabs(dot16_f64_pf(ra, z32 + b * T, T, sub)) > (double)tau ? 1 : 0);
+    };
+    auto credit = [&](int hit, int2 e) {
+      if (sub == 0 && hit) {
+        ++hits;
+        if (e.x & AMB_BOTH) atomicAdd(&count[(int64_t)(e.x & (AMB_BOTH - 1))], 1);
+      }
+    };
+    // Pass 1: the pair's own bound, then the projection bound; the pairs neither settles go to the
+    // wave's queue, which pass 2 drains with all four groups busy (a group waiting on a partner row
+    // while the other three had settled theirs kept the wave for as long as the row path: R6c)
+    int32_t* wq = rs_queue[wv];
+    int nq = 0;  // wave-uniform
+    auto drain = [&]() {
+      for (int base = 0; base < nq; base += 4) {  // wave-uniform trip count
+        const int i = base + grp;
+        if (i < nq) {  // uniform over the group
+          const int2 e = gs[wq[i]];
+          credit(from_rows(e.x & (AMB_BOTH - 1)), e);
+        }
+      }
+      nq = 0;
+    };
+    for (int32_t base = e0; base < e1; base += 4) {
+      const int32_t q = base + grp;
+      int need = 0;
+      if (q < e1) {  // uniform over the group
+        const int2 e = gs[q];
+        const int64_t b = e.x & (AMB_BOTH - 1);
+        const double sb = (double)dn[b];
+        const double band = sa + sb + 3.0 * sa * sb + (double)acc_err + 1e-9;
+        const double v = fabs((double)__int_as_float(e.y));
+        int dec = v > (double)tau + band ? 1 : v <= (double)tau - band ? 0 : -1;
+        if (dec < 0 && proj) {  // 128 B of the partner instead of its row
+          const float2 pb = reinterpret_cast<const float2*>(proj + b * (2 * KP))[sub];
+          double c = (double)pa.x * (double)pb.x + (double)pa.y * (double)pb.y;
           for (int off = 8; off > 0; off >>= 1) c += __shfl_xor(c, off, 16);
           const double est = fabs((double)__int_as_float(e.y) + c);
           const double bp = qza * (double)pqe[b] + qea * (double)pqz[b] + sa * sb + (double)acc_err + 1e-9;
           dec = est > (double)tau + bp ? 1 : est <= (double)tau - bp ? 0 : -1;
         }
-        if (zq && dec < 0) {
-          const double vq = fabs(dot16_q16(ra, zq + b * Tq, Tq, sub) * (double)qs[b]);
-          const double bq = na * (double)qn[b] + 1e-9;
-          dec = vq > (double)tau + bq ? 1 : vq <= (double)tau - bq ? 0 : -1;
-        }
-        hit = dec >= 0 ? dec : fabs(dot16_f64_pf(ra, z32 + b * T, T, sub)) > (double)tau;
+        if (dec >= 0) credit(dec, e);
+        else need = 1;
       }
-      if (sub == 0 && hit) {
-        ++hits;
-        if (e.x & AMB_BOTH) atomicAdd(&count[b], 1);
+      const uint64_t m = __ballot(need && sub == 0);  // one bit per group that queues its pair
+      if (need && sub == 0)
+        wq[nq + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = q;
+      nq += __builtin_popcountll(m);
+      if (nq > RS_QCAP - 4) {  // wave-uniform
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        drain();
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    drain();
     if (sub == 0 && hits) atomicAdd(&count[a], hits);
     // every lane is past its partners before the next pod's row lands in the slot
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -48,7 +48,12 @@ __device__ __forceinline__ uint64_t fnv_mask(uint64_t h) { return fnv(h, kMaskBy
 // The table image (tmpl_dfa.h: kRows x 256 one-byte entries = the next row's index, flags encoded
 // in the row ranges), built at compile time; a workgroup copies it into LDS with 16-byte loads
 // (filling it entry by entry from class tests cost each wave ~550 instructions, R5zt).
-__device__ constexpr tdfa::Table kTable = tdfa::make_table();
+#ifdef KRCA_TMPL_SWZ  // A/B build (make tswz): the bank-swizzled table layout
+constexpr bool kSwz = true;
+#else
+constexpr bool kSwz = false;
+#endif
+__device__ constexpr tdfa::Table kTable = tdfa::make_table<kSwz>();
 constexpr int kTableBytes = tdfa::kRows * 256;
 static_assert(kTableBytes % 16 == 0, "16-byte copy");
 template <int NT>
@@ -89,7 +94,19 @@ __device__ __forceinline__ void tflags(uint32_t t, uint64_t& h, uint64_t& hb, ui
 // byte k of dword w; st = the current row index
 __device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32_t w, int k, uint32_t& st,
                                            uint64_t& h, uint64_t& hb, uint64_t& hu) {
-  const uint32_t t = T[__builtin_amdgcn_perm(st, w, 0x0c0c0400u | (uint32_t)k)];  // (st << 8) | byte k
+  uint32_t t;
+  if constexpr (kSwz) {  // (st << 8) | (byte k ^ st): one SDWA xor, one shift-or
+    uint32_t x;
+    switch (k) {
+      case 0: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(x) : "v"(st), "v"(w)); break;
+      case 1: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(x) : "v"(st), "v"(w)); break;
+      case 2: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(x) : "v"(st), "v"(w)); break;
+      default: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(x) : "v"(st), "v"(w)); break;
+    }
+    t = T[(st << 8) | x];
+  } else {
+    t = T[__builtin_amdgcn_perm(st, w, 0x0c0c0400u | (uint32_t)k)];  // (st << 8) | byte k
+  }
   tflags(t, h, hb, hu);
   h = fnv_mul(xor_byte(h, w, k));
   st = t;
@@ -97,7 +114,7 @@ __device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32
 // the end of a line: the flags of the transition on a non-word byte, without hashing it
 __device__ __forceinline__ void tstep_end(const uint8_t* __restrict__ T, uint32_t st, uint64_t& h, uint64_t& hb,
                                           uint64_t& hu) {
-  tflags(T[(st << 8) | tdfa::kEndByte], h, hb, hu);
+  tflags(T[(st << 8) | (kSwz ? (tdfa::kEndByte ^ st) : tdfa::kEndByte)], h, hb, hu);
 }
 
 // the template hash of line [s, e) read byte by byte from the text, the table from global memory
@@ -109,7 +126,7 @@ __device__ __forceinline__ uint64_t line_hash_global(const uint8_t* __restrict__
   e = e < nbytes ? e : nbytes;
   for (int64_t q = s; q < e; ++q) {
     const uint32_t b = text[q];
-    const uint32_t t = kTable.v[(st << 8) | b];
+    const uint32_t t = kTable.v[(st << 8) | (kSwz ? (b ^ st) : b)];
     tflags(t, h, hb, hu);
     h = fnv(h, b);
     st = t;

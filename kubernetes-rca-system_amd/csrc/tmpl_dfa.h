@@ -124,12 +124,16 @@ constexpr uint32_t kEndByte = ' ';
 struct Table {
   alignas(16) uint8_t v[kRows * 256];
 };
+// SWZ: entry (r, b) at (r << 8) | (b ^ r) instead of (r << 8) | b, so that lanes in different rows
+// reading the same byte value fall in different LDS banks (r < 128: b ^ r stays in the row)
+template <bool SWZ = false>
 __host__ __device__ constexpr Table make_table() {
   Table t{};
   for (int r = 0; r < kRows; ++r)
-    for (uint32_t b = 0; b < 256; ++b) t.v[r * 256 + b] = (uint8_t)next_row(r, b);
+    for (uint32_t b = 0; b < 256; ++b) t.v[r * 256 + (SWZ ? (b ^ (uint32_t)r) : b)] = (uint8_t)next_row(r, b);
   return t;
 }
+static_assert(kRows <= 128, "the swizzled layout XORs the row index into the byte");
 
 // one byte of the walk (the kernel's form, written out in template.hip with its register tricks)
 template <class Mask>
