@@ -302,6 +302,22 @@ def pmc_traffic(args, bytes_alg, world):
         return None, None
 
 
+def corr_pmc(P):
+    """The correlation's counters at P pods from profiles/pmc_mfma_latest.json (tools/gpu_pmc_mfma.sh):
+    DRAM-side bytes per call and the main pass's MFMA-busy fraction at the held clock, or Nones."""
+    f = os.path.join(ROOT, "profiles", "pmc_mfma_latest.json")
+    try:
+        e = json.load(open(f))["pods"][str(P)]
+        m = e["main_pass"]
+        return {"traffic": e["dram_bytes_per_call"],
+                "traffic_source": f"measured: rocprofv3 PMC passes at this shape ({os.path.relpath(f, ROOT)}, "
+                                  f"call {json.load(open(f))['source']})",
+                "mfma_busy_main_pass": m["mfma_busy_at_held_clock"], "mfma_busy_main_pass_vs_2p4ghz": m["mfma_busy_vs_2p4ghz"],
+                "main_pass_clock_ghz": m["clock_ghz"]}
+    except Exception:  # noqa: BLE001
+        return {"traffic": None}
+
+
 def verify_step(args, cfg, mesh, shard, x, part, ppart, rank):
     """Untimed parity of the last step at any N: every rank's fixed-point ranks (its rows of
     `ppart`) and scores (its pods of `part`) are gathered to rank 0 and compared with the C oracle
@@ -512,7 +528,8 @@ def corr_leg(args, eng, world, rank, local):
             "parallelism": "one device" if world == 1 else f"pod-sharded super-tiles x{world} (krca/corr_dist.py)",
             "roofline": {"kernel": "krca_corr_topk (prepare + screening + merges + exact-count re-score)",
                          "bound": "mfma", "achieved": tflops, "peak": MFMA_PEAK_TFLOPS * world, "unit": "TFLOP/s",
-                         "frac": tflops / (MFMA_PEAK_TFLOPS * world), "algorithmic_flop": flop, "traffic": None},
+                         "frac": tflops / (MFMA_PEAK_TFLOPS * world), "algorithmic_flop": flop,
+                         **(corr_pmc(P) if world == 1 else {"traffic": None})},
             "verify": {"rows_checked": int(bad[4]), "counts_exact": bad[0] == 0, "sets_exact": bad[1] == 0,
                        "values_exact": bad[2] == 0, "all_certified": bad[3] == 0,
                        "reference": "float64 products of the device's z32 rows (bit-identical to the C twin)"}}

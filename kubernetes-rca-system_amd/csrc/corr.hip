@@ -342,6 +342,8 @@ struct TileArgs {
   const float* phi;  // MAIN: candidate bound per pod; RECT: phi2
   float* samp_v;
   int32_t* samp_i;
+  const float* samp_run;  // SAMPLE, chunks after the first: the running top-k |r| (corr_theta), else null
+  int k;
   float* selfd;
   int2* buf;
   int32_t* cnt;
@@ -841,9 +843,13 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       // value below 0.25 made a live pod "flat": its top-k the lowest indices)
       const int self = (g < P && g >= c0 && g < c0 + BM) ? (int)(g - c0) : -1;
       if (self >= 0 && (self >= BM / 2) == (part == 1)) A.selfd[g] = rowp[self];  // before part 1's list lands
+      // a later chunk of the sample: only values above the running k-th best of the chunks before
+      // can change the k-th best of the whole sample (corr_theta keeps the running values), so the
+      // lists start at that floor and the scan skips everything below it with one compare
+      const float floor_ = (active && A.samp_run) ? A.samp_run[g * KMAX + A.k - 1] : -1.f;
       if (active) {
         const int cend = (int)std::min<int64_t>(BM, P - c0);
-        float lim = -1.f;
+        float lim = floor_;
         const int cb = part * (BM / 2), ce = std::min(cend, cb + BM / 2);
         for (int c4 = cb; c4 < ce; c4 += 4) {
           const float4 q4 = *reinterpret_cast<const float4*>(rowp + c4);
@@ -853,7 +859,7 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
             const float vu = u == 0 ? q4.x : u == 1 ? q4.y : u == 2 ? q4.z : q4.w;
             if (c < ce && c != self && fabsf(vu) > lim) {
               cd.insert(vu, (int32_t)(c0 + c));
-              lim = cd.thr;
+              lim = fmaxf(cd.thr, floor_);
             }
           }
         }
@@ -868,14 +874,14 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       static_assert(2 * KC <= BM / 2, "part 1's list fits in its columns");
       __syncthreads();
       if (active && part == 0) {
-        float lim = cd.thr;
+        float lim = fmaxf(cd.thr, floor_);
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
           const float vu = rowp[BM / 2 + 2 * q];
           const int32_t iq = __float_as_int(rowp[BM / 2 + 2 * q + 1]);
           if (iq >= 0 && fabsf(vu) > lim) {
             cd.insert(vu, iq);
-            lim = cd.thr;
+            lim = fmaxf(cd.thr, floor_);
           }
         }
         const int64_t slot = g * NSL + (own ? NSB + ch : jb);
@@ -1949,6 +1955,8 @@ int stage_sample(const uint16_t* zh, const Dims& d, int64_t lo, int64_t n, const
     ta.nsb = nsb_c;
     ta.samp_v = ws.samp_v;
     ta.samp_i = ws.samp_i;
+    ta.samp_run = c0 > 0 ? ws.run : nullptr;  // (written by corr_theta after the previous chunk)
+    ta.k = d.k;
     ta.selfd = ws.selfd;
     ta.sh = sh;
     ta.debug = debug_mode();

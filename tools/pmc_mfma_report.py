@@ -70,6 +70,10 @@ def main():
                     e["mfma_busy_vs_2p4ghz"] = g["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0 / (2.4 * ns)
             if g.get("TCC_EA0_RDREQ_DRAM_32B") is not None:
                 e["dram_bytes"] = 32.0 * (g["TCC_EA0_RDREQ_DRAM_32B"] + g.get("TCC_EA0_WRREQ_WRITE_DRAM_32B", 0.0))
+                rd, wr = c2[k]["TCC_EA0_RDREQ_DRAM_32B"], c2[k].get("TCC_EA0_WRREQ_WRITE_DRAM_32B", {})
+                d2 = sorted(rd.keys(), key=int)
+                d2 = d2[len(d2) // 2:] if len(d2) > 1 else d2  # the timed call's dispatches
+                e["dram_bytes_call_total"] = 32.0 * sum(rd[x] + wr.get(x, 0.0) for x in d2)
             out[k] = e
         res[str(pods)] = out
     txt = json.dumps(res, indent=1, sort_keys=True)
