@@ -1126,22 +1126,37 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
 #pragma unroll
   for (int j = 0; j < PJ_J; ++j) bz[j] = be[j] = 0.0;
   double nz = 0.0, ne = 0.0;
+  constexpr int NB = KP * PJ_TC / TPB, NZ = PJ_ROWS * PJ_TC / TPB;  // loads per lane and chunk
   for (int t0 = 0; t0 < T; t0 += PJ_TC) {
-    __syncthreads();
-    for (int i = tid; i < KP * PJ_TC; i += TPB) {
-      const int j = i / PJ_TC, t = i % PJ_TC;
-      sB[j][t] = t0 + t < T ? B[(int64_t)j * T + t0 + t] : 0.0;
+    // every load of the chunk issued before any is used (a loop of dependent load -> store rounds
+    // paid one memory latency per round: 0.96 ms at C3, R6e)
+    double bv[NB];
+    float zv[NZ];
+    uint16_t hv[NZ];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = tid + u * TPB, j = i / PJ_TC, t = i % PJ_TC;
+      bv[u] = t0 + t < T ? B[(int64_t)j * T + t0 + t] : 0.0;
     }
-    for (int i = tid; i < PJ_ROWS * PJ_TC; i += TPB) {  // coalesced along t
-      const int rr = i / PJ_TC, t = i % PJ_TC;
+#pragma unroll
+    for (int u = 0; u < NZ; ++u) {  // coalesced along t
+      const int i = tid + u * TPB, rr = i / PJ_TC, t = i % PJ_TC;
       const int64_t p = p0 + rr;
-      float z = 0.f, e = 0.f;
-      if (p < P && t0 + t < T) {
-        z = z32[p * T + t0 + t];
-        e = (float)((double)z - (double)(float)__builtin_bit_cast(_Float16, zh[p * Tp + t0 + t]));  // exact
-      }
-      sz[rr][t] = z;
-      se[rr][t] = e;
+      const bool in = p < P && t0 + t < T;
+      zv[u] = in ? z32[p * T + t0 + t] : 0.f;
+      hv[u] = in ? zh[p * Tp + t0 + t] : (uint16_t)0;
+    }
+    __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = tid + u * TPB;
+      sB[i / PJ_TC][i % PJ_TC] = bv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NZ; ++u) {
+      const int i = tid + u * TPB, rr = i / PJ_TC, t = i % PJ_TC;
+      sz[rr][t] = zv[u];
+      se[rr][t] = (float)((double)zv[u] - (double)(float)__builtin_bit_cast(_Float16, hv[u]));  // exact
     }
     __syncthreads();
 #pragma unroll 4

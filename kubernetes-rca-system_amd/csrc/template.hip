@@ -48,18 +48,24 @@ __device__ __forceinline__ uint64_t fnv_mask(uint64_t h) { return fnv(h, kMaskBy
 // The table image (tmpl_dfa.h: kRows x 256 one-byte entries = the next row's index, flags encoded
 // in the row ranges), built at compile time; a workgroup copies it into LDS with 16-byte loads
 // (filling it entry by entry from class tests cost each wave ~550 instructions, R5zt).
-#ifdef KRCA_TMPL_SWZ  // A/B build (make tswz): the bank-swizzled table layout
-constexpr bool kSwz = true;
+#ifdef KRCA_TMPL_CLS  // A/B build (make tcls): the machine over byte classes (1.1 KB table)
+constexpr bool kCls = true;
+__device__ constexpr tdfa::ClsTable kClsTable = tdfa::make_cls_table();
+constexpr int kTableBytes = (int)sizeof(tdfa::ClsTable);
 #else
-constexpr bool kSwz = false;
-#endif
-__device__ constexpr tdfa::Table kTable = tdfa::make_table<kSwz>();
+constexpr bool kCls = false;
 constexpr int kTableBytes = tdfa::kRows * 256;
+#endif
+__device__ constexpr tdfa::Table kTable = tdfa::make_table();
 static_assert(kTableBytes % 16 == 0, "16-byte copy");
 template <int NT>
 __device__ __forceinline__ void load_table(uint8_t* __restrict__ tstate) {  // (the caller syncs)
-  for (int i = threadIdx.x; i < kTableBytes / 16; i += NT)
-    reinterpret_cast<uint4*>(tstate)[i] = reinterpret_cast<const uint4*>(kTable.v)[i];
+#ifdef KRCA_TMPL_CLS
+  const uint4* src = reinterpret_cast<const uint4*>(&kClsTable);
+#else
+  const uint4* src = reinterpret_cast<const uint4*>(kTable.v);
+#endif
+  for (int i = threadIdx.x; i < kTableBytes / 16; i += NT) reinterpret_cast<uint4*>(tstate)[i] = src[i];
 }
 
 // h ^ byte k of w in one instruction (the byte read in place as a sub-dword operand; the compiler
@@ -95,15 +101,9 @@ __device__ __forceinline__ void tflags(uint32_t t, uint64_t& h, uint64_t& hb, ui
 __device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32_t w, int k, uint32_t& st,
                                            uint64_t& h, uint64_t& hb, uint64_t& hu) {
   uint32_t t;
-  if constexpr (kSwz) {  // (st << 8) | (byte k ^ st): one SDWA xor, one shift-or
-    uint32_t x;
-    switch (k) {
-      case 0: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(x) : "v"(st), "v"(w)); break;
-      case 1: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(x) : "v"(st), "v"(w)); break;
-      case 2: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(x) : "v"(st), "v"(w)); break;
-      default: asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(x) : "v"(st), "v"(w)); break;
-    }
-    t = T[(st << 8) | x];
+  if constexpr (kCls) {  // class map (independent of the state), then (st << 3) | class
+    const uint32_t c = T[__builtin_amdgcn_perm(0u, w, 0x0c0c0c00u | (uint32_t)k)];
+    t = T[256 + ((st << 3) | c)];
   } else {
     t = T[__builtin_amdgcn_perm(st, w, 0x0c0c0400u | (uint32_t)k)];  // (st << 8) | byte k
   }
@@ -114,7 +114,7 @@ __device__ __forceinline__ void tstep_rows(const uint8_t* __restrict__ T, uint32
 // the end of a line: the flags of the transition on a non-word byte, without hashing it
 __device__ __forceinline__ void tstep_end(const uint8_t* __restrict__ T, uint32_t st, uint64_t& h, uint64_t& hb,
                                           uint64_t& hu) {
-  tflags(T[(st << 8) | (kSwz ? (tdfa::kEndByte ^ st) : tdfa::kEndByte)], h, hb, hu);
+  tflags(T[kCls ? 256 + ((st << 3) | tdfa::C_OTHER) : (st << 8) | tdfa::kEndByte], h, hb, hu);
 }
 
 // the template hash of line [s, e) read byte by byte from the text, the table from global memory
@@ -126,12 +126,12 @@ __device__ __forceinline__ uint64_t line_hash_global(const uint8_t* __restrict__
   e = e < nbytes ? e : nbytes;
   for (int64_t q = s; q < e; ++q) {
     const uint32_t b = text[q];
-    const uint32_t t = kTable.v[(st << 8) | (kSwz ? (b ^ st) : b)];
+    const uint32_t t = kTable.v[(st << 8) | b];
     tflags(t, h, hb, hu);
     h = fnv(h, b);
     st = t;
   }
-  tstep_end(kTable.v, st, h, hb, hu);
+  tflags(kTable.v[(st << 8) | tdfa::kEndByte], h, hb, hu);
   return h;
 }
 

@@ -124,16 +124,27 @@ constexpr uint32_t kEndByte = ' ';
 struct Table {
   alignas(16) uint8_t v[kRows * 256];
 };
-// SWZ: entry (r, b) at (r << 8) | (b ^ r) instead of (r << 8) | b, so that lanes in different rows
-// reading the same byte value fall in different LDS banks (r < 128: b ^ r stays in the row)
-template <bool SWZ = false>
 __host__ __device__ constexpr Table make_table() {
   Table t{};
   for (int r = 0; r < kRows; ++r)
-    for (uint32_t b = 0; b < 256; ++b) t.v[r * 256 + (SWZ ? (b ^ (uint32_t)r) : b)] = (uint8_t)next_row(r, b);
+    for (uint32_t b = 0; b < 256; ++b) t.v[r * 256 + b] = (uint8_t)next_row(r, b);
   return t;
 }
-static_assert(kRows <= 128, "the swizzled layout XORs the row index into the byte");
+// The same machine over byte CLASSES (next_row depends on a byte only through cls_of): a 256-byte
+// class map, then kRows x 8 entries (1.1 KB instead of 25.5 KB; the A/B build of template.hip)
+struct ClsTable {
+  alignas(16) uint8_t cls[256];
+  uint8_t v[kRows * 8];
+  uint8_t pad[(16 - (kRows * 8) % 16) % 16];
+};
+__host__ __device__ constexpr ClsTable make_cls_table() {
+  ClsTable t{};
+  constexpr uint32_t rep[5] = {'0', 'a', 'g', '-', ' '};  // one byte of each class
+  for (uint32_t b = 0; b < 256; ++b) t.cls[b] = (uint8_t)cls_of(b);
+  for (int r = 0; r < kRows; ++r)
+    for (int c = 0; c < 8; ++c) t.v[r * 8 + c] = (uint8_t)next_row(r, rep[c < 5 ? c : 4]);
+  return t;
+}
 
 // one byte of the walk (the kernel's form, written out in template.hip with its register tricks)
 template <class Mask>

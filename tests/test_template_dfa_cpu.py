@@ -21,13 +21,16 @@ def dfa(tmp_path_factory):
     subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", CSRC,
                     os.path.join(HERE, "host", "tmpl_dfa_host.cpp"), "-o", out], check=True)
     lib = ctypes.CDLL(out)
-    lib.tdfa_line_hash.restype = ctypes.c_uint64
-    lib.tdfa_line_hash.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    for fn in (lib.tdfa_line_hash, lib.tdfa_line_hash_cls):
+        fn.restype = ctypes.c_uint64
+        fn.argtypes = [ctypes.c_char_p, ctypes.c_int64]
     return lib
 
 
 def _hash(lib, b):
-    return lib.tdfa_line_hash(b, len(b))
+    h = lib.tdfa_line_hash(b, len(b))
+    assert lib.tdfa_line_hash_cls(b, len(b)) == h, b  # the byte-class table walks the same machine
+    return h
 
 
 def test_dfa_table_shape(dfa):
