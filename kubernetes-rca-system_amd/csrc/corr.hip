@@ -1162,21 +1162,23 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
 #pragma unroll 4
     for (int t = 0; t < PJ_TC; ++t) {
       const double z = (double)sz[r][t], e = (double)se[r][t];
-      nz += z * z;
-      ne += e * e;
+      // explicit fused multiply-adds (the library builds with -ffp-contract=off: a * b + c is a
+      // multiply and an add there, twice the instructions on this float64 loop)
+      nz = fma(z, z, nz);
+      ne = fma(e, e, ne);
 #pragma unroll
       for (int j = 0; j < PJ_J; ++j) {
         const double b = sB[jg * PJ_J + j][t];  // wave-uniform: a broadcast
-        bz[j] += z * b;
-        be[j] += e * b;
+        bz[j] = fma(z, b, bz[j]);
+        be[j] = fma(e, b, be[j]);
       }
     }
   }
   double nbz = 0.0, nbe = 0.0;
 #pragma unroll
   for (int j = 0; j < PJ_J; ++j) {
-    nbz += bz[j] * bz[j];
-    nbe += be[j] * be[j];
+    nbz = fma(bz[j], bz[j], nbz);
+    nbe = fma(be[j], be[j], nbe);
   }
   sn[jg][r][0] = nbz;
   sn[jg][r][1] = nbe;

@@ -10,6 +10,7 @@
 #   c5           tools/bench_stream.py (C5 window)   g8           tools/g8_step_emulation.py --decoupled
 #   graphprobe_J_N / graphprobeoff_J_N  tools/graph_replay_probe.py (--junk J --launches N) with packet capture on / off
 #   tmplcls      template tests + kernel stats with the byte-class table build (lib/dbg/libkrca_tcls.so)
+#   tmplr5       template kernel stats with the round-5 hash kernel (lib/dbg/libkrca_tr5.so; its hashes ignore UUIDs)
 #   pmclds_V_T   LDS / issue counters of prof_kernels.py T (V = base or cls: the library)
 #   pmcmfma      tools/gpu_pmc_mfma.sh (correlation MFMA busy, clock, DRAM bytes at C3 / 1M)
 #   pmcx_T       tools/gpu_pmc_exact.sh with TARGETS=T (one target: cal ppr bench logs tmpl ...)
@@ -66,6 +67,7 @@ for s in "$@"; do
     c5) step c5 400 python3 tools/bench_stream.py ;;
     tmplcls) step tests_tmplcls 300 env KRCA_LIB=kubernetes-rca-system_amd/lib/dbg/libkrca_tcls.so python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "template or c5" &&
              KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/dbg/libkrca_tcls.so prof tmplcls 300 tools/prof_kernels.py tmpl --reps 5 ;;
+    tmplr5) KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/dbg/libkrca_tr5.so prof tmplr5 300 tools/prof_kernels.py tmpl --reps 5 ;;
     pmclds_*) t=${s#pmclds_}; lib=""; [ "${t%%_*}" = cls ] && lib=$PWD/kubernetes-rca-system_amd/lib/dbg/libkrca_tcls.so; t=${t#*_};
               step $s 150 env ${lib:+KRCA_LIB=$lib} timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $O/$s -o run -- python3 tools/prof_kernels.py $t --reps 1 ;;
     graphprobe_*) v=${s#graphprobe_}; step $s 300 env KRCA_LIB=kubernetes-rca-system_amd/lib/dbg/libkrca_gdbg.so python3 -u tools/graph_replay_probe.py --junk ${v%%_*} --launches ${v##*_} ;;
