@@ -2092,10 +2092,19 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
                      d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
   KRCA_LAUNCH_CHECK();
   if (proj_bound()) {
-    hipLaunchKernelGGL(corr_dct_basis, dim3((unsigned)krca::ceil_div((int64_t)KP * d.T, TPB)), dim3(TPB), 0, st, ws.dct,
+    // only the re-score reads the projections: on the side stream (ordered before every re-score
+    // there), beside the main pass rather than in front of it (0.3-1 ms of C3's critical path)
+    hipStream_t ps = st;
+    if (sw.side != st && krca::tuning().corr_side == 0) {  // (every re-score on the side stream)
+      KRCA_HIP(hipEventRecord(sw.ev[4], st));  // (ev[4] is re-recorded on the side stream at the join)
+      KRCA_HIP(hipStreamWaitEvent(sw.side, sw.ev[4], 0));
+      sw.forked = true;
+      ps = sw.side;
+    }
+    hipLaunchKernelGGL(corr_dct_basis, dim3((unsigned)krca::ceil_div((int64_t)KP * d.T, TPB)), dim3(TPB), 0, ps, ws.dct,
                        d.T);
     KRCA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(corr_proj, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
+    hipLaunchKernelGGL(corr_proj, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)), dim3(TPB), 0, ps, z32, zh, d.P, d.T,
                        d.Tp, (const double*)ws.dct, ws.proj, ws.pqz, ws.pqe);
     KRCA_LAUNCH_CHECK();
   }
