@@ -2004,11 +2004,18 @@ inline int cand_cap() {
 
 // the grouped re-score reads int16 partner rows (written by corr_dnorm)
 inline bool q16_rows() { return krca::tuning().corr_rs_q16 && krca::tuning().corr_rs_group; }
-// ... and tries the projection bound before them (KRCA_CORR_PROJ, default on)
-inline bool proj_bound() { return krca::tuning().corr_proj && krca::tuning().corr_rs_group; }
+// ... and tries the projection bound before them (KRCA_CORR_PROJ: 1 = when the main pass runs in more
+// than one batch, the default; 2 = always; 0 = never).  The projections cost ~1 ms at C3 (100k pods,
+// one batch), where they save about as much on the re-score that runs after the main pass (R6e-g);
+// with many batches every re-score runs beside a later batch and its HBM traffic is what slows it.
+inline bool proj_bound(int64_t n_batches) {
+  const int m = krca::tuning().corr_proj;
+  return krca::tuning().corr_rs_group && (m == 2 || (m == 1 && n_batches > 1));
+}
 
 // exact |r| > tau counts of the ambiguous pairs in list l (float64 from z32), added to count
-int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int32_t* count, hipStream_t st) {
+int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int32_t* count, hipStream_t st,
+                   bool use_proj) {
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   const unsigned grid = (unsigned)std::max(8, krca::tuning().corr_rs_grid & ~7);
   const int16_t* zq = q16_rows() ? ws.zq : nullptr;
@@ -2037,7 +2044,7 @@ int launch_rescore(const float* z32, const Dims& d, const CorrWs& ws, int l, int
     hipLaunchKernelGGL(corr_amb_rescore_grouped, dim3(gg), dim3(TPB), lds, st, (const int32_t*)ws.goff,
                        (const int2*)ws.gs, d.P, z32, (const float*)ws.dn, d.T, d.tau, acc_err, count,
                        zq, ws.Tq, (const float*)ws.qs, (const float*)ws.qn, (const float*)ws.nrm,
-                       proj_bound() ? (const float*)ws.proj : nullptr, (const float*)ws.pqz, (const float*)ws.pqe);
+                       use_proj ? (const float*)ws.proj : nullptr, (const float*)ws.pqz, (const float*)ws.pqe);
     KRCA_LAUNCH_CHECK();
     return KRCA_OK;
   }
@@ -2091,7 +2098,10 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
                      d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
   KRCA_LAUNCH_CHECK();
-  if (proj_bound()) {
+  const int64_t n_st_all = n_supertiles(d.nb2);
+  const int64_t n_mine0 = n_st_all > g ? (n_st_all - g + G - 1) / G : 0;
+  const bool use_proj = proj_bound((n_mine0 + sb_batch() - 1) / sb_batch());
+  if (use_proj) {
     // only the re-score reads the projections: on the side stream (ordered before every re-score
     // there), beside the main pass rather than in front of it (0.3-1 ms of C3's critical path)
     hipStream_t ps = st;
@@ -2162,7 +2172,7 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
       KRCA_HIP(hipStreamWaitEvent(sw.side, sw.ev[l], 0));
       sw.forked = true;
     }
-    if (int rc = launch_rescore(z32, d, ws, l, count, fork ? sw.side : st)) return rc;
+    if (int rc = launch_rescore(z32, d, ws, l, count, fork ? sw.side : st, use_proj)) return rc;
     if (side_ok) KRCA_HIP(hipEventRecord(sw.ev[2 + l], fork ? sw.side : st));
   }
   return KRCA_OK;

@@ -201,9 +201,11 @@ def test_corr_batches_and_full_lists_identical(eng):
     # performance knobs that must not change a result: the grouped re-score's grid, and how many
     # candidates past the k-th the merge re-scores (fewer: more pods take the deep merge; the
     # certificate margins may differ, the sets, values and counts not)
-    # (KRCA_CORR_PROJ = 0: the grouped re-score without the projection bound; counts must not move)
+    # (KRCA_CORR_PROJ = 0 / 2: the grouped re-score never / always with the projection bound -- the
+    # default uses it only when the main pass runs in several batches; counts must not move)
     try:
-        for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2), (b"KRCA_CORR_PROJ", 0)):
+        for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2), (b"KRCA_CORR_PROJ", 0),
+                          (b"KRCA_CORR_PROJ", 2)):
             assert lib.krca_tune_set(knob, val) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
             lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 1}[knob])
