@@ -21,7 +21,7 @@
 //   log_hist          lane per container (or a wave for a large one): 13 counts, the first three
 //                     example lines per bin marked in the line masks, no atomics.
 // A/B paths (tests require identical outputs): KRCA_LOG_FUSED = 1 / 2, log_index_match walking the
-// DFA inside the index pass from the LDS-resident tile (+ log_dfa_strad for each tile's last line);
+// DFA inside the index pass from the LDS-resident tile (+ the LOOK bytes after it, for its last line);
 // KRCA_LOG_IMPL = 1, the chunk-lane log_match; = 2, the round-1 walk log_dfa_window.  When the
 // caller's line arrays are too small, krca_log_match finishes from the index in the workspace.
 #include <stdint.h>
@@ -1462,27 +1462,31 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
 // can stream its tile in while the other walks (the walk is bound by LDS throughput, the load by
 // memory latency; one 1024-thread workgroup per CU with a 64 KiB tile ran the phases one after the
 // other: 262 us against 113 + 83 us for the two-kernel path, r4e):
-//   A  each lane loads 4 pieces of 16 bytes, stores them to LDS and computes their line-start /
-//      separator-length bits (piece_flags); per 256-byte chunk counts, their scan inside the tile,
-//      the tile total published for the look-back (aggregate);
+//   A  each lane loads 4 pieces of 16 bytes, stores their symbol offsets to LDS (sym_word) and
+//      computes their line-start / separator-length bits (piece_flags); per 256-byte chunk counts,
+//      their scan inside the tile, the tile total published for the look-back (aggregate).  Wave 0
+//      also takes the LOOK bytes after the tile: the first line start there ends the tile's last line;
 //   B  the tile's lines in windows of LMAX: a list of (start, end) tile offsets in LDS built from
 //      the start bits, then a lane per line walks it with the DFA from LDS (16-byte lockstep blocks
-//      as in log_dfa); masks in LDS;
+//      as in log_dfa, no byte table for ASCII blocks); masks in LDS;
 //   C  the look-back resolves the tile's first line id (its predecessors have long published their
 //      aggregates by then), and the window's line_start / line_end / line_mask go out coalesced by
 //      line id.
-// Deferred: the tile's LAST line, whose end lies in a later tile (straddler queue -> log_dfa_strad,
-// a lane per line), and lines longer than LONG_LINE (long queue -> log_dfa_long, a wave per line).
+// Deferred to log_dfa_long (a wave per line): lines longer than LONG_LINE.
 // Two shapes (KRCA_LOG_FUSED = 1 / 2): 32 KiB tiles, 512 threads, the 16-bit table -- two
 // workgroups per CU; or 64 KiB tiles, 1024 threads, DfaLds4's 32-bit table (the category mask in
 // every entry: no branch per byte) -- one workgroup per CU, 16 waves.
+// Bytes after the tile that log_index_match loads with it: the tile's last line ends in them unless
+// it is longer than LONG_LINE (then log_dfa_long walks it), so no line of a tile waits on the next
+// tile's workgroup (round 5's log_dfa_strad: a lane per straddling line, 35-41 us per scan).
+constexpr int LOOK = LONG_LINE;
 template <int64_t TILE_B, int NT, bool U32>
 struct FCfg {
   static constexpr int64_t FTILE = TILE_B;                    // bytes per tile
   static constexpr int FTPB = NT;                             // threads
   static constexpr int FNIT = (int)(TILE_B / (NT * PIECE));   // 4 pieces of 16 bytes per lane
   static constexpr int FCH = (int)(TILE_B / CH);              // 256-byte chunks per tile
-  static constexpr int FNBW = (int)(TILE_B / 32) + 2;         // container-start bitmap words
+  static constexpr int FNBW = (int)((TILE_B + LOOK) / 32) + 2;  // container-start bitmap words (tile + LOOK)
   static constexpr int LMAX = (int)(TILE_B / 16);             // lines of a tile listed and walked per window
   static constexpr bool W32 = U32;
 };
@@ -1522,9 +1526,6 @@ __device__ __forceinline__ uint32_t dfa2_step(const DfaLds2& d, uint32_t row, ui
   return t;
 }
 
-// The DFA mask of the line at tile offsets [s, e) from the tile text in LDS (e < FTILE; the text
-// array is padded past the tile so a block may read up to 16 bytes beyond e).  Same transitions
-// as log_dfa: ASCII blocks by the byte table, others code point by code point.
 // one byte step of either table: the 32-bit one ORs its entry (mask in the high half), the 16-bit
 // one reads out[] on a reporting entry
 __device__ __forceinline__ uint32_t dstep(const DfaLds4& d, uint32_t row, uint32_t so, uint32_t& acc) {
@@ -1542,85 +1543,124 @@ __device__ __forceinline__ uint32_t dsym_scale(const DfaLds2&) { return 2; }
 __device__ __forceinline__ void dload(DfaLds4& d) { dfa4_load(d); }
 __device__ __forceinline__ void dload(DfaLds2& d) { dfa2_load(d); }
 
+// the step on symbol byte K of a word of symbol offsets: the 32-bit table takes the byte straight
+// into the 16-bit add (SDWA source select), so a step is one add, one LDS read and one OR
+#define KRCA_DSTEP_BYTE(K)                                                                                    \
+  __device__ __forceinline__ uint32_t dstep_b##K(const DfaLds4& d, uint32_t row, uint32_t sw, uint32_t& acc) { \
+    uint32_t a;                                                                                               \
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:BYTE_" #K     \
+        : "=v"(a)                                                                                             \
+        : "v"(row), "v"(sw));                                                                                 \
+    const uint32_t t = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(d.trans) + a);     \
+    acc |= t;                                                                                                 \
+    return t;                                                                                                 \
+  }                                                                                                           \
+  __device__ __forceinline__ uint32_t dstep_b##K(const DfaLds2& d, uint32_t row, uint32_t sw, uint32_t& acc) { \
+    return dfa2_step(d, row, (sw >> (8 * K)) & 0xFFu, acc);                                                  \
+  }
+KRCA_DSTEP_BYTE(0)
+KRCA_DSTEP_BYTE(1)
+KRCA_DSTEP_BYTE(2)
+KRCA_DSTEP_BYTE(3)
+#undef KRCA_DSTEP_BYTE
+
+// s_text of log_index_match holds symbol offsets for ASCII bytes: phase A maps every byte below
+// 0x80 through conv[] to its column's offset in a TAB row (separators -> NOP) and keeps the bytes
+// >= 0x80 (the UTF-8 lead and continuation bytes) as they are, so an all-ASCII block reads no byte
+// table and a block holding a multi-byte code point still decodes it.
+static_assert(NOP_SYM * 4 < 0x80, "symbol offsets must stay below 0x80");
+__device__ __forceinline__ uint32_t sym_word(const uint8_t* conv, uint32_t w) {
+  return (uint32_t)conv[w & 0xFFu] | ((uint32_t)conv[(w >> 8) & 0xFFu] << 8) | ((uint32_t)conv[(w >> 16) & 0xFFu] << 16) |
+         ((uint32_t)conv[w >> 24] << 24);
+}
+
+// the symbol offset of code point cp >= 0x80 in TAB's rows (the reference's case folds and \d
+// classes), by a binary search of the range table copied to LDS (rng: KRCA_DFA_NRANGE x {lo, hi,
+// symbol}; from constant memory each probe was a dependent global load, ~7 per code point, and one
+// line with a non-ASCII character held its wave's walk: +5k cycles per 64 KiB tile)
 template <class TAB>
-__device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx, const TAB& d, int s, int e) {
+__device__ __forceinline__ uint32_t cp_symoff(const TAB& d, const uint32_t* rng, uint32_t cp) {
+  uint32_t sy = KRCA_DFA_OTHER;
+  int a = 0, z = KRCA_DFA_NRANGE - 1;
+  while (a <= z) {
+    const int mid = (a + z) >> 1;
+    if (cp < rng[3 * mid]) z = mid - 1;
+    else if (cp > rng[3 * mid + 1]) a = mid + 1;
+    else {
+      sy = rng[3 * mid + 2];
+      break;
+    }
+  }
+  return sy * dsym_scale(d);
+}
+
+// The DFA mask of the line at tile offsets [s, e) from s_text (e <= FTILE + LOOK; the array is
+// padded so a block may read up to 16 bytes past e): lockstep 16-byte blocks from the line's
+// 4-byte-aligned start as in log_dfa, the next block's words read before this block's 16 dependent
+// steps, each byte stepping on its symbol offset: an ASCII byte's stored offset; NOP (the identity
+// column) for a byte outside the line and for a UTF-8 continuation byte; for a lead byte, the
+// symbol of the code point it starts (decoded from the raw bytes after it, as the reference reads
+// the text) -- so a multi-byte code point is one transition, and only blocks holding a byte >= 0x80
+// do any decoding.
+template <class TAB>
+__device__ __forceinline__ uint32_t dfa_walk_sym(const uint32_t* __restrict__ tx, const TAB& d, const uint32_t* rng,
+                                                 int s, int e) {
   uint32_t row = 0, acc = 0;
   int off = s & ~3;  // this block's first byte (4-byte aligned)
   int rs_ = s & 3;   // s - off: 0..3 at the first block, then negative
   int re_ = e - off;
-  int ncp = rs_;     // next code point start - off
-  while (re_ > 0) {
-    uint32_t w[4];
+  constexpr uint32_t nop = NOP_SYM * sizeof(d.trans[0]);
+  uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + j];
+  for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + j];
+  for (;;) {
     const int lo = max(rs_, 0), hi = min(re_, 16);
     const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = line_hi4x(hi);
-    uint32_t in[4], hib = 0;
+    uint32_t so[4], hib = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      in[j] = word_in_line(j, lo4, hi4x);
-      hib |= w[j] & in[j];
+      const uint32_t in = word_in_line(j, lo4, hi4x);  // 0x80 in each byte of the line
+      hib |= w[j] & in;
+      const uint32_t fm = (in >> 7) * 0xFFu;
+      so[j] = (w[j] & fm) | (nop * 0x01010101u & ~fm);
     }
-    if (!hib && ncp <= lo) {  // all-ASCII line bytes: byte table, no decode
-      uint32_t so[16];
+    const bool more = re_ > 16;
+    if (hib) {  // bytes >= 0x80 in the line (rare): continuation bytes -> NOP, lead bytes -> their code point
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t x = w[j] | (in[j] ^ 0x80808080u);  // outside the line: >= 0x80, NOP
-#pragma unroll
-        for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) row = dstep(d, row, so[k], acc);
-      ncp = 16;
-    } else {  // code points, as the reference decodes them
-#pragma unroll 1
       for (int k = 0; k < 16; ++k) {
-        if (k < ncp || k < lo || k >= hi) continue;
-        auto at = [&](int r) -> uint32_t {
-          const int p = off + r;
-          return (tx[p >> 2] >> (8 * (p & 3))) & 0xFFu;
-        };
-        uint32_t cp;
-        const uint32_t b = at(k);
-        int len;
-        if (b < 0x80) {
-          cp = b;
-          len = 1;
-        } else if (b < 0xE0) {
-          cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
-          len = 2;
-        } else if (b < 0xF0) {
-          cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
-          len = 3;
-        } else {
-          cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
-          len = 4;
-        }
-        uint32_t sy;
-        if (cp < 128) {
-          sy = d.sym[cp];
-        } else {
-          sy = KRCA_DFA_OTHER;
-          int a = 0, z = KRCA_DFA_NRANGE - 1;
-          while (a <= z) {
-            const int mid = (a + z) >> 1;
-            if (cp < krca_dfa_ranges[mid][0]) z = mid - 1;
-            else if (cp > krca_dfa_ranges[mid][1]) a = mid + 1;
-            else {
-              sy = krca_dfa_ranges[mid][2];
-              break;
-            }
+        const uint32_t b = (so[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        if (b >= 0x80) {
+          uint32_t sy = nop;
+          if (b >= 0xC0) {
+            auto at = [&](int r) -> uint32_t {
+              const int p = off + r;
+              return (tx[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+            };
+            uint32_t cp;
+            if (b < 0xE0) cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
+            else if (b < 0xF0) cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
+            else cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
+            sy = cp_symoff(d, rng, cp);
           }
-          sy *= dsym_scale(d);
+          so[k >> 2] = (so[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (sy << (8 * (k & 3)));
         }
-        row = dstep(d, row, sy, acc);
-        ncp = k + len;
       }
     }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + 4 + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      row = dstep_b0(d, row, so[j], acc);
+      row = dstep_b1(d, row, so[j], acc);
+      row = dstep_b2(d, row, so[j], acc);
+      row = dstep_b3(d, row, so[j], acc);
+    }
+    if (!more) break;
     off += 16;
     rs_ -= 16;
     re_ -= 16;
-    ncp -= 16;
   }
   return dmask(d, acc);
 }
@@ -1629,27 +1669,33 @@ __device__ __forceinline__ uint32_t dfa_walk_lds(const uint32_t* __restrict__ tx
 // reads (tile_base[T] = the first line of 32 KiB tile 2T), chunk counts / bases are per 256-byte
 // chunk as before
 template <class CF>
-__global__ __launch_bounds__(CF::FTPB) void log_index_match(
+__global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
     const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ doc_off, int64_t D,
     const int32_t* __restrict__ chunk_doc, int32_t* __restrict__ chunk_cnt, int64_t* __restrict__ tile_base,
     int64_t nt64, unsigned long long* __restrict__ status, unsigned int* __restrict__ ticket, int64_t ntiles,
     int64_t cap, int64_t* __restrict__ line_start, int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
     int64_t* __restrict__ chunk_line0, int64_t* __restrict__ n_lines, int32_t* __restrict__ long_q,
-    int32_t* __restrict__ n_long, int32_t* __restrict__ strad_q, int32_t* __restrict__ n_strad) {
+    int32_t* __restrict__ n_long) {
   constexpr int64_t FTILE = CF::FTILE;
   constexpr int FTPB = CF::FTPB, FNIT = CF::FNIT, FCH = CF::FCH, FNBW = CF::FNBW, LMAX = CF::LMAX;
   using TAB = typename std::conditional<CF::W32, DfaLds4, DfaLds2>::type;
-  __shared__ __attribute__((aligned(16))) uint32_t s_text[FTILE / 4 + 8];  // the tile + 32 zero bytes
+  // the symbol offsets (sym_word) of the tile and the LOOK bytes after it, + 32 zero bytes
+  __shared__ __attribute__((aligned(16))) uint32_t s_text[(FTILE + LOOK) / 4 + 8];
   __shared__ TAB d;
+  __shared__ uint8_t s_conv[256];  // byte -> symbol offset (bytes >= 0x80: themselves)
+  __shared__ uint32_t s_rng[3 * KRCA_DFA_NRANGE];  // the code point ranges' symbols (cp_symoff)
   __shared__ uint32_t s_cs[FNBW];
   __shared__ uint16_t s_ls[LMAX], s_le[LMAX], s_lm[LMAX];
   __shared__ int32_t s_cnt[FCH], s_cb[FCH];  // per 256-byte chunk: line starts, exclusive base in the tile
   __shared__ int32_t s_wsum[FCH / 64];
   __shared__ int32_t s_prev_end;  // tile offset where the previous tile's last line ends (from line 0)
+  __shared__ int32_t s_last_end;  // tile offset where this tile's last line ends (-1: past the LOOK bytes)
   __shared__ int64_t s_tile, s_excl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   dload(d);  // once per workgroup (persistent)
-  if (tid < 8) s_text[FTILE / 4 + tid] = 0u;
+  for (int i = tid; i < 256; i += FTPB) s_conv[i] = (uint8_t)(i < 128 ? d.sym[i] : i);  // (read after the ticket's barrier)
+  for (int i = tid; i < 3 * KRCA_DFA_NRANGE; i += FTPB) s_rng[i] = krca_dfa_ranges[i / 3][i % 3];
+  if (tid < 8) s_text[(FTILE + LOOK) / 4 + tid] = 0u;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   LT_INIT();
   for (;;) {
@@ -1673,7 +1719,14 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
       const int64_t q0 = tile0 + ((int64_t)it * FTPB + (int64_t)__builtin_amdgcn_readfirstlane(wid) * 64) * PIECE;
       pw[it] = q0 >= 4 && q0 <= nbytes ? *reinterpret_cast<const uint32_t*>(text + q0 - 4) : 0u;
     }
-    tile_container_starts_t<FTILE>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order LDS reuse)
+    u32x4 rawx = {0u, 0u, 0u, 0u};  // the last wave: the LOOK bytes after the tile, a piece per lane
+    uint32_t pwx = 0;
+    if (wid == FTPB / 64 - 1) {
+      const int64_t q = tile0 + FTILE + (int64_t)lane * PIECE;
+      rawx = *reinterpret_cast<const u32x4*>(text + (q < nbytes ? q : qlast));
+      pwx = tile0 + FTILE <= nbytes ? *reinterpret_cast<const uint32_t*>(text + tile0 + FTILE - 4) : 0u;
+    }
+    tile_container_starts_t<FTILE + LOOK>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order LDS reuse)
     uint32_t regS[FNIT], regL1[FNIT];  // per piece: starts | odd lengths << 16; lengths 2/3
 #pragma unroll
     for (int it = 0; it < FNIT; ++it) {
@@ -1681,7 +1734,8 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
       const int64_t q = tile0 + (int64_t)pc * PIECE;
       const bool in = q < nbytes;
       uint32_t w[4] = {in ? raw[it].x : 0u, in ? raw[it].y : 0u, in ? raw[it].z : 0u, in ? raw[it].w : 0u};
-      *reinterpret_cast<u32x4*>(s_text + pc * 4) = u32x4{w[0], w[1], w[2], w[3]};
+      *reinterpret_cast<u32x4*>(s_text + pc * 4) =
+          u32x4{sym_word(s_conv, w[0]), sym_word(s_conv, w[1]), sym_word(s_conv, w[2]), sym_word(s_conv, w[3])};
       uint32_t wp = __shfl_up(w[3], 1, 64);  // bytes q-4 .. q-1
       if (lane == 0) wp = pw[it];
       const uint32_t C = in ? piece_container_starts(s_cs, tile0, q) : 0u;
@@ -1727,6 +1781,34 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
                          __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     LT(2);
+    if (wid == FTPB / 64 - 1) {  // the LOOK bytes (the last wave, beside wave 0's look-back): their symbols,
+                                 // and the first line start in them ends the tile's last line
+      const int64_t q = tile0 + FTILE + (int64_t)lane * PIECE;
+      const bool in = q < nbytes;
+      uint32_t w[4] = {in ? rawx.x : 0u, in ? rawx.y : 0u, in ? rawx.z : 0u, in ? rawx.w : 0u};
+      *reinterpret_cast<u32x4*>(s_text + FTILE / 4 + lane * 4) =
+          u32x4{sym_word(s_conv, w[0]), sym_word(s_conv, w[1]), sym_word(s_conv, w[2]), sym_word(s_conv, w[3])};
+      uint32_t wp = __shfl_up(w[3], 1, 64);
+      if (lane == 0) wp = pwx;
+      const uint32_t C = in ? piece_container_starts(s_cs, tile0, q) : 0u;
+      uint32_t S, l0, l1;
+      piece_flags(wp, w, C & 0xFFFFu, S, l0, l1);
+      if (in) {
+        S |= C >> 1;
+        if (q + PIECE > nbytes) S &= (1u << (int)(nbytes - q)) - 1u;
+      } else {
+        S = 0;
+      }
+      const uint64_t any = __ballot(S != 0);
+      if (any) {
+        if (lane == __builtin_ctzll(any)) {
+          const int k = __ffs(S) - 1;
+          s_last_end = FTILE + lane * PIECE + k - ((int)((l0 >> k) & 1u) | (int)(((l1 >> k) & 1u) << 1));
+        }
+      } else if (lane == 0) {  // no line starts there: the text's last line, or one longer than LOOK
+        s_last_end = tile0 + FTILE + LOOK >= nbytes ? (int32_t)(last_line_end(text, nbytes, doc_off, D) - tile0) : -1;
+      }
+    }
     // the look-back right away (wave 0): its inclusive prefix goes out before this tile's walk, so
     // later tiles find it within a round or two instead of summing aggregates back over every tile
     // still walking (published after the walk, the look-backs scanned ~2 x 512 tiles: 443 us, r4g)
@@ -1797,12 +1879,11 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
       }
       __syncthreads();
       LT(4);
-      // the DFA walk: a lane per line, from LDS (the tile's last line and long lines deferred)
+      // the DFA walk: a lane per line, from LDS (long lines: log_dfa_long)
       for (int j = tid; j < hi - lo; j += FTPB) {
-        if (lo + j == total - 1) continue;
-        const int ls = s_ls[j], le = s_le[j];
-        if (le - ls > LONG_LINE) continue;
-        s_lm[j] = (uint16_t)(ls < le ? dfa_walk_lds(s_text, d, ls, le) : 0u);
+        const int ls = s_ls[j], le = lo + j == total - 1 ? s_last_end : (int)s_le[j];
+        if (le < 0 || le - ls > LONG_LINE) continue;
+        s_lm[j] = (uint16_t)(ls < le ? dfa_walk_sym(s_text, d, s_rng, ls, le) : 0u);
       }
       __syncthreads();
       LT(5);
@@ -1818,14 +1899,10 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
       for (int j = tid; j < hi - lo; j += FTPB) {  // coalesced by line id
         const int64_t id = excl + lo + j;
         if (id >= cap) continue;
-        const int ls = s_ls[j];
+        const int ls = s_ls[j], le = lo + j == total - 1 ? s_last_end : (int)s_le[j];
         line_start[id] = tile0 + ls;
-        if (lo + j == total - 1) {  // its end is in a later tile: log_dfa_strad, or log_dfa_long
-          strad_q[atomicAdd(n_strad, 1)] = (int32_t)id;
-          continue;
-        }
-        line_end[id] = tile0 + s_le[j];
-        if (s_le[j] - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;
+        if (le >= 0) line_end[id] = tile0 + le;  // (a last line's end also comes from the next tile)
+        if (le < 0 || le - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;
         else line_mask[id] = s_lm[j];
       }
       __syncthreads();  // the window's lists (and, after the last, the tile's LDS) are rewritten next
@@ -1837,71 +1914,13 @@ __global__ __launch_bounds__(CF::FTPB) void log_index_match(
   }
 }
 
-// the tiles' last lines (one per tile of log_index_match: a few thousand per scan), a lane per line:
-// the lane's line (up to STRAD_B bytes from its 16-byte aligned start) is staged in a lane-private
-// LDS slot with every load issued at once, then walked code point by code point from LDS (a walk
-// through global memory waited on one dependent 16-byte load per block: 58 us for 5.6k lines, r4g).
-// Longer lines go on to log_dfa_long's queue (a wave per line, launched after this kernel).
-constexpr int STRAD_B = 256;
-struct LdsBytes {  // byte p of the text from a lane-private LDS copy of [a0, a0 + STRAD_B)
-  const uint8_t* b;
-  int64_t a0;
-  __device__ __forceinline__ uint32_t at(int64_t p) const { return b[p - a0]; }
-};
-__global__ __launch_bounds__(TPB) void log_dfa_strad(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                     const int64_t* __restrict__ line_start,
-                                                     const int64_t* __restrict__ line_end,
-                                                     uint32_t* __restrict__ line_mask, const int32_t* __restrict__ q,
-                                                     const int32_t* __restrict__ nq, int32_t* __restrict__ long_q,
-                                                     int32_t* __restrict__ n_long) {
-  __shared__ DfaLds dfa;
-  __shared__ __attribute__((aligned(16))) uint4 sbuf[TPB * (STRAD_B / 16)];
-  const int n = *nq;
-  if ((int64_t)blockIdx.x * TPB >= n) return;  // uniform: no line for this block, skip the table fill
-  dfa_load(dfa);
-  for (int i = blockIdx.x * TPB + threadIdx.x; i < n; i += gridDim.x * TPB) {
-    const int64_t l = q[i];
-    const int64_t s = line_start[l], e = line_end[l];
-    const int64_t a0 = s & ~(int64_t)15;
-    if (e + 3 - a0 > STRAD_B) {  // (decode may look up to 3 bytes past e): a wave per line instead
-      long_q[atomicAdd(n_long, 1)] = (int32_t)l;  // (a lane walking it from global memory waited on
-      continue;                                   // one dependent load per block: 44 us per scan, r4i)
-    }
-    uint32_t row = 0, mask = 0;
-    uint4* mine = sbuf + threadIdx.x * (STRAD_B / 16);
-    uint4 v[STRAD_B / 16];
-#pragma unroll
-    for (int k = 0; k < STRAD_B / 16; ++k) {  // an aligned 16-byte block holding a text byte never
-      const int64_t b = a0 + 16 * k;          // crosses the text's last page; blocks past it stay 0
-      v[k] = b < nbytes ? *reinterpret_cast<const uint4*>(text + b) : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int k = 0; k < STRAD_B / 16; ++k) mine[k] = v[k];
-    LdsBytes B{reinterpret_cast<const uint8_t*>(mine), a0};
-    for (int64_t p = s; p < e;) {
-      uint32_t cp;
-      const int len = decode(B, p, cp);
-      const uint32_t t = dfa.trans[row + cp_symbol(dfa, cp)];
-      row = t & (kAcc - 1);
-      if (t & kAcc) mask |= dfa.out[row / KRCA_DFA_NSYM];
-      p += len;
-    }
-    line_mask[l] = mask;
-  }
-}
-
 int64_t num_tiles(int64_t nbytes) { return std::max<int64_t>(1, krca::ceil_div(nbytes, TILE)); }
-// int64 words of the int32 long-line queue (lines longer than LONG_LINE)
-// (lines longer than LONG_LINE: at most nbytes / LONG_LINE; log_dfa_strad's longer straddlers: at
-// most one per 32 KiB tile)
+// int64 words of the int32 long-line queue (lines longer than LONG_LINE: at most nbytes / LONG_LINE,
+// + one per tile whose last line runs past its LOOK bytes)
 int64_t long_q_words(int64_t nbytes) { return krca::ceil_div(nbytes / LONG_LINE + 2 * num_tiles(nbytes) + 2, 2); }
 // krca_log_scan's tail of the workspace (int64 words): look-back status words for the 2 x num_tiles
-// 32 KiB tiles of log_index_match (num_tiles of log_index_lines use the first half), the tile
-// ticket, the straddler count, the int32 straddler queue (one line per 32 KiB tile)
-int64_t scan_tail_words(int64_t nbytes) {
-  const int64_t nt = num_tiles(nbytes);
-  return 2 * nt + 2 + krca::ceil_div(2 * nt + 1, 2);
-}
+// 32 KiB tiles of log_index_match (num_tiles of log_index_lines use the first half), the tile ticket
+int64_t scan_tail_words(int64_t nbytes) { return 2 * num_tiles(nbytes) + 1; }
 
 }  // namespace
 
@@ -1917,7 +1936,7 @@ uint64_t krca_log_dfa_digest(void) { return KRCA_DFA_DIGEST; }
 int64_t krca_log_index_size(int64_t nbytes) {
   const int64_t nt = num_tiles(nbytes);
   return (nt + 1) + 2 * krca::ceil_div(nt * TPB, 2) + 2 + nt * TPB + 1 + long_q_words(nbytes) +
-         scan_tail_words(nbytes);  // + krca_log_scan's look-back status words, ticket, straddler queue
+         scan_tail_words(nbytes);  // + krca_log_scan's look-back status words, ticket, deferred-line queue
 }
 
 int krca_log_index(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, int64_t ndocs, int64_t* ws,
@@ -2015,8 +2034,6 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   unsigned long long* status =
       reinterpret_cast<unsigned long long*>(chunk_line0 + nt * TPB + 1 + long_q_words(nbytes));
   unsigned int* ticket = reinterpret_cast<unsigned int*>(status + 2 * nt);
-  int32_t* n_strad = reinterpret_cast<int32_t*>(status + 2 * nt + 1);
-  int32_t* strad_q = reinterpret_cast<int32_t*>(status + 2 * nt + 2);
   hipStream_t st = krca::as_stream(stream);
   if (nbytes == 0) {
     // no text (the pointer may be null): every container is empty and no kernel may read text --
@@ -2036,14 +2053,14 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
   // look-back status words + ticket and long-line count (no memset launches: each dependent
   // launch costs ~10 us at the front of the scan)
   hipLaunchKernelGGL(log_chunk_doc, dim3((unsigned)krca::ceil_div(ndocs, TPB)), dim3(TPB), 0, st, doc_off, ndocs,
-                     nbytes, cdoc, status, 2 * nt + 2, n_long);  // status words, ticket, straddler count
+                     nbytes, cdoc, status, 2 * nt + 1, n_long);  // status words, ticket
   KRCA_LAUNCH_CHECK();
   const int64_t* Ld = tile + nt;  // the line count, on the device (written by the index's last tile)
   if (krca::tuning().log_fused) {
     // A/B: the line index and the DFA walk in one pass over the text (KRCA_LOG_FUSED = 1: 32 KiB
     // tiles, two 512-thread workgroups per CU; 2: 64 KiB tiles, one 1024-thread workgroup per CU);
-    // the tiles' last lines go to log_dfa_strad, long lines to log_dfa_long.  It reads the text
-    // once but runs its phases one after the other per tile: slower than the default
+    // long lines go to log_dfa_long.  It reads the text once but runs its phases one after the
+    // other per tile
     auto launch = [&](auto cfg) -> int64_t {
       using CF = decltype(cfg);
       const int64_t ntf = num_ftiles(nbytes, CF::FTILE);
@@ -2051,15 +2068,11 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
           krca::resident_workgroups(reinterpret_cast<const void*>(&log_index_match<CF>), CF::FTPB, st, 1);
       hipLaunchKernelGGL(log_index_match<CF>, dim3((unsigned)std::min<int64_t>(ntf, resident)), dim3(CF::FTPB), 0, st,
                          text, nbytes, doc_off, ndocs, (const int32_t*)cdoc, chunk, tile, nt, status, ticket, ntf,
-                         line_cap, line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long, strad_q,
-                         n_strad);
+                         line_cap, line_start, line_end, line_mask, chunk_line0, tile + nt, long_q, n_long);
       return ntf;
     };
-    const int64_t ntf = krca::tuning().log_fused == 2 ? launch(FBig{}) : launch(FSmall{});
-    KRCA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(log_dfa_strad, dim3((unsigned)krca::ceil_div(ntf, TPB)), dim3(TPB), 0, st, text, nbytes,
-                       (const int64_t*)line_start, (const int64_t*)line_end, line_mask, (const int32_t*)strad_q,
-                       (const int32_t*)n_strad, long_q, n_long);
+    if (krca::tuning().log_fused == 2) launch(FBig{});
+    else launch(FSmall{});
     KRCA_LAUNCH_CHECK();
   } else {  // default (KRCA_LOG_FUSED=0): the line index, then a DFA lane per line re-reading the text
     // workgroups the stream's device keeps resident (occupancy API, cached per device)

@@ -306,6 +306,18 @@ def test_log_scan_block_edges(eng):
         _check_docs(eng, ["y" * (37 + tail) + "é" + "panic:"])
 
 
+@pytest.mark.parametrize("fused", [1, 2])
+def test_log_scan_fused_multibyte_lines(eng, fused):
+    """The fused walk keeps bytes >= 0x80 as they are among the ASCII symbol offsets and decodes a
+    block's code points when one is there: a text where nearly every line holds 2-, 3- and 4-byte
+    characters (case folds among them: K, ſ, İ) equals the oracle."""
+    rng = np.random.default_rng(23)
+    words = ["é", "Error", "\u212aILLED", "ſecret not found", "panic:", "x", "Tim\u0130eout", "€", " ", "\U0001d400"]
+    docs = ["\n".join("".join(rng.choice(words, 4)) for _ in range(400)) for _ in range(10)]
+    with native.tune(eng.lib, KRCA_LOG_FUSED=fused):
+        _check_docs(eng, docs)
+
+
 def test_log_scan_synthetic_large(eng):
     docs = synth.make_log_corpus(20000, lines_per_doc=6, seed=3, hazard_rate=0.01)
     _check_docs(eng, docs)
@@ -342,7 +354,8 @@ def test_log_scan_one_call_and_fallback_identical(eng):
 
 def test_log_scan_fused_walk_identical(eng):
     """krca_log_scan's fused pass (log_index_match: the DFA walks each tile's lines from LDS in the
-    line-index pass; each tile's last line goes to log_dfa_strad, lines over 1 KiB to log_dfa_long),
+    line-index pass, a tile's last line over the 1 KiB loaded after the tile; lines over 1 KiB and
+    lines holding a byte >= 0x80 go to log_dfa_long),
     in both shapes (KRCA_LOG_FUSED=1: 32 KiB tiles, 16-bit table; 2: 64 KiB tiles, 32-bit table), equals
     the round-3 path (KRCA_LOG_FUSED=0: the index, then log_dfa re-reading the text) on every
     output, and the oracle: tiles of more than 4,096 lines (several list windows per tile: 2-byte
@@ -361,6 +374,15 @@ def test_log_scan_fused_walk_identical(eng):
         return (-pos - extra) % 65536 + 1
     docs.append("p" * to_tile_end(1) + "\r\nKilled timeout")  # CRLF split across a tile edge
     docs.append("w" * to_tile_end(1) + "\u2028 Traceback")    # U+2028 split across a tile edge
+    # a tile's last line ending in the 1,024 bytes loaded after the tile: its next line starting at
+    # the last of them (+1023) and just past them (+1024: log_dfa_long), lengths 1,024 and 1,025,
+    # a match across the tile edge
+    for m in (1017, 1018):
+        docs.append("r" * to_tile_end(2) + "\n" + "Erro" + "r" + "t" * m + "\nnext")
+    for m in (1018, 1019, 1020):
+        docs.append("s" * to_tile_end(3) + "\n" + "Tim" + "eout" + "u" * (m - 2))
+    docs.append("c" * to_tile_end(4) + "\nKil" + "led é" + "d" * 900 + "\nend")  # a multi-byte character in it
+    docs.append("g" * to_tile_end(2) + "\né" + "\u212a" + "illed")  # one split across the tile edge
     docs += ["".join(rng.choice(["Error ", "\r\n", "é", "\x85", "panic:", "v" * 200, " "]) for _ in range(30))
              for _ in range(300)]
     docs.append("tail Error é")                        # the text ends mid-piece

@@ -12,6 +12,8 @@
 #   tmplcls      template tests + kernel stats with the byte-class table build (lib/dbg/libkrca_tcls.so)
 #   tmplr5       template kernel stats with the round-5 hash kernel (lib/dbg/libkrca_tr5.so; its hashes ignore UUIDs)
 #   pmclds_V_T   LDS / issue counters of prof_kernels.py T (V = base or cls: the library)
+#   pmcldsf_T    the same with KRCA_LOG_FUSED=2 (+ GRBM_GUI_ACTIVE)    logsf  logs stats with KRCA_LOG_FUSED=2
+#   ltime_F      tools/log_timing.py (phase cycles per tile) with KRCA_LOG_FUSED=F and the -DLOG_TIMING build
 #   pmcmfma      tools/gpu_pmc_mfma.sh (correlation MFMA busy, clock, DRAM bytes at C3 / 1M)
 #   pmcx_T       tools/gpu_pmc_exact.sh with TARGETS=T (one target: cal ppr bench logs tmpl ...)
 set -u
@@ -70,6 +72,9 @@ for s in "$@"; do
     tmplr5) KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/dbg/libkrca_tr5.so prof tmplr5 300 tools/prof_kernels.py tmpl --reps 5 ;;
     pmclds_*) t=${s#pmclds_}; lib=""; [ "${t%%_*}" = cls ] && lib=$PWD/kubernetes-rca-system_amd/lib/dbg/libkrca_tcls.so; t=${t#*_};
               step $s 150 env ${lib:+KRCA_LIB=$lib} timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $O/$s -o run -- python3 tools/prof_kernels.py $t --reps 1 ;;
+    pmcldsf_*) t=${s#pmcldsf_}; step $s 150 env KRCA_LOG_FUSED=2 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/$s -o run -- python3 tools/prof_kernels.py $t --reps 1 ;;
+    logsf) step logsf 300 env KRCA_LOG_FUSED=2 rocprofv3 --kernel-trace --stats --output-format csv -d $O/logsf -o run -- python3 tools/prof_kernels.py logs --reps 5 ;;
+    ltime_*) step $s 300 env KRCA_LOG_FUSED=${s#ltime_} KRCA_LIB=$PWD/kubernetes-rca-system_amd/lib/dbg/libkrca_ltime.so python3 -u tools/log_timing.py ;;
     graphprobe_*) v=${s#graphprobe_}; step $s 300 env KRCA_LIB=kubernetes-rca-system_amd/lib/dbg/libkrca_gdbg.so python3 -u tools/graph_replay_probe.py --junk ${v%%_*} --launches ${v##*_} ;;
     graphprobeoff_*) v=${s#graphprobeoff_}; step $s 300 env DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 KRCA_LIB=kubernetes-rca-system_amd/lib/dbg/libkrca_gdbg.so python3 -u tools/graph_replay_probe.py --junk ${v%%_*} --launches ${v##*_} ;;
     pmcmfma) step pmcmfma 1000 env PODS="${PODS:-100000 1000000}" tools/gpu_pmc_mfma.sh $TAG/pmcmfma ;;
