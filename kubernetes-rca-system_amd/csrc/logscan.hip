@@ -731,17 +731,34 @@ __device__ __forceinline__ uint32_t gather4(uint32_t f) { return ((f & 0x8080808
 // (sep_flags + sep_planes: ~390 vector instructions per piece and wave).  cs = container first
 // bytes at q-1+k (bit k): a "\r" there belongs to the previous container, so "\r\n" is not one
 // separator across it.
+// Common case first (round 6): a piece whose bytes, and the two before it, hold no separator but
+// "\n" and no byte >= 0x80 has S = L0 = the positions after its "\n"s, L1 = 0 -- the other tests'
+// gathers and the "\r\n" logic are skipped (a wave takes the full path only when one of its lanes
+// needs it).
 __device__ __forceinline__ void piece_flags(uint32_t wp, const uint32_t (&w)[4], uint32_t cs, uint32_t& S,
                                             uint32_t& L0, uint32_t& L1) {
-  uint32_t nl = 0, cr = 0, sep = 0;  // bit k: byte q+k is "\n" / "\r" / a one-byte separator
+  uint32_t nl = 0, r[4];  // bit k of nl: byte q+k is "\n"; r: the other one-byte separators, per byte
+  uint32_t odd = (wp | w[0] | w[1] | w[2] | w[3]) & 0x80808080u;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     nl |= gather4(swar_eq(w[j], 0x0A)) << (4 * j);
-    cr |= gather4(swar_eq(w[j], 0x0D)) << (4 * j);
-    sep |= gather4(swar_range(w[j], 0x0A, 0x0D) | swar_range(w[j], 0x1C, 0x1E)) << (4 * j);
+    r[j] = swar_range(w[j], 0x0B, 0x0D) | swar_range(w[j], 0x1C, 0x1E);
+    odd |= r[j];
   }
   // bytes q-1, q-2 (bit 0, 1 of the "before" masks)
   const uint32_t b1 = wp >> 24, b2 = (wp >> 16) & 0xFFu;
+  if (!odd && !((b1 >= 0x0B && b1 <= 0x0D) || (b1 >= 0x1C && b1 <= 0x1E) || b2 == 0x0D)) {
+    S = ((nl << 1) | (uint32_t)(b1 == 0x0A)) & 0xFFFFu;
+    L0 = S;
+    L1 = 0;
+    return;
+  }
+  uint32_t cr = 0, sep = nl;  // bit k: byte q+k is "\r" / a one-byte separator
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cr |= gather4(swar_eq(w[j], 0x0D)) << (4 * j);
+    sep |= gather4(r[j]) << (4 * j);
+  }
   const uint32_t sep1 = (sep << 1) | (uint32_t)((b1 >= 0x0A && b1 <= 0x0D) || (b1 >= 0x1C && b1 <= 0x1E));  // byte p-1
   const uint32_t cr1 = (cr << 1) | (uint32_t)(b1 == 0x0D);
   const uint32_t nl1 = (nl << 1) | (uint32_t)(b1 == 0x0A);
@@ -1096,6 +1113,35 @@ __device__ __forceinline__ uint32_t dfa4_step(const DfaLds4& d, uint32_t row, ui
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(d.trans) + a);
 }
 
+// the DFA symbol of code point cp >= 0x80 (the reference's case folds and \d classes), by a binary
+// search of the range table copied to LDS (rng: KRCA_DFA_NRANGE x {lo, hi, symbol}; from constant
+// memory each probe was a dependent global load, ~7 per code point, and one line with a non-ASCII
+// character held its wave: +5k cycles per 64 KiB tile of log_index_match, r6n)
+__device__ __forceinline__ uint32_t cp_sym_lds(const uint32_t* rng, uint32_t cp) {
+  uint32_t sy = KRCA_DFA_OTHER;
+  int a = 0, z = KRCA_DFA_NRANGE - 1;
+  while (a <= z) {
+    const int mid = (a + z) >> 1;
+    if (cp < rng[3 * mid]) z = mid - 1;
+    else if (cp > rng[3 * mid + 1]) a = mid + 1;
+    else {
+      sy = rng[3 * mid + 2];
+      break;
+    }
+  }
+  return sy;
+}
+__device__ __forceinline__ void load_ranges(uint32_t* rng) {
+  for (int i = threadIdx.x; i < 3 * KRCA_DFA_NRANGE; i += blockDim.x) rng[i] = krca_dfa_ranges[i / 3][i % 3];
+}
+// the code point starting with lead byte b (>= 0xC0) whose continuation bytes at(1..3) returns
+template <class AT>
+__device__ __forceinline__ uint32_t utf8_cp(uint32_t b, AT at) {
+  if (b < 0xE0) return ((b & 0x1F) << 6) | (at(1) & 0x3F);
+  if (b < 0xF0) return ((b & 0x0F) << 12) | ((at(1) & 0x3F) << 6) | (at(2) & 0x3F);
+  return ((b & 0x07) << 18) | ((at(1) & 0x3F) << 12) | ((at(2) & 0x3F) << 6) | (at(3) & 0x3F);
+}
+
 // hi4x for word_in_line: the bytes 0x80 + hi - 1 (0x7F for hi = 0), so that hi4x - i has bit 7 set
 // iff i < hi.  (Until round 4 the bytes were 0x80 + hi, which admitted i = hi: the byte at the
 // line's end -- the separator, a NOP, or at a container without a trailing separator the NEXT
@@ -1119,7 +1165,9 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
                                                    const int64_t* __restrict__ line_end, uint32_t* __restrict__ line_mask,
                                                    int32_t* __restrict__ long_q, int32_t* __restrict__ n_long) {
   __shared__ DfaLds4 d;
-  dfa4_load(d);
+  __shared__ uint32_t d_rng[3 * KRCA_DFA_NRANGE];
+  load_ranges(d_rng);
+  dfa4_load(d);  // (its barrier covers d_rng)
   L = lines_of(L, Ld, cap);
   for (int64_t l0 = (int64_t)blockIdx.x * DFA_TPB; l0 < L; l0 += (int64_t)gridDim.x * DFA_TPB) {
     // buffer resource at the group's first line: offsets stay 32-bit (the group's short lines
@@ -1139,15 +1187,19 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
     int off = (int)((s & ~(int64_t)3) - base);  // this block's first byte, from base
     int rs_ = (int)(s & 3);                      // s - P: 0..3 at the first block, then negative
     int re_ = (int)(e - (s & ~(int64_t)3));      // e - P
-    int ncp = rs_;                               // next code point start - P
     const int end_off = (int)min(rem, (int64_t)INT32_MAX);
     auto load = [&](int q) -> uint4 {
       return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, q, 0, 0));
     };
-    // one block: cur holds bytes off .. off+15; the next block is loaded into nxt first (every
-    // lane, every block: the wait on cur is then never a wait on the load just issued)
-    auto block = [&](uint4& cur, uint4& nxt) -> bool {
-      nxt = load(off + 16);
+    // one block: cur holds bytes off .. off+15; the block after the next is loaded into far first
+    // (every lane, every block: a ring of three, so the wait on cur covers a load issued two
+    // blocks -- 32 dependent steps -- earlier).  Each byte steps on its symbol: an in-line ASCII
+    // byte's from the byte table; NOP (the identity column) for a byte outside the line and for a
+    // UTF-8 continuation byte (the table maps bytes >= 0x80 to NOP); a lead byte's entry is then
+    // replaced by the symbol of the code point it starts, decoded as the reference reads the text
+    // -- a multi-byte code point is one transition (round 6: no code-point loop of its own).
+    auto block = [&](uint4& cur, uint4& far) -> bool {
+      far = load(off + 32);
       uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
       if (off + 16 > end_off) {  // the text's last bytes (a buffer load straddling the end reads 0)
 #pragma unroll 1
@@ -1158,86 +1210,44 @@ __global__ __launch_bounds__(DFA_TPB) void log_dfa(const uint8_t* __restrict__ t
       }
       const int lo = max(rs_, 0), hi = min(re_, 16);
       const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = line_hi4x(hi);
-      uint32_t in[4], hib = 0;
+      uint32_t so[16], hib = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        in[j] = word_in_line(j, lo4, hi4x);
-        hib |= w[j] & in[j];
+        const uint32_t in = word_in_line(j, lo4, hi4x);
+        hib |= w[j] & in;
+        const uint32_t x = w[j] | (in ^ 0x80808080u);  // outside the line: >= 0x80, NOP
+#pragma unroll
+        for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
       }
-      // all-ASCII line bytes and no code point running in from the last block (always so for
-      // valid UTF-8, whose continuation bytes are >= 0x80): byte table, no decode
-      if (!hib && ncp <= lo) {
-        uint32_t so[16];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t x = w[j] | (in[j] ^ 0x80808080u);  // outside the line: >= 0x80, NOP
-#pragma unroll
-          for (int k = 0; k < 4; ++k) so[4 * j + k] = d.sym[(x >> (8 * k)) & 0xFFu];
-        }
+      if (hib) {  // in-line bytes >= 0x80 (rare): the lead bytes' code points
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          const uint32_t t = dfa4_step(d, row, so[k]);
-          row = t;
-          acc |= t;
-        }
-        ncp = 16;
-      } else {  // code points, as the reference decodes them (rare: non-ASCII text)
-#pragma unroll 1
-        for (int k = 0; k < 16; ++k) {
-          if (k < ncp || k < lo || k >= hi) continue;
-          auto at = [&](int r) -> uint32_t {
-            if (r < 16) return (w[r >> 2] >> (8 * (r & 3))) & 0xFFu;
-            return off + r < end_off ? (uint32_t)text[base + off + r] : 0u;
-          };
-          uint32_t cp;
-          const uint32_t b = at(k);
-          int len;
-          if (b < 0x80) {
-            cp = b;
-            len = 1;
-          } else if (b < 0xE0) {
-            cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
-            len = 2;
-          } else if (b < 0xF0) {
-            cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
-            len = 3;
-          } else {
-            cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
-            len = 4;
+          const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          if (b >= 0xC0 && k >= lo && k < hi) {
+            const uint32_t cp = utf8_cp(b, [&](int r) -> uint32_t {
+              const int q = k + r;
+              if (q < 16) return (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+              return off + q < end_off ? (uint32_t)text[base + off + q] : 0u;
+            });
+            so[k] = cp_sym_lds(d_rng, cp) * 4;
           }
-          uint32_t sy;
-          if (cp < 128) {
-            sy = d.sym[cp];
-          } else {
-            sy = KRCA_DFA_OTHER;
-            int a = 0, z = KRCA_DFA_NRANGE - 1;
-            while (a <= z) {
-              const int mid = (a + z) >> 1;
-              if (cp < krca_dfa_ranges[mid][0]) z = mid - 1;
-              else if (cp > krca_dfa_ranges[mid][1]) a = mid + 1;
-              else {
-                sy = krca_dfa_ranges[mid][2];
-                break;
-              }
-            }
-            sy *= 4;
-          }
-          const uint32_t t = dfa4_step(d, row, sy);
-          row = t;
-          acc |= t;
-          ncp = k + len;
         }
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t t = dfa4_step(d, row, so[k]);
+        row = t;
+        acc |= t;
       }
       const bool more = re_ > 16;
       off += 16;
       rs_ -= 16;
       re_ -= 16;
-      ncp -= 16;
       return more;
     };
     if (s < e) {
-      uint4 A = load(off), B;
-      while (block(A, B) && block(B, A)) {
+      uint4 R0 = load(off), R1 = load(off + 16), R2;
+      while (block(R0, R2) && block(R1, R0) && block(R2, R1)) {
       }
     }
     line_mask[l] = acc >> 16;
@@ -1574,24 +1584,10 @@ __device__ __forceinline__ uint32_t sym_word(const uint8_t* conv, uint32_t w) {
          ((uint32_t)conv[w >> 24] << 24);
 }
 
-// the symbol offset of code point cp >= 0x80 in TAB's rows (the reference's case folds and \d
-// classes), by a binary search of the range table copied to LDS (rng: KRCA_DFA_NRANGE x {lo, hi,
-// symbol}; from constant memory each probe was a dependent global load, ~7 per code point, and one
-// line with a non-ASCII character held its wave's walk: +5k cycles per 64 KiB tile)
+// the symbol offset of code point cp >= 0x80 in TAB's rows
 template <class TAB>
 __device__ __forceinline__ uint32_t cp_symoff(const TAB& d, const uint32_t* rng, uint32_t cp) {
-  uint32_t sy = KRCA_DFA_OTHER;
-  int a = 0, z = KRCA_DFA_NRANGE - 1;
-  while (a <= z) {
-    const int mid = (a + z) >> 1;
-    if (cp < rng[3 * mid]) z = mid - 1;
-    else if (cp > rng[3 * mid + 1]) a = mid + 1;
-    else {
-      sy = rng[3 * mid + 2];
-      break;
-    }
-  }
-  return sy * dsym_scale(d);
+  return cp_sym_lds(rng, cp) * dsym_scale(d);
 }
 
 // The DFA mask of the line at tile offsets [s, e) from s_text (e <= FTILE + LOOK; the array is
@@ -1632,14 +1628,10 @@ __device__ __forceinline__ uint32_t dfa_walk_sym(const uint32_t* __restrict__ tx
         if (b >= 0x80) {
           uint32_t sy = nop;
           if (b >= 0xC0) {
-            auto at = [&](int r) -> uint32_t {
-              const int p = off + r;
+            const uint32_t cp = utf8_cp(b, [&](int r) -> uint32_t {
+              const int p = off + k + r;
               return (tx[p >> 2] >> (8 * (p & 3))) & 0xFFu;
-            };
-            uint32_t cp;
-            if (b < 0xE0) cp = ((b & 0x1F) << 6) | (at(k + 1) & 0x3F);
-            else if (b < 0xF0) cp = ((b & 0x0F) << 12) | ((at(k + 1) & 0x3F) << 6) | (at(k + 2) & 0x3F);
-            else cp = ((b & 0x07) << 18) | ((at(k + 1) & 0x3F) << 12) | ((at(k + 2) & 0x3F) << 6) | (at(k + 3) & 0x3F);
+            });
             sy = cp_symoff(d, rng, cp);
           }
           so[k >> 2] = (so[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (sy << (8 * (k & 3)));
@@ -1694,12 +1686,15 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   dload(d);  // once per workgroup (persistent)
   for (int i = tid; i < 256; i += FTPB) s_conv[i] = (uint8_t)(i < 128 ? d.sym[i] : i);  // (read after the ticket's barrier)
-  for (int i = tid; i < 3 * KRCA_DFA_NRANGE; i += FTPB) s_rng[i] = krca_dfa_ranges[i / 3][i % 3];
+  load_ranges(s_rng);
   if (tid < 8) s_text[(FTILE + LOOK) / 4 + tid] = 0u;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   LT_INIT();
+  // the next tile's ticket is taken at the start of this tile's writes (its atomic's round trip
+  // under them), after this tile has published its inclusive prefix: a later tile's look-back never
+  // waits on a claimed tile whose holder is still walking
+  if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
   for (;;) {
-    if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
     const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
     if (tile >= ntiles) {  // uniform
@@ -1887,6 +1882,8 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
       }
       __syncthreads();
       LT(5);
+      unsigned int next = 0;
+      if (tid == 0 && win == nwin - 1) next = atomicAdd(ticket, 1u);
       const int64_t excl = s_excl;
       if (win == 0 && tid < FCH) chunk_line0[tile * FCH + tid] = excl + s_cb[tid];
       if (win == 0 && tid == 0 && total > 0 && excl >= 1 && excl - 1 < cap)
@@ -1905,6 +1902,7 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
         if (le < 0 || le - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;
         else line_mask[id] = s_lm[j];
       }
+      if (tid == 0 && win == nwin - 1) s_tile = (int64_t)next;  // (read after the barrier below)
       __syncthreads();  // the window's lists (and, after the last, the tile's LDS) are rewritten next
       LT(6);
     }
