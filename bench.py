@@ -56,9 +56,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-warmup", type=int, default=5)  # 5 warm-up + >= 20 timed runs
     ap.add_argument("--cpu-runs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-full-mesh", action="store_true",
-                    help="also time the C restatement's scoring once over EVERY pod of this rank (chunks copied "
-                         "to the host outside the timing; ~5 s of CPU work at C4), beside the scaled sample")
+    ap.add_argument("--cpu-full-mesh", action="store_true", default=True,
+                    help="(default) also time the C restatement's scoring once over EVERY pod of this rank (chunks "
+                         "copied to the host outside the timing; ~5 s of CPU work at C4), beside the scaled sample")
+    ap.add_argument("--no-cpu-full-mesh", dest="cpu_full_mesh", action="store_false",
+                    help="skip that whole-mesh pass (the sample x pods/sample only)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-corr", action="store_true", help="skip the correlation leg (C4's second half)")

@@ -178,15 +178,19 @@ __device__ __forceinline__ uint32_t sep_flags(uint32_t wprev, uint32_t w) {
 // tile0-32+j): one coalesced pass over doc_off from the container holding byte tile0-1 (chunk_doc),
 // instead of a dependent doc_off walk per 16-byte piece.  Used by log_count and log_lines.
 constexpr int NBW = (int)(TILE / 32) + 2;  // bytes tile0-32 .. tile0+TILE+31
-template <int64_t TL>
+// ZEROED: the caller cleared s_cs after its last read of the previous tile's bitmap (behind a
+// barrier), so no clearing pass and barrier here; the chunk_doc load goes out before either.
+template <int64_t TL, bool ZEROED = false>
 __device__ __forceinline__ void tile_container_starts_t(uint32_t* s_cs, int64_t tile0, int64_t nbytes,
                                                         const int64_t* __restrict__ doc_off, int64_t D,
                                                         const int32_t* __restrict__ chunk_doc) {
   constexpr int NB = (int)(TL / 32) + 2;
-  for (int i = threadIdx.x; i < NB; i += blockDim.x) s_cs[i] = 0u;
-  __syncthreads();
-  const int64_t tend = tile0 + TL;
   int64_t k0 = tile0 < nbytes ? chunk_doc[(tile0 > 0 ? tile0 - 1 : 0) / CH] : D;
+  if (!ZEROED) {
+    for (int i = threadIdx.x; i < NB; i += blockDim.x) s_cs[i] = 0u;
+    __syncthreads();
+  }
+  const int64_t tend = tile0 + TL;
   k0 = k0 < 0 ? 0 : (k0 > D ? D : k0);  // memory safety only: the map is exact under the doc_off contract
   for (int64_t kb = k0;; kb += blockDim.x) {
     const int64_t k = kb + threadIdx.x;
@@ -815,6 +819,11 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   // the next tile's ticket while still on this one, to build its container bitmap during the
   // look-back, measured slower: 113.6 -> 135.8 us, r4r -- a claimed tile publishes its aggregate
   // only after its holder finishes the current one, and later tiles' look-backs wait for it.)
+  // (round 6: the container bitmap is cleared once the flags are done, not in a pass and barrier of
+  // its own at the tile's start.  Taking the next ticket at the start of the writes, as
+  // log_index_match does, was slower here: 109 -> 113 us, the look-back 11k -> 16k cycles per tile,
+  // r6r -- with four workgroups per CU the claimed tile's aggregate waits for the whole writes phase.)
+  for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;
   for (;;) {
   if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
   s_cnt[threadIdx.x] = 0;
@@ -825,7 +834,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
     return;
   }
   const int64_t tile0 = tile * TILE;
-  tile_container_starts(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
+  tile_container_starts_t<TILE, true>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers cover s_cnt)
   LT(0);
   // the pieces' loads go out LOG_IDX_BATCH at a time, unconditionally (a piece past the text
   // reloads the last aligned block, an aligned 16-byte block holding a text byte never crosses the
@@ -873,6 +882,7 @@ __global__ __launch_bounds__(TPB) void log_index_lines(const uint8_t* __restrict
   }
   __syncthreads();
   LT(1);
+  for (int i = threadIdx.x; i < NBW; i += TPB) s_cs[i] = 0u;  // the next tile's bitmap (its reads are done)
   // chunk counts, their scan inside the tile, the tile total
   const int64_t v = s_cnt[threadIdx.x];
   chunk_cnt[tile * TPB + threadIdx.x] = (int32_t)v;
@@ -1490,6 +1500,21 @@ __global__ __launch_bounds__(TPB) void log_hist(const int64_t* __restrict__ doc_
 // it is longer than LONG_LINE (then log_dfa_long walks it), so no line of a tile waits on the next
 // tile's workgroup (round 5's log_dfa_strad: a lane per straddling line, 35-41 us per scan).
 constexpr int LOOK = LONG_LINE;
+// log_index_match's walk: lines longer than SPLIT_T bytes are walked by two lanes (at most SPLIT_MAX
+// per window, and only while the window's lines and halves fit one pass of the workgroup)
+constexpr int SPLIT_T = 88;
+constexpr int SPLIT_MAX = 512;
+// any byte >= 0x80 among tile offsets [a, m) of s_text (a >= 0)
+__device__ __forceinline__ bool any_high(const uint32_t* tx, int a, int m) {
+  uint32_t h = 0;
+  for (int p = a & ~3; p < m; p += 4) {
+    uint32_t msk = 0x80808080u;
+    if (p < a) msk &= 0x80808080u << (8 * (a - p));
+    if (p + 4 > m) msk &= 0x80808080u >> (8 * (p + 4 - m));
+    h |= tx[p >> 2] & msk;
+  }
+  return h != 0;
+}
 template <int64_t TILE_B, int NT, bool U32>
 struct FCfg {
   static constexpr int64_t FTILE = TILE_B;                    // bytes per tile
@@ -1677,7 +1702,10 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
   __shared__ uint8_t s_conv[256];  // byte -> symbol offset (bytes >= 0x80: themselves)
   __shared__ uint32_t s_rng[3 * KRCA_DFA_NRANGE];  // the code point ranges' symbols (cp_symoff)
   __shared__ uint32_t s_cs[FNBW];
-  __shared__ uint16_t s_ls[LMAX], s_le[LMAX], s_lm[LMAX];
+  __shared__ uint16_t s_ls[LMAX], s_le[LMAX];
+  __shared__ uint32_t s_lm[LMAX / 2];  // the window's masks, two per word (atomicOr: a split line's halves)
+  __shared__ int16_t s_sj[SPLIT_MAX];  // the window's split lines
+  __shared__ int32_t s_nsplit;
   __shared__ int32_t s_cnt[FCH], s_cb[FCH];  // per 256-byte chunk: line starts, exclusive base in the tile
   __shared__ int32_t s_wsum[FCH / 64];
   __shared__ int32_t s_prev_end;  // tile offset where the previous tile's last line ends (from line 0)
@@ -1694,6 +1722,7 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
   // under them), after this tile has published its inclusive prefix: a later tile's look-back never
   // waits on a claimed tile whose holder is still walking
   if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+  for (int i = tid; i < FNBW; i += FTPB) s_cs[i] = 0u;
   for (;;) {
     __syncthreads();
     const int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane((int)s_tile);  // < 2^31 tiles
@@ -1721,7 +1750,7 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
       rawx = *reinterpret_cast<const u32x4*>(text + (q < nbytes ? q : qlast));
       pwx = tile0 + FTILE <= nbytes ? *reinterpret_cast<const uint32_t*>(text + tile0 + FTILE - 4) : 0u;
     }
-    tile_container_starts_t<FTILE + LOOK>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order LDS reuse)
+    tile_container_starts_t<FTILE + LOOK, true>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order LDS reuse)
     uint32_t regS[FNIT], regL1[FNIT];  // per piece: starts | odd lengths << 16; lengths 2/3
 #pragma unroll
     for (int it = 0; it < FNIT; ++it) {
@@ -1872,18 +1901,45 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
           ++id;
         }
       }
+      for (int i = tid; i < LMAX / 2; i += FTPB) s_lm[i] = 0u;
+      if (tid == 0) s_nsplit = 0;
       __syncthreads();
       LT(4);
-      // the DFA walk: a lane per line, from LDS (long lines: log_dfa_long)
-      for (int j = tid; j < hi - lo; j += FTPB) {
+      // The DFA walk: a lane per line, from LDS (long lines: log_dfa_long).  The walk phase lasts as
+      // long as the tile's longest line (a lane's steps are one dependent chain of LDS reads), so
+      // lines over SPLIT_T bytes take two lanes when the window has the spare lanes: [s, m) and
+      // [m', e), m' = m - WARM (warm-up: from the start state, every match starting at or after m'
+      // is found, and no match is 24 code points or longer; further back when a byte >= 0x80 there).
+      const int n = hi - lo;
+      for (int j = tid; j < n; j += FTPB) {
+        const int ls = s_ls[j], le = lo + j == total - 1 ? s_last_end : (int)s_le[j];
+        if (le >= 0 && le - ls > SPLIT_T && le - ls <= LONG_LINE) {
+          const int k = atomicAdd(&s_nsplit, 1);
+          if (k < SPLIT_MAX) s_sj[k] = (int16_t)j;
+        }
+      }
+      __syncthreads();
+      const int ns = s_nsplit;
+      const bool split = ns <= SPLIT_MAX && n + ns <= FTPB;
+      for (int t = tid; t < n + (split ? ns : 0); t += FTPB) {
+        const int j = t < n ? t : s_sj[t - n];
         const int ls = s_ls[j], le = lo + j == total - 1 ? s_last_end : (int)s_le[j];
         if (le < 0 || le - ls > LONG_LINE) continue;
-        s_lm[j] = (uint16_t)(ls < le ? dfa_walk_sym(s_text, d, s_rng, ls, le) : 0u);
+        int a = ls, b = le;
+        if (split && le - ls > SPLIT_T) {
+          const int m = ls + (le - ls + WARM) / 2;
+          if (t < n) b = m;
+          else a = max(ls, any_high(s_text, m - WARM, m) ? m - 4 * WARM - 3 : m - WARM);
+        }
+        const uint32_t mk = a < b ? dfa_walk_sym(s_text, d, s_rng, a, b) : 0u;
+        if (mk) atomicOr(&s_lm[j >> 1], mk << (16 * (j & 1)));
       }
       __syncthreads();
       LT(5);
       unsigned int next = 0;
       if (tid == 0 && win == nwin - 1) next = atomicAdd(ticket, 1u);
+      if (win == nwin - 1)  // the next tile's container bitmap (A and the LOOK pass are done with it)
+        for (int i = tid; i < FNBW; i += FTPB) s_cs[i] = 0u;
       const int64_t excl = s_excl;
       if (win == 0 && tid < FCH) chunk_line0[tile * FCH + tid] = excl + s_cb[tid];
       if (win == 0 && tid == 0 && total > 0 && excl >= 1 && excl - 1 < cap)
@@ -1900,7 +1956,7 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
         line_start[id] = tile0 + ls;
         if (le >= 0) line_end[id] = tile0 + le;  // (a last line's end also comes from the next tile)
         if (le < 0 || le - ls > LONG_LINE) long_q[atomicAdd(n_long, 1)] = (int32_t)id;
-        else line_mask[id] = s_lm[j];
+        else line_mask[id] = (s_lm[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
       }
       if (tid == 0 && win == nwin - 1) s_tile = (int64_t)next;  // (read after the barrier below)
       __syncthreads();  // the window's lists (and, after the last, the tile's LDS) are rewritten next

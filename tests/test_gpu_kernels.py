@@ -310,10 +310,13 @@ def test_log_scan_block_edges(eng):
 def test_log_scan_fused_multibyte_lines(eng, fused):
     """The fused walk keeps bytes >= 0x80 as they are among the ASCII symbol offsets and decodes a
     block's code points when one is there: a text where nearly every line holds 2-, 3- and 4-byte
-    characters (case folds among them: K, ſ, İ) equals the oracle."""
+    characters (case folds among them: K, ſ, İ) equals the oracle, short lines and split long ones."""
     rng = np.random.default_rng(23)
     words = ["é", "Error", "\u212aILLED", "ſecret not found", "panic:", "x", "Tim\u0130eout", "€", " ", "\U0001d400"]
     docs = ["\n".join("".join(rng.choice(words, 4)) for _ in range(400)) for _ in range(10)]
+    # lines over 88 bytes are walked by two lanes, the second warmed up over the 23 bytes before the
+    # split point, or 95 when one of them is >= 0x80: matches and multi-byte characters across it
+    docs += ["\n".join("".join(rng.choice(words, int(rng.integers(10, 90)))) for _ in range(60)) for _ in range(10)]
     with native.tune(eng.lib, KRCA_LOG_FUSED=fused):
         _check_docs(eng, docs)
 
