@@ -47,7 +47,7 @@ int krca_device_count(int* n_host);
 /* Kernel-development A/B switches: KRCA_SCORE_IMPL, KRCA_SCORE_CHUNK, KRCA_SCORE_NT, KRCA_PPR_GRID, KRCA_PPR_DICT,
  * KRCA_LOG_IMPL, KRCA_GROUP_IMPL, KRCA_CORR_DEBUG, KRCA_CORR_RS_GRID, KRCA_CORR_BATCH, KRCA_CORR_AMB_TILE,
  * KRCA_PPR_FUSE, KRCA_PPR_NT, KRCA_PPR_XCD, KRCA_LOG_FUSED, KRCA_CORR_RS_GROUP, KRCA_CORR_SIDE, KRCA_CORR_RS_Q16,
- * KRCA_CORR_CAPC, KRCA_CORR_KM_EXTRA, KRCA_CORR_RSG_GRID, KRCA_CORR_PROJ.  Initialised once from the environment variables
+ * KRCA_CORR_CAPC, KRCA_CORR_KM_EXTRA, KRCA_CORR_RSG_GRID, KRCA_CORR_PROJ, KRCA_CORR_PERSIST.  Initialised once from the environment variables
  * of the same names when the library loads; launchers never call getenv.  Process-global, not
  * thread-safe (set them before launching work).  Unknown names: KRCA_EINVAL. */
 int krca_tune_set(const char* name, int32_t value);

@@ -42,6 +42,7 @@ const NamedKnob kKnobs[] = {
     {"KRCA_CORR_KM_EXTRA", &Tuning::corr_km_extra},
     {"KRCA_CORR_RSG_GRID", &Tuning::corr_rsg_grid},
     {"KRCA_CORR_PROJ", &Tuning::corr_proj},
+    {"KRCA_CORR_PERSIST", &Tuning::corr_persist},
 };
 Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20), env_int("KRCA_SCORE_NT", 1),
                  env_int("KRCA_PPR_GRID", 0),   env_int("KRCA_PPR_DICT", 1),     env_int("KRCA_LOG_IMPL", 0),
@@ -52,7 +53,8 @@ Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20),
                  env_int("KRCA_PPR_XCD", 0), env_int("KRCA_LOG_FUSED", 0), env_int("KRCA_CORR_RS_GROUP", 1),
                  env_int("KRCA_CORR_SIDE", 0), env_int("KRCA_CORR_RS_Q16", 1),
                  env_int("KRCA_CORR_CAPC", 0), env_int("KRCA_CORR_KM_EXTRA", 6),
-                 env_int("KRCA_CORR_RSG_GRID", 0), env_int("KRCA_CORR_PROJ", 1)};
+                 env_int("KRCA_CORR_RSG_GRID", 0), env_int("KRCA_CORR_PROJ", 1),
+                 env_int("KRCA_CORR_PERSIST", 0)};
 const NamedKnob* find_knob(const char* name) {
   if (!name) return nullptr;
   for (const NamedKnob& k : kKnobs)

@@ -300,6 +300,10 @@ struct Geo {
   static constexpr int LDS_MAIN = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
   static constexpr int LDS_BYTES = LDS_MAIN;
   static constexpr int CAPL = (LDS_MAIN - EPI_LIST_OFF) / (NW * 8);  // epilogue list entries per wave
+  // persistent main pass (corr_main_persist): the whole 160 KiB, the epilogue's arrays and lists past
+  // the two stage buffers, so the next tile's first stage can land while this tile's epilogue runs
+  static constexpr int LDS_PERSIST = 160 * 1024;
+  static constexpr int CAPL_P = (LDS_PERSIST - LDS_STAGE - EPI_LIST_OFF) / (NW * 8);
   // 16-byte chunk c of staged row r, XOR-swizzled: the 256/ROWB rows of one 256-B bank row sit in
   // distinct granule groups and the key (r / (256/ROWB)) % CPR spreads the rest, so every 16-lane
   // ds_read_b128 phase of 16 rows hits 16 distinct 4-bank granules
@@ -361,15 +365,68 @@ struct TileArgs {
   const float* z32;  // MAIN: fp32 rows for the in-tile re-score of a full list
   int T;
   int64_t st0, st_end;  // MAIN: this launch's batch [st0, st_end) of the rank's super-tiles
+  unsigned* tick;       // MAIN, persistent: one ticket counter per XCD for this batch (zeroed)
 };
+
+// Persistent main pass: the state one workgroup carries from tile to tile.
+struct PState {
+  int b0;        // LDS stage buffer holding this tile's first K stage
+  bool staged;   // that stage was loaded by the previous tile's last K step (no prologue wait)
+  bool redo;     // a later window of the same tile (rare): product again, no ticket, no next-tile load
+  int x;         // this workgroup's XCD (its ticket counter)
+  int* tk_next;  // LDS words {I, J} of the next tile, written by thread 0 during this tile's K loop
+};
+constexpr int TK_OFF = 8176;  // ticket words in the epilogue area (past the epilogue's arrays)
+
+// slot L2 of the main pass's XCD-aware order -> tile (I, J); false for slots below the diagonal or
+// past this batch / the triangle.  Workgroups are dispatched round-robin over the 8 XCDs, so slot
+// L2 = (b % 8) * per_xcd + b / 8 gives each XCD a contiguous run of slots; consecutive slots walk
+// the upper triangle in SUPER x SUPER super-tiles, so the tiles an XCD has in flight share 2*SUPER
+// row blocks through its L2.
+__device__ __forceinline__ bool main_slot(const TileArgs& A, int64_t L, int64_t& I, int64_t& J) {
+  const int64_t ns = (A.nb2 + SUPER - 1) / SUPER;
+  const int64_t sl = A.st0 + L / (SUPER * SUPER);  // this batch's share of the rank's super-tiles
+  if (sl >= A.st_end) return false;
+  const int64_t st = sl * A.sh.G + A.sh.g;
+  if (st >= ns * (ns + 1) / 2) return false;
+  int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
+  while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
+  while (SJ * (SJ + 1) / 2 > st) --SJ;
+  const int64_t SI = st - SJ * (SJ + 1) / 2;
+  const int64_t in = L % (SUPER * SUPER);
+  I = SI * SUPER + in / SUPER;
+  J = SJ * SUPER + in % SUPER;
+  return I <= J && J < A.nb2;
+}
+
+// thread 0 of a persistent workgroup: ticket t of XCD x (and more tickets past invalid slots) -> the
+// next tile, or I = -1 when the XCD's run is used up
+__device__ __forceinline__ void take_tile(const TileArgs& A, int x, unsigned t, int* out) {
+  int64_t I = -1, J = -1;
+  for (;;) {
+    if ((int64_t)t >= A.per_xcd) {
+      I = -1;
+      break;
+    }
+    if (main_slot(A, (int64_t)x * A.per_xcd + t, I, J)) break;
+    t = atomicAdd(&A.tick[x], 1u);
+  }
+  if (I >= 0 && A.debug == 4) I = J = x;  // profiling aid: product only, operands L2-resident
+  out[0] = (int)I;
+  out[1] = (int)J;
+}
 
 // One tile: row block I (256 pods), column block J (TC pods).  Main / rect passes: the epilogue takes
 // the flagged values of list slots [win, win + CAPL) of each wave; returns whether some wave has
 // more (rare: the caller runs the tile again for the next window; the counts of |r| > tau + eps are
 // taken in window 0 only).
-template <int KC, int MODE, int TC>
+// PERSIST (main pass only, corr_main_persist): the first K stage may already be in LDS buffer
+// ps->b0; the last K step loads the NEXT tile's first stage (ps->tk_next) into the idle buffer; the
+// epilogue works past the stage buffers and runs every window itself (the accumulators stay live).
+template <int KC, int MODE, int TC, bool PERSIST = false>
 __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, const int64_t J, const bool own,
-                                          const int win) {
+                                          const int win, const PState* ps = nullptr) {
+  static_assert(!PERSIST || (MODE == MODE_MAIN && TC == 256), "persistent: main pass, 256-column tiles");
   using G = Geo<TC>;
   constexpr bool SAMPLE = MODE == MODE_SAMPLE;
   static_assert(!SAMPLE || TC == 256, "the sample pass parks 256-column tiles");
@@ -378,7 +435,11 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   const int Tp = A.Tp;
   const Shard& sh = A.sh;
   const int debug = A.debug;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // persistent: the thread index made opaque per tile, so that nothing derived from it (epilogue
+  // addresses, list codes) is hoisted out of the tile loop and kept live across it (spills)
+  int tid_ = threadIdx.x;
+  if constexpr (PERSIST) asm volatile("" : "+v"(tid_));
+  const int tid = tid_, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w / G::NWC, wc = w % G::NWC;
   const int64_t rowA = I * TB, rowB = J * TC;
   // main / rect epilogue operands, loaded now so their latency hides behind the K loop: thread rq
@@ -424,30 +485,30 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   const uint16_t* gA = A.zA + rowA * Tp;
   const uint16_t* gB = A.zh + rowB * Tp;
   const int prow = lane / G::CPR, pslot = lane % G::CPR;
-  auto glds_a = [&](int buf, int k0) {
+  auto glds_a = [&](int buf, const uint16_t* src, int k0) {
     char* sbase = smem + buf * G::STAGE;
 #pragma unroll
     for (int q = 0; q < G::NPA; ++q) {
       const int piece = w + G::NW * q;
       const int row = G::RPP * piece + prow;
-      __builtin_amdgcn_global_load_lds(gA + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
+      __builtin_amdgcn_global_load_lds(src + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
                                        (__attribute__((address_space(3))) void*)(sbase + piece * 1024), 16, 0, 0);
     }
   };
-  auto glds_b = [&](int buf, int k0) {
+  auto glds_b = [&](int buf, const uint16_t* src, int k0) {
     char* sbase = smem + buf * G::STAGE;
 #pragma unroll
     for (int q = 0; q < G::NPB; ++q) {
       const int piece = w + G::NW * q;
       const int row = G::RPP * piece + prow;
-      __builtin_amdgcn_global_load_lds(gB + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
+      __builtin_amdgcn_global_load_lds(src + (int64_t)row * Tp + k0 + ((pslot ^ G::key(row)) << 3),
                                        (__attribute__((address_space(3))) void*)(sbase + TB * G::ROWB + piece * 1024),
                                        16, 0, 0);
     }
   };
   auto glds = [&](int buf, int k0) {
-    glds_a(buf, k0);
-    glds_b(buf, k0);
+    glds_a(buf, gA, k0);
+    glds_b(buf, gB, k0);
   };
   const int r16 = lane & 15, g4 = lane >> 4;
   // Fragments (16x16x32: lane l holds A[row l & 15][k = 8 (l >> 4) .. + 7] of a 16-row block, B the
@@ -489,11 +550,24 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
         acc[i + 4][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[i], bfr[set][j], acc[i + 4][j], 0, 0, 0);
   };
   const int nk = Tp / G::BKS;
-  glds(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ld_alo(0, 0);
-  ld_b(0, 0, 0);
+  const int b0 = PERSIST ? ps->b0 : 0;
+  if (!PERSIST || !ps->staged) {
+    glds(b0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // persistent: thread 0 takes the next tile's ticket now and resolves it at step 1 (the atomic's
+  // return lands under step 0); every wave reads the tile at the last step, after the barriers
+  unsigned traw = 0;
+  if constexpr (PERSIST) {
+    if (!ps->redo && tid == 0) {
+      traw = atomicAdd(&A.tick[ps->x], 1u);
+      if (nk < 3) take_tile(A, ps->x, traw, ps->tk_next);
+    }
+    if (!ps->redo && nk < 3) __syncthreads();
+  }
+  ld_alo(b0, 0);
+  ld_b(0, b0, 0);
   // Per stage (64 deep = sub-steps 0 and 1): A(0) alo x b0 while reading ahi(0); B(0) ahi x b0 while
   // reading alo(1), b1; A(1) alo x b1 while reading ahi(1); barrier; B(1) ahi x b1 while reading
   // alo(0), b0 of the next stage.
@@ -504,21 +578,35 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
   }                                                                                       \
   __builtin_amdgcn_sched_barrier(0);
   for (int s = 0; s < nk; ++s) {
-    const int buf = s & 1;
+    const int buf = (s & 1) ^ b0;
     // stage buf ^ 1 was last read in step s-1; every wave retired those reads (lgkmcnt(0)) before
     // the barrier that ended it.  The next stage's A pieces go out before the first MFMA phase, its
     // B pieces after it: issued together (or in three groups) they ran 4 % (2 %) slower.  The last
-    // step re-loads its own stage into the idle buffer (never read), so the loop has no branch.
+    // step re-loads its own stage into the idle buffer (never read), so the loop has no branch --
+    // or, persistent, the next tile's first stage.
     // (An L2 prefetch of step s + 2 by 4-byte LDS-DMA loads, one per 128-B line, ran 7 % slower in
     // the 16x16x32 form: its issue slots and a lower clock cost more than the latency it hid;
     // without any staging in the loop the product ran 9.3 vs 12.8 ms, clock 1.97 vs 1.74 GHz.)
-    const int kn = (s + 1 < nk ? s + 1 : s) * G::BKS;
-    glds_a(buf ^ 1, kn);
+    int kn = (s + 1 < nk ? s + 1 : s) * G::BKS;
+    const uint16_t* sa = gA;
+    const uint16_t* sb = gB;
+    if constexpr (PERSIST) {
+      if (s == 1 && nk >= 3 && tid == 0 && !ps->redo) take_tile(A, ps->x, traw, ps->tk_next);
+      if (s == nk - 1 && !ps->redo) {
+        const int nI = ps->tk_next[0], nJ = ps->tk_next[1];
+        if (nI >= 0) {
+          sa = A.zA + (int64_t)nI * TB * Tp;
+          sb = A.zh + (int64_t)nJ * TC * Tp;
+          kn = 0;
+        }
+      }
+    }
+    glds_a(buf ^ 1, sa, kn);
     __builtin_amdgcn_sched_barrier(0);
     ld_ahi(buf, 0);
     mm_lo(0);
     CORR_PIN(4, 1)
-    glds_b(buf ^ 1, kn);
+    glds_b(buf ^ 1, sb, kn);
     __builtin_amdgcn_sched_barrier(0);
     ld_alo(buf, 1);
     ld_b(1, buf, 1);
@@ -568,10 +656,11 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     constexpr bool RECT = MODE == MODE_RECT;
     constexpr bool HITS = MODE == MODE_MAIN;    // |r| > tau + eps counted in step 1 (first window)
     constexpr bool SETTLE = MODE == MODE_MAIN;  // pairs settled by their bound counted in step 2
-    constexpr int CAPL = G::CAPL;
+    constexpr int CAPL = PERSIST ? G::CAPL_P : G::CAPL;
     // an entry after classification: row | col << 8 | candidate bits << 16 | (ambiguous rank + 1) << 18
     static_assert(G::NW * CAPL < (1 << 14) - 1, "ambiguous ranks of a window fit 14 bits");
-    float* sphr = reinterpret_cast<float*>(smem);  // phi of the 256 row pods
+    char* const ebase = smem + (PERSIST ? G::LDS_STAGE : 0);  // persistent: past the stage buffers
+    float* sphr = reinterpret_cast<float*>(ebase);  // phi of the 256 row pods
     float* sphc = sphr + TB;                        // phi of the TC column pods
     int* srcnt = reinterpret_cast<int*>(sphc + TC);  // |r| > tau counts per row / column
     int* sccnt = srcnt + TB;
@@ -581,7 +670,20 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
     int* wcount = reinterpret_cast<int*>(sdnc + TC);  // list length per wave
     int* sflag = wcount + G::NW;  // [0] a list passed its window, [1] ranked ambiguous pairs
     long long* sbase = reinterpret_cast<long long*>(sflag + 4);  // their base in the list (slots past amb_cap: decided here)
-    int2* lists = reinterpret_cast<int2*>(smem + EPI_LIST_OFF);
+    int2* lists = reinterpret_cast<int2*>(ebase + EPI_LIST_OFF);
+    static_assert(7 * 1024 + 64 <= TK_OFF && TK_OFF + 16 <= EPI_LIST_OFF, "epilogue arrays, ticket words, lists");
+    if (diag) {
+      const int doff = (int)(rowB - rowA);  // global row == global column <=> row - col == doff
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (wr * 128 + i * 16 + 4 * g4 + e == wc * 64 + j * 16 + r16 + doff) acc[i][j][e] = 0.f;
+    }
+    // one window of the lists (slots [win, win + CAPL) of each wave); returns whether one follows
+    auto epi = [&](const int win) -> bool {
     {
       if (rq < TB) {
         sphr[rq] = r_phi;
@@ -600,16 +702,6 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       }
     }
     __syncthreads();
-    if (diag) {
-      const int doff = (int)(rowB - rowA);  // global row == global column <=> row - col == doff
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (wr * 128 + i * 16 + 4 * g4 + e == wc * 64 + j * 16 + r16 + doff) acc[i][j][e] = 0.f;
-    }
     // classification of one flagged value: bit 0 candidate of the row pod, bit 1 of the column pod
     // (never in a diagonal tile: both orders are present), bit 2 ambiguous, bit 3 settled above tau
     auto classify = [&](int row, int col, float v) -> int {
@@ -805,6 +897,8 @@ __device__ __forceinline__ bool tile_body(const TileArgs& A, const int64_t I, co
       }
       return more;
     }
+    };
+    return epi(win);
   } else {
     // ---- sample pass: park each 128-row half in LDS, two lanes per (row, 128-column half) -------
     float* tile = reinterpret_cast<float*>(smem);
@@ -947,19 +1041,8 @@ __global__ __launch_bounds__(Geo<TC>::NTH) __attribute__((amdgpu_waves_per_eu(2)
     const int64_t L2 = (b & 7) * A.per_xcd + (b >> 3);
     const int64_t L = L2 / SPLIT;
     const int part = (int)(L2 % SPLIT);
-    const int64_t ns = (A.nb2 + SUPER - 1) / SUPER;
-    const int64_t sl = A.st0 + L / (SUPER * SUPER);  // this batch's share of the rank's super-tiles
-    if (sl >= A.st_end) return;
-    const int64_t st = sl * A.sh.G + A.sh.g;
-    if (st >= ns * (ns + 1) / 2) return;
-    int64_t SJ = (int64_t)((sqrt(8.0 * (double)st + 1.0) - 1.0) * 0.5);
-    while ((SJ + 1) * (SJ + 2) / 2 <= st) ++SJ;
-    while (SJ * (SJ + 1) / 2 > st) --SJ;
-    const int64_t SI = st - SJ * (SJ + 1) / 2;
-    const int64_t in = L % (SUPER * SUPER);
-    int64_t I = SI * SUPER + in / SUPER;
-    int64_t J = SJ * SUPER + in % SUPER;
-    if (I > J || J >= A.nb2) return;
+    int64_t I, J;
+    if (!main_slot(A, L, I, J)) return;
     if (A.debug == 4) I = J = (blockIdx.x & 7);  // profiling aid: product only, operands L2-resident
     // window 0 outside the loop: the loop's copy may hold more registers (values kept across its
     // iterations); it runs only for a tile whose lists pass CAPL entries in some wave
@@ -968,6 +1051,48 @@ __global__ __launch_bounds__(Geo<TC>::NTH) __attribute__((amdgpu_waves_per_eu(2)
         __syncthreads();  // the next window reuses the LDS
         if (!tile_body<KC, MODE_MAIN, TC>(A, I, J * SPLIT + part, false, win)) break;
       }
+    }
+  }
+}
+
+// The main pass as persistent workgroups (KRCA_CORR_PERSIST=1; A/B only, R7a: 2-5 % slower than a
+// workgroup per tile, so the per-tile prologue and launch were not what the main pass waits on): one 160 KiB workgroup
+// per CU takes the tiles of its XCD's run by ticket (so a workgroup that starts late, its CU busy
+// with a re-score, takes fewer), and each tile's last K step loads the next tile's first stage: no
+// tile waits on a prologue load or a workgroup launch.  Same tiles, same per-tile arithmetic and
+// epilogue as corr_tiles<MODE_MAIN>, so the same bits.
+template <int KC>
+__global__ __launch_bounds__(Geo<256>::NTH) __attribute__((amdgpu_waves_per_eu(2))) void corr_main_persist(TileArgs A) {
+  using G = Geo<256>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* tk = reinterpret_cast<int*>(smem + G::LDS_STAGE + TK_OFF);  // two slots {I, J}: this tile's, the next
+  const int x = blockIdx.x & 7;
+  if (threadIdx.x == 0) take_tile(A, x, atomicAdd(&A.tick[x], 1u), tk);
+  __syncthreads();
+  const int nk = A.Tp / G::BKS;
+  PState ps;
+  ps.b0 = 0;
+  ps.staged = false;
+  ps.redo = false;
+  ps.x = x;
+  for (int cur = 0;; cur ^= 1) {
+    const int I = tk[2 * cur], J = tk[2 * cur + 1];
+    if (I < 0) break;  // uniform: every wave read the slot after the same barriers
+    ps.tk_next = tk + 2 * (cur ^ 1);
+    const bool more = tile_body<KC, MODE_MAIN, 256, true>(A, I, J, false, 0, &ps);
+    ps.b0 ^= nk & 1;  // the last K step loaded the next tile's first stage into the other buffer
+    ps.staged = true;
+    if (more) {
+      // rare: some wave listed more than CAPL_P values; each later window runs the product again
+      // (its own stage loads: the next tile's prefetched stage is overwritten and loaded again)
+      PState pr = ps;
+      pr.redo = true;
+      pr.staged = false;
+      for (int win = Geo<256>::CAPL_P;; win += Geo<256>::CAPL_P) {
+        __syncthreads();  // the window reuses the LDS
+        if (!tile_body<KC, MODE_MAIN, 256, true>(A, I, J, false, win, &pr)) break;
+      }
+      ps.staged = false;
     }
   }
 }
@@ -1838,6 +1963,7 @@ struct CorrWs {  // views into a caller's candidate workspace
   double* dct;          // [KP][T] the basis
   int Tq;               // T rounded up to 8
   unsigned long long* amb_n;  // [2]: the lists' fill
+  unsigned* tick;             // [8 * batches]: the persistent main pass's ticket counters per XCD
   int32_t *gcnt, *goff, *gcur, *gsum;  // grouped re-score: entries per row pod, offsets [P + 1], cursors, scan blocks
   int2* gs;                            // [amb_cap] a list's entries grouped by row pod
   uint16_t* zs;         // [RECT_ROWS][Tp]
@@ -1891,6 +2017,7 @@ int64_t ws_layout(int64_t P, int T, int Tp, int KC, int64_t n_loc, int G, char* 
     w.dct = reinterpret_cast<double*>(take(2 * (int64_t)KP * T));
   }
   w.amb_n = reinterpret_cast<unsigned long long*>(take(4));
+  w.tick = reinterpret_cast<unsigned*>(take(8 * krca::ceil_div(n_st, SB)));
   w.gcnt = reinterpret_cast<int32_t*>(take(P));
   w.goff = reinterpret_cast<int32_t*>(take(P + 1));
   w.gcur = reinterpret_cast<int32_t*>(take(P));
@@ -1921,7 +2048,21 @@ int set_lds_attr() {
   int rc = set_lds_attr1<KC, MODE_MAIN, 256>();
   if (!rc) rc = set_lds_attr1<KC, MODE_SAMPLE, 256>();
   if (!rc) rc = set_lds_attr1<KC, MODE_RECT, 256>();
+  static bool done_p = false;
+  if (!rc && !done_p) {
+    KRCA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_main_persist<KC>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256>::LDS_PERSIST));
+    done_p = true;
+  }
   return rc;
+}
+
+// compute units of the current device (the persistent main pass: one workgroup per CU)
+inline int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 256;
+  return n > 0 ? n : 256;
 }
 
 struct Dims {
@@ -2092,6 +2233,10 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   KRCA_HIP(hipMemsetAsync(count, 0, (size_t)d.P * sizeof(int32_t), st));
   KRCA_HIP(hipMemsetAsync(ws.amb_n, 0, 2 * sizeof(unsigned long long), st));
   const int64_t n_st = n_supertiles(d.nb2);
+  const bool persist = krca::tuning().corr_persist != 0;
+  if (persist)  // the ticket counters of every batch (a rank runs at most as many as one device)
+    KRCA_HIP(hipMemsetAsync(ws.tick, 0, (size_t)8 * krca::ceil_div(n_st, sb_batch()) * sizeof(unsigned), st));
+  const int cu_per_xcd = std::max(1, cu_count() / 8);
   const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
   if (n_mine == 0) return KRCA_OK;
   const Shard sh{0, G, g, 0};
@@ -2163,8 +2308,15 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
     ta.st_end = std::min(n_mine, s0 + SB);
     // 256 x 256 tiles, XCD-aware slots
     ta.per_xcd = ((ta.st_end - s0) * SUPER * SUPER + 7) / 8;
-    hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, 256>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<256>::NTH),
-                       Geo<256>::LDS_BYTES, st, ta);
+    if (persist) {
+      ta.tick = ws.tick + 8 * b;
+      const int64_t wg_x = std::min<int64_t>(cu_per_xcd, ta.per_xcd);  // workgroups per XCD
+      hipLaunchKernelGGL(corr_main_persist<KC>, dim3((unsigned)(8 * wg_x)), dim3(Geo<256>::NTH),
+                         Geo<256>::LDS_PERSIST, st, ta);
+    } else {
+      hipLaunchKernelGGL((corr_tiles<KC, MODE_MAIN, 256>), dim3((unsigned)(8 * ta.per_xcd)), dim3(Geo<256>::NTH),
+                         Geo<256>::LDS_BYTES, st, ta);
+    }
     KRCA_LAUNCH_CHECK();
     if (dbg != 0) continue;
     if (fork) {

@@ -119,6 +119,9 @@ struct Tuning {
   int corr_proj;      // KRCA_CORR_PROJ: the grouped re-score tries the projection bound (DCT basis) before the
                       // partner's int16 row: 1 when the main pass runs in several batches, 2 always, 0 never
                       // (identical counts)
+  int corr_persist;   // KRCA_CORR_PERSIST: the main pass as persistent workgroups that load the next tile's first
+                      // K stage under the current one (1) or one workgroup per tile (0, default: R7a, the
+                      // persistent form ran 2-5 % slower); same bits
 };
 const Tuning& tuning();
 int tuning_ppr_dict();

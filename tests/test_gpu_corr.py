@@ -204,11 +204,13 @@ def test_corr_batches_and_full_lists_identical(eng):
     # (KRCA_CORR_PROJ = 0 / 2: the grouped re-score never / always with the projection bound -- the
     # default uses it only when the main pass runs in several batches; counts must not move)
     try:
+        # (KRCA_CORR_PERSIST = 1: persistent main-pass workgroups instead of one per tile)
         for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2), (b"KRCA_CORR_PROJ", 0),
-                          (b"KRCA_CORR_PROJ", 2)):
+                          (b"KRCA_CORR_PROJ", 2), (b"KRCA_CORR_PERSIST", 1)):
             assert lib.krca_tune_set(knob, val) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
-            lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 1}[knob])
+            lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 1,
+                                     b"KRCA_CORR_PERSIST": 0}[knob])
             for key in ("idx", "val", "count"):
                 assert np.array_equal(got[key], ref[key]), (knob, key)
             assert (got["cert"] > 0).all(), knob
@@ -216,6 +218,7 @@ def test_corr_batches_and_full_lists_identical(eng):
         lib.krca_tune_set(b"KRCA_CORR_RSG_GRID", 0)
         lib.krca_tune_set(b"KRCA_CORR_KM_EXTRA", 6)
         lib.krca_tune_set(b"KRCA_CORR_PROJ", 1)
+        lib.krca_tune_set(b"KRCA_CORR_PERSIST", 0)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
     _, _, bad = device_check(ref, z, [rows], k)
