@@ -86,24 +86,30 @@ def main():
         e1.record()
     torch.cuda.synchronize()
     ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+    iters_run, _ = sh.ctl_read()  # the stop rule's count: the launches past it return at once
     N, E = a.pods, m.n_edges
     plan = sh.plan.cpu().numpy().reshape(-1, 4)
     nu = plan[:, 0] >> 32
     ne = plan[:, 3] - plan[:, 2]
     d = nu > 0
     edge_bytes = int(4 * nu[d].sum() + 2 * ne[d].sum() + 4 * ne[~d].sum())
-    # algorithmic bytes per iteration: plan + lane info (a 2-byte word per lane and
-    # a 2-byte sum slot per row) + packed columns + q and the alpha/outdeg coefficients read + weight
+    # algorithmic bytes per iteration: plan + lane info (two 2-byte words per
+    # ppr_step lane, krca_ppr_lane_size) + packed columns + q and the alpha/outdeg coefficients read + weight
     # codes written + codes gathered once (compulsory); r is written on the last iteration.
     # fabric_bytes_per_iter prices the gathered table once per XCD instead (8 XCDs, each with its
     # own L2: the least an L2-miss counter can show for a table that every XCD's rows gather from
     # at random).
-    base = 32 * len(plan) + 4 * 256 * len(plan) + edge_bytes + 8 * N + 8 * N + 4 * N
+    lane_bytes = 2 * int(eng.lib.krca_ppr_lane_size(4 * len(plan)))
+    base = 32 * len(plan) + lane_bytes + edge_bytes + 8 * N + 8 * N + 4 * N
     per_iter = base + 4 * N
     fabric_per_iter = base + 8 * 4 * N
     out = dict(kernel="ppr propagate (init + 30 x (step + reduce))", dict=a.dict, order=a.order, xcd=a.xcd, pods=N, edges=E,
                dict_blocks=int(d.sum()), blocks=len(plan), gathers=int(nu[d].sum() + ne[~d].sum()),
                ms=ms, ms_median=float(np.median(ms)), us_per_iter=float(np.median(ms)) * 1e3 / cfg.iters,
+               iters_run=iters_run,
+               # the whole propagate per iteration that did work (an upper bound: it includes the
+               # launches past the stop rule, ~5 us each); per-dispatch times are in the kernel trace
+               us_per_working_iter=float(np.median(ms)) * 1e3 / max(iters_run, 1),
                bytes_per_iter=per_iter, fabric_bytes_per_iter=fabric_per_iter)
     if a.check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
