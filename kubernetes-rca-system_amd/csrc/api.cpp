@@ -53,7 +53,7 @@ Tuning g_tune = {env_int("KRCA_SCORE_IMPL", 0), env_int("KRCA_SCORE_CHUNK", 20),
                  env_int("KRCA_PPR_XCD", 0), env_int("KRCA_LOG_FUSED", 0), env_int("KRCA_CORR_RS_GROUP", 1),
                  env_int("KRCA_CORR_SIDE", 0), env_int("KRCA_CORR_RS_Q16", 1),
                  env_int("KRCA_CORR_CAPC", 0), env_int("KRCA_CORR_KM_EXTRA", 6),
-                 env_int("KRCA_CORR_RSG_GRID", 0), env_int("KRCA_CORR_PROJ", 1),
+                 env_int("KRCA_CORR_RSG_GRID", 0), env_int("KRCA_CORR_PROJ", 2),
                  env_int("KRCA_CORR_PERSIST", 0)};
 const NamedKnob* find_knob(const char* name) {
   if (!name) return nullptr;

@@ -61,8 +61,13 @@ constexpr int KM = 24;    // candidates re-scored per pod in the merge (>= k + 6
 constexpr int KMAX = 16;  // largest k served
 constexpr int NSB = 16;   // 128-pod column blocks in the threshold sample (2048 pods)
 constexpr int NSL = NSB + 2;  // sample lists per pod: NSB sample blocks + the pod's own 256-block
-constexpr int CAPC = 2048;    // candidate buffer per pod (main pass appends; 1024 overflowed ~1 % of
-                              // the pods at C3 / 1M, whose rectangle pass cost 1.8 ms / 123 ms, R5k)
+#ifndef KRCA_CORR_CAPC_SLOTS
+#define KRCA_CORR_CAPC_SLOTS 4096  // (an A/B build can set it: tools/build_variant.sh ... -DKRCA_CORR_CAPC_SLOTS=2048)
+#endif
+constexpr int CAPC = KRCA_CORR_CAPC_SLOTS;  // candidate buffer per pod (main pass appends; 1024 overflowed ~1 % of
+                              // the pods at C3 / 1M, whose rectangle pass cost 1.8 ms / 123 ms, R5k;
+                              // 2048 still overflowed at C3: rectangle pass 1.4-1.7 ms on the merge
+                              // chain, R7a / R7d; 4096 since R7d: 32 GB of buffer at 1M pods)
 // Ambiguous |r| ~ tau pairs (screening value within eps of tau, not settled by the pair's own
 // bound) are re-scored in float64 for exact counts.  C3's random-walk series put ~130 partners per
 // pod within eps of tau = 0.5 (~170 in EVERY 256 x 256 tile, about half settled in the tile), so the
@@ -2145,10 +2150,12 @@ inline int cand_cap() {
 
 // the grouped re-score reads int16 partner rows (written by corr_dnorm)
 inline bool q16_rows() { return krca::tuning().corr_rs_q16 && krca::tuning().corr_rs_group; }
-// ... and tries the projection bound before them (KRCA_CORR_PROJ: 1 = when the main pass runs in more
-// than one batch, the default; 2 = always; 0 = never).  The projections cost ~1 ms at C3 (100k pods,
-// one batch), where they save about as much on the re-score that runs after the main pass (R6e-g);
-// with many batches every re-score runs beside a later batch and its HBM traffic is what slows it.
+// ... and tries the projection bound before them (KRCA_CORR_PROJ: 2 = always, the default since R7d;
+// 1 = when the main pass runs in more than one batch; 0 = never).  The projections cost ~1 ms at C3
+// (100k pods, one batch): beside the main pass they slowed it by about as much as they saved on the
+// re-score after it (R6e-g), so round 6 kept them for several batches only; krca_corr_topk now
+// launches them on the side stream beside the threshold sample instead (launch_proj), where they
+// slow nothing on the critical path: C3 21.85 -> ~21.3 ms, the re-score 5.8 -> 4.3 ms (R7d).
 inline bool proj_bound(int64_t n_batches) {
   const int m = krca::tuning().corr_proj;
   return krca::tuning().corr_rs_group && (m == 2 || (m == 1 && n_batches > 1));
@@ -2220,13 +2227,40 @@ struct SideWork {
   }
 };
 
+// the projection bound's rows (corr_dct_basis, corr_proj) on the side stream, ordered before every
+// re-score there; only the re-score reads them
+int launch_proj(const uint16_t* zh, const float* z32, const Dims& d, const CorrWs& ws, SideWork& sw) {
+  hipStream_t ps = sw.st;
+  if (sw.side != sw.st && krca::tuning().corr_side == 0) {  // (every re-score on the side stream)
+    KRCA_HIP(hipEventRecord(sw.ev[4], sw.st));  // (ev[4] is re-recorded on the side stream at the join)
+    KRCA_HIP(hipStreamWaitEvent(sw.side, sw.ev[4], 0));
+    sw.forked = true;
+    ps = sw.side;
+  }
+  hipLaunchKernelGGL(corr_dct_basis, dim3((unsigned)krca::ceil_div((int64_t)KP * d.T, TPB)), dim3(TPB), 0, ps, ws.dct,
+                     d.T);
+  KRCA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(corr_proj, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)), dim3(TPB), 0, ps, z32, zh, d.P, d.T,
+                     d.Tp, (const double*)ws.dct, ws.proj, ws.pqz, ws.pqe);
+  KRCA_LAUNCH_CHECK();
+  return KRCA_OK;
+}
+
+// whether rank g of G re-scores with the projection bound (its share of the super-tiles in batches)
+inline bool proj_for(const Dims& d, int G, int g) {
+  const int64_t n_st_all = n_supertiles(d.nb2);
+  const int64_t n_mine0 = n_st_all > g ? (n_st_all - g + G - 1) / G : 0;
+  return proj_bound((n_mine0 + sb_batch() - 1) / sb_batch());
+}
+
 // 2. upper-triangle tiles (every G-th super-tile from g): appends into ws.buf, tau counts.  The
 //    main pass runs in batches of SB super-tiles; after batch b its ambiguous list (b & 1) is
 //    re-scored on `sw.side` (the caller's stream itself when no side stream is wanted) while batch
 //    b + 1 fills the other list.  count is final on sw.st once sw is destroyed (joined).
+//    proj_launched: the caller already launched the projections (krca_corr_topk: beside the sample).
 template <int KC>
 int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int g, const float* phi, const CorrWs& ws,
-                int32_t* count, int dbg, SideWork& sw) {
+                int32_t* count, int dbg, SideWork& sw, bool proj_launched = false) {
   hipStream_t st = sw.st;
   if (int rc = set_lds_attr<KC>()) return rc;
   KRCA_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)d.P * sizeof(int32_t), st));
@@ -2243,25 +2277,9 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
                      d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
   KRCA_LAUNCH_CHECK();
-  const int64_t n_st_all = n_supertiles(d.nb2);
-  const int64_t n_mine0 = n_st_all > g ? (n_st_all - g + G - 1) / G : 0;
-  const bool use_proj = proj_bound((n_mine0 + sb_batch() - 1) / sb_batch());
-  if (use_proj) {
-    // only the re-score reads the projections: on the side stream (ordered before every re-score
-    // there), beside the main pass rather than in front of it (0.3-1 ms of C3's critical path)
-    hipStream_t ps = st;
-    if (sw.side != st && krca::tuning().corr_side == 0) {  // (every re-score on the side stream)
-      KRCA_HIP(hipEventRecord(sw.ev[4], st));  // (ev[4] is re-recorded on the side stream at the join)
-      KRCA_HIP(hipStreamWaitEvent(sw.side, sw.ev[4], 0));
-      sw.forked = true;
-      ps = sw.side;
-    }
-    hipLaunchKernelGGL(corr_dct_basis, dim3((unsigned)krca::ceil_div((int64_t)KP * d.T, TPB)), dim3(TPB), 0, ps, ws.dct,
-                       d.T);
-    KRCA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(corr_proj, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)), dim3(TPB), 0, ps, z32, zh, d.P, d.T,
-                       d.Tp, (const double*)ws.dct, ws.proj, ws.pqz, ws.pqe);
-    KRCA_LAUNCH_CHECK();
+  const bool use_proj = proj_for(d, G, g);
+  if (use_proj && !proj_launched) {  // (the sharded path: beside the main pass)
+    if (int rc = launch_proj(zh, z32, d, ws, sw)) return rc;
   }
   const float acc_err = (float)(std::ldexp((double)d.T, -24) + std::ldexp(std::sqrt((double)d.T), -23));
   // screening counts: certain above tau + eps, decided in the tile by the pair's own bound or
@@ -2403,14 +2421,18 @@ int run_single(const uint16_t* zh, const float* z32, const Dims& d, char* cand, 
   // every launch below goes to st's device (the side stream is that device's)
   krca::DeviceGuard dg(st);
   if (int rc = dg.status()) return rc;
-  if (int rc = stage_sample<KC>(zh, d, 0, d.P, ws, phi, st)) return rc;
   // the exact-count re-scores (memory-bound, write count only) and the merge chain (sort, float64
   // top-k re-scoring, rectangle and deep passes: candidate buffers and outputs only) are
   // independent: the re-scores run on a side stream forked from st per main-pass batch (the last
-  // one beside the merge chain) and joined back into st when sw goes out of scope
+  // one beside the merge chain) and joined back into st when sw goes out of scope.  The
+  // projection bound's rows go first on the side stream, beside the threshold sample.
   SideWork sw(st, dbg ? st : krca::side_stream(st));
   if (int rc = sw.init()) return rc;
-  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, sw)) return rc;
+  const bool proj = dbg == 0 && proj_for(d, 1, 0);
+  if (proj)
+    if (int rc = launch_proj(zh, z32, d, ws, sw)) return rc;
+  if (int rc = stage_sample<KC>(zh, d, 0, d.P, ws, phi, st)) return rc;
+  if (int rc = stage_tiles<KC>(zh, z32, d, 1, 0, phi, ws, count, dbg, sw, proj)) return rc;
   return stage_merge<KC>(zh, z32, d, 0, d.P, phi, ws.buf, ws.cnt, ws, out_idx, out_val, cert, dbg, st);
 }
 

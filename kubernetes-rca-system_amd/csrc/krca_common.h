@@ -117,8 +117,8 @@ struct Tuning {
   int corr_km_extra;  // KRCA_CORR_KM_EXTRA: candidates the merge re-scores in float64 past the k-th (1..8, default 6)
   int corr_rsg_grid;  // KRCA_CORR_RSG_GRID: workgroups of the grouped re-score (0 = 2048)
   int corr_proj;      // KRCA_CORR_PROJ: the grouped re-score tries the projection bound (DCT basis) before the
-                      // partner's int16 row: 1 when the main pass runs in several batches, 2 always, 0 never
-                      // (identical counts)
+                      // partner's int16 row: 2 always (default), 1 when the main pass runs in several batches,
+                      // 0 never (identical counts)
   int corr_persist;   // KRCA_CORR_PERSIST: the main pass as persistent workgroups that load the next tile's first
                       // K stage under the current one (1) or one workgroup per tile (0, default: R7a, the
                       // persistent form ran 2-5 % slower); same bits

@@ -201,15 +201,15 @@ def test_corr_batches_and_full_lists_identical(eng):
     # performance knobs that must not change a result: the grouped re-score's grid, and how many
     # candidates past the k-th the merge re-scores (fewer: more pods take the deep merge; the
     # certificate margins may differ, the sets, values and counts not)
-    # (KRCA_CORR_PROJ = 0 / 2: the grouped re-score never / always with the projection bound -- the
-    # default uses it only when the main pass runs in several batches; counts must not move)
+    # (KRCA_CORR_PROJ = 0 / 1: the grouped re-score never with the projection bound / only when the
+    # main pass runs in several batches -- the default uses it always; counts must not move)
     try:
         # (KRCA_CORR_PERSIST = 1: persistent main-pass workgroups instead of one per tile)
         for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2), (b"KRCA_CORR_PROJ", 0),
-                          (b"KRCA_CORR_PROJ", 2), (b"KRCA_CORR_PERSIST", 1)):
+                          (b"KRCA_CORR_PROJ", 1), (b"KRCA_CORR_PERSIST", 1)):
             assert lib.krca_tune_set(knob, val) == 0
             got = eng.corr_topk(x, k=k, tau=TAU)
-            lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 1,
+            lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 2,
                                      b"KRCA_CORR_PERSIST": 0}[knob])
             for key in ("idx", "val", "count"):
                 assert np.array_equal(got[key], ref[key]), (knob, key)
@@ -217,7 +217,7 @@ def test_corr_batches_and_full_lists_identical(eng):
     finally:
         lib.krca_tune_set(b"KRCA_CORR_RSG_GRID", 0)
         lib.krca_tune_set(b"KRCA_CORR_KM_EXTRA", 6)
-        lib.krca_tune_set(b"KRCA_CORR_PROJ", 1)
+        lib.krca_tune_set(b"KRCA_CORR_PROJ", 2)
         lib.krca_tune_set(b"KRCA_CORR_PERSIST", 0)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
