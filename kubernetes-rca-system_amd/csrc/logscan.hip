@@ -680,10 +680,13 @@ __global__ void log_last_end(const uint8_t* __restrict__ text, int64_t nbytes, c
 
 // per-phase cycle counters of the tile kernels (a -DLOG_TIMING build, tools/log_timing.py)
 #ifdef LOG_TIMING
-__device__ unsigned long long g_log_timing[1024 * 8];  // per workgroup: phase cycles (log_index_match: ticket, A, scan, look-back, list, walk, write; log_index_lines: ticket + container starts, loads + flags, scan, look-back, writes), tiles
-#define LT_INIT() uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t lt_p = clock64()
+// per workgroup: phase cycles (log_index_match: ticket, A, scan, look-back, list, walk, write, [7] tiles, then
+// A's parts: loads issued, container starts, pieces; log_index_lines: ticket + container starts, loads + flags,
+// scan, look-back, writes), 16 slots
+__device__ unsigned long long g_log_timing[1024 * 16];
+#define LT_INIT() uint64_t lt_acc[16] = {}; uint64_t lt_p = clock64()
 #define LT(i) do { const uint64_t tn = clock64(); lt_acc[i] += tn - lt_p; lt_p = tn; } while (0)
-#define LT_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 1024) for (int i_ = 0; i_ < 8; ++i_) g_log_timing[blockIdx.x * 8 + i_] += lt_acc[i_]; } while (0)
+#define LT_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 1024) for (int i_ = 0; i_ < 16; ++i_) g_log_timing[blockIdx.x * 16 + i_] += lt_acc[i_]; } while (0)
 #else
 #define LT_INIT() do {} while (0)
 #define LT(i) do {} while (0)
@@ -1616,8 +1619,8 @@ __device__ __forceinline__ uint32_t cp_symoff(const TAB& d, const uint32_t* rng,
 }
 
 // The DFA mask of the line at tile offsets [s, e) from s_text (e <= FTILE + LOOK; the array is
-// padded so a block may read up to 16 bytes past e): lockstep 16-byte blocks from the line's
-// 4-byte-aligned start as in log_dfa, the next block's words read before this block's 16 dependent
+// padded so a block may read up to 20 bytes past e): lockstep 16-byte blocks from the line's first
+// byte (funnel-shifted words), the next block's words read before this block's 16 dependent
 // steps, each byte stepping on its symbol offset: an ASCII byte's stored offset; NOP (the identity
 // column) for a byte outside the line and for a UTF-8 continuation byte; for a lead byte, the
 // symbol of the code point it starts (decoded from the raw bytes after it, as the reference reads
@@ -1626,27 +1629,32 @@ __device__ __forceinline__ uint32_t cp_symoff(const TAB& d, const uint32_t* rng,
 template <class TAB>
 __device__ __forceinline__ uint32_t dfa_walk_sym(const uint32_t* __restrict__ tx, const TAB& d, const uint32_t* rng,
                                                  int s, int e) {
+  // Blocks start at s itself (round 7; until then at s & ~3, with the bytes before s masked in every
+  // block): each block's words are funnel-shifted out of five LDS words (one alignbyte per word, the
+  // shift s & 3 fixed for the walk), so only the line's END is masked, one compare per word (~20 of
+  // ~87 vector instructions per block fewer).
   uint32_t row = 0, acc = 0;
-  int off = s & ~3;  // this block's first byte (4-byte aligned)
-  int rs_ = s & 3;   // s - off: 0..3 at the first block, then negative
-  int re_ = e - off;
+  int p = s;       // this block's first byte
+  int re_ = e - s;  // e - p
+  const uint32_t sh = (uint32_t)(s & 3);
+  int q = s >> 2;  // the word holding byte p
   constexpr uint32_t nop = NOP_SYM * sizeof(d.trans[0]);
-  uint32_t w[4];
+  uint32_t x[5];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + j];
+  for (int j = 0; j < 5; ++j) x[j] = tx[q + j];
   for (;;) {
-    const int lo = max(rs_, 0), hi = min(re_, 16);
-    const uint32_t lo4 = (uint32_t)lo * 0x01010101u, hi4x = line_hi4x(hi);
+    const uint32_t hi4x = line_hi4x(min(re_, 16));
     uint32_t so[4], hib = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t in = word_in_line(j, lo4, hi4x);  // 0x80 in each byte of the line
-      hib |= w[j] & in;
+      const uint32_t w = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);  // bytes p + 4j .. p + 4j + 3
+      const uint32_t in = (hi4x - (0x03020100u + 0x04040404u * (uint32_t)j)) & 0x80808080u;  // byte < hi
       const uint32_t fm = (in >> 7) * 0xFFu;
-      so[j] = (w[j] & fm) | (nop * 0x01010101u & ~fm);
+      so[j] = (w & fm) | (nop * 0x01010101u & ~fm);
+      hib |= so[j];
     }
     const bool more = re_ > 16;
-    if (hib) {  // bytes >= 0x80 in the line (rare): continuation bytes -> NOP, lead bytes -> their code point
+    if (hib & 0x80808080u) {  // bytes >= 0x80 in the line (rare): continuation bytes -> NOP, lead bytes -> their code point
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const uint32_t b = (so[k >> 2] >> (8 * (k & 3))) & 0xFFu;
@@ -1654,8 +1662,8 @@ __device__ __forceinline__ uint32_t dfa_walk_sym(const uint32_t* __restrict__ tx
           uint32_t sy = nop;
           if (b >= 0xC0) {
             const uint32_t cp = utf8_cp(b, [&](int r) -> uint32_t {
-              const int p = off + k + r;
-              return (tx[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+              const int pp = p + k + r;
+              return (tx[pp >> 2] >> (8 * (pp & 3))) & 0xFFu;
             });
             sy = cp_symoff(d, rng, cp);
           }
@@ -1664,8 +1672,9 @@ __device__ __forceinline__ uint32_t dfa_walk_sym(const uint32_t* __restrict__ tx
       }
     }
     if (more) {
+      x[0] = x[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = tx[(off >> 2) + 4 + j];
+      for (int j = 1; j < 5; ++j) x[j] = tx[q + 4 + j];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1675,8 +1684,8 @@ __device__ __forceinline__ uint32_t dfa_walk_sym(const uint32_t* __restrict__ tx
       row = dstep_b3(d, row, so[j], acc);
     }
     if (!more) break;
-    off += 16;
-    rs_ -= 16;
+    p += 16;
+    q += 4;
     re_ -= 16;
   }
   return dmask(d, acc);
@@ -1750,7 +1759,9 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
       rawx = *reinterpret_cast<const u32x4*>(text + (q < nbytes ? q : qlast));
       pwx = tile0 + FTILE <= nbytes ? *reinterpret_cast<const uint32_t*>(text + tile0 + FTILE - 4) : 0u;
     }
+    LT(8);
     tile_container_starts_t<FTILE + LOOK, true>(s_cs, tile0, nbytes, doc_off, D, chunk_doc);  // (its barriers order LDS reuse)
+    LT(9);
     uint32_t regS[FNIT], regL1[FNIT];  // per piece: starts | odd lengths << 16; lengths 2/3
 #pragma unroll
     for (int it = 0; it < FNIT; ++it) {
@@ -1778,6 +1789,7 @@ __global__ __launch_bounds__(CF::FTPB, 4) void log_index_match(
       for (int o = LANES_PER_CHUNK / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);  // 16 lanes = one chunk
       if ((tid & (LANES_PER_CHUNK - 1)) == 0) s_cnt[pc / LANES_PER_CHUNK] = (int32_t)c;
     }
+    LT(10);
     __syncthreads();
     LT(1);
     if (tid < FCH) {  // chunk counts -> exclusive bases inside the tile
@@ -2157,7 +2169,7 @@ int krca_log_scan(const uint8_t* text, int64_t nbytes, const int64_t* doc_off, i
 int krca_log_debug_timing(unsigned long long* host, int reset) {  // timing variant builds only
   KRCA_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_log_timing), sizeof(g_log_timing)));
   if (reset) {
-    static unsigned long long zero[1024 * 8];
+    static unsigned long long zero[1024 * 16];
     KRCA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_log_timing), zero, sizeof(zero)));
   }
   return KRCA_OK;

@@ -26,7 +26,7 @@ def main():
     tb, toff = eng.upload_blob(blob), torch.from_numpy(off).cuda()
     fn = eng.lib.krca_log_debug_timing
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = np.zeros(1024 * 8, np.uint64)
+    buf = np.zeros(1024 * 16, np.uint64)
     eng.log_scan_device(tb, toff, validate=False)
     eng.log_scan_device(tb, toff, validate=False)
     torch.cuda.synchronize()
@@ -34,15 +34,17 @@ def main():
     eng.log_scan_device(tb, toff, validate=False)
     torch.cuda.synchronize()
     fn(buf.ctypes.data_as(ctypes.c_void_p), 1)
-    t = buf.reshape(1024, 8).astype(np.float64)
+    t = buf.reshape(1024, 16).astype(np.float64)
     t = t[t[:, 7] > 0]
     fused = int(os.environ.get("KRCA_LOG_FUSED", "0")) != 0
-    names = (["ticket", "A_loads_flags", "scan_agg", "lookback", "list", "walk", "write"] if fused else
+    names = (["ticket", "A_tail_barrier", "scan_agg", "lookback", "list", "walk", "write", "-", "A_issue_loads",
+              "A_container_starts", "A_pieces"] if fused else
              ["ticket_container_starts", "loads_flags", "scan", "lookback", "writes", "-", "-"])
     tiles = t[:, 7].sum()
-    per_tile = {n: float(t[:, i].sum() / tiles) for i, n in enumerate(names)}
+    per_tile = {n: float(t[:, i].sum() / tiles) for i, n in enumerate(names) if n != "-"}
     out = dict(kernel="log_index_match" if fused else "log_index_lines", bytes=len(blob), workgroups=int(len(t)), tiles=int(tiles), cycles_per_tile=per_tile,
-               total_cycles_per_wg_mean=float(t[:, :7].sum(1).mean()), total_cycles_per_wg_max=float(t[:, :7].sum(1).max()))
+               total_cycles_per_wg_mean=float((t[:, :7].sum(1) + t[:, 8:].sum(1)).mean()),
+               total_cycles_per_wg_max=float((t[:, :7].sum(1) + t[:, 8:].sum(1)).max()))
     print(json.dumps(out), flush=True)
 
 
