@@ -8,6 +8,7 @@ C=kubernetes-rca-system_amd/csrc
 mkdir -p $C/build/v_$N
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -ffp-contract=off "$@" \
   -c $C/$SRC.hip -o $C/build/v_$N/$SRC.o
-OBJS=$(ls $C/build/*.o | grep -v "/$SRC.o\$")
+# the objects of the product build only (one per source file; not the ltime / gdbg / tcls variants)
+OBJS=$(for f in $C/*.hip $C/*.cpp; do b=$(basename ${f%.*}); [ $b != $SRC ] && echo $C/build/$b.o; done)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o kubernetes-rca-system_amd/lib/libkrca_$N.so $OBJS $C/build/v_$N/$SRC.o
 echo built kubernetes-rca-system_amd/lib/libkrca_$N.so
