@@ -1241,6 +1241,7 @@ __global__ __launch_bounds__(TPB) void corr_dct_basis(double* __restrict__ B, in
 // basis rows 512 B apart, a 4-way bank conflict per read, 1.08 ms.)
 constexpr int PJ_ROWS = 64, PJ_TC = 64, PJ_J = KP / 4;
 static_assert(TPB == 4 * PJ_ROWS, "four waves: one per basis group");
+template <bool VEC>
 __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, const uint16_t* __restrict__ zh,
                                                  int64_t P, int T, int Tp, const double* __restrict__ B,
                                                  float* __restrict__ proj, float* __restrict__ pqz,
@@ -1248,60 +1249,117 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
   __shared__ double sB[KP][PJ_TC];
   __shared__ float sz[PJ_ROWS][PJ_TC + 1];
   __shared__ float se[PJ_ROWS][PJ_TC + 1];
-  __shared__ double sn[4][PJ_ROWS][2];  // per basis group: |B z|^2, |B e|^2 of its vectors
+  __shared__ double sn[4][PJ_ROWS][4];  // per wave: |B z|^2, |B e|^2 of its vectors, its share of |z|^2, |e|^2
   const int tid = threadIdx.x, r = tid & 63;
   const int jg = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t p0 = (int64_t)blockIdx.x * PJ_ROWS;
   double bz[PJ_J], be[PJ_J];
 #pragma unroll
   for (int j = 0; j < PJ_J; ++j) bz[j] = be[j] = 0.0;
-  double nz = 0.0, ne = 0.0;
-  constexpr int NB = KP * PJ_TC / TPB, NZ = PJ_ROWS * PJ_TC / TPB;  // loads per lane and chunk
+  double nz = 0.0, ne = 0.0;  // this wave's steps [16 jg, 16 jg + 16) of every chunk
+  constexpr int NB = KP * PJ_TC / TPB, NZ = PJ_ROWS * PJ_TC / TPB;  // values per lane and chunk
+  // a chunk's loads all go out before any is used (a loop of dependent load -> store rounds paid one
+  // memory latency per round: 0.96 ms at C3, R6e), and the next chunk's right after this one is in
+  // LDS, so they are in flight during its sums (the registers are free by then).  VEC (T % 4 == 0):
+  // 16-byte loads, 4 floats / halves or 2 basis values each, so 10 loads per lane and chunk instead
+  // of 36 (the scalar form's addresses took the kernel to 212 VGPRs, 2 waves per SIMD)
+  constexpr int NZV = VEC ? NZ / 4 : NZ, NBV = VEC ? NB / 2 : NB;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  typedef unsigned short h4 __attribute__((ext_vector_type(4)));
+  d2 bv[NBV];
+  f4 zv[NZV];
+  h4 hv[NZV];
+  auto load = [&](const int t0) {
+    if constexpr (VEC) {
+#pragma unroll
+      for (int u = 0; u < NBV; ++u) {  // basis row j, steps t, t + 1
+        const int i = tid + u * TPB, j = i >> 5, t = 2 * (i & 31);
+        const bool in = t0 + t < T;
+        const d2 v = *reinterpret_cast<const d2*>(B + (int64_t)j * T + (in ? t0 + t : 0));
+        bv[u] = in ? v : d2{0.0, 0.0};
+      }
+#pragma unroll
+      for (int u = 0; u < NZV; ++u) {  // row rr, steps t .. t + 3 (16 lanes per row: coalesced)
+        const int i = tid + u * TPB, rr = i >> 4, t = 4 * (i & 15);
+        const int64_t p = p0 + rr;
+        const bool in = p < P && t0 + t < T;
+        const int64_t pc = in ? p : 0, tc = in ? t0 + t : 0;
+        const f4 zz = *reinterpret_cast<const f4*>(z32 + pc * T + tc);
+        const h4 hh = *reinterpret_cast<const h4*>(zh + pc * Tp + tc);
+        zv[u] = in ? zz : f4{0.f, 0.f, 0.f, 0.f};
+        hv[u] = in ? hh : h4{0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int i = tid + u * TPB, j = i / PJ_TC, t = i % PJ_TC;
+        bv[u].x = t0 + t < T ? B[(int64_t)j * T + t0 + t] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < NZ; ++u) {  // coalesced along t
+        const int i = tid + u * TPB, rr = i / PJ_TC, t = i % PJ_TC;
+        const int64_t p = p0 + rr;
+        const bool in = p < P && t0 + t < T;
+        zv[u].x = in ? z32[p * T + t0 + t] : 0.f;
+        hv[u].x = in ? zh[p * Tp + t0 + t] : (uint16_t)0;
+      }
+    }
+  };
+  auto err = [](float z, unsigned short h) {  // z - fp16(z), exact in float
+    return (float)((double)z - (double)(float)__builtin_bit_cast(_Float16, h));
+  };
+  load(0);
   for (int t0 = 0; t0 < T; t0 += PJ_TC) {
-    // every load of the chunk issued before any is used (a loop of dependent load -> store rounds
-    // paid one memory latency per round: 0.96 ms at C3, R6e)
-    double bv[NB];
-    float zv[NZ];
-    uint16_t hv[NZ];
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int i = tid + u * TPB, j = i / PJ_TC, t = i % PJ_TC;
-      bv[u] = t0 + t < T ? B[(int64_t)j * T + t0 + t] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < NZ; ++u) {  // coalesced along t
-      const int i = tid + u * TPB, rr = i / PJ_TC, t = i % PJ_TC;
-      const int64_t p = p0 + rr;
-      const bool in = p < P && t0 + t < T;
-      zv[u] = in ? z32[p * T + t0 + t] : 0.f;
-      hv[u] = in ? zh[p * Tp + t0 + t] : (uint16_t)0;
-    }
     __syncthreads();  // the previous chunk's reads are done
+    if constexpr (VEC) {
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int i = tid + u * TPB;
-      sB[i / PJ_TC][i % PJ_TC] = bv[u];
-    }
+      for (int u = 0; u < NBV; ++u) {
+        const int i = tid + u * TPB, j = i >> 5, t = 2 * (i & 31);
+        sB[j][t] = bv[u].x;
+        sB[j][t + 1] = bv[u].y;
+      }
 #pragma unroll
-    for (int u = 0; u < NZ; ++u) {
-      const int i = tid + u * TPB, rr = i / PJ_TC, t = i % PJ_TC;
-      sz[rr][t] = zv[u];
-      se[rr][t] = (float)((double)zv[u] - (double)(float)__builtin_bit_cast(_Float16, hv[u]));  // exact
+      for (int u = 0; u < NZV; ++u) {
+        const int i = tid + u * TPB, rr = i >> 4, t = 4 * (i & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sz[rr][t + q] = zv[u][q];
+          se[rr][t + q] = err(zv[u][q], hv[u][q]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int i = tid + u * TPB;
+        sB[i / PJ_TC][i % PJ_TC] = bv[u].x;
+      }
+#pragma unroll
+      for (int u = 0; u < NZ; ++u) {
+        const int i = tid + u * TPB, rr = i / PJ_TC, t = i % PJ_TC;
+        sz[rr][t] = zv[u].x;
+        se[rr][t] = err(zv[u].x, hv[u].x);
+      }
     }
     __syncthreads();
+    if (t0 + PJ_TC < T) load(t0 + PJ_TC);
 #pragma unroll 4
     for (int t = 0; t < PJ_TC; ++t) {
       const double z = (double)sz[r][t], e = (double)se[r][t];
       // explicit fused multiply-adds (the library builds with -ffp-contract=off: a * b + c is a
       // multiply and an add there, twice the instructions on this float64 loop)
-      nz = fma(z, z, nz);
-      ne = fma(e, e, ne);
 #pragma unroll
       for (int j = 0; j < PJ_J; ++j) {
         const double b = sB[jg * PJ_J + j][t];  // wave-uniform: a broadcast
         bz[j] = fma(z, b, bz[j]);
         be[j] = fma(e, b, be[j]);
       }
+    }
+#pragma unroll 4
+    for (int t = 16 * jg; t < 16 * jg + 16; ++t) {  // the norms: a quarter of the steps per wave
+      const double z = (double)sz[r][t], e = (double)se[r][t];
+      nz = fma(z, z, nz);
+      ne = fma(e, e, ne);
     }
   }
   double nbz = 0.0, nbe = 0.0;
@@ -1312,6 +1370,8 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
   }
   sn[jg][r][0] = nbz;
   sn[jg][r][1] = nbe;
+  sn[jg][r][2] = nz;
+  sn[jg][r][3] = ne;
   const int64_t p = p0 + r;
   if (p < P) {
     float* out = proj + p * (2 * KP);
@@ -1325,6 +1385,8 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
   if (jg == 0 && p < P) {  // |Q x| = sqrt(|x|^2 - |B x|^2), rounded up (+ the float64 sums' and B's rounding)
     const double bz2 = sn[0][r][0] + sn[1][r][0] + sn[2][r][0] + sn[3][r][0];
     const double be2 = sn[0][r][1] + sn[1][r][1] + sn[2][r][1] + sn[3][r][1];
+    const double nz = sn[0][r][2] + sn[1][r][2] + sn[2][r][2] + sn[3][r][2];
+    const double ne = sn[0][r][3] + sn[1][r][3] + sn[2][r][3] + sn[3][r][3];
     pqz[p] = (float)(sqrt(fmax(nz - bz2, 0.0) + 1e-12) * (1.0 + 1e-6));
     pqe[p] = (float)(sqrt(fmax(ne - be2, 0.0) + 1e-24) * (1.0 + 1e-6));
   }
@@ -1791,6 +1853,7 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
   __shared__ double ex[CAPC];
   __shared__ int32_t ci[CAPC];
   __shared__ int srest;  // pass 0: the largest screening |r| left out (float bits, >= 0), INT_MIN = none
+  __shared__ int ssel;   // pass 0: candidates taken (packed at the front of ci)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nd = pods[0];  // list length first (device-held: no host round trip)
   for (int b = blockIdx.x; b < nd; b += gridDim.x) {
@@ -1803,36 +1866,45 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
   const float thr = fabsf(out_v[gl * k + k - 1]) - 2.f * eps - 1e-6f;
   for (int pass = 0; pass < 2; ++pass) {
   __syncthreads();  // ex / ci / srest of the previous pod or pass
-  if (tid == 0) srest = INT_MIN;
+  if (tid == 0) {
+    srest = INT_MIN;
+    ssel = 0;
+  }
   __syncthreads();
-  for (int i = tid; i < np; i += TPB) {
-    int32_t c = -1;
-    if (i < n) {
+  int ns = np;  // slots re-scored and sorted
+  if (pass == 0) {
+    // the near-ties only, packed at the front (their order is free: the sort below is total), so
+    // the re-score and the sort run over a power of two >= their count, not over the whole buffer
+    for (int i = tid; i < n; i += TPB) {
       const int2 e = buf[gl * CAPC + i];
       const float a = fabsf(__int_as_float(e.x));
-      if (pass == 1 || a >= thr) {
-        c = e.y;
-      } else {
-        atomicMax(&srest, __float_as_int(a));
-      }
+      if (a >= thr) ci[atomicAdd(&ssel, 1)] = e.y;
+      else atomicMax(&srest, __float_as_int(a));
     }
-    ci[i] = c;
+    __syncthreads();
+    const int m = ssel;
+    ns = 32;
+    while (ns < m) ns <<= 1;
+    for (int i = m + tid; i < ns; i += TPB) ci[i] = -1;
+  } else {
+    for (int i = tid; i < np; i += TPB) ci[i] = i < n ? buf[gl * CAPC + i].y : -1;
   }
   __syncthreads();
   const float* zg = z32 + g * T;
   // wave w re-scores candidates 4w .. 4w + 3, then 4w + 16 .., together (independent loads in flight;
   // float4 loads when the rows are 16-B aligned)
   constexpr int PD = 4;
-  for (int c0 = PD * w; c0 < np; c0 += PD * (TPB / 64)) {
+  for (int c0 = PD * w; c0 < ns; c0 += PD * (TPB / 64)) {
     const float* zj[PD];
     double acc[PD];
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
-      const int32_t j = c0 + u < np ? ci[c0 + u] : -1;
+      const int32_t j = c0 + u < ns ? ci[c0 + u] : -1;
       zj[u] = j >= 0 ? z32 + (int64_t)j * T : nullptr;
       acc[u] = 0.0;
     }
-    if ((T & 3) == 0) {
+    if (!zj[0]) {  // (slots past the taken candidates: every one of the group is empty)
+    } else if ((T & 3) == 0) {
       const float4* g4 = reinterpret_cast<const float4*>(zg);
       for (int t = lane; t < T / 4; t += 64) {
         const float4 a = g4[t];
@@ -1856,13 +1928,13 @@ __global__ __launch_bounds__(TPB) void corr_merge_deep(const int2* __restrict__ 
     for (int u = 0; u < PD; ++u) {
       double v = acc[u];
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0 && c0 + u < np) ex[c0 + u] = zj[u] ? v : 0.0;
+      if (lane == 0 && c0 + u < ns) ex[c0 + u] = zj[u] ? v : 0.0;
     }
   }
   __syncthreads();
-  for (int kk = 2; kk <= np; kk <<= 1) {  // bitonic: |r| desc, index asc, empties last
+  for (int kk = 2; kk <= ns; kk <<= 1) {  // bitonic: |r| desc, index asc, empties last
     for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < np; i += TPB) {
+      for (int i = tid; i < ns; i += TPB) {
         const int l = i ^ j;
         if (l > i) {
           const bool desc = (i & kk) == 0;
@@ -2240,11 +2312,19 @@ int launch_proj(const uint16_t* zh, const float* z32, const Dims& d, const CorrW
   hipLaunchKernelGGL(corr_dct_basis, dim3((unsigned)krca::ceil_div((int64_t)KP * d.T, TPB)), dim3(TPB), 0, ps, ws.dct,
                      d.T);
   KRCA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(corr_proj, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)), dim3(TPB), 0, ps, z32, zh, d.P, d.T,
+  hipLaunchKernelGGL(d.T % 4 == 0 ? corr_proj<true> : corr_proj<false>, dim3((unsigned)krca::ceil_div(d.P, PJ_ROWS)),
+                     dim3(TPB), 0, ps, z32, zh, d.P, d.T,
                      d.Tp, (const double*)ws.dct, ws.proj, ws.pqz, ws.pqe);
   KRCA_LAUNCH_CHECK();
   return KRCA_OK;
 }
+
+// the rows' rounding-error norms and int16 copies (corr_dnorm): the main pass and the re-score read them
+void launch_dnorm(const uint16_t* zh, const float* z32, const Dims& d, const CorrWs& ws, hipStream_t s) {
+  hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, s, z32, zh, d.P, d.T,
+                     d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
+}
+
 
 // whether rank g of G re-scores with the projection bound (its share of the super-tiles in batches)
 inline bool proj_for(const Dims& d, int G, int g) {
@@ -2274,8 +2354,7 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   const int64_t n_mine = n_st > g ? (n_st - g + G - 1) / G : 0;
   if (n_mine == 0) return KRCA_OK;
   const Shard sh{0, G, g, 0};
-  hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, st, z32, zh, d.P, d.T,
-                     d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
+  launch_dnorm(zh, z32, d, ws, st);
   KRCA_LAUNCH_CHECK();
   const bool use_proj = proj_for(d, G, g);
   if (use_proj && !proj_launched) {  // (the sharded path: beside the main pass)

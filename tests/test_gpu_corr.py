@@ -203,22 +203,14 @@ def test_corr_batches_and_full_lists_identical(eng):
     # certificate margins may differ, the sets, values and counts not)
     # (KRCA_CORR_PROJ = 0 / 1: the grouped re-score never with the projection bound / only when the
     # main pass runs in several batches -- the default uses it always; counts must not move)
-    try:
-        # (KRCA_CORR_PERSIST = 1: persistent main-pass workgroups instead of one per tile)
-        for knob, val in ((b"KRCA_CORR_RSG_GRID", 256), (b"KRCA_CORR_KM_EXTRA", 2), (b"KRCA_CORR_PROJ", 0),
-                          (b"KRCA_CORR_PROJ", 1), (b"KRCA_CORR_PERSIST", 1)):
-            assert lib.krca_tune_set(knob, val) == 0
+    # (KRCA_CORR_PERSIST = 1: persistent main-pass workgroups instead of one per tile)
+    for knob, val in (("KRCA_CORR_RSG_GRID", 256), ("KRCA_CORR_KM_EXTRA", 2), ("KRCA_CORR_PROJ", 0),
+                      ("KRCA_CORR_PROJ", 1), ("KRCA_CORR_PERSIST", 1)):
+        with native.tune(lib, **{knob: val}):
             got = eng.corr_topk(x, k=k, tau=TAU)
-            lib.krca_tune_set(knob, {b"KRCA_CORR_RSG_GRID": 0, b"KRCA_CORR_KM_EXTRA": 6, b"KRCA_CORR_PROJ": 2,
-                                     b"KRCA_CORR_PERSIST": 0}[knob])
-            for key in ("idx", "val", "count"):
-                assert np.array_equal(got[key], ref[key]), (knob, key)
-            assert (got["cert"] > 0).all(), knob
-    finally:
-        lib.krca_tune_set(b"KRCA_CORR_RSG_GRID", 0)
-        lib.krca_tune_set(b"KRCA_CORR_KM_EXTRA", 6)
-        lib.krca_tune_set(b"KRCA_CORR_PROJ", 2)
-        lib.krca_tune_set(b"KRCA_CORR_PERSIST", 0)
+        for key in ("idx", "val", "count"):
+            assert np.array_equal(got[key], ref[key]), (knob, val, key)
+        assert (got["cert"] > 0).all(), (knob, val)
     z = torch.from_numpy(twin_z(x)).cuda().double()
     rows = np.random.default_rng(0).choice(P, 2048, replace=False)
     _, _, bad = device_check(ref, z, [rows], k)
