@@ -164,7 +164,8 @@ int krca_template_hist_huge(const uint64_t* hash, int64_t n_lines, void* workspa
  * r(p,q) = Pearson over the T samples of metric channel `channel` of x[T][P][M] (population
  * std; a flat series correlates 0 with everything).  Per pod p: the k partners with the largest
  * |r| (self excluded, ties -> lower index) with r re-scored exactly (float64 over fp32 z), the
- * exact count of partners with |r| > tau (the fp16 MFMA screening product decides every pair
+ * exact count of partners with |r| > tau (tau is float64, the type r is compared in: a float tau
+ * of 0.6 would be 0.60000002 and miss pairs just above 0.6; the fp16 MFMA screening product decides every pair
  * farther than krca_corr_eps(T) from tau; the pairs within it are re-scored in float64: fails with
  * KRCA_EINVAL if more than 256*P + 2^20 pairs fall there, i.e. tau sits in the bulk of |r|), and
  * cert[p] > 0 iff the reported set is provably the exact top-k (pods whose first merge cannot
@@ -188,7 +189,7 @@ int32_t krca_corr_cand_cap(void);
 float krca_corr_eps(int32_t T);
 int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t channel, float* mean, float* scale,
                       float* z32, uint16_t* zh, void* stream);
-int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, void* cand,
+int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, double tau, void* cand,
                    int32_t* count, int32_t* out_idx, float* out_val, float* cert, void* stream);
 /* a9 pod-sharded (kubernetes-rca-system_amd/krca/corr_dist.py): rank g of G owns pods
  * [lo, lo + n_loc), lo a multiple of 256; zh / z32 / phi are the all-gathered full arrays.  The
@@ -198,7 +199,7 @@ int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, i
 int64_t krca_corr_shard_ws_size(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G);
 int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, int64_t lo, int64_t n_loc,
                            int32_t G, void* ws, float* phi, void* stream);
-int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, int32_t G,
+int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, double tau, int32_t G,
                           int32_t g, const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt,
                           void* stream);
 int krca_corr_shard_pack_sizes(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t n_max, void* ws,
@@ -207,7 +208,7 @@ int krca_corr_shard_pack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t
                          void* send, void* stream);
 int krca_corr_shard_unpack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32_t G, int64_t lo, void* ws,
                            const void* recv, int64_t n_recv, void* stream);
-int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau,
+int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, double tau,
                           int64_t lo, int64_t n_loc, int32_t G, const float* phi, int32_t* lcnt, void* ws,
                           int32_t* out_idx, float* out_val, float* cert, void* stream);
 

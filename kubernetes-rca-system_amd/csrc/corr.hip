@@ -346,7 +346,7 @@ struct TileArgs {
   int nsb;
   float tau_hi;   // MAIN: tau + eps, every screening |r| above it is a hit
   float tau_lo;   // MAIN: tau - eps, none at or below it is
-  float tau;      // MAIN: the caller's tau (the per-pair band in between)
+  double tau;     // MAIN: the caller's tau, float64 as the exact r it is compared with (the per-pair band in between)
   float acc_err;  // MAIN: the fp32 accumulation terms of eps
   const float* phi;  // MAIN: candidate bound per pod; RECT: phi2
   float* samp_v;
@@ -1398,7 +1398,7 @@ __global__ __launch_bounds__(TPB) void corr_proj(const float* __restrict__ z32, 
 __global__ __launch_bounds__(TPB) void corr_amb_rescore(const int2* __restrict__ amb, const float* __restrict__ ambv,
                                                         const unsigned long long* __restrict__ amb_n, int64_t cap,
                                                         const float* __restrict__ z32, const float* __restrict__ dn,
-                                                        int T, float tau, float acc_err, int32_t* __restrict__ count) {
+                                                        int T, double tau, float acc_err, int32_t* __restrict__ count) {
   const int sub = threadIdx.x & 15;
   const int64_t n = (int64_t)min(*amb_n, (unsigned long long)cap);  // entries past cap were decided in their tiles
   // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs; XCD x takes the contiguous
@@ -1530,7 +1530,7 @@ constexpr int RS_WAVES = TPB / 64;
 constexpr int RS_QCAP = 64;  // pairs queued per wave for the row path
 __global__ __launch_bounds__(TPB) void corr_amb_rescore_grouped(const int32_t* __restrict__ goff, const int2* __restrict__ gs,
                                                                 int64_t P, const float* __restrict__ z32,
-                                                                const float* __restrict__ dn, int T, float tau,
+                                                                const float* __restrict__ dn, int T, double tau,
                                                                 float acc_err, int32_t* __restrict__ count,
                                                                 const int16_t* __restrict__ zq, int Tq,
                                                                 const float* __restrict__ qs, const float* __restrict__ qn,
@@ -2145,10 +2145,11 @@ inline int cu_count() {
 struct Dims {
   int64_t P;
   int T, Tp, nb2, nsb, k;
-  float tau, eps;
+  double tau;  // float64: the exact r of a pair is compared with it (a float tau = 0.6 is 0.60000002)
+  float eps;
 };
 
-Dims dims_of(int64_t P, int T, int k, float tau) {
+Dims dims_of(int64_t P, int T, int k, double tau) {
   Dims d;
   d.P = P;
   d.T = T;
@@ -2370,8 +2371,8 @@ int stage_tiles(const uint16_t* zh, const float* z32, const Dims& d, int G, int 
   ta.Tp = d.Tp;
   ta.nb2 = d.nb2;
   ta.nsb = d.nsb;
-  ta.tau_hi = d.tau + d.eps;
-  ta.tau_lo = d.tau - d.eps;
+  ta.tau_hi = (float)(d.tau + d.eps);  // (eps carries 1e-6 of slack over the float roundings)
+  ta.tau_lo = (float)(d.tau - d.eps);
   ta.tau = d.tau;
   ta.acc_err = acc_err;
   ta.phi = phi;
@@ -2549,11 +2550,11 @@ int krca_corr_prepare(const float* x, int64_t P, int32_t M, int32_t T, int32_t c
   return KRCA_OK;
 }
 
-int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, void* cand,
+int krca_corr_topk(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, double tau, void* cand,
                    int32_t* count, int32_t* out_idx, float* out_val, float* cert, void* stream) {
   KRCA_CHECK_ARG(P > 1 && P <= (int64_t(1) << 22) && T > 0, "krca_corr_topk: P must be in [2, 2^22]");
   KRCA_CHECK_ARG(k >= 1 && k <= KMAX && k < P, "krca_corr_topk: k must be in [1, %d] and < P", KMAX);
-  KRCA_CHECK_ARG(tau >= 0.f, "krca_corr_topk: tau must be >= 0");
+  KRCA_CHECK_ARG(tau >= 0.0, "krca_corr_topk: tau must be >= 0");
   KRCA_CHECK_ARG(zh && z32 && cand && count && out_idx && out_val && cert, "krca_corr_topk: null pointer");
   const Dims d = dims_of(P, T, k, tau);
   hipStream_t st = krca::as_stream(stream);
@@ -2595,11 +2596,11 @@ int krca_corr_shard_sample(const uint16_t* zh, int64_t P, int32_t T, int32_t k, 
   }
 }
 
-int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau, int32_t G,
+int krca_corr_shard_tiles(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, double tau, int32_t G,
                           int32_t g, const float* phi, int64_t n_loc, void* ws, int32_t* count, int32_t* raw_cnt,
                           void* stream) {
   KRCA_CORR_SHARD_ARGS("krca_corr_shard_tiles")
-  KRCA_CHECK_ARG(zh && z32 && phi && count && raw_cnt && g >= 0 && g < G && tau >= 0.f,
+  KRCA_CHECK_ARG(zh && z32 && phi && count && raw_cnt && g >= 0 && g < G && tau >= 0.0,
                  "krca_corr_shard_tiles: bad args");
   const Dims d = dims_of(P, T, k, tau);
   int rc;
@@ -2663,7 +2664,7 @@ int krca_corr_shard_unpack(int64_t P, int32_t T, int32_t k, int64_t n_loc, int32
 }
 
 // own pods: lcnt = this rank's slice of the all-reduced raw counts ([n_loc], may be reset here)
-int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, float tau,
+int krca_corr_shard_merge(const uint16_t* zh, const float* z32, int64_t P, int32_t T, int32_t k, double tau,
                           int64_t lo, int64_t n_loc, int32_t G, const float* phi, int32_t* lcnt, void* ws,
                           int32_t* out_idx, float* out_val, float* cert, void* stream) {
   KRCA_CORR_SHARD_ARGS("krca_corr_shard_merge")

@@ -52,16 +52,16 @@ SIGNATURES = {
     "krca_corr_cand_cap": (c_i32, []),
     "krca_corr_eps": (c_f32, [c_i32]),
     "krca_corr_prepare": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "krca_corr_topk": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "krca_corr_topk": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "krca_corr_shard_ws_size": (c_i64, [c_i64, c_i32, c_i32, c_i64, c_i32]),
     "krca_corr_shard_sample": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
-    "krca_corr_shard_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
+    "krca_corr_shard_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f64, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
                                       c_vp]),
     "krca_corr_shard_pack_sizes": (c_i32, [c_i64, c_i32, c_i32, c_i64, c_i32, c_i64, c_vp, ctypes.POINTER(c_i64),
                                            c_vp]),
     "krca_corr_shard_pack": (c_i32, [c_i64, c_i32, c_i32, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp]),
     "krca_corr_shard_unpack": (c_i32, [c_i64, c_i32, c_i32, c_i64, c_i32, c_i64, c_vp, c_vp, c_i64, c_vp]),
-    "krca_corr_shard_merge": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp,
+    "krca_corr_shard_merge": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_f64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp]),
     "krca_ppr_plan_size": (c_i64, [c_vp, c_i64]),
     "krca_ppr_plan": (c_i32, [c_vp, c_i64, c_vp, c_i64]),

@@ -149,6 +149,22 @@ def test_corr_c3_every_row(eng):
     assert banded <= 1000
 
 
+@pytest.mark.parametrize("T,k,tau", [(1001, 10, 0.5), (1437, 16, 0.6)])
+def test_corr_odd_steps_every_row(eng, T, k, tau):
+    """T not a multiple of 4 (the projection kernel's scalar-load form, corr_proj<false>) and of 64 (a
+    partial last chunk), at 30k pods: every row against the float64 reference on the device, so the
+    projection bound, the packed deep merge and the certificates are exercised away from T = 1440."""
+    P = 30_000
+    x = synth.make_metrics(P, 1, T, seed=T, group_size=20, device="cuda")
+    res = eng.corr_topk(x, k=k, tau=tau)
+    z32 = twin_z(x)
+    del x
+    assert (res["cert"] > 0).all(), np.nonzero(res["cert"] <= 0)[0][:10]
+    z = torch.from_numpy(z32).cuda().double()
+    _, _, bad = device_check(res, z, (np.arange(r0, min(P, r0 + 2048)) for r0 in range(0, P, 2048)), k, tau)
+    assert bad == (0, 0, 0), bad
+
+
 def test_corr_odd_sample_self_products(eng):
     """An odd threshold sample (P = 120k, k = 10: 19 blocks of 128 pods) leaves the second half of
     its last 256-block unscanned, and that block is nobody's own block either: the self products
