@@ -8,9 +8,7 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "kubernetes-rca-system_amd"), os.path.join(ROOT, "oracle"), ROOT):
-    sys.path.insert(0, p)
-import oracle  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-rca-system_amd"))
 from krca import native, synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -22,8 +20,8 @@ a = ap.parse_args()
 eng = native.NativeEngine()
 lib = eng.lib
 x = synth.make_metrics(a.pods, 1, a.T, seed=a.T, group_size=20, device="cuda")
-z32 = oracle.c_corr_z32(x.cpu().numpy(), 0)[0]
-z = torch.from_numpy(z32).cuda().double()
+# the device's standardised rows (bit-identical to the C twin's: test_corr_prepare_matches_twin)
+z = eng.corr_prepare_device(x)["z32"].double()
 BAND = 1e-12
 
 
