@@ -165,6 +165,22 @@ def test_corr_odd_steps_every_row(eng, T, k, tau):
     assert bad == (0, 0, 0), bad
 
 
+@pytest.mark.parametrize("tau,k", [(0.3, 1), (0.7, 8), (0.9, 12), (0.123456789, 5), (0.95, 16)])
+def test_corr_tau_not_float32_every_row(eng, tau, k):
+    """tau values a float32 cannot hold (0.3, 0.7, 0.9, ...) and the smallest / largest k: every row of
+    a 20k-pod run against the float64 reference on the device (the counts compare the float64 r with
+    the float64 tau; a float tau missed pairs just above it, R8c)."""
+    P, T = 20_000, 500
+    x = synth.make_metrics(P, 1, T, seed=int(tau * 1000) + k, group_size=20, device="cuda")
+    res = eng.corr_topk(x, k=k, tau=tau)
+    z32 = twin_z(x)
+    del x
+    assert (res["cert"] > 0).all(), np.nonzero(res["cert"] <= 0)[0][:10]
+    z = torch.from_numpy(z32).cuda().double()
+    _, _, bad = device_check(res, z, (np.arange(r0, min(P, r0 + 2048)) for r0 in range(0, P, 2048)), k, tau)
+    assert bad == (0, 0, 0), bad
+
+
 def test_corr_odd_sample_self_products(eng):
     """An odd threshold sample (P = 120k, k = 10: 19 blocks of 128 pods) leaves the second half of
     its last 256-block unscanned, and that block is nobody's own block either: the self products
