@@ -1167,6 +1167,11 @@ __global__ __launch_bounds__(TPB) void corr_theta(const float* __restrict__ sv, 
 // qs[p] = max|z32[p]| / 32767, zq[p][t] = rint(z32[p][t] / qs[p]) (zero past T up to Tq, a multiple
 // of 8), qn[p] = || z32[p] - qs[p] zq[p] || and nrm[p] = || z32[p] || (float64, rounded up).  A
 // pair's za . (qs_b zq_b) then differs from za . zb by at most nrm_a qn_b (~4e-5 at T = 1440).
+// VEC (T % 4 == 0): 16-byte loads of z32 and 8-byte loads of zh, 4 steps per lane and load (the
+// scalar form was one 4-byte and one 2-byte load per step, 0.38 ms at C3).  zq rounds z / qs by a
+// multiply with the reciprocal: any integer q is a valid copy, because qn is the norm of the residual
+// z - qs q actually left.
+template <bool VEC>
 __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32, const uint16_t* __restrict__ zh,
                                                   int64_t P, int T, int Tp, float* __restrict__ dn,
                                                   int16_t* __restrict__ zq, int Tq, float* __restrict__ qs,
@@ -1174,14 +1179,28 @@ __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32,
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   if (p >= P) return;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  typedef unsigned short h4 __attribute__((ext_vector_type(4)));
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const float* zr = z32 + p * T;
+  const uint16_t* hr = zh + p * Tp;
   double s2 = 0.0, n2 = 0.0;
   float mx = 0.f;
-  for (int t = lane; t < T; t += 64) {
-    const float z = z32[p * T + t];
-    const double d = (double)z - (double)(float)__builtin_bit_cast(_Float16, zh[p * Tp + t]);
+  auto acc = [&](float z, uint16_t h) {
+    const double d = (double)z - (double)(float)__builtin_bit_cast(_Float16, h);
     s2 += d * d;
     n2 += (double)z * (double)z;
     mx = fmaxf(mx, fabsf(z));
+  };
+  if constexpr (VEC) {
+    for (int t = 4 * lane; t < T; t += 256) {
+      const f4 z = *reinterpret_cast<const f4*>(zr + t);
+      const h4 h = *reinterpret_cast<const h4*>(hr + t);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc(z[q], h[q]);
+    }
+  } else {
+    for (int t = lane; t < T; t += 64) acc(zr[t], hr[t]);
   }
   for (int off = 32; off > 0; off >>= 1) {
     s2 += __shfl_xor(s2, off, 64);
@@ -1191,17 +1210,28 @@ __global__ __launch_bounds__(TPB) void corr_dnorm(const float* __restrict__ z32,
   if (lane == 0) dn[p] = (float)(sqrt(s2) * (1.0 + 1e-6)) + 1e-12f;
   if (!zq) return;
   const float s = mx / 32767.f;  // 0 for a flat row: every q is 0 and so is the error
+  const float inv = s > 0.f ? 1.f / s : 0.f;
   double e2 = 0.0;
-  for (int t = lane; t < Tq; t += 64) {
-    int q = 0;
-    if (t < T && s > 0.f) {
-      const float z = z32[p * T + t];
-      q = (int)rint((double)z / (double)s);
-      q = q > 32767 ? 32767 : q < -32767 ? -32767 : q;
-      const double e = (double)z - (double)q * (double)s;
-      e2 += e * e;
+  auto quant = [&](float z) -> int {
+    int q = (int)rintf(z * inv);
+    q = q > 32767 ? 32767 : q < -32767 ? -32767 : q;
+    const double e = (double)z - (double)q * (double)s;
+    e2 += e * e;
+    return q;
+  };
+  int16_t* qr = zq + p * Tq;
+  if constexpr (VEC) {
+    for (int t = 4 * lane; t < Tq; t += 256) {  // (Tq is a multiple of 8, T of 4: a group is all in or all out)
+      s4 o = {0, 0, 0, 0};
+      if (t < T) {
+        const f4 z = *reinterpret_cast<const f4*>(zr + t);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (short)quant(z[q]);
+      }
+      *reinterpret_cast<s4*>(qr + t) = o;
     }
-    zq[p * Tq + t] = (int16_t)q;
+  } else {
+    for (int t = lane; t < Tq; t += 64) qr[t] = (int16_t)(t < T ? quant(zr[t]) : 0);
   }
   for (int off = 32; off > 0; off >>= 1) e2 += __shfl_xor(e2, off, 64);
   if (lane == 0) {
@@ -2322,7 +2352,8 @@ int launch_proj(const uint16_t* zh, const float* z32, const Dims& d, const CorrW
 
 // the rows' rounding-error norms and int16 copies (corr_dnorm): the main pass and the re-score read them
 void launch_dnorm(const uint16_t* zh, const float* z32, const Dims& d, const CorrWs& ws, hipStream_t s) {
-  hipLaunchKernelGGL(corr_dnorm, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)), dim3(TPB), 0, s, z32, zh, d.P, d.T,
+  hipLaunchKernelGGL(d.T % 4 == 0 ? corr_dnorm<true> : corr_dnorm<false>, dim3((unsigned)krca::ceil_div(d.P, TPB / 64)),
+                     dim3(TPB), 0, s, z32, zh, d.P, d.T,
                      d.Tp, ws.dn, q16_rows() ? ws.zq : nullptr, ws.Tq, ws.qs, ws.qn, ws.nrm);
 }
 
