@@ -76,7 +76,7 @@ constexpr int CAPC = KRCA_CORR_CAPC_SLOTS;  // candidate buffer per pod (main pa
 // drains while the next batch runs; a tile that finds its batch's list full decides its ambiguous
 // pairs itself (float64 from z32, in the epilogue), so no valid tau ever fails.
 // (knobs KRCA_CORR_BATCH / KRCA_CORR_AMB_TILE, for tests: many batches, lists that fill early)
-inline int64_t sb_batch() { return krca::tuning().corr_batch > 0 ? krca::tuning().corr_batch : 2048; }
+inline int64_t sb_batch() { return krca::tuning().corr_batch > 0 ? krca::tuning().corr_batch : 8192; }  // R9d/R9e: 1M pods 1.81 -> 1.77 s
 inline int64_t amb_per_tile() {  // list budget per tile of a batch (C3 data: ~85 on average)
   return krca::tuning().corr_amb_tile >= 0 ? krca::tuning().corr_amb_tile : 512;
 }

@@ -98,7 +98,7 @@ struct Tuning {
   int group_impl;   // KRCA_GROUP_IMPL: 0 peeled atomics, 1 one atomic per lane
   int corr_debug;   // KRCA_CORR_DEBUG: profiling aid (results wrong when != 0)
   int corr_rs_grid; // KRCA_CORR_RS_GRID: workgroups of the ambiguous-pair re-score (a multiple of 8)
-  int corr_batch;   // KRCA_CORR_BATCH: super-tiles per main-pass batch (0 = 2048)
+  int corr_batch;   // KRCA_CORR_BATCH: super-tiles per main-pass batch (0 = 8192)
   int corr_amb_tile;  // KRCA_CORR_AMB_TILE: ambiguous-list budget per tile of a batch (-1 = 512; 0 = every
                       // tile decides its pairs in place)
   int ppr_fuse;     // KRCA_PPR_FUSE: single device, the iteration's reduction in the step's last workgroup
